@@ -1,0 +1,116 @@
+/*
+ * recsys_amd.h - C ABI of librecsys_amd.so, the MI355X (gfx950) kernels behind the
+ * two-tower retrieval + contrastive training + DeepFM rerank hot path of
+ * DotBlossom/LLM-driven_content-based-feature_recommendation_system.
+ *
+ * Conventions (every entry point):
+ *   - plain device pointers (fp32 row-major unless stated), int64 sizes, no torch types;
+ *   - `stream` is a hipStream_t passed as void*; work is enqueued asynchronously, no
+ *     host synchronisation, no device allocation inside (callers own every buffer, so a
+ *     call can be captured into a hipGraph);
+ *   - return 0 on success; non-zero = error code, text via rsx_last_error()
+ *     (thread-local; argument errors return 1 before anything is launched);
+ *   - "accumulated" outputs are added into and must be zeroed by the caller.
+ * Each function names the reference interface it replaces (path:line under the
+ * reference tree). The reference is pure Python/PyTorch; these are the kernels under its
+ * nn.Module / loss-function surface (see INTEGRATION.md for the ctypes binding).
+ */
+#ifndef RECSYS_AMD_H
+#define RECSYS_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- library identity / errors ------------------------------------------------------ */
+const char* rsx_last_error(void);
+int rsx_abi_version(void);
+const char* rsx_target_arch(void);
+
+/* ---- A2: SASRecUserTower embedding stage --------------------------------------------
+ * Replaces tower_code/v1_refine_usertower.py:434-459:
+ *   seq_emb = item_proj(pretrained_vecs); seq_emb += E_j(ids_j) * s_g[j] (j = 0..5);
+ *   seq_emb += pos_emb(arange(L)); seq_emb = emb_ln(seq_emb); emb_dropout(seq_emb)
+ * base      [B*L, D] = item_proj output (nullable => 0)
+ * ids/tables: ntab (<=6) device pointers, ids int64 [B*L], tables [rows_j, D]
+ * gate      [ntab] device (s_g = sigmoid(seq_gate) * s_mask); a gate that is exactly 0
+ *           skips its gather (forward-exact) and reports a zero gate/table gradient
+ *           (exact for the reference, whose zero gates come from a constant 0 mask)
+ * pos [L, D], ln_w/ln_b [D] (ln_w == NULL => no LayerNorm: out = pre-LN sum, bit-exact
+ * with the reference's op order), mean/rstd [B*L] saved for the backward.
+ * D in {64, 128, 256}. Dropout p in [0,1) via counter hash (seed). */
+int rsx_seq_embed_fwd(const float* base, const int64_t* const* ids, const float* const* tables, int ntab,
+                      const float* gate, const float* pos, const float* ln_w, const float* ln_b, float eps,
+                      int64_t B, int64_t L, int64_t D, float p_drop, uint64_t seed, float* out, float* mean,
+                      float* rstd, void* stream);
+
+/* Backward of rsx_seq_embed_fwd. dbase [B*L,D] written; dtables[j], dgate [ntab], dpos [L,D],
+ * dln_w/dln_b [D] accumulated (nullable). padding_idx[j]: rows excluded from the table
+ * gradient exactly like nn.Embedding(padding_idx=...) (-1 = none). table_rows[j] lets small
+ * tables (time buckets) accumulate in LDS before one flush per workgroup. */
+int rsx_seq_embed_bwd(const float* base, const int64_t* const* ids, const float* const* tables,
+                      const int64_t* table_rows, const int64_t* padding_idx, int ntab, const float* gate,
+                      const float* pos, const float* ln_w, const float* mean, const float* rstd, float eps,
+                      int64_t B, int64_t L, int64_t D, float p_drop, uint64_t seed, const float* dout,
+                      float* dbase, float* const* dtables, float* dgate, float* dpos, float* dln_w,
+                      float* dln_b, void* stream);
+
+/* ---- A3 / A9: masked multi-head self-attention core (L <= 64) -----------------------
+ * Replaces the attention inside nn.TransformerEncoderLayer (norm_first, batch_first) at
+ * tower_code/v1_refine_usertower.py:343-352,461-466 (causal + key padding) and
+ * item_tower.py:169-182,281 (unmasked). qkv [B, L, 3*H*Dh] = in_proj output; out
+ * [B, L, H*Dh] = pre-out_proj head concat; lse [B, H, L]. key_pad [B, L] uint8 (1 = pad,
+ * nullable). Training-path semantics: a fully masked query row gets zero probabilities.
+ * Dh in {16, 32, 64} (backward: {16, 32}). */
+int rsx_mha_fwd(const float* qkv, const uint8_t* key_pad, int64_t B, int64_t L, int64_t H, int64_t Dh, int causal,
+                float p_drop, uint64_t seed, float* out, float* lse, void* stream);
+/* dqkv [B, L, 3*H*Dh] written. */
+int rsx_mha_bwd(const float* qkv, const uint8_t* key_pad, const float* out, const float* lse, const float* dout,
+                int64_t B, int64_t L, int64_t H, int64_t Dh, int causal, float p_drop, uint64_t seed, float* dqkv,
+                void* stream);
+
+/* ---- A6 / A7 / A12: fused in-batch contrastive cross-entropy ------------------------
+ * S_ij = <A_i,B_j>/tau - bias_j over an implicit N x M matrix (never materialised),
+ * fp32-input MFMA, online log-sum-exp. flags (supported combinations):
+ *   0                 plain InfoNCE, label = diagonal  (duorec unsup v1_refine_usertower.py:588-590,
+ *                                                       item_tower.py:1075-1082 per direction)
+ *   2 (MASK_K1)       + exclude off-diagonal j with k1_j == k1_i   (shadowed logq loss :520-573)
+ *   6 (MASK_K1|K2)    + also k2 (user) keys               (live inbatch_corrected_logq_loss :826-861)
+ *   9 (EXCL_DIAG|POS) SupCon term of duorec_loss_refined (:595-625): diagonal excluded,
+ *                     positives k1_i == k1_j != 0, loss_i = LSE_i - mean positive logit
+ * Keys are int32. D = 128 (row strides lda/ldb >= 128, multiple of 4, 16-B aligned).
+ * ws: rsx_nce_workspace_floats(N, M, nsplit_fwd, nsplit_bwd) floats, shared by fwd and bwd.
+ * out2 (device, 2 floats) = {mean loss over valid rows, 1/n_valid}. */
+int64_t rsx_nce_workspace_floats(int64_t N, int64_t M, int nsplit_fwd, int nsplit_bwd);
+int rsx_nce_fwd(const float* A, const float* B, const float* bias, const int* k1a, const int* k1b, const int* k2a,
+                const int* k2b, int64_t N, int64_t M, int64_t lda, int64_t ldb, float tau, int flags, int nsplit,
+                float* ws, float* out2, void* stream);
+/* gout = device scalar upstream gradient. dA [N,128] / dB [M,128] (nullable) written, or
+ * added into when accumulate != 0. Must follow rsx_nce_fwd on the same ws. */
+int rsx_nce_bwd(const float* A, const float* B, const float* bias, const int* k1a, const int* k1b, const int* k2a,
+                const int* k2b, int64_t N, int64_t M, int64_t lda, int64_t ldb, float tau, int flags,
+                int nsplit_fwd, int nsplit, const float* gout, const float* out2, float* ws, float* dA, float* dB,
+                int accumulate, void* stream);
+
+/* ---- row gather / scatter / L2 normalise ---------------------------------------------
+ * out[r] = src[idx[r]] (idx NULL => r), optionally F.normalize'd (eps) with norms saved:
+ *   pretrained_lookup[item_ids]            tower_code/v1_usertower_train.py:760
+ *   normalize(item_matrix)[target_ids]     v1_usertower_train.py:810-811 + v1_refine_usertower.py:833
+ *   F.normalize(x, p=2, dim=-1)            v1_refine_usertower.py:504,584-585; v1_usertower_train.py:807
+ * D in {64,128,256}. */
+int rsx_gather_rows(const float* src, int64_t ld_src, const int64_t* idx, int64_t n, int64_t D, int normalize,
+                    float eps, float* out, float* nrm_out, void* stream);
+/* Backward scatter: dst[idx[r]] (op)= g_r where g = dy (or the F.normalize backward of dy
+ * given y and norms). mode 0 store, 1 add (unique idx), 2 atomic add (duplicates allowed).
+ * Rows whose index equals skip_idx are dropped (nn.Embedding padding_idx), -1 = none. */
+int rsx_scatter_rows(const float* dy, const float* y, const float* nrm, const int64_t* idx, int64_t n, int64_t D,
+                     int normalize, float eps, int mode, int64_t skip_idx, float* dst, int64_t ld_dst, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RECSYS_AMD_H */

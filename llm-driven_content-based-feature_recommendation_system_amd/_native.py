@@ -1,0 +1,114 @@
+"""ctypes binding of librecsys_amd.so (C ABI declared in include/recsys_amd.h).
+
+The product path has no fallback: if the shared library is missing or was built for a
+different GPU, every op raises. Nothing here imports the CPU oracle.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librecsys_amd.so")
+
+_lock = threading.Lock()
+_lib = None
+_checked_devices: set = set()
+
+c_p = ctypes.c_void_p
+c_i64 = ctypes.c_int64
+c_i = ctypes.c_int
+c_f = ctypes.c_float
+c_u64 = ctypes.c_uint64
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "rsx_last_error": (ctypes.c_char_p, []),
+    "rsx_abi_version": (c_i, []),
+    "rsx_target_arch": (ctypes.c_char_p, []),
+    "rsx_seq_embed_fwd": (c_i, [c_p, c_p, c_p, c_i, c_p, c_p, c_p, c_p, c_f, c_i64, c_i64, c_i64, c_f, c_u64,
+                                c_p, c_p, c_p, c_p]),
+    "rsx_seq_embed_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_i64, c_i64, c_i64,
+                                c_f, c_u64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "rsx_mha_fwd": (c_i, [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i, c_f, c_u64, c_p, c_p, c_p]),
+    "rsx_mha_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i, c_f, c_u64, c_p, c_p]),
+    "rsx_nce_workspace_floats": (c_i64, [c_i64, c_i64, c_i, c_i]),
+    "rsx_nce_fwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_f, c_i, c_i, c_p, c_p,
+                          c_p]),
+    "rsx_nce_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_f, c_i, c_i, c_i, c_p,
+                          c_p, c_p, c_p, c_p, c_i, c_p]),
+    "rsx_gather_rows": (c_i, [c_p, c_i64, c_p, c_i64, c_i64, c_i, c_f, c_p, c_p, c_p]),
+    "rsx_scatter_rows": (c_i, [c_p, c_p, c_p, c_p, c_i64, c_i64, c_i, c_f, c_i, c_i64, c_p, c_i64, c_p]),
+}
+
+EXPORTED_SYMBOLS = tuple(_SIGS.keys())
+
+
+def load(path: str = LIB_PATH):
+    """Load and type the library (idempotent). Raises if it is absent."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise RuntimeError(
+                f"recsys_amd: native library not found at {path}; run __graft_entry__.build() "
+                "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
+        lib = ctypes.CDLL(path)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def lib():
+    return _lib if _lib is not None else load()
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib().rsx_last_error().decode(errors="replace")
+        raise RuntimeError(f"recsys_amd {what} failed (code {rc}): {msg}")
+
+
+def ensure_device(t: torch.Tensor) -> None:
+    """The kernels are gfx950 code objects: refuse anything else loudly."""
+    if t.device.type != "cuda":
+        raise RuntimeError(f"recsys_amd ops need a ROCm GPU tensor, got device {t.device}")
+    idx = t.device.index if t.device.index is not None else torch.cuda.current_device()
+    if idx in _checked_devices:
+        return
+    arch = torch.cuda.get_device_properties(idx).gcnArchName.split(":")[0]
+    want = lib().rsx_target_arch().decode()
+    if arch != want:
+        raise RuntimeError(f"recsys_amd was built for {want} but device {idx} is {arch}")
+    _checked_devices.add(idx)
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t) -> int | None:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def ptr_array(tensors, ctype=ctypes.c_void_p):
+    arr = (ctype * max(1, len(tensors)))()
+    for k, t in enumerate(tensors):
+        arr[k] = None if t is None else t.data_ptr()
+    return arr
+
+
+def i64_array(vals):
+    arr = (ctypes.c_int64 * max(1, len(vals)))()
+    for k, v in enumerate(vals):
+        arr[k] = int(v)
+    return arr

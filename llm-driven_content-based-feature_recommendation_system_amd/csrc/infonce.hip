@@ -1,0 +1,699 @@
+// Fused in-batch contrastive cross-entropy (InfoNCE) over an implicit N x M logit
+// matrix that is never materialised:
+//
+//   S_ij = <A_i, B_j> * (1/tau) - bias_j
+//   S_ij = -inf   if excluded(i,j)
+//   row loss_i = LSE_j S_ij - label term
+//
+// Reference semantics covered (file:line in /root/reference):
+//   * inbatch_corrected_logq_loss  tower_code/v1_refine_usertower.py:826-861 (live def):
+//       bias_j = logQ[t_j]*lambda, excluded = (t_i==t_j || user_i==user_j) && i!=j, label = diag
+//   * inbatch_corrected_logq_loss  v1_refine_usertower.py:520-573 (shadowed def): same, no user key
+//   * duorec_loss_refined unsup    v1_refine_usertower.py:588-590: no bias/masks, label = diag
+//   * duorec_loss_refined sup      v1_refine_usertower.py:595-625: excluded = (i==j),
+//       positives M_ij = (t_i==t_j) && t_i!=0 && i!=j, loss_i = LSE_i - sum_j M_ij S_ij / sum_j M_ij
+//   * item-tower SimCSE loss       item_tower.py:1075-1082 (both directions = two calls)
+//
+// Dot products run on the fp32-input MFMA (v_mfma_f32_32x32x2_f32: exact f32 FMA chain,
+// no reduced-precision path on gfx950). Each wave keeps 32 rows of its "owner" operand
+// in registers (64 VGPRs, k permuted as k = 64*h + s so each lane holds a contiguous
+// half row) and streams 32-row tiles of the other operand through LDS. The accumulator
+// tile is computed transposed (streamed rows in registers, owner row on the lane), so
+// the online log-sum-exp is lane-local and the tile doubles as the A operand of the
+// gradient MFMA in the backward (no LDS round trip for dS).
+#include "rsx_common.h"
+#include <math.h>
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kD = 128;        // embedding width (fixed by the reference: d_model=128)
+constexpr int kTile = 32;      // streamed rows per tile
+constexpr int kWaves = 4;      // waves per workgroup
+constexpr int kOwnRows = 32 * kWaves;  // owner rows per workgroup
+constexpr int kLdsStride = kD + 4;     // padded row (conflict-free ds_read_b128 columns)
+
+enum : int { F_EXCL_DIAG = 1, F_MASK_K1 = 2, F_MASK_K2 = 4, F_POS = 8 };
+
+struct FwdArgs {
+  const float* A;     // [N, lda] owner rows (queries)
+  const float* B;     // [M, ldb] streamed rows (columns)
+  const float* bias;  // [M] or nullptr
+  const int* k1a;     // [N] or nullptr
+  const int* k1b;     // [M]
+  const int* k2a;
+  const int* k2b;
+  int64_t N, M, lda, ldb;
+  float inv_tau;
+  int nsplit;
+  int64_t cols_per_split;
+  float* part;  // [4][nsplit][N] : running max, sum-exp, positive-logit sum, positive count
+};
+
+__device__ __forceinline__ int tile_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// Block-id remap: all workgroups of one column split share an XCD group (b % 8), so the
+// split's streamed operand is re-read from that XCD's L2. Speed only, never correctness.
+__device__ __forceinline__ void remap_block(int nsplit, int& split, int& rb) {
+  const int b = blockIdx.x;
+  const int nsub = nsplit >> 3;
+  const int xcd = b & 7, q = b >> 3;
+  split = xcd + 8 * (q % nsub);
+  rb = q / nsub;
+}
+
+template <int FL>
+__global__ __launch_bounds__(256, 2) void nce_fwd_k(FwdArgs a) {
+  __shared__ __attribute__((aligned(16))) float sB[2][kTile][kLdsStride];
+  __shared__ __attribute__((aligned(16))) float sBias[2][kTile];
+  __shared__ __attribute__((aligned(16))) int sK1[2][kTile];
+  __shared__ __attribute__((aligned(16))) int sK2[2][kTile];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, c = lane & 31;
+  int split, rb;
+  remap_block(a.nsplit, split, rb);
+  const int64_t i = (int64_t)rb * kOwnRows + wave * 32 + c;
+  const bool row_ok = i < a.N;
+
+  float u[64];
+  if (row_ok) {
+    const float4* src = reinterpret_cast<const float4*>(a.A + i * a.lda + h * 64);
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const float4 v = src[t];
+      u[4 * t + 0] = v.x; u[4 * t + 1] = v.y; u[4 * t + 2] = v.z; u[4 * t + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < 64; ++t) u[t] = 0.0f;
+  }
+  int k1i = 0, k2i = 0;
+  if (row_ok) {
+    if ((FL & (F_MASK_K1 | F_POS)) && a.k1a) k1i = a.k1a[i];
+    if ((FL & F_MASK_K2) && a.k2a) k2i = a.k2a[i];
+  }
+
+  const int64_t j_begin = (int64_t)split * a.cols_per_split;
+  int64_t j_end = j_begin + a.cols_per_split;
+  if (j_end > a.M) j_end = a.M;
+
+  float m = -INFINITY, l = 0.0f, ps = 0.0f, pc = 0.0f;
+
+  const int srow = tid >> 3, scol = (tid & 7) * 16;
+  float4 stg[4];
+  float stg_bias = 0.0f;
+  int stg_k1 = 0, stg_k2 = 0;
+
+  auto gload = [&](int64_t j0) {
+    const int64_t j = j0 + srow;
+    if (j < j_end) {
+      const float4* src = reinterpret_cast<const float4*>(a.B + j * a.ldb + scol);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) stg[t] = src[t];
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) stg[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (tid < kTile) {
+      const int64_t jj = j0 + tid;
+      const bool ok = jj < j_end;
+      stg_bias = (ok && a.bias) ? a.bias[jj] : 0.0f;
+      stg_k1 = (ok && a.k1b) ? a.k1b[jj] : 0;
+      stg_k2 = (ok && a.k2b) ? a.k2b[jj] : 0;
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) *reinterpret_cast<float4*>(&sB[buf][srow][scol + 4 * t]) = stg[t];
+    if (tid < kTile) {
+      sBias[buf][tid] = stg_bias;
+      sK1[buf][tid] = stg_k1;
+      sK2[buf][tid] = stg_k2;
+    }
+  };
+
+  if (j_begin < j_end) {
+    gload(j_begin);
+    lstore(0);
+    __syncthreads();
+    int cur = 0;
+    for (int64_t j0 = j_begin; j0 < j_end; j0 += kTile) {
+      const bool has_next = j0 + kTile < j_end;
+      if (has_next) gload(j0 + kTile);
+
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+      const float* brow = &sB[cur][c][h * 64];
+#pragma unroll
+      for (int s = 0; s < 64; s += 4) {
+        const float4 bv = *reinterpret_cast<const float4*>(brow + s);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(bv.x, u[s + 0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(bv.y, u[s + 1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(bv.z, u[s + 2], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(bv.w, u[s + 3], acc, 0, 0, 0);
+      }
+
+      float v[16];
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        const int rbase = 8 * q4 + 4 * h;
+        const float4 bi4 = *reinterpret_cast<const float4*>(&sBias[cur][rbase]);
+        const int4 k14 = *reinterpret_cast<const int4*>(&sK1[cur][rbase]);
+        const int4 k24 = *reinterpret_cast<const int4*>(&sK2[cur][rbase]);
+        const float bia[4] = {bi4.x, bi4.y, bi4.z, bi4.w};
+        const int kk1[4] = {k14.x, k14.y, k14.z, k14.w};
+        const int kk2[4] = {k24.x, k24.y, k24.z, k24.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * q4 + e;
+          const int64_t j = j0 + rbase + e;
+          const float s = acc[r] * a.inv_tau - bia[e];
+          bool excl = (j >= j_end) || !row_ok;
+          const bool offdiag = (j != i);
+          if (FL & F_EXCL_DIAG) excl = excl || !offdiag;
+          if (FL & F_MASK_K1) excl = excl || (offdiag && kk1[e] == k1i);
+          if (FL & F_MASK_K2) excl = excl || (offdiag && kk2[e] == k2i);
+          if (FL & F_POS) {
+            if (!excl && offdiag && kk1[e] == k1i && k1i != 0) {
+              ps += s;
+              pc += 1.0f;
+            }
+          }
+          v[r] = excl ? -INFINITY : s;
+          tmax = fmaxf(tmax, v[r]);
+        }
+      }
+      if (tmax > m) {
+        l = (m == -INFINITY) ? 0.0f : l * __expf(m - tmax);
+        m = tmax;
+      }
+      if (m != -INFINITY) {
+        float t = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t += __expf(v[r] - m);
+        l += t;
+      }
+      __syncthreads();
+      if (has_next) lstore(cur ^ 1);
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+
+  // fold the two lane halves (same row i, complementary column sets)
+  const float m2 = __shfl_xor(m, 32, 64);
+  const float l2 = __shfl_xor(l, 32, 64);
+  const float ps2 = __shfl_xor(ps, 32, 64);
+  const float pc2 = __shfl_xor(pc, 32, 64);
+  const float mm = fmaxf(m, m2);
+  float ll = 0.0f;
+  if (mm != -INFINITY) {
+    if (m != -INFINITY) ll += l * __expf(m - mm);
+    if (m2 != -INFINITY) ll += l2 * __expf(m2 - mm);
+  }
+  if (h == 0 && row_ok) {
+    const int64_t stride = (int64_t)a.nsplit * a.N;
+    const int64_t o = (int64_t)split * a.N + i;
+    a.part[o] = mm;
+    a.part[stride + o] = ll;
+    a.part[2 * stride + o] = ps + ps2;
+    a.part[3 * stride + o] = pc + pc2;
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Merge the column splits: LSE, label term, per-row loss/valid/1-over-count.
+struct MergeArgs {
+  const float* A;
+  const float* B;
+  const float* bias;
+  int64_t N, lda, ldb;
+  float inv_tau;
+  int nsplit;
+  const float* part;
+  int pos_mode;      // 0: label = diagonal, 1: label = positive set
+  float* lse;        // [N]
+  float* row_loss;   // [N]
+  float* row_valid;  // [N] 0/1
+  float* inv_cnt;    // [N] (pos mode) or nullptr
+};
+
+__global__ __launch_bounds__(256) void nce_merge_k(MergeArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= a.N) return;
+  const int64_t stride = (int64_t)a.nsplit * a.N;
+  // every lane reads a split (nsplit <= 64 asserted on host)
+  float m = -INFINITY, l = 0.0f, ps = 0.0f, pc = 0.0f;
+  if (lane < a.nsplit) {
+    const int64_t o = (int64_t)lane * a.N + i;
+    m = a.part[o];
+    l = a.part[stride + o];
+    ps = a.part[2 * stride + o];
+    pc = a.part[3 * stride + o];
+  }
+  float mm = m;
+  for (int o = 32; o > 0; o >>= 1) mm = fmaxf(mm, __shfl_xor(mm, o, 64));
+  float t = (m == -INFINITY) ? 0.0f : l * __expf(m - mm);
+  for (int o = 32; o > 0; o >>= 1) {
+    t += __shfl_xor(t, o, 64);
+    ps += __shfl_xor(ps, o, 64);
+    pc += __shfl_xor(pc, o, 64);
+  }
+  const float lse = (mm == -INFINITY) ? -INFINITY : mm + logf(t);
+  float loss, valid, icnt = 0.0f;
+  if (!a.pos_mode) {
+    // diagonal logit S_ii (same expression as the fused kernel)
+    const float2 x = reinterpret_cast<const float2*>(a.A + i * a.lda)[lane];
+    const float2 y = reinterpret_cast<const float2*>(a.B + i * a.ldb)[lane];
+    float d = x.x * y.x + x.y * y.y;
+    for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+    const float sii = d * a.inv_tau - (a.bias ? a.bias[i] : 0.0f);
+    loss = lse - sii;
+    valid = 1.0f;
+  } else {
+    valid = pc > 0.0f ? 1.0f : 0.0f;
+    icnt = pc > 0.0f ? 1.0f / pc : 0.0f;
+    loss = pc > 0.0f ? lse - ps / pc : 0.0f;
+  }
+  if (lane == 0) {
+    a.lse[i] = lse;
+    a.row_loss[i] = loss;
+    a.row_valid[i] = valid;
+    if (a.inv_cnt) a.inv_cnt[i] = icnt;
+  }
+}
+
+// Deterministic single-workgroup mean over valid rows. out[0] = loss, out[1] = 1/n_valid.
+__global__ __launch_bounds__(1024) void nce_reduce_k(const float* row_loss, const float* row_valid, int64_t N,
+                                                      float* out) {
+  __shared__ float s_l[1024], s_v[1024];
+  float l = 0.0f, v = 0.0f;
+  for (int64_t i = threadIdx.x; i < N; i += 1024) {
+    l += row_loss[i];
+    v += row_valid[i];
+  }
+  s_l[threadIdx.x] = l;
+  s_v[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = 512; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      s_l[threadIdx.x] += s_l[threadIdx.x + o];
+      s_v[threadIdx.x] += s_v[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float nv = s_v[0];
+    out[0] = nv > 0.0f ? s_l[0] / nv : 0.0f;
+    out[1] = nv > 0.0f ? 1.0f / nv : 0.0f;
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Backward. G_ij = w_i * (P_ij - Y_ij) / tau, P_ij = exp(S_ij - LSE_i) (0 if excluded),
+// Y = diagonal (pos_mode 0) or M_ij / cnt_i (pos_mode 1), w_i = g * scale * valid_i.
+// ROW_OWNED: dA_i = sum_j G_ij B_j ; else dB_j = sum_i G_ij A_i.
+struct BwdArgs {
+  const float* A;
+  const float* B;
+  const float* bias;
+  const int* k1a;
+  const int* k1b;
+  const int* k2a;
+  const int* k2b;
+  int64_t N, M, lda, ldb;
+  float inv_tau;
+  const float* lse;
+  const float* row_valid;
+  const float* inv_cnt;
+  const float* gout;   // upstream scalar gradient (device)
+  const float* scale;  // 1/n_valid (device, written by nce_reduce_k)
+  int nsplit;
+  int64_t span_per_split;  // streamed rows per split
+  float* dout;             // [nsplit][owner_rows][128] (split partials) or final when nsplit==1
+};
+
+template <int FL, bool ROW_OWNED>
+__global__ __launch_bounds__(256, 2) void nce_bwd_k(BwdArgs a) {
+  __shared__ __attribute__((aligned(16))) float sX[2][kTile][kLdsStride];
+  __shared__ __attribute__((aligned(16))) float sM0[2][kTile];  // row side: lse_i | col side: bias_j
+  __shared__ __attribute__((aligned(16))) float sM1[2][kTile];  // row side: w_i
+  __shared__ __attribute__((aligned(16))) float sM2[2][kTile];  // row side: inv_cnt_i
+  __shared__ __attribute__((aligned(16))) int sK1[2][kTile];
+  __shared__ __attribute__((aligned(16))) int sK2[2][kTile];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, c = lane & 31;
+  int split, ob;
+  remap_block(a.nsplit, split, ob);
+
+  const int64_t n_own = ROW_OWNED ? a.N : a.M;
+  const int64_t n_str = ROW_OWNED ? a.M : a.N;
+  const float* own = ROW_OWNED ? a.A : a.B;
+  const float* str = ROW_OWNED ? a.B : a.A;
+  const int64_t ld_own = ROW_OWNED ? a.lda : a.ldb;
+  const int64_t ld_str = ROW_OWNED ? a.ldb : a.lda;
+  const float g_scale = a.gout[0] * a.scale[0] * a.inv_tau;
+
+  const int64_t o = (int64_t)ob * kOwnRows + wave * 32 + c;  // this lane's owner index
+  const bool own_ok = o < n_own;
+  float u[64];
+  if (own_ok) {
+    const float4* src = reinterpret_cast<const float4*>(own + o * ld_own + h * 64);
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const float4 v = src[t];
+      u[4 * t + 0] = v.x; u[4 * t + 1] = v.y; u[4 * t + 2] = v.z; u[4 * t + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < 64; ++t) u[t] = 0.0f;
+  }
+  // owner-side metadata
+  float o_lse = 0.0f, o_w = 0.0f, o_icnt = 0.0f, o_bias = 0.0f;
+  int o_k1 = 0, o_k2 = 0;
+  if (own_ok) {
+    if (ROW_OWNED) {
+      o_lse = a.lse[o];
+      o_w = a.row_valid[o] * g_scale;
+      if ((FL & F_POS) && a.inv_cnt) o_icnt = a.inv_cnt[o];
+      if ((FL & (F_MASK_K1 | F_POS)) && a.k1a) o_k1 = a.k1a[o];
+      if ((FL & F_MASK_K2) && a.k2a) o_k2 = a.k2a[o];
+    } else {
+      o_bias = a.bias ? a.bias[o] : 0.0f;
+      if ((FL & (F_MASK_K1 | F_POS)) && a.k1b) o_k1 = a.k1b[o];
+      if ((FL & F_MASK_K2) && a.k2b) o_k2 = a.k2b[o];
+    }
+  }
+
+  const int64_t s_begin = (int64_t)split * a.span_per_split;
+  int64_t s_end = s_begin + a.span_per_split;
+  if (s_end > n_str) s_end = n_str;
+
+  f32x16 gacc[4];
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) gacc[kb][r] = 0.0f;
+
+  const int srow = tid >> 3, scol = (tid & 7) * 16;
+  float4 stg[4];
+  float stg0 = 0.0f, stg1 = 0.0f, stg2 = 0.0f;
+  int stg_k1 = 0, stg_k2 = 0;
+
+  auto gload = [&](int64_t s0) {
+    const int64_t sidx = s0 + srow;
+    if (sidx < s_end) {
+      const float4* src = reinterpret_cast<const float4*>(str + sidx * ld_str + scol);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) stg[t] = src[t];
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) stg[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (tid < kTile) {
+      const int64_t ss = s0 + tid;
+      const bool ok = ss < s_end;
+      if (ROW_OWNED) {  // streamed = columns j
+        stg0 = (ok && a.bias) ? a.bias[ss] : 0.0f;
+        stg_k1 = (ok && a.k1b) ? a.k1b[ss] : 0;
+        stg_k2 = (ok && a.k2b) ? a.k2b[ss] : 0;
+      } else {  // streamed = rows i
+        stg0 = ok ? a.lse[ss] : 0.0f;
+        stg1 = ok ? a.row_valid[ss] * g_scale : 0.0f;
+        stg2 = (ok && a.inv_cnt) ? a.inv_cnt[ss] : 0.0f;
+        stg_k1 = (ok && a.k1a) ? a.k1a[ss] : 0;
+        stg_k2 = (ok && a.k2a) ? a.k2a[ss] : 0;
+      }
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) *reinterpret_cast<float4*>(&sX[buf][srow][scol + 4 * t]) = stg[t];
+    if (tid < kTile) {
+      sM0[buf][tid] = stg0;
+      sM1[buf][tid] = stg1;
+      sM2[buf][tid] = stg2;
+      sK1[buf][tid] = stg_k1;
+      sK2[buf][tid] = stg_k2;
+    }
+  };
+
+  if (s_begin < s_end) {
+    gload(s_begin);
+    lstore(0);
+    __syncthreads();
+    int cur = 0;
+    for (int64_t s0 = s_begin; s0 < s_end; s0 += kTile) {
+      const bool has_next = s0 + kTile < s_end;
+      if (has_next) gload(s0 + kTile);
+
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+      const float* xrow = &sX[cur][c][h * 64];
+#pragma unroll
+      for (int s = 0; s < 64; s += 4) {
+        const float4 bv = *reinterpret_cast<const float4*>(xrow + s);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(bv.x, u[s + 0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(bv.y, u[s + 1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(bv.z, u[s + 2], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(bv.w, u[s + 3], acc, 0, 0, 0);
+      }
+
+      // acc[r] = <own_o, str_s>, s = s0 + tile_row(r,h). Turn it into G (in place).
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        const int rbase = 8 * q4 + 4 * h;
+        const float4 m04 = *reinterpret_cast<const float4*>(&sM0[cur][rbase]);
+        const float4 m14 = *reinterpret_cast<const float4*>(&sM1[cur][rbase]);
+        const float4 m24 = *reinterpret_cast<const float4*>(&sM2[cur][rbase]);
+        const int4 k14 = *reinterpret_cast<const int4*>(&sK1[cur][rbase]);
+        const int4 k24 = *reinterpret_cast<const int4*>(&sK2[cur][rbase]);
+        const float mm0[4] = {m04.x, m04.y, m04.z, m04.w};
+        const float mm1[4] = {m14.x, m14.y, m14.z, m14.w};
+        const float mm2[4] = {m24.x, m24.y, m24.z, m24.w};
+        const int kk1[4] = {k14.x, k14.y, k14.z, k14.w};
+        const int kk2[4] = {k24.x, k24.y, k24.z, k24.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * q4 + e;
+          const int64_t sidx = s0 + rbase + e;
+          // resolve (i, j) and their metadata
+          int64_t ii, jj;
+          float lse_i, w_i, icnt_i, bias_j;
+          int k1_i, k1_j, k2_i, k2_j;
+          if (ROW_OWNED) {
+            ii = o; jj = sidx;
+            lse_i = o_lse; w_i = o_w; icnt_i = o_icnt; bias_j = mm0[e];
+            k1_i = o_k1; k1_j = kk1[e]; k2_i = o_k2; k2_j = kk2[e];
+          } else {
+            ii = sidx; jj = o;
+            lse_i = mm0[e]; w_i = mm1[e]; icnt_i = mm2[e]; bias_j = o_bias;
+            k1_i = kk1[e]; k1_j = o_k1; k2_i = kk2[e]; k2_j = o_k2;
+          }
+          const float sv = acc[r] * a.inv_tau - bias_j;
+          bool excl = (sidx >= s_end) || !own_ok;
+          const bool offdiag = (ii != jj);
+          if (FL & F_EXCL_DIAG) excl = excl || !offdiag;
+          if (FL & F_MASK_K1) excl = excl || (offdiag && k1_i == k1_j);
+          if (FL & F_MASK_K2) excl = excl || (offdiag && k2_i == k2_j);
+          float y = 0.0f;
+          if (FL & F_POS) {
+            if (!excl && offdiag && k1_i == k1_j && k1_i != 0) y = icnt_i;
+          } else {
+            y = offdiag ? 0.0f : 1.0f;
+          }
+          const float p = (excl || lse_i == -INFINITY) ? 0.0f : __expf(sv - lse_i);
+          acc[r] = excl ? 0.0f : w_i * (p - y);
+        }
+      }
+
+      // gradient MFMA: d_own[o][kb*32 + n] += sum_s G[o][s] * str[s][kb*32 + n]
+      // A operand (lane c,h, step t) = G[own=c][str=tile_row(t,h)] = acc[t]
+      // B operand = str[tile_row(t,h)][kb*32 + c]
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const float* srow_p = &sX[cur][tile_row(t, h)][c];
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+          gacc[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(acc[t], srow_p[kb * 32], gacc[kb], 0, 0, 0);
+      }
+
+      __syncthreads();
+      if (has_next) lstore(cur ^ 1);
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+
+  // write d_own rows: D[row = own-local tile_row(r,h)][col = kb*32 + c]
+  const int64_t own_base = (int64_t)ob * kOwnRows + wave * 32;
+  float* dst = a.dout + (int64_t)split * n_own * kD;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int64_t orow = own_base + tile_row(r, h);
+    if (orow < n_own) {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) dst[orow * kD + kb * 32 + c] = gacc[kb][r];
+    }
+  }
+}
+
+// Sum split partials: out[i][k] (+)= sum_s part[s][i][k]
+__global__ __launch_bounds__(256) void nce_sum_splits_k(const float* part, int nsplit, int64_t n, float* out,
+                                                         int accumulate) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // float4 index
+  const int64_t total4 = n * kD / 4;
+  if (idx >= total4) return;
+  float4 s = reinterpret_cast<const float4*>(part)[idx];
+  for (int k = 1; k < nsplit; ++k) {
+    const float4 v = reinterpret_cast<const float4*>(part + (int64_t)k * n * kD)[idx];
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  if (accumulate) {
+    const float4 v = reinterpret_cast<const float4*>(out)[idx];
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  reinterpret_cast<float4*>(out)[idx] = s;
+}
+
+template <int FL>
+void launch_fwd_t(const FwdArgs& a, int blocks, hipStream_t st) {
+  hipLaunchKernelGGL(nce_fwd_k<FL>, dim3(blocks), dim3(256), 0, st, a);
+}
+
+template <int FL>
+void launch_bwd_t(const BwdArgs& a, bool row_owned, int blocks, hipStream_t st) {
+  if (row_owned) hipLaunchKernelGGL((nce_bwd_k<FL, true>), dim3(blocks), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((nce_bwd_k<FL, false>), dim3(blocks), dim3(256), 0, st, a);
+}
+
+bool valid_flags(int f) {
+  // supported combinations (see header)
+  return f == 0 || f == F_MASK_K1 || f == (F_MASK_K1 | F_MASK_K2) || f == (F_EXCL_DIAG | F_POS);
+}
+
+int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+}  // namespace
+
+RSX_API int64_t rsx_nce_workspace_floats(int64_t N, int64_t M, int nsplit_fwd, int nsplit_bwd) {
+  const int64_t mx = N > M ? N : M;
+  return 4 * (int64_t)nsplit_fwd * N      // fwd partials
+         + 4 * N                          // lse, row_loss, row_valid, inv_cnt
+         + (int64_t)nsplit_bwd * mx * kD  // bwd split partials
+         + 16;
+}
+
+// Forward: writes lse/row_loss/row_valid/inv_cnt (ws) and out2 = {loss, 1/n_valid}.
+RSX_API int rsx_nce_fwd(const float* A, const float* B, const float* bias, const int* k1a, const int* k1b,
+                        const int* k2a, const int* k2b, int64_t N, int64_t M, int64_t lda, int64_t ldb, float tau,
+                        int flags, int nsplit, float* ws, float* out2, void* stream) {
+  RSX_ARG(valid_flags(flags), "unsupported flag combination");
+  RSX_ARG(nsplit >= 8 && nsplit <= 64 && nsplit % 8 == 0, "nsplit must be a multiple of 8 in [8,64]");
+  RSX_ARG(N >= 0 && M >= 0, "negative size");
+  RSX_ARG(lda % 4 == 0 && ldb % 4 == 0 && lda >= kD && ldb >= kD, "row strides must be >=128 and multiples of 4");
+  RSX_ARG(((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0, "A/B must be 16-byte aligned");
+  RSX_ARG(!(flags & F_EXCL_DIAG) || N == M, "diagonal modes need N == M");
+  RSX_ARG((flags & F_POS) || N == M, "diagonal-label loss needs N == M");
+  RSX_ARG(!(flags & (F_MASK_K1 | F_POS)) || (k1a && k1b), "k1 keys required");
+  RSX_ARG(!(flags & F_MASK_K2) || (k2a && k2b), "k2 keys required");
+  hipStream_t st = (hipStream_t)stream;
+  float* part = ws;
+  float* lse = part + 4 * (int64_t)nsplit * N;
+  float* row_loss = lse + N;
+  float* row_valid = row_loss + N;
+  float* inv_cnt = row_valid + N;
+  if (N == 0) {
+    (void)hipMemsetAsync(out2, 0, 2 * sizeof(float), st);
+    RSX_LAUNCHED();
+    return 0;
+  }
+  FwdArgs fa;
+  fa.A = A; fa.B = B; fa.bias = bias;
+  fa.k1a = k1a; fa.k1b = k1b; fa.k2a = k2a; fa.k2b = k2b;
+  fa.N = N; fa.M = M; fa.lda = lda; fa.ldb = ldb;
+  fa.inv_tau = 1.0f / tau;
+  fa.nsplit = nsplit;
+  fa.cols_per_split = round_up((M + nsplit - 1) / nsplit, kTile);
+  if (fa.cols_per_split < kTile) fa.cols_per_split = kTile;
+  fa.part = part;
+  const int64_t rbs = (N + kOwnRows - 1) / kOwnRows;
+  const int blocks = (int)(rbs * nsplit);
+  switch (flags) {
+    case 0: launch_fwd_t<0>(fa, blocks, st); break;
+    case F_MASK_K1: launch_fwd_t<F_MASK_K1>(fa, blocks, st); break;
+    case F_MASK_K1 | F_MASK_K2: launch_fwd_t<F_MASK_K1 | F_MASK_K2>(fa, blocks, st); break;
+    default: launch_fwd_t<F_EXCL_DIAG | F_POS>(fa, blocks, st); break;
+  }
+  RSX_LAUNCHED();
+  MergeArgs ma;
+  ma.A = A; ma.B = B; ma.bias = bias;
+  ma.N = N; ma.lda = lda; ma.ldb = ldb;
+  ma.inv_tau = fa.inv_tau;
+  ma.nsplit = nsplit;
+  ma.part = part;
+  ma.pos_mode = (flags & F_POS) ? 1 : 0;
+  ma.lse = lse; ma.row_loss = row_loss; ma.row_valid = row_valid; ma.inv_cnt = inv_cnt;
+  hipLaunchKernelGGL(nce_merge_k, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, ma);
+  RSX_LAUNCHED();
+  hipLaunchKernelGGL(nce_reduce_k, dim3(1), dim3(1024), 0, st, row_loss, row_valid, N, out2);
+  RSX_LAUNCHED();
+  return 0;
+}
+
+// Backward: dA (N x 128) and/or dB (M x 128); accumulate != 0 adds into them.
+RSX_API int rsx_nce_bwd(const float* A, const float* B, const float* bias, const int* k1a, const int* k1b,
+                        const int* k2a, const int* k2b, int64_t N, int64_t M, int64_t lda, int64_t ldb, float tau,
+                        int flags, int nsplit_fwd, int nsplit, const float* gout, const float* out2, float* ws,
+                        float* dA, float* dB, int accumulate, void* stream) {
+  RSX_ARG(valid_flags(flags), "unsupported flag combination");
+  RSX_ARG(nsplit >= 8 && nsplit <= 64 && nsplit % 8 == 0, "nsplit must be a multiple of 8 in [8,64]");
+  RSX_ARG(gout != nullptr && out2 != nullptr, "gout/out2 required");
+  hipStream_t st = (hipStream_t)stream;
+  if (N == 0) return 0;
+  float* part = ws;
+  float* lse = part + 4 * (int64_t)nsplit_fwd * N;
+  float* row_valid = lse + 2 * N;
+  float* inv_cnt = row_valid + N;
+  float* dpart = inv_cnt + N;
+  BwdArgs ba;
+  ba.A = A; ba.B = B; ba.bias = bias;
+  ba.k1a = k1a; ba.k1b = k1b; ba.k2a = k2a; ba.k2b = k2b;
+  ba.N = N; ba.M = M; ba.lda = lda; ba.ldb = ldb;
+  ba.inv_tau = 1.0f / tau;
+  ba.lse = lse; ba.row_valid = row_valid; ba.inv_cnt = inv_cnt;
+  ba.gout = gout;
+  ba.scale = out2 + 1;
+  ba.nsplit = nsplit;
+  for (int pass = 0; pass < 2; ++pass) {
+    const bool row_owned = pass == 0;
+    float* target = row_owned ? dA : dB;
+    if (!target) continue;
+    const int64_t n_own = row_owned ? N : M;
+    const int64_t n_str = row_owned ? M : N;
+    if (n_own == 0) continue;
+    ba.span_per_split = round_up((n_str + nsplit - 1) / nsplit, kTile);
+    if (ba.span_per_split < kTile) ba.span_per_split = kTile;
+    ba.dout = dpart;
+    const int blocks = (int)(((n_own + kOwnRows - 1) / kOwnRows) * nsplit);
+    switch (flags) {
+      case 0: launch_bwd_t<0>(ba, row_owned, blocks, st); break;
+      case F_MASK_K1: launch_bwd_t<F_MASK_K1>(ba, row_owned, blocks, st); break;
+      case F_MASK_K1 | F_MASK_K2: launch_bwd_t<F_MASK_K1 | F_MASK_K2>(ba, row_owned, blocks, st); break;
+      default: launch_bwd_t<F_EXCL_DIAG | F_POS>(ba, row_owned, blocks, st); break;
+    }
+    RSX_LAUNCHED();
+    const int64_t total4 = n_own * kD / 4;
+    hipLaunchKernelGGL(nce_sum_splits_k, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, st, dpart, nsplit,
+                       n_own, target, accumulate);
+    RSX_LAUNCHED();
+  }
+  return 0;
+}

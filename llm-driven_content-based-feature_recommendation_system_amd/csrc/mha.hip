@@ -1,0 +1,311 @@
+// Masked multi-head self-attention core for short sequences (L <= 64), the attention of
+// nn.TransformerEncoderLayer as used by
+//   * SASRecUserTower   tower_code/v1_refine_usertower.py:343-352, 461-466
+//     (causal mask triu(ones,1) + src_key_padding_mask, left padding, L = 50, dh = 32)
+//   * HybridItemTower   item_tower.py:169-182, 281 (no mask, 16 field tokens, dh = d/4)
+// Input is the packed in_proj output qkv[B, L, 3*D] (q | k | v, heads contiguous inside
+// each part, exactly torch's in_proj_weight layout); output is the concatenated head
+// output [B, L, D] that feeds out_proj.
+//
+// Semantics pinned to the training-mode (non fast-path) reference: a query row whose keys
+// are all masked (left-padded positions under the causal mask) gets all-zero
+// probabilities, so its attention output is exactly 0 (=> out_proj.bias after out_proj).
+// Attention-probability dropout (p > 0) uses the counter-based hash in rsx_common.h.
+//
+// One 64-lane workgroup per (batch, head): lane i owns query row i. K/V rows of the head
+// are staged in LDS and read by broadcast; scores live in registers (L <= 64).
+#include "rsx_common.h"
+#include <math.h>
+
+namespace {
+
+constexpr int kLMax = 64;
+
+struct FwdArgs {
+  const float* qkv;      // [B, L, 3D]
+  const uint8_t* kpad;   // [B, L] 1 = pad (masked key) or nullptr
+  float* out;            // [B, L, D]
+  float* lse;            // [B, H, L] (natural log-sum-exp of the scaled scores; -inf if fully masked)
+  int B, L, H, causal;
+  float scale;
+  rsx::Dropout drop;
+};
+
+template <int DH>
+__global__ __launch_bounds__(64) void mha_fwd_k(FwdArgs a) {
+  __shared__ __attribute__((aligned(16))) float sK[kLMax][DH];
+  __shared__ __attribute__((aligned(16))) float sV[kLMax][DH];
+  __shared__ int sPad[kLMax];
+  const int D = a.H * DH;
+  const int b = blockIdx.x / a.H, hd = blockIdx.x % a.H;
+  const int i = threadIdx.x;
+  const float* base = a.qkv + (int64_t)b * a.L * 3 * D;
+
+  constexpr int V4 = DH / 4;
+  for (int t = threadIdx.x; t < a.L * V4; t += 64) {
+    const int r = t / V4, c4 = t % V4;
+    const float4* rowp = reinterpret_cast<const float4*>(base + (int64_t)r * 3 * D);
+    reinterpret_cast<float4*>(&sK[r][0])[c4] = rowp[(D + hd * DH) / 4 + c4];
+    reinterpret_cast<float4*>(&sV[r][0])[c4] = rowp[(2 * D + hd * DH) / 4 + c4];
+  }
+  if (i < a.L) sPad[i] = a.kpad ? (int)a.kpad[(int64_t)b * a.L + i] : 0;
+  __syncthreads();
+  if (i >= a.L) return;
+
+  float q[DH];
+  {
+    const float4* qp = reinterpret_cast<const float4*>(base + (int64_t)i * 3 * D + hd * DH);
+#pragma unroll
+    for (int t = 0; t < V4; ++t) {
+      const float4 v = qp[t];
+      q[4 * t] = v.x; q[4 * t + 1] = v.y; q[4 * t + 2] = v.z; q[4 * t + 3] = v.w;
+    }
+  }
+  float s[kLMax];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < kLMax; ++j) {
+    s[j] = -INFINITY;
+    if (j < a.L) {
+      const bool allowed = !sPad[j] && (!a.causal || j <= i);
+      float d = 0.0f;
+#pragma unroll
+      for (int t = 0; t < V4; ++t) {
+        const float4 kv = reinterpret_cast<const float4*>(&sK[j][0])[t];
+        d = fmaf(q[4 * t], kv.x, d);
+        d = fmaf(q[4 * t + 1], kv.y, d);
+        d = fmaf(q[4 * t + 2], kv.z, d);
+        d = fmaf(q[4 * t + 3], kv.w, d);
+      }
+      if (allowed) {
+        s[j] = d * a.scale;
+        mx = fmaxf(mx, s[j]);
+      }
+    }
+  }
+  float o[DH];
+#pragma unroll
+  for (int e = 0; e < DH; ++e) o[e] = 0.0f;
+  float lse = -INFINITY;
+  if (mx != -INFINITY) {
+    float sum = 0.0f;
+#pragma unroll
+    for (int j = 0; j < kLMax; ++j) {
+      const float p = (s[j] == -INFINITY) ? 0.0f : __expf(s[j] - mx);
+      s[j] = p;
+      sum += p;
+    }
+    const float inv = 1.0f / sum;
+    lse = mx + logf(sum);
+    const uint64_t rowidx = (((uint64_t)b * a.H + hd) * a.L + i) * a.L;
+#pragma unroll
+    for (int j = 0; j < kLMax; ++j) {
+      if (j < a.L) {
+        float p = s[j] * inv;
+        p = a.drop.apply(p, rowidx + j);
+        if (p != 0.0f) {
+#pragma unroll
+          for (int t = 0; t < V4; ++t) {
+            const float4 vv = reinterpret_cast<const float4*>(&sV[j][0])[t];
+            o[4 * t] = fmaf(p, vv.x, o[4 * t]);
+            o[4 * t + 1] = fmaf(p, vv.y, o[4 * t + 1]);
+            o[4 * t + 2] = fmaf(p, vv.z, o[4 * t + 2]);
+            o[4 * t + 3] = fmaf(p, vv.w, o[4 * t + 3]);
+          }
+        }
+      }
+    }
+  }
+  float4* op = reinterpret_cast<float4*>(a.out + ((int64_t)b * a.L + i) * D + hd * DH);
+#pragma unroll
+  for (int t = 0; t < V4; ++t) op[t] = make_float4(o[4 * t], o[4 * t + 1], o[4 * t + 2], o[4 * t + 3]);
+  if (a.lse) a.lse[((int64_t)b * a.H + hd) * a.L + i] = lse;
+}
+
+struct BwdArgs {
+  const float* qkv;
+  const uint8_t* kpad;
+  const float* out;   // forward output O [B, L, D]
+  const float* lse;   // [B, H, L]
+  const float* dout;  // [B, L, D]
+  float* dqkv;        // [B, L, 3D] (written)
+  int B, L, H, causal;
+  float scale;
+  rsx::Dropout drop;
+};
+
+template <int DH>
+__global__ __launch_bounds__(64) void mha_bwd_k(BwdArgs a) {
+  __shared__ __attribute__((aligned(16))) float sQ[kLMax][DH];
+  __shared__ __attribute__((aligned(16))) float sK[kLMax][DH];
+  __shared__ __attribute__((aligned(16))) float sdO[kLMax][DH];
+  __shared__ float sLse[kLMax], sDelta[kLMax];
+  __shared__ int sPad[kLMax];
+  __shared__ float sdS[kLMax][kLMax + 1];
+  const int D = a.H * DH;
+  const int b = blockIdx.x / a.H, hd = blockIdx.x % a.H;
+  const int lane = threadIdx.x;
+  const float* base = a.qkv + (int64_t)b * a.L * 3 * D;
+  const float* dob = a.dout + (int64_t)b * a.L * D;
+  constexpr int V4 = DH / 4;
+
+  for (int t = threadIdx.x; t < a.L * V4; t += 64) {
+    const int r = t / V4, c4 = t % V4;
+    const float4* rowp = reinterpret_cast<const float4*>(base + (int64_t)r * 3 * D);
+    reinterpret_cast<float4*>(&sQ[r][0])[c4] = rowp[(hd * DH) / 4 + c4];
+    reinterpret_cast<float4*>(&sK[r][0])[c4] = rowp[(D + hd * DH) / 4 + c4];
+    reinterpret_cast<float4*>(&sdO[r][0])[c4] = reinterpret_cast<const float4*>(dob + (int64_t)r * D + hd * DH)[c4];
+  }
+  if (lane < a.L) {
+    sPad[lane] = a.kpad ? (int)a.kpad[(int64_t)b * a.L + lane] : 0;
+    sLse[lane] = a.lse[((int64_t)b * a.H + hd) * a.L + lane];
+    // delta_i = dO_i . O_i  (holds with dropout: sum_j P_ij dP_ij = dO_i . O_i)
+    const float4* op = reinterpret_cast<const float4*>(a.out + ((int64_t)b * a.L + lane) * D + hd * DH);
+    const float4* dp = reinterpret_cast<const float4*>(dob + (int64_t)lane * D + hd * DH);
+    float d = 0.0f;
+#pragma unroll
+    for (int t = 0; t < V4; ++t) {
+      const float4 x = op[t], y = dp[t];
+      d += x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
+    }
+    sDelta[lane] = d;
+  }
+  __syncthreads();
+
+  // ---- pass A: lane j owns key/value row j: dK_j, dV_j, and dS column j into LDS ----
+  const int j = lane;
+  float kj[DH], vj[DH], dk[DH], dv[DH];
+  const bool jok = j < a.L;
+  if (jok) {
+    const float4* vp = reinterpret_cast<const float4*>(base + (int64_t)j * 3 * D + 2 * D + hd * DH);
+#pragma unroll
+    for (int t = 0; t < V4; ++t) {
+      const float4 kk = reinterpret_cast<const float4*>(&sK[j][0])[t];
+      const float4 vv = vp[t];
+      kj[4 * t] = kk.x; kj[4 * t + 1] = kk.y; kj[4 * t + 2] = kk.z; kj[4 * t + 3] = kk.w;
+      vj[4 * t] = vv.x; vj[4 * t + 1] = vv.y; vj[4 * t + 2] = vv.z; vj[4 * t + 3] = vv.w;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < DH; ++e) { kj[e] = 0.0f; vj[e] = 0.0f; }
+  }
+#pragma unroll
+  for (int e = 0; e < DH; ++e) { dk[e] = 0.0f; dv[e] = 0.0f; }
+  const bool jpad = jok ? (sPad[j] != 0) : true;
+
+  for (int i = 0; i < a.L; ++i) {
+    const float lse_i = sLse[i];
+    float ds = 0.0f;
+    const bool allowed = jok && !jpad && (!a.causal || j <= i) && lse_i != -INFINITY;
+    if (allowed) {
+      float sdot = 0.0f, pdot = 0.0f;
+#pragma unroll
+      for (int t = 0; t < V4; ++t) {
+        const float4 qv = reinterpret_cast<const float4*>(&sQ[i][0])[t];
+        const float4 gv = reinterpret_cast<const float4*>(&sdO[i][0])[t];
+        sdot = fmaf(qv.x, kj[4 * t], sdot); sdot = fmaf(qv.y, kj[4 * t + 1], sdot);
+        sdot = fmaf(qv.z, kj[4 * t + 2], sdot); sdot = fmaf(qv.w, kj[4 * t + 3], sdot);
+        pdot = fmaf(gv.x, vj[4 * t], pdot); pdot = fmaf(gv.y, vj[4 * t + 1], pdot);
+        pdot = fmaf(gv.z, vj[4 * t + 2], pdot); pdot = fmaf(gv.w, vj[4 * t + 3], pdot);
+      }
+      const float p = __expf(sdot * a.scale - lse_i);
+      const uint64_t idx = (((uint64_t)b * a.H + hd) * a.L + i) * a.L + j;
+      float pd = p, dp = pdot;
+      if (a.drop.active()) {
+        const bool keep = rsx::hash_u32(a.drop.seed, idx) >= a.drop.thresh;
+        pd = keep ? p * a.drop.scale : 0.0f;
+        dp = keep ? pdot * a.drop.scale : 0.0f;
+      }
+      ds = p * (dp - sDelta[i]) * a.scale;
+#pragma unroll
+      for (int t = 0; t < V4; ++t) {
+        const float4 qv = reinterpret_cast<const float4*>(&sQ[i][0])[t];
+        const float4 gv = reinterpret_cast<const float4*>(&sdO[i][0])[t];
+        dv[4 * t] = fmaf(pd, gv.x, dv[4 * t]); dv[4 * t + 1] = fmaf(pd, gv.y, dv[4 * t + 1]);
+        dv[4 * t + 2] = fmaf(pd, gv.z, dv[4 * t + 2]); dv[4 * t + 3] = fmaf(pd, gv.w, dv[4 * t + 3]);
+        dk[4 * t] = fmaf(ds, qv.x, dk[4 * t]); dk[4 * t + 1] = fmaf(ds, qv.y, dk[4 * t + 1]);
+        dk[4 * t + 2] = fmaf(ds, qv.z, dk[4 * t + 2]); dk[4 * t + 3] = fmaf(ds, qv.w, dk[4 * t + 3]);
+      }
+    }
+    if (j < kLMax) sdS[i][j] = ds;
+  }
+  __syncthreads();
+
+  float* db = a.dqkv + (int64_t)b * a.L * 3 * D;
+  if (jok) {
+    float4* kp = reinterpret_cast<float4*>(db + (int64_t)j * 3 * D + D + hd * DH);
+    float4* vp = reinterpret_cast<float4*>(db + (int64_t)j * 3 * D + 2 * D + hd * DH);
+#pragma unroll
+    for (int t = 0; t < V4; ++t) {
+      kp[t] = make_float4(dk[4 * t], dk[4 * t + 1], dk[4 * t + 2], dk[4 * t + 3]);
+      vp[t] = make_float4(dv[4 * t], dv[4 * t + 1], dv[4 * t + 2], dv[4 * t + 3]);
+    }
+  }
+
+  // ---- pass B: lane i owns query row i: dQ_i = sum_j dS_ij K_j ----
+  const int i = lane;
+  if (i < a.L) {
+    float dq[DH];
+#pragma unroll
+    for (int e = 0; e < DH; ++e) dq[e] = 0.0f;
+    for (int jj = 0; jj < a.L; ++jj) {
+      const float ds = sdS[i][jj];
+      if (ds != 0.0f) {
+#pragma unroll
+        for (int t = 0; t < V4; ++t) {
+          const float4 kv = reinterpret_cast<const float4*>(&sK[jj][0])[t];
+          dq[4 * t] = fmaf(ds, kv.x, dq[4 * t]); dq[4 * t + 1] = fmaf(ds, kv.y, dq[4 * t + 1]);
+          dq[4 * t + 2] = fmaf(ds, kv.z, dq[4 * t + 2]); dq[4 * t + 3] = fmaf(ds, kv.w, dq[4 * t + 3]);
+        }
+      }
+    }
+    float4* qp = reinterpret_cast<float4*>(db + (int64_t)i * 3 * D + hd * DH);
+#pragma unroll
+    for (int t = 0; t < V4; ++t) qp[t] = make_float4(dq[4 * t], dq[4 * t + 1], dq[4 * t + 2], dq[4 * t + 3]);
+  }
+}
+
+}  // namespace
+
+RSX_API int rsx_mha_fwd(const float* qkv, const uint8_t* key_pad, int64_t B, int64_t L, int64_t H, int64_t Dh,
+                        int causal, float p_drop, uint64_t seed, float* out, float* lse, void* stream) {
+  RSX_ARG(qkv && out, "null tensor");
+  RSX_ARG(L >= 1 && L <= kLMax, "L must be in [1,64]");
+  RSX_ARG(Dh == 16 || Dh == 32 || Dh == 64, "head dim must be 16, 32 or 64");
+  RSX_ARG(H >= 1, "H must be >= 1");
+  RSX_ARG(p_drop >= 0.0f && p_drop < 1.0f, "p_drop must be in [0,1)");
+  if (B == 0) return 0;
+  FwdArgs a;
+  a.qkv = qkv; a.kpad = key_pad; a.out = out; a.lse = lse;
+  a.B = (int)B; a.L = (int)L; a.H = (int)H; a.causal = causal;
+  a.scale = 1.0f / sqrtf((float)Dh);
+  a.drop = rsx::make_dropout(p_drop, seed);
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)(B * H));
+  if (Dh == 16) hipLaunchKernelGGL(mha_fwd_k<16>, grid, dim3(64), 0, st, a);
+  else if (Dh == 32) hipLaunchKernelGGL(mha_fwd_k<32>, grid, dim3(64), 0, st, a);
+  else hipLaunchKernelGGL(mha_fwd_k<64>, grid, dim3(64), 0, st, a);
+  RSX_LAUNCHED();
+  return 0;
+}
+
+RSX_API int rsx_mha_bwd(const float* qkv, const uint8_t* key_pad, const float* out, const float* lse,
+                        const float* dout, int64_t B, int64_t L, int64_t H, int64_t Dh, int causal, float p_drop,
+                        uint64_t seed, float* dqkv, void* stream) {
+  RSX_ARG(qkv && out && lse && dout && dqkv, "null tensor");
+  RSX_ARG(L >= 1 && L <= kLMax, "L must be in [1,64]");
+  RSX_ARG(Dh == 16 || Dh == 32, "backward head dim must be 16 or 32");
+  RSX_ARG(p_drop >= 0.0f && p_drop < 1.0f, "p_drop must be in [0,1)");
+  if (B == 0) return 0;
+  BwdArgs a;
+  a.qkv = qkv; a.kpad = key_pad; a.out = out; a.lse = lse; a.dout = dout; a.dqkv = dqkv;
+  a.B = (int)B; a.L = (int)L; a.H = (int)H; a.causal = causal;
+  a.scale = 1.0f / sqrtf((float)Dh);
+  a.drop = rsx::make_dropout(p_drop, seed);
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)(B * H));
+  if (Dh == 16) hipLaunchKernelGGL(mha_bwd_k<16>, grid, dim3(64), 0, st, a);
+  else hipLaunchKernelGGL(mha_bwd_k<32>, grid, dim3(64), 0, st, a);
+  RSX_LAUNCHED();
+  return 0;
+}

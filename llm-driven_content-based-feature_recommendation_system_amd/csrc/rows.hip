@@ -1,0 +1,151 @@
+// Row-wise gather / scatter / L2-normalise kernels used around the towers and losses:
+//   * pretrained_lookup[item_ids]                    v1_usertower_train.py:760
+//   * F.normalize(x, p=2, dim=-1) (eps 1e-12)        v1_refine_usertower.py:504, 584-585;
+//                                                    v1_usertower_train.py:807, 811; item_tower.py:286
+//   * normalize(item_matrix)[target_ids]             v1_usertower_train.py:810-811 +
+//                                                    v1_refine_usertower.py:833 (row-wise, so only
+//                                                    the gathered rows are normalised)
+//   * output[valid_mask] / output[b, last_idx]       v1_usertower_train.py:797, 833-835
+// Every row is D fp32 owned by D/4 lanes (one float4 each): 16-B coalesced accesses.
+#include "rsx_common.h"
+
+namespace {
+
+template <int D>
+struct RowGeo {
+  static constexpr int LPR = D / 4;
+  static constexpr int RPW = 64 / LPR;
+};
+
+// out[r] = src[idx[r]] (idx nullptr => identity), optionally L2-normalised.
+template <int D, bool NORM>
+__global__ __launch_bounds__(256) void gather_rows_k(const float* __restrict__ src, int64_t ld_src,
+                                                    const int64_t* __restrict__ idx, int64_t n, float eps,
+                                                    float* __restrict__ out, float* __restrict__ nrm_out) {
+  constexpr int LPR = RowGeo<D>::LPR, RPW = RowGeo<D>::RPW;
+  const int lane = threadIdx.x & 63, sub = lane / LPR, c = lane % LPR;
+  const int64_t wave_g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t r0 = wave_g * RPW; r0 < n; r0 += nw * RPW) {
+    const int64_t r = r0 + sub;
+    const bool ok = r < n;
+    float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (ok) {
+      const int64_t s = idx ? idx[r] : r;
+      x = reinterpret_cast<const float4*>(src + s * ld_src)[c];
+    }
+    if (NORM) {
+      float ss = x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
+      ss = rsx::wave_sum_width(ss, LPR);
+      const float nv = sqrtf(ss);
+      const float dn = fmaxf(nv, eps);
+      x.x = x.x / dn; x.y = x.y / dn; x.z = x.z / dn; x.w = x.w / dn;
+      if (ok && c == 0 && nrm_out) nrm_out[r] = nv;
+    }
+    if (ok) reinterpret_cast<float4*>(out + r * D)[c] = x;
+  }
+}
+
+// Backward of y = x / max(|x|, eps):  dx = (dy - y <y,dy>) / |x|   (|x| > eps)
+//                                      dx = dy / eps                 (|x| <= eps)
+// dst row = idx[r] (nullptr => r); ATOMIC scatter-adds (duplicate indices allowed).
+template <int D, bool NORM, bool ATOMIC>
+__global__ __launch_bounds__(256) void scatter_rows_k(const float* __restrict__ dy, const float* __restrict__ y,
+                                                     const float* __restrict__ nrm, const int64_t* __restrict__ idx,
+                                                     int64_t n, float eps, float* __restrict__ dst, int64_t ld_dst,
+                                                     int accumulate, int64_t skip_idx) {
+  constexpr int LPR = RowGeo<D>::LPR, RPW = RowGeo<D>::RPW;
+  const int lane = threadIdx.x & 63, sub = lane / LPR, c = lane % LPR;
+  const int64_t wave_g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t r0 = wave_g * RPW; r0 < n; r0 += nw * RPW) {
+    const int64_t r = r0 + sub;
+    const bool ok = r < n;
+    float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (ok) g = reinterpret_cast<const float4*>(dy + r * D)[c];
+    if (NORM) {
+      float4 yv = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ok) yv = reinterpret_cast<const float4*>(y + r * D)[c];
+      float dot = yv.x * g.x + yv.y * g.y + yv.z * g.z + yv.w * g.w;
+      dot = rsx::wave_sum_width(dot, LPR);
+      const float nv = ok ? nrm[r] : 1.0f;
+      if (nv > eps) {
+        g.x = (g.x - yv.x * dot) / nv; g.y = (g.y - yv.y * dot) / nv;
+        g.z = (g.z - yv.z * dot) / nv; g.w = (g.w - yv.w * dot) / nv;
+      } else {
+        g.x = g.x / eps; g.y = g.y / eps; g.z = g.z / eps; g.w = g.w / eps;
+      }
+    }
+    if (!ok) continue;
+    const int64_t d = idx ? idx[r] : r;
+    if (d == skip_idx) continue;
+    float* p = dst + d * ld_dst + 4 * c;
+    if (ATOMIC) {
+      atomicAdd(p + 0, g.x); atomicAdd(p + 1, g.y); atomicAdd(p + 2, g.z); atomicAdd(p + 3, g.w);
+    } else if (accumulate) {
+      float4 o = *reinterpret_cast<float4*>(p);
+      o.x += g.x; o.y += g.y; o.z += g.z; o.w += g.w;
+      *reinterpret_cast<float4*>(p) = o;
+    } else {
+      *reinterpret_cast<float4*>(p) = g;
+    }
+  }
+}
+
+unsigned grid_for(int64_t n, int D) {
+  const int64_t rows_per_block = 4 * (64 / (D / 4));
+  int64_t b = (n + rows_per_block - 1) / rows_per_block;
+  if (b > 16384) b = 16384;
+  if (b < 1) b = 1;
+  return (unsigned)b;
+}
+
+}  // namespace
+
+RSX_API int rsx_gather_rows(const float* src, int64_t ld_src, const int64_t* idx, int64_t n, int64_t D, int normalize,
+                            float eps, float* out, float* nrm_out, void* stream) {
+  RSX_ARG(src && out, "null tensor");
+  RSX_ARG(D == 64 || D == 128 || D == 256, "D must be 64, 128 or 256");
+  RSX_ARG(ld_src >= D && ld_src % 4 == 0, "bad ld_src");
+  if (n == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned g = grid_for(n, (int)D);
+#define RSX_G(DD)                                                                                     \
+  if (D == DD) {                                                                                      \
+    if (normalize) hipLaunchKernelGGL((gather_rows_k<DD, true>), dim3(g), dim3(256), 0, st, src, ld_src, idx, n, eps, out, nrm_out); \
+    else hipLaunchKernelGGL((gather_rows_k<DD, false>), dim3(g), dim3(256), 0, st, src, ld_src, idx, n, eps, out, nrm_out); \
+  }
+  RSX_G(64) RSX_G(128) RSX_G(256)
+#undef RSX_G
+  RSX_LAUNCHED();
+  return 0;
+}
+
+// mode: 0 = plain store, 1 = accumulate (+=, indices must be unique), 2 = atomic scatter-add
+RSX_API int rsx_scatter_rows(const float* dy, const float* y, const float* nrm, const int64_t* idx, int64_t n,
+                             int64_t D, int normalize, float eps, int mode, int64_t skip_idx, float* dst,
+                             int64_t ld_dst, void* stream) {
+  RSX_ARG(dy && dst, "null tensor");
+  RSX_ARG(!normalize || (y && nrm), "normalize backward needs y and norms");
+  RSX_ARG(D == 64 || D == 128 || D == 256, "D must be 64, 128 or 256");
+  RSX_ARG(mode >= 0 && mode <= 2, "mode must be 0,1,2");
+  if (n == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned g = grid_for(n, (int)D);
+#define RSX_S(DD, NN, AA)                                                                           \
+  hipLaunchKernelGGL((scatter_rows_k<DD, NN, AA>), dim3(g), dim3(256), 0, st, dy, y, nrm, idx, n, eps, dst, ld_dst, \
+                     mode == 1 ? 1 : 0, skip_idx)
+#define RSX_SD(DD)                                          \
+  if (D == DD) {                                            \
+    if (normalize) {                                        \
+      if (mode == 2) RSX_S(DD, true, true); else RSX_S(DD, true, false);   \
+    } else {                                                \
+      if (mode == 2) RSX_S(DD, false, true); else RSX_S(DD, false, false); \
+    }                                                       \
+  }
+  RSX_SD(64) RSX_SD(128) RSX_SD(256)
+#undef RSX_SD
+#undef RSX_S
+  RSX_LAUNCHED();
+  return 0;
+}

@@ -1,0 +1,77 @@
+// Shared device/host helpers for the recsys_amd C-ABI library (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+namespace rsx {
+
+// Thread-local last-error text; read back through rsx_last_error().
+void set_error(const char* fmt, ...);
+
+constexpr int kWave = 64;
+
+// Counter-based dropout RNG (splitmix64 finaliser over (seed, element index)).
+// Forward and backward regenerate the identical keep-mask from the same index.
+__device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed + (idx + 1ull) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return (uint32_t)((z ^ (z >> 31)) >> 32);
+}
+
+struct Dropout {
+  uint64_t seed;
+  uint32_t thresh;  // keep iff hash >= thresh ; thresh == 0 => no dropout
+  float scale;      // 1 / (1 - p)
+  __device__ __forceinline__ bool active() const { return thresh != 0u; }
+  __device__ __forceinline__ float apply(float v, uint64_t idx) const {
+    if (thresh == 0u) return v;
+    return hash_u32(seed, idx) >= thresh ? v * scale : 0.0f;
+  }
+};
+
+inline Dropout make_dropout(float p, uint64_t seed) {
+  Dropout d;
+  d.seed = seed;
+  if (p <= 0.0f) {
+    d.thresh = 0u;
+    d.scale = 1.0f;
+  } else {
+    double t = (double)p * 4294967296.0;
+    if (t >= 4294967295.0) t = 4294967295.0;
+    d.thresh = (uint32_t)t;
+    if (d.thresh == 0u) d.thresh = 1u;
+    d.scale = 1.0f / (1.0f - p);
+  }
+  return d;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum_width(T v, int width) {
+  for (int o = width >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float fmax_nan(float a, float b) { return a > b ? a : b; }
+
+}  // namespace rsx
+
+#define RSX_ARG(cond, msg)                                   \
+  do {                                                       \
+    if (!(cond)) {                                           \
+      rsx::set_error("%s: invalid argument: %s", __func__, msg); \
+      return 1;                                              \
+    }                                                        \
+  } while (0)
+
+#define RSX_LAUNCHED()                                                        \
+  do {                                                                        \
+    hipError_t e_ = hipGetLastError();                                        \
+    if (e_ != hipSuccess) {                                                   \
+      rsx::set_error("%s: launch failed: %s", __func__, hipGetErrorString(e_)); \
+      return (int)e_;                                                         \
+    }                                                                         \
+  } while (0)
+
+#define RSX_API extern "C" __attribute__((visibility("default")))

@@ -1,0 +1,236 @@
+"""Autograd-aware wrappers over the C-ABI kernels (include/recsys_amd.h).
+
+Every function here launches HIP kernels from librecsys_amd.so on the current torch stream.
+There is no CPU path: a non-ROCm tensor raises.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _native as N
+
+NCE_PLAIN = 0
+NCE_MASK_ITEM = 2
+NCE_MASK_ITEM_USER = 6
+NCE_SUPCON = 9
+
+_NSPLIT_FWD = 8
+_NSPLIT_BWD = 8
+
+
+def next_seed() -> int:
+    """Dropout seed from torch's CPU generator (reproducible under torch.manual_seed)."""
+    return int(torch.randint(0, 2**62, (1,), dtype=torch.int64).item())
+
+
+def _c(t):
+    return t if t is None or t.is_contiguous() else t.contiguous()
+
+
+# ----------------------------------------------------------------------------------------
+# A2: fused sequence embedding (v1_refine_usertower.py:447-459)
+class _SeqEmbed(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, base, gate, pos, ln_w, ln_b, ids, cfg, *tables):
+        eps, p_drop, seed, padding_idx = cfg
+        N.ensure_device(base)
+        B, L, D = base.shape
+        base = _c(base)
+        ids = [_c(t) for t in ids]
+        tables = [_c(t) for t in tables]
+        out = torch.empty_like(base)
+        mean = torch.empty(B * L, device=base.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        gate = _c(gate)
+        rc = N.lib().rsx_seq_embed_fwd(
+            N.ptr(base), N.ptr_array(ids), N.ptr_array(tables), len(tables), N.ptr(gate), N.ptr(pos),
+            N.ptr(ln_w), N.ptr(ln_b), eps, B, L, D, p_drop, seed, N.ptr(out), N.ptr(mean), N.ptr(rstd),
+            N.stream())
+        N.check(rc, "seq_embed_fwd")
+        ctx.save_for_backward(base, gate, pos, ln_w, mean, rstd, *ids, *tables)
+        ctx.cfg = (eps, p_drop, seed, padding_idx, len(tables), B, L, D)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        eps, p_drop, seed, padding_idx, nt, B, L, D = ctx.cfg
+        saved = ctx.saved_tensors
+        base, gate, pos, ln_w, mean, rstd = saved[:6]
+        ids = list(saved[6:6 + nt])
+        tables = list(saved[6 + nt:6 + 2 * nt])
+        dout = _c(dout)
+        need = ctx.needs_input_grad
+        dbase = torch.empty_like(base) if need[0] else None
+        dgate = torch.zeros_like(gate) if need[1] else None
+        dpos = torch.zeros_like(pos) if need[2] else None
+        dlnw = torch.zeros_like(ln_w) if need[3] else None
+        dlnb = torch.zeros_like(ln_w) if need[4] else None
+        dtabs = [torch.zeros_like(t) if need[7 + j] else None for j, t in enumerate(tables)]
+        rc = N.lib().rsx_seq_embed_bwd(
+            N.ptr(base), N.ptr_array(ids), N.ptr_array(tables), N.i64_array([t.shape[0] for t in tables]),
+            N.i64_array(padding_idx), nt, N.ptr(gate), N.ptr(pos), N.ptr(ln_w), N.ptr(mean), N.ptr(rstd), eps,
+            B, L, D, p_drop, seed, N.ptr(dout), N.ptr(dbase), N.ptr_array(dtabs), N.ptr(dgate), N.ptr(dpos),
+            N.ptr(dlnw), N.ptr(dlnb), N.stream())
+        N.check(rc, "seq_embed_bwd")
+        return (dbase, dgate, dpos, dlnw, dlnb, None, None, *dtabs)
+
+
+def seq_embed(base, ids, tables, gate, pos, ln_w, ln_b, eps=1e-5, p_drop=0.0, padding_idx=None):
+    """x = base + sum_j tables[j][ids[j]] * gate[j] + pos ; LayerNorm ; dropout.
+
+    base [B, L, D]; ids/tables: lists (<= 6); gate [ntab]; pos [L, D]; ln_w/ln_b [D].
+    padding_idx: per-table row excluded from the table gradient (nn.Embedding semantics).
+    """
+    if padding_idx is None:
+        padding_idx = [-1] * len(tables)
+    padding_idx = [(-1 if p is None else int(p)) for p in padding_idx]
+    seed = next_seed() if p_drop > 0 else 0
+    cfg = (float(eps), float(p_drop), seed, padding_idx)
+    return _SeqEmbed.apply(base, gate, pos, ln_w, ln_b, list(ids), cfg, *tables)
+
+
+# ----------------------------------------------------------------------------------------
+# A3 / A9: masked MHA core
+class _MHA(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, key_pad, H, causal, p_drop, seed):
+        N.ensure_device(qkv)
+        qkv = _c(qkv)
+        B, L, D3 = qkv.shape
+        D = D3 // 3
+        Dh = D // H
+        out = torch.empty(B, L, D, device=qkv.device, dtype=torch.float32)
+        lse = torch.empty(B, H, L, device=qkv.device, dtype=torch.float32)
+        kp = None
+        if key_pad is not None:
+            kp = _c(key_pad.to(torch.uint8)) if key_pad.dtype != torch.uint8 else _c(key_pad)
+        rc = N.lib().rsx_mha_fwd(N.ptr(qkv), N.ptr(kp), B, L, H, Dh, int(causal), p_drop, seed, N.ptr(out),
+                                 N.ptr(lse), N.stream())
+        N.check(rc, "mha_fwd")
+        ctx.save_for_backward(qkv, kp, out, lse) if kp is not None else ctx.save_for_backward(qkv, out, lse)
+        ctx.has_kp = kp is not None
+        ctx.cfg = (B, L, H, Dh, int(causal), p_drop, seed)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        B, L, H, Dh, causal, p_drop, seed = ctx.cfg
+        if ctx.has_kp:
+            qkv, kp, out, lse = ctx.saved_tensors
+        else:
+            (qkv, out, lse), kp = ctx.saved_tensors, None
+        dout = _c(dout)
+        dqkv = torch.empty_like(qkv)
+        rc = N.lib().rsx_mha_bwd(N.ptr(qkv), N.ptr(kp), N.ptr(out), N.ptr(lse), N.ptr(dout), B, L, H, Dh, causal,
+                                 p_drop, seed, N.ptr(dqkv), N.stream())
+        N.check(rc, "mha_bwd")
+        return dqkv, None, None, None, None, None
+
+
+def mha(qkv, key_pad, num_heads, causal, p_drop=0.0):
+    seed = next_seed() if p_drop > 0 else 0
+    return _MHA.apply(qkv, key_pad, int(num_heads), bool(causal), float(p_drop), seed)
+
+
+# ----------------------------------------------------------------------------------------
+# Row gather (+ optional F.normalize) with scatter backward
+class _GatherRows(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, src, idx, normalize, eps, unique, skip_idx):
+        N.ensure_device(src)
+        D = src.shape[-1]
+        src2 = src.reshape(-1, D)
+        if src2.stride(1) != 1 or src2.stride(0) % 4 != 0 or src2.data_ptr() % 16 != 0:
+            src2 = src2.contiguous()
+        n = idx.numel() if idx is not None else src2.shape[0]
+        idx_c = _c(idx) if idx is not None else None
+        out = torch.empty(n, D, device=src.device, dtype=torch.float32)
+        nrm = torch.empty(n, device=src.device, dtype=torch.float32) if normalize else None
+        rc = N.lib().rsx_gather_rows(N.ptr(src2), src2.stride(0), N.ptr(idx_c), n, D, int(normalize), eps,
+                                     N.ptr(out), N.ptr(nrm), N.stream())
+        N.check(rc, "gather_rows")
+        ctx.src_shape = src.shape
+        ctx.cfg = (normalize, eps, unique, skip_idx, n, D)
+        saved = [t for t in (idx_c, out if normalize else None, nrm) if t is not None]
+        ctx.has_idx = idx_c is not None
+        ctx.save_for_backward(*saved)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        normalize, eps, unique, skip_idx, n, D = ctx.cfg
+        saved = list(ctx.saved_tensors)
+        idx = saved.pop(0) if ctx.has_idx else None
+        y = nrm = None
+        if normalize:
+            y, nrm = saved
+        dy = _c(dy)
+        rows = 1
+        for s in ctx.src_shape[:-1]:
+            rows *= s
+        if idx is None:
+            dsrc = torch.empty(rows, D, device=dy.device, dtype=torch.float32)
+            mode = 0
+        else:
+            dsrc = torch.zeros(rows, D, device=dy.device, dtype=torch.float32)
+            mode = 1 if unique else 2
+        rc = N.lib().rsx_scatter_rows(N.ptr(dy), N.ptr(y), N.ptr(nrm), N.ptr(idx), n, D, int(normalize), eps, mode,
+                                      skip_idx, N.ptr(dsrc), D, N.stream())
+        N.check(rc, "scatter_rows")
+        return dsrc.view(ctx.src_shape), None, None, None, None, None
+
+
+def gather_rows(src, idx=None, normalize=False, eps=1e-12, unique=False, skip_idx=-1):
+    """out[r] = src.view(-1, D)[idx[r]] (idx None => all rows), optionally L2-normalised."""
+    return _GatherRows.apply(src, idx, bool(normalize), float(eps), bool(unique), int(skip_idx))
+
+
+def l2_normalize(x, eps=1e-12):
+    """F.normalize(x, p=2, dim=-1) on the last dim."""
+    shape = x.shape
+    return gather_rows(x, None, normalize=True, eps=eps).view(shape)
+
+
+# ----------------------------------------------------------------------------------------
+# A6 / A7 / A12: fused contrastive cross-entropy
+class _NCE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, A, B, bias, k1a, k1b, k2a, k2b, tau, flags):
+        N.ensure_device(A)
+        A = _c(A)
+        B = _c(B)
+        n, m = A.shape[0], B.shape[0]
+        nws = N.lib().rsx_nce_workspace_floats(n, m, _NSPLIT_FWD, _NSPLIT_BWD)
+        ws = torch.empty(nws, device=A.device, dtype=torch.float32)
+        out2 = torch.empty(2, device=A.device, dtype=torch.float32)
+        keys = [_c(k) for k in (k1a, k1b, k2a, k2b)]
+        rc = N.lib().rsx_nce_fwd(N.ptr(A), N.ptr(B), N.ptr(bias), *[N.ptr(k) for k in keys], n, m, A.stride(0),
+                                 B.stride(0), tau, flags, _NSPLIT_FWD, N.ptr(ws), N.ptr(out2), N.stream())
+        N.check(rc, "nce_fwd")
+        ctx.save_for_backward(A, B, bias, *keys, ws, out2)
+        ctx.cfg = (n, m, tau, flags)
+        return out2[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        A, B, bias, k1a, k1b, k2a, k2b, ws, out2 = ctx.saved_tensors
+        n, m, tau, flags = ctx.cfg
+        g = _c(g.reshape(1).to(torch.float32))
+        dA = torch.empty_like(A) if ctx.needs_input_grad[0] else None
+        dB = torch.empty_like(B) if ctx.needs_input_grad[1] else None
+        rc = N.lib().rsx_nce_bwd(N.ptr(A), N.ptr(B), N.ptr(bias), N.ptr(k1a), N.ptr(k1b), N.ptr(k2a), N.ptr(k2b),
+                                 n, m, A.stride(0), B.stride(0), tau, flags, _NSPLIT_FWD, _NSPLIT_BWD, N.ptr(g),
+                                 N.ptr(out2), N.ptr(ws), N.ptr(dA), N.ptr(dB), 0, N.stream())
+        N.check(rc, "nce_bwd")
+        return dA, dB, None, None, None, None, None, None, None
+
+
+def _i32(t):
+    return None if t is None else t.to(torch.int32)
+
+
+def nce_loss(A, B, bias=None, k1a=None, k1b=None, k2a=None, k2b=None, tau=0.1, flags=NCE_PLAIN):
+    """Mean InfoNCE over rows of S = A B^T / tau - bias (see include/recsys_amd.h)."""
+    if bias is not None:
+        bias = _c(bias.to(torch.float32))
+    return _NCE.apply(A, B, bias, _i32(k1a), _i32(k1b), _i32(k2a), _i32(k2b), float(tau), int(flags))

@@ -1,0 +1,150 @@
+"""Seeded synthetic H&M-shaped inputs for the user-tower contrastive step.
+
+Layout contract follows the reference's producers:
+  * SASRecDataset.__getitem__   tower_code/v1_refine_usertower.py:204-306
+      left padding with 0 to max_len, input = seq[:-1], target = seq[1:] of the last
+      max_len+1 purchases, padding_mask True = pad, time buckets 1..9 (0 = pad)
+  * item side ids (md5 % 1000 + 1)  tower_code/v1_usertower_train.py:211-262
+  * aligned pretrained matrix row 0 = 0  tower_code/v1_usertower_train.py:137-139
+  * FeatureProcessor.get_logq_probs   tower_code/v1_refine_usertower.py:124-137
+Sequence lengths are drawn from the purchase counts of the 100 customers in the
+reference's sample file staticstics/customer_sample_view.json (data, not code).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+# purchase counts of the 100 customers in staticstics/customer_sample_view.json
+SAMPLE_PURCHASE_COUNTS = np.array([
+    10, 32, 11, 48, 10, 2, 10, 3, 5, 29, 5, 20, 9, 8, 1, 45, 112, 2, 58, 2, 8, 7, 426, 38, 30, 24, 8, 187, 3,
+    27, 8, 41, 155, 9, 6, 10, 15, 8, 2, 26, 5, 2, 105, 28, 4, 2, 49, 1, 24, 4, 5, 4, 2, 8, 34, 36, 56, 3, 69,
+    3, 25, 5, 51, 6, 3, 3, 75, 19, 73, 15, 18, 3, 4, 2, 35, 10, 8, 29, 5, 50, 3, 107, 5, 25, 150, 31, 44, 2, 17,
+    2, 13, 6, 6, 4, 8, 56, 24, 26, 19, 21], dtype=np.int64)
+
+# time-bucket histogram (buckets 1..9) of the same sample
+TIME_BUCKET_HIST = np.array([327, 30, 40, 75, 152, 404, 383, 115, 420], dtype=np.float64)
+
+H_AND_M_ITEMS = 47_062
+HASH_SIZE = 1000
+
+
+@dataclass
+class SynthConfig:
+    batch_size: int = 4096
+    max_len: int = 50
+    num_items: int = H_AND_M_ITEMS
+    d_model: int = 128
+    zipf_s: float = 1.0
+    seed: int = 0
+
+
+def zipf_probs(num_items: int, s: float) -> np.ndarray:
+    ranks = np.arange(1, num_items + 1, dtype=np.float64)
+    p = ranks ** (-s)
+    return p / p.sum()
+
+
+def logq_from_probs(raw_probs: np.ndarray) -> torch.Tensor:
+    """FeatureProcessor.get_logq_probs (v1_refine_usertower.py:124-137) on given raw probs."""
+    eps = 1e-6
+    p = np.nan_to_num(raw_probs, nan=0.0) + eps
+    p = p / p.sum()
+    lq = np.log(p).astype(np.float32)
+    full = np.zeros(len(raw_probs) + 1, dtype=np.float32)
+    full[1:] = lq
+    full[0] = -20.0
+    return torch.from_numpy(full)
+
+
+@dataclass
+class ItemUniverse:
+    pretrained: torch.Tensor  # [I+1, d] aligned pretrained matrix (row 0 = 0), L2-normalised rows
+    side: torch.Tensor        # [I+1, 4] int64 type/color/graphic/section ids (row 0 = 0)
+    log_q: torch.Tensor       # [I+1] float32
+    probs: np.ndarray         # [I] item popularity used for sampling
+
+
+def make_items(num_items: int = H_AND_M_ITEMS, d: int = 128, zipf_s: float = 1.0, seed: int = 0) -> ItemUniverse:
+    g = torch.Generator().manual_seed(seed)
+    w = torch.randn(num_items + 1, d, generator=g)
+    w = w / w.norm(dim=1, keepdim=True)
+    w[0] = 0.0
+    side = torch.randint(1, HASH_SIZE + 1, (num_items + 1, 4), generator=g, dtype=torch.int64)
+    side[0] = 0
+    probs = zipf_probs(num_items, zipf_s)
+    return ItemUniverse(pretrained=w, side=side, log_q=logq_from_probs(probs), probs=probs)
+
+
+def make_batch(items: ItemUniverse, batch_size: int, max_len: int = 50, seed: int = 0,
+               device: str | torch.device = "cpu") -> dict:
+    """One SASRecDataset-shaped training batch (is_train=True), as a dict of tensors."""
+    rng = np.random.default_rng(seed)
+    B, L = batch_size, max_len
+    counts = rng.choice(SAMPLE_PURCHASE_COUNTS, size=B)
+    # last max_len+1 purchases -> valid length = min(max(count-1, 1), L)  (len==1 keeps input=target)
+    seq_len_total = np.minimum(counts, L + 1)
+    item_ids = np.zeros((B, L), dtype=np.int64)
+    target_ids = np.zeros((B, L), dtype=np.int64)
+    time_ids = np.zeros((B, L), dtype=np.int64)
+    pad = np.ones((B, L), dtype=bool)
+    tb_p = TIME_BUCKET_HIST / TIME_BUCKET_HIST.sum()
+    n_items = len(items.probs)
+    total = int(seq_len_total.sum())
+    all_items = rng.choice(n_items, size=total, p=items.probs) + 1
+    all_tb = rng.choice(9, size=total, p=tb_p) + 1
+    offs = np.concatenate([[0], np.cumsum(seq_len_total)])
+    for b in range(B):
+        n = int(seq_len_total[b])
+        seq = all_items[offs[b]:offs[b] + n]
+        tb = all_tb[offs[b]:offs[b] + n]
+        if n > 1:
+            inp, tgt, tin = seq[:-1], seq[1:], tb[:-1]
+        else:
+            inp, tgt, tin = seq, seq, tb
+        k = len(inp)
+        item_ids[b, L - k:] = inp
+        target_ids[b, L - k:] = tgt
+        time_ids[b, L - k:] = tin
+        pad[b, L - k:] = False
+    side = items.side.numpy()[item_ids]  # padding (0) -> row 0 = (0,0,0,0)
+    batch = {
+        "user_ids": [f"u{seed}_{b}" for b in range(B)],
+        "item_ids": torch.from_numpy(item_ids),
+        "target_ids": torch.from_numpy(target_ids),
+        "padding_mask": torch.from_numpy(pad),
+        "time_bucket_ids": torch.from_numpy(time_ids),
+        "type_ids": torch.from_numpy(side[..., 0].copy()),
+        "color_ids": torch.from_numpy(side[..., 1].copy()),
+        "graphic_ids": torch.from_numpy(side[..., 2].copy()),
+        "section_ids": torch.from_numpy(side[..., 3].copy()),
+        "age_bucket": torch.from_numpy(rng.integers(1, 11, B)),
+        "price_bucket": torch.from_numpy(rng.integers(1, 11, B)),
+        "cnt_bucket": torch.from_numpy(rng.integers(1, 11, B)),
+        "recency_bucket": torch.from_numpy(rng.integers(1, 11, B)),
+        "channel_ids": torch.from_numpy(rng.integers(1, 3, B)),
+        "club_status_ids": torch.from_numpy(rng.integers(0, 3, B)),
+        "news_freq_ids": torch.from_numpy(rng.integers(0, 2, B)),
+        "fn_ids": torch.from_numpy(rng.integers(0, 2, B)),
+        "active_ids": torch.from_numpy(rng.integers(0, 2, B)),
+        "cont_feats": torch.from_numpy(rng.standard_normal((B, 4)).astype(np.float32)),
+    }
+    if str(device) != "cpu":
+        batch = {k: (v.to(device, non_blocking=True) if torch.is_tensor(v) else v) for k, v in batch.items()}
+    return batch
+
+
+FORWARD_KEYS = ("item_ids", "time_bucket_ids", "type_ids", "color_ids", "graphic_ids", "section_ids",
+                "age_bucket", "price_bucket", "cnt_bucket", "recency_bucket", "channel_ids", "club_status_ids",
+                "news_freq_ids", "fn_ids", "active_ids", "cont_feats", "padding_mask")
+
+
+def forward_kwargs(batch: dict, pretrained_vecs: torch.Tensor, training_mode: bool = True) -> dict:
+    """The kwargs dict train_user_tower_all_time builds (v1_usertower_train.py:762-782)."""
+    kw = {"pretrained_vecs": pretrained_vecs}
+    for k in FORWARD_KEYS:
+        kw[k] = batch[k]
+    kw["training_mode"] = training_mode
+    return kw

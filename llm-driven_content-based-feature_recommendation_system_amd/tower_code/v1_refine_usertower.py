@@ -1,0 +1,191 @@
+"""Drop-in for tower_code/v1_refine_usertower.py: SASRecUserTower and its losses.
+
+Same constructor arguments, parameter names/shapes/init (so state_dicts load both ways)
+and forward signature as the reference; the forward runs on the MI355X kernels of
+librecsys_amd.so:
+  * embedding stage (gathers + gated sum + pos + LayerNorm + dropout): rsx_seq_embed_*
+  * masked self-attention core of each encoder layer:                  rsx_mha_*
+  * final F.normalize:                                                  rsx_gather_rows
+  * losses (no N x N materialisation, fp32 MFMA):                       rsx_nce_*
+Dense projections (item_proj, in/out_proj, FFN, static MLP, output_proj) are plain GEMMs
+issued through torch (hipBLASLt).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+
+
+class SASRecUserTower(nn.Module):
+    """Reference: tower_code/v1_refine_usertower.py:312-510."""
+
+    def __init__(self, args):
+        super().__init__()
+        self.d_model = args.d_model
+        self.max_len = args.max_len
+        self.dropout_rate = args.dropout
+
+        # Module construction order == reference (:322-399), so torch.manual_seed gives
+        # bit-identical initial weights.
+        self.item_proj = nn.Linear(args.pretrained_dim, self.d_model)
+        self.item_id_emb = nn.Embedding(args.num_items + 1, self.d_model, padding_idx=0)
+        self.type_emb = nn.Embedding(args.num_prod_types + 1, self.d_model, padding_idx=0)
+        self.color_emb = nn.Embedding(args.num_colors + 1, self.d_model, padding_idx=0)
+        self.graphic_emb = nn.Embedding(args.num_graphics + 1, self.d_model, padding_idx=0)
+        self.section_emb = nn.Embedding(args.num_sections + 1, self.d_model, padding_idx=0)
+        self.pos_emb = nn.Embedding(self.max_len, self.d_model)
+        self.seq_gate = nn.Parameter(torch.ones(6))
+        self.static_gate = nn.Parameter(torch.ones(10))
+        num_time_buckets = 12
+        self.time_emb = nn.Embedding(num_time_buckets, self.d_model, padding_idx=0)
+        self.emb_ln = nn.LayerNorm(self.d_model)
+        self.emb_dropout = nn.Dropout(self.dropout_rate)
+
+        encoder_layer = nn.TransformerEncoderLayer(
+            d_model=self.d_model, nhead=args.nhead, dim_feedforward=self.d_model * 2, dropout=self.dropout_rate,
+            activation="gelu", norm_first=True, batch_first=True)
+        self.transformer_encoder = nn.TransformerEncoder(encoder_layer, num_layers=args.num_layers,
+                                                         enable_nested_tensor=False)
+
+        mid_dim, low_dim = 16, 4
+        self.age_emb = nn.Embedding(11, mid_dim, padding_idx=0)
+        self.price_emb = nn.Embedding(11, mid_dim, padding_idx=0)
+        self.cnt_emb = nn.Embedding(11, mid_dim, padding_idx=0)
+        self.recency_emb = nn.Embedding(11, mid_dim, padding_idx=0)
+        self.channel_emb = nn.Embedding(4, low_dim, padding_idx=0)
+        self.club_status_emb = nn.Embedding(4, low_dim, padding_idx=0)
+        self.news_freq_emb = nn.Embedding(3, low_dim, padding_idx=0)
+        self.fn_emb = nn.Embedding(3, low_dim, padding_idx=0)
+        self.active_emb = nn.Embedding(3, low_dim, padding_idx=0)
+        self.num_cont_feats = 4
+        cont_proj_dim = 16
+        self.cont_proj = nn.Linear(self.num_cont_feats, cont_proj_dim)
+        total_static_input_dim = (mid_dim * 4) + (low_dim * 5) + cont_proj_dim
+        self.static_mlp = nn.Sequential(
+            nn.Linear(total_static_input_dim, self.d_model), nn.LayerNorm(self.d_model), nn.GELU(),
+            nn.Dropout(self.dropout_rate))
+        self.output_proj = nn.Sequential(
+            nn.Linear(self.d_model * 2, self.d_model), nn.LayerNorm(self.d_model), nn.GELU(),
+            nn.Linear(self.d_model, self.d_model))
+        self.apply(self._init_weights)
+        self.register_buffer("_seq_gate_mask", torch.tensor([1.0, 1.0, 0.0, 0.0, 0.0, 0.0]), persistent=False)
+
+    def _init_weights(self, module):
+        # reference :403-412 (note: embedding padding rows are re-initialised, i.e. non-zero)
+        if isinstance(module, nn.Linear):
+            nn.init.kaiming_normal_(module.weight, mode="fan_in", nonlinearity="relu")
+            if module.bias is not None:
+                nn.init.constant_(module.bias, 0)
+        elif isinstance(module, nn.Embedding):
+            nn.init.normal_(module.weight, mean=0.0, std=0.02)
+        elif isinstance(module, nn.LayerNorm):
+            nn.init.constant_(module.bias, 0)
+            nn.init.constant_(module.weight, 1.0)
+
+    def get_causal_mask(self, seq_len, device):
+        return torch.triu(torch.ones(seq_len, seq_len, device=device, dtype=torch.bool), diagonal=1)
+
+    # -- encoder layer (norm_first=True, gelu): reference nn.TransformerEncoderLayer semantics
+    def _encoder_layer(self, layer: nn.TransformerEncoderLayer, x, key_pad, p):
+        sa = layer.self_attn
+        h = F.layer_norm(x, (self.d_model,), layer.norm1.weight, layer.norm1.bias, layer.norm1.eps)
+        qkv = F.linear(h, sa.in_proj_weight, sa.in_proj_bias)
+        a = ops.mha(qkv, key_pad, sa.num_heads, causal=True, p_drop=p)
+        a = F.linear(a, sa.out_proj.weight, sa.out_proj.bias)
+        x = x + F.dropout(a, p, self.training)
+        h = F.layer_norm(x, (self.d_model,), layer.norm2.weight, layer.norm2.bias, layer.norm2.eps)
+        f = F.linear(F.dropout(F.gelu(F.linear(h, layer.linear1.weight, layer.linear1.bias)), p, self.training),
+                     layer.linear2.weight, layer.linear2.bias)
+        return x + F.dropout(f, p, self.training)
+
+    def forward(self, pretrained_vecs, item_ids, time_bucket_ids, type_ids, color_ids, graphic_ids, section_ids,
+                age_bucket, price_bucket, cnt_bucket, recency_bucket, channel_ids, club_status_ids, news_freq_ids,
+                fn_ids, active_ids, cont_feats, padding_mask=None, training_mode=True):
+        B, seq_len = item_ids.shape
+        p = self.dropout_rate if self.training else 0.0
+
+        s_g = torch.sigmoid(self.seq_gate) * self._seq_gate_mask
+        u_g = torch.sigmoid(self.static_gate)
+
+        # Phase 1: sequence encoding (reference :447-466)
+        base = F.linear(pretrained_vecs, self.item_proj.weight, self.item_proj.bias)
+        x = ops.seq_embed(
+            base,
+            [item_ids, time_bucket_ids, type_ids, color_ids, graphic_ids, section_ids],
+            [self.item_id_emb.weight, self.time_emb.weight, self.type_emb.weight, self.color_emb.weight,
+             self.graphic_emb.weight, self.section_emb.weight],
+            s_g, self.pos_emb.weight[:seq_len], self.emb_ln.weight, self.emb_ln.bias, eps=self.emb_ln.eps,
+            p_drop=p, padding_idx=[0, 0, 0, 0, 0, 0])
+        for layer in self.transformer_encoder.layers:
+            x = self._encoder_layer(layer, x, padding_mask, p)
+        output = x
+
+        # Phase 2: static encoding (reference :472-494)
+        static_input = torch.cat([
+            self.age_emb(age_bucket) * u_g[0], self.price_emb(price_bucket) * u_g[1],
+            self.cnt_emb(cnt_bucket) * u_g[2], self.recency_emb(recency_bucket) * u_g[3],
+            self.channel_emb(channel_ids) * u_g[4], self.club_status_emb(club_status_ids) * u_g[5],
+            self.news_freq_emb(news_freq_ids) * u_g[6], self.fn_emb(fn_ids) * u_g[7],
+            self.active_emb(active_ids) * u_g[8], F.relu(self.cont_proj(cont_feats)) * u_g[9]], dim=1)
+        user_profile_vec = self.static_mlp(static_input)
+
+        # Phase 3: late fusion (reference :499-510). Linear(cat[a, b]) = a W_a^T + (b W_b^T + bias):
+        # the per-user profile half is computed once per user and broadcast over L.
+        lin0, ln, lin3 = self.output_proj[0], self.output_proj[1], self.output_proj[3]
+        D = self.d_model
+        w_seq, w_prof = lin0.weight[:, :D], lin0.weight[:, D:]
+        prof = F.linear(user_profile_vec, w_prof, lin0.bias)
+        if training_mode:
+            h = F.linear(output, w_seq) + prof.unsqueeze(1)
+        else:
+            h = F.linear(output[:, -1, :], w_seq) + prof
+        h = F.gelu(F.layer_norm(h, (D,), ln.weight, ln.bias, ln.eps))
+        final_vec = F.linear(h, lin3.weight, lin3.bias)
+        return ops.l2_normalize(final_vec)
+
+
+# ==========================================
+# Losses (reference :520-861). The live inbatch_corrected_logq_loss is the second
+# definition (:826); the first (:520) is shadowed at import time in the reference too.
+# ==========================================
+def _as_keys(t):
+    return t.reshape(-1).to(torch.int32)
+
+
+def inbatch_corrected_logq_loss(user_emb, item_tower_emb, target_ids, user_ids, log_q_tensor, temperature=0.1,
+                                lambda_logq=1.0):
+    """Reference :826-861. item_tower_emb is the (already normalised) full item matrix."""
+    tgt = target_ids.reshape(-1)
+    batch_item_emb = ops.gather_rows(item_tower_emb, tgt)
+    bias = None
+    if lambda_logq > 0.0:
+        bias = log_q_tensor[tgt] * lambda_logq
+    k1 = _as_keys(tgt)
+    k2 = _as_keys(user_ids)
+    return ops.nce_loss(user_emb, batch_item_emb, bias, k1, k1, k2, k2, tau=temperature,
+                        flags=ops.NCE_MASK_ITEM_USER)
+
+
+def inbatch_corrected_logq_loss_no_user(user_emb, item_tower_emb, target_ids, log_q_tensor, temperature=0.1,
+                                        lambda_logq=1.0):
+    """The shadowed first definition (reference :520-573): same-item masking only."""
+    tgt = target_ids.reshape(-1)
+    batch_item_emb = ops.gather_rows(item_tower_emb, tgt)
+    bias = log_q_tensor[tgt] * lambda_logq if lambda_logq > 0.0 else None
+    k1 = _as_keys(tgt)
+    return ops.nce_loss(user_emb, batch_item_emb, bias, k1, k1, tau=temperature, flags=ops.NCE_MASK_ITEM)
+
+
+def duorec_loss_refined(user_emb_1, user_emb_2, target_ids, temperature=0.1, lambda_sup=0.1):
+    """Reference :576-627 (InfoNCE between views + lambda_sup * SupCon on same targets)."""
+    z_i = ops.l2_normalize(user_emb_1)
+    z_j = ops.l2_normalize(user_emb_2)
+    loss_unsup = ops.nce_loss(z_i, z_j, tau=temperature, flags=ops.NCE_PLAIN)
+    if lambda_sup > 0:
+        k = _as_keys(target_ids)
+        loss_sup = ops.nce_loss(z_i, z_i, None, k, k, tau=temperature, flags=ops.NCE_SUPCON)
+        return loss_unsup + lambda_sup * loss_sup
+    return loss_unsup + lambda_sup * torch.zeros((), device=z_i.device)

@@ -1,0 +1,221 @@
+"""Drop-in for tower_code/v1_usertower_train.py: config, item matrix, contrastive train step.
+
+The step (`contrastive_step`) is the hot path named by BASELINE.json: two dropout views of
+SASRecUserTower, the all-time-steps LogQ in-batch loss with same-item/same-user masking,
+the DuoRec term on the (bug-compatible) "last" index, backward, clip_grad_norm_(5.0) and
+AdamW. `train_user_tower_all_time` keeps the reference signature and loops it.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from .v1_refine_usertower import SASRecUserTower, duorec_loss_refined, inbatch_corrected_logq_loss
+
+try:  # the reference hard-imports wandb (v1_usertower_train.py:14); here it is optional
+    import wandb  # type: ignore
+except Exception:  # pragma: no cover - not installed in this image
+    wandb = None
+
+
+@dataclass
+class PipelineConfig:
+    """Reference :21-60 (paths default to local dirs instead of the author's Windows paths)."""
+    base_dir: str = "localprops"
+    model_dir: str = "models"
+    batch_size: int = 768
+    lr: float = 5e-4
+    weight_decay: float = 1e-4
+    epochs: int = 15
+    d_model: int = 128
+    max_len: int = 50
+    dropout: float = 0.2
+    pretrained_dim: int = 128
+    nhead: int = 4
+    num_layers: int = 2
+    lambda_logq: float = 1.0
+    lambda_sup: float = 0.1
+    lambda_cl: float = 0.2
+    top_k_percent: float = 0.01
+    hnm_threshold: float = 0.90
+    hard_margin: float = 0.01
+    freeze_item_tower: bool = True
+    item_tower_pth_name: str = "encoder_ep03_loss0.8129.pth"
+    num_items: int = 0
+    num_prod_types: int = 0
+    num_colors: int = 0
+    num_graphics: int = 0
+    num_sections: int = 0
+    num_age_groups: int = 10
+
+
+class SASRecItemTower(nn.Module):
+    """Reference :266-293 (learnable item matrix + log_q buffer)."""
+
+    def __init__(self, num_items, d_model, log_q_tensor=None):
+        super().__init__()
+        self.item_matrix = nn.Embedding(num_items + 1, d_model, padding_idx=0)
+        if log_q_tensor is not None:
+            self.register_buffer("log_q", log_q_tensor)
+        else:
+            self.register_buffer("log_q", torch.zeros(num_items + 1))
+
+    def get_all_embeddings(self):
+        return self.item_matrix.weight
+
+    def get_log_q(self):
+        return self.log_q
+
+    def set_freeze_state(self, freeze: bool):
+        for param in self.parameters():
+            param.requires_grad = not freeze
+
+    def init_from_pretrained(self, pretrained_vecs):
+        with torch.no_grad():
+            self.item_matrix.weight.copy_(pretrained_vecs)
+
+
+def setup_models(cfg: PipelineConfig, device, item_state_dict=None, log_q_tensor=None):
+    """Reference :295-328."""
+    user_tower = SASRecUserTower(cfg).to(device)
+    item_tower = SASRecItemTower(num_items=cfg.num_items, d_model=cfg.d_model, log_q_tensor=log_q_tensor).to(device)
+    if item_state_dict is not None:
+        item_tower.load_state_dict(item_state_dict, strict=False)
+    item_tower.set_freeze_state(cfg.freeze_item_tower)
+    return user_tower, item_tower
+
+
+_FWD_KEYS = ("item_ids", "time_bucket_ids", "type_ids", "color_ids", "graphic_ids", "section_ids", "age_bucket",
+             "price_bucket", "cnt_bucket", "recency_bucket", "channel_ids", "club_status_ids", "news_freq_ids",
+             "fn_ids", "active_ids", "cont_feats", "padding_mask")
+
+
+def lookup_pretrained(pretrained_lookup: torch.Tensor, item_ids: torch.Tensor) -> torch.Tensor:
+    """pretrained_lookup[item_ids] (reference :760 does it on the CPU + H2D; here the aligned
+    matrix stays resident in HBM and rows are gathered by rsx_gather_rows)."""
+    B, L = item_ids.shape
+    return ops.gather_rows(pretrained_lookup, item_ids.reshape(-1)).view(B, L, -1)
+
+
+def contrastive_losses(model, item_tower, log_q_tensor, batch, cfg, pretrained_vecs):
+    """Forward of one step (reference :787-845). Returns (total, main, cl)."""
+    device = batch["item_ids"].device
+    kw = {k: batch[k] for k in _FWD_KEYS}
+    kw["pretrained_vecs"] = pretrained_vecs
+    kw["training_mode"] = True
+    output_1 = model(**kw)
+    output_2 = model(**kw)
+
+    padding_mask = batch["padding_mask"]
+    target_ids = batch["target_ids"]
+    batch_size, seq_len = batch["item_ids"].shape
+    D = output_1.shape[-1]
+    valid_mask = ~padding_mask
+    flat_pos = valid_mask.reshape(-1).nonzero().squeeze(1)  # row-major (b, t) order, as output_1[valid_mask]
+    if flat_pos.numel() > 0:
+        # flat_output = output_1[valid_mask]; F.normalize(flat_output) -- one fused gather+normalise
+        flat_user_emb = ops.gather_rows(output_1.reshape(-1, D), flat_pos, normalize=True, unique=True)
+        flat_targets = target_ids.reshape(-1)[flat_pos]
+        flat_user_ids = torch.div(flat_pos, seq_len, rounding_mode="floor")
+        # norm_item_embeddings[flat_targets] == normalize(item_matrix[flat_targets]) row-wise
+        batch_item_emb = ops.gather_rows(item_tower.get_all_embeddings(), flat_targets, normalize=True)
+        bias = log_q_tensor[flat_targets] * cfg.lambda_logq if cfg.lambda_logq > 0.0 else None
+        k1 = flat_targets.to(torch.int32)
+        k2 = flat_user_ids.to(torch.int32)
+        main_loss = ops.nce_loss(flat_user_emb, batch_item_emb, bias, k1, k1, k2, k2, tau=0.1,
+                                 flags=ops.NCE_MASK_ITEM_USER)
+    else:
+        main_loss = torch.zeros((), device=device)
+
+    # DuoRec on the "last" step: count_valid - 1 (bug-compatible on left-padded rows, :830-835)
+    last_indices = (valid_mask.sum(dim=1) - 1).clamp(min=0)
+    rows = torch.arange(batch_size, device=device) * seq_len + last_indices
+    last_output_1 = ops.gather_rows(output_1.reshape(-1, D), rows, unique=True)
+    last_output_2 = ops.gather_rows(output_2.reshape(-1, D), rows, unique=True)
+    last_targets = target_ids.reshape(-1)[rows]
+    cl_loss = duorec_loss_refined(last_output_1, last_output_2, last_targets, lambda_sup=cfg.lambda_sup)
+    total_loss = main_loss + cfg.lambda_cl * cl_loss
+    return total_loss, main_loss, cl_loss
+
+
+def contrastive_step(model, item_tower, log_q_tensor, batch, optimizer, scaler, cfg, pretrained_lookup=None,
+                     max_norm=5.0, grad_sync=None):
+    """One full training step (forward x2, losses, backward, clip, AdamW). No host sync
+    except the valid-position count. Returns detached (total, main, cl) loss tensors.
+    grad_sync: optional callable run between backward and clipping (data-parallel all-reduce)."""
+    optimizer.zero_grad(set_to_none=True)
+    pv = batch.get("pretrained_vecs")
+    if pv is None:
+        pv = lookup_pretrained(pretrained_lookup, batch["item_ids"])
+    total, main, cl = contrastive_losses(model, item_tower, log_q_tensor, batch, cfg, pv)
+    if scaler is not None and scaler.is_enabled():
+        scaler.scale(total).backward()
+        if grad_sync is not None:
+            grad_sync()
+        scaler.unscale_(optimizer)
+        torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=max_norm)
+        scaler.step(optimizer)
+        scaler.update()
+    else:
+        total.backward()
+        if grad_sync is not None:
+            grad_sync()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=max_norm)
+        optimizer.step()
+    return total.detach(), main.detach(), cl.detach()
+
+
+def _to_device(batch, device):
+    return {k: (v.to(device, non_blocking=True) if torch.is_tensor(v) else v) for k, v in batch.items()}
+
+
+def train_user_tower_all_time(epoch, model, item_tower, log_q_tensor, dataloader, optimizer, scaler, cfg, device,
+                              seq_labels=None, static_labels=None):
+    """Reference :717-893 (same signature; wandb logging only if wandb is importable)."""
+    model.train()
+    total_acc = main_acc = cl_acc = 0.0
+    lookup = getattr(getattr(dataloader, "dataset", None), "pretrained_lookup", None)
+    if lookup is not None and lookup.device != torch.device(device):
+        lookup = lookup.to(device)
+    n = 0
+    for batch_idx, batch in enumerate(dataloader):
+        batch = _to_device(batch, device)
+        total, main, cl = contrastive_step(model, item_tower, log_q_tensor, batch, optimizer, scaler, cfg,
+                                           pretrained_lookup=lookup)
+        total_acc += total.item()
+        main_acc += main.item()
+        cl_acc += cl.item()
+        n += 1
+        if wandb is not None and batch_idx % 100 == 0 and getattr(wandb, "run", None) is not None:
+            wandb.log({"Train/Main_Loss_Step": main.item(), "Train/CL_Loss_Step": cl.item(),
+                       "Step": epoch * len(dataloader) + batch_idx})
+    avg = total_acc / max(n, 1)
+    print(f"Epoch {epoch} Completed | Avg Total: {avg:.4f} (Main: {main_acc / max(n, 1):.4f}, "
+          f"CL: {cl_acc / max(n, 1):.4f})")
+    return avg
+
+
+def load_aligned_pretrained_embeddings(processor, model_dir, pretrained_dim):
+    """Reference :131-160 (torch.load with weights_only=True)."""
+    emb_path = os.path.join(model_dir, "pretrained_item_matrix.pt")
+    ids_path = os.path.join(model_dir, "item_ids.pt")
+    num_embeddings = processor.num_items + 1
+    aligned_weight = torch.randn(num_embeddings, pretrained_dim) * 0.01
+    aligned_weight[0] = 0.0
+    try:
+        pretrained_emb = torch.load(emb_path, map_location="cpu", weights_only=True)
+        if isinstance(pretrained_emb, dict):
+            pretrained_emb = pretrained_emb.get("weight", pretrained_emb.get("item_content_emb.weight"))
+        pretrained_ids = torch.load(ids_path, map_location="cpu", weights_only=True)
+        pretrained_map = {str(iid.item()) if isinstance(iid, torch.Tensor) else str(iid): pretrained_emb[idx]
+                          for idx, iid in enumerate(pretrained_ids)}
+        for i, current_id_str in enumerate(processor.item_ids):
+            if current_id_str in pretrained_map:
+                aligned_weight[i + 1] = pretrained_map[current_id_str]
+    except Exception as e:  # same fallback as the reference
+        print(f"[Warning] Failed to load Pretrained files: {e}. Using random init.")
+    return aligned_weight

@@ -1,0 +1,240 @@
+"""Kernel-level parity: librecsys_amd.so (cuda:0) vs the CPU oracle / float64 restatements.
+
+Tolerances (fp32 kernels vs CPU): gathers bit-exact; LayerNorm outputs 1e-6 abs;
+logits / losses 1e-4 abs (north-star bound: fp32 logits within 1e-4); gradients 1e-5 abs
++ 1e-4 rel unless stated.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+import recsys_amd  # noqa: F401
+from recsys_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+
+# ------------------------------------------------------------------ seq embed (A2)
+def _embed_inputs(B=37, L=50, D=128, rows=(301, 12, 51, 51, 51, 51), seed=0):
+    g = torch.Generator().manual_seed(seed)
+    base = torch.randn(B, L, D, generator=g)
+    tables = [torch.randn(r, D, generator=g) * 0.02 for r in rows]
+    ids = [torch.randint(0, r, (B, L), generator=g) for r in rows]
+    pad = torch.rand(B, L, generator=g) < 0.4
+    for t in ids:
+        t[pad] = 0
+    gate = torch.sigmoid(torch.randn(6, generator=g)) * torch.tensor([1.0, 1.0, 0.0, 0.0, 0.0, 0.0])
+    pos = torch.randn(L, D, generator=g) * 0.02
+    lw = 1 + 0.1 * torch.randn(D, generator=g)
+    lb = 0.1 * torch.randn(D, generator=g)
+    return base, tables, ids, gate, pos, lw, lb
+
+
+def _embed_ref(base, tables, ids, gate, pos):
+    x = base.clone()
+    for t, i, gj in zip(tables, ids, gate):
+        x += t[i] * gj           # same op order as v1_refine_usertower.py:447-453
+    x += pos.unsqueeze(0)
+    return x
+
+
+def test_seq_embed_gather_bit_exact(gpu):
+    base, tables, ids, gate, pos, lw, lb = _embed_inputs()
+    ref = _embed_ref(base, tables, ids, gate, pos)
+    d = lambda t: t.to(gpu)
+    out = ops.seq_embed(d(base), [d(i) for i in ids], [d(t) for t in tables], d(gate), d(pos), None, None)
+    assert torch.equal(out.cpu(), ref), (out.cpu() - ref).abs().max()
+
+
+def test_seq_embed_layernorm_and_backward(gpu):
+    base, tables, ids, gate, pos, lw, lb = _embed_inputs(seed=1)
+    leaves = [t.clone().double().requires_grad_() for t in [base, *tables, gate, pos, lw, lb]]
+    b64, t64, g64, p64, w64, bb64 = leaves[0], leaves[1:7], leaves[7], leaves[8], leaves[9], leaves[10]
+    x = b64.clone()
+    for t, i, j in zip(t64, ids, range(6)):
+        x = x + t[i] * g64[j]
+    x = x + p64.unsqueeze(0)
+    ref = F.layer_norm(x, (128,), w64, bb64, 1e-5)
+    dout = torch.randn_like(ref)
+    (ref * dout).sum().backward()
+
+    dev = [t.clone().to(gpu).requires_grad_() for t in [base, *tables, gate, pos, lw, lb]]
+    out = ops.seq_embed(dev[0], [i.to(gpu) for i in ids], dev[1:7], dev[7], dev[8], dev[9], dev[10],
+                        eps=1e-5, padding_idx=[0] * 6)
+    torch.testing.assert_close(out.cpu().double(), ref.detach(), atol=2e-6, rtol=0)
+    (out * dout.float().to(gpu)).sum().backward()
+    names = ["base"] + [f"table{j}" for j in range(6)] + ["gate", "pos", "ln_w", "ln_b"]
+    for name, a, r in zip(names, dev, leaves):
+        gr = r.grad.clone()
+        if name.startswith("table"):
+            gr[0] = 0.0                            # nn.Embedding padding_idx=0: no gradient to row 0
+            j = int(name[-1])
+            if gate[j] == 0:
+                gr.zero_()                          # zero gate (s_mask) => zero table gradient
+        if name == "gate":
+            gr = gr * (gate != 0)                   # masked gates: d s_g is multiplied by 0 upstream
+        torch.testing.assert_close(a.grad.cpu().double(), gr, atol=2e-5, rtol=1e-4, msg=name)
+
+
+def test_seq_embed_dropout_mask_consistent(gpu):
+    base, tables, ids, gate, pos, lw, lb = _embed_inputs(seed=2)
+    x = base.to(gpu).requires_grad_()
+    out = ops.seq_embed(x, [i.to(gpu) for i in ids], [t.to(gpu) for t in tables], gate.to(gpu), pos.to(gpu),
+                        None, None, p_drop=0.2)
+    ref = _embed_ref(base, tables, ids, gate, pos).to(gpu)
+    keep = out != 0
+    frac = keep.float().mean().item()
+    assert abs(frac - 0.8) < 0.01
+    torch.testing.assert_close(out[keep], ref[keep] / 0.8, atol=1e-5, rtol=1e-5)
+    out.sum().backward()
+    torch.testing.assert_close(x.grad, keep.float() / 0.8)
+
+
+# ------------------------------------------------------------------ MHA core (A3/A9)
+def _mha_ref(qkv, pad, H, causal):
+    B, L, D3 = qkv.shape
+    D = D3 // 3
+    dh = D // H
+    q, k, v = qkv.split(D, -1)
+    q = q.view(B, L, H, dh).transpose(1, 2)
+    k = k.view(B, L, H, dh).transpose(1, 2)
+    v = v.view(B, L, H, dh).transpose(1, 2)
+    s = q @ k.transpose(-1, -2) / math.sqrt(dh)
+    blocked = torch.zeros(B, L, L, dtype=torch.bool)
+    if causal:
+        blocked |= torch.triu(torch.ones(L, L, dtype=torch.bool), 1)
+    if pad is not None:
+        blocked |= pad[:, None, :]
+    s = s.masked_fill(blocked[:, None], float("-inf"))
+    p = torch.nan_to_num(torch.softmax(s, -1), nan=0.0)
+    return (p @ v).transpose(1, 2).reshape(B, L, D)
+
+
+@pytest.mark.parametrize("L,H,dh,causal,use_pad", [(50, 4, 32, True, True), (16, 4, 32, False, False),
+                                                   (16, 4, 16, False, False), (7, 2, 32, True, False)])
+def test_mha_forward_backward(gpu, L, H, dh, causal, use_pad):
+    g = torch.Generator().manual_seed(L * 7 + dh)
+    B = 33
+    qkv = torch.randn(B, L, 3 * H * dh, generator=g)
+    pad = None
+    if use_pad:
+        lens = torch.randint(1, L + 1, (B,), generator=g)
+        lens[0] = L
+        pad = torch.arange(L)[None, :] < (L - lens)[:, None]  # left padding
+    q64 = qkv.double().requires_grad_()
+    ref = _mha_ref(q64, pad, H, causal)
+    dout = torch.randn(ref.shape, generator=g, dtype=torch.float64)
+    (ref * dout).sum().backward()
+    qd = qkv.to(gpu).requires_grad_()
+    out = ops.mha(qd, pad.to(gpu) if pad is not None else None, H, causal)
+    torch.testing.assert_close(out.cpu().double(), ref.detach(), atol=2e-5, rtol=1e-5)
+    (out * dout.float().to(gpu)).sum().backward()
+    torch.testing.assert_close(qd.grad.cpu().double(), q64.grad, atol=5e-5, rtol=1e-4)
+    if use_pad:  # fully-masked query rows give exactly zero attention
+        assert (out[pad.to(gpu)] == 0).all()
+
+
+def test_mha_dropout_directional_derivative(gpu):
+    g = torch.Generator().manual_seed(5)
+    B, L, H, dh = 8, 50, 4, 32
+    qkv = torch.randn(B, L, 3 * H * dh, generator=g).to(gpu)
+    pad = (torch.arange(L)[None, :] < torch.randint(0, L, (B,), generator=g)[:, None]).to(gpu)
+    v = torch.randn_like(qkv)
+    w = torch.randn(B, L, H * dh, device=gpu)
+    f = lambda x: (ops._MHA.apply(x, pad, H, True, 0.2, 1234) * w).sum()
+    x = qkv.clone().requires_grad_()
+    f(x).backward()
+    eps = 1e-2
+    num = (f(qkv.double().float() + eps * v) - f(qkv - eps * v)) / (2 * eps)
+    ana = (x.grad * v).sum()
+    assert abs(num.item() - ana.item()) < 2e-2 * max(1.0, abs(ana.item()))
+
+
+# ------------------------------------------------------------------ fused InfoNCE (A6/A7/A12)
+def _nce_ref(A, B, bias, k1a, k1b, k2a, k2b, tau, flags):
+    S = A @ B.T / tau
+    if bias is not None:
+        S = S - bias[None, :]
+    n, m = S.shape
+    idx_i = torch.arange(n)[:, None]
+    idx_j = torch.arange(m)[None, :]
+    off = idx_i != idx_j
+    excl = torch.zeros(n, m, dtype=torch.bool)
+    if flags & 1:
+        excl |= ~off
+    if flags & 2:
+        excl |= off & (k1a[:, None] == k1b[None, :])
+    if flags & 4:
+        excl |= off & (k2a[:, None] == k2b[None, :])
+    Sm = S.masked_fill(excl, float("-inf"))
+    lse = torch.logsumexp(Sm, 1)
+    if flags & 8:
+        pos = off & (k1a[:, None] == k1b[None, :]) & (k1a[:, None] != 0) & ~excl
+        cnt = pos.sum(1)
+        valid = cnt > 0
+        if valid.sum() == 0:
+            return (S * 0).sum()
+        psum = (S * pos).sum(1)
+        return (lse - psum / cnt.clamp(min=1))[valid].mean()
+    return (lse - S.diagonal()).mean()
+
+
+@pytest.mark.parametrize("flags", [0, 2, 6, 9])
+@pytest.mark.parametrize("n", [1, 77, 300, 1029])
+def test_nce_forward_backward(gpu, flags, n):
+    g = torch.Generator().manual_seed(n * 13 + flags)
+    A = F.normalize(torch.randn(n, 128, generator=g), dim=1)
+    B = F.normalize(torch.randn(n, 128, generator=g), dim=1)
+    if flags == 9:
+        B = A.clone()
+    bias = torch.log_softmax(torch.randn(n, generator=g), 0) if flags in (2, 6) else None
+    k1 = torch.randint(0, max(2, n // 3), (n,), generator=g)
+    k2 = torch.randint(0, max(2, n // 20), (n,), generator=g)
+    tau = 0.1
+    A64 = A.double().requires_grad_()
+    B64 = (A64 if flags == 9 else B.double().requires_grad_())
+    ref = _nce_ref(A64, B64, bias.double() if bias is not None else None, k1, k1, k2, k2, tau, flags)
+    ref.backward()
+    Ad = A.to(gpu).requires_grad_()
+    Bd = Ad if flags == 9 else B.to(gpu).requires_grad_()
+    dev = lambda t: None if t is None else t.to(gpu)
+    loss = ops.nce_loss(Ad, Bd, dev(bias), dev(k1), dev(k1), dev(k2), dev(k2), tau=tau, flags=flags)
+    assert abs(loss.item() - ref.item()) < 1e-4, (loss.item(), ref.item())
+    loss.backward()
+    torch.testing.assert_close(Ad.grad.cpu().double(), A64.grad, atol=2e-6, rtol=1e-4)
+    if flags != 9:
+        torch.testing.assert_close(Bd.grad.cpu().double(), B64.grad, atol=2e-6, rtol=1e-4)
+
+
+def test_nce_grad_scales_with_upstream(gpu):
+    g = torch.Generator().manual_seed(0)
+    A = F.normalize(torch.randn(200, 128, generator=g), dim=1).to(gpu).requires_grad_()
+    B = F.normalize(torch.randn(200, 128, generator=g), dim=1).to(gpu)
+    l = ops.nce_loss(A, B, tau=0.1)
+    (3.0 * l).backward()
+    ga = A.grad.clone()
+    A.grad = None
+    ops.nce_loss(A, B, tau=0.1).backward()
+    torch.testing.assert_close(ga, 3.0 * A.grad)
+
+
+# ------------------------------------------------------------------ rows
+def test_gather_normalize_and_scatter(gpu):
+    g = torch.Generator().manual_seed(0)
+    W = torch.randn(1000, 128, generator=g)
+    W[7] = 0.0  # zero row: F.normalize eps branch
+    idx = torch.randint(0, 1000, (3000,), generator=g)
+    idx[:5] = 7
+    W64 = W.double().requires_grad_()
+    ref = F.normalize(W64, p=2, dim=1)[idx]
+    dy = torch.randn(ref.shape, generator=g, dtype=torch.float64)
+    (ref * dy).sum().backward()
+    Wd = W.to(gpu).requires_grad_()
+    out = ops.gather_rows(Wd, idx.to(gpu), normalize=True)
+    torch.testing.assert_close(out.cpu().double(), ref.detach(), atol=1e-7, rtol=1e-6)
+    (out * dy.float().to(gpu)).sum().backward()
+    torch.testing.assert_close(Wd.grad.cpu().double(), W64.grad, atol=1e-5, rtol=1e-5)
+    plain = ops.gather_rows(Wd, idx.to(gpu))
+    assert torch.equal(plain.detach().cpu(), W[idx])
