@@ -34,18 +34,20 @@ struct FwdArgs {
 __device__ __forceinline__ float4 f4_axpy_rn(float4 x, float4 e, float g) {
   // seq_emb += E[id] * g  -- product rounded, then sum rounded (no FMA contraction),
   // matching the reference's separate `* s_g[j]` and `+=` tensor ops.
-  x.x = __fadd_rn(x.x, __fmul_rn(e.x, g));
-  x.y = __fadd_rn(x.y, __fmul_rn(e.y, g));
-  x.z = __fadd_rn(x.z, __fmul_rn(e.z, g));
-  x.w = __fadd_rn(x.w, __fmul_rn(e.w, g));
+#pragma clang fp contract(off)
+  x.x = x.x + e.x * g;
+  x.y = x.y + e.y * g;
+  x.z = x.z + e.z * g;
+  x.w = x.w + e.w * g;
   return x;
 }
 
 __device__ __forceinline__ float4 f4_add_rn(float4 x, float4 p) {
-  x.x = __fadd_rn(x.x, p.x);
-  x.y = __fadd_rn(x.y, p.y);
-  x.z = __fadd_rn(x.z, p.z);
-  x.w = __fadd_rn(x.w, p.w);
+#pragma clang fp contract(off)
+  x.x = x.x + p.x;
+  x.y = x.y + p.y;
+  x.z = x.z + p.z;
+  x.w = x.w + p.w;
   return x;
 }
 
