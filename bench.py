@@ -1,0 +1,198 @@
+#!/usr/bin/env python
+"""Headline benchmark: SimCSE/DuoRec contrastive train step of the user tower (BASELINE.json
+configs[1]: two-tower forward + in-batch contrastive loss, batch 4096, d=128, 1 x MI355X).
+
+A step = one full training step of tower_code/v1_usertower_train.py:717-893 on one global
+batch of synthetic H&M-shaped users: two dropout views (p=0.2) of SASRecUserTower, the
+all-time-steps LogQ in-batch loss (N ~ 75.7k valid positions, N x N implicit logits), DuoRec
+(InfoNCE + SupCon), backward, clip_grad_norm_(5.0), AdamW (item matrix unfrozen, lr x 0.05:
+the reference's epoch >= 2 steady state). Inputs are resident in HBM before timing.
+
+Multi-GPU (torchrun, one process per GPU, RCCL): the global batch stays fixed (strong
+scaling) and is split by users across ranks; see dist.py. Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32-input MFMA (= f32 vector peak)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=4096, help="global batch (users)")
+    ap.add_argument("--items", type=int, default=47_062)
+    ap.add_argument("--dropout", type=float, default=0.2)
+    ap.add_argument("--freeze-items", action="store_true", help="epoch-1 regime (item matrix frozen)")
+    ap.add_argument("--cpu-sample-batch", type=int, default=384)
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--seed", type=int, default=0)
+    return ap.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group(backend="nccl", init_method="env://", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return rank, world, torch.device("cuda", local if world > 1 else 0)
+
+
+def cpu_baseline(args, items, cfg):
+    """The oracle (CPU PyTorch fp32 restatement of the reference step) on a bounded sample."""
+    from oracle import user_tower as O
+    from recsys_amd import synth
+    torch.manual_seed(args.seed)
+    model = O.OracleUserTower(cfg)
+    model.train()
+    W = torch.nn.Parameter(items.pretrained.clone())
+    opt = torch.optim.AdamW(model.parameters(), lr=cfg.lr, weight_decay=cfg.weight_decay)
+    opt.add_param_group({"params": [W], "lr": cfg.lr * 0.05})
+    batch = synth.make_batch(items, args.cpu_sample_batch, seed=args.seed + 7)
+    O.contrastive_step(model, W, items.log_q, batch, opt, items.pretrained)  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(args.cpu_steps):
+        O.contrastive_step(model, W, items.log_q, batch, opt, items.pretrained)
+    dt = (time.perf_counter() - t0) / args.cpu_steps
+    n_valid = int((~batch["padding_mask"]).sum())
+    return {"value": round(args.cpu_sample_batch / dt, 2), "unit": "pairs/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": (f"oracle/user_tower.py contrastive_step (fp32 PyTorch CPU, dropout 0.2, AdamW) on "
+                       f"{args.cpu_sample_batch} users ({n_valid} valid steps), mean of {args.cpu_steps} steps "
+                       f"after 1 warm-up, {dt:.2f} s/step; smaller batch than the GPU run (CPU loss cost "
+                       f"grows with N^2)")}
+
+
+def main():
+    args = parse()
+    rank, world, device = setup_dist(args)
+    import recsys_amd  # noqa: F401
+    from recsys_amd import dist as D
+    from recsys_amd import ops, synth
+    from recsys_amd.tower_code import v1_usertower_train as TT
+    from recsys_amd.tower_code.v1_refine_usertower import SASRecUserTower
+
+    assert args.batch % world == 0, "global batch must divide by the number of GPUs"
+    b_loc = args.batch // world
+    hs = synth.HASH_SIZE
+    cfg = TT.PipelineConfig(num_items=args.items, num_prod_types=hs, num_colors=hs, num_graphics=hs,
+                            num_sections=hs, dropout=args.dropout)
+    items = synth.make_items(num_items=args.items, d=cfg.d_model, seed=args.seed)
+    torch.manual_seed(args.seed)
+    model = SASRecUserTower(cfg).to(device)
+    model.train()
+    item_tower = TT.SASRecItemTower(args.items, cfg.d_model, items.log_q.clone()).to(device)
+    item_tower.init_from_pretrained(items.pretrained.to(device))
+    item_tower.set_freeze_state(args.freeze_items)
+    opt = torch.optim.AdamW(model.parameters(), lr=cfg.lr, weight_decay=cfg.weight_decay)
+    if not args.freeze_items:
+        opt.add_param_group({"params": list(item_tower.parameters()), "lr": cfg.lr * 0.05})
+    bucket = D.GradBucket(list(model.parameters()) + list(item_tower.parameters()))
+    lookup = items.pretrained.to(device)
+    log_q = item_tower.log_q
+
+    # two distinct global batches, this rank's user slice of each, resident in HBM
+    batches = []
+    for s in range(2):
+        g = synth.make_batch(items, args.batch, seed=args.seed + 100 + s)
+        sl = {k: (v[rank * b_loc:(rank + 1) * b_loc] if torch.is_tensor(v) else v) for k, v in g.items()}
+        batches.append({k: (v.to(device) if torch.is_tensor(v) else v) for k, v in sl.items()})
+    n_valid = [int((~b["padding_mask"]).sum()) for b in batches]
+    n_glob = [D.all_gather_counts(n, device) for n in n_valid]
+    torch.cuda.synchronize()
+
+    def step(i):
+        return D.contrastive_step_dp(model, item_tower, log_q, batches[i % 2], opt, cfg, lookup, bucket)
+
+    for i in range(args.warmup):
+        step(i)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    ops.timing_start()
+    t0 = time.perf_counter()
+    losses = None
+    for i in range(args.steps):
+        losses = step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    kernel_times = ops.timing_stop()
+    elapsed = torch.tensor([t1 - t0], device=device, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    total_loss = float(losses[0].item())
+
+    # roofline of the dominant kernel: main-loss InfoNCE backward, row-owned pass
+    # (S recompute + dU product on fp32 MFMA). Algorithmic FLOPs per launch =
+    # 4 * N_local * N_global * 128 (2N^2 d per product; the bwd's one S
+    # recompute is attributed to this launch, the column pass counts only its product).
+    flops = 0.0
+    for i in range(args.steps):
+        cnts = n_glob[i % 2]
+        flops += 4.0 * cnts[rank] * sum(cnts) * 128
+    launches, ms = kernel_times.get("main/nce_bwd_rows", (0, 0.0))
+    avg_s = (ms / 1e3) / max(launches, 1)
+    achieved = (flops / max(launches, 1)) / avg_s / 1e12 if launches else None
+
+    kt = {k: {"launches": n, "avg_ms": round(t / max(n, 1), 4)} for k, (n, t) in sorted(kernel_times.items())}
+    result = {
+        "metric": "SimCSE train-step pairs/sec at d=128 (global batch %d)" % args.batch,
+        "value": round(args.batch * args.steps / elapsed, 2),
+        "unit": "pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (seeded H&M-shaped users/items: sample-calibrated lengths, Zipf(1.0) items; "
+                "random-init weights)",
+        "config": {"workload": "user-tower two-view contrastive train step (fwd x2 + LogQ in-batch loss + "
+                               "DuoRec + bwd + clip + AdamW), BASELINE configs[1]",
+                   "global_batch": args.batch, "seq_len": 50, "d_model": 128, "items": args.items,
+                   "valid_positions_per_batch": [sum(c) for c in n_glob], "dropout": args.dropout,
+                   "item_matrix": "frozen" if args.freeze_items else "unfrozen (lr x0.05)",
+                   "parallelism": f"dp{world} (users split by rank, RCCL all-gather of ids/z, grad all-reduce)"},
+        "roofline": {"kernel": "nce_bwd_k<6,row-owned> (main LogQ loss backward)", "bound": "mfma",
+                     "achieved": round(achieved, 2) if achieved else None, "peak": FP32_MFMA_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4) if achieved else None,
+                     "traffic": None, "avg_launch_ms": round(avg_s * 1e3, 4)},
+        "kernels": kt,
+        "final_loss": round(total_loss, 5),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args, items, cfg)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -74,7 +74,9 @@ int rsx_mha_bwd(const float* qkv, const uint8_t* key_pad, const float* out, cons
 
 /* ---- A6 / A7 / A12: fused in-batch contrastive cross-entropy ------------------------
  * S_ij = <A_i,B_j>/tau - bias_j over an implicit N x M matrix (never materialised),
- * fp32-input MFMA, online log-sum-exp. flags (supported combinations):
+ * fp32-input MFMA, online log-sum-exp. Row i's label column is i + diag_offset (0 on one
+ * GPU; the shard offset when A holds one rank's rows and B the all-gathered columns).
+ * flags (supported combinations):
  *   0                 plain InfoNCE, label = diagonal  (duorec unsup v1_refine_usertower.py:588-590,
  *                                                       item_tower.py:1075-1082 per direction)
  *   2 (MASK_K1)       + exclude off-diagonal j with k1_j == k1_i   (shadowed logq loss :520-573)
@@ -83,16 +85,18 @@ int rsx_mha_bwd(const float* qkv, const uint8_t* key_pad, const float* out, cons
  *                     positives k1_i == k1_j != 0, loss_i = LSE_i - mean positive logit
  * Keys are int32. D = 128 (row strides lda/ldb >= 128, multiple of 4, 16-B aligned).
  * ws: rsx_nce_workspace_floats(N, M, nsplit_fwd, nsplit_bwd) floats, shared by fwd and bwd.
- * out2 (device, 2 floats) = {mean loss over valid rows, 1/n_valid}. */
+ * out2 (device, 2 floats) = {sum of row losses over valid rows, number of valid rows};
+ * the reference's mean is out2[0] / out2[1] (0 when no row is valid). */
 int64_t rsx_nce_workspace_floats(int64_t N, int64_t M, int nsplit_fwd, int nsplit_bwd);
 int rsx_nce_fwd(const float* A, const float* B, const float* bias, const int* k1a, const int* k1b, const int* k2a,
-                const int* k2b, int64_t N, int64_t M, int64_t lda, int64_t ldb, float tau, int flags, int nsplit,
-                float* ws, float* out2, void* stream);
-/* gout = device scalar upstream gradient. dA [N,128] / dB [M,128] (nullable) written, or
- * added into when accumulate != 0. Must follow rsx_nce_fwd on the same ws. */
+                const int* k2b, int64_t N, int64_t M, int64_t lda, int64_t ldb, int64_t diag_offset, float tau,
+                int flags, int nsplit, float* ws, float* out2, void* stream);
+/* gout = device scalar: gradient of the objective w.r.t. the row-loss SUM out2[0].
+ * dA [N,128] / dB [M,128] (nullable; NULL skips that pass) written, or added into when
+ * accumulate != 0. Must follow rsx_nce_fwd on the same ws. */
 int rsx_nce_bwd(const float* A, const float* B, const float* bias, const int* k1a, const int* k1b, const int* k2a,
-                const int* k2b, int64_t N, int64_t M, int64_t lda, int64_t ldb, float tau, int flags,
-                int nsplit_fwd, int nsplit, const float* gout, const float* out2, float* ws, float* dA, float* dB,
+                const int* k2b, int64_t N, int64_t M, int64_t lda, int64_t ldb, int64_t diag_offset, float tau,
+                int flags, int nsplit_fwd, int nsplit, const float* gout, float* ws, float* dA, float* dB,
                 int accumulate, void* stream);
 
 /* ---- row gather / scatter / L2 normalise ---------------------------------------------

@@ -36,9 +36,9 @@ _SIGS = {
     "rsx_mha_fwd": (c_i, [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i, c_f, c_u64, c_p, c_p, c_p]),
     "rsx_mha_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i, c_f, c_u64, c_p, c_p]),
     "rsx_nce_workspace_floats": (c_i64, [c_i64, c_i64, c_i, c_i]),
-    "rsx_nce_fwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_f, c_i, c_i, c_p, c_p,
-                          c_p]),
-    "rsx_nce_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_f, c_i, c_i, c_i, c_p,
+    "rsx_nce_fwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_f, c_i, c_i, c_p,
+                          c_p, c_p]),
+    "rsx_nce_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_f, c_i, c_i, c_i,
                           c_p, c_p, c_p, c_p, c_i, c_p]),
     "rsx_gather_rows": (c_i, [c_p, c_i64, c_p, c_i64, c_i64, c_i, c_f, c_p, c_p, c_p]),
     "rsx_scatter_rows": (c_i, [c_p, c_p, c_p, c_p, c_i64, c_i64, c_i, c_f, c_i, c_i64, c_p, c_i64, c_p]),

@@ -45,6 +45,7 @@ struct FwdArgs {
   const int* k2a;
   const int* k2b;
   int64_t N, M, lda, ldb;
+  int64_t diag_off;  // row i's label / diagonal column is i + diag_off (data-parallel shards)
   float inv_tau;
   int nsplit;
   int64_t cols_per_split;
@@ -173,7 +174,7 @@ __global__ __launch_bounds__(256, 2) void nce_fwd_k(FwdArgs a) {
           const int64_t j = j0 + rbase + e;
           const float s = acc[r] * a.inv_tau - bia[e];
           bool excl = (j >= j_end) || !row_ok;
-          const bool offdiag = (j != i);
+          const bool offdiag = (j != i + a.diag_off);
           if (FL & F_EXCL_DIAG) excl = excl || !offdiag;
           if (FL & F_MASK_K1) excl = excl || (offdiag && kk1[e] == k1i);
           if (FL & F_MASK_K2) excl = excl || (offdiag && kk2[e] == k2i);
@@ -232,6 +233,7 @@ struct MergeArgs {
   const float* B;
   const float* bias;
   int64_t N, lda, ldb;
+  int64_t diag_off;
   float inv_tau;
   int nsplit;
   const float* part;
@@ -269,10 +271,10 @@ __global__ __launch_bounds__(256) void nce_merge_k(MergeArgs a) {
   if (!a.pos_mode) {
     // diagonal logit S_ii (same expression as the fused kernel)
     const float2 x = reinterpret_cast<const float2*>(a.A + i * a.lda)[lane];
-    const float2 y = reinterpret_cast<const float2*>(a.B + i * a.ldb)[lane];
+    const float2 y = reinterpret_cast<const float2*>(a.B + (i + a.diag_off) * a.ldb)[lane];
     float d = x.x * y.x + x.y * y.y;
     for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
-    const float sii = d * a.inv_tau - (a.bias ? a.bias[i] : 0.0f);
+    const float sii = d * a.inv_tau - (a.bias ? a.bias[i + a.diag_off] : 0.0f);
     loss = lse - sii;
     valid = 1.0f;
   } else {
@@ -288,7 +290,7 @@ __global__ __launch_bounds__(256) void nce_merge_k(MergeArgs a) {
   }
 }
 
-// Deterministic single-workgroup mean over valid rows. out[0] = loss, out[1] = 1/n_valid.
+// Deterministic single-workgroup sums over rows. out[0] = sum of row losses, out[1] = n_valid.
 __global__ __launch_bounds__(1024) void nce_reduce_k(const float* row_loss, const float* row_valid, int64_t N,
                                                       float* out) {
   __shared__ float s_l[1024], s_v[1024];
@@ -308,15 +310,15 @@ __global__ __launch_bounds__(1024) void nce_reduce_k(const float* row_loss, cons
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    const float nv = s_v[0];
-    out[0] = nv > 0.0f ? s_l[0] / nv : 0.0f;
-    out[1] = nv > 0.0f ? 1.0f / nv : 0.0f;
+    out[0] = s_l[0];
+    out[1] = s_v[0];
   }
 }
 
 // ---------------------------------------------------------------------------------
 // Backward. G_ij = w_i * (P_ij - Y_ij) / tau, P_ij = exp(S_ij - LSE_i) (0 if excluded),
-// Y = diagonal (pos_mode 0) or M_ij / cnt_i (pos_mode 1), w_i = g * scale * valid_i.
+// Y = diagonal (pos_mode 0) or M_ij / cnt_i (pos_mode 1), w_i = g * valid_i where g is the
+// upstream gradient of the row-loss SUM (device scalar).
 // ROW_OWNED: dA_i = sum_j G_ij B_j ; else dB_j = sum_i G_ij A_i.
 struct BwdArgs {
   const float* A;
@@ -327,12 +329,12 @@ struct BwdArgs {
   const int* k2a;
   const int* k2b;
   int64_t N, M, lda, ldb;
+  int64_t diag_off;
   float inv_tau;
   const float* lse;
   const float* row_valid;
   const float* inv_cnt;
-  const float* gout;   // upstream scalar gradient (device)
-  const float* scale;  // 1/n_valid (device, written by nce_reduce_k)
+  const float* gout;   // upstream gradient of the row-loss sum (device scalar)
   int nsplit;
   int64_t span_per_split;  // streamed rows per split
   float* dout;             // [nsplit][owner_rows][128] (split partials) or final when nsplit==1
@@ -358,7 +360,7 @@ __global__ __launch_bounds__(256, 2) void nce_bwd_k(BwdArgs a) {
   const float* str = ROW_OWNED ? a.B : a.A;
   const int64_t ld_own = ROW_OWNED ? a.lda : a.ldb;
   const int64_t ld_str = ROW_OWNED ? a.ldb : a.lda;
-  const float g_scale = a.gout[0] * a.scale[0] * a.inv_tau;
+  const float g_scale = a.gout[0] * a.inv_tau;
 
   const int64_t o = (int64_t)ob * kOwnRows + wave * 32 + c;  // this lane's owner index
   const bool own_ok = o < n_own;
@@ -499,7 +501,7 @@ __global__ __launch_bounds__(256, 2) void nce_bwd_k(BwdArgs a) {
           }
           const float sv = acc[r] * a.inv_tau - bias_j;
           bool excl = (sidx >= s_end) || !own_ok;
-          const bool offdiag = (ii != jj);
+          const bool offdiag = (jj != ii + a.diag_off);
           if (FL & F_EXCL_DIAG) excl = excl || !offdiag;
           if (FL & F_MASK_K1) excl = excl || (offdiag && k1_i == k1_j);
           if (FL & F_MASK_K2) excl = excl || (offdiag && k2_i == k2_j);
@@ -591,17 +593,17 @@ RSX_API int64_t rsx_nce_workspace_floats(int64_t N, int64_t M, int nsplit_fwd, i
          + 16;
 }
 
-// Forward: writes lse/row_loss/row_valid/inv_cnt (ws) and out2 = {loss, 1/n_valid}.
+// Forward: writes lse/row_loss/row_valid/inv_cnt (ws) and out2 = {sum of row losses, n_valid}.
 RSX_API int rsx_nce_fwd(const float* A, const float* B, const float* bias, const int* k1a, const int* k1b,
-                        const int* k2a, const int* k2b, int64_t N, int64_t M, int64_t lda, int64_t ldb, float tau,
-                        int flags, int nsplit, float* ws, float* out2, void* stream) {
+                        const int* k2a, const int* k2b, int64_t N, int64_t M, int64_t lda, int64_t ldb,
+                        int64_t diag_offset, float tau, int flags, int nsplit, float* ws, float* out2,
+                        void* stream) {
   RSX_ARG(valid_flags(flags), "unsupported flag combination");
   RSX_ARG(nsplit >= 8 && nsplit <= 64 && nsplit % 8 == 0, "nsplit must be a multiple of 8 in [8,64]");
   RSX_ARG(N >= 0 && M >= 0, "negative size");
   RSX_ARG(lda % 4 == 0 && ldb % 4 == 0 && lda >= kD && ldb >= kD, "row strides must be >=128 and multiples of 4");
   RSX_ARG(((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0, "A/B must be 16-byte aligned");
-  RSX_ARG(!(flags & F_EXCL_DIAG) || N == M, "diagonal modes need N == M");
-  RSX_ARG((flags & F_POS) || N == M, "diagonal-label loss needs N == M");
+  RSX_ARG(diag_offset >= 0 && diag_offset + N <= M, "need 0 <= diag_offset and diag_offset + N <= M");
   RSX_ARG(!(flags & (F_MASK_K1 | F_POS)) || (k1a && k1b), "k1 keys required");
   RSX_ARG(!(flags & F_MASK_K2) || (k2a && k2b), "k2 keys required");
   hipStream_t st = (hipStream_t)stream;
@@ -619,6 +621,7 @@ RSX_API int rsx_nce_fwd(const float* A, const float* B, const float* bias, const
   fa.A = A; fa.B = B; fa.bias = bias;
   fa.k1a = k1a; fa.k1b = k1b; fa.k2a = k2a; fa.k2b = k2b;
   fa.N = N; fa.M = M; fa.lda = lda; fa.ldb = ldb;
+  fa.diag_off = diag_offset;
   fa.inv_tau = 1.0f / tau;
   fa.nsplit = nsplit;
   fa.cols_per_split = round_up((M + nsplit - 1) / nsplit, kTile);
@@ -636,6 +639,7 @@ RSX_API int rsx_nce_fwd(const float* A, const float* B, const float* bias, const
   MergeArgs ma;
   ma.A = A; ma.B = B; ma.bias = bias;
   ma.N = N; ma.lda = lda; ma.ldb = ldb;
+  ma.diag_off = diag_offset;
   ma.inv_tau = fa.inv_tau;
   ma.nsplit = nsplit;
   ma.part = part;
@@ -650,12 +654,13 @@ RSX_API int rsx_nce_fwd(const float* A, const float* B, const float* bias, const
 
 // Backward: dA (N x 128) and/or dB (M x 128); accumulate != 0 adds into them.
 RSX_API int rsx_nce_bwd(const float* A, const float* B, const float* bias, const int* k1a, const int* k1b,
-                        const int* k2a, const int* k2b, int64_t N, int64_t M, int64_t lda, int64_t ldb, float tau,
-                        int flags, int nsplit_fwd, int nsplit, const float* gout, const float* out2, float* ws,
-                        float* dA, float* dB, int accumulate, void* stream) {
+                        const int* k2a, const int* k2b, int64_t N, int64_t M, int64_t lda, int64_t ldb,
+                        int64_t diag_offset, float tau, int flags, int nsplit_fwd, int nsplit, const float* gout,
+                        float* ws, float* dA, float* dB, int accumulate, void* stream) {
   RSX_ARG(valid_flags(flags), "unsupported flag combination");
   RSX_ARG(nsplit >= 8 && nsplit <= 64 && nsplit % 8 == 0, "nsplit must be a multiple of 8 in [8,64]");
-  RSX_ARG(gout != nullptr && out2 != nullptr, "gout/out2 required");
+  RSX_ARG(gout != nullptr, "gout required");
+  RSX_ARG(diag_offset >= 0 && diag_offset + N <= M, "need 0 <= diag_offset and diag_offset + N <= M");
   hipStream_t st = (hipStream_t)stream;
   if (N == 0) return 0;
   float* part = ws;
@@ -667,10 +672,10 @@ RSX_API int rsx_nce_bwd(const float* A, const float* B, const float* bias, const
   ba.A = A; ba.B = B; ba.bias = bias;
   ba.k1a = k1a; ba.k1b = k1b; ba.k2a = k2a; ba.k2b = k2b;
   ba.N = N; ba.M = M; ba.lda = lda; ba.ldb = ldb;
+  ba.diag_off = diag_offset;
   ba.inv_tau = 1.0f / tau;
   ba.lse = lse; ba.row_valid = row_valid; ba.inv_cnt = inv_cnt;
   ba.gout = gout;
-  ba.scale = out2 + 1;
   ba.nsplit = nsplit;
   for (int pass = 0; pass < 2; ++pass) {
     const bool row_owned = pass == 0;

@@ -1,0 +1,209 @@
+"""Data-parallel contrastive step over RCCL (torch.distributed backend "nccl" on ROCm).
+
+The reference is single-device; this is the MI355X-native multi-GPU form of
+train_user_tower_all_time (tower_code/v1_usertower_train.py:717-893) whose result equals the
+single-GPU step on the rank-major concatenated global batch:
+
+  * each rank owns a contiguous slice of the global batch's users and runs both tower
+    views locally;
+  * the main LogQ loss needs every rank's target *ids* as columns. The item matrix is
+    replicated, so each rank rebuilds the normalised global column pool from the gathered
+    ids itself: one all-gather of ids (~8 B/step-position) instead of 512 B embeddings;
+  * DuoRec needs the other ranks' user vectors: the L2-normalised last-step vectors z1/z2
+    are all-gathered (autograd-aware: their gradients are all-reduced back to the owners);
+  * every loss is a sum over local rows divided by the GLOBAL row count, so the per-rank
+    objectives add up to the single-GPU objective, and the replicated parameters' gradients
+    are summed with one bucketed all-reduce before clipping.
+Only the collective helpers here are device-agnostic (gloo-tested on CPU); the losses call
+the HIP kernels through ops.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from . import ops
+
+
+def world():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def all_gather_counts(n: int, device) -> list:
+    """Every rank's local row count (one tiny all-gather + host read)."""
+    rank, ws = world()
+    if ws == 1:
+        return [int(n)]
+    t = torch.tensor([int(n)], device=device, dtype=torch.int64)
+    out = [torch.empty_like(t) for _ in range(ws)]
+    dist.all_gather(out, t)
+    return [int(x.item()) for x in out]
+
+
+def all_gather_var(x: torch.Tensor, counts: list) -> torch.Tensor:
+    """Concatenate every rank's x[:counts[r]] (rank-major). Not differentiable."""
+    rank, ws = world()
+    if ws == 1:
+        return x
+    mx = max(counts)
+    pad = torch.zeros((mx,) + tuple(x.shape[1:]), device=x.device, dtype=x.dtype)
+    pad[: x.shape[0]] = x
+    bufs = [torch.empty_like(pad) for _ in range(ws)]
+    dist.all_gather(bufs, pad)
+    return torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0)
+
+
+class _AllGatherRows(torch.autograd.Function):
+    """Rank-major all-gather of [n_r, D] rows; backward sums every rank's gradient of the
+    gathered matrix and returns this rank's slice (the reduce half of the exchange)."""
+
+    @staticmethod
+    def forward(ctx, x, counts):
+        rank, _ = world()
+        ctx.lo = sum(counts[:rank])
+        ctx.n = counts[rank]
+        return all_gather_var(x.contiguous(), counts)
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        if world()[1] > 1:
+            dist.all_reduce(g)
+        return g[ctx.lo: ctx.lo + ctx.n], None
+
+
+def all_gather_rows(x: torch.Tensor, counts: list) -> torch.Tensor:
+    if world()[1] == 1:
+        return x
+    return _AllGatherRows.apply(x, counts)
+
+
+def all_reduce_sum_(t: torch.Tensor) -> torch.Tensor:
+    if world()[1] > 1:
+        dist.all_reduce(t)
+    return t
+
+
+class GradBucket:
+    """One flat fp32 all-reduce over every replicated parameter's gradient (DDP semantics,
+    sum over ranks). Parameters without a gradient contribute zeros, so every rank issues
+    the same collective."""
+
+    def __init__(self, params):
+        self.params = [p for p in params if p.requires_grad]
+        self.numel = sum(p.numel() for p in self.params)
+        self.flat = None
+
+    def __call__(self):
+        if world()[1] == 1 or not self.params:
+            return
+        dev = self.params[0].device
+        if self.flat is None or self.flat.device != dev:
+            self.flat = torch.empty(self.numel, device=dev, dtype=torch.float32)
+        o = 0
+        for p in self.params:
+            n = p.numel()
+            if p.grad is None:
+                self.flat[o:o + n].zero_()
+            else:
+                self.flat[o:o + n].copy_(p.grad.reshape(-1))
+            o += n
+        dist.all_reduce(self.flat)
+        o = 0
+        for p in self.params:
+            n = p.numel()
+            g = self.flat[o:o + n].view_as(p)
+            if p.grad is None:
+                p.grad = g.clone()
+            else:
+                p.grad.copy_(g)
+            o += n
+
+
+_FWD_KEYS = ("item_ids", "time_bucket_ids", "type_ids", "color_ids", "graphic_ids", "section_ids", "age_bucket",
+             "price_bucket", "cnt_bucket", "recency_bucket", "channel_ids", "club_status_ids", "news_freq_ids",
+             "fn_ids", "active_ids", "cont_feats", "padding_mask")
+
+
+def contrastive_objective_dp(model, item_tower, log_q_tensor, batch, cfg, pretrained_vecs, temperature=0.1):
+    """This rank's share of the global objective (reference :787-845 on the global batch).
+
+    batch holds this rank's users (global user index = rank * B_local + b).
+    Returns (local objective to backward, global total / main / cl for logging; the
+    logging values are all-reduced and detached)."""
+    rank, ws = world()
+    device = batch["item_ids"].device
+    kw = {k: batch[k] for k in _FWD_KEYS}
+    kw["pretrained_vecs"] = pretrained_vecs
+    kw["training_mode"] = True
+    out1 = model(**kw)
+    out2 = model(**kw)
+    B, L = batch["item_ids"].shape
+    D = out1.shape[-1]
+    valid = ~batch["padding_mask"]
+    target_ids = batch["target_ids"]
+
+    # ---- main LogQ loss over all valid steps of the global batch
+    flat_pos = valid.reshape(-1).nonzero().squeeze(1)
+    counts = all_gather_counts(flat_pos.numel(), device)
+    n_glob = sum(counts)
+    offset = sum(counts[:rank])
+    if n_glob > 0:
+        u_loc = ops.gather_rows(out1.reshape(-1, D), flat_pos, normalize=True, unique=True)
+        t_loc = target_ids.reshape(-1)[flat_pos]
+        user_loc = torch.div(flat_pos, L, rounding_mode="floor") + rank * B
+        t_glob = all_gather_var(t_loc, counts)
+        user_glob = all_gather_var(user_loc, counts)
+        items_glob = ops.gather_rows(item_tower.get_all_embeddings(), t_glob, normalize=True)
+        bias = log_q_tensor[t_glob] * cfg.lambda_logq if cfg.lambda_logq > 0.0 else None
+        main_sum, _ = ops.nce_sum(u_loc, items_glob, bias, t_loc, t_glob, user_loc, user_glob, tau=temperature,
+                                  flags=ops.NCE_MASK_ITEM_USER, diag_offset=offset, tag="main")
+        main_local = main_sum / float(n_glob)
+    else:
+        main_local = torch.zeros((), device=device)
+
+    # ---- DuoRec on the bug-compatible "last" index (count_valid - 1), global B x B
+    last = (valid.sum(dim=1) - 1).clamp(min=0)
+    rows = torch.arange(B, device=device) * L + last
+    z1 = ops.l2_normalize(ops.gather_rows(out1.reshape(-1, D), rows, unique=True))
+    z2 = ops.l2_normalize(ops.gather_rows(out2.reshape(-1, D), rows, unique=True))
+    last_t = target_ids.reshape(-1)[rows]
+    bcounts = [B] * ws
+    b_glob = B * ws
+    z1_glob = all_gather_rows(z1, bcounts)
+    z2_glob = all_gather_rows(z2, bcounts)
+    t_glob_last = all_gather_var(last_t, bcounts)
+    un_sum, _ = ops.nce_sum(z1, z2_glob, tau=temperature, flags=ops.NCE_PLAIN, diag_offset=rank * B,
+                            tag="duorec")
+    unsup_local = un_sum / float(b_glob)
+    if cfg.lambda_sup > 0:
+        sup_sum, sup_cnt = ops.nce_sum(z1, z1_glob, None, last_t, t_glob_last, tau=temperature,
+                                       flags=ops.NCE_SUPCON, diag_offset=rank * B, tag="supcon")
+        cnt_glob = all_reduce_sum_(sup_cnt.detach().clone())
+        sup_local = sup_sum / cnt_glob.clamp(min=1.0)
+    else:
+        sup_local = torch.zeros((), device=device)
+    cl_local = unsup_local + cfg.lambda_sup * sup_local
+    objective = main_local + cfg.lambda_cl * cl_local
+
+    logs = torch.stack([objective.detach(), main_local.detach(), cl_local.detach()])
+    all_reduce_sum_(logs)
+    return objective, logs[0], logs[1], logs[2]
+
+
+def contrastive_step_dp(model, item_tower, log_q_tensor, batch, optimizer, cfg, pretrained_lookup, bucket,
+                        max_norm=5.0):
+    """Full data-parallel step: local forward/loss/backward, one gradient all-reduce,
+    clip_grad_norm_(5.0) on the summed gradients, AdamW (replicated, identical on all ranks)."""
+    from .tower_code.v1_usertower_train import lookup_pretrained
+
+    optimizer.zero_grad(set_to_none=True)
+    pv = lookup_pretrained(pretrained_lookup, batch["item_ids"])
+    objective, total, main, cl = contrastive_objective_dp(model, item_tower, log_q_tensor, batch, cfg, pv)
+    objective.backward()
+    bucket()
+    torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=max_norm)
+    optimizer.step()
+    return total, main, cl

@@ -194,8 +194,10 @@ def l2_normalize(x, eps=1e-12):
 # ----------------------------------------------------------------------------------------
 # A6 / A7 / A12: fused contrastive cross-entropy
 class _NCE(torch.autograd.Function):
+    """Returns (sum of row losses over valid rows, number of valid rows)."""
+
     @staticmethod
-    def forward(ctx, A, B, bias, k1a, k1b, k2a, k2b, tau, flags):
+    def forward(ctx, A, B, bias, k1a, k1b, k2a, k2b, tau, flags, diag_offset, tag):
         N.ensure_device(A)
         A = _c(A)
         B = _c(B)
@@ -204,33 +206,91 @@ class _NCE(torch.autograd.Function):
         ws = torch.empty(nws, device=A.device, dtype=torch.float32)
         out2 = torch.empty(2, device=A.device, dtype=torch.float32)
         keys = [_c(k) for k in (k1a, k1b, k2a, k2b)]
-        rc = N.lib().rsx_nce_fwd(N.ptr(A), N.ptr(B), N.ptr(bias), *[N.ptr(k) for k in keys], n, m, A.stride(0),
-                                 B.stride(0), tau, flags, _NSPLIT_FWD, N.ptr(ws), N.ptr(out2), N.stream())
+        with timed(f"{tag}/nce_fwd"):
+            rc = N.lib().rsx_nce_fwd(N.ptr(A), N.ptr(B), N.ptr(bias), *[N.ptr(k) for k in keys], n, m, A.stride(0),
+                                     B.stride(0), diag_offset, tau, flags, _NSPLIT_FWD, N.ptr(ws), N.ptr(out2),
+                                     N.stream())
         N.check(rc, "nce_fwd")
-        ctx.save_for_backward(A, B, bias, *keys, ws, out2)
-        ctx.cfg = (n, m, tau, flags)
-        return out2[0]
+        ctx.save_for_backward(A, B, bias, *keys, ws)
+        ctx.cfg = (n, m, tau, flags, diag_offset, tag)
+        cnt = out2[1]
+        ctx.mark_non_differentiable(cnt)
+        return out2[0], cnt
 
     @staticmethod
-    def backward(ctx, g):
-        A, B, bias, k1a, k1b, k2a, k2b, ws, out2 = ctx.saved_tensors
-        n, m, tau, flags = ctx.cfg
+    def backward(ctx, g, _gcnt):
+        A, B, bias, k1a, k1b, k2a, k2b, ws = ctx.saved_tensors
+        n, m, tau, flags, off, tag = ctx.cfg
         g = _c(g.reshape(1).to(torch.float32))
-        dA = torch.empty_like(A) if ctx.needs_input_grad[0] else None
-        dB = torch.empty_like(B) if ctx.needs_input_grad[1] else None
-        rc = N.lib().rsx_nce_bwd(N.ptr(A), N.ptr(B), N.ptr(bias), N.ptr(k1a), N.ptr(k1b), N.ptr(k2a), N.ptr(k2b),
-                                 n, m, A.stride(0), B.stride(0), tau, flags, _NSPLIT_FWD, _NSPLIT_BWD, N.ptr(g),
-                                 N.ptr(out2), N.ptr(ws), N.ptr(dA), N.ptr(dB), 0, N.stream())
-        N.check(rc, "nce_bwd")
-        return dA, dB, None, None, None, None, None, None, None
+        args = (N.ptr(A), N.ptr(B), N.ptr(bias), N.ptr(k1a), N.ptr(k1b), N.ptr(k2a), N.ptr(k2b), n, m, A.stride(0),
+                B.stride(0), off, tau, flags, _NSPLIT_FWD, _NSPLIT_BWD, N.ptr(g), N.ptr(ws))
+        dA = dB = None
+        if ctx.needs_input_grad[0]:
+            dA = torch.empty_like(A)
+            with timed(f"{tag}/nce_bwd_rows"):
+                rc = N.lib().rsx_nce_bwd(*args, N.ptr(dA), None, 0, N.stream())
+            N.check(rc, "nce_bwd(rows)")
+        if ctx.needs_input_grad[1]:
+            dB = torch.empty_like(B)
+            with timed(f"{tag}/nce_bwd_cols"):
+                rc = N.lib().rsx_nce_bwd(*args, None, N.ptr(dB), 0, N.stream())
+            N.check(rc, "nce_bwd(cols)")
+        return dA, dB, None, None, None, None, None, None, None, None, None
 
 
 def _i32(t):
     return None if t is None else t.to(torch.int32)
 
 
-def nce_loss(A, B, bias=None, k1a=None, k1b=None, k2a=None, k2b=None, tau=0.1, flags=NCE_PLAIN):
-    """Mean InfoNCE over rows of S = A B^T / tau - bias (see include/recsys_amd.h)."""
+def nce_sum(A, B, bias=None, k1a=None, k1b=None, k2a=None, k2b=None, tau=0.1, flags=NCE_PLAIN, diag_offset=0,
+            tag="nce"):
+    """(sum of row losses, valid-row count) of S = A B^T / tau - bias; row i's label column
+    is i + diag_offset (see include/recsys_amd.h)."""
     if bias is not None:
         bias = _c(bias.to(torch.float32))
-    return _NCE.apply(A, B, bias, _i32(k1a), _i32(k1b), _i32(k2a), _i32(k2b), float(tau), int(flags))
+    return _NCE.apply(A, B, bias, _i32(k1a), _i32(k1b), _i32(k2a), _i32(k2b), float(tau), int(flags),
+                      int(diag_offset), str(tag))
+
+
+def nce_loss(A, B, bias=None, k1a=None, k1b=None, k2a=None, k2b=None, tau=0.1, flags=NCE_PLAIN, tag="nce"):
+    """Mean InfoNCE over valid rows (0 if none), the reference's F.cross_entropy mean."""
+    total, cnt = nce_sum(A, B, bias, k1a, k1b, k2a, k2b, tau, flags, tag=tag)
+    return total / cnt.clamp(min=1.0)
+
+
+# ----------------------------------------------------------------------------------------
+# Optional per-op device timing (bench.py): HIP events on the launching (current) stream.
+_TIMING = {"on": False, "events": {}}
+
+
+class timed:
+    def __init__(self, name):
+        self.name = name
+
+    def __enter__(self):
+        if _TIMING["on"]:
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e0.record()
+        return self
+
+    def __exit__(self, *exc):
+        if _TIMING["on"]:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            _TIMING["events"].setdefault(self.name, []).append((self.e0, e1))
+        return False
+
+
+def timing_start():
+    _TIMING["on"] = True
+    _TIMING["events"] = {}
+
+
+def timing_stop():
+    """-> {name: (launches, total_ms)} (synchronises)."""
+    _TIMING["on"] = False
+    torch.cuda.synchronize()
+    out = {}
+    for k, evs in _TIMING["events"].items():
+        out[k] = (len(evs), sum(a.elapsed_time(b) for a, b in evs))
+    return out

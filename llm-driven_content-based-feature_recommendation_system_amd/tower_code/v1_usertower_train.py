@@ -127,7 +127,7 @@ def contrastive_losses(model, item_tower, log_q_tensor, batch, cfg, pretrained_v
         k1 = flat_targets.to(torch.int32)
         k2 = flat_user_ids.to(torch.int32)
         main_loss = ops.nce_loss(flat_user_emb, batch_item_emb, bias, k1, k1, k2, k2, tau=0.1,
-                                 flags=ops.NCE_MASK_ITEM_USER)
+                                 flags=ops.NCE_MASK_ITEM_USER, tag="main")
     else:
         main_loss = torch.zeros((), device=device)
 

@@ -238,3 +238,49 @@ def test_gather_normalize_and_scatter(gpu):
     torch.testing.assert_close(Wd.grad.cpu().double(), W64.grad, atol=1e-5, rtol=1e-5)
     plain = ops.gather_rows(Wd, idx.to(gpu))
     assert torch.equal(plain.detach().cpu(), W[idx])
+
+
+def _nce_rows_ref(A, B, bias, k1a, k1b, k2a, k2b, tau, flags, off):
+    """Per-row losses (and validity) with row i's label at column i + off (float64)."""
+    S = A @ B.T / tau
+    if bias is not None:
+        S = S - bias[None, :]
+    n, m = S.shape
+    lab = torch.arange(n)[:, None] + off
+    off_d = torch.arange(m)[None, :] != lab
+    excl = torch.zeros(n, m, dtype=torch.bool)
+    if flags & 1:
+        excl |= ~off_d
+    if flags & 2:
+        excl |= off_d & (k1a[:, None] == k1b[None, :])
+    if flags & 4:
+        excl |= off_d & (k2a[:, None] == k2b[None, :])
+    lse = torch.logsumexp(S.masked_fill(excl, float("-inf")), 1)
+    if flags & 8:
+        pos = off_d & (k1a[:, None] == k1b[None, :]) & (k1a[:, None] != 0) & ~excl
+        cnt = pos.sum(1)
+        valid = cnt > 0
+        loss = torch.where(valid, lse - (S * pos).sum(1) / cnt.clamp(min=1), torch.zeros_like(lse))
+        return loss, valid
+    return lse - S.gather(1, lab).squeeze(1), torch.ones(n, dtype=torch.bool)
+
+
+@pytest.mark.parametrize("flags", [0, 6, 9])
+def test_nce_diag_offset_shards(gpu, flags):
+    """Rows [lo, hi) against all columns with diag_offset=lo reproduce those rows of the
+    single-device problem: the per-rank computation of the data-parallel step."""
+    g = torch.Generator().manual_seed(flags + 100)
+    n = 611
+    A = F.normalize(torch.randn(n, 128, generator=g), dim=1)
+    B = A.clone() if flags == 9 else F.normalize(torch.randn(n, 128, generator=g), dim=1)
+    bias = torch.log_softmax(torch.randn(n, generator=g), 0) if flags == 6 else None
+    k1 = torch.randint(0, 150, (n,), generator=g)
+    k2 = torch.randint(0, 40, (n,), generator=g)
+    dev = lambda t: None if t is None else t.to(gpu)
+    for lo, hi in [(0, 130), (130, 371), (371, 611)]:
+        ref, valid = _nce_rows_ref(A[lo:hi].double(), B.double(), None if bias is None else bias.double(),
+                                   k1[lo:hi], k1, k2[lo:hi], k2, 0.1, flags, lo)
+        s, c = ops.nce_sum(dev(A[lo:hi]), dev(B), dev(bias), dev(k1[lo:hi]), dev(k1), dev(k2[lo:hi]), dev(k2),
+                           tau=0.1, flags=flags, diag_offset=lo)
+        assert abs(s.item() - ref.sum().item()) < 1e-3, (lo, s.item(), ref.sum().item())
+        assert c.item() == valid.sum().item()

@@ -84,3 +84,29 @@ def test_step_runs_with_dropout_and_updates(gpu):
     assert not torch.equal(before, model.item_proj.weight.detach())
     # the two dropout views differ, so the DuoRec InfoNCE term is not at its p=0 minimum
     assert cl.item() > 0
+
+
+def test_dp_objective_single_rank_equals_single_gpu_step(gpu):
+    """dist.contrastive_objective_dp at world size 1 == v1_usertower_train.contrastive_losses."""
+    from recsys_amd import dist as Dd
+    cfg = small_cfg(num_items=500)
+    items = small_universe(500)
+    bd = to_dev(synth.make_batch(items, 64, seed=21), gpu)
+    _, dut = paired_towers(cfg, gpu)
+    dut.train()
+    it = TT.SASRecItemTower(500, 128, items.log_q.clone()).to(gpu)
+    it.init_from_pretrained(items.pretrained.to(gpu))
+    it.set_freeze_state(False)
+    pv = TT.lookup_pretrained(items.pretrained.to(gpu), bd["item_ids"])
+    tot, main, cl = TT.contrastive_losses(dut, it, it.log_q, bd, cfg, pv)
+    tot.backward()
+    g1 = [p.grad.clone() for p in dut.parameters()]
+    gw1 = it.item_matrix.weight.grad.clone()
+    dut.zero_grad(); it.zero_grad()
+    obj, tot2, main2, cl2 = Dd.contrastive_objective_dp(dut, it, it.log_q, bd, cfg, pv)
+    for a, b in [(obj, tot), (tot2, tot), (main2, main), (cl2, cl)]:
+        assert abs(a.item() - b.item()) < 1e-5
+    obj.backward()
+    for a, p in zip(g1, dut.parameters()):
+        torch.testing.assert_close(p.grad, a, atol=1e-6, rtol=1e-4)
+    torch.testing.assert_close(it.item_matrix.weight.grad, gw1, atol=1e-6, rtol=1e-4)
