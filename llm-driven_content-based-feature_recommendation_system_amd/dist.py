@@ -155,11 +155,10 @@ def contrastive_objective_dp(model, item_tower, log_q_tensor, batch, cfg, pretra
         t_loc = target_ids.reshape(-1)[flat_pos]
         user_loc = torch.div(flat_pos, L, rounding_mode="floor") + rank * B
         t_glob = all_gather_var(t_loc, counts)
-        user_glob = all_gather_var(user_loc, counts)
-        items_glob = ops.gather_rows(item_tower.get_all_embeddings(), t_glob, normalize=True)
-        bias = log_q_tensor[t_glob] * cfg.lambda_logq if cfg.lambda_logq > 0.0 else None
-        main_sum, _ = ops.nce_sum(u_loc, items_glob, bias, t_loc, t_glob, user_loc, user_glob, tau=temperature,
-                                  flags=ops.NCE_MASK_ITEM_USER, diag_offset=offset, tag="main")
+        groups = ops.TargetGroups(t_loc, user_loc, t_cols=t_glob)
+        items_d = ops.gather_rows(item_tower.get_all_embeddings(), groups.uniq, normalize=True, unique=True)
+        bias = log_q_tensor[groups.uniq] * cfg.lambda_logq if cfg.lambda_logq > 0.0 else None
+        main_sum, _ = ops.nce_grouped_sum(u_loc, items_d, bias, groups, tau=temperature, tag="main")
         main_local = main_sum / float(n_glob)
     else:
         main_local = torch.zeros((), device=device)

@@ -259,6 +259,104 @@ def nce_loss(A, B, bias=None, k1a=None, k1b=None, k2a=None, k2b=None, tau=0.1, f
 
 
 # ----------------------------------------------------------------------------------------
+# Grouped form of the live LogQ loss (distinct targets as columns, exact multiplicities)
+class TargetGroups:
+    """Index structures for rsx_nce_grouped_*: built on the GPU with a few sorts.
+
+    t_rows/u_rows: this process's rows (flat order; rows of one user are contiguous and user
+    ids are non-decreasing). t_cols: every column's target (all ranks' rows; defaults to
+    t_rows). The distinct targets of t_cols are the grouped columns."""
+
+    def __init__(self, t_rows, u_rows, t_cols=None):
+        t_cols = t_rows if t_cols is None else t_cols
+        dev = t_rows.device
+        self.uniq, col_cnt = torch.unique(t_cols, sorted=True, return_counts=True)
+        D = self.uniq.numel()
+        self.colcnt = col_cnt.to(torch.float32)
+        inv = torch.searchsorted(self.uniq, t_rows)
+        self.row_col = inv.to(torch.int32)
+        n = t_rows.numel()
+        # rows of each user: [start, end) in flat order
+        users, ucnt = torch.unique_consecutive(u_rows, return_counts=True)
+        ends = torch.cumsum(ucnt, 0)
+        starts = ends - ucnt
+        self.row_beg = torch.repeat_interleave(starts, ucnt).to(torch.int32)
+        self.row_end = torch.repeat_interleave(ends, ucnt).to(torch.int32)
+        # per-row exception list = the user's own targets, sorted within each user segment
+        seg = torch.repeat_interleave(torch.arange(users.numel(), device=dev), ucnt)
+        key = seg * D + inv
+        self.exc_cols = (torch.sort(key).values % D).to(torch.int32)
+        # per-column list of (user row range, multiplicity), sorted by column then user
+        key2 = inv * users.numel() + seg
+        k2, kn = torch.unique_consecutive(torch.sort(key2).values, return_counts=True)
+        pd = torch.div(k2, users.numel(), rounding_mode="floor")
+        pseg = k2 % users.numel()
+        self.exc_s = starts[pseg].to(torch.int32)
+        self.exc_e = ends[pseg].to(torch.int32)
+        self.exc_n = kn.to(torch.int32)
+        ar = torch.arange(D, device=dev)
+        self.col_beg = torch.searchsorted(pd, ar).to(torch.int32)
+        self.col_end = torch.searchsorted(pd, ar, right=True).to(torch.int32)
+        self.n_rows = n
+        self.n_cols = D
+
+
+class _NCEGrouped(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, A, B, bias, grp, tau, tag):
+        N.ensure_device(A)
+        A = _c(A)
+        B = _c(B)
+        n, d = A.shape[0], B.shape[0]
+        nws = N.lib().rsx_nce_workspace_floats(n, d, _NSPLIT_FWD, _NSPLIT_BWD)
+        ws = torch.empty(nws, device=A.device, dtype=torch.float32)
+        out2 = torch.empty(2, device=A.device, dtype=torch.float32)
+        with timed(f"{tag}/nce_fwd"):
+            rc = N.lib().rsx_nce_grouped_fwd(N.ptr(A), N.ptr(B), N.ptr(bias), N.ptr(grp.colcnt), N.ptr(grp.row_col),
+                                             N.ptr(grp.row_beg), N.ptr(grp.row_end), N.ptr(grp.exc_cols), n, d,
+                                             A.stride(0), B.stride(0), tau, _NSPLIT_FWD, N.ptr(ws), N.ptr(out2),
+                                             N.stream())
+        N.check(rc, "nce_grouped_fwd")
+        ctx.save_for_backward(A, B, bias, ws)
+        ctx.grp = grp
+        ctx.cfg = (n, d, tau, tag)
+        cnt = out2[1]
+        ctx.mark_non_differentiable(cnt)
+        return out2[0], cnt
+
+    @staticmethod
+    def backward(ctx, g, _gcnt):
+        A, B, bias, ws = ctx.saved_tensors
+        grp = ctx.grp
+        n, d, tau, tag = ctx.cfg
+        g = _c(g.reshape(1).to(torch.float32))
+        args = (N.ptr(A), N.ptr(B), N.ptr(bias), N.ptr(grp.colcnt), N.ptr(grp.row_col), N.ptr(grp.row_beg),
+                N.ptr(grp.row_end), N.ptr(grp.exc_cols), N.ptr(grp.col_beg), N.ptr(grp.col_end), N.ptr(grp.exc_s),
+                N.ptr(grp.exc_e), N.ptr(grp.exc_n), n, d, A.stride(0), B.stride(0), tau, _NSPLIT_FWD, _NSPLIT_BWD,
+                N.ptr(g), N.ptr(ws))
+        dA = dB = None
+        if ctx.needs_input_grad[0]:
+            dA = torch.empty_like(A)
+            with timed(f"{tag}/nce_bwd_rows"):
+                rc = N.lib().rsx_nce_grouped_bwd(*args, N.ptr(dA), None, 0, N.stream())
+            N.check(rc, "nce_grouped_bwd(rows)")
+        if ctx.needs_input_grad[1]:
+            dB = torch.empty_like(B)
+            with timed(f"{tag}/nce_bwd_cols"):
+                rc = N.lib().rsx_nce_grouped_bwd(*args, None, N.ptr(dB), 0, N.stream())
+            N.check(rc, "nce_grouped_bwd(cols)")
+        return dA, dB, None, None, None, None
+
+
+def nce_grouped_sum(A, B_distinct, bias, groups: TargetGroups, tau=0.1, tag="nce"):
+    """(sum of row losses, N) of the live LogQ loss with same-item / same-user masking, with
+    the columns given as the distinct targets (B_distinct[d] = normalised item groups.uniq[d])."""
+    if bias is not None:
+        bias = _c(bias.to(torch.float32))
+    return _NCEGrouped.apply(A, B_distinct, bias, groups, float(tau), str(tag))
+
+
+# ----------------------------------------------------------------------------------------
 # Optional per-op device timing (bench.py): HIP events on the launching (current) stream.
 _TIMING = {"on": False, "events": {}}
 

@@ -121,13 +121,14 @@ def contrastive_losses(model, item_tower, log_q_tensor, batch, cfg, pretrained_v
         flat_user_emb = ops.gather_rows(output_1.reshape(-1, D), flat_pos, normalize=True, unique=True)
         flat_targets = target_ids.reshape(-1)[flat_pos]
         flat_user_ids = torch.div(flat_pos, seq_len, rounding_mode="floor")
-        # norm_item_embeddings[flat_targets] == normalize(item_matrix[flat_targets]) row-wise
-        batch_item_emb = ops.gather_rows(item_tower.get_all_embeddings(), flat_targets, normalize=True)
-        bias = log_q_tensor[flat_targets] * cfg.lambda_logq if cfg.lambda_logq > 0.0 else None
-        k1 = flat_targets.to(torch.int32)
-        k2 = flat_user_ids.to(torch.int32)
-        main_loss = ops.nce_loss(flat_user_emb, batch_item_emb, bias, k1, k1, k2, k2, tau=0.1,
-                                 flags=ops.NCE_MASK_ITEM_USER, tag="main")
+        # Grouped evaluation of inbatch_corrected_logq_loss (v1_refine_usertower.py:826-861):
+        # the columns normalize(item_matrix)[flat_targets] collapse onto the distinct targets
+        # with exact multiplicities (see csrc/infonce.hip); same result, N/D fewer FLOPs.
+        groups = ops.TargetGroups(flat_targets, flat_user_ids)
+        items_d = ops.gather_rows(item_tower.get_all_embeddings(), groups.uniq, normalize=True, unique=True)
+        bias = log_q_tensor[groups.uniq] * cfg.lambda_logq if cfg.lambda_logq > 0.0 else None
+        main_sum, main_cnt = ops.nce_grouped_sum(flat_user_emb, items_d, bias, groups, tau=0.1, tag="main")
+        main_loss = main_sum / main_cnt.clamp(min=1.0)
     else:
         main_loss = torch.zeros((), device=device)
 

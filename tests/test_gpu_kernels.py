@@ -284,3 +284,58 @@ def test_nce_diag_offset_shards(gpu, flags):
                            tau=0.1, flags=flags, diag_offset=lo)
         assert abs(s.item() - ref.sum().item()) < 1e-3, (lo, s.item(), ref.sum().item())
         assert c.item() == valid.sum().item()
+
+
+@pytest.mark.parametrize("n_users,max_len,n_items,seed", [(40, 30, 25, 0), (300, 50, 400, 1), (7, 3, 5, 2)])
+def test_nce_grouped_equals_plain(gpu, n_users, max_len, n_items, seed):
+    """Grouped (distinct-target columns, exact multiplicities) == the plain N x N kernel with
+    same-item + same-user masks, loss and both gradients (through the column gather)."""
+    g = torch.Generator().manual_seed(seed)
+    lens = torch.randint(1, max_len + 1, (n_users,), generator=g)
+    users = torch.repeat_interleave(torch.arange(n_users), lens)
+    n = users.numel()
+    t = torch.randint(1, n_items + 1, (n,), generator=g)
+    W = torch.randn(n_items + 1, 128, generator=g)
+    lq = torch.log_softmax(torch.randn(n_items + 1, generator=g), 0)
+    U = F.normalize(torch.randn(n, 128, generator=g), dim=1)
+    d = lambda x: x.to(gpu)
+    # plain: columns = normalize(W)[t]
+    U1 = d(U).requires_grad_()
+    W1 = d(W).requires_grad_()
+    cols = ops.gather_rows(W1, d(t), normalize=True)
+    s1, c1 = ops.nce_sum(U1, cols, d(lq)[d(t)], d(t), d(t), d(users), d(users), tau=0.1, flags=6)
+    (s1 / c1).backward()
+    # grouped
+    U2 = d(U).requires_grad_()
+    W2 = d(W).requires_grad_()
+    grp = ops.TargetGroups(d(t), d(users))
+    items_d = ops.gather_rows(W2, grp.uniq, normalize=True, unique=True)
+    s2, c2 = ops.nce_grouped_sum(U2, items_d, d(lq)[grp.uniq], grp, tau=0.1)
+    (s2 / c2).backward()
+    assert c1.item() == c2.item() == n
+    assert abs(s1.item() - s2.item()) < 1e-3 * max(1.0, abs(s1.item())), (s1.item(), s2.item())
+    torch.testing.assert_close(U2.grad, U1.grad, atol=1e-6, rtol=1e-4)
+    torch.testing.assert_close(W2.grad, W1.grad, atol=1e-6, rtol=1e-4)
+
+
+def test_nce_grouped_sharded_rows(gpu):
+    """Rows of one shard against the distinct targets of all shards (the data-parallel form)."""
+    g = torch.Generator().manual_seed(9)
+    n_users, n_items = 120, 60
+    lens = torch.randint(1, 40, (n_users,), generator=g)
+    users = torch.repeat_interleave(torch.arange(n_users), lens)
+    n = users.numel()
+    t = torch.randint(1, n_items + 1, (n,), generator=g)
+    W = F.normalize(torch.randn(n_items + 1, 128, generator=g), dim=1)
+    lq = torch.log_softmax(torch.randn(n_items + 1, generator=g), 0)
+    U = F.normalize(torch.randn(n, 128, generator=g), dim=1)
+    d = lambda x: x.to(gpu)
+    ref, _ = _nce_rows_ref(U.double(), W[t].double(), lq[t].double(), t, t, users, users, 0.1, 6, 0)
+    cut = int(torch.nonzero(users == 50)[0])  # shard boundary on a user boundary
+    tot = 0.0
+    for lo, hi in [(0, cut), (cut, n)]:
+        grp = ops.TargetGroups(d(t[lo:hi]), d(users[lo:hi]), t_cols=d(t))
+        s, c = ops.nce_grouped_sum(d(U[lo:hi]), d(W)[grp.uniq], d(lq)[grp.uniq], grp, tau=0.1)
+        assert abs(s.item() - ref[lo:hi].sum().item()) < 1e-3
+        tot += s.item()
+    assert abs(tot - ref.sum().item()) < 2e-3
