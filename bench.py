@@ -119,6 +119,11 @@ def main():
         batches.append({k: (v.to(device) if torch.is_tensor(v) else v) for k, v in sl.items()})
     n_valid = [int((~b["padding_mask"]).sum()) for b in batches]
     n_glob = [D.all_gather_counts(n, device) for n in n_valid]
+    # distinct targets of each global batch = the grouped loss's column count
+    n_dist = []
+    for s in range(2):
+        g = synth.make_batch(items, args.batch, seed=args.seed + 100 + s)
+        n_dist.append(int(torch.unique(g["target_ids"][~g["padding_mask"]]).numel()))
     torch.cuda.synchronize()
 
     def step(i):
@@ -146,14 +151,14 @@ def main():
     elapsed = float(elapsed.item())
     total_loss = float(losses[0].item())
 
-    # roofline of the dominant kernel: main-loss InfoNCE backward, row-owned pass
-    # (S recompute + dU product on fp32 MFMA). Algorithmic FLOPs per launch =
-    # 4 * N_local * N_global * 128 (2N^2 d per product; the bwd's one S
-    # recompute is attributed to this launch, the column pass counts only its product).
+    # roofline of the dominant kernel: the main-loss InfoNCE backward, row-owned pass
+    # (grouped form: S recompute + dU product over N_local x D distinct-target columns on the
+    # fp32 MFMA). FLOPs per launch = 4 * N_local * D * 128 (2 * N * D * d per product;
+    # SURVEY.md §8d counts 2 N^2 d per product for the ungrouped reference formulation).
     flops = 0.0
     for i in range(args.steps):
         cnts = n_glob[i % 2]
-        flops += 4.0 * cnts[rank] * sum(cnts) * 128
+        flops += 4.0 * cnts[rank] * n_dist[i % 2] * 128
     launches, ms = kernel_times.get("main/nce_bwd_rows", (0, 0.0))
     avg_s = (ms / 1e3) / max(launches, 1)
     achieved = (flops / max(launches, 1)) / avg_s / 1e12 if launches else None
@@ -176,10 +181,11 @@ def main():
         "config": {"workload": "user-tower two-view contrastive train step (fwd x2 + LogQ in-batch loss + "
                                "DuoRec + bwd + clip + AdamW), BASELINE configs[1]",
                    "global_batch": args.batch, "seq_len": 50, "d_model": 128, "items": args.items,
-                   "valid_positions_per_batch": [sum(c) for c in n_glob], "dropout": args.dropout,
+                   "valid_positions_per_batch": [sum(c) for c in n_glob],
+                   "distinct_targets_per_batch": n_dist, "dropout": args.dropout,
                    "item_matrix": "frozen" if args.freeze_items else "unfrozen (lr x0.05)",
                    "parallelism": f"dp{world} (users split by rank, RCCL all-gather of ids/z, grad all-reduce)"},
-        "roofline": {"kernel": "nce_bwd_k<6,row-owned> (main LogQ loss backward)", "bound": "mfma",
+        "roofline": {"kernel": "nce_grouped_bwd_k<row-owned> (main LogQ loss backward)", "bound": "mfma",
                      "achieved": round(achieved, 2) if achieved else None, "peak": FP32_MFMA_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4) if achieved else None,
                      "traffic": None, "avg_launch_ms": round(avg_s * 1e3, 4)},

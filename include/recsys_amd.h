@@ -34,43 +34,47 @@ const char* rsx_target_arch(void);
  * Replaces tower_code/v1_refine_usertower.py:434-459:
  *   seq_emb = item_proj(pretrained_vecs); seq_emb += E_j(ids_j) * s_g[j] (j = 0..5);
  *   seq_emb += pos_emb(arange(L)); seq_emb = emb_ln(seq_emb); emb_dropout(seq_emb)
- * base      [B*L, D] = item_proj output (nullable => 0)
- * ids/tables: ntab (<=6) device pointers, ids int64 [B*L], tables [rows_j, D]
+ * over T tokens: dense [B, L] (tok_pos NULL => position = token % L) or any packed token
+ * list with tok_pos[T] (int64) giving each token's position (L <= 64).
+ * base      [T, D] = item_proj output (nullable => 0)
+ * ids/tables: ntab (<=6) device pointers, ids int64 [T], tables [rows_j, D]
  * gate      [ntab] device (s_g = sigmoid(seq_gate) * s_mask); a gate that is exactly 0
  *           skips its gather (forward-exact) and reports a zero gate/table gradient
  *           (exact for the reference, whose zero gates come from a constant 0 mask)
  * pos [L, D], ln_w/ln_b [D] (ln_w == NULL => no LayerNorm: out = pre-LN sum, bit-exact
- * with the reference's op order), mean/rstd [B*L] saved for the backward.
+ * with the reference's op order), mean/rstd [T] saved for the backward.
  * D in {64, 128, 256}. Dropout p in [0,1) via counter hash (seed). */
 int rsx_seq_embed_fwd(const float* base, const int64_t* const* ids, const float* const* tables, int ntab,
-                      const float* gate, const float* pos, const float* ln_w, const float* ln_b, float eps,
-                      int64_t B, int64_t L, int64_t D, float p_drop, uint64_t seed, float* out, float* mean,
-                      float* rstd, void* stream);
+                      const float* gate, const float* pos, const int64_t* tok_pos, const float* ln_w,
+                      const float* ln_b, float eps, int64_t T, int64_t L, int64_t D, float p_drop, uint64_t seed,
+                      float* out, float* mean, float* rstd, void* stream);
 
-/* Backward of rsx_seq_embed_fwd. dbase [B*L,D] written; dtables[j], dgate [ntab], dpos [L,D],
+/* Backward of rsx_seq_embed_fwd. dbase [T,D] written; dtables[j], dgate [ntab], dpos [L,D],
  * dln_w/dln_b [D] accumulated (nullable). padding_idx[j]: rows excluded from the table
  * gradient exactly like nn.Embedding(padding_idx=...) (-1 = none). table_rows[j] lets small
  * tables (time buckets) accumulate in LDS before one flush per workgroup. */
 int rsx_seq_embed_bwd(const float* base, const int64_t* const* ids, const float* const* tables,
                       const int64_t* table_rows, const int64_t* padding_idx, int ntab, const float* gate,
-                      const float* pos, const float* ln_w, const float* mean, const float* rstd, float eps,
-                      int64_t B, int64_t L, int64_t D, float p_drop, uint64_t seed, const float* dout,
-                      float* dbase, float* const* dtables, float* dgate, float* dpos, float* dln_w,
-                      float* dln_b, void* stream);
+                      const float* pos, const int64_t* tok_pos, const float* ln_w, const float* mean,
+                      const float* rstd, float eps, int64_t T, int64_t L, int64_t D, float p_drop, uint64_t seed,
+                      const float* dout, float* dbase, float* const* dtables, float* dgate, float* dpos,
+                      float* dln_w, float* dln_b, void* stream);
 
 /* ---- A3 / A9: masked multi-head self-attention core (L <= 64) -----------------------
  * Replaces the attention inside nn.TransformerEncoderLayer (norm_first, batch_first) at
  * tower_code/v1_refine_usertower.py:343-352,461-466 (causal + key padding) and
- * item_tower.py:169-182,281 (unmasked). qkv [B, L, 3*H*Dh] = in_proj output; out
- * [B, L, H*Dh] = pre-out_proj head concat; lse [B, H, L]. key_pad [B, L] uint8 (1 = pad,
- * nullable). Training-path semantics: a fully masked query row gets zero probabilities.
+ * item_tower.py:169-182,281 (unmasked). Tokens are dense sequences (seg_off NULL: T = B*L)
+ * or packed variable-length segments (seg_off [B+1] int32 token offsets, each <= 64 long).
+ * qkv [T, 3*H*Dh] = in_proj output; out [T, H*Dh] = pre-out_proj head concat; lse [T, H].
+ * key_pad [T] uint8 (1 = pad, nullable). Causal = key position <= query position within
+ * the sequence. Training-path semantics: a fully masked query row gets zero probabilities.
  * Dh in {16, 32, 64} (backward: {16, 32}). */
-int rsx_mha_fwd(const float* qkv, const uint8_t* key_pad, int64_t B, int64_t L, int64_t H, int64_t Dh, int causal,
-                float p_drop, uint64_t seed, float* out, float* lse, void* stream);
-/* dqkv [B, L, 3*H*Dh] written. */
-int rsx_mha_bwd(const float* qkv, const uint8_t* key_pad, const float* out, const float* lse, const float* dout,
-                int64_t B, int64_t L, int64_t H, int64_t Dh, int causal, float p_drop, uint64_t seed, float* dqkv,
-                void* stream);
+int rsx_mha_fwd(const float* qkv, const uint8_t* key_pad, const int* seg_off, int64_t B, int64_t L, int64_t H,
+                int64_t Dh, int causal, float p_drop, uint64_t seed, float* out, float* lse, void* stream);
+/* dqkv [T, 3*H*Dh] written. */
+int rsx_mha_bwd(const float* qkv, const uint8_t* key_pad, const int* seg_off, const float* out, const float* lse,
+                const float* dout, int64_t B, int64_t L, int64_t H, int64_t Dh, int causal, float p_drop,
+                uint64_t seed, float* dqkv, void* stream);
 
 /* ---- A6 / A7 / A12: fused in-batch contrastive cross-entropy ------------------------
  * S_ij = <A_i,B_j>/tau - bias_j over an implicit N x M matrix (never materialised),

@@ -29,12 +29,12 @@ _SIGS = {
     "rsx_last_error": (ctypes.c_char_p, []),
     "rsx_abi_version": (c_i, []),
     "rsx_target_arch": (ctypes.c_char_p, []),
-    "rsx_seq_embed_fwd": (c_i, [c_p, c_p, c_p, c_i, c_p, c_p, c_p, c_p, c_f, c_i64, c_i64, c_i64, c_f, c_u64,
+    "rsx_seq_embed_fwd": (c_i, [c_p, c_p, c_p, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_i64, c_i64, c_i64, c_f, c_u64,
                                 c_p, c_p, c_p, c_p]),
-    "rsx_seq_embed_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_i64, c_i64, c_i64,
-                                c_f, c_u64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
-    "rsx_mha_fwd": (c_i, [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i, c_f, c_u64, c_p, c_p, c_p]),
-    "rsx_mha_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i, c_f, c_u64, c_p, c_p]),
+    "rsx_seq_embed_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_i64, c_i64,
+                                c_i64, c_f, c_u64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "rsx_mha_fwd": (c_i, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i, c_f, c_u64, c_p, c_p, c_p]),
+    "rsx_mha_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i, c_f, c_u64, c_p, c_p]),
     "rsx_nce_workspace_floats": (c_i64, [c_i64, c_i64, c_i, c_i]),
     "rsx_nce_fwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_f, c_i, c_i, c_p,
                           c_p, c_p]),

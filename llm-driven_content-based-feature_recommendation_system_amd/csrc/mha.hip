@@ -3,9 +3,10 @@
 //   * SASRecUserTower   tower_code/v1_refine_usertower.py:343-352, 461-466
 //     (causal mask triu(ones,1) + src_key_padding_mask, left padding, L = 50, dh = 32)
 //   * HybridItemTower   item_tower.py:169-182, 281 (no mask, 16 field tokens, dh = d/4)
-// Input is the packed in_proj output qkv[B, L, 3*D] (q | k | v, heads contiguous inside
-// each part, exactly torch's in_proj_weight layout); output is the concatenated head
-// output [B, L, D] that feeds out_proj.
+// Input is the in_proj output qkv[T, 3*D] (q | k | v, heads contiguous inside each part,
+// exactly torch's in_proj_weight layout) for T tokens: dense sequences (T = B*L) or packed
+// variable-length segments (seg_off, used by the training step to skip left padding);
+// output is the concatenated head output [T, D] that feeds out_proj.
 //
 // Semantics pinned to the training-mode (non fast-path) reference: a query row whose keys
 // are all masked (left-padded positions under the causal mask) gets all-zero
@@ -22,10 +23,11 @@ namespace {
 constexpr int kLMax = 64;
 
 struct FwdArgs {
-  const float* qkv;      // [B, L, 3D]
-  const uint8_t* kpad;   // [B, L] 1 = pad (masked key) or nullptr
-  float* out;            // [B, L, D]
-  float* lse;            // [B, H, L] (natural log-sum-exp of the scaled scores; -inf if fully masked)
+  const float* qkv;      // [T, 3D] tokens (dense: T = B*L, token b*L+l; packed: segments by seg)
+  const uint8_t* kpad;   // [T] 1 = pad (masked key) or nullptr
+  const int* seg;        // [B+1] token offsets of each sequence (packed) or nullptr (dense, length L)
+  float* out;            // [T, D]
+  float* lse;            // [T, H] (natural log-sum-exp of the scaled scores; -inf if fully masked)
   int B, L, H, causal;
   float scale;
   rsx::Dropout drop;
@@ -39,18 +41,21 @@ __global__ __launch_bounds__(64) void mha_fwd_k(FwdArgs a) {
   const int D = a.H * DH;
   const int b = blockIdx.x / a.H, hd = blockIdx.x % a.H;
   const int i = threadIdx.x;
-  const float* base = a.qkv + (int64_t)b * a.L * 3 * D;
+  const int64_t tok0 = a.seg ? (int64_t)a.seg[b] : (int64_t)b * a.L;
+  int L = a.seg ? (a.seg[b + 1] - a.seg[b]) : a.L;
+  if (L > kLMax) L = kLMax;  // packed segments are <= 51 by construction
+  const float* base = a.qkv + tok0 * 3 * D;
 
   constexpr int V4 = DH / 4;
-  for (int t = threadIdx.x; t < a.L * V4; t += 64) {
+  for (int t = threadIdx.x; t < L * V4; t += 64) {
     const int r = t / V4, c4 = t % V4;
     const float4* rowp = reinterpret_cast<const float4*>(base + (int64_t)r * 3 * D);
     reinterpret_cast<float4*>(&sK[r][0])[c4] = rowp[(D + hd * DH) / 4 + c4];
     reinterpret_cast<float4*>(&sV[r][0])[c4] = rowp[(2 * D + hd * DH) / 4 + c4];
   }
-  if (i < a.L) sPad[i] = a.kpad ? (int)a.kpad[(int64_t)b * a.L + i] : 0;
+  if (i < L) sPad[i] = a.kpad ? (int)a.kpad[tok0 + i] : 0;
   __syncthreads();
-  if (i >= a.L) return;
+  if (i >= L) return;
 
   float q[DH];
   {
@@ -66,7 +71,7 @@ __global__ __launch_bounds__(64) void mha_fwd_k(FwdArgs a) {
 #pragma unroll
   for (int j = 0; j < kLMax; ++j) {
     s[j] = -INFINITY;
-    if (j < a.L) {
+    if (j < L) {
       const bool allowed = !sPad[j] && (!a.causal || j <= i);
       float d = 0.0f;
 #pragma unroll
@@ -97,10 +102,10 @@ __global__ __launch_bounds__(64) void mha_fwd_k(FwdArgs a) {
     }
     const float inv = 1.0f / sum;
     lse = mx + logf(sum);
-    const uint64_t rowidx = (((uint64_t)b * a.H + hd) * a.L + i) * a.L;
+    const uint64_t rowidx = ((uint64_t)(tok0 + i) * a.H + hd) * kLMax;
 #pragma unroll
     for (int j = 0; j < kLMax; ++j) {
-      if (j < a.L) {
+      if (j < L) {
         float p = s[j] * inv;
         p = a.drop.apply(p, rowidx + j);
         if (p != 0.0f) {
@@ -116,19 +121,20 @@ __global__ __launch_bounds__(64) void mha_fwd_k(FwdArgs a) {
       }
     }
   }
-  float4* op = reinterpret_cast<float4*>(a.out + ((int64_t)b * a.L + i) * D + hd * DH);
+  float4* op = reinterpret_cast<float4*>(a.out + (tok0 + i) * D + hd * DH);
 #pragma unroll
   for (int t = 0; t < V4; ++t) op[t] = make_float4(o[4 * t], o[4 * t + 1], o[4 * t + 2], o[4 * t + 3]);
-  if (a.lse) a.lse[((int64_t)b * a.H + hd) * a.L + i] = lse;
+  if (a.lse) a.lse[(tok0 + i) * a.H + hd] = lse;
 }
 
 struct BwdArgs {
   const float* qkv;
   const uint8_t* kpad;
-  const float* out;   // forward output O [B, L, D]
-  const float* lse;   // [B, H, L]
-  const float* dout;  // [B, L, D]
-  float* dqkv;        // [B, L, 3D] (written)
+  const int* seg;
+  const float* out;   // forward output O [T, D]
+  const float* lse;   // [T, H]
+  const float* dout;  // [T, D]
+  float* dqkv;        // [T, 3D] (written)
   int B, L, H, causal;
   float scale;
   rsx::Dropout drop;
@@ -145,22 +151,25 @@ __global__ __launch_bounds__(64) void mha_bwd_k(BwdArgs a) {
   const int D = a.H * DH;
   const int b = blockIdx.x / a.H, hd = blockIdx.x % a.H;
   const int lane = threadIdx.x;
-  const float* base = a.qkv + (int64_t)b * a.L * 3 * D;
-  const float* dob = a.dout + (int64_t)b * a.L * D;
+  const int64_t tok0 = a.seg ? (int64_t)a.seg[b] : (int64_t)b * a.L;
+  int L = a.seg ? (a.seg[b + 1] - a.seg[b]) : a.L;
+  if (L > kLMax) L = kLMax;  // packed segments are <= 51 by construction
+  const float* base = a.qkv + tok0 * 3 * D;
+  const float* dob = a.dout + tok0 * D;
   constexpr int V4 = DH / 4;
 
-  for (int t = threadIdx.x; t < a.L * V4; t += 64) {
+  for (int t = threadIdx.x; t < L * V4; t += 64) {
     const int r = t / V4, c4 = t % V4;
     const float4* rowp = reinterpret_cast<const float4*>(base + (int64_t)r * 3 * D);
     reinterpret_cast<float4*>(&sQ[r][0])[c4] = rowp[(hd * DH) / 4 + c4];
     reinterpret_cast<float4*>(&sK[r][0])[c4] = rowp[(D + hd * DH) / 4 + c4];
     reinterpret_cast<float4*>(&sdO[r][0])[c4] = reinterpret_cast<const float4*>(dob + (int64_t)r * D + hd * DH)[c4];
   }
-  if (lane < a.L) {
-    sPad[lane] = a.kpad ? (int)a.kpad[(int64_t)b * a.L + lane] : 0;
-    sLse[lane] = a.lse[((int64_t)b * a.H + hd) * a.L + lane];
+  if (lane < L) {
+    sPad[lane] = a.kpad ? (int)a.kpad[tok0 + lane] : 0;
+    sLse[lane] = a.lse[(tok0 + lane) * a.H + hd];
     // delta_i = dO_i . O_i  (holds with dropout: sum_j P_ij dP_ij = dO_i . O_i)
-    const float4* op = reinterpret_cast<const float4*>(a.out + ((int64_t)b * a.L + lane) * D + hd * DH);
+    const float4* op = reinterpret_cast<const float4*>(a.out + (tok0 + lane) * D + hd * DH);
     const float4* dp = reinterpret_cast<const float4*>(dob + (int64_t)lane * D + hd * DH);
     float d = 0.0f;
 #pragma unroll
@@ -175,7 +184,7 @@ __global__ __launch_bounds__(64) void mha_bwd_k(BwdArgs a) {
   // ---- pass A: lane j owns key/value row j: dK_j, dV_j, and dS column j into LDS ----
   const int j = lane;
   float kj[DH], vj[DH], dk[DH], dv[DH];
-  const bool jok = j < a.L;
+  const bool jok = j < L;
   if (jok) {
     const float4* vp = reinterpret_cast<const float4*>(base + (int64_t)j * 3 * D + 2 * D + hd * DH);
 #pragma unroll
@@ -193,7 +202,7 @@ __global__ __launch_bounds__(64) void mha_bwd_k(BwdArgs a) {
   for (int e = 0; e < DH; ++e) { dk[e] = 0.0f; dv[e] = 0.0f; }
   const bool jpad = jok ? (sPad[j] != 0) : true;
 
-  for (int i = 0; i < a.L; ++i) {
+  for (int i = 0; i < L; ++i) {
     const float lse_i = sLse[i];
     float ds = 0.0f;
     const bool allowed = jok && !jpad && (!a.causal || j <= i) && lse_i != -INFINITY;
@@ -209,7 +218,7 @@ __global__ __launch_bounds__(64) void mha_bwd_k(BwdArgs a) {
         pdot = fmaf(gv.z, vj[4 * t + 2], pdot); pdot = fmaf(gv.w, vj[4 * t + 3], pdot);
       }
       const float p = __expf(sdot * a.scale - lse_i);
-      const uint64_t idx = (((uint64_t)b * a.H + hd) * a.L + i) * a.L + j;
+      const uint64_t idx = ((uint64_t)(tok0 + i) * a.H + hd) * kLMax + j;
       float pd = p, dp = pdot;
       if (a.drop.active()) {
         const bool keep = rsx::hash_u32(a.drop.seed, idx) >= a.drop.thresh;
@@ -231,7 +240,7 @@ __global__ __launch_bounds__(64) void mha_bwd_k(BwdArgs a) {
   }
   __syncthreads();
 
-  float* db = a.dqkv + (int64_t)b * a.L * 3 * D;
+  float* db = a.dqkv + tok0 * 3 * D;
   if (jok) {
     float4* kp = reinterpret_cast<float4*>(db + (int64_t)j * 3 * D + D + hd * DH);
     float4* vp = reinterpret_cast<float4*>(db + (int64_t)j * 3 * D + 2 * D + hd * DH);
@@ -244,11 +253,11 @@ __global__ __launch_bounds__(64) void mha_bwd_k(BwdArgs a) {
 
   // ---- pass B: lane i owns query row i: dQ_i = sum_j dS_ij K_j ----
   const int i = lane;
-  if (i < a.L) {
+  if (i < L) {
     float dq[DH];
 #pragma unroll
     for (int e = 0; e < DH; ++e) dq[e] = 0.0f;
-    for (int jj = 0; jj < a.L; ++jj) {
+    for (int jj = 0; jj < L; ++jj) {
       const float ds = sdS[i][jj];
       if (ds != 0.0f) {
 #pragma unroll
@@ -267,8 +276,9 @@ __global__ __launch_bounds__(64) void mha_bwd_k(BwdArgs a) {
 
 }  // namespace
 
-RSX_API int rsx_mha_fwd(const float* qkv, const uint8_t* key_pad, int64_t B, int64_t L, int64_t H, int64_t Dh,
-                        int causal, float p_drop, uint64_t seed, float* out, float* lse, void* stream) {
+RSX_API int rsx_mha_fwd(const float* qkv, const uint8_t* key_pad, const int* seg_off, int64_t B, int64_t L,
+                        int64_t H, int64_t Dh, int causal, float p_drop, uint64_t seed, float* out, float* lse,
+                        void* stream) {
   RSX_ARG(qkv && out, "null tensor");
   RSX_ARG(L >= 1 && L <= kLMax, "L must be in [1,64]");
   RSX_ARG(Dh == 16 || Dh == 32 || Dh == 64, "head dim must be 16, 32 or 64");
@@ -276,7 +286,7 @@ RSX_API int rsx_mha_fwd(const float* qkv, const uint8_t* key_pad, int64_t B, int
   RSX_ARG(p_drop >= 0.0f && p_drop < 1.0f, "p_drop must be in [0,1)");
   if (B == 0) return 0;
   FwdArgs a;
-  a.qkv = qkv; a.kpad = key_pad; a.out = out; a.lse = lse;
+  a.qkv = qkv; a.kpad = key_pad; a.seg = seg_off; a.out = out; a.lse = lse;
   a.B = (int)B; a.L = (int)L; a.H = (int)H; a.causal = causal;
   a.scale = 1.0f / sqrtf((float)Dh);
   a.drop = rsx::make_dropout(p_drop, seed);
@@ -289,16 +299,16 @@ RSX_API int rsx_mha_fwd(const float* qkv, const uint8_t* key_pad, int64_t B, int
   return 0;
 }
 
-RSX_API int rsx_mha_bwd(const float* qkv, const uint8_t* key_pad, const float* out, const float* lse,
-                        const float* dout, int64_t B, int64_t L, int64_t H, int64_t Dh, int causal, float p_drop,
-                        uint64_t seed, float* dqkv, void* stream) {
+RSX_API int rsx_mha_bwd(const float* qkv, const uint8_t* key_pad, const int* seg_off, const float* out,
+                        const float* lse, const float* dout, int64_t B, int64_t L, int64_t H, int64_t Dh, int causal,
+                        float p_drop, uint64_t seed, float* dqkv, void* stream) {
   RSX_ARG(qkv && out && lse && dout && dqkv, "null tensor");
   RSX_ARG(L >= 1 && L <= kLMax, "L must be in [1,64]");
   RSX_ARG(Dh == 16 || Dh == 32, "backward head dim must be 16 or 32");
   RSX_ARG(p_drop >= 0.0f && p_drop < 1.0f, "p_drop must be in [0,1)");
   if (B == 0) return 0;
   BwdArgs a;
-  a.qkv = qkv; a.kpad = key_pad; a.out = out; a.lse = lse; a.dout = dout; a.dqkv = dqkv;
+  a.qkv = qkv; a.kpad = key_pad; a.seg = seg_off; a.out = out; a.lse = lse; a.dout = dout; a.dqkv = dqkv;
   a.B = (int)B; a.L = (int)L; a.H = (int)H; a.causal = causal;
   a.scale = 1.0f / sqrtf((float)Dh);
   a.drop = rsx::make_dropout(p_drop, seed);

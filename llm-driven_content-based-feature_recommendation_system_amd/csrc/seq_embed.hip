@@ -19,6 +19,7 @@ struct FwdArgs {
   const float* tab[kMaxTab];
   const float* gate;  // [ntab] on device, nullptr => 1.0
   const float* pos;   // [L,D] or nullptr
+  const int64_t* tok_pos;  // [T] position of each token (packed layouts) or nullptr => r % L
   const float* ln_w;  // [D]  (nullptr => no LayerNorm, out = x)
   const float* ln_b;  // [D]
   float* out;
@@ -64,7 +65,7 @@ __device__ __forceinline__ float4 build_row(const FwdArgs& a, int64_t r, int c, 
     }
   }
   if (a.pos) {
-    const int l = (int)(r % a.L);
+    const int l = a.tok_pos ? (int)a.tok_pos[r] : (int)(r % a.L);
     x = f4_add_rn(x, reinterpret_cast<const float4*>(a.pos + (int64_t)l * D)[c]);
   }
   return x;
@@ -135,30 +136,32 @@ struct BwdArgs {
   float* dpos;            // [L,D] accumulated or nullptr
   float* dln_w;           // [D] accumulated or nullptr
   float* dln_b;
-  int64_t B;
-  int chunks;
+  int64_t rows_per_block;
   int small_total;        // floats of LDS for small tables
 };
 
 constexpr int kSmallMax = 8192;  // floats (32 KiB)
 
+// One workgroup per contiguous chunk of tokens. Position, small-table, LN and gate gradients
+// accumulate in LDS / registers and are flushed once per workgroup (no per-token atomics on
+// the hot 50-row position table); big-table rows are scatter-added with float atomics.
 template <int D>
 __global__ __launch_bounds__(256) void seq_embed_bwd_k(BwdArgs a) {
   constexpr int LPR = D / 4;
   constexpr int RPW = 64 / LPR;
   constexpr int NW = 4;
-  extern __shared__ __attribute__((aligned(16))) float s_small[];  // small-table grads
-  __shared__ __attribute__((aligned(16))) float s_red[NW][3][D];
+  extern __shared__ __attribute__((aligned(16))) float s_dyn[];  // [L*D] positions + small tables
+  __shared__ __attribute__((aligned(16))) float s_red[NW][2][D];
   __shared__ float s_gate[NW][kMaxTab];
 
   const FwdArgs& f = a.f;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int sub = lane / LPR, c = lane % LPR;
-  const int l = blockIdx.x % f.L;
-  const int chunk = blockIdx.x / f.L;
-
-  for (int i = tid; i < a.small_total; i += blockDim.x) s_small[i] = 0.0f;
+  float* s_pos = s_dyn;
+  float* s_small = s_dyn + (int64_t)f.L * D;
+  const int lds_total = f.L * D + a.small_total;
+  for (int i = tid; i < lds_total; i += blockDim.x) s_dyn[i] = 0.0f;
   __syncthreads();
 
   float g[kMaxTab];
@@ -168,69 +171,63 @@ __global__ __launch_bounds__(256) void seq_embed_bwd_k(BwdArgs a) {
   float4 w = make_float4(1.f, 1.f, 1.f, 1.f);
   if (do_ln) w = reinterpret_cast<const float4*>(f.ln_w)[c];
 
-  float4 acc_pos = make_float4(0.f, 0.f, 0.f, 0.f);
   float4 acc_w = make_float4(0.f, 0.f, 0.f, 0.f);
   float4 acc_b = make_float4(0.f, 0.f, 0.f, 0.f);
   float acc_g[kMaxTab];
 #pragma unroll
   for (int j = 0; j < kMaxTab; ++j) acc_g[j] = 0.0f;
 
-  const int64_t per_block = (a.B - chunk + a.chunks - 1) / a.chunks;  // rows b = chunk + k*chunks
-  for (int64_t k0 = 0; k0 < per_block; k0 += NW * RPW) {
-    const int64_t k = k0 + wave * RPW + sub;
-    const bool ok = k < per_block;
-    const int64_t b = chunk + k * a.chunks;
-    const int64_t r = b * f.L + l;
-    float4 dx = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (ok) {
-      float4 dy = reinterpret_cast<const float4*>(a.dout + r * D)[c];
-      if (f.drop.active()) {
-        const uint64_t bi = (uint64_t)r * D + 4 * c;
-        dy.x = f.drop.apply(dy.x, bi + 0);
-        dy.y = f.drop.apply(dy.y, bi + 1);
-        dy.z = f.drop.apply(dy.z, bi + 2);
-        dy.w = f.drop.apply(dy.w, bi + 3);
-      }
-      dx = dy;
-      if (do_ln) {
-        const float4 x = build_row<D>(f, r, c, g);
-        const float mu = f.mean[r], rs = f.rstd[r];
-        const float4 xh = make_float4((x.x - mu) * rs, (x.y - mu) * rs, (x.z - mu) * rs, (x.w - mu) * rs);
-        acc_w.x += dy.x * xh.x; acc_w.y += dy.y * xh.y; acc_w.z += dy.z * xh.z; acc_w.w += dy.w * xh.w;
-        acc_b.x += dy.x; acc_b.y += dy.y; acc_b.z += dy.z; acc_b.w += dy.w;
-        const float4 dh = make_float4(dy.x * w.x, dy.y * w.y, dy.z * w.z, dy.w * w.w);
-        dx = dh;  // reductions happen below (all lanes of the row participate)
-        float c1 = (dh.x + dh.y) + (dh.z + dh.w);
-        float c2 = dh.x * xh.x + dh.y * xh.y + dh.z * xh.z + dh.w * xh.w;
-        c1 = rsx::wave_sum_width(c1, LPR) / (float)D;
-        c2 = rsx::wave_sum_width(c2, LPR) / (float)D;
-        dx.x = (dh.x - c1 - xh.x * c2) * rs;
-        dx.y = (dh.y - c1 - xh.y * c2) * rs;
-        dx.z = (dh.z - c1 - xh.z * c2) * rs;
-        dx.w = (dh.w - c1 - xh.w * c2) * rs;
-      }
-      if (a.dbase) reinterpret_cast<float4*>(a.dbase + r * D)[c] = dx;
-      acc_pos.x += dx.x; acc_pos.y += dx.y; acc_pos.z += dx.z; acc_pos.w += dx.w;
+  const int64_t r_begin = (int64_t)blockIdx.x * a.rows_per_block;
+  int64_t r_end = r_begin + a.rows_per_block;
+  if (r_end > f.T) r_end = f.T;
+  for (int64_t r0 = r_begin; r0 < r_end; r0 += NW * RPW) {
+    const int64_t r = r0 + wave * RPW + sub;
+    const bool ok = r < r_end;
+    if (!ok) continue;  // row groups are lane-aligned: shuffles below stay inside active groups
+    float4 dy = reinterpret_cast<const float4*>(a.dout + r * D)[c];
+    if (f.drop.active()) {
+      const uint64_t bi = (uint64_t)r * D + 4 * c;
+      dy.x = f.drop.apply(dy.x, bi + 0);
+      dy.y = f.drop.apply(dy.y, bi + 1);
+      dy.z = f.drop.apply(dy.z, bi + 2);
+      dy.w = f.drop.apply(dy.w, bi + 3);
+    }
+    float4 dx = dy;
+    if (do_ln) {
+      const float4 x = build_row<D>(f, r, c, g);
+      const float mu = f.mean[r], rs = f.rstd[r];
+      const float4 xh = make_float4((x.x - mu) * rs, (x.y - mu) * rs, (x.z - mu) * rs, (x.w - mu) * rs);
+      acc_w.x += dy.x * xh.x; acc_w.y += dy.y * xh.y; acc_w.z += dy.z * xh.z; acc_w.w += dy.w * xh.w;
+      acc_b.x += dy.x; acc_b.y += dy.y; acc_b.z += dy.z; acc_b.w += dy.w;
+      const float4 dh = make_float4(dy.x * w.x, dy.y * w.y, dy.z * w.z, dy.w * w.w);
+      float c1 = (dh.x + dh.y) + (dh.z + dh.w);
+      float c2 = dh.x * xh.x + dh.y * xh.y + dh.z * xh.z + dh.w * xh.w;
+      c1 = rsx::wave_sum_width(c1, LPR) / (float)D;
+      c2 = rsx::wave_sum_width(c2, LPR) / (float)D;
+      dx.x = (dh.x - c1 - xh.x * c2) * rs;
+      dx.y = (dh.y - c1 - xh.y * c2) * rs;
+      dx.z = (dh.z - c1 - xh.z * c2) * rs;
+      dx.w = (dh.w - c1 - xh.w * c2) * rs;
+    }
+    if (a.dbase) reinterpret_cast<float4*>(a.dbase + r * D)[c] = dx;
+    if (a.dpos) {
+      const int l = f.tok_pos ? (int)f.tok_pos[r] : (int)(r % f.L);
+      float* dst = s_pos + l * D + 4 * c;
+      atomicAdd(dst + 0, dx.x); atomicAdd(dst + 1, dx.y); atomicAdd(dst + 2, dx.z); atomicAdd(dst + 3, dx.w);
+    }
 #pragma unroll
-      for (int j = 0; j < kMaxTab; ++j) {
-        if (j < f.ntab && g[j] != 0.0f) {
-          const int64_t id = f.ids[j][r];
-          if (a.dgate) {
-            const float4 e = reinterpret_cast<const float4*>(f.tab[j] + id * D)[c];
-            acc_g[j] += dx.x * e.x + dx.y * e.y + dx.z * e.z + dx.w * e.w;
-          }
-          if (a.dtab[j] && id != a.pad_idx[j]) {
-            const float4 v = make_float4(dx.x * g[j], dx.y * g[j], dx.z * g[j], dx.w * g[j]);
-            if (a.small_off[j] >= 0) {
-              float* dst = s_small + a.small_off[j] + id * D + 4 * c;
-              atomicAdd(dst + 0, v.x); atomicAdd(dst + 1, v.y);
-              atomicAdd(dst + 2, v.z); atomicAdd(dst + 3, v.w);
-            } else {
-              float* dst = a.dtab[j] + id * D + 4 * c;
-              atomicAdd(dst + 0, v.x); atomicAdd(dst + 1, v.y);
-              atomicAdd(dst + 2, v.z); atomicAdd(dst + 3, v.w);
-            }
-          }
+    for (int j = 0; j < kMaxTab; ++j) {
+      if (j < f.ntab && g[j] != 0.0f) {
+        const int64_t id = f.ids[j][r];
+        if (a.dgate) {
+          const float4 e = reinterpret_cast<const float4*>(f.tab[j] + id * D)[c];
+          acc_g[j] += dx.x * e.x + dx.y * e.y + dx.z * e.z + dx.w * e.w;
+        }
+        if (a.dtab[j] && id != a.pad_idx[j]) {
+          const float4 v = make_float4(dx.x * g[j], dx.y * g[j], dx.z * g[j], dx.w * g[j]);
+          float* dst = (a.small_off[j] >= 0) ? (s_small + a.small_off[j] + id * D + 4 * c)
+                                             : (a.dtab[j] + id * D + 4 * c);
+          atomicAdd(dst + 0, v.x); atomicAdd(dst + 1, v.y); atomicAdd(dst + 2, v.z); atomicAdd(dst + 3, v.w);
         }
       }
     }
@@ -239,8 +236,6 @@ __global__ __launch_bounds__(256) void seq_embed_bwd_k(BwdArgs a) {
   // ---- block reductions: fold the RPW row slots of each wave, then the waves ----
 #pragma unroll
   for (int o = LPR; o < 64; o <<= 1) {
-    acc_pos.x += __shfl_xor(acc_pos.x, o, 64); acc_pos.y += __shfl_xor(acc_pos.y, o, 64);
-    acc_pos.z += __shfl_xor(acc_pos.z, o, 64); acc_pos.w += __shfl_xor(acc_pos.w, o, 64);
     acc_w.x += __shfl_xor(acc_w.x, o, 64); acc_w.y += __shfl_xor(acc_w.y, o, 64);
     acc_w.z += __shfl_xor(acc_w.z, o, 64); acc_w.w += __shfl_xor(acc_w.w, o, 64);
     acc_b.x += __shfl_xor(acc_b.x, o, 64); acc_b.y += __shfl_xor(acc_b.y, o, 64);
@@ -253,26 +248,22 @@ __global__ __launch_bounds__(256) void seq_embed_bwd_k(BwdArgs a) {
     acc_g[j] = v;
   }
   if (sub == 0) {
-    reinterpret_cast<float4*>(&s_red[wave][0][0])[c] = acc_pos;
-    reinterpret_cast<float4*>(&s_red[wave][1][0])[c] = acc_w;
-    reinterpret_cast<float4*>(&s_red[wave][2][0])[c] = acc_b;
+    reinterpret_cast<float4*>(&s_red[wave][0][0])[c] = acc_w;
+    reinterpret_cast<float4*>(&s_red[wave][1][0])[c] = acc_b;
   }
   if (lane == 0) {
 #pragma unroll
     for (int j = 0; j < kMaxTab; ++j) s_gate[wave][j] = acc_g[j];
   }
   __syncthreads();
-  for (int i = tid; i < 3 * D; i += blockDim.x) {
-    const int which = i / D, col = i % D;
-    float v = 0.0f;
+  if (do_ln) {
+    for (int i = tid; i < 2 * D; i += blockDim.x) {
+      const int which = i / D, col = i % D;
+      float v = 0.0f;
 #pragma unroll
-    for (int wv = 0; wv < NW; ++wv) v += s_red[wv][which][col];
-    if (which == 0) {
-      if (a.dpos) atomicAdd(a.dpos + (int64_t)l * D + col, v);
-    } else if (which == 1) {
-      if (a.dln_w && do_ln) atomicAdd(a.dln_w + col, v);
-    } else {
-      if (a.dln_b && do_ln) atomicAdd(a.dln_b + col, v);
+      for (int wv = 0; wv < NW; ++wv) v += s_red[wv][which][col];
+      float* dst = which == 0 ? a.dln_w : a.dln_b;
+      if (dst) atomicAdd(dst + col, v);
     }
   }
   if (tid < f.ntab && a.dgate) {
@@ -281,7 +272,12 @@ __global__ __launch_bounds__(256) void seq_embed_bwd_k(BwdArgs a) {
     for (int wv = 0; wv < NW; ++wv) v += s_gate[wv][tid];
     atomicAdd(a.dgate + tid, v);
   }
-  // flush block-local small-table accumulators
+  if (a.dpos) {
+    for (int i = tid; i < f.L * D; i += blockDim.x) {
+      const float v = s_pos[i];
+      if (v != 0.0f) atomicAdd(a.dpos + i, v);
+    }
+  }
   for (int j = 0; j < f.ntab; ++j) {
     if (a.small_off[j] < 0 || !a.dtab[j]) continue;
     const int n = a.small_rows[j] * D;
@@ -304,15 +300,15 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
 
 template <int D>
 int launch_bwd(const BwdArgs& a, hipStream_t st) {
-  const int64_t blocks = (int64_t)a.f.L * a.chunks;
-  const size_t lds = (size_t)a.small_total * sizeof(float);
+  const int64_t blocks = (a.f.T + a.rows_per_block - 1) / a.rows_per_block;
+  const size_t lds = (size_t)(a.f.L * D + a.small_total) * sizeof(float);
   hipLaunchKernelGGL(seq_embed_bwd_k<D>, dim3((unsigned)blocks), dim3(256), lds, st, a);
   return 0;
 }
 
 bool fill_fwd(FwdArgs& a, const float* base, const int64_t* const* ids, const float* const* tabs, int ntab,
-              const float* gate, const float* pos, const float* ln_w, const float* ln_b, float eps, int64_t B,
-              int64_t L, float* out, float* mean, float* rstd, float p_drop, uint64_t seed) {
+              const float* gate, const float* pos, const int64_t* tok_pos, const float* ln_w, const float* ln_b,
+              float eps, int64_t T, int64_t L, float* out, float* mean, float* rstd, float p_drop, uint64_t seed) {
   if (ntab < 0 || ntab > kMaxTab) return false;
   a.base = base;
   for (int j = 0; j < kMaxTab; ++j) {
@@ -321,12 +317,13 @@ bool fill_fwd(FwdArgs& a, const float* base, const int64_t* const* ids, const fl
   }
   a.gate = gate;
   a.pos = pos;
+  a.tok_pos = tok_pos;
   a.ln_w = ln_w;
   a.ln_b = ln_b;
   a.out = out;
   a.mean = mean;
   a.rstd = rstd;
-  a.T = B * L;
+  a.T = T;
   a.L = (int)L;
   a.ntab = ntab;
   a.eps = eps;
@@ -337,19 +334,19 @@ bool fill_fwd(FwdArgs& a, const float* base, const int64_t* const* ids, const fl
 }  // namespace
 
 RSX_API int rsx_seq_embed_fwd(const float* base, const int64_t* const* ids, const float* const* tables, int ntab,
-                              const float* gate, const float* pos, const float* ln_w, const float* ln_b, float eps,
-                              int64_t B, int64_t L, int64_t D, float p_drop, uint64_t seed, float* out, float* mean,
-                              float* rstd, void* stream) {
+                              const float* gate, const float* pos, const int64_t* tok_pos, const float* ln_w,
+                              const float* ln_b, float eps, int64_t T, int64_t L, int64_t D, float p_drop,
+                              uint64_t seed, float* out, float* mean, float* rstd, void* stream) {
   RSX_ARG(out != nullptr, "out is null");
-  RSX_ARG(B >= 0 && L > 0, "bad B/L");
+  RSX_ARG(T >= 0 && L > 0 && L <= 64, "need T >= 0 and 0 < L <= 64");
   RSX_ARG(D == 64 || D == 128 || D == 256, "D must be 64, 128 or 256");
   RSX_ARG(ntab >= 0 && ntab <= kMaxTab, "ntab must be in [0,6]");
   RSX_ARG(ln_w == nullptr || (ln_b != nullptr), "ln_b required with ln_w");
   RSX_ARG(p_drop >= 0.0f && p_drop < 1.0f, "p_drop must be in [0,1)");
   for (int j = 0; j < ntab; ++j) RSX_ARG(ids[j] != nullptr && tables[j] != nullptr, "null table/ids");
-  if (B == 0) return 0;
+  if (T == 0) return 0;
   FwdArgs a;
-  fill_fwd(a, base, ids, tables, ntab, gate, pos, ln_w, ln_b, eps, B, L, out, mean, rstd, p_drop, seed);
+  fill_fwd(a, base, ids, tables, ntab, gate, pos, tok_pos, ln_w, ln_b, eps, T, L, out, mean, rstd, p_drop, seed);
   hipStream_t st = (hipStream_t)stream;
   if (D == 64) launch_fwd<64>(a, st);
   else if (D == 128) launch_fwd<128>(a, st);
@@ -360,19 +357,20 @@ RSX_API int rsx_seq_embed_fwd(const float* base, const int64_t* const* ids, cons
 
 RSX_API int rsx_seq_embed_bwd(const float* base, const int64_t* const* ids, const float* const* tables,
                               const int64_t* table_rows, const int64_t* padding_idx, int ntab, const float* gate,
-                              const float* pos, const float* ln_w, const float* mean, const float* rstd, float eps,
-                              int64_t B, int64_t L, int64_t D, float p_drop, uint64_t seed, const float* dout,
-                              float* dbase, float* const* dtables, float* dgate, float* dpos, float* dln_w,
-                              float* dln_b, void* stream) {
+                              const float* pos, const int64_t* tok_pos, const float* ln_w, const float* mean,
+                              const float* rstd, float eps, int64_t T, int64_t L, int64_t D, float p_drop,
+                              uint64_t seed, const float* dout, float* dbase, float* const* dtables, float* dgate,
+                              float* dpos, float* dln_w, float* dln_b, void* stream) {
   RSX_ARG(dout != nullptr, "dout is null");
   RSX_ARG(D == 64 || D == 128 || D == 256, "D must be 64, 128 or 256");
   RSX_ARG(ntab >= 0 && ntab <= kMaxTab, "ntab must be in [0,6]");
   RSX_ARG(ln_w == nullptr || (mean != nullptr && rstd != nullptr), "mean/rstd required with ln_w");
   RSX_ARG(p_drop >= 0.0f && p_drop < 1.0f, "p_drop must be in [0,1)");
-  if (B == 0) return 0;
+  RSX_ARG(L > 0 && L <= 64, "need 0 < L <= 64");
+  if (T == 0) return 0;
   BwdArgs a;
-  fill_fwd(a.f, base, ids, tables, ntab, gate, pos, ln_w, nullptr, eps, B, L, nullptr, const_cast<float*>(mean),
-           const_cast<float*>(rstd), p_drop, seed);
+  fill_fwd(a.f, base, ids, tables, ntab, gate, pos, tok_pos, ln_w, nullptr, eps, T, L, nullptr,
+           const_cast<float*>(mean), const_cast<float*>(rstd), p_drop, seed);
   a.dout = dout;
   a.dbase = dbase;
   int off = 0;
@@ -392,11 +390,11 @@ RSX_API int rsx_seq_embed_bwd(const float* base, const int64_t* const* ids, cons
   a.dpos = dpos;
   a.dln_w = dln_w;
   a.dln_b = dln_b;
-  a.B = B;
-  int chunks = (int)((B + 63) / 64);
-  if (chunks > 64) chunks = 64;
-  if (chunks < 1) chunks = 1;
-  a.chunks = chunks;
+  // ~4 rows per lane-group per workgroup: enough blocks to fill 256 CUs several times
+  int64_t rpb = 4 * 4 * (64 / (D / 4)) * 8;
+  if (T / rpb < 1024) rpb = (T + 1023) / 1024;
+  if (rpb < 16) rpb = 16;
+  a.rows_per_block = rpb;
   hipStream_t st = (hipStream_t)stream;
   if (D == 64) launch_bwd<64>(a, st);
   else if (D == 128) launch_bwd<128>(a, st);

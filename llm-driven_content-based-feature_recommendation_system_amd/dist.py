@@ -122,38 +122,29 @@ class GradBucket:
             o += n
 
 
-_FWD_KEYS = ("item_ids", "time_bucket_ids", "type_ids", "color_ids", "graphic_ids", "section_ids", "age_bucket",
-             "price_bucket", "cnt_bucket", "recency_bucket", "channel_ids", "club_status_ids", "news_freq_ids",
-             "fn_ids", "active_ids", "cont_feats", "padding_mask")
-
-
-def contrastive_objective_dp(model, item_tower, log_q_tensor, batch, cfg, pretrained_vecs, temperature=0.1):
+def contrastive_objective_dp(model, item_tower, log_q_tensor, batch, cfg, pretrained_lookup=None,
+                             pretrained_vecs=None, temperature=0.1):
     """This rank's share of the global objective (reference :787-845 on the global batch).
 
     batch holds this rank's users (global user index = rank * B_local + b).
     Returns (local objective to backward, global total / main / cl for logging; the
     logging values are all-reduced and detached)."""
+    from .tower_code.v1_usertower_train import packed_views
+
     rank, ws = world()
     device = batch["item_ids"].device
-    kw = {k: batch[k] for k in _FWD_KEYS}
-    kw["pretrained_vecs"] = pretrained_vecs
-    kw["training_mode"] = True
-    out1 = model(**kw)
-    out2 = model(**kw)
     B, L = batch["item_ids"].shape
-    D = out1.shape[-1]
-    valid = ~batch["padding_mask"]
     target_ids = batch["target_ids"]
+    pk, out1, out2 = packed_views(model, batch, pretrained_vecs, pretrained_lookup)
 
     # ---- main LogQ loss over all valid steps of the global batch
-    flat_pos = valid.reshape(-1).nonzero().squeeze(1)
-    counts = all_gather_counts(flat_pos.numel(), device)
+    n_loc = pk.valid_tok.numel()
+    counts = all_gather_counts(n_loc, device)
     n_glob = sum(counts)
-    offset = sum(counts[:rank])
     if n_glob > 0:
-        u_loc = ops.gather_rows(out1.reshape(-1, D), flat_pos, normalize=True, unique=True)
-        t_loc = target_ids.reshape(-1)[flat_pos]
-        user_loc = torch.div(flat_pos, L, rounding_mode="floor") + rank * B
+        u_loc = ops.gather_rows(out1, pk.valid_tok, normalize=True, unique=True)
+        t_loc = target_ids.reshape(-1)[pk.flat[pk.valid_tok]]
+        user_loc = pk.tok_user[pk.valid_tok] + rank * B
         t_glob = all_gather_var(t_loc, counts)
         groups = ops.TargetGroups(t_loc, user_loc, t_cols=t_glob)
         items_d = ops.gather_rows(item_tower.get_all_embeddings(), groups.uniq, normalize=True, unique=True)
@@ -164,11 +155,9 @@ def contrastive_objective_dp(model, item_tower, log_q_tensor, batch, cfg, pretra
         main_local = torch.zeros((), device=device)
 
     # ---- DuoRec on the bug-compatible "last" index (count_valid - 1), global B x B
-    last = (valid.sum(dim=1) - 1).clamp(min=0)
-    rows = torch.arange(B, device=device) * L + last
-    z1 = ops.l2_normalize(ops.gather_rows(out1.reshape(-1, D), rows, unique=True))
-    z2 = ops.l2_normalize(ops.gather_rows(out2.reshape(-1, D), rows, unique=True))
-    last_t = target_ids.reshape(-1)[rows]
+    z1 = ops.l2_normalize(ops.gather_rows(out1, pk.last_tok, unique=True))
+    z2 = ops.l2_normalize(ops.gather_rows(out2, pk.last_tok, unique=True))
+    last_t = target_ids.reshape(-1)[pk.flat[pk.last_tok]]
     bcounts = [B] * ws
     b_glob = B * ws
     z1_glob = all_gather_rows(z1, bcounts)
@@ -196,11 +185,9 @@ def contrastive_step_dp(model, item_tower, log_q_tensor, batch, optimizer, cfg, 
                         max_norm=5.0):
     """Full data-parallel step: local forward/loss/backward, one gradient all-reduce,
     clip_grad_norm_(5.0) on the summed gradients, AdamW (replicated, identical on all ranks)."""
-    from .tower_code.v1_usertower_train import lookup_pretrained
-
     optimizer.zero_grad(set_to_none=True)
-    pv = lookup_pretrained(pretrained_lookup, batch["item_ids"])
-    objective, total, main, cl = contrastive_objective_dp(model, item_tower, log_q_tensor, batch, cfg, pv)
+    objective, total, main, cl = contrastive_objective_dp(model, item_tower, log_q_tensor, batch, cfg,
+                                                          pretrained_lookup=pretrained_lookup)
     objective.backward()
     bucket()
     torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=max_norm)

@@ -31,33 +31,34 @@ def _c(t):
 # A2: fused sequence embedding (v1_refine_usertower.py:447-459)
 class _SeqEmbed(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, base, gate, pos, ln_w, ln_b, ids, cfg, *tables):
-        eps, p_drop, seed, padding_idx = cfg
+    def forward(ctx, base, gate, pos, ln_w, ln_b, ids, cfg, tok_pos, *tables):
+        eps, p_drop, seed, padding_idx, L = cfg
         N.ensure_device(base)
-        B, L, D = base.shape
+        D = base.shape[-1]
+        T = base.numel() // D
         base = _c(base)
         ids = [_c(t) for t in ids]
         tables = [_c(t) for t in tables]
         out = torch.empty_like(base)
-        mean = torch.empty(B * L, device=base.device, dtype=torch.float32)
+        mean = torch.empty(T, device=base.device, dtype=torch.float32)
         rstd = torch.empty_like(mean)
         gate = _c(gate)
         rc = N.lib().rsx_seq_embed_fwd(
             N.ptr(base), N.ptr_array(ids), N.ptr_array(tables), len(tables), N.ptr(gate), N.ptr(pos),
-            N.ptr(ln_w), N.ptr(ln_b), eps, B, L, D, p_drop, seed, N.ptr(out), N.ptr(mean), N.ptr(rstd),
-            N.stream())
+            N.ptr(tok_pos), N.ptr(ln_w), N.ptr(ln_b), eps, T, L, D, p_drop, seed, N.ptr(out), N.ptr(mean),
+            N.ptr(rstd), N.stream())
         N.check(rc, "seq_embed_fwd")
-        ctx.save_for_backward(base, gate, pos, ln_w, mean, rstd, *ids, *tables)
-        ctx.cfg = (eps, p_drop, seed, padding_idx, len(tables), B, L, D)
+        ctx.save_for_backward(base, gate, pos, ln_w, mean, rstd, tok_pos, *ids, *tables)
+        ctx.cfg = (eps, p_drop, seed, padding_idx, len(tables), T, L, D)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        eps, p_drop, seed, padding_idx, nt, B, L, D = ctx.cfg
+        eps, p_drop, seed, padding_idx, nt, T, L, D = ctx.cfg
         saved = ctx.saved_tensors
-        base, gate, pos, ln_w, mean, rstd = saved[:6]
-        ids = list(saved[6:6 + nt])
-        tables = list(saved[6 + nt:6 + 2 * nt])
+        base, gate, pos, ln_w, mean, rstd, tok_pos = saved[:7]
+        ids = list(saved[7:7 + nt])
+        tables = list(saved[7 + nt:7 + 2 * nt])
         dout = _c(dout)
         need = ctx.needs_input_grad
         dbase = torch.empty_like(base) if need[0] else None
@@ -65,71 +66,83 @@ class _SeqEmbed(torch.autograd.Function):
         dpos = torch.zeros_like(pos) if need[2] else None
         dlnw = torch.zeros_like(ln_w) if need[3] else None
         dlnb = torch.zeros_like(ln_w) if need[4] else None
-        dtabs = [torch.zeros_like(t) if need[7 + j] else None for j, t in enumerate(tables)]
+        dtabs = [torch.zeros_like(t) if need[8 + j] else None for j, t in enumerate(tables)]
         rc = N.lib().rsx_seq_embed_bwd(
             N.ptr(base), N.ptr_array(ids), N.ptr_array(tables), N.i64_array([t.shape[0] for t in tables]),
-            N.i64_array(padding_idx), nt, N.ptr(gate), N.ptr(pos), N.ptr(ln_w), N.ptr(mean), N.ptr(rstd), eps,
-            B, L, D, p_drop, seed, N.ptr(dout), N.ptr(dbase), N.ptr_array(dtabs), N.ptr(dgate), N.ptr(dpos),
-            N.ptr(dlnw), N.ptr(dlnb), N.stream())
+            N.i64_array(padding_idx), nt, N.ptr(gate), N.ptr(pos), N.ptr(tok_pos), N.ptr(ln_w), N.ptr(mean),
+            N.ptr(rstd), eps, T, L, D, p_drop, seed, N.ptr(dout), N.ptr(dbase), N.ptr_array(dtabs), N.ptr(dgate),
+            N.ptr(dpos), N.ptr(dlnw), N.ptr(dlnb), N.stream())
         N.check(rc, "seq_embed_bwd")
-        return (dbase, dgate, dpos, dlnw, dlnb, None, None, *dtabs)
+        return (dbase, dgate, dpos, dlnw, dlnb, None, None, None, *dtabs)
 
 
-def seq_embed(base, ids, tables, gate, pos, ln_w, ln_b, eps=1e-5, p_drop=0.0, padding_idx=None):
-    """x = base + sum_j tables[j][ids[j]] * gate[j] + pos ; LayerNorm ; dropout.
+def seq_embed(base, ids, tables, gate, pos, ln_w, ln_b, eps=1e-5, p_drop=0.0, padding_idx=None, tok_pos=None):
+    """x = base + sum_j tables[j][ids[j]] * gate[j] + pos[l] ; LayerNorm ; dropout.
 
-    base [B, L, D]; ids/tables: lists (<= 6); gate [ntab]; pos [L, D]; ln_w/ln_b [D].
-    padding_idx: per-table row excluded from the table gradient (nn.Embedding semantics).
+    Dense: base [B, L, D], ids [B, L], pos [>= L, D] (position = token % L).
+    Packed: base [T, D], ids [T], tok_pos [T] int64 positions, pos [L, D].
+    gate [ntab]; ln_w/ln_b [D]. padding_idx: per-table row excluded from the table gradient
+    (nn.Embedding semantics).
     """
     if padding_idx is None:
         padding_idx = [-1] * len(tables)
     padding_idx = [(-1 if p is None else int(p)) for p in padding_idx]
     seed = next_seed() if p_drop > 0 else 0
-    cfg = (float(eps), float(p_drop), seed, padding_idx)
-    return _SeqEmbed.apply(base, gate, pos, ln_w, ln_b, list(ids), cfg, *tables)
+    if tok_pos is None:
+        L = base.shape[1]
+        pos = pos[:L]
+    else:
+        L = pos.shape[0]
+        tok_pos = _c(tok_pos)
+    cfg = (float(eps), float(p_drop), seed, padding_idx, int(L))
+    return _SeqEmbed.apply(base, gate, pos, ln_w, ln_b, list(ids), cfg, tok_pos, *tables)
 
 
 # ----------------------------------------------------------------------------------------
 # A3 / A9: masked MHA core
 class _MHA(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, key_pad, H, causal, p_drop, seed):
+    def forward(ctx, qkv, key_pad, seg_off, H, causal, p_drop, seed):
         N.ensure_device(qkv)
         qkv = _c(qkv)
-        B, L, D3 = qkv.shape
+        D3 = qkv.shape[-1]
+        T = qkv.numel() // D3
         D = D3 // 3
         Dh = D // H
-        out = torch.empty(B, L, D, device=qkv.device, dtype=torch.float32)
-        lse = torch.empty(B, H, L, device=qkv.device, dtype=torch.float32)
+        if seg_off is None:
+            B, L = qkv.shape[0], qkv.shape[1]
+        else:
+            B, L = seg_off.numel() - 1, 64
+        out = torch.empty(qkv.shape[:-1] + (D,), device=qkv.device, dtype=torch.float32)
+        lse = torch.empty(T, H, device=qkv.device, dtype=torch.float32)
         kp = None
         if key_pad is not None:
             kp = _c(key_pad.to(torch.uint8)) if key_pad.dtype != torch.uint8 else _c(key_pad)
-        rc = N.lib().rsx_mha_fwd(N.ptr(qkv), N.ptr(kp), B, L, H, Dh, int(causal), p_drop, seed, N.ptr(out),
-                                 N.ptr(lse), N.stream())
+        rc = N.lib().rsx_mha_fwd(N.ptr(qkv), N.ptr(kp), N.ptr(seg_off), B, L, H, Dh, int(causal), p_drop, seed,
+                                 N.ptr(out), N.ptr(lse), N.stream())
         N.check(rc, "mha_fwd")
-        ctx.save_for_backward(qkv, kp, out, lse) if kp is not None else ctx.save_for_backward(qkv, out, lse)
-        ctx.has_kp = kp is not None
+        ctx.save_for_backward(qkv, kp, seg_off, out, lse)
         ctx.cfg = (B, L, H, Dh, int(causal), p_drop, seed)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         B, L, H, Dh, causal, p_drop, seed = ctx.cfg
-        if ctx.has_kp:
-            qkv, kp, out, lse = ctx.saved_tensors
-        else:
-            (qkv, out, lse), kp = ctx.saved_tensors, None
+        qkv, kp, seg_off, out, lse = ctx.saved_tensors
         dout = _c(dout)
         dqkv = torch.empty_like(qkv)
-        rc = N.lib().rsx_mha_bwd(N.ptr(qkv), N.ptr(kp), N.ptr(out), N.ptr(lse), N.ptr(dout), B, L, H, Dh, causal,
-                                 p_drop, seed, N.ptr(dqkv), N.stream())
+        rc = N.lib().rsx_mha_bwd(N.ptr(qkv), N.ptr(kp), N.ptr(seg_off), N.ptr(out), N.ptr(lse), N.ptr(dout), B, L, H,
+                                 Dh, causal, p_drop, seed, N.ptr(dqkv), N.stream())
         N.check(rc, "mha_bwd")
-        return dqkv, None, None, None, None, None
+        return dqkv, None, None, None, None, None, None
 
 
-def mha(qkv, key_pad, num_heads, causal, p_drop=0.0):
+def mha(qkv, key_pad, num_heads, causal, p_drop=0.0, seg_off=None):
+    """Dense: qkv [B, L, 3D], key_pad [B, L]. Packed: qkv [T, 3D], key_pad [T], seg_off [B+1] int32."""
     seed = next_seed() if p_drop > 0 else 0
-    return _MHA.apply(qkv, key_pad, int(num_heads), bool(causal), float(p_drop), seed)
+    if seg_off is not None:
+        seg_off = _c(seg_off.to(torch.int32))
+    return _MHA.apply(qkv, key_pad, seg_off, int(num_heads), bool(causal), float(p_drop), seed)
 
 
 # ----------------------------------------------------------------------------------------

@@ -89,11 +89,11 @@ class SASRecUserTower(nn.Module):
         return torch.triu(torch.ones(seq_len, seq_len, device=device, dtype=torch.bool), diagonal=1)
 
     # -- encoder layer (norm_first=True, gelu): reference nn.TransformerEncoderLayer semantics
-    def _encoder_layer(self, layer: nn.TransformerEncoderLayer, x, key_pad, p):
+    def _encoder_layer(self, layer: nn.TransformerEncoderLayer, x, key_pad, p, seg_off=None):
         sa = layer.self_attn
         h = F.layer_norm(x, (self.d_model,), layer.norm1.weight, layer.norm1.bias, layer.norm1.eps)
         qkv = F.linear(h, sa.in_proj_weight, sa.in_proj_bias)
-        a = ops.mha(qkv, key_pad, sa.num_heads, causal=True, p_drop=p)
+        a = ops.mha(qkv, key_pad, sa.num_heads, causal=True, p_drop=p, seg_off=seg_off)
         a = F.linear(a, sa.out_proj.weight, sa.out_proj.bias)
         x = x + F.dropout(a, p, self.training)
         h = F.layer_norm(x, (self.d_model,), layer.norm2.weight, layer.norm2.bias, layer.norm2.eps)
@@ -123,14 +123,8 @@ class SASRecUserTower(nn.Module):
             x = self._encoder_layer(layer, x, padding_mask, p)
         output = x
 
-        # Phase 2: static encoding (reference :472-494)
-        static_input = torch.cat([
-            self.age_emb(age_bucket) * u_g[0], self.price_emb(price_bucket) * u_g[1],
-            self.cnt_emb(cnt_bucket) * u_g[2], self.recency_emb(recency_bucket) * u_g[3],
-            self.channel_emb(channel_ids) * u_g[4], self.club_status_emb(club_status_ids) * u_g[5],
-            self.news_freq_emb(news_freq_ids) * u_g[6], self.fn_emb(fn_ids) * u_g[7],
-            self.active_emb(active_ids) * u_g[8], F.relu(self.cont_proj(cont_feats)) * u_g[9]], dim=1)
-        user_profile_vec = self.static_mlp(static_input)
+        user_profile_vec = self._static_profile(age_bucket, price_bucket, cnt_bucket, recency_bucket, channel_ids,
+                                                club_status_ids, news_freq_ids, fn_ids, active_ids, cont_feats, u_g)
 
         # Phase 3: late fusion (reference :499-510). Linear(cat[a, b]) = a W_a^T + (b W_b^T + bias):
         # the per-user profile half is computed once per user and broadcast over L.
@@ -145,6 +139,80 @@ class SASRecUserTower(nn.Module):
         h = F.gelu(F.layer_norm(h, (D,), ln.weight, ln.bias, ln.eps))
         final_vec = F.linear(h, lin3.weight, lin3.bias)
         return ops.l2_normalize(final_vec)
+
+    def _static_profile(self, age_bucket, price_bucket, cnt_bucket, recency_bucket, channel_ids, club_status_ids,
+                        news_freq_ids, fn_ids, active_ids, cont_feats, u_g):
+        # Phase 2: static encoding (reference :472-494)
+        static_input = torch.cat([
+            self.age_emb(age_bucket) * u_g[0], self.price_emb(price_bucket) * u_g[1],
+            self.cnt_emb(cnt_bucket) * u_g[2], self.recency_emb(recency_bucket) * u_g[3],
+            self.channel_emb(channel_ids) * u_g[4], self.club_status_emb(club_status_ids) * u_g[5],
+            self.news_freq_emb(news_freq_ids) * u_g[6], self.fn_emb(fn_ids) * u_g[7],
+            self.active_emb(active_ids) * u_g[8], F.relu(self.cont_proj(cont_feats)) * u_g[9]], dim=1)
+        return self.static_mlp(static_input)
+
+    def forward_packed(self, packed, pretrained_tok, tok_ids, age_bucket, price_bucket, cnt_bucket, recency_bucket,
+                       channel_ids, club_status_ids, news_freq_ids, fn_ids, active_ids, cont_feats):
+        """Training-mode forward restricted to the tokens whose outputs the contrastive step
+        reads (every valid step + the bug-compatible DuoRec "last" position of each user).
+
+        Returns the L2-normalised outputs of those tokens [T, D] in packed (b, t) order; each
+        equals the corresponding row of forward(..., training_mode=True): with left padding a
+        valid query never attends to padded keys, a padded query attends to nothing, and
+        every other op is per token, so dropping the other padded tokens changes no value
+        the losses see. tok_ids: [item, time, type, color, graphic, section] ids per token."""
+        p = self.dropout_rate if self.training else 0.0
+        s_g = torch.sigmoid(self.seq_gate) * self._seq_gate_mask
+        u_g = torch.sigmoid(self.static_gate)
+        base = F.linear(pretrained_tok, self.item_proj.weight, self.item_proj.bias)
+        x = ops.seq_embed(
+            base, tok_ids,
+            [self.item_id_emb.weight, self.time_emb.weight, self.type_emb.weight, self.color_emb.weight,
+             self.graphic_emb.weight, self.section_emb.weight],
+            s_g, self.pos_emb.weight, self.emb_ln.weight, self.emb_ln.bias, eps=self.emb_ln.eps, p_drop=p,
+            padding_idx=[0, 0, 0, 0, 0, 0], tok_pos=packed.tok_pos)
+        for layer in self.transformer_encoder.layers:
+            x = self._encoder_layer(layer, x, packed.tok_pad, p, seg_off=packed.seg_off)
+        profile = self._static_profile(age_bucket, price_bucket, cnt_bucket, recency_bucket, channel_ids,
+                                       club_status_ids, news_freq_ids, fn_ids, active_ids, cont_feats, u_g)
+        lin0, ln, lin3 = self.output_proj[0], self.output_proj[1], self.output_proj[3]
+        D = self.d_model
+        prof = F.linear(profile, lin0.weight[:, D:], lin0.bias)
+        h = F.linear(x, lin0.weight[:, :D]) + ops.gather_rows(prof, packed.tok_user)
+        h = F.gelu(F.layer_norm(h, (D,), ln.weight, ln.bias, ln.eps))
+        return ops.l2_normalize(F.linear(h, lin3.weight, lin3.bias))
+
+
+class PackedTokens:
+    """Token selection of the contrastive step for a left-padded [B, L] batch: all valid
+    positions plus, per user, the DuoRec "last" index count-1 when it falls on padding
+    (v1_usertower_train.py:830-835), in row-major (b, t) order, segmented by user."""
+
+    def __init__(self, padding_mask: torch.Tensor):
+        B, L = padding_mask.shape
+        dev = padding_mask.device
+        valid = ~padding_mask
+        cnt = valid.sum(1)
+        last = (cnt - 1).clamp(min=0)
+        ar = torch.arange(B, device=dev)
+        need_extra = padding_mask[ar, last]
+        sel = valid.clone()
+        sel[ar, last] = sel[ar, last] | need_extra
+        self.flat = sel.reshape(-1).nonzero().squeeze(1)             # [T] flat (b*L + t)
+        self.tok_user = torch.div(self.flat, L, rounding_mode="floor")
+        self.tok_pos = self.flat % L
+        self.tok_pad = padding_mask.reshape(-1)[self.flat].to(torch.uint8)
+        seg = torch.zeros(B + 1, device=dev, dtype=torch.int64)
+        seg[1:] = torch.cumsum(torch.bincount(self.tok_user, minlength=B), 0)
+        self.seg_off = seg.to(torch.int32)
+        self.valid_tok = (self.tok_pad == 0).nonzero().squeeze(1)   # loss rows (valid steps, flat order)
+        pad_len = L - cnt
+        self.last_tok = seg[:-1] + torch.where(need_extra, torch.zeros_like(last), last - pad_len)
+        self.B, self.L = B, L
+
+    def take(self, t: torch.Tensor) -> torch.Tensor:
+        """[B, L] (or [B, L, ...]) per-position tensor -> per packed token."""
+        return t.reshape((-1,) + tuple(t.shape[2:]))[self.flat]
 
 
 # ==========================================

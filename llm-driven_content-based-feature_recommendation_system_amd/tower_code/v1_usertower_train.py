@@ -14,7 +14,7 @@ import torch
 import torch.nn as nn
 
 from .. import ops
-from .v1_refine_usertower import SASRecUserTower, duorec_loss_refined, inbatch_corrected_logq_loss
+from .v1_refine_usertower import PackedTokens, SASRecUserTower, duorec_loss_refined, inbatch_corrected_logq_loss
 
 try:  # the reference hard-imports wandb (v1_usertower_train.py:14); here it is optional
     import wandb  # type: ignore
@@ -101,26 +101,38 @@ def lookup_pretrained(pretrained_lookup: torch.Tensor, item_ids: torch.Tensor) -
     return ops.gather_rows(pretrained_lookup, item_ids.reshape(-1)).view(B, L, -1)
 
 
-def contrastive_losses(model, item_tower, log_q_tensor, batch, cfg, pretrained_vecs):
-    """Forward of one step (reference :787-845). Returns (total, main, cl)."""
-    device = batch["item_ids"].device
-    kw = {k: batch[k] for k in _FWD_KEYS}
-    kw["pretrained_vecs"] = pretrained_vecs
-    kw["training_mode"] = True
-    output_1 = model(**kw)
-    output_2 = model(**kw)
+_STATIC_KEYS = ("age_bucket", "price_bucket", "cnt_bucket", "recency_bucket", "channel_ids", "club_status_ids",
+                "news_freq_ids", "fn_ids", "active_ids", "cont_feats")
+_SEQ_ID_KEYS = ("item_ids", "time_bucket_ids", "type_ids", "color_ids", "graphic_ids", "section_ids")
 
-    padding_mask = batch["padding_mask"]
+
+def packed_views(model, batch, pretrained_vecs=None, pretrained_lookup=None):
+    """Both dropout views (reference :788-789) on the packed token set of the step.
+    Returns (packed tokens, out_1 [T, D], out_2 [T, D])."""
+    pk = PackedTokens(batch["padding_mask"])
+    tok_ids = [pk.take(batch[k]) for k in _SEQ_ID_KEYS]
+    if pretrained_vecs is not None:
+        pv_tok = pk.take(pretrained_vecs)
+    else:
+        pv_tok = ops.gather_rows(pretrained_lookup, tok_ids[0])
+    static = [batch[k] for k in _STATIC_KEYS]
+    out1 = model.forward_packed(pk, pv_tok, tok_ids, *static)
+    out2 = model.forward_packed(pk, pv_tok, tok_ids, *static)
+    return pk, out1, out2
+
+
+def contrastive_losses(model, item_tower, log_q_tensor, batch, cfg, pretrained_vecs=None, pretrained_lookup=None):
+    """Forward of one step (reference :787-845) on the packed token set. Returns (total, main, cl)."""
+    device = batch["item_ids"].device
     target_ids = batch["target_ids"]
-    batch_size, seq_len = batch["item_ids"].shape
-    D = output_1.shape[-1]
-    valid_mask = ~padding_mask
-    flat_pos = valid_mask.reshape(-1).nonzero().squeeze(1)  # row-major (b, t) order, as output_1[valid_mask]
-    if flat_pos.numel() > 0:
-        # flat_output = output_1[valid_mask]; F.normalize(flat_output) -- one fused gather+normalise
-        flat_user_emb = ops.gather_rows(output_1.reshape(-1, D), flat_pos, normalize=True, unique=True)
+    pk, out1, out2 = packed_views(model, batch, pretrained_vecs, pretrained_lookup)
+    n_valid = pk.valid_tok.numel()
+    if n_valid > 0:
+        # flat_output = output_1[valid_mask] (row-major b, t); F.normalize(flat_output)
+        flat_user_emb = ops.gather_rows(out1, pk.valid_tok, normalize=True, unique=True)
+        flat_pos = pk.flat[pk.valid_tok]
         flat_targets = target_ids.reshape(-1)[flat_pos]
-        flat_user_ids = torch.div(flat_pos, seq_len, rounding_mode="floor")
+        flat_user_ids = pk.tok_user[pk.valid_tok]
         # Grouped evaluation of inbatch_corrected_logq_loss (v1_refine_usertower.py:826-861):
         # the columns normalize(item_matrix)[flat_targets] collapse onto the distinct targets
         # with exact multiplicities (see csrc/infonce.hip); same result, N/D fewer FLOPs.
@@ -133,11 +145,9 @@ def contrastive_losses(model, item_tower, log_q_tensor, batch, cfg, pretrained_v
         main_loss = torch.zeros((), device=device)
 
     # DuoRec on the "last" step: count_valid - 1 (bug-compatible on left-padded rows, :830-835)
-    last_indices = (valid_mask.sum(dim=1) - 1).clamp(min=0)
-    rows = torch.arange(batch_size, device=device) * seq_len + last_indices
-    last_output_1 = ops.gather_rows(output_1.reshape(-1, D), rows, unique=True)
-    last_output_2 = ops.gather_rows(output_2.reshape(-1, D), rows, unique=True)
-    last_targets = target_ids.reshape(-1)[rows]
+    last_output_1 = ops.gather_rows(out1, pk.last_tok, unique=True)
+    last_output_2 = ops.gather_rows(out2, pk.last_tok, unique=True)
+    last_targets = target_ids.reshape(-1)[pk.flat[pk.last_tok]]
     cl_loss = duorec_loss_refined(last_output_1, last_output_2, last_targets, lambda_sup=cfg.lambda_sup)
     total_loss = main_loss + cfg.lambda_cl * cl_loss
     return total_loss, main_loss, cl_loss
@@ -149,10 +159,9 @@ def contrastive_step(model, item_tower, log_q_tensor, batch, optimizer, scaler, 
     except the valid-position count. Returns detached (total, main, cl) loss tensors.
     grad_sync: optional callable run between backward and clipping (data-parallel all-reduce)."""
     optimizer.zero_grad(set_to_none=True)
-    pv = batch.get("pretrained_vecs")
-    if pv is None:
-        pv = lookup_pretrained(pretrained_lookup, batch["item_ids"])
-    total, main, cl = contrastive_losses(model, item_tower, log_q_tensor, batch, cfg, pv)
+    total, main, cl = contrastive_losses(model, item_tower, log_q_tensor, batch, cfg,
+                                         pretrained_vecs=batch.get("pretrained_vecs"),
+                                         pretrained_lookup=pretrained_lookup)
     if scaler is not None and scaler.is_enabled():
         scaler.scale(total).backward()
         if grad_sync is not None:

@@ -143,7 +143,7 @@ def test_mha_dropout_directional_derivative(gpu):
     pad = (torch.arange(L)[None, :] < torch.randint(0, L, (B,), generator=g)[:, None]).to(gpu)
     v = torch.randn_like(qkv)
     w = torch.randn(B, L, H * dh, device=gpu)
-    f = lambda x: (ops._MHA.apply(x, pad, H, True, 0.2, 1234) * w).sum()
+    f = lambda x: (ops._MHA.apply(x, pad, None, H, True, 0.2, 1234) * w).sum()
     x = qkv.clone().requires_grad_()
     f(x).backward()
     eps = 1e-2

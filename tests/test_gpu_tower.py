@@ -103,10 +103,25 @@ def test_dp_objective_single_rank_equals_single_gpu_step(gpu):
     g1 = [p.grad.clone() for p in dut.parameters()]
     gw1 = it.item_matrix.weight.grad.clone()
     dut.zero_grad(); it.zero_grad()
-    obj, tot2, main2, cl2 = Dd.contrastive_objective_dp(dut, it, it.log_q, bd, cfg, pv)
+    obj, tot2, main2, cl2 = Dd.contrastive_objective_dp(dut, it, it.log_q, bd, cfg, pretrained_vecs=pv)
     for a, b in [(obj, tot), (tot2, tot), (main2, main), (cl2, cl)]:
         assert abs(a.item() - b.item()) < 1e-5
     obj.backward()
     for a, p in zip(g1, dut.parameters()):
         torch.testing.assert_close(p.grad, a, atol=1e-6, rtol=1e-4)
     torch.testing.assert_close(it.item_matrix.weight.grad, gw1, atol=1e-6, rtol=1e-4)
+
+
+def test_packed_forward_equals_dense_rows(gpu):
+    """forward_packed outputs == forward(training_mode=True) at the packed positions, including
+    the padded DuoRec "last" positions (dropout 0)."""
+    cfg = small_cfg(num_items=500)
+    items = small_universe(500)
+    bd = to_dev(synth.make_batch(items, 40, seed=31), gpu)
+    _, dut = paired_towers(cfg, gpu)
+    dut.train()
+    pv = items.pretrained.to(gpu)[bd["item_ids"]]
+    dense = dut(**{k: bd[k] for k in O._FWD_KEYS}, pretrained_vecs=pv, training_mode=True)
+    pk, o1, _ = TT.packed_views(dut, bd, pretrained_vecs=pv)
+    assert (pk.tok_pad == 1).sum() > 0  # some users' last index falls on padding
+    torch.testing.assert_close(o1, dense.reshape(-1, dense.shape[-1])[pk.flat], atol=2e-6, rtol=1e-5)

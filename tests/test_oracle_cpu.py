@@ -107,3 +107,24 @@ def test_oracle_loss_equals_row_lse_form():
     s = s.masked_fill(excl, float("-inf"))
     alt = (torch.logsumexp(s, 1) - s.diagonal()).mean()
     torch.testing.assert_close(ref, alt)
+
+
+def test_packed_tokens_layout():
+    from recsys_amd.tower_code.v1_refine_usertower import PackedTokens
+    items, batch = _batch(B=64, seed=9)
+    pad = batch["padding_mask"]
+    B, L = pad.shape
+    pk = PackedTokens(pad)
+    valid = ~pad
+    # loss rows == output[valid_mask] order (row-major b, t)
+    assert torch.equal(pk.flat[pk.valid_tok], valid.reshape(-1).nonzero().squeeze(1))
+    last = (valid.sum(1) - 1).clamp(min=0)
+    assert torch.equal(pk.flat[pk.last_tok], torch.arange(B) * L + last)
+    seg = pk.seg_off.long()
+    for b in range(B):
+        toks = pk.flat[seg[b]:seg[b + 1]]
+        assert ((toks // L) == b).all() and (toks.diff() > 0).all()
+        assert (seg[b + 1] - seg[b]) <= L
+    # the extra (padded) token of a user is its first packed token and has no valid key before it
+    extra = pk.tok_pad.bool()
+    assert torch.equal(extra.nonzero().squeeze(1), seg[:-1][pad[torch.arange(B), last]])
