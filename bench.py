@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--blas", default="default", choices=["default", "hipblaslt", "rocblas", "ck"],
+                    help="library torch uses for the tower's dense projections")
     return ap.parse_args()
 
 
@@ -86,6 +88,12 @@ def cpu_baseline(args, items, cfg):
 def main():
     args = parse()
     rank, world, device = setup_dist(args)
+    if args.blas == "rocblas":
+        torch.backends.cuda.preferred_blas_library("hipblas")
+    elif args.blas == "hipblaslt":
+        torch.backends.cuda.preferred_blas_library("hipblaslt")
+    elif args.blas == "ck":
+        torch.backends.cuda.preferred_blas_library("ck")
     import recsys_amd  # noqa: F401
     from recsys_amd import dist as D
     from recsys_amd import ops, synth
@@ -184,7 +192,8 @@ def main():
                    "valid_positions_per_batch": [sum(c) for c in n_glob],
                    "distinct_targets_per_batch": n_dist, "dropout": args.dropout,
                    "item_matrix": "frozen" if args.freeze_items else "unfrozen (lr x0.05)",
-                   "parallelism": f"dp{world} (users split by rank, RCCL all-gather of ids/z, grad all-reduce)"},
+                   "parallelism": f"dp{world} (users split by rank, RCCL all-gather of ids/z, grad all-reduce)",
+                   "dense_projection_blas": args.blas},
         "roofline": {"kernel": "nce_grouped_bwd_k<row-owned> (main LogQ loss backward)", "bound": "mfma",
                      "achieved": round(achieved, 2) if achieved else None, "peak": FP32_MFMA_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4) if achieved else None,

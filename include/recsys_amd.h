@@ -52,13 +52,16 @@ int rsx_seq_embed_fwd(const float* base, const int64_t* const* ids, const float*
 /* Backward of rsx_seq_embed_fwd. dbase [T,D] written; dtables[j], dgate [ntab], dpos [L,D],
  * dln_w/dln_b [D] accumulated (nullable). padding_idx[j]: rows excluded from the table
  * gradient exactly like nn.Embedding(padding_idx=...) (-1 = none). table_rows[j] lets small
- * tables (time buckets) accumulate in LDS before one flush per workgroup. */
+ * tables (time buckets) accumulate in LDS; position and small-table gradients leave each
+ * workgroup as a partial slab in ws (rsx_seq_embed_bwd_workspace_floats floats) and are
+ * summed deterministically. */
+int64_t rsx_seq_embed_bwd_workspace_floats(int64_t T, int64_t L, int64_t D, int ntab, const int64_t* table_rows);
 int rsx_seq_embed_bwd(const float* base, const int64_t* const* ids, const float* const* tables,
                       const int64_t* table_rows, const int64_t* padding_idx, int ntab, const float* gate,
                       const float* pos, const int64_t* tok_pos, const float* ln_w, const float* mean,
                       const float* rstd, float eps, int64_t T, int64_t L, int64_t D, float p_drop, uint64_t seed,
                       const float* dout, float* dbase, float* const* dtables, float* dgate, float* dpos,
-                      float* dln_w, float* dln_b, void* stream);
+                      float* dln_w, float* dln_b, float* ws, void* stream);
 
 /* ---- A3 / A9: masked multi-head self-attention core (L <= 64) -----------------------
  * Replaces the attention inside nn.TransformerEncoderLayer (norm_first, batch_first) at
@@ -102,6 +105,25 @@ int rsx_nce_bwd(const float* A, const float* B, const float* bias, const int* k1
                 const int* k2b, int64_t N, int64_t M, int64_t lda, int64_t ldb, int64_t diag_offset, float tau,
                 int flags, int nsplit_fwd, int nsplit, const float* gout, float* ws, float* dA, float* dB,
                 int accumulate, void* stream);
+
+/* ---- A6 grouped: the live LogQ loss over the batch's DISTINCT targets ------------------
+ * Same objective as rsx_nce_fwd flags 6 on columns normalize(item_matrix)[t_j], evaluated
+ * over the D distinct targets (B[d] = normalised item uniq[d], bias[d] = logQ*lambda) with
+ * exact integer multiplicities w_{i,d} = 1 if d == d(i) else c_d - n_{user(i),d}:
+ *   colcnt [D] float  c_d = number of columns with target d
+ *   row_col [N] int   d(i), the row's own target column
+ *   row_beg/row_end [N] int  range of the row's user's targets in exc_cols (sorted d's)
+ *   col_beg/col_end [D] int  range into exc_s/exc_e/exc_n: the user row ranges [s,e) that
+ *                            hold target d and their multiplicity n (backward, dB pass only)
+ * Rows of one user must be contiguous (flat (b, t) order). FLOPs: N*D instead of N*N. */
+int rsx_nce_grouped_fwd(const float* A, const float* B, const float* bias, const float* colcnt, const int* row_col,
+                        const int* row_beg, const int* row_end, const int* exc_cols, int64_t N, int64_t D,
+                        int64_t lda, int64_t ldb, float tau, int nsplit, float* ws, float* out2, void* stream);
+int rsx_nce_grouped_bwd(const float* A, const float* B, const float* bias, const float* colcnt, const int* row_col,
+                        const int* row_beg, const int* row_end, const int* exc_cols, const int* col_beg,
+                        const int* col_end, const int* exc_s, const int* exc_e, const int* exc_n, int64_t N,
+                        int64_t D, int64_t lda, int64_t ldb, float tau, int nsplit_fwd, int nsplit,
+                        const float* gout, float* ws, float* dA, float* dB, int accumulate, void* stream);
 
 /* ---- row gather / scatter / L2 normalise ---------------------------------------------
  * out[r] = src[idx[r]] (idx NULL => r), optionally F.normalize'd (eps) with norms saved:

@@ -32,7 +32,8 @@ _SIGS = {
     "rsx_seq_embed_fwd": (c_i, [c_p, c_p, c_p, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_i64, c_i64, c_i64, c_f, c_u64,
                                 c_p, c_p, c_p, c_p]),
     "rsx_seq_embed_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_i64, c_i64,
-                                c_i64, c_f, c_u64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+                                c_i64, c_f, c_u64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "rsx_seq_embed_bwd_workspace_floats": (c_i64, [c_i64, c_i64, c_i64, c_i, c_p]),
     "rsx_mha_fwd": (c_i, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i, c_f, c_u64, c_p, c_p, c_p]),
     "rsx_mha_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i, c_f, c_u64, c_p, c_p]),
     "rsx_nce_workspace_floats": (c_i64, [c_i64, c_i64, c_i, c_i]),

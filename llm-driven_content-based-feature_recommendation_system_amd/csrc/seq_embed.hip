@@ -138,13 +138,15 @@ struct BwdArgs {
   float* dln_b;
   int64_t rows_per_block;
   int small_total;        // floats of LDS for small tables
+  float* ws;              // [gridDim.x][L*D + small_total] per-workgroup partials
 };
 
 constexpr int kSmallMax = 8192;  // floats (32 KiB)
 
-// One workgroup per contiguous chunk of tokens. Position, small-table, LN and gate gradients
-// accumulate in LDS / registers and are flushed once per workgroup (no per-token atomics on
-// the hot 50-row position table); big-table rows are scatter-added with float atomics.
+// One workgroup per contiguous chunk of tokens. Position and small-table gradients accumulate
+// in LDS and leave as one per-workgroup partial slab (summed deterministically by
+// seq_embed_bwd_reduce_k: no contended atomics on the 50-row position table); LN and gate
+// gradients fold in registers; big-table rows are scatter-added with float atomics.
 template <int D>
 __global__ __launch_bounds__(256) void seq_embed_bwd_k(BwdArgs a) {
   constexpr int LPR = D / 4;
@@ -272,18 +274,36 @@ __global__ __launch_bounds__(256) void seq_embed_bwd_k(BwdArgs a) {
     for (int wv = 0; wv < NW; ++wv) v += s_gate[wv][tid];
     atomicAdd(a.dgate + tid, v);
   }
-  if (a.dpos) {
-    for (int i = tid; i < f.L * D; i += blockDim.x) {
-      const float v = s_pos[i];
-      if (v != 0.0f) atomicAdd(a.dpos + i, v);
-    }
+  float* slab = a.ws + (int64_t)blockIdx.x * lds_total;
+  for (int i = tid; i < lds_total; i += blockDim.x) slab[i] = s_dyn[i];
+}
+
+// dst_k += sum_b ws[b][k] for the position table (k < L*D) and the LDS-resident small tables.
+struct ReduceArgs {
+  const float* ws;
+  int nblocks;
+  int total;
+  int LD;
+  float* dpos;
+  float* dtab[kMaxTab];
+  int small_off[kMaxTab];
+  int small_len[kMaxTab];
+};
+
+__global__ __launch_bounds__(256) void seq_embed_bwd_reduce_k(ReduceArgs r) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= r.total) return;
+  float v = 0.0f;
+  for (int b = 0; b < r.nblocks; ++b) v += r.ws[(int64_t)b * r.total + k];
+  if (k < r.LD) {
+    if (r.dpos) r.dpos[k] += v;
+    return;
   }
-  for (int j = 0; j < f.ntab; ++j) {
-    if (a.small_off[j] < 0 || !a.dtab[j]) continue;
-    const int n = a.small_rows[j] * D;
-    for (int i = tid; i < n; i += blockDim.x) {
-      const float v = s_small[a.small_off[j] + i];
-      if (v != 0.0f) atomicAdd(a.dtab[j] + i, v);
+  const int ks = k - r.LD;
+#pragma unroll
+  for (int j = 0; j < kMaxTab; ++j) {
+    if (r.dtab[j] && ks >= r.small_off[j] && ks < r.small_off[j] + r.small_len[j]) {
+      r.dtab[j][ks - r.small_off[j]] += v;
     }
   }
 }
@@ -301,9 +321,47 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
 template <int D>
 int launch_bwd(const BwdArgs& a, hipStream_t st) {
   const int64_t blocks = (a.f.T + a.rows_per_block - 1) / a.rows_per_block;
-  const size_t lds = (size_t)(a.f.L * D + a.small_total) * sizeof(float);
+  const int total = a.f.L * D + a.small_total;
+  const size_t lds = (size_t)total * sizeof(float);
   hipLaunchKernelGGL(seq_embed_bwd_k<D>, dim3((unsigned)blocks), dim3(256), lds, st, a);
+  ReduceArgs r;
+  r.ws = a.ws;
+  r.nblocks = (int)blocks;
+  r.total = total;
+  r.LD = a.f.L * D;
+  r.dpos = a.dpos;
+  for (int j = 0; j < kMaxTab; ++j) {
+    const bool small = a.small_off[j] >= 0 && a.dtab[j];
+    r.dtab[j] = small ? a.dtab[j] : nullptr;
+    r.small_off[j] = small ? a.small_off[j] : 0;
+    r.small_len[j] = small ? a.small_rows[j] * D : 0;
+  }
+  hipLaunchKernelGGL(seq_embed_bwd_reduce_k, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, r);
   return 0;
+}
+
+int64_t bwd_rows_per_block(int64_t T, int64_t D) {
+  // enough workgroups to fill 256 CUs ~4x; each owns a contiguous token chunk
+  int64_t rpb = (T + 1023) / 1024;
+  const int64_t quantum = 4 * (64 / (D / 4));
+  rpb = (rpb + quantum - 1) / quantum * quantum;
+  if (rpb < quantum) rpb = quantum;
+  return rpb;
+}
+
+int small_layout(const int64_t* table_rows, int ntab, int64_t D, bool has_grad_j[kMaxTab], int off[kMaxTab],
+                 int rows[kMaxTab]) {
+  int o = 0;
+  for (int j = 0; j < kMaxTab; ++j) {
+    off[j] = -1;
+    rows[j] = 0;
+    if (j < ntab && has_grad_j[j] && table_rows && table_rows[j] * D <= 4096 && o + table_rows[j] * D <= kSmallMax) {
+      off[j] = o;
+      rows[j] = (int)table_rows[j];
+      o += (int)(table_rows[j] * D);
+    }
+  }
+  return o;
 }
 
 bool fill_fwd(FwdArgs& a, const float* base, const int64_t* const* ids, const float* const* tabs, int ntab,
@@ -360,45 +418,49 @@ RSX_API int rsx_seq_embed_bwd(const float* base, const int64_t* const* ids, cons
                               const float* pos, const int64_t* tok_pos, const float* ln_w, const float* mean,
                               const float* rstd, float eps, int64_t T, int64_t L, int64_t D, float p_drop,
                               uint64_t seed, const float* dout, float* dbase, float* const* dtables, float* dgate,
-                              float* dpos, float* dln_w, float* dln_b, void* stream) {
+                              float* dpos, float* dln_w, float* dln_b, float* ws, void* stream) {
   RSX_ARG(dout != nullptr, "dout is null");
   RSX_ARG(D == 64 || D == 128 || D == 256, "D must be 64, 128 or 256");
   RSX_ARG(ntab >= 0 && ntab <= kMaxTab, "ntab must be in [0,6]");
   RSX_ARG(ln_w == nullptr || (mean != nullptr && rstd != nullptr), "mean/rstd required with ln_w");
   RSX_ARG(p_drop >= 0.0f && p_drop < 1.0f, "p_drop must be in [0,1)");
   RSX_ARG(L > 0 && L <= 64, "need 0 < L <= 64");
+  RSX_ARG(ws != nullptr, "workspace required (rsx_seq_embed_bwd_workspace_floats)");
   if (T == 0) return 0;
   BwdArgs a;
   fill_fwd(a.f, base, ids, tables, ntab, gate, pos, tok_pos, ln_w, nullptr, eps, T, L, nullptr,
            const_cast<float*>(mean), const_cast<float*>(rstd), p_drop, seed);
   a.dout = dout;
   a.dbase = dbase;
-  int off = 0;
+  bool has_grad[kMaxTab];
   for (int j = 0; j < kMaxTab; ++j) {
     a.dtab[j] = (j < ntab && dtables) ? dtables[j] : nullptr;
     a.pad_idx[j] = (j < ntab && padding_idx) ? padding_idx[j] : -1;
-    a.small_off[j] = -1;
-    a.small_rows[j] = 0;
-    if (j < ntab && a.dtab[j] && table_rows && table_rows[j] * D <= 4096 && off + table_rows[j] * D <= kSmallMax) {
-      a.small_off[j] = off;
-      a.small_rows[j] = (int)table_rows[j];
-      off += (int)(table_rows[j] * D);
-    }
+    has_grad[j] = a.dtab[j] != nullptr;
   }
-  a.small_total = off;
+  a.small_total = small_layout(table_rows, ntab, D, has_grad, a.small_off, a.small_rows);
+  a.ws = ws;
   a.dgate = dgate;
   a.dpos = dpos;
   a.dln_w = dln_w;
   a.dln_b = dln_b;
-  // ~4 rows per lane-group per workgroup: enough blocks to fill 256 CUs several times
-  int64_t rpb = 4 * 4 * (64 / (D / 4)) * 8;
-  if (T / rpb < 1024) rpb = (T + 1023) / 1024;
-  if (rpb < 16) rpb = 16;
-  a.rows_per_block = rpb;
+  a.rows_per_block = bwd_rows_per_block(T, D);
   hipStream_t st = (hipStream_t)stream;
   if (D == 64) launch_bwd<64>(a, st);
   else if (D == 128) launch_bwd<128>(a, st);
   else launch_bwd<256>(a, st);
   RSX_LAUNCHED();
   return 0;
+}
+
+RSX_API int64_t rsx_seq_embed_bwd_workspace_floats(int64_t T, int64_t L, int64_t D, int ntab,
+                                                   const int64_t* table_rows) {
+  if (T <= 0 || D <= 0) return 1;
+  bool has_grad[kMaxTab];
+  int off[kMaxTab], rows[kMaxTab];
+  for (int j = 0; j < kMaxTab; ++j) has_grad[j] = true;
+  const int small = small_layout(table_rows, ntab, D, has_grad, off, rows);
+  const int64_t rpb = bwd_rows_per_block(T, D);
+  const int64_t blocks = (T + rpb - 1) / rpb;
+  return blocks * (L * D + small);
 }

@@ -67,11 +67,14 @@ class _SeqEmbed(torch.autograd.Function):
         dlnw = torch.zeros_like(ln_w) if need[3] else None
         dlnb = torch.zeros_like(ln_w) if need[4] else None
         dtabs = [torch.zeros_like(t) if need[8 + j] else None for j, t in enumerate(tables)]
+        rows = N.i64_array([t.shape[0] for t in tables])
+        nws = N.lib().rsx_seq_embed_bwd_workspace_floats(T, L, D, nt, rows)
+        ws = torch.empty(nws, device=dout.device, dtype=torch.float32)
         rc = N.lib().rsx_seq_embed_bwd(
-            N.ptr(base), N.ptr_array(ids), N.ptr_array(tables), N.i64_array([t.shape[0] for t in tables]),
+            N.ptr(base), N.ptr_array(ids), N.ptr_array(tables), rows,
             N.i64_array(padding_idx), nt, N.ptr(gate), N.ptr(pos), N.ptr(tok_pos), N.ptr(ln_w), N.ptr(mean),
             N.ptr(rstd), eps, T, L, D, p_drop, seed, N.ptr(dout), N.ptr(dbase), N.ptr_array(dtabs), N.ptr(dgate),
-            N.ptr(dpos), N.ptr(dlnw), N.ptr(dlnb), N.stream())
+            N.ptr(dpos), N.ptr(dlnw), N.ptr(dlnb), N.ptr(ws), N.stream())
         N.check(rc, "seq_embed_bwd")
         return (dbase, dgate, dpos, dlnw, dlnb, None, None, None, *dtabs)
 

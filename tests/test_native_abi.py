@@ -1,0 +1,51 @@
+"""CPU checks of the C ABI: the library loads (no GPU needed), exports every entry point
+declared in include/recsys_amd.h with a ctypes signature, and rejects bad arguments before
+launching anything."""
+import ctypes
+import os
+import re
+
+import pytest
+
+import recsys_amd  # noqa: F401
+from recsys_amd import _native
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "recsys_amd.h")
+
+
+def _declared():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^(?:int64_t|int|const char\*)\s+(rsx_\w+)\(", text, flags=re.M)))
+
+
+def test_header_declares_entry_points():
+    names = _declared()
+    assert "rsx_nce_grouped_fwd" in names and "rsx_seq_embed_fwd" in names
+    assert len(names) >= 14
+
+
+def test_library_exports_every_declared_symbol():
+    if not os.path.exists(_native.LIB_PATH):
+        pytest.skip("library not built (run __graft_entry__.build())")
+    lib = _native.load()
+    for name in _declared():
+        assert hasattr(lib, name), f"{name} declared in recsys_amd.h but not exported"
+        assert name in _native._SIGS, f"{name} has no ctypes signature in _native.py"
+    assert lib.rsx_target_arch() == b"gfx950"
+
+
+def test_argument_errors_are_reported_without_a_gpu():
+    if not os.path.exists(_native.LIB_PATH):
+        pytest.skip("library not built")
+    lib = _native.load()
+    # D = 100 is rejected before any launch
+    rc = lib.rsx_gather_rows(None, 100, None, 10, 100, 0, 1e-12, None, None, None)
+    assert rc == 1
+    assert b"null tensor" in lib.rsx_last_error() or b"D must be" in lib.rsx_last_error()
+    rc = lib.rsx_mha_fwd(ctypes.c_void_p(16), None, None, 2, 65, 4, 32, 1, 0.0, 0, ctypes.c_void_p(16), None, None)
+    assert rc == 1 and b"L must be" in lib.rsx_last_error()
+    rc = lib.rsx_nce_fwd(None, None, None, None, None, None, None, 4, 4, 128, 128, 0, 0.1, 3, 8, None, None, None)
+    assert rc == 1 and b"unsupported flag" in lib.rsx_last_error()
+    with pytest.raises(RuntimeError):
+        _native.check(1, "probe")
