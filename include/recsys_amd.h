@@ -52,16 +52,14 @@ int rsx_seq_embed_fwd(const float* base, const int64_t* const* ids, const float*
 /* Backward of rsx_seq_embed_fwd. dbase [T,D] written; dtables[j], dgate [ntab], dpos [L,D],
  * dln_w/dln_b [D] accumulated (nullable). padding_idx[j]: rows excluded from the table
  * gradient exactly like nn.Embedding(padding_idx=...) (-1 = none). table_rows[j] lets small
- * tables (time buckets) accumulate in LDS; position and small-table gradients leave each
- * workgroup as a partial slab in ws (rsx_seq_embed_bwd_workspace_floats floats) and are
- * summed deterministically. */
-int64_t rsx_seq_embed_bwd_workspace_floats(int64_t T, int64_t L, int64_t D, int ntab, const int64_t* table_rows);
+ * tables (time buckets) accumulate in LDS; position and small-table gradients are flushed
+ * once per workgroup (float atomics: summation order varies run to run in the last bits). */
 int rsx_seq_embed_bwd(const float* base, const int64_t* const* ids, const float* const* tables,
                       const int64_t* table_rows, const int64_t* padding_idx, int ntab, const float* gate,
                       const float* pos, const int64_t* tok_pos, const float* ln_w, const float* mean,
                       const float* rstd, float eps, int64_t T, int64_t L, int64_t D, float p_drop, uint64_t seed,
                       const float* dout, float* dbase, float* const* dtables, float* dgate, float* dpos,
-                      float* dln_w, float* dln_b, float* ws, void* stream);
+                      float* dln_w, float* dln_b, void* stream);
 
 /* ---- A3 / A9: masked multi-head self-attention core (L <= 64) -----------------------
  * Replaces the attention inside nn.TransformerEncoderLayer (norm_first, batch_first) at
@@ -124,6 +122,32 @@ int rsx_nce_grouped_bwd(const float* A, const float* B, const float* bias, const
                         const int* col_end, const int* exc_s, const int* exc_e, const int* exc_n, int64_t N,
                         int64_t D, int64_t lda, int64_t ldb, float tau, int nsplit_fwd, int nsplit,
                         const float* gout, float* ws, float* dA, float* dB, int accumulate, void* stream);
+
+/* ---- A14: retrieval top-k ------------------------------------------------------------
+ * scores = U I^T (fp32 MFMA, never materialised), per query the k best items sorted by
+ * (score desc, index asc). Replaces `scores = matmul(user, items.T); topk(k)` at
+ * tower_code/v1_usertower_train.py:672-675 and temp_model/ranker_skelet.py:193-196.
+ * U [Q, ldu], I [NI, ldi], D = 128, 1 <= k <= 512. ws: rsx_topk_workspace_bytes(Q, NI, k).
+ * out_idx = -1 where fewer than k items exist. */
+int64_t rsx_topk_workspace_bytes(int64_t Q, int64_t NI, int64_t k);
+int rsx_retrieve_topk(const float* U, int64_t ldu, const float* I, int64_t ldi, int64_t Q, int64_t NI, int64_t k,
+                      void* ws, float* out_scores, int64_t* out_idx, void* stream);
+
+/* ---- A16: DeepFM rerank forward ------------------------------------------------------
+ * deepctr-torch 0.2.9 DeepFM semantics (absent from the reference tree).
+ * rsx_deepfm_embed: x [R, F] int64 per-field ids, V[f] [vocab_f, 16], W[f] [vocab_f] (nullable)
+ *   -> emb_out [R, F*16] (concatenated DNN input, nullable) and
+ *      lin_out[r] = bias + sum_f W[f][x] + 0.5 * sum_k((sum_f v)^2 - sum_f v^2).
+ * rsx_linear_fwd: Y [M, N] = act(X W^T + b), W [N, K] torch Linear layout, N <= 256,
+ *   K % 4 == 0, act 0 none / 1 relu / 2 gelu (erf). fp32 MFMA.
+ * rsx_linear_dot_fwd: logit[m] = sum_n act(X W^T + b)[m, n] * wo[n] + add[m];
+ *   prob = sigmoid(logit) (nullable). */
+int rsx_deepfm_embed(const int64_t* x, int64_t R, int F, int E, const float* const* V, const float* const* W,
+                     float bias, float* emb_out, float* lin_out, void* stream);
+int rsx_linear_fwd(const float* X, int64_t ldx, const float* W, const float* b, int64_t M, int64_t N, int64_t K,
+                   int act, float* Y, void* stream);
+int rsx_linear_dot_fwd(const float* X, int64_t ldx, const float* W, const float* b, int64_t M, int64_t N, int64_t K,
+                       int act, const float* wo, const float* add, float* logit, float* prob, void* stream);
 
 /* ---- row gather / scatter / L2 normalise ---------------------------------------------
  * out[r] = src[idx[r]] (idx NULL => r), optionally F.normalize'd (eps) with norms saved:

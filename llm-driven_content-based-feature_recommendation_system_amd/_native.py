@@ -32,8 +32,7 @@ _SIGS = {
     "rsx_seq_embed_fwd": (c_i, [c_p, c_p, c_p, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_i64, c_i64, c_i64, c_f, c_u64,
                                 c_p, c_p, c_p, c_p]),
     "rsx_seq_embed_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_i64, c_i64,
-                                c_i64, c_f, c_u64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
-    "rsx_seq_embed_bwd_workspace_floats": (c_i64, [c_i64, c_i64, c_i64, c_i, c_p]),
+                                c_i64, c_f, c_u64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "rsx_mha_fwd": (c_i, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i, c_f, c_u64, c_p, c_p, c_p]),
     "rsx_mha_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i, c_f, c_u64, c_p, c_p]),
     "rsx_nce_workspace_floats": (c_i64, [c_i64, c_i64, c_i, c_i]),
@@ -45,6 +44,11 @@ _SIGS = {
                                   c_p, c_p]),
     "rsx_nce_grouped_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64,
                                   c_i64, c_i64, c_f, c_i, c_i, c_p, c_p, c_p, c_p, c_i, c_p]),
+    "rsx_deepfm_embed": (c_i, [c_p, c_i64, c_i, c_i, c_p, c_p, c_f, c_p, c_p, c_p]),
+    "rsx_linear_fwd": (c_i, [c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i64, c_i, c_p, c_p]),
+    "rsx_linear_dot_fwd": (c_i, [c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i64, c_i, c_p, c_p, c_p, c_p, c_p]),
+    "rsx_topk_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64]),
+    "rsx_retrieve_topk": (c_i, [c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p]),
     "rsx_gather_rows": (c_i, [c_p, c_i64, c_p, c_i64, c_i64, c_i, c_f, c_p, c_p, c_p]),
     "rsx_scatter_rows": (c_i, [c_p, c_p, c_p, c_p, c_i64, c_i64, c_i, c_f, c_i, c_i64, c_p, c_i64, c_p]),
 }

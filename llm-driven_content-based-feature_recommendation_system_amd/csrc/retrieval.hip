@@ -1,0 +1,251 @@
+// Retrieval: top-k items by inner product, without materialising the [Q, I] score matrix.
+// Reference: evaluate_model (tower_code/v1_usertower_train.py:672-675: scores = U W_n^T;
+// topk(max_k)) and ReRankingSystem.recommend (temp_model/ranker_skelet.py:193-196).
+//
+// Pass 1 (topk_scan_k): every workgroup owns 128 query rows (32 per wave, in registers as
+// in the InfoNCE kernels) and one item split; 32-item tiles stream through LDS and the
+// fp32-input MFMA produces a 32x32 score tile per wave. Each lane sees 16 of the tile's
+// items for its query and keeps the best KMAX of its stream in a private list (L1/L2
+// resident, replacement of the current minimum + rescan; after the first KMAX items an
+// insertion is rare, ~K ln(n/K) per stream).
+// Pass 2 (topk_merge_k): per query, the 2 * nsplit lists are bitonic-sorted in LDS by
+// (score desc, index asc) and the first k are written. Ties therefore resolve to the lower
+// item index (documented tie-break; torch.topk leaves tie order unspecified).
+#include "rsx_common.h"
+#include <math.h>
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int kD = 128;
+constexpr int kTile = 32;
+constexpr int kOwnRows = 128;
+constexpr int kLdsStride = kD + 4;
+
+__device__ __forceinline__ int tile_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+struct ScanArgs {
+  const float* U;  // [Q, ldu]
+  const float* I;  // [NI, ldi]
+  int64_t Q, NI, ldu, ldi;
+  int nsplit;
+  int64_t span;
+  int K;          // k (<= KMAX)
+  float* cs;      // [Q][nsplit][2][KMAX] scores
+  int* ci;        // [Q][nsplit][2][KMAX] indices
+};
+
+// (a beats b) <=> a.score > b.score or (equal and a.idx < b.idx)
+__device__ __forceinline__ bool better(float sa, int ia, float sb, int ib) {
+  return sa > sb || (sa == sb && ia < ib);
+}
+
+template <int KMAX>
+__global__ __launch_bounds__(256, 2) void topk_scan_k(ScanArgs a) {
+  __shared__ __attribute__((aligned(16))) float sI[2][kTile][kLdsStride];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, c = lane & 31;
+  const int b = blockIdx.x;
+  const int nsub = a.nsplit >> 3;
+  const int split = (b & 7) + 8 * ((b >> 3) % nsub);
+  const int rb = (b >> 3) / nsub;
+  const int64_t q = (int64_t)rb * kOwnRows + wave * 32 + c;
+  const bool q_ok = q < a.Q;
+  float u[64];
+  if (q_ok) {
+    const float4* src = reinterpret_cast<const float4*>(a.U + q * a.ldu + h * 64);
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const float4 v = src[t];
+      u[4 * t] = v.x; u[4 * t + 1] = v.y; u[4 * t + 2] = v.z; u[4 * t + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < 64; ++t) u[t] = 0.0f;
+  }
+  const int64_t j_begin = (int64_t)split * a.span;
+  int64_t j_end = j_begin + a.span;
+  if (j_end > a.NI) j_end = a.NI;
+
+  const int64_t lbase = ((q_ok ? q : 0) * a.nsplit + split) * 2 + h;
+  float* ls = a.cs + lbase * KMAX;
+  int* li = a.ci + lbase * KMAX;
+  const int K = a.K;
+  int cnt = 0, minslot = 0;
+  float thr = -INFINITY;
+  int thr_i = 0x7fffffff;
+
+  auto rescan = [&]() {
+    float ms = ls[0];
+    int mi = li[0], mslot = 0;
+    for (int t = 1; t < K; ++t) {
+      const float s = ls[t];
+      const int ii = li[t];
+      if (better(ms, mi, s, ii)) { ms = s; mi = ii; mslot = t; }
+    }
+    thr = ms; thr_i = mi; minslot = mslot;
+  };
+
+  const int srow = tid >> 3, scol = (tid & 7) * 16;
+  float4 stg[4];
+  auto gload = [&](int64_t j0) {
+    const int64_t j = j0 + srow;
+    if (j < j_end) {
+      const float4* src = reinterpret_cast<const float4*>(a.I + j * a.ldi + scol);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) stg[t] = src[t];
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) stg[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) *reinterpret_cast<float4*>(&sI[buf][srow][scol + 4 * t]) = stg[t];
+  };
+
+  if (j_begin < j_end) {
+    gload(j_begin);
+    lstore(0);
+    __syncthreads();
+    int cur = 0;
+    for (int64_t j0 = j_begin; j0 < j_end; j0 += kTile) {
+      const bool has_next = j0 + kTile < j_end;
+      if (has_next) gload(j0 + kTile);
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+      const float* xrow = &sI[cur][c][h * 64];
+#pragma unroll
+      for (int s = 0; s < 64; s += 4) {
+        const float4 bv = *reinterpret_cast<const float4*>(xrow + s);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(bv.x, u[s + 0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(bv.y, u[s + 1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(bv.z, u[s + 2], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(bv.w, u[s + 3], acc, 0, 0, 0);
+      }
+      if (q_ok) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int64_t j = j0 + tile_row(r, h);
+          const float s = acc[r];
+          if (j < j_end) {
+            if (cnt < K) {
+              ls[cnt] = s;
+              li[cnt] = (int)j;
+              ++cnt;
+              if (cnt == K) rescan();
+            } else if (better(s, (int)j, thr, thr_i)) {
+              ls[minslot] = s;
+              li[minslot] = (int)j;
+              rescan();
+            }
+          }
+        }
+      }
+      __syncthreads();
+      if (has_next) lstore(cur ^ 1);
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+  if (q_ok) {
+    for (int t = cnt; t < KMAX; ++t) {
+      ls[t] = -INFINITY;
+      li[t] = 0x7fffffff;
+    }
+  }
+}
+
+// One workgroup per query: bitonic sort of NC = 2*nsplit*KMAX candidates, descending.
+template <int NC>
+__global__ __launch_bounds__(256) void topk_merge_k(const float* cs, const int* ci, int64_t Q, int ncand, int K,
+                                                    float* out_s, int64_t* out_i) {
+  __shared__ float ss[NC];
+  __shared__ int si[NC];
+  const int64_t q = blockIdx.x;
+  const float* s = cs + q * ncand;
+  const int* ii = ci + q * ncand;
+  for (int t = threadIdx.x; t < NC; t += blockDim.x) {
+    if (t < ncand) {
+      ss[t] = s[t];
+      si[t] = ii[t];
+    } else {
+      ss[t] = -INFINITY;
+      si[t] = 0x7fffffff;
+    }
+  }
+  __syncthreads();
+  for (int size = 2; size <= NC; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = threadIdx.x; t < NC / 2; t += blockDim.x) {
+        const int lo = 2 * t - (t & (stride - 1));
+        const int hi = lo + stride;
+        const bool desc = ((lo & size) == 0);  // descending runs first => overall descending
+        const float a0 = ss[lo], a1 = ss[hi];
+        const int b0 = si[lo], b1 = si[hi];
+        const bool swap = desc ? better(a1, b1, a0, b0) : better(a0, b0, a1, b1);
+        if (swap) {
+          ss[lo] = a1; ss[hi] = a0;
+          si[lo] = b1; si[hi] = b0;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int t = threadIdx.x; t < K; t += blockDim.x) {
+    out_s[q * K + t] = ss[t];
+    out_i[q * K + t] = (si[t] == 0x7fffffff) ? -1 : (int64_t)si[t];
+  }
+}
+
+int choose_nsplit(int64_t Q, int64_t NI, int kmax) {
+  // >= ~1024 workgroups when there are enough items; each split keeps >= 2048 items; the
+  // merge sorts at most 8192 candidates per query in LDS (2 * nsplit * kmax <= 8192)
+  const int64_t rbs = (Q + kOwnRows - 1) / kOwnRows;
+  const int ns_max = 8192 / (2 * kmax);
+  int ns = 8;
+  while (ns < ns_max && rbs * ns < 1024 && NI / (ns * 2) >= 2048) ns *= 2;
+  return ns;
+}
+
+}  // namespace
+
+RSX_API int64_t rsx_topk_workspace_bytes(int64_t Q, int64_t NI, int64_t k) {
+  const int kmax = k <= 128 ? 128 : 512;
+  const int ns = choose_nsplit(Q, NI, kmax);
+  return Q * ns * 2 * (int64_t)kmax * 8 + 256;
+}
+
+// scores [Q, k] (desc), idx [Q, k] int64 (-1 where fewer than k items exist).
+RSX_API int rsx_retrieve_topk(const float* U, int64_t ldu, const float* I, int64_t ldi, int64_t Q, int64_t NI,
+                              int64_t k, void* ws, float* out_scores, int64_t* out_idx, void* stream) {
+  RSX_ARG(U && I && ws && out_scores && out_idx, "null tensor");
+  RSX_ARG(k >= 1 && k <= 512, "k must be in [1,512]");
+  RSX_ARG(ldu >= kD && ldi >= kD && ldu % 4 == 0 && ldi % 4 == 0, "D must be 128 (row strides >= 128)");
+  RSX_ARG(NI < 0x7fffffff, "item count must fit int32");
+  if (Q == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const int kmax = k <= 128 ? 128 : 512;
+  ScanArgs a;
+  a.U = U; a.I = I; a.Q = Q; a.NI = NI; a.ldu = ldu; a.ldi = ldi;
+  a.nsplit = choose_nsplit(Q, NI, kmax);
+  a.span = ((NI + a.nsplit - 1) / a.nsplit + kTile - 1) / kTile * kTile;
+  if (a.span < kTile) a.span = kTile;
+  a.K = (int)k;
+  a.cs = reinterpret_cast<float*>(ws);
+  a.ci = reinterpret_cast<int*>(reinterpret_cast<char*>(ws) + Q * a.nsplit * 2 * (int64_t)kmax * 4);
+  const int blocks = (int)(((Q + kOwnRows - 1) / kOwnRows) * a.nsplit);
+  if (kmax == 128) hipLaunchKernelGGL(topk_scan_k<128>, dim3(blocks), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(topk_scan_k<512>, dim3(blocks), dim3(256), 0, st, a);
+  RSX_LAUNCHED();
+  const int ncand = a.nsplit * 2 * kmax;
+  if (ncand <= 2048)
+    hipLaunchKernelGGL(topk_merge_k<2048>, dim3((unsigned)Q), dim3(256), 0, st, a.cs, a.ci, Q, ncand, (int)k,
+                       out_scores, out_idx);
+  else
+    hipLaunchKernelGGL(topk_merge_k<8192>, dim3((unsigned)Q), dim3(256), 0, st, a.cs, a.ci, Q, ncand, (int)k,
+                       out_scores, out_idx);
+  RSX_LAUNCHED();
+  return 0;
+}

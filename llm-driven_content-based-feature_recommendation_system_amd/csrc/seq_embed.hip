@@ -138,15 +138,15 @@ struct BwdArgs {
   float* dln_b;
   int64_t rows_per_block;
   int small_total;        // floats of LDS for small tables
-  float* ws;              // [gridDim.x][L*D + small_total] per-workgroup partials
 };
 
 constexpr int kSmallMax = 8192;  // floats (32 KiB)
 
-// One workgroup per contiguous chunk of tokens. Position and small-table gradients accumulate
-// in LDS and leave as one per-workgroup partial slab (summed deterministically by
-// seq_embed_bwd_reduce_k: no contended atomics on the 50-row position table); LN and gate
-// gradients fold in registers; big-table rows are scatter-added with float atomics.
+// One workgroup per contiguous chunk of tokens (~2 per CU). Position and small-table
+// gradients accumulate in LDS (ds_add_f32) and are flushed once per workgroup; LN and gate
+// gradients fold in registers; big-table rows are scatter-added with global float atomics.
+// The LDS and global scatter paths are kept apart so no flat (address-space-generic)
+// atomics are emitted.
 template <int D>
 __global__ __launch_bounds__(256) void seq_embed_bwd_k(BwdArgs a) {
   constexpr int LPR = D / 4;
@@ -227,9 +227,16 @@ __global__ __launch_bounds__(256) void seq_embed_bwd_k(BwdArgs a) {
         }
         if (a.dtab[j] && id != a.pad_idx[j]) {
           const float4 v = make_float4(dx.x * g[j], dx.y * g[j], dx.z * g[j], dx.w * g[j]);
-          float* dst = (a.small_off[j] >= 0) ? (s_small + a.small_off[j] + id * D + 4 * c)
-                                             : (a.dtab[j] + id * D + 4 * c);
-          atomicAdd(dst + 0, v.x); atomicAdd(dst + 1, v.y); atomicAdd(dst + 2, v.z); atomicAdd(dst + 3, v.w);
+          if (a.small_off[j] >= 0) {
+            float* dst = s_small + a.small_off[j] + id * D + 4 * c;
+            __hip_atomic_fetch_add(dst + 0, v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(dst + 1, v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(dst + 2, v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(dst + 3, v.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          } else {
+            float* dst = a.dtab[j] + id * D + 4 * c;
+            atomicAdd(dst + 0, v.x); atomicAdd(dst + 1, v.y); atomicAdd(dst + 2, v.z); atomicAdd(dst + 3, v.w);
+          }
         }
       }
     }
@@ -274,36 +281,18 @@ __global__ __launch_bounds__(256) void seq_embed_bwd_k(BwdArgs a) {
     for (int wv = 0; wv < NW; ++wv) v += s_gate[wv][tid];
     atomicAdd(a.dgate + tid, v);
   }
-  float* slab = a.ws + (int64_t)blockIdx.x * lds_total;
-  for (int i = tid; i < lds_total; i += blockDim.x) slab[i] = s_dyn[i];
-}
-
-// dst_k += sum_b ws[b][k] for the position table (k < L*D) and the LDS-resident small tables.
-struct ReduceArgs {
-  const float* ws;
-  int nblocks;
-  int total;
-  int LD;
-  float* dpos;
-  float* dtab[kMaxTab];
-  int small_off[kMaxTab];
-  int small_len[kMaxTab];
-};
-
-__global__ __launch_bounds__(256) void seq_embed_bwd_reduce_k(ReduceArgs r) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= r.total) return;
-  float v = 0.0f;
-  for (int b = 0; b < r.nblocks; ++b) v += r.ws[(int64_t)b * r.total + k];
-  if (k < r.LD) {
-    if (r.dpos) r.dpos[k] += v;
-    return;
+  if (a.dpos) {
+    for (int i = tid; i < f.L * D; i += blockDim.x) {
+      const float v = s_pos[i];
+      if (v != 0.0f) atomicAdd(a.dpos + i, v);
+    }
   }
-  const int ks = k - r.LD;
-#pragma unroll
-  for (int j = 0; j < kMaxTab; ++j) {
-    if (r.dtab[j] && ks >= r.small_off[j] && ks < r.small_off[j] + r.small_len[j]) {
-      r.dtab[j][ks - r.small_off[j]] += v;
+  for (int j = 0; j < f.ntab; ++j) {
+    if (a.small_off[j] < 0 || !a.dtab[j]) continue;
+    const int n = a.small_rows[j] * D;
+    for (int i = tid; i < n; i += blockDim.x) {
+      const float v = s_small[a.small_off[j] + i];
+      if (v != 0.0f) atomicAdd(a.dtab[j] + i, v);
     }
   }
 }
@@ -321,28 +310,14 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
 template <int D>
 int launch_bwd(const BwdArgs& a, hipStream_t st) {
   const int64_t blocks = (a.f.T + a.rows_per_block - 1) / a.rows_per_block;
-  const int total = a.f.L * D + a.small_total;
-  const size_t lds = (size_t)total * sizeof(float);
+  const size_t lds = (size_t)(a.f.L * D + a.small_total) * sizeof(float);
   hipLaunchKernelGGL(seq_embed_bwd_k<D>, dim3((unsigned)blocks), dim3(256), lds, st, a);
-  ReduceArgs r;
-  r.ws = a.ws;
-  r.nblocks = (int)blocks;
-  r.total = total;
-  r.LD = a.f.L * D;
-  r.dpos = a.dpos;
-  for (int j = 0; j < kMaxTab; ++j) {
-    const bool small = a.small_off[j] >= 0 && a.dtab[j];
-    r.dtab[j] = small ? a.dtab[j] : nullptr;
-    r.small_off[j] = small ? a.small_off[j] : 0;
-    r.small_len[j] = small ? a.small_rows[j] * D : 0;
-  }
-  hipLaunchKernelGGL(seq_embed_bwd_reduce_k, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, r);
   return 0;
 }
 
 int64_t bwd_rows_per_block(int64_t T, int64_t D) {
-  // enough workgroups to fill 256 CUs ~4x; each owns a contiguous token chunk
-  int64_t rpb = (T + 1023) / 1024;
+  // ~2 workgroups per CU, each owning a contiguous token chunk
+  int64_t rpb = (T + 511) / 512;
   const int64_t quantum = 4 * (64 / (D / 4));
   rpb = (rpb + quantum - 1) / quantum * quantum;
   if (rpb < quantum) rpb = quantum;
@@ -418,14 +393,13 @@ RSX_API int rsx_seq_embed_bwd(const float* base, const int64_t* const* ids, cons
                               const float* pos, const int64_t* tok_pos, const float* ln_w, const float* mean,
                               const float* rstd, float eps, int64_t T, int64_t L, int64_t D, float p_drop,
                               uint64_t seed, const float* dout, float* dbase, float* const* dtables, float* dgate,
-                              float* dpos, float* dln_w, float* dln_b, float* ws, void* stream) {
+                              float* dpos, float* dln_w, float* dln_b, void* stream) {
   RSX_ARG(dout != nullptr, "dout is null");
   RSX_ARG(D == 64 || D == 128 || D == 256, "D must be 64, 128 or 256");
   RSX_ARG(ntab >= 0 && ntab <= kMaxTab, "ntab must be in [0,6]");
   RSX_ARG(ln_w == nullptr || (mean != nullptr && rstd != nullptr), "mean/rstd required with ln_w");
   RSX_ARG(p_drop >= 0.0f && p_drop < 1.0f, "p_drop must be in [0,1)");
   RSX_ARG(L > 0 && L <= 64, "need 0 < L <= 64");
-  RSX_ARG(ws != nullptr, "workspace required (rsx_seq_embed_bwd_workspace_floats)");
   if (T == 0) return 0;
   BwdArgs a;
   fill_fwd(a.f, base, ids, tables, ntab, gate, pos, tok_pos, ln_w, nullptr, eps, T, L, nullptr,
@@ -439,7 +413,6 @@ RSX_API int rsx_seq_embed_bwd(const float* base, const int64_t* const* ids, cons
     has_grad[j] = a.dtab[j] != nullptr;
   }
   a.small_total = small_layout(table_rows, ntab, D, has_grad, a.small_off, a.small_rows);
-  a.ws = ws;
   a.dgate = dgate;
   a.dpos = dpos;
   a.dln_w = dln_w;
@@ -453,14 +426,3 @@ RSX_API int rsx_seq_embed_bwd(const float* base, const int64_t* const* ids, cons
   return 0;
 }
 
-RSX_API int64_t rsx_seq_embed_bwd_workspace_floats(int64_t T, int64_t L, int64_t D, int ntab,
-                                                   const int64_t* table_rows) {
-  if (T <= 0 || D <= 0) return 1;
-  bool has_grad[kMaxTab];
-  int off[kMaxTab], rows[kMaxTab];
-  for (int j = 0; j < kMaxTab; ++j) has_grad[j] = true;
-  const int small = small_layout(table_rows, ntab, D, has_grad, off, rows);
-  const int64_t rpb = bwd_rows_per_block(T, D);
-  const int64_t blocks = (T + rpb - 1) / rpb;
-  return blocks * (L * D + small);
-}

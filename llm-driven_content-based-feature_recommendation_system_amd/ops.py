@@ -68,13 +68,11 @@ class _SeqEmbed(torch.autograd.Function):
         dlnb = torch.zeros_like(ln_w) if need[4] else None
         dtabs = [torch.zeros_like(t) if need[8 + j] else None for j, t in enumerate(tables)]
         rows = N.i64_array([t.shape[0] for t in tables])
-        nws = N.lib().rsx_seq_embed_bwd_workspace_floats(T, L, D, nt, rows)
-        ws = torch.empty(nws, device=dout.device, dtype=torch.float32)
         rc = N.lib().rsx_seq_embed_bwd(
             N.ptr(base), N.ptr_array(ids), N.ptr_array(tables), rows,
             N.i64_array(padding_idx), nt, N.ptr(gate), N.ptr(pos), N.ptr(tok_pos), N.ptr(ln_w), N.ptr(mean),
             N.ptr(rstd), eps, T, L, D, p_drop, seed, N.ptr(dout), N.ptr(dbase), N.ptr_array(dtabs), N.ptr(dgate),
-            N.ptr(dpos), N.ptr(dlnw), N.ptr(dlnb), N.ptr(ws), N.stream())
+            N.ptr(dpos), N.ptr(dlnw), N.ptr(dlnb), N.stream())
         N.check(rc, "seq_embed_bwd")
         return (dbase, dgate, dpos, dlnw, dlnb, None, None, None, *dtabs)
 
@@ -370,6 +368,81 @@ def nce_grouped_sum(A, B_distinct, bias, groups: TargetGroups, tau=0.1, tag="nce
     if bias is not None:
         bias = _c(bias.to(torch.float32))
     return _NCEGrouped.apply(A, B_distinct, bias, groups, float(tau), str(tag))
+
+
+# ----------------------------------------------------------------------------------------
+# A16: DeepFM forward (inference)
+ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
+
+
+def linear(x, weight, bias=None, act=ACT_NONE):
+    """act(x @ weight.T + bias) on the fp32 MFMA (forward only). x [M, K], weight [N<=256, K]."""
+    N.ensure_device(x)
+    x = _c(x)
+    M, K = x.shape
+    n = weight.shape[0]
+    y = torch.empty(M, n, device=x.device, dtype=torch.float32)
+    with timed("linear"):
+        rc = N.lib().rsx_linear_fwd(N.ptr(x), x.stride(0), N.ptr(_c(weight)), N.ptr(bias), M, n, K, act, N.ptr(y),
+                                    N.stream())
+    N.check(rc, "linear_fwd")
+    return y
+
+
+def deepfm_forward(x, emb_tables, lin_tables, out_bias, dnn_weights, dnn_biases, w_out):
+    """DeepFM logits/probabilities for x [R, F] int64 (see csrc/deepfm.hip).
+
+    emb_tables: F tensors [vocab_f, 16]; lin_tables: F tensors [vocab_f] (or [vocab_f, 1]);
+    dnn_weights/dnn_biases: torch Linear layout, ReLU between layers; w_out [H_last].
+    Returns (logit [R], prob [R])."""
+    N.ensure_device(x)
+    x = _c(x)
+    R, F = x.shape
+    E = emb_tables[0].shape[1]
+    dev = x.device
+    emb = torch.empty(R, F * E, device=dev, dtype=torch.float32)
+    lin = torch.empty(R, device=dev, dtype=torch.float32)
+    with timed("deepfm/embed"):
+        rc = N.lib().rsx_deepfm_embed(N.ptr(x), R, F, E, N.ptr_array([_c(t) for t in emb_tables]),
+                                      N.ptr_array([_c(t) for t in lin_tables]), float(out_bias), N.ptr(emb),
+                                      N.ptr(lin), N.stream())
+    N.check(rc, "deepfm_embed")
+    h = emb
+    for w, b in zip(dnn_weights[:-1], dnn_biases[:-1]):
+        with timed("deepfm/linear"):
+            y = torch.empty(R, w.shape[0], device=dev, dtype=torch.float32)
+            rc = N.lib().rsx_linear_fwd(N.ptr(h), h.stride(0), N.ptr(_c(w)), N.ptr(b), R, w.shape[0], h.shape[1],
+                                        ACT_RELU, N.ptr(y), N.stream())
+        N.check(rc, "linear_fwd")
+        h = y
+    logit = torch.empty(R, device=dev, dtype=torch.float32)
+    prob = torch.empty(R, device=dev, dtype=torch.float32)
+    w, b = dnn_weights[-1], dnn_biases[-1]
+    with timed("deepfm/linear_dot"):
+        rc = N.lib().rsx_linear_dot_fwd(N.ptr(h), h.stride(0), N.ptr(_c(w)), N.ptr(b), R, w.shape[0], h.shape[1],
+                                        ACT_RELU, N.ptr(_c(w_out.reshape(-1))), N.ptr(lin), N.ptr(logit),
+                                        N.ptr(prob), N.stream())
+    N.check(rc, "linear_dot_fwd")
+    return logit, prob
+
+
+# ----------------------------------------------------------------------------------------
+# A14: retrieval top-k
+def retrieve_topk(queries, items, k):
+    """(scores [Q, k] desc, indices [Q, k] int64) of queries @ items.T without materialising
+    the score matrix. Ties resolve to the lower item index. D = 128."""
+    N.ensure_device(queries)
+    q = _c(queries.to(torch.float32))
+    it = items if (items.stride(-1) == 1 and items.stride(0) % 4 == 0) else items.contiguous()
+    Q, NI = q.shape[0], it.shape[0]
+    ws = torch.empty(N.lib().rsx_topk_workspace_bytes(Q, NI, k), device=q.device, dtype=torch.uint8)
+    sc = torch.empty(Q, k, device=q.device, dtype=torch.float32)
+    ix = torch.empty(Q, k, device=q.device, dtype=torch.int64)
+    with timed("retrieve_topk"):
+        rc = N.lib().rsx_retrieve_topk(N.ptr(q), q.stride(0), N.ptr(it), it.stride(0), Q, NI, k, N.ptr(ws),
+                                       N.ptr(sc), N.ptr(ix), N.stream())
+    N.check(rc, "retrieve_topk")
+    return sc, ix
 
 
 # ----------------------------------------------------------------------------------------

@@ -1,0 +1,160 @@
+"""Drop-in for temp_model/ranker_skelet.py: retrieval -> rerank.
+
+Reference (temp_model/ranker_skelet.py):
+  * FeatureEngineer :13-89, RecommendationRanker (CatBoost) :95-149, ReRankingSystem :155-237
+  * the neural ranker the north star asks for (DeepFM) does not exist in the reference; it
+    is specified by deepctr-torch 0.2.9 (pinned in requirements.txt:41, never imported) and
+    lives here as `DeepFM`, with a CatBoost-compatible `predict_proba` wrapper.
+Compute: DeepFM forward = rsx_deepfm_embed + rsx_linear_fwd + rsx_linear_dot_fwd; retrieval
+(user_vec @ item_vectors.T -> topk, :193-196) = rsx_retrieve_topk (see ops.retrieve_topk).
+"""
+from __future__ import annotations
+
+from typing import Dict, List
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from .. import ops
+
+
+class DeepFM(nn.Module):
+    """deepctr-torch-style DeepFM over F sparse fields (binary task).
+
+    Parameter names follow deepctr-torch's module tree (embedding_dict.C{i}, linear_model.
+    embedding_dict.C{i}, dnn.linears.{j}, dnn_linear, out.bias) so its checkpoints map 1:1.
+    forward(X [R, F] int64) -> prob [R, 1] (as deepctr's BaseModel.forward)."""
+
+    def __init__(self, field_vocab_sizes, embed_dim=16, dnn_hidden_units=(256, 128), init_std=1e-4, seed=1024,
+                 device="cpu"):
+        super().__init__()
+        if embed_dim != 16:
+            raise ValueError("the fused kernel is specialised for embed_dim=16 (config 3)")
+        torch.manual_seed(seed)
+        self.field_names = [f"C{i + 1}" for i in range(len(field_vocab_sizes))]
+        self.embed_dim = embed_dim
+        self.embedding_dict = nn.ModuleDict(
+            {n: nn.Embedding(v, embed_dim) for n, v in zip(self.field_names, field_vocab_sizes)})
+        self.linear_model = nn.Module()
+        self.linear_model.embedding_dict = nn.ModuleDict(
+            {n: nn.Embedding(v, 1) for n, v in zip(self.field_names, field_vocab_sizes)})
+        dims = [len(field_vocab_sizes) * embed_dim] + list(dnn_hidden_units)
+        self.dnn = nn.Module()
+        self.dnn.linears = nn.ModuleList([nn.Linear(dims[i], dims[i + 1]) for i in range(len(dims) - 1)])
+        self.dnn_linear = nn.Linear(dims[-1], 1, bias=False)
+        self.out = nn.Module()
+        self.out.bias = nn.Parameter(torch.zeros((1,)))
+        for emb in list(self.embedding_dict.values()) + list(self.linear_model.embedding_dict.values()):
+            nn.init.normal_(emb.weight, mean=0, std=init_std)
+        for name, t in self.dnn.linears.named_parameters():
+            if "weight" in name:
+                nn.init.normal_(t, mean=0, std=init_std)
+        self.to(device)
+
+    @torch.no_grad()
+    def forward(self, X):
+        _, prob = self.forward_logits(X)
+        return prob.unsqueeze(1)
+
+    @torch.no_grad()
+    def forward_logits(self, X):
+        return ops.deepfm_forward(
+            X, [self.embedding_dict[n].weight for n in self.field_names],
+            [self.linear_model.embedding_dict[n].weight for n in self.field_names], float(self.out.bias.item()),
+            [l.weight for l in self.dnn.linears], [l.bias for l in self.dnn.linears], self.dnn_linear.weight)
+
+    def predict_proba(self, X) -> np.ndarray:
+        """CatBoost-compatible: probability of class 1 (RecommendationRanker.predict_proba :148-149)."""
+        if not torch.is_tensor(X):
+            X = torch.as_tensor(np.asarray(X), dtype=torch.int64)
+        dev = next(self.parameters()).device
+        return self.forward_logits(X.to(dev))[1].cpu().numpy()
+
+
+class FeatureEngineer:
+    """Reference :13-89 (per-candidate tabular features for the CatBoost ranker)."""
+
+    def __init__(self):
+        self.cat_features = ["season", "gender", "item_category", "item_material", "item_fit", "time_of_day"]
+
+    def create_features(self, user_meta: Dict, item_meta: Dict, two_tower_score: float, user_vector: np.ndarray,
+                        item_vector: np.ndarray) -> Dict:
+        inter = user_vector * item_vector
+        f = {"two_tower_score": two_tower_score, "vec_prod_mean": float(np.mean(inter)),
+             "vec_prod_max": float(np.max(inter)), "vec_prod_std": float(np.std(inter)),
+             "season": user_meta.get("season", "unknown"), "gender": user_meta.get("gender", "unknown"),
+             "user_avg_price": user_meta.get("avg_price", 0.0),
+             "item_category": item_meta.get("category", "unknown"),
+             "item_material": item_meta.get("material", "unknown"), "item_fit": item_meta.get("fit", "unknown"),
+             "item_price": item_meta.get("price", 0)}
+        f["price_diff_ratio"] = ((f["item_price"] - f["user_avg_price"]) / f["user_avg_price"]
+                                 if f["user_avg_price"] > 0 else 0.0)
+        return f
+
+    def prepare_batch(self, batch_data: List[Dict]):
+        import pandas as pd
+        rows = []
+        for d in batch_data:
+            row = self.create_features(d["user_meta"], d["item_meta"], d["two_tower_score"], d["user_vector"],
+                                       d["item_vector"])
+            if "label" in d:
+                row["target"] = d["label"]
+            rows.append(row)
+        return pd.DataFrame(rows)
+
+
+class RecommendationRanker:
+    """Reference :95-149 (CatBoost). Importable without catboost; constructing it needs it."""
+
+    def __init__(self, model_path: str = None):
+        from catboost import CatBoostClassifier  # noqa: F401  (absent in this image: raises ImportError)
+        self.engineer = FeatureEngineer()
+        self.model = CatBoostClassifier(iterations=1000, learning_rate=0.05, depth=6, loss_function="Logloss",
+                                        eval_metric="AUC", verbose=100, early_stopping_rounds=50,
+                                        cat_features=self.engineer.cat_features, random_seed=42)
+        self.is_fitted = False
+        if model_path:
+            self.model.load_model(model_path)
+            self.is_fitted = True
+
+    def predict_proba(self, X) -> np.ndarray:
+        return self.model.predict_proba(X)[:, 1]
+
+
+class ReRankingSystem:
+    """Reference :155-237: retrieval (user_vec @ item_vectors.T, top-k) then rerank.
+
+    ranker: a DeepFM (rerank features = `rerank_features(user_vec, candidate_ids)` -> [k, F]
+    int64 ids, e.g. hashed (user bucket, item) crosses) or a RecommendationRanker (CatBoost
+    on FeatureEngineer rows, as the reference)."""
+
+    def __init__(self, user_tower, item_tower, ranker, item_db_metadata: Dict[int, Dict],
+                 item_db_vectors: torch.Tensor, rerank_features=None):
+        self.user_tower = user_tower
+        self.item_tower = item_tower
+        self.ranker = ranker
+        self.item_metadata = item_db_metadata
+        self.item_vectors = item_db_vectors
+        self.rerank_features = rerank_features
+        self.device = item_db_vectors.device
+
+    def recommend(self, user_vector: torch.Tensor, user_meta_raw: Dict = None, top_k_retrieval: int = 100,
+                  final_k: int = 10):
+        uv = user_vector.reshape(1, -1).to(self.device, torch.float32)
+        top_scores, top_idx = ops.retrieve_topk(uv, self.item_vectors, top_k_retrieval)
+        idx = top_idx[0]
+        if isinstance(self.ranker, DeepFM):
+            feats = self.rerank_features(uv, idx)
+            probs = self.ranker.predict_proba(feats)
+        else:
+            rows = [{"user_meta": user_meta_raw or {}, "item_meta": self.item_metadata.get(int(i), {}),
+                     "two_tower_score": float(s), "user_vector": uv[0].cpu().numpy(),
+                     "item_vector": self.item_vectors[int(i)].cpu().numpy()}
+                    for s, i in zip(top_scores[0].tolist(), idx.tolist())]
+            probs = self.ranker.predict_proba(self.ranker.engineer.prepare_batch(rows))
+        order = np.argsort(probs)[::-1][:final_k]
+        idx_cpu = idx.cpu().numpy()
+        sc_cpu = top_scores[0].cpu().numpy()
+        return [{"product_id": int(idx_cpu[o]), "two_tower_score": float(sc_cpu[o]), "final_score": float(probs[o])}
+                for o in order]

@@ -1,0 +1,91 @@
+"""DeepFM forward (A16) and retrieval top-k (A14) vs the CPU oracles."""
+import pytest
+import torch
+
+import recsys_amd  # noqa: F401
+from recsys_amd import ops
+from recsys_amd.temp_model.ranker_skelet import DeepFM, ReRankingSystem
+from oracle import deepfm as OD
+from oracle import retrieval as OR
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("R,F,vocab", [(1000, 39, 500), (77, 5, 50), (4096, 39, 10000)])
+def test_deepfm_forward_matches_oracle(gpu, R, F, vocab):
+    model = DeepFM([vocab] * F, init_std=0.05, device=gpu)  # larger init than 1e-4 so every term matters
+    g = torch.Generator().manual_seed(R)
+    x = torch.randint(0, vocab, (R, F), generator=g)
+    with torch.no_grad():
+        model.out.bias.fill_(0.1)
+        for l in model.dnn.linears:
+            l.bias.normal_(0, 0.05)
+    logit, prob = model.forward_logits(x.to(gpu))
+    names = model.field_names
+    ref_l, ref_p = OD.deepfm_forward(
+        x, [model.embedding_dict[n].weight.cpu() for n in names],
+        [model.linear_model.embedding_dict[n].weight.cpu() for n in names], 0.1,
+        [l.weight.cpu() for l in model.dnn.linears], [l.bias.cpu() for l in model.dnn.linears],
+        model.dnn_linear.weight.cpu())
+    torch.testing.assert_close(logit.cpu().double(), ref_l, atol=1e-4, rtol=1e-5)
+    torch.testing.assert_close(prob.cpu().double(), ref_p, atol=1e-5, rtol=1e-5)
+    out = model(x.to(gpu))
+    assert out.shape == (R, 1)
+
+
+def test_linear_act_variants(gpu):
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(300, 96, generator=g)
+    for n, act in [(256, ops.ACT_RELU), (100, ops.ACT_GELU), (32, ops.ACT_NONE)]:
+        w = torch.randn(n, 96, generator=g) * 0.1
+        b = torch.randn(n, generator=g)
+        y = ops.linear(x.to(gpu), w.to(gpu), b.to(gpu), act)
+        ref = x.double() @ w.double().T + b.double()
+        ref = torch.relu(ref) if act == ops.ACT_RELU else (torch.nn.functional.gelu(ref) if act == ops.ACT_GELU else ref)
+        torch.testing.assert_close(y.cpu().double(), ref, atol=2e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("Q,NI,k", [(50, 3000, 100), (130, 20000, 500), (7, 90, 100), (300, 70000, 10)])
+def test_retrieve_topk_bit_exact_on_dyadic_inputs(gpu, Q, NI, k):
+    """Dyadic inputs make every fp32 dot product exact (no rounding), so the indices must be
+    identical to the oracle's (score desc, index asc) order, ties included."""
+    g = torch.Generator().manual_seed(Q + NI)
+    U = torch.randint(-4, 5, (Q, 128), generator=g).float() / 8.0
+    I = torch.randint(-4, 5, (NI, 128), generator=g).float() / 8.0
+    s, i = ops.retrieve_topk(U.to(gpu), I.to(gpu), k)
+    rs, ri = OR.retrieve_topk(U, I, min(k, NI))
+    kk = min(k, NI)
+    assert torch.equal(i[:, :kk].cpu(), ri)
+    assert torch.equal(s[:, :kk].cpu().double(), rs)
+    if k > NI:
+        assert (i[:, NI:] == -1).all()
+
+
+def test_retrieve_topk_realistic(gpu):
+    g = torch.Generator().manual_seed(1)
+    U = torch.nn.functional.normalize(torch.randn(64, 128, generator=g), dim=1)
+    I = torch.nn.functional.normalize(torch.randn(50000, 128, generator=g), dim=1)
+    s, i = ops.retrieve_topk(U.to(gpu), I.to(gpu), 100)
+    rs, ri = OR.retrieve_topk(U, I, 100)
+    torch.testing.assert_close(s.cpu().double(), rs, atol=1e-6, rtol=0)
+    # indices agree except where the oracle's own neighbouring scores are within fp32 noise
+    mism = (i.cpu() != ri)
+    if mism.any():
+        gaps = (rs[:, :-1] - rs[:, 1:]).abs()
+        assert (gaps[mism[:, :-1]] < 1e-6).all()
+
+
+def test_reranking_system_deepfm(gpu):
+    g = torch.Generator().manual_seed(2)
+    items = torch.nn.functional.normalize(torch.randn(5000, 128, generator=g), dim=1).to(gpu)
+    model = DeepFM([1000] * 39, device=gpu)
+
+    def feats(uv, idx):
+        return torch.stack([(idx * 131 + f * 17) % 1000 for f in range(39)], dim=1)
+
+    sys_ = ReRankingSystem(None, None, model, {}, items, rerank_features=feats)
+    uv = torch.nn.functional.normalize(torch.randn(128, generator=g), dim=0)
+    recs = sys_.recommend(uv, top_k_retrieval=100, final_k=10)
+    assert len(recs) == 10
+    scores = [r["final_score"] for r in recs]
+    assert scores == sorted(scores, reverse=True)
