@@ -41,6 +41,9 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-deepfm", action="store_true", help="skip the DeepFM rerank secondary metric")
+    ap.add_argument("--deepfm-rows", type=int, default=65536)
+    ap.add_argument("--deepfm-vocab", type=int, default=1_000_000)
     ap.add_argument("--blas", default="default", choices=["default", "hipblaslt", "rocblas", "ck"],
                     help="library torch uses for the tower's dense projections")
     return ap.parse_args()
@@ -83,6 +86,47 @@ def cpu_baseline(args, items, cfg):
                        f"{args.cpu_sample_batch} users ({n_valid} valid steps), mean of {args.cpu_steps} steps "
                        f"after 1 warm-up, {dt:.2f} s/step; smaller batch than the GPU run (CPU loss cost "
                        f"grows with N^2)")}
+
+
+def bench_deepfm(args, device):
+    """BASELINE configs[2]: DeepFM forward, 65,536 rows x 39 sparse fields, d=16, per-field
+    vocab 1e6, Zipf(1.1) ids. rows/s with inputs resident in HBM."""
+    import numpy as np
+    from recsys_amd import ops
+    from recsys_amd.temp_model.ranker_skelet import DeepFM
+    R, F, V = args.deepfm_rows, 39, args.deepfm_vocab
+    model = DeepFM([V] * F, device=device)
+    rng = np.random.default_rng(args.seed + 3)
+    x = torch.from_numpy(((rng.zipf(1.1, size=(R, F)) - 1) % V).astype(np.int64)).to(device)
+    for _ in range(3):
+        model.forward_logits(x)
+    torch.cuda.synchronize()
+    iters = 20
+    ops.timing_start()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        model.forward_logits(x)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / iters
+    kt = ops.timing_stop()
+    emb_n, emb_ms = kt.get("deepfm/embed", (1, 0.0))
+    lin_n, lin_ms = kt.get("deepfm/linear", (1, 0.0))
+    dot_n, dot_ms = kt.get("deepfm/linear_dot", (1, 0.0))
+    # algorithmic bytes per row of the gather kernel: 39 ids (8 B) + 39 x (16 + 1) fp32 reads +
+    # the 624-float DNN input row written + 4 B linear/FM term
+    bytes_row = F * 8 + F * 17 * 4 + F * 16 * 4 + 4
+    emb_s = emb_ms / 1e3 / emb_n
+    dnn_flops = 2.0 * R * (F * 16 * 256 + 256 * 128 + 128)
+    dnn_s = (lin_ms / lin_n + dot_ms / dot_n) / 1e3
+    return {"metric": "DeepFM rerank rows/sec (forward, 39 fields, d=16, vocab 1e6/field)",
+            "value": round(R / dt, 1), "unit": "rows/s", "rows": R, "ms_per_batch": round(dt * 1e3, 4),
+            "data": "synthetic Zipf(1.1) ids, deepctr-style N(0,1e-4) init",
+            "gather_fm": {"avg_ms": round(emb_s * 1e3, 4), "bytes_per_row": bytes_row,
+                          "achieved_GBs": round(bytes_row * R / emb_s / 1e9, 1), "peak_GBs": HBM_PEAK_GBS,
+                          "frac": round(bytes_row * R / emb_s / 1e9 / HBM_PEAK_GBS, 4)},
+            "dnn": {"avg_ms": round(dnn_s * 1e3, 4), "achieved_TFLOPs": round(dnn_flops / dnn_s / 1e12, 2),
+                    "peak_TFLOPs": FP32_MFMA_PEAK_TFLOPS,
+                    "frac": round(dnn_flops / dnn_s / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)}}
 
 
 def main():
@@ -201,6 +245,10 @@ def main():
         "kernels": kt,
         "final_loss": round(total_loss, 5),
     }
+    if rank == 0 and world == 1 and not args.no_deepfm:
+        del batches
+        torch.cuda.empty_cache()
+        result["secondary"] = bench_deepfm(args, device)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, items, cfg)
     if rank == 0:
