@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--no-deepfm", action="store_true", help="skip the DeepFM rerank secondary metric")
     ap.add_argument("--deepfm-rows", type=int, default=65536)
     ap.add_argument("--deepfm-vocab", type=int, default=1_000_000)
+    ap.add_argument("--nce-precision", default="bf16x3", choices=["bf16x3", "fp32"],
+                    help="logit precision of the grouped LogQ loss kernels (ops.set_nce_precision)")
     ap.add_argument("--blas", default="default", choices=["default", "hipblaslt", "rocblas", "ck"],
                     help="library torch uses for the tower's dense projections")
     return ap.parse_args()
@@ -143,6 +145,7 @@ def main():
     from recsys_amd import ops, synth
     from recsys_amd.tower_code import v1_usertower_train as TT
     from recsys_amd.tower_code.v1_refine_usertower import SASRecUserTower
+    ops.set_nce_precision(args.nce_precision)
 
     assert args.batch % world == 0, "global batch must divide by the number of GPUs"
     b_loc = args.batch // world
@@ -237,7 +240,7 @@ def main():
                    "distinct_targets_per_batch": n_dist, "dropout": args.dropout,
                    "item_matrix": "frozen" if args.freeze_items else "unfrozen (lr x0.05)",
                    "parallelism": f"dp{world} (users split by rank, RCCL all-gather of ids/z, grad all-reduce)",
-                   "dense_projection_blas": args.blas},
+                   "dense_projection_blas": args.blas, "nce_logit_precision": args.nce_precision},
         "roofline": {"kernel": "nce_grouped_bwd_k<row-owned> (main LogQ loss backward)", "bound": "mfma",
                      "achieved": round(achieved, 2) if achieved else None, "peak": FP32_MFMA_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4) if achieved else None,

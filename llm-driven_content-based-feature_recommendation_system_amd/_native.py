@@ -40,10 +40,10 @@ _SIGS = {
                           c_p, c_p]),
     "rsx_nce_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_f, c_i, c_i, c_i,
                           c_p, c_p, c_p, c_p, c_i, c_p]),
-    "rsx_nce_grouped_fwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_f, c_i, c_p,
-                                  c_p, c_p]),
+    "rsx_nce_grouped_fwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_f, c_i, c_i,
+                                  c_p, c_p, c_p]),
     "rsx_nce_grouped_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64,
-                                  c_i64, c_i64, c_f, c_i, c_i, c_p, c_p, c_p, c_p, c_i, c_p]),
+                                  c_i64, c_i64, c_f, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_i, c_p]),
     "rsx_deepfm_embed": (c_i, [c_p, c_i64, c_i, c_i, c_p, c_p, c_f, c_p, c_p, c_p]),
     "rsx_linear_fwd": (c_i, [c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i64, c_i, c_p, c_p]),
     "rsx_linear_dot_fwd": (c_i, [c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i64, c_i, c_p, c_p, c_p, c_p, c_p]),

@@ -35,6 +35,7 @@ constexpr int kOwnRows = 32 * kWaves;  // owner rows per workgroup
 constexpr int kLdsStride = kD + 4;     // padded row (conflict-free ds_read_b128 columns)
 
 enum : int { F_EXCL_DIAG = 1, F_MASK_K1 = 2, F_MASK_K2 = 4, F_POS = 8 };
+enum : int { RSX_NCE_FP32 = 0, RSX_NCE_BF16X3 = 1 };  // logit/gradient precision of the grouped kernels
 
 struct FwdArgs {
   const float* A;     // [N, lda] owner rows (queries)
@@ -986,6 +987,461 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_bwd_k(GArgs a) {
   }
 }
 
+
+// =====================================================================================
+// bf16x3 form of the grouped kernels (precision RSX_NCE_BF16X3).
+// Every fp32 operand x is split x = hi + lo, hi = bf16(x), lo = bf16(x - hi) (x - hi is exact
+// in fp32), and a product is hi*hi' + hi*lo' + lo*hi' on v_mfma_f32_32x32x16_bf16 with fp32
+// accumulation (bf16 products are exact; the dropped lo*lo' and the rounding of lo leave
+// ~2^-17 relative error per term: max |dot error| 2.7e-6 on unit vectors against 5e-7 for
+// the fp32 MFMA and 1.2e-3 for plain bf16). Both products of the backward use it:
+//   S tile  : streamed rows (A, ds_read_b128 row reads) x owner rows (B, registers)
+//   gradient: G^T (A, straight from the S accumulator: its rows are the k index) x streamed
+//             rows (B, ds_read_b64_tr_b16 transposed reads of the same LDS image)
+// 3 x 32 cycles per 16 k per 32x32 tile instead of 8 x 64 for the fp32 MFMA (5.3x fewer
+// MFMA cycles). The log-sum-exp runs in base 2 (v_exp_f32 without the log2e multiply).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+// [32][128] bf16 image: 320-B rows plus a 16-B skew per 8-row group, i.e. byte offset
+// 320*row + 16*(row>>3) + 2*col. Conflict-free for the row reads (ds_read_b128, lane (c,h)
+// -> row c, chunk 8h+s), the transposed reads (ds_read_b64_tr_b16) and the staging stores
+// (ds_write_b128), and every read address is a per-lane base + an immediate (no per-step
+// address registers); checked with tools/lds_banks.py.
+constexpr int kImgRow = 160;  // bf16 elements per image row
+constexpr int kImgElems = 5120;
+__device__ __forceinline__ int img_off(int row, int col) { return row * kImgRow + 8 * (row >> 3) + col; }
+
+struct X3Tile {
+  __bf16 hi[kImgElems];
+  __bf16 lo[kImgElems];
+};
+
+__device__ __forceinline__ void split8(const float4& a, const float4& b, bf16x8& h, bf16x8& l) {
+  const float f[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const __bf16 hk = (__bf16)f[k];
+    h[k] = hk;
+    l[k] = (__bf16)(f[k] - (float)hk);
+  }
+}
+
+// owner row (dims 64h .. 64h+63 on lane half h) -> hi/lo fragments of k-steps s = 0..7
+// (fragment s, element j = dim 64h + 8s + j: the chunk 8h + s of the streamed row reads)
+__device__ __forceinline__ void load_owner_x3(bf16x8 (&uh)[8], bf16x8 (&ul)[8], const float* base, int64_t row,
+                                              int64_t ld, bool ok, int h) {
+  const float4* src = reinterpret_cast<const float4*>(base + (ok ? row : 0) * ld + h * 64);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
+    if (ok) {
+      v0 = src[2 * s];
+      v1 = src[2 * s + 1];
+    }
+    split8(v0, v1, uh[s], ul[s]);
+  }
+}
+
+// staging of one 32-row tile: thread tid holds row tid>>3, chunks tid&7 and 8+(tid&7)
+struct X3Stage {
+  float4 v[4];
+  __device__ __forceinline__ void load(const float* base, int64_t row, int64_t ld, bool ok, int tid) {
+    if (ok) {
+      const float* r = base + row * ld + (tid & 7) * 8;
+      const float4* s0 = reinterpret_cast<const float4*>(r);
+      const float4* s1 = reinterpret_cast<const float4*>(r + 64);
+      v[0] = s0[0]; v[1] = s0[1]; v[2] = s1[0]; v[3] = s1[1];
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) v[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  __device__ __forceinline__ void store(X3Tile& t, int tid) const {
+    const int row = tid >> 3, ch = tid & 7;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      bf16x8 hh, ll;
+      split8(v[2 * k], v[2 * k + 1], hh, ll);
+      const int off = img_off(row, 64 * k + 8 * ch);
+      *reinterpret_cast<bf16x8*>(&t.hi[off]) = hh;
+      *reinterpret_cast<bf16x8*>(&t.lo[off]) = ll;
+    }
+  }
+};
+
+// S tile: acc[r] = <streamed row tile_row(r,h), owner row c> (owner on the lane).
+// The next k-step's fragments are read before this step's MFMAs (LDS latency under MFMA);
+// the scheduling barrier keeps the compiler from hoisting more reads (VGPR budget).
+__device__ __forceinline__ f32x16 dots_x3(const X3Tile& t, int c, int h, const bf16x8 (&uh)[8],
+                                          const bf16x8 (&ul)[8]) {
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+  const int base = img_off(c, 64 * h);
+  bf16x8 ah = *reinterpret_cast<const bf16x8*>(&t.hi[base]);
+  bf16x8 al = *reinterpret_cast<const bf16x8*>(&t.lo[base]);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    bf16x8 nh = ah, nl = al;
+    if (s < 7) {
+      nh = *reinterpret_cast<const bf16x8*>(&t.hi[base + 8 * (s + 1)]);
+      nl = *reinterpret_cast<const bf16x8*>(&t.lo[base + 8 * (s + 1)]);
+    }
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, uh[s], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, ul[s], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, uh[s], acc, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    ah = nh;
+    al = nl;
+  }
+  return acc;
+}
+
+// gacc[nb] += G^T X over the tile: G = the 32x32 gradient tile (acc layout: streamed row
+// tile_row(r,h) in register r, owner on the lane). k-step ks takes registers 8ks..8ks+7, i.e.
+// streamed rows 16ks + 8(j>>2) + 4h + (j&3); the B fragment is those rows of dims 32nb + c,
+// two transposed 4-row reads per image. Steps (ks, nb) are software-pipelined by one.
+__device__ __forceinline__ void grad_x3(f32x16 (&gacc)[4], const f32x16& g, const X3Tile& t, int lane) {
+  const int q = (lane >> 2) & 3, p = lane & 3, h = lane >> 5, cb = (lane >> 4) & 1;
+  bf16x8 gh[2], gl[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float x = g[8 * ks + j];
+      const __bf16 hj = (__bf16)x;
+      gh[ks][j] = hj;
+      gl[ks][j] = (__bf16)(x - (float)hj);
+    }
+  const int base = img_off(4 * h + q, 16 * cb + 4 * p);  // + img_off(16ks + 8half, 32nb) - img_off(0,0)
+  auto rd = [&](const __bf16* img, int step, bf16x8& out) {
+    const int ks = step >> 2, nb = step & 3;
+    const int o0 = base + img_off(16 * ks, 32 * nb), o1 = base + img_off(16 * ks + 8, 32 * nb);
+    const bf16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(&img[o0]));
+    const bf16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(&img[o1]));
+    out = __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+  bf16x8 bh, bl;
+  rd(t.hi, 0, bh);
+  rd(t.lo, 0, bl);
+#pragma unroll
+  for (int step = 0; step < 8; ++step) {
+    bf16x8 nh = bh, nl = bl;
+    if (step < 7) {
+      rd(t.hi, step + 1, nh);
+      rd(t.lo, step + 1, nl);
+    }
+    const int ks = step >> 2, nb = step & 3;
+    gacc[nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gl[ks], bh, gacc[nb], 0, 0, 0);
+    gacc[nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gh[ks], bl, gacc[nb], 0, 0, 0);
+    gacc[nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gh[ks], bh, gacc[nb], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    bh = nh;
+    bl = nl;
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void nce_grouped_fwd_x3_k(GArgs a) {
+  __shared__ __attribute__((aligned(16))) X3Tile sT[2];
+  __shared__ __attribute__((aligned(16))) float sB2[2][kTile];   // bias_d * log2e (0 past the split)
+  __shared__ __attribute__((aligned(16))) float sCnt[2][kTile];  // c_d (0 past the split)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, c = lane & 31;
+  int split, rb;
+  remap_block(a.nsplit, split, rb);
+  const int64_t i = (int64_t)rb * kOwnRows + wave * 32 + c;
+  const bool row_ok = i < a.N;
+  bf16x8 uh[8], ul[8];
+  load_owner_x3(uh, ul, a.A, i, a.lda, row_ok, h);
+  const int64_t j_begin = (int64_t)split * a.span;
+  int64_t j_end = j_begin + a.span;
+  if (j_end > a.M) j_end = a.M;
+  int di = -1, p = 0, e = 0, next = 0x7fffffff;
+  if (row_ok) {
+    di = a.row_col[i];
+    p = a.row_beg[i];
+    e = a.row_end[i];
+    p = lower_bound_i(a.exc_cols, p, e, j_begin);
+    next = (p < e) ? a.exc_cols[p] : 0x7fffffff;
+  }
+  const float it2 = a.inv_tau * kLog2e;
+  float m = -INFINITY, l = 0.0f;  // base 2
+  X3Stage stg;
+  float stg_b = 0.0f, stg_c = 0.0f;
+  auto gload = [&](int64_t j0) {
+    const int64_t j = j0 + (tid >> 3);
+    stg.load(a.B, j, a.ldb, j < j_end, tid);
+    if (tid < kTile) {
+      const int64_t jj = j0 + tid;
+      const bool ok = jj < j_end;
+      stg_b = (ok && a.bias) ? a.bias[jj] : 0.0f;  // raw: no math on a load in flight
+      stg_c = ok ? a.colcnt[jj] : 0.0f;
+    }
+  };
+  auto lstore = [&](int buf) {
+    stg.store(sT[buf], tid);
+    if (tid < kTile) {
+      sB2[buf][tid] = stg_b * kLog2e;
+      sCnt[buf][tid] = stg_c;
+    }
+  };
+  if (j_begin < j_end) {
+    gload(j_begin);
+    lstore(0);
+    __syncthreads();
+    int cur = 0;
+    for (int64_t j0 = j_begin; j0 < j_end; j0 += kTile) {
+      const bool has_next = j0 + kTile < j_end;
+      if (has_next) gload(j0 + kTile);
+      const f32x16 acc = dots_x3(sT[cur], c, h, uh, ul);
+      float w[16], v[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int tr = tile_row(r, h);
+        w[r] = sCnt[cur][tr];
+        v[r] = fmaf(acc[r], it2, -sB2[cur][tr]);
+      }
+      if ((int64_t)next < j0 + kTile) {
+        // rare: some of the user's own targets (d(i) among them) fall in this tile
+        int q = p;
+        while (q < e && (int64_t)a.exc_cols[q] < j0 + kTile) ++q;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int64_t d = j0 + tile_row(r, h);
+          int n = 0;
+          for (int k = p; k < q; ++k) n += (a.exc_cols[k] == (int)d);
+          if (d < j_end) w[r] = (d == di) ? 1.0f : w[r] - (float)n;
+        }
+        p = q;
+        next = (p < e) ? a.exc_cols[p] : 0x7fffffff;
+      }
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (!(w[r] > 0.0f)) v[r] = -INFINITY;
+        tmax = fmaxf(tmax, v[r]);
+      }
+      if (!row_ok) tmax = -INFINITY;
+      if (tmax > m) {
+        l = (m == -INFINITY) ? 0.0f : l * __builtin_amdgcn_exp2f(m - tmax);
+        m = tmax;
+      }
+      if (m != -INFINITY) {
+        float t = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t = fmaf(w[r], __builtin_amdgcn_exp2f(v[r] - m), t);  // w >= 0
+        l += t;
+      }
+      // buffer cur^1 was last read in the previous tile, which every wave finished before the
+      // barrier that ended it: one barrier per tile
+      if (has_next) lstore(cur ^ 1);
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+  const float m2 = __shfl_xor(m, 32, 64);
+  const float l2 = __shfl_xor(l, 32, 64);
+  const float mm = fmaxf(m, m2);
+  float ll = 0.0f;
+  if (mm != -INFINITY) {
+    if (m != -INFINITY) ll += l * __builtin_amdgcn_exp2f(m - mm);
+    if (m2 != -INFINITY) ll += l2 * __builtin_amdgcn_exp2f(m2 - mm);
+  }
+  if (h == 0 && row_ok) {
+    const int64_t stride = (int64_t)a.nsplit * a.N;
+    const int64_t o = (int64_t)split * a.N + i;
+    a.part[o] = (mm == -INFINITY) ? -INFINITY : mm * kLn2;  // natural-log max, same sum
+    a.part[stride + o] = ll;
+    a.part[2 * stride + o] = 0.0f;
+    a.part[3 * stride + o] = 0.0f;
+  }
+}
+
+template <bool ROW_OWNED>
+__global__ __launch_bounds__(256, 2) void nce_grouped_bwd_x3_k(GArgs a) {
+  __shared__ __attribute__((aligned(16))) X3Tile sT[2];
+  __shared__ __attribute__((aligned(16))) float sM0[2][kTile];  // rows: bias_d*log2e | cols: lse_i*log2e (+inf past the split)
+  __shared__ __attribute__((aligned(16))) float sM1[2][kTile];  // rows: c_d (0 past the split) | cols: unused
+  __shared__ __attribute__((aligned(16))) int sM2[2][kTile];    // cols: d(i)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, c = lane & 31;
+  int split, ob;
+  remap_block(a.nsplit, split, ob);
+  const int64_t n_own = ROW_OWNED ? a.N : a.M;
+  const int64_t n_str = ROW_OWNED ? a.M : a.N;
+  const float* own = ROW_OWNED ? a.A : a.B;
+  const float* str = ROW_OWNED ? a.B : a.A;
+  const int64_t ld_own = ROW_OWNED ? a.lda : a.ldb;
+  const int64_t ld_str = ROW_OWNED ? a.ldb : a.lda;
+  const float gs = a.gout[0] * a.inv_tau;
+  const float it2 = a.inv_tau * kLog2e;
+  const int64_t o = (int64_t)ob * kOwnRows + wave * 32 + c;
+  const bool own_ok = o < n_own;
+  bf16x8 uh[8], ul[8];
+  load_owner_x3(uh, ul, own, o, ld_own, own_ok, h);
+  const int64_t s_begin = (int64_t)split * a.span;
+  int64_t s_end = s_begin + a.span;
+  if (s_end > n_str) s_end = n_str;
+
+  float o_m2 = 0.0f, o_cnt = 0.0f;  // rows: lse_o*log2e | cols: bias_o*log2e, c_o
+  int o_d = -1, p = 0, e = 0, next = 0x7fffffff;
+  if (own_ok) {
+    if (ROW_OWNED) {
+      o_m2 = a.lse[o] * kLog2e;
+      o_d = a.row_col[o];
+      p = a.row_beg[o];
+      e = a.row_end[o];
+      p = lower_bound_i(a.exc_cols, p, e, s_begin);
+      next = (p < e) ? a.exc_cols[p] : 0x7fffffff;
+    } else {
+      o_m2 = a.bias ? a.bias[o] * kLog2e : 0.0f;
+      o_cnt = a.colcnt[o];
+      p = a.col_beg[o];
+      e = a.col_end[o];
+      p = lower_bound_i(a.exc_e, p, e, s_begin + 1);  // first user range ending after s_begin
+    }
+  }
+  // cols: ranges [p, q) intersect the current tile; e_first = end of range p (if p < q),
+  // s_next = start of range q: the per-tile window update is register compares only
+  int q = p, e_first = 0, s_next = 0x7fffffff;
+  if (!ROW_OWNED && own_ok && q < e) s_next = a.exc_s[q];
+
+  f32x16 gacc[4];
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) gacc[kb][r] = 0.0f;
+
+  X3Stage stg;
+  float stg0 = 0.0f, stg1 = 0.0f;
+  int stg2 = 0;
+  auto gload = [&](int64_t s0) {
+    const int64_t sidx = s0 + (tid >> 3);
+    stg.load(str, sidx, ld_str, sidx < s_end, tid);
+    if (tid < kTile) {
+      const int64_t ss = s0 + tid;
+      const bool ok = ss < s_end;
+      // raw loads only (math on a value in flight would wait for the whole tile load here)
+      if (ROW_OWNED) {
+        stg0 = (ok && a.bias) ? a.bias[ss] : 0.0f;
+        stg1 = ok ? a.colcnt[ss] : 0.0f;
+      } else {
+        stg0 = ok ? a.lse[ss] : INFINITY;  // past the split: 2^(x - inf) = 0
+        stg1 = 0.0f;
+        stg2 = ok ? a.row_col[ss] : -2;
+      }
+    }
+  };
+  auto lstore = [&](int buf) {
+    stg.store(sT[buf], tid);
+    if (tid < kTile) {
+      sM0[buf][tid] = stg0 * kLog2e;
+      sM1[buf][tid] = stg1;
+      sM2[buf][tid] = stg2;
+    }
+  };
+
+  if (s_begin < s_end) {
+    gload(s_begin);
+    lstore(0);
+    __syncthreads();
+    int cur = 0;
+    for (int64_t s0 = s_begin; s0 < s_end; s0 += kTile) {
+      const bool has_next = s0 + kTile < s_end;
+      if (has_next) gload(s0 + kTile);
+      f32x16 acc = dots_x3(sT[cur], c, h, uh, ul);
+      // acc -> g = w * 2^(S*log2e - (bias + lse)*log2e) (- 1 on the label), in place
+      if (ROW_OWNED) {
+        if ((int64_t)next >= s0 + kTile) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int tr = tile_row(r, h);
+            acc[r] = sM1[cur][tr] * __builtin_amdgcn_exp2f(fmaf(acc[r], it2, -(sM0[cur][tr] + o_m2)));
+          }
+        } else {  // rare: the user's own targets (d(o) among them) fall in this tile
+          int q = p;
+          while (q < e && (int64_t)a.exc_cols[q] < s0 + kTile) ++q;
+          float n[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) n[r] = 0.0f;
+          for (int k = p; k < q; ++k) {
+            const int tk = (int)(a.exc_cols[k] - s0);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) n[r] += (tk == tile_row(r, h)) ? 1.0f : 0.0f;
+          }
+          const int tl = ((int64_t)o_d < s_end) ? (int)(o_d - s0) : -1;  // label column, if this split owns it
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int tr = tile_row(r, h);
+            const bool lab = tr == tl;
+            const float wr = lab ? 1.0f : sM1[cur][tr] - n[r];
+            const float x = fmaf(acc[r], it2, -(sM0[cur][tr] + o_m2));
+            acc[r] = (wr > 0.0f ? wr * __builtin_amdgcn_exp2f(x) : 0.0f) - (lab ? 1.0f : 0.0f);
+          }
+          p = q;
+          next = (p < e) ? a.exc_cols[p] : 0x7fffffff;
+        }
+      } else {
+        // user row ranges holding target o that intersect this tile: [p, q)
+        while (p < q && (int64_t)e_first <= s0) {
+          ++p;
+          if (p < q) e_first = a.exc_e[p];
+        }
+        while ((int64_t)s_next < s0 + kTile) {
+          if (p == q) e_first = a.exc_e[q];
+          ++q;
+          s_next = (q < e) ? a.exc_s[q] : 0x7fffffff;
+        }
+        if (q == p) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int tr = tile_row(r, h);
+            acc[r] = o_cnt * __builtin_amdgcn_exp2f(fmaf(acc[r], it2, -(o_m2 + sM0[cur][tr])));
+          }
+        } else {
+          float n[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) n[r] = 0.0f;
+          for (int k = p; k < q; ++k) {
+            const int ks = (int)(a.exc_s[k] - s0), ke = (int)(a.exc_e[k] - s0);
+            const float nk = (float)a.exc_n[k];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) n[r] += (tile_row(r, h) >= ks && tile_row(r, h) < ke) ? nk : 0.0f;
+          }
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int tr = tile_row(r, h);
+            const bool lab = sM2[cur][tr] == (int)o;
+            const float wr = lab ? 1.0f : o_cnt - n[r];
+            const float x = fmaf(acc[r], it2, -(o_m2 + sM0[cur][tr]));
+            acc[r] = (wr > 0.0f ? wr * __builtin_amdgcn_exp2f(x) : 0.0f) - (lab ? 1.0f : 0.0f);
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = own_ok ? gs * acc[r] : 0.0f;
+      grad_x3(gacc, acc, sT[cur], lane);
+      if (has_next) lstore(cur ^ 1);  // cur^1: read in the previous tile, fenced by its barrier
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+  const int64_t own_base = (int64_t)ob * kOwnRows + wave * 32;
+  float* dst = a.dout + (int64_t)split * n_own * kD;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int64_t orow = own_base + tile_row(r, h);
+    if (orow < n_own) {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) dst[orow * kD + kb * 32 + c] = gacc[kb][r];
+    }
+  }
+}
+
 }  // namespace
 
 RSX_API int64_t rsx_nce_workspace_floats(int64_t N, int64_t M, int nsplit_fwd, int nsplit_bwd) {
@@ -1109,9 +1565,10 @@ RSX_API int rsx_nce_bwd(const float* A, const float* B, const float* bias, const
 
 RSX_API int rsx_nce_grouped_fwd(const float* A, const float* B, const float* bias, const float* colcnt,
                                 const int* row_col, const int* row_beg, const int* row_end, const int* exc_cols,
-                                int64_t N, int64_t D, int64_t lda, int64_t ldb, float tau, int nsplit, float* ws,
-                                float* out2, void* stream) {
+                                int64_t N, int64_t D, int64_t lda, int64_t ldb, float tau, int precision, int nsplit,
+                                float* ws, float* out2, void* stream) {
   RSX_ARG(A && B && colcnt && row_col && row_beg && row_end && exc_cols && ws && out2, "null tensor");
+  RSX_ARG(precision == RSX_NCE_FP32 || precision == RSX_NCE_BF16X3, "precision must be 0 (fp32) or 1 (bf16x3)");
   RSX_ARG(nsplit >= 8 && nsplit <= 64 && nsplit % 8 == 0, "nsplit must be a multiple of 8 in [8,64]");
   RSX_ARG(lda % 4 == 0 && ldb % 4 == 0 && lda >= kD && ldb >= kD, "row strides must be >=128 and multiples of 4");
   RSX_ARG(((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0, "A/B must be 16-byte aligned");
@@ -1135,7 +1592,8 @@ RSX_API int rsx_nce_grouped_fwd(const float* A, const float* B, const float* bia
   if (g.span < kTile) g.span = kTile;
   g.part = part;
   const int blocks = (int)(((N + kOwnRows - 1) / kOwnRows) * nsplit);
-  hipLaunchKernelGGL(nce_grouped_fwd_k, dim3(blocks), dim3(256), 0, st, g);
+  if (precision == RSX_NCE_BF16X3) hipLaunchKernelGGL(nce_grouped_fwd_x3_k, dim3(blocks), dim3(256), 0, st, g);
+  else hipLaunchKernelGGL(nce_grouped_fwd_k, dim3(blocks), dim3(256), 0, st, g);
   RSX_LAUNCHED();
   hipLaunchKernelGGL(nce_grouped_merge_k, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, A, B, bias, row_col, N,
                      lda, ldb, g.inv_tau, nsplit, part, lse, row_loss, row_valid);
@@ -1149,10 +1607,11 @@ RSX_API int rsx_nce_grouped_bwd(const float* A, const float* B, const float* bia
                                 const int* row_col, const int* row_beg, const int* row_end, const int* exc_cols,
                                 const int* col_beg, const int* col_end, const int* exc_s, const int* exc_e,
                                 const int* exc_n, int64_t N, int64_t D, int64_t lda, int64_t ldb, float tau,
-                                int nsplit_fwd, int nsplit, const float* gout, float* ws, float* dA, float* dB,
+                                int precision, int nsplit_fwd, int nsplit, const float* gout, float* ws, float* dA, float* dB,
                                 int accumulate, void* stream) {
   RSX_ARG(gout != nullptr && ws != nullptr, "gout/ws required");
   RSX_ARG(nsplit >= 8 && nsplit <= 64 && nsplit % 8 == 0, "nsplit must be a multiple of 8 in [8,64]");
+  RSX_ARG(precision == RSX_NCE_FP32 || precision == RSX_NCE_BF16X3, "precision must be 0 (fp32) or 1 (bf16x3)");
   RSX_ARG(!dB || (col_beg && col_end && exc_s && exc_e && exc_n), "column exception lists required for dB");
   hipStream_t st = (hipStream_t)stream;
   if (N == 0) return 0;
@@ -1179,7 +1638,10 @@ RSX_API int rsx_nce_grouped_bwd(const float* A, const float* B, const float* bia
     g.span = round_up((n_str + nsplit - 1) / nsplit, kTile);
     if (g.span < kTile) g.span = kTile;
     const int blocks = (int)(((n_own + kOwnRows - 1) / kOwnRows) * nsplit);
-    if (row_owned) hipLaunchKernelGGL(nce_grouped_bwd_k<true>, dim3(blocks), dim3(256), 0, st, g);
+    const bool x3 = precision == RSX_NCE_BF16X3;
+    if (row_owned && x3) hipLaunchKernelGGL(nce_grouped_bwd_x3_k<true>, dim3(blocks), dim3(256), 0, st, g);
+    else if (x3) hipLaunchKernelGGL(nce_grouped_bwd_x3_k<false>, dim3(blocks), dim3(256), 0, st, g);
+    else if (row_owned) hipLaunchKernelGGL(nce_grouped_bwd_k<true>, dim3(blocks), dim3(256), 0, st, g);
     else hipLaunchKernelGGL(nce_grouped_bwd_k<false>, dim3(blocks), dim3(256), 0, st, g);
     RSX_LAUNCHED();
     const int64_t total4 = n_own * kD / 4;

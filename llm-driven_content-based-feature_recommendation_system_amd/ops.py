@@ -5,6 +5,8 @@ There is no CPU path: a non-ROCm tensor raises.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _native as N
@@ -16,6 +18,27 @@ NCE_SUPCON = 9
 
 _NSPLIT_FWD = 8
 _NSPLIT_BWD = 8
+
+# Logit precision of the grouped (live LogQ) loss kernels, include/recsys_amd.h RSX_NCE_*:
+# "bf16x3" = hi/lo bf16 split on the bf16 MFMA (max |dot error| ~3e-6 on unit vectors; the
+# reference computes these logits in fp16 under AMP), "fp32" = fp32-input MFMA.
+NCE_PRECISIONS = {"fp32": 0, "bf16x3": 1}
+_nce_precision = os.environ.get("RSX_NCE_PRECISION", "bf16x3")
+if _nce_precision not in NCE_PRECISIONS:
+    raise ValueError(f"RSX_NCE_PRECISION must be one of {sorted(NCE_PRECISIONS)}")
+
+
+def set_nce_precision(mode: str) -> str:
+    """Set the grouped-loss logit precision ("fp32" | "bf16x3"); returns the previous mode."""
+    global _nce_precision
+    if mode not in NCE_PRECISIONS:
+        raise ValueError(f"precision must be one of {sorted(NCE_PRECISIONS)}")
+    prev, _nce_precision = _nce_precision, mode
+    return prev
+
+
+def nce_precision() -> str:
+    return _nce_precision
 
 
 def next_seed() -> int:
@@ -317,7 +340,7 @@ class TargetGroups:
 
 class _NCEGrouped(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, A, B, bias, grp, tau, tag):
+    def forward(ctx, A, B, bias, grp, tau, tag, prec):
         N.ensure_device(A)
         A = _c(A)
         B = _c(B)
@@ -328,12 +351,12 @@ class _NCEGrouped(torch.autograd.Function):
         with timed(f"{tag}/nce_fwd"):
             rc = N.lib().rsx_nce_grouped_fwd(N.ptr(A), N.ptr(B), N.ptr(bias), N.ptr(grp.colcnt), N.ptr(grp.row_col),
                                              N.ptr(grp.row_beg), N.ptr(grp.row_end), N.ptr(grp.exc_cols), n, d,
-                                             A.stride(0), B.stride(0), tau, _NSPLIT_FWD, N.ptr(ws), N.ptr(out2),
-                                             N.stream())
+                                             A.stride(0), B.stride(0), tau, prec, _NSPLIT_FWD, N.ptr(ws),
+                                             N.ptr(out2), N.stream())
         N.check(rc, "nce_grouped_fwd")
         ctx.save_for_backward(A, B, bias, ws)
         ctx.grp = grp
-        ctx.cfg = (n, d, tau, tag)
+        ctx.cfg = (n, d, tau, tag, prec)
         cnt = out2[1]
         ctx.mark_non_differentiable(cnt)
         return out2[0], cnt
@@ -342,11 +365,11 @@ class _NCEGrouped(torch.autograd.Function):
     def backward(ctx, g, _gcnt):
         A, B, bias, ws = ctx.saved_tensors
         grp = ctx.grp
-        n, d, tau, tag = ctx.cfg
+        n, d, tau, tag, prec = ctx.cfg
         g = _c(g.reshape(1).to(torch.float32))
         args = (N.ptr(A), N.ptr(B), N.ptr(bias), N.ptr(grp.colcnt), N.ptr(grp.row_col), N.ptr(grp.row_beg),
                 N.ptr(grp.row_end), N.ptr(grp.exc_cols), N.ptr(grp.col_beg), N.ptr(grp.col_end), N.ptr(grp.exc_s),
-                N.ptr(grp.exc_e), N.ptr(grp.exc_n), n, d, A.stride(0), B.stride(0), tau, _NSPLIT_FWD, _NSPLIT_BWD,
+                N.ptr(grp.exc_e), N.ptr(grp.exc_n), n, d, A.stride(0), B.stride(0), tau, prec, _NSPLIT_FWD, _NSPLIT_BWD,
                 N.ptr(g), N.ptr(ws))
         dA = dB = None
         if ctx.needs_input_grad[0]:
@@ -359,15 +382,17 @@ class _NCEGrouped(torch.autograd.Function):
             with timed(f"{tag}/nce_bwd_cols"):
                 rc = N.lib().rsx_nce_grouped_bwd(*args, None, N.ptr(dB), 0, N.stream())
             N.check(rc, "nce_grouped_bwd(cols)")
-        return dA, dB, None, None, None, None
+        return dA, dB, None, None, None, None, None
 
 
-def nce_grouped_sum(A, B_distinct, bias, groups: TargetGroups, tau=0.1, tag="nce"):
+def nce_grouped_sum(A, B_distinct, bias, groups: TargetGroups, tau=0.1, tag="nce", precision=None):
     """(sum of row losses, N) of the live LogQ loss with same-item / same-user masking, with
-    the columns given as the distinct targets (B_distinct[d] = normalised item groups.uniq[d])."""
+    the columns given as the distinct targets (B_distinct[d] = normalised item groups.uniq[d]).
+    precision: "fp32" | "bf16x3" | None (= set_nce_precision / RSX_NCE_PRECISION)."""
     if bias is not None:
         bias = _c(bias.to(torch.float32))
-    return _NCEGrouped.apply(A, B_distinct, bias, groups, float(tau), str(tag))
+    prec = NCE_PRECISIONS[precision or _nce_precision]
+    return _NCEGrouped.apply(A, B_distinct, bias, groups, float(tau), str(tag), prec)
 
 
 # ----------------------------------------------------------------------------------------

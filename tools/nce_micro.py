@@ -1,0 +1,62 @@
+"""Micro-benchmark of the grouped LogQ-loss kernels at the bench workload's shape.
+
+Builds one global batch exactly as bench.py does (4096 users, H&M-shaped lengths, Zipf(1.0)
+targets), with random L2-normalised step embeddings in place of the tower output, and runs
+the grouped fwd + both backward passes. Prints per-kernel average ms. Meant to be run under
+rocprofv3 (kernel trace / PMC passes) so a profile isolates these kernels.
+
+  python tools/nce_micro.py --iters 20 --precision bf16x3
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import recsys_amd  # noqa: E402,F401
+from recsys_amd import ops, synth  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "fp32"])
+    ap.add_argument("--seed", type=int, default=0)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    items = synth.make_items(seed=args.seed)
+    b = synth.make_batch(items, args.batch, seed=args.seed + 100)
+    valid = ~b["padding_mask"]
+    t = b["target_ids"][valid].to(dev)
+    users = torch.arange(args.batch).unsqueeze(1).expand_as(valid)[valid].to(dev)
+    n = t.numel()
+    g = torch.Generator(device="cpu").manual_seed(args.seed)
+    U = F.normalize(torch.randn(n, 128, generator=g), dim=1).to(dev).requires_grad_()
+    W = items.pretrained.to(dev)
+    grp = ops.TargetGroups(t, users)
+    B = W[grp.uniq].contiguous().requires_grad_()
+    bias = items.log_q.to(dev)[grp.uniq].contiguous()
+    for i in range(3):
+        s, c = ops.nce_grouped_sum(U, B, bias, grp, tau=0.1, tag="micro", precision=args.precision)
+        s.backward()
+    torch.cuda.synchronize()
+    ops.timing_start()
+    for i in range(args.iters):
+        s, c = ops.nce_grouped_sum(U, B, bias, grp, tau=0.1, tag="micro", precision=args.precision)
+        s.backward()
+    torch.cuda.synchronize()
+    kt = ops.timing_stop()
+    out = {"rows": n, "distinct_targets": int(grp.uniq.numel()), "precision": args.precision,
+           "loss_sum": float(s.item()),
+           "avg_ms": {k: round(ms / max(cnt, 1), 4) for k, (cnt, ms) in sorted(kt.items())}}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
