@@ -131,6 +131,16 @@ int rsx_nce_grouped_bwd(const float* A, const float* B, const float* bias, const
                         int nsplit, const float* gout, float* ws, float* dA, float* dB, int accumulate,
                         void* stream);
 
+/* ---- weight gradient of token-level linear layers ---------------------------------------
+ * dW[n][k] (+)= sum_t dY[t][n] X[t][k], db[n] (+)= sum_t dY[t][n] (db nullable), fp32 MFMA,
+ * split over tokens with a deterministic partial reduction. Replaces autograd's weight-grad
+ * GEMM of every per-token nn.Linear in the user tower's step (tower_code/v1_refine_usertower.py
+ * :447-510 — item_proj, in_proj/out_proj/linear1/linear2 of both encoder layers, output_proj).
+ * N, K multiples of 16; ws >= rsx_linear_wgrad_workspace_floats(T, N, K) floats. */
+int64_t rsx_linear_wgrad_workspace_floats(int64_t T, int64_t N, int64_t K);
+int rsx_linear_wgrad(const float* dY, int64_t ldy, const float* X, int64_t ldx, int64_t T, int64_t N, int64_t K,
+                     float* dW, int64_t ldw, float* db, int accumulate, float* ws, int64_t ws_floats, void* stream);
+
 /* ---- A14: retrieval top-k ------------------------------------------------------------
  * scores = U I^T (fp32 MFMA, never materialised), per query the k best items sorted by
  * (score desc, index asc). Replaces `scores = matmul(user, items.T); topk(k)` at

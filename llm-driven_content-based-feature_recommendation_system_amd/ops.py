@@ -396,6 +396,56 @@ def nce_grouped_sum(A, B_distinct, bias, groups: TargetGroups, tau=0.1, tag="nce
 
 
 # ----------------------------------------------------------------------------------------
+# Token-level linear layer: forward/dX on the BLAS GEMM, dW/db on rsx_linear_wgrad (split-K)
+def linear_wgrad(dy, x, weight_shape, need_bias, tag="wgrad"):
+    """(dW [N, K], db [N] or None) for dy [T, N], x [T, K] (fp32, contiguous)."""
+    N.ensure_device(dy)
+    dy = _c(dy)
+    x = _c(x)
+    t, n = dy.shape
+    k = x.shape[1]
+    assert (n, k) == tuple(weight_shape)
+    nws = N.lib().rsx_linear_wgrad_workspace_floats(t, n, k)
+    ws = torch.empty(nws, device=dy.device, dtype=torch.float32)
+    dw = torch.empty(n, k, device=dy.device, dtype=torch.float32)
+    db = torch.empty(n, device=dy.device, dtype=torch.float32) if need_bias else None
+    with timed(tag):
+        rc = N.lib().rsx_linear_wgrad(N.ptr(dy), dy.stride(0), N.ptr(x), x.stride(0), t, n, k, N.ptr(dw), dw.stride(0),
+                                      N.ptr(db), 0, N.ptr(ws), nws, N.stream())
+    N.check(rc, "linear_wgrad")
+    return dw, db
+
+
+class _TokLinear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return torch.nn.functional.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        dy = _c(dy)
+        dx = dy @ weight if ctx.needs_input_grad[0] else None
+        dw = db = None
+        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+            dw, db = linear_wgrad(dy, x, weight.shape, ctx.has_bias and ctx.needs_input_grad[2])
+        return dx, dw, db
+
+
+def linear_tok(x, weight, bias=None):
+    """F.linear over a token axis (x [..., K]) whose weight/bias gradients come from the
+    split-K rsx_linear_wgrad kernel instead of the library GEMM (T >> N, K)."""
+    shp = x.shape
+    x2 = _c(x.reshape(-1, shp[-1]))
+    if x2.shape[0] == 0 or shp[-1] % 16 or weight.shape[0] % 16:
+        return torch.nn.functional.linear(x, weight, bias)
+    y = _TokLinear.apply(x2, weight, bias)
+    return y.reshape(*shp[:-1], weight.shape[0])
+
+
+# ----------------------------------------------------------------------------------------
 # A16: DeepFM forward (inference)
 ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
 

@@ -92,13 +92,13 @@ class SASRecUserTower(nn.Module):
     def _encoder_layer(self, layer: nn.TransformerEncoderLayer, x, key_pad, p, seg_off=None):
         sa = layer.self_attn
         h = F.layer_norm(x, (self.d_model,), layer.norm1.weight, layer.norm1.bias, layer.norm1.eps)
-        qkv = F.linear(h, sa.in_proj_weight, sa.in_proj_bias)
+        qkv = ops.linear_tok(h, sa.in_proj_weight, sa.in_proj_bias)
         a = ops.mha(qkv, key_pad, sa.num_heads, causal=True, p_drop=p, seg_off=seg_off)
-        a = F.linear(a, sa.out_proj.weight, sa.out_proj.bias)
+        a = ops.linear_tok(a, sa.out_proj.weight, sa.out_proj.bias)
         x = x + F.dropout(a, p, self.training)
         h = F.layer_norm(x, (self.d_model,), layer.norm2.weight, layer.norm2.bias, layer.norm2.eps)
-        f = F.linear(F.dropout(F.gelu(F.linear(h, layer.linear1.weight, layer.linear1.bias)), p, self.training),
-                     layer.linear2.weight, layer.linear2.bias)
+        f = ops.linear_tok(F.dropout(F.gelu(ops.linear_tok(h, layer.linear1.weight, layer.linear1.bias)), p,
+                                     self.training), layer.linear2.weight, layer.linear2.bias)
         return x + F.dropout(f, p, self.training)
 
     def forward(self, pretrained_vecs, item_ids, time_bucket_ids, type_ids, color_ids, graphic_ids, section_ids,
@@ -164,7 +164,7 @@ class SASRecUserTower(nn.Module):
         p = self.dropout_rate if self.training else 0.0
         s_g = torch.sigmoid(self.seq_gate) * self._seq_gate_mask
         u_g = torch.sigmoid(self.static_gate)
-        base = F.linear(pretrained_tok, self.item_proj.weight, self.item_proj.bias)
+        base = ops.linear_tok(pretrained_tok, self.item_proj.weight, self.item_proj.bias)
         x = ops.seq_embed(
             base, tok_ids,
             [self.item_id_emb.weight, self.time_emb.weight, self.type_emb.weight, self.color_emb.weight,
@@ -178,9 +178,9 @@ class SASRecUserTower(nn.Module):
         lin0, ln, lin3 = self.output_proj[0], self.output_proj[1], self.output_proj[3]
         D = self.d_model
         prof = F.linear(profile, lin0.weight[:, D:], lin0.bias)
-        h = F.linear(x, lin0.weight[:, :D]) + ops.gather_rows(prof, packed.tok_user)
+        h = ops.linear_tok(x, lin0.weight[:, :D]) + ops.gather_rows(prof, packed.tok_user)
         h = F.gelu(F.layer_norm(h, (D,), ln.weight, ln.bias, ln.eps))
-        return ops.l2_normalize(F.linear(h, lin3.weight, lin3.bias))
+        return ops.l2_normalize(ops.linear_tok(h, lin3.weight, lin3.bias))
 
 
 class PackedTokens:

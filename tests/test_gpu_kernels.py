@@ -347,3 +347,39 @@ def test_nce_grouped_sharded_rows(gpu, precision):
         assert abs(s.item() - ref[lo:hi].sum().item()) < 1e-3
         tot += s.item()
     assert abs(tot - ref.sum().item()) < 2e-3
+
+
+@pytest.mark.parametrize("T,N,K", [(80001, 384, 128), (4133, 128, 256), (37, 64, 48), (5, 16, 16), (0, 32, 32),
+                                   (70000, 256, 128)])
+def test_linear_wgrad_against_float64(gpu, T, N, K):
+    """dW = dY^T X and db = sum_t dY (split-K fp32 MFMA) vs a float64 product: max error
+    <= 1e-5 * (sum_t |dY||X| scale) — fp32 accumulation over T terms."""
+    g = torch.Generator().manual_seed(T + N + K)
+    dy = torch.randn(T, N, generator=g)
+    x = torch.randn(T, K, generator=g)
+    dw, db = ops.linear_wgrad(dy.to(gpu), x.to(gpu), (N, K), True)
+    ref_w = dy.double().t() @ x.double()
+    ref_b = dy.double().sum(0)
+    scale = max(1.0, math.sqrt(max(T, 1)))
+    assert (dw.cpu().double() - ref_w).abs().max().item() <= 2e-5 * scale
+    assert (db.cpu().double() - ref_b).abs().max().item() <= 2e-5 * scale
+
+
+def test_linear_tok_autograd_matches_linear(gpu):
+    """linear_tok == F.linear in value and in all three gradients (dX via the BLAS GEMM,
+    dW/db via rsx_linear_wgrad), including a weight slice view (output_proj[0].weight[:, :D])."""
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(3, 700, 128, generator=g).to(gpu)
+    w_full = torch.randn(128, 256, generator=g).to(gpu)
+    b = torch.randn(128, generator=g).to(gpu)
+    gy = torch.randn(3, 700, 128, generator=g).to(gpu)
+    outs = []
+    for fn in (ops.linear_tok, F.linear):
+        xx = x.clone().requires_grad_()
+        ww = w_full.clone().requires_grad_()
+        bb = b.clone().requires_grad_()
+        y = fn(xx, ww[:, :128], bb)
+        (y * gy).sum().backward()
+        outs.append((y.detach(), xx.grad, ww.grad, bb.grad))
+    for a, r in zip(*outs):
+        torch.testing.assert_close(a, r, atol=2e-4, rtol=1e-4)
