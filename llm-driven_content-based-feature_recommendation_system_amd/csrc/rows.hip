@@ -55,6 +55,7 @@ __global__ __launch_bounds__(256) void scatter_rows_k(const float* __restrict__ 
                                                      int64_t n, float eps, float* __restrict__ dst, int64_t ld_dst,
                                                      int accumulate, int64_t skip_idx) {
   constexpr int LPR = RowGeo<D>::LPR, RPW = RowGeo<D>::RPW;
+  __shared__ __attribute__((aligned(16))) float s_xr[ATOMIC ? 4 : 1][ATOMIC ? RPW : 1][ATOMIC ? D : 4];
   const int lane = threadIdx.x & 63, sub = lane / LPR, c = lane % LPR;
   const int64_t wave_g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t nw = (int64_t)gridDim.x * 4;
@@ -76,13 +77,29 @@ __global__ __launch_bounds__(256) void scatter_rows_k(const float* __restrict__ 
         g.x = g.x / eps; g.y = g.y / eps; g.z = g.z / eps; g.w = g.w / eps;
       }
     }
+    if (ATOMIC) {
+      // lane-strided order for the atomics (lane c adds elements c + LPR*k): one line per row
+      // per instruction instead of four (see seq_embed.hip); exchanged through a per-wave row
+      float* xr = &s_xr[threadIdx.x >> 6][sub][0];
+      reinterpret_cast<float4*>(xr)[c] = g;
+      __builtin_amdgcn_wave_barrier();
+      float xs[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) xs[k] = xr[c + LPR * k];
+      __builtin_amdgcn_wave_barrier();
+      if (!ok) continue;
+      const int64_t d = idx ? idx[r] : r;
+      if (d == skip_idx) continue;
+      float* q = dst + d * ld_dst + c;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) atomicAdd(q + LPR * k, xs[k]);
+      continue;
+    }
     if (!ok) continue;
     const int64_t d = idx ? idx[r] : r;
     if (d == skip_idx) continue;
     float* p = dst + d * ld_dst + 4 * c;
-    if (ATOMIC) {
-      atomicAdd(p + 0, g.x); atomicAdd(p + 1, g.y); atomicAdd(p + 2, g.z); atomicAdd(p + 3, g.w);
-    } else if (accumulate) {
+    if (accumulate) {
       float4 o = *reinterpret_cast<float4*>(p);
       o.x += g.x; o.y += g.y; o.z += g.z; o.w += g.w;
       *reinterpret_cast<float4*>(p) = o;
