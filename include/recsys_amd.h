@@ -131,6 +131,21 @@ int rsx_nce_grouped_bwd(const float* A, const float* B, const float* bias, const
                         int nsplit, const float* gout, float* ws, float* dA, float* dB, int accumulate,
                         void* stream);
 
+/* ---- LayerNorm fused with the preceding residual add + dropout and a following GELU ----
+ * s = x + dropout(res) (res nullable), y = act(LN(s) * w + b), act 0 none / 2 GELU(erf).
+ * Replaces norm1/norm2 and the residual adds of the norm_first TransformerEncoderLayer and the
+ * output head LayerNorm+GELU (tower_code/v1_refine_usertower.py:40-50, 68-72, 447-510).
+ * sum_out (nullable) receives s when res is given; mean/rstd [T] are saved for the backward.
+ * Backward: ds_out = LN-backward(dy) + ds_in (ds_in nullable), dres = dropout-backward(ds_out),
+ * dw/db via per-block partials (ws >= rsx_ln_bwd_workspace_floats). D in {64, 128, 256}. */
+int rsx_ln_fwd(const float* x, const float* res, float p_drop, uint64_t seed, const float* w, const float* b,
+               float eps, int act, int64_t T, int64_t D, float* sum_out, float* y, float* mean, float* rstd,
+               void* stream);
+int64_t rsx_ln_bwd_workspace_floats(int64_t T, int64_t D);
+int rsx_ln_bwd(const float* s, const float* mean, const float* rstd, const float* w, const float* b, int act,
+               const float* dy, const float* ds_in, float p_drop, uint64_t seed, int64_t T, int64_t D, float* ds_out,
+               float* dres, float* dw, float* db, float* ws, int64_t ws_floats, void* stream);
+
 /* ---- weight gradient of token-level linear layers ---------------------------------------
  * dW[n][k] (+)= sum_t dY[t][n] X[t][k], db[n] (+)= sum_t dY[t][n] (db nullable), fp32 MFMA,
  * split over tokens with a deterministic partial reduction. Replaces autograd's weight-grad

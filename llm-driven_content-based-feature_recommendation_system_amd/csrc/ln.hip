@@ -1,0 +1,258 @@
+// LayerNorm over the last dim of token rows, fused with the residual add + dropout that
+// precedes it and the GELU that may follow it:
+//
+//   s = x + dropout(res)         (res nullable: s = x)
+//   y = act(LN(s) * w + b)       act: 0 none, 2 GELU (erf form, torch default)
+//
+// Reference: the norm_first nn.TransformerEncoderLayer of the user tower
+// (tower_code/v1_refine_usertower.py:40-50: x + dropout(sa(norm1(x))), norm2, ...) and the
+// output head Linear -> LayerNorm -> GELU (:68-72, 499-510). The backward returns the
+// gradient of s (plus an optional incoming residual-path gradient), the dropout-masked
+// gradient of res, and dw/db through per-block partials summed in a fixed order.
+//
+// A row of D fp32 is owned by D/4 lanes (one float4 each); row statistics are two-pass
+// (mean, then centred variance) in fp32. Dropout keeps element (row, col) iff the counter
+// hash of (seed, row*D + col) passes (rsx_common.h): the same mask in forward and backward.
+#include "rsx_common.h"
+#include <math.h>
+
+namespace {
+
+template <int D>
+struct Geo {
+  static constexpr int LPR = D / 4;
+  static constexpr int RPW = 64 / LPR;
+};
+
+__device__ __forceinline__ float gelu_erf(float z) { return 0.5f * z * (1.0f + erff(z * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_erf_grad(float z) {
+  const float cdf = 0.5f * (1.0f + erff(z * 0.70710678118654752f));
+  const float pdf = 0.3989422804014327f * __expf(-0.5f * z * z);
+  return cdf + z * pdf;
+}
+
+struct FArgs {
+  const float* x;
+  const float* res;
+  const float* w;
+  const float* b;
+  float* sum_out;
+  float* y;
+  float* mean;
+  float* rstd;
+  int64_t T;
+  float eps;
+  int act;
+  rsx::Dropout drop;
+};
+
+template <int D>
+__global__ __launch_bounds__(256) void ln_fwd_k(FArgs a) {
+  constexpr int LPR = Geo<D>::LPR, RPW = Geo<D>::RPW;
+  const int lane = threadIdx.x & 63, sub = lane / LPR, c = lane % LPR;
+  const int64_t wave_g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const float4 w = a.w ? reinterpret_cast<const float4*>(a.w)[c] : make_float4(1.f, 1.f, 1.f, 1.f);
+  const float4 b = a.b ? reinterpret_cast<const float4*>(a.b)[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t r0 = wave_g * RPW; r0 < a.T; r0 += nw * RPW) {
+    const int64_t r = r0 + sub;
+    if (r >= a.T) continue;  // row groups are lane-aligned: the shuffles below stay in the group
+    float4 s = reinterpret_cast<const float4*>(a.x + r * D)[c];
+    if (a.res) {
+      float4 q = reinterpret_cast<const float4*>(a.res + r * D)[c];
+      const uint64_t bi = (uint64_t)r * D + 4 * c;
+      q.x = a.drop.apply(q.x, bi + 0);
+      q.y = a.drop.apply(q.y, bi + 1);
+      q.z = a.drop.apply(q.z, bi + 2);
+      q.w = a.drop.apply(q.w, bi + 3);
+      s.x += q.x; s.y += q.y; s.z += q.z; s.w += q.w;
+      if (a.sum_out) reinterpret_cast<float4*>(a.sum_out + r * D)[c] = s;
+    }
+    const float mu = rsx::wave_sum_width((s.x + s.y) + (s.z + s.w), LPR) * (1.0f / D);
+    const float4 d = make_float4(s.x - mu, s.y - mu, s.z - mu, s.w - mu);
+    const float var = rsx::wave_sum_width(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w, LPR) * (1.0f / D);
+    const float rs = 1.0f / sqrtf(var + a.eps);
+    float4 z = make_float4(d.x * rs * w.x + b.x, d.y * rs * w.y + b.y, d.z * rs * w.z + b.z, d.w * rs * w.w + b.w);
+    if (a.act == 2) z = make_float4(gelu_erf(z.x), gelu_erf(z.y), gelu_erf(z.z), gelu_erf(z.w));
+    reinterpret_cast<float4*>(a.y + r * D)[c] = z;
+    if (c == 0) {
+      if (a.mean) a.mean[r] = mu;
+      if (a.rstd) a.rstd[r] = rs;
+    }
+  }
+}
+
+struct BArgs {
+  const float* s;
+  const float* mean;
+  const float* rstd;
+  const float* w;
+  const float* b;
+  const float* dy;
+  const float* ds_in;
+  float* ds_out;
+  float* dres;
+  float* part;  // [nblocks][2][D] (dw, db partials) or nullptr
+  int64_t T, rows_per_block;
+  int act;
+  rsx::Dropout drop;
+};
+
+template <int D>
+__global__ __launch_bounds__(256) void ln_bwd_k(BArgs a) {
+  constexpr int LPR = Geo<D>::LPR, RPW = Geo<D>::RPW;
+  __shared__ __attribute__((aligned(16))) float s_red[4][2][D];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, sub = lane / LPR, c = lane % LPR;
+  const float4 w = a.w ? reinterpret_cast<const float4*>(a.w)[c] : make_float4(1.f, 1.f, 1.f, 1.f);
+  const float4 b = a.b ? reinterpret_cast<const float4*>(a.b)[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 acc_w = make_float4(0.f, 0.f, 0.f, 0.f), acc_b = acc_w;
+  const int64_t r_begin = (int64_t)blockIdx.x * a.rows_per_block;
+  int64_t r_end = r_begin + a.rows_per_block;
+  if (r_end > a.T) r_end = a.T;
+  for (int64_t r0 = r_begin; r0 < r_end; r0 += 4 * RPW) {
+    const int64_t r = r0 + wave * RPW + sub;
+    if (r >= r_end) continue;
+    const float4 s = reinterpret_cast<const float4*>(a.s + r * D)[c];
+    float4 g = reinterpret_cast<const float4*>(a.dy + r * D)[c];
+    const float mu = a.mean[r], rs = a.rstd[r];
+    const float4 xh = make_float4((s.x - mu) * rs, (s.y - mu) * rs, (s.z - mu) * rs, (s.w - mu) * rs);
+    if (a.act == 2) {
+      g.x *= gelu_erf_grad(xh.x * w.x + b.x);
+      g.y *= gelu_erf_grad(xh.y * w.y + b.y);
+      g.z *= gelu_erf_grad(xh.z * w.z + b.z);
+      g.w *= gelu_erf_grad(xh.w * w.w + b.w);
+    }
+    acc_w.x += g.x * xh.x; acc_w.y += g.y * xh.y; acc_w.z += g.z * xh.z; acc_w.w += g.w * xh.w;
+    acc_b.x += g.x; acc_b.y += g.y; acc_b.z += g.z; acc_b.w += g.w;
+    const float4 dh = make_float4(g.x * w.x, g.y * w.y, g.z * w.z, g.w * w.w);
+    const float c1 = rsx::wave_sum_width((dh.x + dh.y) + (dh.z + dh.w), LPR) * (1.0f / D);
+    const float c2 =
+        rsx::wave_sum_width(dh.x * xh.x + dh.y * xh.y + dh.z * xh.z + dh.w * xh.w, LPR) * (1.0f / D);
+    float4 dx = make_float4((dh.x - c1 - xh.x * c2) * rs, (dh.y - c1 - xh.y * c2) * rs,
+                            (dh.z - c1 - xh.z * c2) * rs, (dh.w - c1 - xh.w * c2) * rs);
+    if (a.ds_in) {
+      const float4 e = reinterpret_cast<const float4*>(a.ds_in + r * D)[c];
+      dx.x += e.x; dx.y += e.y; dx.z += e.z; dx.w += e.w;
+    }
+    if (a.ds_out) reinterpret_cast<float4*>(a.ds_out + r * D)[c] = dx;
+    if (a.dres) {
+      const uint64_t bi = (uint64_t)r * D + 4 * c;
+      float4 q;
+      q.x = a.drop.apply(dx.x, bi + 0);
+      q.y = a.drop.apply(dx.y, bi + 1);
+      q.z = a.drop.apply(dx.z, bi + 2);
+      q.w = a.drop.apply(dx.w, bi + 3);
+      reinterpret_cast<float4*>(a.dres + r * D)[c] = q;
+    }
+  }
+  if (!a.part) return;
+#pragma unroll
+  for (int o = LPR; o < 64; o <<= 1) {
+    acc_w.x += __shfl_xor(acc_w.x, o, 64); acc_w.y += __shfl_xor(acc_w.y, o, 64);
+    acc_w.z += __shfl_xor(acc_w.z, o, 64); acc_w.w += __shfl_xor(acc_w.w, o, 64);
+    acc_b.x += __shfl_xor(acc_b.x, o, 64); acc_b.y += __shfl_xor(acc_b.y, o, 64);
+    acc_b.z += __shfl_xor(acc_b.z, o, 64); acc_b.w += __shfl_xor(acc_b.w, o, 64);
+  }
+  if (sub == 0) {
+    reinterpret_cast<float4*>(&s_red[wave][0][0])[c] = acc_w;
+    reinterpret_cast<float4*>(&s_red[wave][1][0])[c] = acc_b;
+  }
+  __syncthreads();
+  for (int i = tid; i < 2 * D; i += blockDim.x) {
+    const float v = (s_red[0][0][i] + s_red[1][0][i]) + (s_red[2][0][i] + s_red[3][0][i]);
+    a.part[(int64_t)blockIdx.x * 2 * D + i] = v;
+  }
+}
+
+// out[i] = sum_k part[k][i] over nblk rows of width n (fixed order, 16 groups per output)
+__global__ __launch_bounds__(256) void colsum_k(const float* part, int nblk, int n, float* out0, float* out1,
+                                                int split) {
+  __shared__ float red[16][16];
+  const int o = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int i = blockIdx.x * 16 + o;
+  float s = 0.0f;
+  if (i < n)
+    for (int k = g; k < nblk; k += 16) s += part[(int64_t)k * n + i];
+  red[g][o] = s;
+  __syncthreads();
+  if (g != 0 || i >= n) return;
+  for (int k = 1; k < 16; ++k) s += red[k][o];
+  if (i < split) {
+    if (out0) out0[i] = s;
+  } else if (out1) {
+    out1[i - split] = s;
+  }
+}
+
+constexpr int kMaxBlocks = 1024;
+
+int64_t bwd_blocks(int64_t T, int64_t D, int64_t& rpb) {
+  const int64_t quantum = 4 * (64 / (D / 4));
+  rpb = (T + kMaxBlocks - 1) / kMaxBlocks;
+  rpb = (rpb + quantum - 1) / quantum * quantum;
+  if (rpb < quantum) rpb = quantum;
+  return (T + rpb - 1) / rpb;
+}
+
+}  // namespace
+
+RSX_API int rsx_ln_fwd(const float* x, const float* res, float p_drop, uint64_t seed, const float* w, const float* b,
+                       float eps, int act, int64_t T, int64_t D, float* sum_out, float* y, float* mean, float* rstd,
+                       void* stream) {
+  RSX_ARG(x && y, "null tensor");
+  RSX_ARG(D == 64 || D == 128 || D == 256, "D must be 64, 128 or 256");
+  RSX_ARG(act == 0 || act == 2, "act must be 0 (none) or 2 (gelu)");
+  RSX_ARG(p_drop >= 0.0f && p_drop < 1.0f, "p_drop must be in [0,1)");
+  if (T == 0) return 0;
+  FArgs a;
+  a.x = x; a.res = res; a.w = w; a.b = b; a.sum_out = sum_out; a.y = y; a.mean = mean; a.rstd = rstd;
+  a.T = T; a.eps = eps; a.act = act;
+  a.drop = rsx::make_dropout(res ? p_drop : 0.0f, seed);
+  const int64_t rows_per_block = 4 * (64 / (D / 4));
+  int64_t blocks = (T + rows_per_block - 1) / rows_per_block;
+  if (blocks > 8192) blocks = 8192;
+  hipStream_t st = (hipStream_t)stream;
+  if (D == 64) hipLaunchKernelGGL(ln_fwd_k<64>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  else if (D == 128) hipLaunchKernelGGL(ln_fwd_k<128>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(ln_fwd_k<256>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  RSX_LAUNCHED();
+  return 0;
+}
+
+RSX_API int64_t rsx_ln_bwd_workspace_floats(int64_t T, int64_t D) {
+  int64_t rpb;
+  return bwd_blocks(T, D, rpb) * 2 * D + 64;
+}
+
+RSX_API int rsx_ln_bwd(const float* s, const float* mean, const float* rstd, const float* w, const float* b, int act,
+                       const float* dy, const float* ds_in, float p_drop, uint64_t seed, int64_t T, int64_t D,
+                       float* ds_out, float* dres, float* dw, float* db, float* ws, int64_t ws_floats, void* stream) {
+  RSX_ARG(s && mean && rstd && dy, "null tensor");
+  RSX_ARG(D == 64 || D == 128 || D == 256, "D must be 64, 128 or 256");
+  RSX_ARG(act == 0 || act == 2, "act must be 0 (none) or 2 (gelu)");
+  RSX_ARG(!(dw || db) || (ws && ws_floats >= rsx_ln_bwd_workspace_floats(T, D)), "workspace too small");
+  RSX_ARG(act == 0 || w, "gelu needs the LayerNorm weight");
+  hipStream_t st = (hipStream_t)stream;
+  if (T == 0) {
+    if (dw) (void)hipMemsetAsync(dw, 0, D * sizeof(float), st);
+    if (db) (void)hipMemsetAsync(db, 0, D * sizeof(float), st);
+    RSX_LAUNCHED();
+    return 0;
+  }
+  BArgs a;
+  a.s = s; a.mean = mean; a.rstd = rstd; a.w = w; a.b = b; a.dy = dy; a.ds_in = ds_in; a.ds_out = ds_out;
+  a.dres = dres; a.part = (dw || db) ? ws : nullptr; a.T = T; a.act = act;
+  a.drop = rsx::make_dropout(p_drop, seed);
+  const int64_t blocks = bwd_blocks(T, D, a.rows_per_block);
+  if (D == 64) hipLaunchKernelGGL(ln_bwd_k<64>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  else if (D == 128) hipLaunchKernelGGL(ln_bwd_k<128>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(ln_bwd_k<256>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  RSX_LAUNCHED();
+  if (dw || db) {
+    const int n = (int)(2 * D);
+    hipLaunchKernelGGL(colsum_k, dim3((unsigned)((n + 15) / 16)), dim3(256), 0, st, ws, (int)blocks, n, dw, db,
+                       (int)D);
+    RSX_LAUNCHED();
+  }
+  return 0;
+}

@@ -396,6 +396,100 @@ def nce_grouped_sum(A, B_distinct, bias, groups: TargetGroups, tau=0.1, tag="nce
 
 
 # ----------------------------------------------------------------------------------------
+# LayerNorm (+ residual add + dropout before it, + GELU after it): rsx_ln_fwd / rsx_ln_bwd
+ACT_GELU_ERF = 2
+
+
+def _ln_bwd(s, mean, rstd, w, b, act, dy, ds_in, p_drop, seed, want_dx, want_dres, want_w, want_b):
+    T, D = s.shape
+    dx = torch.empty_like(s) if want_dx or want_dres else None
+    dres = torch.empty_like(s) if want_dres else None
+    dw = torch.empty(D, device=s.device, dtype=torch.float32) if want_w else None
+    db = torch.empty(D, device=s.device, dtype=torch.float32) if want_b else None
+    nws = N.lib().rsx_ln_bwd_workspace_floats(T, D)
+    ws = torch.empty(nws, device=s.device, dtype=torch.float32) if (want_w or want_b) else None
+    with timed("ln_bwd"):
+        rc = N.lib().rsx_ln_bwd(N.ptr(s), N.ptr(mean), N.ptr(rstd), N.ptr(w), N.ptr(b), act, N.ptr(_c(dy)),
+                                N.ptr(None if ds_in is None else _c(ds_in)), p_drop, seed, T, D, N.ptr(dx),
+                                N.ptr(dres), N.ptr(dw), N.ptr(db), N.ptr(ws), nws if ws is not None else 0,
+                                N.stream())
+    N.check(rc, "ln_bwd")
+    return dx, dres, dw, db
+
+
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, eps, act):
+        N.ensure_device(x)
+        x = _c(x)
+        T, D = x.shape
+        y = torch.empty_like(x)
+        mean = torch.empty(T, device=x.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        with timed("ln_fwd"):
+            rc = N.lib().rsx_ln_fwd(N.ptr(x), None, 0.0, 0, N.ptr(w), N.ptr(b), eps, act, T, D, None, N.ptr(y),
+                                    N.ptr(mean), N.ptr(rstd), N.stream())
+        N.check(rc, "ln_fwd")
+        ctx.save_for_backward(x, mean, rstd, w, b)
+        ctx.act = act
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, mean, rstd, w, b = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        dx, _, dw, db = _ln_bwd(x, mean, rstd, w, b, ctx.act, dy, None, 0.0, 0, need[0], False, need[1], need[2])
+        return dx, dw, db, None, None
+
+
+class _AddLayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, res, w, b, eps, p_drop, seed):
+        N.ensure_device(x)
+        x = _c(x)
+        res = _c(res)
+        T, D = x.shape
+        s = torch.empty_like(x)
+        y = torch.empty_like(x)
+        mean = torch.empty(T, device=x.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        with timed("ln_fwd"):
+            rc = N.lib().rsx_ln_fwd(N.ptr(x), N.ptr(res), p_drop, seed, N.ptr(w), N.ptr(b), eps, 0, T, D, N.ptr(s),
+                                    N.ptr(y), N.ptr(mean), N.ptr(rstd), N.stream())
+        N.check(rc, "ln_fwd")
+        ctx.save_for_backward(s, mean, rstd, w, b)
+        ctx.cfg = (p_drop, seed)
+        return s, y
+
+    @staticmethod
+    def backward(ctx, ds, dy):
+        s, mean, rstd, w, b = ctx.saved_tensors
+        p_drop, seed = ctx.cfg
+        need = ctx.needs_input_grad
+        if dy is None:
+            dy = torch.zeros_like(s)
+        dx, dres, dw, db = _ln_bwd(s, mean, rstd, w, b, 0, dy, ds, p_drop, seed, need[0], need[1], need[2], need[3])
+        return dx, dres, dw, db, None, None, None
+
+
+def layer_norm(x, weight, bias, eps=1e-5, act=0):
+    """act(LayerNorm(x)) over the last dim (act 0 none / ACT_GELU_ERF)."""
+    shp = x.shape
+    y = _LayerNorm.apply(x.reshape(-1, shp[-1]), weight, bias, float(eps), int(act))
+    return y.reshape(shp)
+
+
+def add_layer_norm(x, res, weight, bias, eps=1e-5, p_drop=0.0):
+    """(s, LayerNorm(s)) with s = x + dropout(res): the residual add of a norm_first encoder
+    layer fused with the next LayerNorm."""
+    shp = x.shape
+    seed = next_seed() if p_drop > 0 else 0
+    s, y = _AddLayerNorm.apply(x.reshape(-1, shp[-1]), res.reshape(-1, shp[-1]), weight, bias, float(eps),
+                               float(p_drop), seed)
+    return s.reshape(shp), y.reshape(shp)
+
+
+# ----------------------------------------------------------------------------------------
 # Token-level linear layer: forward/dX on the BLAS GEMM, dW/db on rsx_linear_wgrad (split-K)
 def linear_wgrad(dy, x, weight_shape, need_bias, tag="wgrad"):
     """(dW [N, K], db [N] or None) for dy [T, N], x [T, K] (fp32, contiguous)."""

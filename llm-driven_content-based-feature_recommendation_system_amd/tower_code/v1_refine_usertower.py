@@ -88,18 +88,26 @@ class SASRecUserTower(nn.Module):
     def get_causal_mask(self, seq_len, device):
         return torch.triu(torch.ones(seq_len, seq_len, device=device, dtype=torch.bool), diagonal=1)
 
-    # -- encoder layer (norm_first=True, gelu): reference nn.TransformerEncoderLayer semantics
-    def _encoder_layer(self, layer: nn.TransformerEncoderLayer, x, key_pad, p, seg_off=None):
-        sa = layer.self_attn
-        h = F.layer_norm(x, (self.d_model,), layer.norm1.weight, layer.norm1.bias, layer.norm1.eps)
-        qkv = ops.linear_tok(h, sa.in_proj_weight, sa.in_proj_bias)
-        a = ops.mha(qkv, key_pad, sa.num_heads, causal=True, p_drop=p, seg_off=seg_off)
-        a = ops.linear_tok(a, sa.out_proj.weight, sa.out_proj.bias)
-        x = x + F.dropout(a, p, self.training)
-        h = F.layer_norm(x, (self.d_model,), layer.norm2.weight, layer.norm2.bias, layer.norm2.eps)
-        f = ops.linear_tok(F.dropout(F.gelu(ops.linear_tok(h, layer.linear1.weight, layer.linear1.bias)), p,
-                                     self.training), layer.linear2.weight, layer.linear2.bias)
-        return x + F.dropout(f, p, self.training)
+    # -- encoder stack (norm_first=True, gelu): reference nn.TransformerEncoderLayer semantics
+    #    x = x + drop(out_proj(mha(norm1(x)))) ; x = x + drop(linear2(drop(gelu(linear1(norm2(x))))))
+    # Each residual add is fused with the LayerNorm that follows it (ops.add_layer_norm).
+    def _encoder_stack(self, x, key_pad, p, seg_off=None):
+        layers = list(self.transformer_encoder.layers)
+        h = ops.layer_norm(x, layers[0].norm1.weight, layers[0].norm1.bias, layers[0].norm1.eps)
+        for i, layer in enumerate(layers):
+            sa = layer.self_attn
+            qkv = ops.linear_tok(h, sa.in_proj_weight, sa.in_proj_bias)
+            a = ops.mha(qkv, key_pad, sa.num_heads, causal=True, p_drop=p, seg_off=seg_off)
+            a = ops.linear_tok(a, sa.out_proj.weight, sa.out_proj.bias)
+            x, h = ops.add_layer_norm(x, a, layer.norm2.weight, layer.norm2.bias, layer.norm2.eps, p)
+            f = ops.linear_tok(F.dropout(F.gelu(ops.linear_tok(h, layer.linear1.weight, layer.linear1.bias)), p,
+                                         self.training), layer.linear2.weight, layer.linear2.bias)
+            if i + 1 < len(layers):
+                nxt = layers[i + 1].norm1
+                x, h = ops.add_layer_norm(x, f, nxt.weight, nxt.bias, nxt.eps, p)
+            else:
+                x = x + F.dropout(f, p, self.training)
+        return x
 
     def forward(self, pretrained_vecs, item_ids, time_bucket_ids, type_ids, color_ids, graphic_ids, section_ids,
                 age_bucket, price_bucket, cnt_bucket, recency_bucket, channel_ids, club_status_ids, news_freq_ids,
@@ -119,9 +127,7 @@ class SASRecUserTower(nn.Module):
              self.graphic_emb.weight, self.section_emb.weight],
             s_g, self.pos_emb.weight[:seq_len], self.emb_ln.weight, self.emb_ln.bias, eps=self.emb_ln.eps,
             p_drop=p, padding_idx=[0, 0, 0, 0, 0, 0])
-        for layer in self.transformer_encoder.layers:
-            x = self._encoder_layer(layer, x, padding_mask, p)
-        output = x
+        output = self._encoder_stack(x, padding_mask, p)
 
         user_profile_vec = self._static_profile(age_bucket, price_bucket, cnt_bucket, recency_bucket, channel_ids,
                                                 club_status_ids, news_freq_ids, fn_ids, active_ids, cont_feats, u_g)
@@ -136,7 +142,7 @@ class SASRecUserTower(nn.Module):
             h = F.linear(output, w_seq) + prof.unsqueeze(1)
         else:
             h = F.linear(output[:, -1, :], w_seq) + prof
-        h = F.gelu(F.layer_norm(h, (D,), ln.weight, ln.bias, ln.eps))
+        h = ops.layer_norm(h, ln.weight, ln.bias, ln.eps, act=ops.ACT_GELU_ERF)
         final_vec = F.linear(h, lin3.weight, lin3.bias)
         return ops.l2_normalize(final_vec)
 
@@ -171,15 +177,14 @@ class SASRecUserTower(nn.Module):
              self.graphic_emb.weight, self.section_emb.weight],
             s_g, self.pos_emb.weight, self.emb_ln.weight, self.emb_ln.bias, eps=self.emb_ln.eps, p_drop=p,
             padding_idx=[0, 0, 0, 0, 0, 0], tok_pos=packed.tok_pos)
-        for layer in self.transformer_encoder.layers:
-            x = self._encoder_layer(layer, x, packed.tok_pad, p, seg_off=packed.seg_off)
+        x = self._encoder_stack(x, packed.tok_pad, p, seg_off=packed.seg_off)
         profile = self._static_profile(age_bucket, price_bucket, cnt_bucket, recency_bucket, channel_ids,
                                        club_status_ids, news_freq_ids, fn_ids, active_ids, cont_feats, u_g)
         lin0, ln, lin3 = self.output_proj[0], self.output_proj[1], self.output_proj[3]
         D = self.d_model
         prof = F.linear(profile, lin0.weight[:, D:], lin0.bias)
         h = ops.linear_tok(x, lin0.weight[:, :D]) + ops.gather_rows(prof, packed.tok_user)
-        h = F.gelu(F.layer_norm(h, (D,), ln.weight, ln.bias, ln.eps))
+        h = ops.layer_norm(h, ln.weight, ln.bias, ln.eps, act=ops.ACT_GELU_ERF)
         return ops.l2_normalize(ops.linear_tok(h, lin3.weight, lin3.bias))
 
 

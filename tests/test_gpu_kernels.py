@@ -383,3 +383,61 @@ def test_linear_tok_autograd_matches_linear(gpu):
         outs.append((y.detach(), xx.grad, ww.grad, bb.grad))
     for a, r in zip(*outs):
         torch.testing.assert_close(a, r, atol=2e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("D,act", [(128, 0), (128, 2), (64, 0), (256, 2)])
+def test_layer_norm_against_torch(gpu, D, act):
+    """rsx LayerNorm (+GELU) forward and all gradients vs torch fp32 (atol 2e-5 / rtol 1e-4)."""
+    g = torch.Generator().manual_seed(D + act)
+    x = (torch.randn(1337, D, generator=g) * 3 + 1).to(gpu)
+    w = (torch.rand(D, generator=g) + 0.5).to(gpu)
+    b = torch.randn(D, generator=g).to(gpu)
+    gy = torch.randn(1337, D, generator=g).to(gpu)
+    outs = []
+    for impl in ("rsx", "torch"):
+        xx, ww, bb = (t.clone().requires_grad_() for t in (x, w, b))
+        if impl == "rsx":
+            y = ops.layer_norm(xx, ww, bb, 1e-5, act=act)
+        else:
+            y = F.layer_norm(xx, (D,), ww, bb, 1e-5)
+            if act == 2:
+                y = F.gelu(y)
+        (y * gy).sum().backward()
+        outs.append((y.detach(), xx.grad, ww.grad, bb.grad))
+    for a, r in zip(*outs):
+        torch.testing.assert_close(a, r, atol=2e-4, rtol=1e-4)
+
+
+def test_add_layer_norm_residual_and_dropout(gpu):
+    """s = x + dropout(res), y = LN(s): p=0 equals torch; p>0: s - x is res*scale or 0, and the
+    residual gradient is the incoming gradient through the same mask."""
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(999, 128, generator=g).to(gpu)
+    r = torch.randn(999, 128, generator=g).to(gpu)
+    w = (torch.rand(128, generator=g) + 0.5).to(gpu)
+    b = torch.randn(128, generator=g).to(gpu)
+    gs = torch.randn(999, 128, generator=g).to(gpu)
+    gy = torch.randn(999, 128, generator=g).to(gpu)
+    outs = []
+    for impl in ("rsx", "torch"):
+        xx, rr, ww, bb = (t.clone().requires_grad_() for t in (x, r, w, b))
+        if impl == "rsx":
+            s, y = ops.add_layer_norm(xx, rr, ww, bb, 1e-5, 0.0)
+        else:
+            s = xx + rr
+            y = F.layer_norm(s, (128,), ww, bb, 1e-5)
+        ((s * gs).sum() + (y * gy).sum()).backward()
+        outs.append((s.detach(), y.detach(), xx.grad, rr.grad, ww.grad, bb.grad))
+    for a, ref in zip(*outs):
+        torch.testing.assert_close(a, ref, atol=2e-4, rtol=1e-4)
+    p = 0.3
+    rr = r.clone().requires_grad_()
+    xx = x.clone().requires_grad_()
+    s, y = ops.add_layer_norm(xx, rr, w, b, 1e-5, p)
+    kept = (s - x).abs() > 1e-6
+    torch.testing.assert_close((s - x)[kept], (r / (1 - p))[kept], atol=1e-5, rtol=1e-5)
+    frac = kept.float().mean().item()
+    assert abs(frac - (1 - p)) < 0.01, frac
+    (s * gs).sum().backward()
+    torch.testing.assert_close(xx.grad, gs, atol=1e-6, rtol=0)
+    torch.testing.assert_close(rr.grad, torch.where(kept, gs / (1 - p), torch.zeros_like(gs)), atol=1e-5, rtol=1e-5)
