@@ -120,6 +120,10 @@ int rsx_nce_bwd(const float* A, const float* B, const float* bias, const int* k1
  * The gradient product (dS x rows) is fp32 MFMA in both modes. */
 #define RSX_NCE_FP32 0
 #define RSX_NCE_BF16X3 1
+/* ws for the grouped pair: >= rsx_nce_grouped_workspace_floats(N, D, nsplit_fwd, 8, precision)
+ * (bf16x3 adds the hi/lo bf16 images of A and B; the forward writes B's, the backward's
+ * column pass A's). The grouped backward's nsplit is 8. */
+int64_t rsx_nce_grouped_workspace_floats(int64_t N, int64_t D, int nsplit_fwd, int nsplit_bwd, int precision);
 int rsx_nce_grouped_fwd(const float* A, const float* B, const float* bias, const float* colcnt, const int* row_col,
                         const int* row_beg, const int* row_end, const int* exc_cols, int64_t N, int64_t D,
                         int64_t lda, int64_t ldb, float tau, int precision, int nsplit, float* ws, float* out2,

@@ -35,7 +35,8 @@ constexpr int kOwnRows = 32 * kWaves;  // owner rows per workgroup
 constexpr int kLdsStride = kD + 4;     // padded row (conflict-free ds_read_b128 columns)
 
 enum : int { F_EXCL_DIAG = 1, F_MASK_K1 = 2, F_MASK_K2 = 4, F_POS = 8 };
-enum : int { RSX_NCE_FP32 = 0, RSX_NCE_BF16X3 = 1 };  // logit/gradient precision of the grouped kernels
+enum : int { RSX_NCE_FP32 = 0, RSX_NCE_BF16X3 = 1 };
+constexpr int kNsplitBwdGrouped = 8;  // fixed: the image region's offset in ws depends on it  // logit/gradient precision of the grouped kernels
 
 struct FwdArgs {
   const float* A;     // [N, lda] owner rows (queries)
@@ -619,6 +620,10 @@ struct GArgs {
   const float* lse;      // bwd
   const float* gout;     // bwd: gradient of the row-loss sum
   float* dout;           // bwd: [nsplit][owner][128]
+  const __bf16* ahi;     // bf16x3: hi/lo images of A [N][128] and B [M][128]
+  const __bf16* alo;
+  const __bf16* bhi;
+  const __bf16* blo;
 };
 
 __device__ __forceinline__ int lower_bound_i(const int* a, int lo, int hi, int64_t key) {
@@ -1046,32 +1051,46 @@ __device__ __forceinline__ void load_owner_x3(bf16x8 (&uh)[8], bf16x8 (&ul)[8], 
   }
 }
 
-// staging of one 32-row tile: thread tid holds row tid>>3, chunks tid&7 and 8+(tid&7)
+// Streamed operands are split once per call into global hi/lo bf16 images ([rows][128] each,
+// nce_split_k), so staging a tile is a plain copy: thread tid moves row tid>>3, 16-B chunks
+// tid&7 and 8+(tid&7) of both images (4 x 16-B loads, 4 ds_write_b128).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 struct X3Stage {
-  float4 v[4];
-  __device__ __forceinline__ void load(const float* base, int64_t row, int64_t ld, bool ok, int tid) {
+  u32x4 v[4];  // hi chunk0, hi chunk1, lo chunk0, lo chunk1
+  __device__ __forceinline__ void load(const __bf16* hi, const __bf16* lo, int64_t row, bool ok, int tid) {
     if (ok) {
-      const float* r = base + row * ld + (tid & 7) * 8;
-      const float4* s0 = reinterpret_cast<const float4*>(r);
-      const float4* s1 = reinterpret_cast<const float4*>(r + 64);
-      v[0] = s0[0]; v[1] = s0[1]; v[2] = s1[0]; v[3] = s1[1];
+      const int64_t o = row * kD + (tid & 7) * 8;
+      v[0] = *reinterpret_cast<const u32x4*>(hi + o);
+      v[1] = *reinterpret_cast<const u32x4*>(hi + o + 64);
+      v[2] = *reinterpret_cast<const u32x4*>(lo + o);
+      v[3] = *reinterpret_cast<const u32x4*>(lo + o + 64);
     } else {
 #pragma unroll
-      for (int t = 0; t < 4; ++t) v[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int t = 0; t < 4; ++t) v[t] = u32x4{0u, 0u, 0u, 0u};
     }
   }
   __device__ __forceinline__ void store(X3Tile& t, int tid) const {
     const int row = tid >> 3, ch = tid & 7;
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      bf16x8 hh, ll;
-      split8(v[2 * k], v[2 * k + 1], hh, ll);
-      const int off = img_off(row, 64 * k + 8 * ch);
-      *reinterpret_cast<bf16x8*>(&t.hi[off]) = hh;
-      *reinterpret_cast<bf16x8*>(&t.lo[off]) = ll;
-    }
+    const int o0 = img_off(row, 8 * ch), o1 = img_off(row, 64 + 8 * ch);
+    *reinterpret_cast<u32x4*>(&t.hi[o0]) = v[0];
+    *reinterpret_cast<u32x4*>(&t.hi[o1]) = v[1];
+    *reinterpret_cast<u32x4*>(&t.lo[o0]) = v[2];
+    *reinterpret_cast<u32x4*>(&t.lo[o1]) = v[3];
   }
 };
+
+// rows x 128 fp32 (row stride ld) -> hi/lo bf16 images [rows][128]; one thread per 8 floats
+__global__ __launch_bounds__(256) void nce_split_k(const float* src, int64_t ld, int64_t rows, __bf16* hi,
+                                                   __bf16* lo) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // 8-float chunk index
+  if (i >= rows * (kD / 8)) return;
+  const int64_t r = i / (kD / 8), c8 = i % (kD / 8);
+  const float4* p = reinterpret_cast<const float4*>(src + r * ld + c8 * 8);
+  bf16x8 h, l;
+  split8(p[0], p[1], h, l);
+  *reinterpret_cast<bf16x8*>(hi + r * kD + c8 * 8) = h;
+  *reinterpret_cast<bf16x8*>(lo + r * kD + c8 * 8) = l;
+}
 
 // S tile: acc[r] = <streamed row tile_row(r,h), owner row c> (owner on the lane).
 // The next k-step's fragments are read before this step's MFMAs (LDS latency under MFMA);
@@ -1174,11 +1193,13 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_fwd_x3_k(GArgs a) {
   float stg_b = 0.0f, stg_c = 0.0f;
   auto gload = [&](int64_t j0) {
     const int64_t j = j0 + (tid >> 3);
-    stg.load(a.B, j, a.ldb, j < j_end, tid);
+    stg.load(a.bhi, a.blo, j, j < j_end, tid);
     if (tid < kTile) {
       const int64_t jj = j0 + tid;
       const bool ok = jj < j_end;
-      stg_b = (ok && a.bias) ? a.bias[jj] : 0.0f;  // raw: no math on a load in flight
+      // raw values only (math on a load in flight would wait for it here); columns past the
+      // split get bias +inf, i.e. logit -inf, so the common path needs no mask
+      stg_b = ok ? (a.bias ? a.bias[jj] : 0.0f) : INFINITY;
       stg_c = ok ? a.colcnt[jj] : 0.0f;
     }
   };
@@ -1206,25 +1227,31 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_fwd_x3_k(GArgs a) {
         v[r] = fmaf(acc[r], it2, -sB2[cur][tr]);
       }
       if ((int64_t)next < j0 + kTile) {
-        // rare: some of the user's own targets (d(i) among them) fall in this tile
+        // rare: some of the user's own targets (d(i) among them) fall in this tile; a column
+        // whose multiplicity drops to 0 is masked
         int q = p;
         while (q < e && (int64_t)a.exc_cols[q] < j0 + kTile) ++q;
+        float n[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) n[r] = 0.0f;
+        for (int k = p; k < q; ++k) {
+          const int tk = (int)(a.exc_cols[k] - j0);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) n[r] += (tk == tile_row(r, h)) ? 1.0f : 0.0f;
+        }
+        const int tl = ((int64_t)di < j_end) ? (int)(di - j0) : -1;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int64_t d = j0 + tile_row(r, h);
-          int n = 0;
-          for (int k = p; k < q; ++k) n += (a.exc_cols[k] == (int)d);
-          if (d < j_end) w[r] = (d == di) ? 1.0f : w[r] - (float)n;
+          const int tr = tile_row(r, h);
+          w[r] = (tr == tl) ? 1.0f : w[r] - n[r];
+          if (!(w[r] > 0.0f)) v[r] = -INFINITY;
         }
         p = q;
         next = (p < e) ? a.exc_cols[p] : 0x7fffffff;
       }
       float tmax = -INFINITY;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        if (!(w[r] > 0.0f)) v[r] = -INFINITY;
-        tmax = fmaxf(tmax, v[r]);
-      }
+      for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, v[r]);
       if (!row_ok) tmax = -INFINITY;
       if (tmax > m) {
         l = (m == -INFINITY) ? 0.0f : l * __builtin_amdgcn_exp2f(m - tmax);
@@ -1274,9 +1301,7 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_bwd_x3_k(GArgs a) {
   const int64_t n_own = ROW_OWNED ? a.N : a.M;
   const int64_t n_str = ROW_OWNED ? a.M : a.N;
   const float* own = ROW_OWNED ? a.A : a.B;
-  const float* str = ROW_OWNED ? a.B : a.A;
   const int64_t ld_own = ROW_OWNED ? a.lda : a.ldb;
-  const int64_t ld_str = ROW_OWNED ? a.ldb : a.lda;
   const float gs = a.gout[0] * a.inv_tau;
   const float it2 = a.inv_tau * kLog2e;
   const int64_t o = (int64_t)ob * kOwnRows + wave * 32 + c;
@@ -1321,7 +1346,7 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_bwd_x3_k(GArgs a) {
   int stg2 = 0;
   auto gload = [&](int64_t s0) {
     const int64_t sidx = s0 + (tid >> 3);
-    stg.load(str, sidx, ld_str, sidx < s_end, tid);
+    stg.load(ROW_OWNED ? a.bhi : a.ahi, ROW_OWNED ? a.blo : a.alo, sidx, sidx < s_end, tid);
     if (tid < kTile) {
       const int64_t ss = s0 + tid;
       const bool ok = ss < s_end;
@@ -1451,6 +1476,33 @@ RSX_API int64_t rsx_nce_workspace_floats(int64_t N, int64_t M, int nsplit_fwd, i
          + (int64_t)nsplit_bwd * mx * kD  // bwd split partials
          + 16;
 }
+
+// Grouped kernels: the plain layout, then (bf16x3) the hi/lo images of A [N][128] and B [D][128].
+RSX_API int64_t rsx_nce_grouped_workspace_floats(int64_t N, int64_t D, int nsplit_fwd, int nsplit_bwd,
+                                                 int precision) {
+  const int64_t base = (rsx_nce_workspace_floats(N, D, nsplit_fwd, nsplit_bwd) + 63) / 64 * 64;
+  return base + (precision == RSX_NCE_BF16X3 ? (N + D) * kD + 64 : 0);
+}
+
+namespace {
+struct Images {
+  __bf16 *ahi, *alo, *bhi, *blo;
+};
+Images grouped_images(float* ws, int64_t N, int64_t D, int nsplit_fwd, int nsplit_bwd) {
+  const int64_t base = (rsx_nce_workspace_floats(N, D, nsplit_fwd, nsplit_bwd) + 63) / 64 * 64;
+  __bf16* p = reinterpret_cast<__bf16*>(ws + base);
+  Images im;
+  im.ahi = p;
+  im.alo = p + N * kD;
+  im.bhi = p + 2 * N * kD;
+  im.blo = p + 2 * N * kD + D * kD;
+  return im;
+}
+void launch_split(const float* src, int64_t ld, int64_t rows, __bf16* hi, __bf16* lo, hipStream_t st) {
+  const int64_t n = rows * (kD / 8);
+  if (n > 0) hipLaunchKernelGGL(nce_split_k, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, src, ld, rows, hi, lo);
+}
+}  // namespace
 
 // Forward: writes lse/row_loss/row_valid/inv_cnt (ws) and out2 = {sum of row losses, n_valid}.
 RSX_API int rsx_nce_fwd(const float* A, const float* B, const float* bias, const int* k1a, const int* k1b,
@@ -1592,8 +1644,16 @@ RSX_API int rsx_nce_grouped_fwd(const float* A, const float* B, const float* bia
   if (g.span < kTile) g.span = kTile;
   g.part = part;
   const int blocks = (int)(((N + kOwnRows - 1) / kOwnRows) * nsplit);
-  if (precision == RSX_NCE_BF16X3) hipLaunchKernelGGL(nce_grouped_fwd_x3_k, dim3(blocks), dim3(256), 0, st, g);
-  else hipLaunchKernelGGL(nce_grouped_fwd_k, dim3(blocks), dim3(256), 0, st, g);
+  if (precision == RSX_NCE_BF16X3) {
+    const Images im = grouped_images(ws, N, D, nsplit, kNsplitBwdGrouped);
+    g.bhi = im.bhi;
+    g.blo = im.blo;
+    launch_split(B, ldb, D, im.bhi, im.blo, st);  // kept in ws for the backward's row pass
+    RSX_LAUNCHED();
+    hipLaunchKernelGGL(nce_grouped_fwd_x3_k, dim3(blocks), dim3(256), 0, st, g);
+  } else {
+    hipLaunchKernelGGL(nce_grouped_fwd_k, dim3(blocks), dim3(256), 0, st, g);
+  }
   RSX_LAUNCHED();
   hipLaunchKernelGGL(nce_grouped_merge_k, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, A, B, bias, row_col, N,
                      lda, ldb, g.inv_tau, nsplit, part, lse, row_loss, row_valid);
@@ -1610,7 +1670,7 @@ RSX_API int rsx_nce_grouped_bwd(const float* A, const float* B, const float* bia
                                 int precision, int nsplit_fwd, int nsplit, const float* gout, float* ws, float* dA, float* dB,
                                 int accumulate, void* stream) {
   RSX_ARG(gout != nullptr && ws != nullptr, "gout/ws required");
-  RSX_ARG(nsplit >= 8 && nsplit <= 64 && nsplit % 8 == 0, "nsplit must be a multiple of 8 in [8,64]");
+  RSX_ARG(nsplit == kNsplitBwdGrouped, "grouped backward nsplit must be 8");
   RSX_ARG(precision == RSX_NCE_FP32 || precision == RSX_NCE_BF16X3, "precision must be 0 (fp32) or 1 (bf16x3)");
   RSX_ARG(!dB || (col_beg && col_end && exc_s && exc_e && exc_n), "column exception lists required for dB");
   hipStream_t st = (hipStream_t)stream;
@@ -1639,6 +1699,14 @@ RSX_API int rsx_nce_grouped_bwd(const float* A, const float* B, const float* bia
     if (g.span < kTile) g.span = kTile;
     const int blocks = (int)(((n_own + kOwnRows - 1) / kOwnRows) * nsplit);
     const bool x3 = precision == RSX_NCE_BF16X3;
+    if (x3) {
+      const Images im = grouped_images(ws, N, D, nsplit_fwd, kNsplitBwdGrouped);
+      g.ahi = im.ahi; g.alo = im.alo; g.bhi = im.bhi; g.blo = im.blo;
+      if (!row_owned) {  // B's images come from the forward; A's are made here, for the col pass
+        launch_split(A, lda, N, im.ahi, im.alo, st);
+        RSX_LAUNCHED();
+      }
+    }
     if (row_owned && x3) hipLaunchKernelGGL(nce_grouped_bwd_x3_k<true>, dim3(blocks), dim3(256), 0, st, g);
     else if (x3) hipLaunchKernelGGL(nce_grouped_bwd_x3_k<false>, dim3(blocks), dim3(256), 0, st, g);
     else if (row_owned) hipLaunchKernelGGL(nce_grouped_bwd_k<true>, dim3(blocks), dim3(256), 0, st, g);

@@ -345,7 +345,7 @@ class _NCEGrouped(torch.autograd.Function):
         A = _c(A)
         B = _c(B)
         n, d = A.shape[0], B.shape[0]
-        nws = N.lib().rsx_nce_workspace_floats(n, d, _NSPLIT_FWD, _NSPLIT_BWD)
+        nws = N.lib().rsx_nce_grouped_workspace_floats(n, d, _NSPLIT_FWD, _NSPLIT_BWD, prec)
         ws = torch.empty(nws, device=A.device, dtype=torch.float32)
         out2 = torch.empty(2, device=A.device, dtype=torch.float32)
         with timed(f"{tag}/nce_fwd"):
