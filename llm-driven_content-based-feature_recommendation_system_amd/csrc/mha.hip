@@ -274,6 +274,195 @@ __global__ __launch_bounds__(64) void mha_bwd_k(BwdArgs a) {
   }
 }
 
+// ---- backward on the fp32-input MFMA (head dim 32) ---------------------------------------
+// One wave per (sequence, head), four independent waves per workgroup, no LDS: every MFMA
+// operand is either a token row the lane loads itself (16 contiguous floats of dims
+// 16h..16h+15 for k-step (s, h) -> dim 16h + s) or a column slice X[row_s][e] read by 32
+// consecutive lanes (coalesced), and every accumulator tile is consumed in place:
+//   key on the lane (dK, dV):  S = Q K^T, dP' = dO V^T   -> dS, Pd   -> dV^T += dO^T Pd,
+//                                                                        dK^T += Q^T dS
+//   query on the lane (dQ):    S^T = K Q^T, dP'^T = V dO^T -> dS^T   -> dQ^T += K^T dS^T
+// S and dP' are computed in both orientations (the MFMA work is small; no transposes). The
+// per-element mask, dropout hash, softmax and dS formulas are those of mha_bwd_k.
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ int tile_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// 16 dims (16h .. 16h+15) of token row `row` of matrix base (row stride ld), zeros if !ok
+__device__ __forceinline__ void load_row16(float (&x)[16], const float* base, int64_t ld, int64_t row, bool ok,
+                                           int h) {
+  if (ok) {
+    const float4* p = reinterpret_cast<const float4*>(base + row * ld + 16 * h);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float4 v = p[t];
+      x[4 * t] = v.x; x[4 * t + 1] = v.y; x[4 * t + 2] = v.z; x[4 * t + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < 16; ++t) x[t] = 0.0f;
+  }
+}
+
+// acc[r] = sum_e A_row(lane-a)[e] * B_row(lane-b)[e] over 32 dims: rows on A's lanes become
+// the accumulator rows, B's lanes the columns
+__device__ __forceinline__ f32x16 dot_tile(const float (&a)[16], const float (&b)[16]) {
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+#pragma unroll
+  for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
+  return acc;
+}
+
+// acc += X^T T: X = 32 rows (row0 + tile_row(s,h)) of a matrix, column e = lane&31 (coalesced),
+// T = an accumulator tile whose register s holds row tile_row(s,h): k index (s, h)
+__device__ __forceinline__ void acc_colT(f32x16& acc, const float* base, int64_t ld, int64_t row0, int nrows,
+                                         const f32x16& t, int c, int h) {
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const int rr = tile_row(s, h);
+    const float x = (rr < nrows) ? base[(row0 + rr) * ld + c] : 0.0f;
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(x, t[s], acc, 0, 0, 0);
+  }
+}
+
+__global__ __launch_bounds__(256) void mha_bwd_mfma_k(BwdArgs a) {
+  constexpr int DH = 32;
+  const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
+  const int64_t unit = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (unit >= (int64_t)a.B * a.H) return;  // whole wave exits together
+  const int b = (int)(unit / a.H), hd = (int)(unit % a.H);
+  const int D = a.H * DH;
+  const int64_t ld = 3 * (int64_t)D;
+  const int64_t tok0 = a.seg ? (int64_t)a.seg[b] : (int64_t)b * a.L;
+  int L = a.seg ? (a.seg[b + 1] - a.seg[b]) : a.L;
+  if (L > kLMax) L = kLMax;
+  if (L <= 0) return;
+  const int nb = (L + 31) >> 5;
+  const float* Qb = a.qkv + tok0 * ld + hd * DH;
+  const float* Kb = Qb + D;
+  const float* Vb = Qb + 2 * D;
+  const float* dOb = a.dout + tok0 * D + hd * DH;
+  const float* Ob = a.out + tok0 * D + hd * DH;
+  float* dQb = a.dqkv + tok0 * ld + hd * DH;
+  float* dKb = dQb + D;
+  float* dVb = dQb + 2 * D;
+  const float sc = a.scale;
+
+  // per-token softmax statistics of this head: lse_i and delta_i = dO_i . O_i
+  // (token t < L lives on lane t; fetched by shuffle where needed)
+  float my_lse = -INFINITY, my_delta = 0.0f;
+  int my_pad = 1;
+  if (lane < L) {
+    my_lse = a.lse[(tok0 + lane) * a.H + hd];
+    const float4* op = reinterpret_cast<const float4*>(Ob + (int64_t)lane * D);
+    const float4* gp = reinterpret_cast<const float4*>(dOb + (int64_t)lane * D);
+    float d = 0.0f;
+#pragma unroll
+    for (int t = 0; t < DH / 4; ++t) {
+      const float4 x = op[t], y = gp[t];
+      d += x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
+    }
+    my_delta = d;
+    my_pad = a.kpad ? (int)a.kpad[tok0 + lane] : 0;
+  }
+
+  // element (query i, key j) -> (p, pd, dpd factor) ; returns dS and Pd
+  auto grad_elem = [&](int i, int j, float s, float dp, float lse_i, float delta_i, bool allowed, float& pd_out) {
+    pd_out = 0.0f;
+    if (!allowed) return 0.0f;
+    const float p = __expf(s * sc - lse_i);
+    float pd = p, dpd = dp;
+    if (a.drop.active()) {
+      const uint64_t idx = ((uint64_t)(tok0 + i) * a.H + hd) * kLMax + j;
+      const bool keep = rsx::hash_u32(a.drop.seed, idx) >= a.drop.thresh;
+      pd = keep ? p * a.drop.scale : 0.0f;
+      dpd = keep ? dp * a.drop.scale : 0.0f;
+    }
+    pd_out = pd;
+    return p * (dpd - delta_i) * sc;
+  };
+
+  // ---- key block on the lanes: dK, dV ----
+  for (int kb = 0; kb < nb; ++kb) {
+    const int j = 32 * kb + c;
+    const bool jok = j < L;
+    const int jpad = __shfl(my_pad, j & 63, 64);
+    float kr[16], vr[16];
+    load_row16(kr, Kb, ld, j, jok, h);
+    load_row16(vr, Vb, ld, j, jok, h);
+    f32x16 dkT, dvT;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { dkT[r] = 0.0f; dvT[r] = 0.0f; }
+    for (int qb = kb; qb < nb; ++qb) {
+      float qr[16], gr[16];
+      const int iq = 32 * qb + c;
+      load_row16(qr, Qb, ld, iq, iq < L, h);
+      load_row16(gr, dOb, D, iq, iq < L, h);
+      f32x16 S = dot_tile(qr, kr);   // [i][j]
+      f32x16 dP = dot_tile(gr, vr);  // [i][j]
+      f32x16 Pd;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = 32 * qb + tile_row(r, h);
+        const float lse_i = __shfl(my_lse, i & 63, 64);
+        const float del_i = __shfl(my_delta, i & 63, 64);
+        const bool allowed = jok && i < L && !jpad && (!a.causal || j <= i) && lse_i != -INFINITY;
+        float pd;
+        S[r] = grad_elem(i, j, S[r], dP[r], lse_i, del_i, allowed, pd);
+        Pd[r] = pd;
+      }
+      const int nrows = L - 32 * qb;
+      acc_colT(dvT, dOb, D, 32 * qb, nrows, Pd, c, h);  // dV^T[e][j] += sum_i dO[i][e] Pd[i][j]
+      acc_colT(dkT, Qb, ld, 32 * qb, nrows, S, c, h);   // dK^T[e][j] += sum_i Q[i][e] dS[i][j]
+    }
+    if (jok) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int e = tile_row(r, h);
+        dKb[(int64_t)j * ld + e] = dkT[r];
+        dVb[(int64_t)j * ld + e] = dvT[r];
+      }
+    }
+  }
+
+  // ---- query block on the lanes: dQ ----
+  for (int qb = 0; qb < nb; ++qb) {
+    const int i = 32 * qb + c;
+    const bool iok = i < L;
+    const float lse_i = __shfl(my_lse, i & 63, 64);
+    const float del_i = __shfl(my_delta, i & 63, 64);
+    float qr[16], gr[16];
+    load_row16(qr, Qb, ld, i, iok, h);
+    load_row16(gr, dOb, D, i, iok, h);
+    f32x16 dqT;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dqT[r] = 0.0f;
+    const int kb_end = a.causal ? qb + 1 : nb;
+    for (int kb = 0; kb < kb_end; ++kb) {
+      float kr[16], vr[16];
+      const int jk = 32 * kb + c;
+      load_row16(kr, Kb, ld, jk, jk < L, h);
+      load_row16(vr, Vb, ld, jk, jk < L, h);
+      f32x16 S = dot_tile(kr, qr);   // [j][i]
+      f32x16 dP = dot_tile(vr, gr);  // [j][i]
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int j = 32 * kb + tile_row(r, h);
+        const int jpad = __shfl(my_pad, j & 63, 64);
+        const bool allowed = iok && j < L && !jpad && (!a.causal || j <= i) && lse_i != -INFINITY;
+        float pd;
+        S[r] = grad_elem(i, j, S[r], dP[r], lse_i, del_i, allowed, pd);
+      }
+      acc_colT(dqT, Kb, ld, 32 * kb, L - 32 * kb, S, c, h);  // dQ^T[e][i] += sum_j K[j][e] dS^T[j][i]
+    }
+    if (iok) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dQb[(int64_t)i * ld + tile_row(r, h)] = dqT[r];
+    }
+  }
+}
+
 }  // namespace
 
 RSX_API int rsx_mha_fwd(const float* qkv, const uint8_t* key_pad, const int* seg_off, int64_t B, int64_t L,
@@ -315,7 +504,7 @@ RSX_API int rsx_mha_bwd(const float* qkv, const uint8_t* key_pad, const int* seg
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)(B * H));
   if (Dh == 16) hipLaunchKernelGGL(mha_bwd_k<16>, grid, dim3(64), 0, st, a);
-  else hipLaunchKernelGGL(mha_bwd_k<32>, grid, dim3(64), 0, st, a);
+  else hipLaunchKernelGGL(mha_bwd_mfma_k, dim3((unsigned)((B * H + 3) / 4)), dim3(256), 0, st, a);
   RSX_LAUNCHED();
   return 0;
 }
