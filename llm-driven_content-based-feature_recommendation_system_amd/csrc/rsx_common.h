@@ -11,13 +11,19 @@ void set_error(const char* fmt, ...);
 
 constexpr int kWave = 64;
 
-// Counter-based dropout RNG (splitmix64 finaliser over (seed, element index)).
-// Forward and backward regenerate the identical keep-mask from the same index.
+// Counter-based dropout RNG: murmur3's fmix32 finaliser over the element index mixed with
+// the 64-bit seed (32-bit integer ops only: ~10 VALU per element, cheap enough to evaluate
+// per attention score). Forward and backward regenerate the identical keep-mask from the
+// same (seed, index).
 __device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t idx) {
-  uint64_t z = seed + (idx + 1ull) * 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return (uint32_t)((z ^ (z >> 31)) >> 32);
+  uint32_t x = (uint32_t)idx ^ ((uint32_t)(idx >> 32) * 0x9E3779B1u) ^ (uint32_t)seed;
+  x ^= (uint32_t)(seed >> 32) * 0x85EBCA77u;
+  x ^= x >> 16;
+  x *= 0x85EBCA6Bu;
+  x ^= x >> 13;
+  x *= 0xC2B2AE35u;
+  x ^= x >> 16;
+  return x;
 }
 
 struct Dropout {
