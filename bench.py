@@ -25,6 +25,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32-input MFMA (= f32 vector peak)
+BF16_MFMA_PEAK_TFLOPS = 16 * FP32_MFMA_PEAK_TFLOPS  # 2516.8: dense bf16 MFMA (16x the f32 rate, same guide)
+# bf16x3: every fp32-equivalent FLOP is three bf16 MFMA products (hi*hi + hi*lo + lo*hi)
+BF16X3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 3
+TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_nce_bwd_rows_traffic.json")
 HBM_PEAK_GBS = 8000.0
 
 
@@ -206,10 +210,11 @@ def main():
     elapsed = float(elapsed.item())
     total_loss = float(losses[0].item())
 
-    # roofline of the dominant kernel: the main-loss InfoNCE backward, row-owned pass
-    # (grouped form: S recompute + dU product over N_local x D distinct-target columns on the
-    # fp32 MFMA). FLOPs per launch = 4 * N_local * D * 128 (2 * N * D * d per product;
-    # SURVEY.md §8d counts 2 N^2 d per product for the ungrouped reference formulation).
+    # roofline of the dominant kernel: the main-loss InfoNCE backward, row-owned pass (grouped
+    # form: S recompute + dU product over N_local x D distinct-target columns). Algorithmic
+    # FLOPs per launch = 4 * N_local * D * 128 (2 * N * D * d per product; SURVEY.md 8d counts
+    # 2 N^2 d per product for the ungrouped reference formulation). Peak: the MFMA rate of the
+    # arithmetic used — fp32 MFMA, or bf16 MFMA / 3 for the bf16x3 split products.
     flops = 0.0
     for i in range(args.steps):
         cnts = n_glob[i % 2]
@@ -217,6 +222,14 @@ def main():
     launches, ms = kernel_times.get("main/nce_bwd_rows", (0, 0.0))
     avg_s = (ms / 1e3) / max(launches, 1)
     achieved = (flops / max(launches, 1)) / avg_s / 1e12 if launches else None
+    x3 = args.nce_precision == "bf16x3"
+    peak = BF16X3_PEAK_TFLOPS if x3 else FP32_MFMA_PEAK_TFLOPS
+    traffic = None
+    if os.path.exists(TRAFFIC_FILE):
+        with open(TRAFFIC_FILE) as f:
+            tr = json.load(f)
+        if tr.get("precision") == args.nce_precision and tr.get("global_batch") == args.batch and world == 1:
+            traffic = tr.get("hbm_bytes_per_launch")
 
     kt = {k: {"launches": n, "avg_ms": round(t / max(n, 1), 4)} for k, (n, t) in sorted(kernel_times.items())}
     result = {
@@ -230,7 +243,7 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": "fp32+bf16x3" if x3 else "fp32",
         "data": "synthetic (seeded H&M-shaped users/items: sample-calibrated lengths, Zipf(1.0) items; "
                 "random-init weights)",
         "config": {"workload": "user-tower two-view contrastive train step (fwd x2 + LogQ in-batch loss + "
@@ -241,10 +254,14 @@ def main():
                    "item_matrix": "frozen" if args.freeze_items else "unfrozen (lr x0.05)",
                    "parallelism": f"dp{world} (users split by rank, RCCL all-gather of ids/z, grad all-reduce)",
                    "dense_projection_blas": args.blas, "nce_logit_precision": args.nce_precision},
-        "roofline": {"kernel": "nce_grouped_bwd_k<row-owned> (main LogQ loss backward)", "bound": "mfma",
-                     "achieved": round(achieved, 2) if achieved else None, "peak": FP32_MFMA_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4) if achieved else None,
-                     "traffic": None, "avg_launch_ms": round(avg_s * 1e3, 4)},
+        "roofline": {"kernel": ("nce_grouped_bwd_x3_k<true>" if x3 else "nce_grouped_bwd_k<true>")
+                     + " (main LogQ loss backward, row-owned)", "bound": "mfma",
+                     "achieved": round(achieved, 2) if achieved else None, "peak": round(peak, 1),
+                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
+                     "traffic": traffic, "traffic_source": os.path.basename(TRAFFIC_FILE) if traffic else None,
+                     "avg_launch_ms": round(avg_s * 1e3, 4),
+                     "peak_note": ("bf16 dense MFMA 2516.8 TF / 3 split products" if x3
+                                   else "fp32-input MFMA dense")},
         "kernels": kt,
         "final_loss": round(total_loss, 5),
     }

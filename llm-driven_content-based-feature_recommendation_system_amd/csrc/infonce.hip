@@ -60,10 +60,15 @@ __device__ __forceinline__ int tile_row(int r, int h) { return (r & 3) + 8 * (r 
 // split's streamed operand is re-read from that XCD's L2. Speed only, never correctness.
 __device__ __forceinline__ void remap_block(int nsplit, int& split, int& rb) {
   const int b = blockIdx.x;
-  const int nsub = nsplit >> 3;
   const int xcd = b & 7, q = b >> 3;
-  split = xcd + 8 * (q % nsub);
-  rb = q / nsub;
+  if (nsplit >= 8) {  // multiple of 8: each split on one XCD group
+    const int nsub = nsplit >> 3;
+    split = xcd + 8 * (q % nsub);
+    rb = q / nsub;
+  } else {  // nsplit in {1, 2, 4}: 8 / nsplit XCD groups per split
+    split = xcd % nsplit;
+    rb = (8 / nsplit) * q + xcd / nsplit;
+  }
 }
 
 template <int FL>
@@ -1621,7 +1626,8 @@ RSX_API int rsx_nce_grouped_fwd(const float* A, const float* B, const float* bia
                                 float* ws, float* out2, void* stream) {
   RSX_ARG(A && B && colcnt && row_col && row_beg && row_end && exc_cols && ws && out2, "null tensor");
   RSX_ARG(precision == RSX_NCE_FP32 || precision == RSX_NCE_BF16X3, "precision must be 0 (fp32) or 1 (bf16x3)");
-  RSX_ARG(nsplit >= 8 && nsplit <= 64 && nsplit % 8 == 0, "nsplit must be a multiple of 8 in [8,64]");
+  RSX_ARG(nsplit == 1 || nsplit == 2 || nsplit == 4 || (nsplit >= 8 && nsplit <= 64 && nsplit % 8 == 0),
+          "nsplit must be 1, 2, 4 or a multiple of 8 in [8,64]");
   RSX_ARG(lda % 4 == 0 && ldb % 4 == 0 && lda >= kD && ldb >= kD, "row strides must be >=128 and multiples of 4");
   RSX_ARG(((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0, "A/B must be 16-byte aligned");
   hipStream_t st = (hipStream_t)stream;
@@ -1695,9 +1701,14 @@ RSX_API int rsx_nce_grouped_bwd(const float* A, const float* B, const float* bia
     const int64_t n_own = row_owned ? N : D;
     const int64_t n_str = row_owned ? D : N;
     if (n_own == 0) continue;
-    g.span = round_up((n_str + nsplit - 1) / nsplit, kTile);
+    // split count of this pass: fewer splits when the owner side alone fills the chip (>= 1024
+    // workgroups), which halves the partial-gradient traffic of the row pass
+    const int64_t own_blocks = (n_own + kOwnRows - 1) / kOwnRows;
+    const int ps = (own_blocks * 4 >= 1024) ? 4 : nsplit;
+    g.nsplit = ps;
+    g.span = round_up((n_str + ps - 1) / ps, kTile);
     if (g.span < kTile) g.span = kTile;
-    const int blocks = (int)(((n_own + kOwnRows - 1) / kOwnRows) * nsplit);
+    const int blocks = (int)(own_blocks * ps);
     const bool x3 = precision == RSX_NCE_BF16X3;
     if (x3) {
       const Images im = grouped_images(ws, N, D, nsplit_fwd, kNsplitBwdGrouped);
@@ -1713,7 +1724,7 @@ RSX_API int rsx_nce_grouped_bwd(const float* A, const float* B, const float* bia
     else hipLaunchKernelGGL(nce_grouped_bwd_k<false>, dim3(blocks), dim3(256), 0, st, g);
     RSX_LAUNCHED();
     const int64_t total4 = n_own * kD / 4;
-    hipLaunchKernelGGL(nce_sum_splits_k, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, st, dpart, nsplit,
+    hipLaunchKernelGGL(nce_sum_splits_k, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, st, dpart, ps,
                        n_own, target, accumulate);
     RSX_LAUNCHED();
   }

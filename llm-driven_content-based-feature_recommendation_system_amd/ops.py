@@ -17,6 +17,7 @@ NCE_MASK_ITEM_USER = 6
 NCE_SUPCON = 9
 
 _NSPLIT_FWD = 8
+_NSPLIT_FWD_GROUPED = 4  # the grouped forward has N/128 >= 600 row blocks: 4 column splits fill the chip
 _NSPLIT_BWD = 8
 
 # Logit precision of the grouped (live LogQ) loss kernels, include/recsys_amd.h RSX_NCE_*:
@@ -345,13 +346,13 @@ class _NCEGrouped(torch.autograd.Function):
         A = _c(A)
         B = _c(B)
         n, d = A.shape[0], B.shape[0]
-        nws = N.lib().rsx_nce_grouped_workspace_floats(n, d, _NSPLIT_FWD, _NSPLIT_BWD, prec)
+        nws = N.lib().rsx_nce_grouped_workspace_floats(n, d, _NSPLIT_FWD_GROUPED, _NSPLIT_BWD, prec)
         ws = torch.empty(nws, device=A.device, dtype=torch.float32)
         out2 = torch.empty(2, device=A.device, dtype=torch.float32)
         with timed(f"{tag}/nce_fwd"):
             rc = N.lib().rsx_nce_grouped_fwd(N.ptr(A), N.ptr(B), N.ptr(bias), N.ptr(grp.colcnt), N.ptr(grp.row_col),
                                              N.ptr(grp.row_beg), N.ptr(grp.row_end), N.ptr(grp.exc_cols), n, d,
-                                             A.stride(0), B.stride(0), tau, prec, _NSPLIT_FWD, N.ptr(ws),
+                                             A.stride(0), B.stride(0), tau, prec, _NSPLIT_FWD_GROUPED, N.ptr(ws),
                                              N.ptr(out2), N.stream())
         N.check(rc, "nce_grouped_fwd")
         ctx.save_for_backward(A, B, bias, ws)
@@ -369,7 +370,8 @@ class _NCEGrouped(torch.autograd.Function):
         g = _c(g.reshape(1).to(torch.float32))
         args = (N.ptr(A), N.ptr(B), N.ptr(bias), N.ptr(grp.colcnt), N.ptr(grp.row_col), N.ptr(grp.row_beg),
                 N.ptr(grp.row_end), N.ptr(grp.exc_cols), N.ptr(grp.col_beg), N.ptr(grp.col_end), N.ptr(grp.exc_s),
-                N.ptr(grp.exc_e), N.ptr(grp.exc_n), n, d, A.stride(0), B.stride(0), tau, prec, _NSPLIT_FWD, _NSPLIT_BWD,
+                N.ptr(grp.exc_e), N.ptr(grp.exc_n), n, d, A.stride(0), B.stride(0), tau, prec, _NSPLIT_FWD_GROUPED,
+                _NSPLIT_BWD,
                 N.ptr(g), N.ptr(ws))
         dA = dB = None
         if ctx.needs_input_grad[0]:
