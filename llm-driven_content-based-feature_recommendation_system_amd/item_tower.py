@@ -1,0 +1,216 @@
+"""Drop-in for item_tower.py's model half: HybridItemTower, its head blocks, the SimCSE
+projector / wrapper and the symmetric SimCSE loss, on the MI355X kernels.
+
+Reference (item_tower.py):
+  * SEResidualBlock :41-75, DeepResidualHead :77-128, HybridItemTower :131-286,
+    OptimizedItemTower :289-305, SimCSEModelWrapper :308-322
+  * SimCSE loss in train_simcse_from_db :1069-1082 (S = e1 e2^T / 0.08, CE both directions)
+  * calculate_metrics :607-645 (alignment / uniformity health check)
+Module trees and parameter names are the reference's, so state_dicts load unchanged.
+
+Differences by design:
+  * the BERT is injected (``bert_model=``) or built locally from a config — the reference
+    downloads ``bert-base-uncased`` by name (:149-150), which has no offline equivalent;
+  * forward runs the token work on this package's kernels: fused LayerNorm(+GELU), the
+    token linears with split-K weight gradients, the MHA kernel (no mask, 16 field tokens)
+    and the InfoNCE kernel for the loss. BERT itself stays on PyTorch (hipBLASLt GEMMs).
+The DB-backed training driver (train_simcse_from_db :887+) needs PostgreSQL/pgvector and is
+out of scope; ``simcse_train_step`` is its per-batch GPU step.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import ops
+from .tower_code.v1_refine_usertower import encoder_stack
+
+PAD_ID = 0   # utils/vocab.py PAD_ID
+UNK_ID = 1
+EMBED_DIM = 128
+OUTPUT_DIM_ENCODER = 128
+OUTPUT_DIM_PROJECTOR = 128
+
+
+def _ln(x, ln: nn.LayerNorm, gelu: bool = False):
+    """LayerNorm (+ exact GELU) on the fused kernel where the width fits it, else PyTorch."""
+    if x.is_cuda and x.shape[-1] in (64, 128, 256):
+        return ops.layer_norm(x, ln.weight, ln.bias, ln.eps, act=ops.ACT_GELU_ERF if gelu else 0)
+    y = F.layer_norm(x, (x.shape[-1],), ln.weight, ln.bias, ln.eps)
+    return F.gelu(y) if gelu else y
+
+
+def _lin(x, layer: nn.Linear):
+    return ops.linear_tok(x, layer.weight, layer.bias) if x.is_cuda else layer(x)
+
+
+class SEResidualBlock(nn.Module):
+    """item_tower.py:41-75: x + block(x) * sigmoid(SE(block(x)))."""
+
+    def __init__(self, dim, dropout=0.2, expansion_factor=4):
+        super().__init__()
+        self.block = nn.Sequential(
+            nn.Linear(dim, dim * expansion_factor), nn.LayerNorm(dim * expansion_factor), nn.GELU(),
+            nn.Dropout(dropout), nn.Linear(dim * expansion_factor, dim), nn.LayerNorm(dim))
+        self.se_block = nn.Sequential(nn.Linear(dim, dim // 4), nn.ReLU(), nn.Linear(dim // 4, dim), nn.Sigmoid())
+
+    def forward(self, x):
+        b = self.block
+        h = _ln(_lin(x, b[0]), b[1], gelu=True)
+        h = b[3](h)
+        out = _ln(_lin(h, b[4]), b[5])
+        s = self.se_block
+        w = torch.sigmoid(_lin(F.relu(_lin(out, s[0])), s[2]))
+        return x + out * w
+
+
+class DeepResidualHead(nn.Module):
+    """item_tower.py:77-128: d -> 2d -> 4d, two SE residual blocks, 4d -> out, plus a d -> out
+    input shortcut."""
+
+    def __init__(self, input_dim, output_dim=128):
+        super().__init__()
+        mid_dim, hidden_dim = input_dim * 2, input_dim * 4
+        self.expand_layer1 = nn.Sequential(nn.Linear(input_dim, mid_dim), nn.LayerNorm(mid_dim), nn.GELU(),
+                                           nn.Dropout(0.1))
+        self.expand_layer2 = nn.Sequential(nn.Linear(mid_dim, hidden_dim), nn.LayerNorm(hidden_dim), nn.GELU(),
+                                           nn.Dropout(0.1))
+        self.res_blocks = nn.Sequential(SEResidualBlock(hidden_dim, dropout=0.2),
+                                        SEResidualBlock(hidden_dim, dropout=0.2))
+        self.final_proj = nn.Linear(hidden_dim, output_dim)
+        self.input_skip = nn.Linear(input_dim, output_dim)
+
+    def forward(self, x):
+        e1, e2 = self.expand_layer1, self.expand_layer2
+        m = e1[3](_ln(_lin(x, e1[0]), e1[1], gelu=True))
+        h = e2[3](_ln(_lin(m, e2[0]), e2[1], gelu=True))
+        h = self.res_blocks(h)
+        return _lin(h, self.final_proj) + _lin(x, self.input_skip)
+
+
+def build_local_bert(hidden_size: int = 768, num_layers: int = 12, num_heads: int = 12, intermediate: int = 3072,
+                     vocab_size: int = 30522, max_position: int = 512, seed: int = 0):
+    """A randomly initialised BertModel of the given shape (bert-base by default): the offline
+    stand-in for AutoModel.from_pretrained("bert-base-uncased") (item_tower.py:149-150)."""
+    from transformers import BertConfig, BertModel
+    cfg = BertConfig(vocab_size=vocab_size, hidden_size=hidden_size, num_hidden_layers=num_layers,
+                     num_attention_heads=num_heads, intermediate_size=intermediate,
+                     max_position_embeddings=max_position)
+    torch.manual_seed(seed)
+    return BertModel(cfg)
+
+
+class HybridItemTower(nn.Module):
+    """item_tower.py:131-286. forward(std_input [B,F], re_input_ids [B,9,R], re_attn_mask [B,9,R],
+    text_input_ids [B,S], text_attn_mask [B,S]) -> L2-normalised [B, output_dim]."""
+
+    def __init__(self, std_vocab_size: int, num_std_fields: int, embed_dim: int = 128, output_dim: int = 128,
+                 bert_model: Optional[nn.Module] = None):
+        super().__init__()
+        self.std_embedding = nn.Embedding(std_vocab_size, embed_dim, padding_idx=PAD_ID)
+        self.std_field_emb = nn.Parameter(torch.randn(1, num_std_fields, embed_dim))
+        self.std_ln = nn.LayerNorm(embed_dim)
+        self.re_ln = nn.LayerNorm(embed_dim)
+        self.bert_model = bert_model if bert_model is not None else build_local_bert()
+        self.bert_config = self.bert_model.config
+        bert_dim = self.bert_config.hidden_size
+        self.re_proj = nn.Sequential(nn.Linear(bert_dim, embed_dim), nn.LayerNorm(embed_dim), nn.GELU())
+        self.re_field_position = nn.Parameter(torch.randn(1, 9, embed_dim))
+        self.text_proj = nn.Sequential(nn.Linear(bert_dim, embed_dim), nn.LayerNorm(embed_dim), nn.GELU())
+        encoder_layer = nn.TransformerEncoderLayer(d_model=embed_dim, nhead=4, dim_feedforward=embed_dim * 4,
+                                                   batch_first=True, dropout=0.1, activation="gelu",
+                                                   norm_first=True)
+        self.transformer = nn.TransformerEncoder(encoder_layer, num_layers=2, enable_nested_tensor=False)
+        self.head = DeepResidualHead(input_dim=embed_dim, output_dim=output_dim)
+        self.embed_dim = embed_dim
+
+    def re_vectors(self, re_input_ids, re_attn_mask):
+        """RE fields: BERT word embeddings (no grad) -> re_proj -> masked mean over the field's
+        tokens (count clamped at 1e-9) -> + field position -> LayerNorm  (:247-262)."""
+        B, nf, R = re_input_ids.shape
+        flat_ids = re_input_ids.reshape(-1, R)
+        with torch.no_grad():
+            word = self.bert_model.embeddings(input_ids=flat_ids)
+        p = self.re_proj
+        feats = _ln(_lin(word, p[0]), p[1], gelu=True)                      # [B*9, R, d]
+        m = re_attn_mask.reshape(-1, R, 1).to(feats.dtype)
+        vec = (feats * m).sum(dim=1) / torch.clamp(m.sum(dim=1), min=1e-9)
+        vec = vec.reshape(B, nf, -1) + self.re_field_position
+        return _ln(vec, self.re_ln)
+
+    def forward(self, std_input, re_input_ids, re_attn_mask, text_input_ids, text_attn_mask):
+        std_emb = _ln(self.std_embedding(std_input) + self.std_field_emb, self.std_ln)        # :240-243
+        re_vec = self.re_vectors(re_input_ids, re_attn_mask)                                   # :247-262
+        cls = self.bert_model(input_ids=text_input_ids, attention_mask=text_attn_mask).last_hidden_state[:, 0, :]
+        t = self.text_proj
+        text_vec = _ln(_lin(cls, t[0]), t[1], gelu=True).unsqueeze(1)                         # :269-271
+        seq = torch.cat([std_emb, re_vec, text_vec], dim=1)                                   # [B, 16, d]
+        p = self.transformer.layers[0].dropout.p if self.training else 0.0
+        if seq.is_cuda:
+            ctx = encoder_stack(self.transformer.layers, seq.contiguous(), None, p, self.training, causal=False)
+        else:
+            ctx = self.transformer(seq)
+        out = self.head(ctx.mean(dim=1))
+        return ops.l2_normalize(out) if out.is_cuda else F.normalize(out, p=2, dim=1)
+
+
+class OptimizedItemTower(nn.Module):
+    """item_tower.py:289-305: normalize(Linear -> LayerNorm -> GELU -> Linear)."""
+
+    def __init__(self, input_dim=OUTPUT_DIM_ENCODER, output_dim=OUTPUT_DIM_PROJECTOR):
+        super().__init__()
+        self.layer = nn.Sequential(nn.Linear(input_dim, input_dim), nn.LayerNorm(input_dim), nn.GELU(),
+                                   nn.Linear(input_dim, output_dim))
+
+    def forward(self, x):
+        L = self.layer
+        y = _lin(_ln(_lin(x, L[0]), L[1], gelu=True), L[3])
+        return ops.l2_normalize(y) if y.is_cuda else F.normalize(y, p=2, dim=1)
+
+
+class SimCSEModelWrapper(nn.Module):
+    """item_tower.py:308-322: encoder -> projector."""
+
+    def __init__(self, encoder: nn.Module, projector: nn.Module):
+        super().__init__()
+        self.encoder = encoder
+        self.projector = projector
+
+    def forward(self, std, re_ids, re_mask, txt_ids, txt_mask):
+        return self.projector(self.encoder(std, re_ids, re_mask, txt_ids, txt_mask))
+
+
+def simcse_loss(emb1, emb2, temperature: float = 0.08):
+    """(CE(e1 e2^T / tau, arange) + CE(e2 e1^T / tau, arange)) / 2 (item_tower.py:1072-1079) on
+    the fused InfoNCE kernel (no logit matrix): row direction A=e1/B=e2, column direction
+    A=e2/B=e1, each the mean over rows of LSE_j S_ij - S_ii."""
+    l1 = ops.nce_loss(emb1, emb2, tau=temperature, flags=ops.NCE_PLAIN, tag="simcse")
+    l2 = ops.nce_loss(emb2, emb1, tau=temperature, flags=ops.NCE_PLAIN, tag="simcse")
+    return (l1 + l2) / 2
+
+
+@torch.no_grad()
+def calculate_metrics(x, y, t=2):
+    """item_tower.py:607-629: alignment E||x-y||^2 and uniformity log E exp(-t ||a_i - a_j||^2)
+    over the pairs of cat([x, y])."""
+    align = (x - y).norm(p=2, dim=1).pow(2).mean().item()
+    allv = torch.cat([x, y], dim=0)
+    uni = torch.pdist(allv, p=2).pow(2).mul(-t).exp().mean().log().item()
+    return align, uni
+
+
+def simcse_train_step(model, inputs_v1, inputs_v2, optimizer, temperature: float = 0.08, scheduler=None):
+    """One batch of train_simcse_from_db's loop (item_tower.py:1060-1085): two dropout views,
+    symmetric SimCSE loss, backward, optimizer (+ scheduler) step. fp32 (no GradScaler)."""
+    optimizer.zero_grad(set_to_none=True)
+    emb1 = model(*inputs_v1)
+    emb2 = model(*inputs_v2)
+    loss = simcse_loss(emb1, emb2, temperature)
+    loss.backward()
+    optimizer.step()
+    if scheduler is not None:
+        scheduler.step()
+    return loss.detach(), emb1.detach(), emb2.detach()

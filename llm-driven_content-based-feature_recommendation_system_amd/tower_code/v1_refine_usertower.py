@@ -19,6 +19,30 @@ import torch.nn.functional as F
 from .. import ops
 
 
+def encoder_stack(layers, x, key_pad, p, training, causal=True, seg_off=None):
+    """norm_first nn.TransformerEncoderLayer stack (gelu), reference semantics
+    (v1_refine_usertower.py:343-352, item_tower.py:169-182):
+      x = x + drop(out_proj(mha(norm1(x)))) ; x = x + drop(linear2(drop(gelu(linear1(norm2(x))))))
+    Each residual add is fused with the LayerNorm that follows it (ops.add_layer_norm); the
+    token linears take their weight gradients from rsx_linear_wgrad (ops.linear_tok)."""
+    layers = list(layers)
+    h = ops.layer_norm(x, layers[0].norm1.weight, layers[0].norm1.bias, layers[0].norm1.eps)
+    for i, layer in enumerate(layers):
+        sa = layer.self_attn
+        qkv = ops.linear_tok(h, sa.in_proj_weight, sa.in_proj_bias)
+        a = ops.mha(qkv, key_pad, sa.num_heads, causal=causal, p_drop=p, seg_off=seg_off)
+        a = ops.linear_tok(a, sa.out_proj.weight, sa.out_proj.bias)
+        x, h = ops.add_layer_norm(x, a, layer.norm2.weight, layer.norm2.bias, layer.norm2.eps, p)
+        f = ops.linear_tok(F.dropout(F.gelu(ops.linear_tok(h, layer.linear1.weight, layer.linear1.bias)), p,
+                                     training), layer.linear2.weight, layer.linear2.bias)
+        if i + 1 < len(layers):
+            nxt = layers[i + 1].norm1
+            x, h = ops.add_layer_norm(x, f, nxt.weight, nxt.bias, nxt.eps, p)
+        else:
+            x = x + F.dropout(f, p, training)
+    return x
+
+
 class SASRecUserTower(nn.Module):
     """Reference: tower_code/v1_refine_usertower.py:312-510."""
 
@@ -88,26 +112,9 @@ class SASRecUserTower(nn.Module):
     def get_causal_mask(self, seq_len, device):
         return torch.triu(torch.ones(seq_len, seq_len, device=device, dtype=torch.bool), diagonal=1)
 
-    # -- encoder stack (norm_first=True, gelu): reference nn.TransformerEncoderLayer semantics
-    #    x = x + drop(out_proj(mha(norm1(x)))) ; x = x + drop(linear2(drop(gelu(linear1(norm2(x))))))
-    # Each residual add is fused with the LayerNorm that follows it (ops.add_layer_norm).
     def _encoder_stack(self, x, key_pad, p, seg_off=None):
-        layers = list(self.transformer_encoder.layers)
-        h = ops.layer_norm(x, layers[0].norm1.weight, layers[0].norm1.bias, layers[0].norm1.eps)
-        for i, layer in enumerate(layers):
-            sa = layer.self_attn
-            qkv = ops.linear_tok(h, sa.in_proj_weight, sa.in_proj_bias)
-            a = ops.mha(qkv, key_pad, sa.num_heads, causal=True, p_drop=p, seg_off=seg_off)
-            a = ops.linear_tok(a, sa.out_proj.weight, sa.out_proj.bias)
-            x, h = ops.add_layer_norm(x, a, layer.norm2.weight, layer.norm2.bias, layer.norm2.eps, p)
-            f = ops.linear_tok(F.dropout(F.gelu(ops.linear_tok(h, layer.linear1.weight, layer.linear1.bias)), p,
-                                         self.training), layer.linear2.weight, layer.linear2.bias)
-            if i + 1 < len(layers):
-                nxt = layers[i + 1].norm1
-                x, h = ops.add_layer_norm(x, f, nxt.weight, nxt.bias, nxt.eps, p)
-            else:
-                x = x + F.dropout(f, p, self.training)
-        return x
+        return encoder_stack(self.transformer_encoder.layers, x, key_pad, p, self.training, causal=True,
+                             seg_off=seg_off)
 
     def forward(self, pretrained_vecs, item_ids, time_bucket_ids, type_ids, color_ids, graphic_ids, section_ids,
                 age_bucket, price_bucket, cnt_bucket, recency_bucket, channel_ids, club_status_ids, news_freq_ids,
@@ -262,3 +269,36 @@ def duorec_loss_refined(user_emb_1, user_emb_2, target_ids, temperature=0.1, lam
         loss_sup = ops.nce_loss(z_i, z_i, None, k, k, tau=temperature, flags=ops.NCE_SUPCON)
         return loss_unsup + lambda_sup * loss_sup
     return loss_unsup + lambda_sup * torch.zeros((), device=z_i.device)
+
+
+def full_batch_hard_emphasis_loss(user_emb, item_tower_emb, target_ids, log_q_tensor, top_k_percent=0.01,
+                                  hard_margin=0.2, hnm_threshold=0.90, temperature=0.1, lambda_logq=1.0):
+    """Reference :762-822 (the loss of train_user_tower, v1_usertower_train.py:459-469).
+    N x N over the batch (N <= a few thousand last-step rows): cosine logits, ignore mask
+    (same item, or item-item cosine > hnm_threshold off the diagonal), top-k hard negatives
+    (k = max(1, floor((N-1) * top_k_percent))) mined on the masked cosines get +margin/tau,
+    same-item off-diagonal columns -> -inf, CE against the diagonal. The column rows are
+    gathered + L2-normalised by rsx_gather_rows; the N x N products and top-k are PyTorch
+    (hipBLASLt / rocPRIM) — this is the secondary (resume) path, not the step's hot loop.
+    Returns (loss, {"avg_hn_similarity", "num_hard"})."""
+    N = user_emb.size(0)
+    device = user_emb.device
+    u = ops.l2_normalize(user_emb)
+    it = ops.gather_rows(item_tower_emb, target_ids, normalize=True)
+    cos = u @ it.T
+    same = target_ids.unsqueeze(1) == target_ids.unsqueeze(0)
+    diag = torch.eye(N, dtype=torch.bool, device=device)
+    with torch.no_grad():
+        ignore = same | (((it @ it.T) > hnm_threshold) & ~diag)
+        mining = cos.detach().masked_fill(ignore, float("-inf"))
+        num_k = max(1, int((N - 1) * top_k_percent))
+        _, top_idx = torch.topk(mining, k=num_k, dim=1)
+    logits = cos / temperature
+    if lambda_logq > 0.0:
+        logits = logits - log_q_tensor[target_ids].view(1, -1) * lambda_logq
+    emphasis = torch.zeros_like(logits).scatter_(1, top_idx, hard_margin / temperature)
+    logits = (logits + emphasis).masked_fill(same & ~diag, float("-inf"))
+    loss = F.cross_entropy(logits, torch.arange(N, device=device))
+    with torch.no_grad():
+        avg_hn = torch.gather(cos, 1, top_idx).mean().item()
+    return loss, {"avg_hn_similarity": avg_hn, "num_hard": num_k}

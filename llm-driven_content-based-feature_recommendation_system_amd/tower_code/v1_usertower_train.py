@@ -14,7 +14,8 @@ import torch
 import torch.nn as nn
 
 from .. import ops
-from .v1_refine_usertower import PackedTokens, SASRecUserTower, duorec_loss_refined, inbatch_corrected_logq_loss
+from .v1_refine_usertower import (PackedTokens, SASRecUserTower, duorec_loss_refined, full_batch_hard_emphasis_loss,
+                                  inbatch_corrected_logq_loss)
 
 try:  # the reference hard-imports wandb (v1_usertower_train.py:14); here it is optional
     import wandb  # type: ignore
@@ -204,6 +205,65 @@ def train_user_tower_all_time(epoch, model, item_tower, log_q_tensor, dataloader
             wandb.log({"Train/Main_Loss_Step": main.item(), "Train/CL_Loss_Step": cl.item(),
                        "Step": epoch * len(dataloader) + batch_idx})
     avg = total_acc / max(n, 1)
+    print(f"Epoch {epoch} Completed | Avg Total: {avg:.4f} (Main: {main_acc / max(n, 1):.4f}, "
+          f"CL: {cl_acc / max(n, 1):.4f})")
+    return avg
+
+
+def hard_emphasis_losses(model, item_tower, log_q_tensor, batch, cfg, pretrained_lookup=None):
+    """Forward of train_user_tower's step (reference :431-483): two dropout views, main loss =
+    full_batch_hard_emphasis_loss on the last position of users whose last position is valid
+    (tau 0.15), DuoRec on the last position. Only the last position's output is needed, so the
+    tower runs with training_mode=False (same values as output[:, -1] of the full-length
+    training-mode output; dropout follows model.training). Returns (total, main, cl, stats)."""
+    pv = batch.get("pretrained_vecs")
+    if pv is None:
+        pv = lookup_pretrained(pretrained_lookup, batch["item_ids"])
+    kw = {k: batch[k] for k in _SEQ_ID_KEYS + _STATIC_KEYS}
+    kw["padding_mask"] = batch["padding_mask"]
+    last_1 = model(pretrained_vecs=pv, training_mode=False, **kw)
+    last_2 = model(pretrained_vecs=pv, training_mode=False, **kw)
+    last_targets = batch["target_ids"][:, -1]
+    valid = ~batch["padding_mask"][:, -1]
+    vidx = valid.nonzero().squeeze(1)
+    if vidx.numel() > 0:
+        user = ops.l2_normalize(ops.gather_rows(last_1, vidx))
+        main, stats = full_batch_hard_emphasis_loss(user, item_tower.get_all_embeddings(), last_targets[vidx],
+                                                    log_q_tensor, top_k_percent=cfg.top_k_percent,
+                                                    hard_margin=cfg.hard_margin, hnm_threshold=cfg.hnm_threshold,
+                                                    temperature=0.15, lambda_logq=cfg.lambda_logq)
+    else:
+        main = torch.zeros((), device=last_1.device)
+        stats = {"avg_hn_similarity": 0.0, "num_active_hard_negs": 0}
+    cl = duorec_loss_refined(last_1, last_2, last_targets, lambda_sup=cfg.lambda_sup)
+    return main + cfg.lambda_cl * cl, main, cl, stats
+
+
+def train_user_tower(epoch, model, item_tower, log_q_tensor, dataloader, optimizer, scaler, cfg, device,
+                     seq_labels=None, static_labels=None):
+    """Reference train_user_tower (v1_usertower_train.py:367-540): hard-emphasis main loss on
+    the last position + DuoRec; clip 5.0; AdamW. Same signature; wandb only if importable."""
+    model.train()
+    lookup = getattr(getattr(dataloader, "dataset", None), "pretrained_lookup", None)
+    if lookup is not None and lookup.device != torch.device(device):
+        lookup = lookup.to(device)
+    tot = main_acc = cl_acc = 0.0
+    n = 0
+    for batch_idx, batch in enumerate(dataloader):
+        batch = _to_device(batch, device)
+        optimizer.zero_grad(set_to_none=True)
+        total, main, cl, stats = hard_emphasis_losses(model, item_tower, log_q_tensor, batch, cfg, lookup)
+        total.backward()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=5.0)
+        optimizer.step()
+        tot += total.item()
+        main_acc += main.item()
+        cl_acc += cl.item()
+        n += 1
+        if wandb is not None and batch_idx % 100 == 0 and getattr(wandb, "run", None) is not None:
+            wandb.log({"Train/Main_Loss_Step": main.item(), "HNM/Avg_Hard_Negative_Sim": stats.get(
+                "avg_hn_similarity", 0), "Step": epoch * len(dataloader) + batch_idx})
+    avg = tot / max(n, 1)
     print(f"Epoch {epoch} Completed | Avg Total: {avg:.4f} (Main: {main_acc / max(n, 1):.4f}, "
           f"CL: {cl_acc / max(n, 1):.4f})")
     return avg

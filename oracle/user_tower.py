@@ -244,3 +244,29 @@ def contrastive_step(model, item_matrix_param, log_q_tensor, batch, optimizer, p
     torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=max_norm)
     optimizer.step()
     return total.detach(), main.detach(), cl.detach()
+
+
+def full_batch_hard_emphasis_loss(user_emb, item_tower_emb, target_ids, log_q_tensor, top_k_percent=0.01,
+                                  hard_margin=0.2, hnm_threshold=0.90, temperature=0.1, lambda_logq=1.0):
+    """v1_refine_usertower.py:762-822, restated (CPU fp32)."""
+    N = user_emb.size(0)
+    u_norm = F.normalize(user_emb, p=2, dim=1)
+    i_norm = F.normalize(item_tower_emb[target_ids], p=2, dim=1)
+    cos_sim = u_norm @ i_norm.T
+    same = target_ids.unsqueeze(1) == target_ids.unsqueeze(0)
+    diag = torch.eye(N, dtype=torch.bool)
+    ignore = same | ((i_norm @ i_norm.T > hnm_threshold) & ~diag)
+    with torch.no_grad():
+        mining = cos_sim.detach().clone().masked_fill_(ignore, float("-inf"))
+        num_k = max(1, int((N - 1) * top_k_percent))
+        _, top_k_indices = torch.topk(mining, k=num_k, dim=1)
+    logits = cos_sim / temperature
+    if lambda_logq > 0.0:
+        logits = logits - log_q_tensor[target_ids].view(1, -1) * lambda_logq
+    emphasis = torch.zeros_like(logits, dtype=torch.bool)
+    emphasis.scatter_(1, top_k_indices, True)
+    logits = logits + emphasis.float() * (hard_margin / temperature)
+    logits = logits.masked_fill(same & ~diag, float("-inf"))
+    loss = F.cross_entropy(logits, torch.arange(N))
+    avg = torch.gather(cos_sim, 1, top_k_indices).mean().item()
+    return loss, {"avg_hn_similarity": avg, "num_hard": num_k}

@@ -1,0 +1,175 @@
+"""Item tower (item_tower.py:41-322), SimCSE loss (:1069-1082) and the hard-emphasis loss
+(v1_refine_usertower.py:762-822): recsys_amd on cuda:0 vs the CPU oracle with identical
+weights. The BERT on both sides is one locally built, randomly initialised BertModel
+(no pretrained weights offline: parity unpinned against the reference's bert-base-uncased)."""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+import recsys_amd  # noqa: F401
+from recsys_amd import item_tower as IT
+from recsys_amd.tower_code import v1_refine_usertower as T
+from recsys_amd.tower_code import v1_usertower_train as TT
+from recsys_amd import synth
+from oracle import item_tower as OIT
+from oracle import user_tower as O
+from tests.helpers import paired_towers, small_cfg, small_universe, to_dev
+
+pytestmark = pytest.mark.gpu
+
+
+def _tiny_bert(hidden=64):
+    return IT.build_local_bert(hidden_size=hidden, num_layers=2, num_heads=2, intermediate=2 * hidden,
+                               vocab_size=2000, max_position=64, seed=3)
+
+
+def _inputs(B, n_std=6, vocab=384, R=32, S=32, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    std = torch.randint(0, vocab, (B, n_std), generator=g)
+    std[torch.rand(B, n_std, generator=g) < 0.1] = 0
+    lens = torch.randint(2, R + 1, (B, 9), generator=g)
+    re_ids = torch.randint(1000, 2000, (B, 9, R), generator=g)
+    re_mask = (torch.arange(R).view(1, 1, R) < lens.unsqueeze(-1)).long()
+    re_ids = re_ids * re_mask
+    re_ids[:, :, 0] = 101
+    tl = torch.randint(2, S + 1, (B,), generator=g)
+    txt_mask = (torch.arange(S).view(1, S) < tl.unsqueeze(-1)).long()
+    txt = torch.randint(1000, 2000, (B, S), generator=g) * txt_mask
+    txt[:, 0] = 101
+    return [std, re_ids, re_mask, txt, txt_mask]
+
+
+def _pair(embed_dim, out_dim=128):
+    bert = _tiny_bert()
+    torch.manual_seed(7)
+    ref = OIT.OracleHybridItemTower(384, 6, embed_dim, out_dim, bert_model=bert)
+    dut = IT.HybridItemTower(384, 6, embed_dim, out_dim, bert_model=copy.deepcopy(bert))
+    dut.load_state_dict(ref.state_dict())
+    return ref, dut
+
+
+@pytest.mark.parametrize("embed_dim", [64, 128])
+def test_hybrid_item_tower_forward_and_grads(gpu, embed_dim):
+    """Eval-mode forward (dropout off) and the gradients of a scalar of the output, every
+    parameter: rtol 1e-4 / atol 2e-5 (value), 1e-3 relative to the gradient's max (grads)."""
+    ref, dut = _pair(embed_dim)
+    ref.eval()
+    dut = dut.to(gpu).eval()
+    x = _inputs(24, seed=embed_dim)
+    g = torch.Generator().manual_seed(1)
+    w = torch.randn(24, 128, generator=g)
+    y_ref = ref(*x)
+    (y_ref * w).sum().backward()
+    y = dut(*[t.to(gpu) for t in x])
+    (y * w.to(gpu)).sum().backward()
+    torch.testing.assert_close(y.detach().cpu(), y_ref.detach(), atol=2e-5, rtol=1e-4)
+    ref_p = dict(ref.named_parameters())
+    n = 0
+    for name, p in dut.named_parameters():
+        if p.grad is None:
+            assert ref_p[name].grad is None or ref_p[name].grad.abs().max() == 0, name
+            continue
+        gr = ref_p[name].grad
+        scale = gr.abs().max().item() + 1e-12
+        err = (p.grad.cpu() - gr).abs().max().item()
+        assert err <= 1e-3 * scale + 1e-7, (name, err, scale)
+        n += 1
+    assert n > 30
+
+
+def test_projector_wrapper_and_simcse_loss(gpu):
+    """OptimizedItemTower + SimCSEModelWrapper forward and the symmetric SimCSE loss (fused
+    InfoNCE, both directions) vs the oracle: loss within 1e-5 relative, grads 1e-4."""
+    torch.manual_seed(2)
+    ref_proj = OIT.OracleOptimizedItemTower(128, 128)
+    dut_proj = IT.OptimizedItemTower(128, 128)
+    dut_proj.load_state_dict(ref_proj.state_dict())
+    dut_proj = dut_proj.to(gpu)
+    g = torch.Generator().manual_seed(4)
+    e = torch.randn(300, 128, generator=g)
+    e2 = e + 0.3 * torch.randn(300, 128, generator=g)
+    a1 = e.clone().requires_grad_()
+    a2 = e2.clone().requires_grad_()
+    l_ref = OIT.simcse_loss(ref_proj(a1), ref_proj(a2))
+    l_ref.backward()
+    b1 = e.to(gpu).requires_grad_()
+    b2 = e2.to(gpu).requires_grad_()
+    l_dut = IT.simcse_loss(dut_proj(b1), dut_proj(b2))
+    l_dut.backward()
+    assert abs(l_dut.item() - l_ref.item()) <= 1e-5 * abs(l_ref.item()) + 1e-6
+    torch.testing.assert_close(b1.grad.cpu(), a1.grad, atol=1e-6, rtol=1e-4)
+    torch.testing.assert_close(b2.grad.cpu(), a2.grad, atol=1e-6, rtol=1e-4)
+
+
+def test_simcse_train_step_runs(gpu):
+    """Train-mode SimCSE step (dropout on, two views) through the wrapper: finite loss, every
+    trainable non-BERT parameter receives a gradient, calculate_metrics is finite."""
+    _, dut = _pair(64)
+    model = IT.SimCSEModelWrapper(dut, IT.OptimizedItemTower(128, 128)).to(gpu).train()
+    opt = torch.optim.AdamW([p for n, p in model.named_parameters() if "bert_model" not in n], lr=1e-4)
+    x = [t.to(gpu) for t in _inputs(32, seed=9)]
+    loss, e1, e2 = IT.simcse_train_step(model, x, x, opt)
+    assert torch.isfinite(loss)
+    align, uni = IT.calculate_metrics(e1, e2)
+    assert align >= 0 and uni == uni
+
+
+@pytest.mark.parametrize("N,lambda_logq", [(700, 1.0), (257, 0.0)])
+def test_hard_emphasis_loss_parity(gpu, N, lambda_logq):
+    """full_batch_hard_emphasis_loss vs the oracle: loss 1e-5 relative, user / item-matrix
+    gradients 1e-4; near-duplicate items exercise the item-similarity mask."""
+    g = torch.Generator().manual_seed(N)
+    I = 200
+    W = torch.randn(I + 1, 128, generator=g)
+    W[5] = W[4] + 0.01 * torch.randn(128, generator=g)   # cos > 0.9 pair
+    lq = torch.log_softmax(torch.randn(I + 1, generator=g), 0)
+    t = torch.randint(1, I + 1, (N,), generator=g)
+    t[:3] = 4
+    t[3:6] = 5
+    U = torch.randn(N, 128, generator=g)
+    u1 = U.clone().requires_grad_()
+    w1 = W.clone().requires_grad_()
+    l_ref, s_ref = O.full_batch_hard_emphasis_loss(u1, w1, t, lq, hard_margin=0.2, temperature=0.15,
+                                                   lambda_logq=lambda_logq)
+    l_ref.backward()
+    u2 = U.to(gpu).requires_grad_()
+    w2 = W.to(gpu).requires_grad_()
+    l_dut, s_dut = T.full_batch_hard_emphasis_loss(u2, w2, t.to(gpu), lq.to(gpu), hard_margin=0.2,
+                                                   temperature=0.15, lambda_logq=lambda_logq)
+    l_dut.backward()
+    assert s_dut["num_hard"] == s_ref["num_hard"]
+    assert abs(l_dut.item() - l_ref.item()) <= 1e-5 * abs(l_ref.item())
+    assert abs(s_dut["avg_hn_similarity"] - s_ref["avg_hn_similarity"]) < 1e-5
+    torch.testing.assert_close(u2.grad.cpu(), u1.grad, atol=1e-6, rtol=1e-4)
+    torch.testing.assert_close(w2.grad.cpu(), w1.grad, atol=1e-6, rtol=1e-4)
+
+
+def test_hard_emphasis_step_parity(gpu):
+    """train_user_tower's step losses (eval mode: dropout off, both views equal) vs the oracle
+    tower + oracle losses with the same weights."""
+    cfg = small_cfg(num_items=500)
+    items = small_universe(500)
+    batch = synth.make_batch(items, 96, seed=21)
+    ref, dut = paired_towers(cfg, gpu)
+    ref.eval(); dut.eval()
+    log_q = items.log_q
+    kw = {k: batch[k] for k in O._FWD_KEYS}
+    kw["pretrained_vecs"] = items.pretrained[batch["item_ids"]]
+    out = ref(**kw, training_mode=True)
+    last = out[:, -1, :]
+    valid = ~batch["padding_mask"][:, -1]
+    m_ref, _ = O.full_batch_hard_emphasis_loss(F.normalize(last[valid], dim=1), items.pretrained,
+                                               batch["target_ids"][:, -1][valid], log_q,
+                                               top_k_percent=cfg.top_k_percent, hard_margin=cfg.hard_margin,
+                                               hnm_threshold=cfg.hnm_threshold, temperature=0.15,
+                                               lambda_logq=cfg.lambda_logq)
+    c_ref = O.duorec_loss_refined(last, last, batch["target_ids"][:, -1], lambda_sup=cfg.lambda_sup)
+    it = TT.SASRecItemTower(500, 128, log_q.clone()).to(gpu)
+    it.init_from_pretrained(items.pretrained.to(gpu))
+    b = to_dev(batch, gpu)
+    b["pretrained_vecs"] = items.pretrained.to(gpu)[b["item_ids"]]
+    total, main, cl, _ = TT.hard_emphasis_losses(dut, it, log_q.to(gpu), b, cfg)
+    assert abs(main.item() - m_ref.item()) <= 1e-4 * abs(m_ref.item())
+    assert abs(cl.item() - c_ref.item()) <= 1e-4 * abs(c_ref.item())
