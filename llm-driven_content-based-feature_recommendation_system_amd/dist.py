@@ -193,3 +193,46 @@ def contrastive_step_dp(model, item_tower, log_q_tensor, batch, optimizer, cfg, 
     torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=max_norm)
     optimizer.step()
     return total, main, cl
+
+
+def merge_topk(scores, idx, k):
+    """Top-k of candidate lists [Q, C] by (score desc, index asc): the deterministic merge
+    of per-shard results."""
+    order = torch.argsort(idx, dim=1, stable=True)
+    s1 = torch.gather(scores, 1, order)
+    i1 = torch.gather(idx, 1, order)
+    o2 = torch.argsort(-s1, dim=1, stable=True)[:, :k]
+    return torch.gather(s1, 1, o2), torch.gather(i1, 1, o2)
+
+
+def retrieve_topk_sharded(queries, item_shard, shard_offset, k, local_topk=None, group=None):
+    """Retrieval over an item corpus sharded by row range across ranks:
+    each rank takes the top-k of its shard (rsx_retrieve_topk, indices made global with
+    shard_offset), the [Q, k] lists are all-gathered, and every rank merges them by
+    (score desc, index asc). Shards with fewer than k rows pad with (-inf, -1).
+    local_topk(queries, items, k) -> (scores, idx) defaults to ops.retrieve_topk."""
+    local_topk = local_topk or ops.retrieve_topk
+    kk = min(k, item_shard.shape[0])
+    if kk > 0:
+        s, i = local_topk(queries, item_shard, kk)
+        s = s.to(torch.float32)
+        i = torch.where(i >= 0, i + shard_offset, torch.full_like(i, -1))
+    else:
+        s = queries.new_empty(queries.shape[0], 0)
+        i = torch.empty(queries.shape[0], 0, dtype=torch.int64, device=queries.device)
+    if kk < k:
+        pad = k - kk
+        s = torch.cat([s, s.new_full((s.shape[0], pad), float("-inf"))], 1)
+        i = torch.cat([i, i.new_full((i.shape[0], pad), -1)], 1)
+    i = torch.where(i < 0, torch.full_like(i, torch.iinfo(torch.int64).max), i)
+    rank, ws = world()
+    if ws > 1:
+        ss = [torch.empty_like(s) for _ in range(ws)]
+        ii = [torch.empty_like(i) for _ in range(ws)]
+        dist.all_gather(ss, s.contiguous(), group=group)
+        dist.all_gather(ii, i.contiguous(), group=group)
+        s = torch.cat(ss, 1)
+        i = torch.cat(ii, 1)
+    s, i = merge_topk(s, i, k)
+    i = torch.where(i == torch.iinfo(torch.int64).max, torch.full_like(i, -1), i)
+    return s, i

@@ -19,6 +19,34 @@ import torch.nn.functional as F
 from .. import ops
 
 
+def get_logq_probs(raw_probs, device="cpu"):
+    """FeatureProcessor.get_logq_probs (reference :124-137) on the item-ordered raw
+    probabilities: nan -> 0, + 1e-6, normalise, log; index 0 (padding) = -20. [I+1] fp32."""
+    import numpy as np
+    p = np.nan_to_num(np.asarray(raw_probs, dtype=np.float64), nan=0.0) + 1e-6
+    p = p / p.sum()
+    full = np.zeros(len(p) + 1, dtype=np.float32)
+    full[1:] = np.log(p).astype(np.float32)
+    full[0] = -20.0
+    return torch.tensor(full, dtype=torch.float32).to(device)
+
+
+class FeatureProcessor:
+    """The part of the reference FeatureProcessor (:40-140) the GPU path consumes: item
+    vocabulary (item2id, 1-based; 0 = padding) and get_logq_probs. The per-user/-item
+    feature tables it builds from pandas frames are host-side data preparation (out of
+    scope)."""
+
+    def __init__(self, items_df, item_id_col="article_id"):
+        self.items = items_df.set_index(item_id_col) if item_id_col in items_df.columns else items_df
+        self.item_ids = list(self.items.index)
+        self.item2id = {iid: i + 1 for i, iid in enumerate(self.item_ids)}
+        self.num_items = len(self.item_ids)
+
+    def get_logq_probs(self, device):
+        return get_logq_probs(self.items["raw_probability"].reindex(self.item_ids).values, device)
+
+
 def encoder_stack(layers, x, key_pad, p, training, causal=True, seg_off=None):
     """norm_first nn.TransformerEncoderLayer stack (gelu), reference semantics
     (v1_refine_usertower.py:343-352, item_tower.py:169-182):

@@ -269,6 +269,59 @@ def train_user_tower(epoch, model, item_tower, log_q_tensor, dataloader, optimiz
     return avg
 
 
+def evaluate_model(model, item_tower, dataloader, target_df_path, device, processor, k_list=[20, 100, 500]):
+    """Reference :548-711 (same signature and result dict {"Recall@K": percent}).
+    Per batch: eval-mode tower (last position, training_mode=False), F.normalize, then the
+    top-max_k items of U normalize(W)^T by rsx_retrieve_topk (no [Q, I] score matrix; ties
+    -> lower item index, torch.topk leaves them unspecified). Hits are counted on the host
+    against target_df's sets exactly as the reference (users with no known target skipped)."""
+    import pandas as pd
+    model.eval()
+    item_tower.eval()
+    target_df = pd.read_parquet(target_df_path)
+    target_dict = target_df.set_index("customer_id")["target_ids"].to_dict()
+    max_k = max(k_list)
+    hits = {k: 0.0 for k in k_list}
+    n_users = 0
+    lookup = getattr(getattr(dataloader, "dataset", None), "pretrained_lookup", None)
+    with torch.no_grad():
+        items_n = ops.l2_normalize(item_tower.get_all_embeddings())
+        for batch in dataloader:
+            user_ids = batch["user_ids"]
+            dev_batch = {k: (v.to(device) if torch.is_tensor(v) else v) for k, v in batch.items()}
+            if "pretrained_vecs" in dev_batch:
+                pv = dev_batch["pretrained_vecs"]
+            else:
+                lk = lookup if lookup.device == torch.device(device) else lookup.to(device)
+                pv = lookup_pretrained(lk, dev_batch["item_ids"])
+            kw = {k: dev_batch[k] for k in _SEQ_ID_KEYS + _STATIC_KEYS}
+            out = model(pretrained_vecs=pv, padding_mask=dev_batch["padding_mask"], training_mode=False, **kw)
+            user = ops.l2_normalize(out)
+            valid = [i for i, u in enumerate(user_ids) if u in target_dict and len(target_dict[u]) > 0]
+            if not valid:
+                continue
+            v_idx = torch.tensor(valid, device=device)
+            _, top = ops.retrieve_topk(user[v_idx], items_n, max_k)
+            pred = top.cpu().numpy()
+            for i, orig in enumerate(valid):
+                raw = target_dict[user_ids[orig]]
+                if isinstance(raw, str) or not hasattr(raw, "__iter__"):
+                    raw = [raw]
+                actual = set(processor.item2id[t] for t in raw if t in processor.item2id)
+                if not actual:
+                    continue
+                n_users += 1
+                for k in k_list:
+                    if not actual.isdisjoint(pred[i, :k].tolist()):
+                        hits[k] += 1
+    res = {}
+    if n_users > 0:
+        for k in k_list:
+            res[f"Recall@{k}"] = hits[k] / n_users * 100
+    print(f"[Validation Results] Valid Users: {n_users}")
+    return res
+
+
 def load_aligned_pretrained_embeddings(processor, model_dir, pretrained_dim):
     """Reference :131-160 (torch.load with weights_only=True)."""
     emb_path = os.path.join(model_dir, "pretrained_item_matrix.pt")

@@ -83,3 +83,48 @@ def test_dp_plumbing_world2_gloo():
     for p in procs:
         p.join(timeout=60)
     assert res == {0: "ok", 1: "ok"}, res
+
+
+def _retrieval_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import recsys_amd  # noqa: F401
+        from recsys_amd import dist as D
+        from oracle.retrieval import retrieve_topk as ref_topk
+        g = torch.Generator().manual_seed(3)
+        corpus = torch.randn(1001, 128, generator=g)
+        corpus[700] = corpus[10]               # exact tie across shards: lower index must win
+        queries = torch.randn(6, 128, generator=g)
+        bounds = [0, 523, 1001]
+        lo, hi = bounds[rank], bounds[rank + 1]
+
+        def local(qv, items, k):
+            s, i = ref_topk(qv, items, k)
+            return s.float(), i
+
+        s, i = D.retrieve_topk_sharded(queries, corpus[lo:hi], lo, 50, local_topk=local)
+        s_ref, i_ref = ref_topk(queries, corpus, 50)
+        assert torch.equal(i, i_ref), (i[0, :10], i_ref[0, :10])
+        torch.testing.assert_close(s, s_ref.float())
+        q.put((rank, "ok"))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_retrieval_merge_gloo():
+    """Item-range sharded top-k: per-shard top-k with global indices,
+    all-gather, (score desc, index asc) merge == top-k over the whole corpus."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_retrieval_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert res == {0: "ok", 1: "ok"}, res

@@ -173,3 +173,54 @@ def test_hard_emphasis_step_parity(gpu):
     total, main, cl, _ = TT.hard_emphasis_losses(dut, it, log_q.to(gpu), b, cfg)
     assert abs(main.item() - m_ref.item()) <= 1e-4 * abs(m_ref.item())
     assert abs(cl.item() - c_ref.item()) <= 1e-4 * abs(c_ref.item())
+
+
+def test_evaluate_model_recall_matches_oracle(gpu, tmp_path):
+    """evaluate_model (v1_usertower_train.py:548-711): Recall@K from the GPU tower + fused
+    top-k equals the oracle tower + explicit top-k on the same weights / targets."""
+    import pandas as pd
+    from oracle.retrieval import retrieve_topk as ref_topk
+    cfg = small_cfg(num_items=500)
+    items = small_universe(500)
+    ref, dut = paired_towers(cfg, gpu)
+    ref.eval(); dut.eval()
+    batches = []
+    targets = {}
+    g = torch.Generator().manual_seed(8)
+    for bi in range(3):
+        b = synth.make_batch(items, 40, seed=30 + bi)
+        b["user_ids"] = [f"u{bi}_{j}" for j in range(40)]
+        b["pretrained_vecs"] = items.pretrained[b["item_ids"]]
+        for j, u in enumerate(b["user_ids"]):
+            if j % 7 == 3:
+                continue                      # users without targets are skipped
+            n = int(torch.randint(1, 4, (1,), generator=g))
+            targets[u] = [f"a{int(t)}" for t in torch.randint(1, 501, (n,), generator=g)]
+        batches.append(b)
+    path = tmp_path / "targets.parquet"
+    pd.DataFrame({"customer_id": list(targets), "target_ids": list(targets.values())}).to_parquet(path)
+
+    class Proc:
+        item2id = {f"a{i}": i for i in range(1, 501)}
+
+    it = TT.SASRecItemTower(500, 128, items.log_q.clone()).to(gpu)
+    it.init_from_pretrained(items.pretrained.to(gpu))
+    res = TT.evaluate_model(dut, it, batches, str(path), gpu, Proc(), k_list=[5, 20, 100])
+    # oracle
+    hits = {k: 0 for k in (5, 20, 100)}
+    n = 0
+    W = F.normalize(items.pretrained, dim=1)
+    for b in batches:
+        kw = {k: b[k] for k in O._FWD_KEYS}
+        kw["pretrained_vecs"] = b["pretrained_vecs"]
+        with torch.no_grad():
+            u = F.normalize(ref(**kw, training_mode=False), dim=1)
+        valid = [i for i, uid in enumerate(b["user_ids"]) if uid in targets]
+        _, top = ref_topk(u[valid], W, 100)
+        for r, i in enumerate(valid):
+            actual = {Proc.item2id[t] for t in targets[b["user_ids"][i]]}
+            n += 1
+            for k in hits:
+                hits[k] += int(not actual.isdisjoint(top[r, :k].tolist()))
+    for k in hits:
+        assert abs(res[f"Recall@{k}"] - hits[k] / n * 100) < 1e-9, (k, res, hits, n)

@@ -5,6 +5,10 @@ import torch
 from oracle import item_tower as OIT
 from oracle import user_tower as O
 
+import recsys_amd  # noqa: F401
+from recsys_amd import synth
+from recsys_amd.tower_code import v1_refine_usertower as T
+
 
 def test_oracle_item_tower_shapes_and_norm():
     from transformers import BertConfig, BertModel
@@ -39,3 +43,17 @@ def test_oracle_hard_emphasis_num_k():
     t = torch.randint(0, 50, (301,))
     loss, st = O.full_batch_hard_emphasis_loss(u, w, t, torch.zeros(50), top_k_percent=0.01)
     assert st["num_hard"] == 3 and torch.isfinite(loss)
+
+
+def test_feature_processor_logq():
+    """get_logq_probs (v1_refine_usertower.py:124-137): nan -> 0, + 1e-6, normalise, log,
+    padding row -20 — identical to the synthetic-universe helper on the same probs."""
+    import numpy as np
+    import pandas as pd
+    probs = np.array([0.5, np.nan, 0.2, 0.0, 0.3])
+    df = pd.DataFrame({"article_id": [11, 12, 13, 14, 15], "raw_probability": probs})
+    fp = T.FeatureProcessor(df)
+    lq = fp.get_logq_probs("cpu")
+    exp = synth.logq_from_probs(probs)
+    assert torch.equal(lq, exp)
+    assert fp.item2id[13] == 3 and lq[0].item() == -20.0
