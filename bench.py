@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--no-deepfm", action="store_true", help="skip the DeepFM rerank secondary metric")
     ap.add_argument("--deepfm-rows", type=int, default=65536)
     ap.add_argument("--deepfm-vocab", type=int, default=1_000_000)
+    ap.add_argument("--no-rerank", action="store_true", help="skip the retrieve->rerank secondary metric")
+    ap.add_argument("--corpus", type=int, default=1_000_000, help="retrieve->rerank corpus size")
+    ap.add_argument("--no-item-tower", action="store_true", help="skip the item-tower secondary metric")
     ap.add_argument("--nce-precision", default="bf16x3", choices=["bf16x3", "fp32"],
                     help="logit precision of the grouped LogQ loss kernels (ops.set_nce_precision)")
     ap.add_argument("--blas", default="default", choices=["default", "hipblaslt", "rocblas", "ck"],
@@ -124,7 +127,7 @@ def bench_deepfm(args, device):
     emb_s = emb_ms / 1e3 / emb_n
     dnn_flops = 2.0 * R * (F * 16 * 256 + 256 * 128 + 128)
     dnn_s = (lin_ms / lin_n + dot_ms / dot_n) / 1e3
-    return {"metric": "DeepFM rerank rows/sec (forward, 39 fields, d=16, vocab 1e6/field)",
+    return model, {"metric": "DeepFM rerank rows/sec (forward, 39 fields, d=16, vocab 1e6/field)",
             "value": round(R / dt, 1), "unit": "rows/s", "rows": R, "ms_per_batch": round(dt * 1e3, 4),
             "data": "synthetic Zipf(1.1) ids, deepctr-style N(0,1e-4) init",
             "gather_fm": {"avg_ms": round(emb_s * 1e3, 4), "bytes_per_row": bytes_row,
@@ -133,6 +136,82 @@ def bench_deepfm(args, device):
             "dnn": {"avg_ms": round(dnn_s * 1e3, 4), "achieved_TFLOPs": round(dnn_flops / dnn_s / 1e12, 2),
                     "peak_TFLOPs": FP32_MFMA_PEAK_TFLOPS,
                     "frac": round(dnn_flops / dnn_s / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)}}
+
+
+def bench_retrieve_rerank(args, device, deepfm):
+    """BASELINE configs[4] on one GPU: Q=4096 normalised user vectors against a 1M-item
+    normalised corpus (seed 5), top-100 by rsx_retrieve_topk, 39 hashed (user bucket, item)
+    sparse ids per candidate, DeepFM on the Q x 100 rows, final top-10 per query by
+    probability. queries/s; the retrieval kernel priced at the fp32 MFMA peak."""
+    from recsys_amd import ops
+    Q, I, K, F = 4096, args.corpus, 100, 39
+    g = torch.Generator(device="cpu").manual_seed(5)
+    corpus = torch.nn.functional.normalize(torch.randn(I, 128, generator=g), dim=1).to(device)
+    users = torch.nn.functional.normalize(torch.randn(Q, 128, generator=g), dim=1).to(device)
+    V = args.deepfm_vocab
+    fld = torch.arange(F, device=device, dtype=torch.int64).view(1, 1, F)
+    ubucket = (torch.arange(Q, device=device, dtype=torch.int64) % 1000).view(Q, 1, 1)
+
+    def step():
+        sc, idx = ops.retrieve_topk(users, corpus, K)
+        h = idx.unsqueeze(-1) * 0x9E3779B1 + ubucket * 0x85EBCA77 + fld * 0xC2B2AE35
+        feats = ((h ^ (h >> 29)) & 0x7FFFFFFF) % V
+        _, prob = deepfm.forward_logits(feats.view(Q * K, F))
+        top_p, top_j = torch.topk(prob.view(Q, K), 10, dim=1)
+        return torch.gather(idx, 1, top_j), top_p
+
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    iters = 5
+    ops.timing_start()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        step()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / iters
+    kt = ops.timing_stop()
+    n, ms = kt.get("retrieve_topk", (1, 0.0))
+    rs = ms / 1e3 / max(n, 1)
+    flops = 2.0 * Q * I * 128  # algorithmic (one score per (query, item)); the exact path scores twice
+    return {"metric": "retrieve->rerank queries/sec (1M-item corpus, top-100, DeepFM rerank, top-10)",
+            "value": round(Q / dt, 1), "unit": "queries/s", "queries": Q, "corpus": I,
+            "ms_per_batch": round(dt * 1e3, 3), "rerank_rows_per_s": round(Q * K / dt, 1),
+            "data": "synthetic normalised N(0,1) corpus / users, hashed rerank ids",
+            "retrieval": {"kernel": "topk_fast_scan_k (candidates + collect passes) + topk_thresh_k + topk_final_k", "avg_ms": round(rs * 1e3, 4),
+                          "achieved_TFLOPs": round(flops / rs / 1e12, 2), "peak_TFLOPs": FP32_MFMA_PEAK_TFLOPS,
+                          "frac": round(flops / rs / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)}}
+
+
+def bench_item_tower(args, device):
+    """BASELINE configs[0] shape on the GPU: HybridItemTower forward (eval) for 256 items,
+    d=64, with a locally built bert-base-shaped BERT (random weights). items/s."""
+    import numpy as np
+    from recsys_amd import item_tower as IT
+    B, R, S = 256, 32, 32
+    torch.manual_seed(args.seed)
+    model = IT.HybridItemTower(384, 6, 64, 128, bert_model=IT.build_local_bert()).to(device).eval()
+    rng = np.random.default_rng(args.seed + 7)
+    std = torch.from_numpy(rng.integers(0, 384, (B, 6))).to(device)
+    lens = rng.integers(2, R + 1, (B, 9))
+    re_mask = torch.from_numpy((np.arange(R)[None, None, :] < lens[..., None]).astype(np.int64)).to(device)
+    re_ids = torch.from_numpy(rng.integers(1000, 30521, (B, 9, R))).to(device) * re_mask
+    tl = rng.integers(2, S + 1, (B,))
+    txt_mask = torch.from_numpy((np.arange(S)[None, :] < tl[:, None]).astype(np.int64)).to(device)
+    txt = torch.from_numpy(rng.integers(1000, 30521, (B, S))).to(device) * txt_mask
+    with torch.no_grad():
+        for _ in range(3):
+            model(std, re_ids, re_mask, txt, txt_mask)
+        torch.cuda.synchronize()
+        iters = 10
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            model(std, re_ids, re_mask, txt, txt_mask)
+        torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / iters
+    return {"metric": "HybridItemTower forward items/sec (256 items, d=64, bert-base-shaped local BERT)",
+            "value": round(B / dt, 1), "unit": "items/s", "ms_per_batch": round(dt * 1e3, 3),
+            "data": "synthetic std/RE/text ids (SURVEY.md 8d config 1), random BERT weights"}
 
 
 def main():
@@ -268,7 +347,13 @@ def main():
     if rank == 0 and world == 1 and not args.no_deepfm:
         del batches
         torch.cuda.empty_cache()
-        result["secondary"] = bench_deepfm(args, device)
+        deepfm, result["secondary"] = bench_deepfm(args, device)
+        if not args.no_rerank:
+            result["secondary_retrieve_rerank"] = bench_retrieve_rerank(args, device, deepfm)
+        del deepfm
+        torch.cuda.empty_cache()
+    if rank == 0 and world == 1 and not args.no_item_tower:
+        result["secondary_item_tower"] = bench_item_tower(args, device)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, items, cfg)
     if rank == 0:

@@ -1,4 +1,7 @@
 // Retrieval: top-k items by inner product, without materialising the [Q, I] score matrix.
+// Two exact paths: the list-based scan below (small corpora, and the gated fallback), and the
+// candidate -> threshold -> collect path further down (large corpora: two MFMA scans, no
+// per-insertion list maintenance).
 // Reference: evaluate_model (tower_code/v1_usertower_train.py:672-675: scores = U W_n^T;
 // topk(max_k)) and ReRankingSystem.recommend (temp_model/ranker_skelet.py:193-196).
 //
@@ -25,6 +28,7 @@ constexpr int kLdsStride = kD + 4;
 __device__ __forceinline__ int tile_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 struct ScanArgs {
+  const int* gate;  // nullptr, or: run only if *gate != 0 (the exact fallback of the fast path)
   const float* U;  // [Q, ldu]
   const float* I;  // [NI, ldi]
   int64_t Q, NI, ldu, ldi;
@@ -42,6 +46,7 @@ __device__ __forceinline__ bool better(float sa, int ia, float sb, int ib) {
 
 template <int KMAX>
 __global__ __launch_bounds__(256, 2) void topk_scan_k(ScanArgs a) {
+  if (a.gate && *a.gate == 0) return;
   __shared__ __attribute__((aligned(16))) float sI[2][kTile][kLdsStride];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, c = lane & 31;
@@ -160,7 +165,8 @@ __global__ __launch_bounds__(256, 2) void topk_scan_k(ScanArgs a) {
 // One workgroup per query: bitonic sort of NC = 2*nsplit*KMAX candidates, descending.
 template <int NC>
 __global__ __launch_bounds__(256) void topk_merge_k(const float* cs, const int* ci, int64_t Q, int ncand, int K,
-                                                    float* out_s, int64_t* out_i) {
+                                                    float* out_s, int64_t* out_i, const int* gate) {
+  if (gate && *gate == 0) return;
   __shared__ float ss[NC];
   __shared__ int si[NC];
   const int64_t q = blockIdx.x;
@@ -199,6 +205,231 @@ __global__ __launch_bounds__(256) void topk_merge_k(const float* cs, const int* 
   }
 }
 
+// ---- fast exact path (large corpora): candidates -> threshold -> collect -> final sort -----
+// K1 (MODE 0): the scan above, but each lane keeps only the best T of its stream in registers.
+// K2: per query, the k-th best of the 2*nsplit*T candidates is a lower bound t_q of the true
+//     k-th best score (the candidates are real items).
+// K3 (MODE 1): the scan again; every item with score >= t_q is appended to the query's buffer
+//     (a superset of the true top-k, ties included; typically ~k entries).
+// K4: per query, sort the buffer by (score desc, index asc) and write the first k.
+// If a buffer overflows (massive exact ties at t_q), K4 raises a device flag and the exact
+// list-based kernels above re-run for the whole batch, gated on that flag (no host sync).
+struct FastArgs {
+  const float* U;
+  const float* I;
+  int64_t Q, NI, ldu, ldi;
+  int nsplit;
+  int64_t span;
+  int K, cap;
+  float* cand_s;        // [Q][nsplit][2][T]
+  int* cand_i;
+  const float* thresh;  // [Q]
+  int* count;           // [Q]
+  float* buf_s;         // [Q][cap]
+  int* buf_i;
+};
+
+template <int MODE, int T>
+__global__ __launch_bounds__(256, 2) void topk_fast_scan_k(FastArgs a) {
+  __shared__ __attribute__((aligned(16))) float sI[2][kTile][kLdsStride];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, c = lane & 31;
+  const int b = blockIdx.x;
+  const int nsub = a.nsplit >> 3;
+  const int split = (b & 7) + 8 * ((b >> 3) % nsub);
+  const int rb = (b >> 3) / nsub;
+  const int64_t q = (int64_t)rb * kOwnRows + wave * 32 + c;
+  const bool q_ok = q < a.Q;
+  float u[64];
+  if (q_ok) {
+    const float4* src = reinterpret_cast<const float4*>(a.U + q * a.ldu + h * 64);
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const float4 v = src[t];
+      u[4 * t] = v.x; u[4 * t + 1] = v.y; u[4 * t + 2] = v.z; u[4 * t + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < 64; ++t) u[t] = 0.0f;
+  }
+  const int64_t j_begin = (int64_t)split * a.span;
+  int64_t j_end = j_begin + a.span;
+  if (j_end > a.NI) j_end = a.NI;
+
+  float ts[T];
+  int ti[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) { ts[t] = -INFINITY; ti[t] = 0x7fffffff; }
+  const float th = (MODE == 1 && q_ok) ? a.thresh[q] : INFINITY;
+
+  const int srow = tid >> 3, scol = (tid & 7) * 16;
+  float4 stg[4];
+  auto gload = [&](int64_t j0) {
+    const int64_t j = j0 + srow;
+    if (j < j_end) {
+      const float4* src = reinterpret_cast<const float4*>(a.I + j * a.ldi + scol);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) stg[t] = src[t];
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) stg[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) *reinterpret_cast<float4*>(&sI[buf][srow][scol + 4 * t]) = stg[t];
+  };
+  if (j_begin < j_end) {
+    gload(j_begin);
+    lstore(0);
+    __syncthreads();
+    int cur = 0;
+    for (int64_t j0 = j_begin; j0 < j_end; j0 += kTile) {
+      const bool has_next = j0 + kTile < j_end;
+      if (has_next) gload(j0 + kTile);
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+      const float* xrow = &sI[cur][c][h * 64];
+#pragma unroll
+      for (int s4 = 0; s4 < 64; s4 += 4) {
+        const float4 bv = *reinterpret_cast<const float4*>(xrow + s4);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(bv.x, u[s4 + 0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(bv.y, u[s4 + 1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(bv.z, u[s4 + 2], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(bv.w, u[s4 + 3], acc, 0, 0, 0);
+      }
+      if (q_ok) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int64_t j = j0 + tile_row(r, h);
+          const float sc = acc[r];
+          if (j >= j_end) continue;
+          if (MODE == 0) {
+            if (better(sc, (int)j, ts[T - 1], ti[T - 1])) {  // rare after the first T items
+              ts[T - 1] = sc;
+              ti[T - 1] = (int)j;
+#pragma unroll
+              for (int t = T - 1; t > 0; --t) {
+                if (better(ts[t], ti[t], ts[t - 1], ti[t - 1])) {
+                  const float fs = ts[t]; ts[t] = ts[t - 1]; ts[t - 1] = fs;
+                  const int fi = ti[t]; ti[t] = ti[t - 1]; ti[t - 1] = fi;
+                }
+              }
+            }
+          } else if (sc >= th) {
+            const int pos = atomicAdd(a.count + q, 1);
+            if (pos < a.cap) {
+              a.buf_s[q * a.cap + pos] = sc;
+              a.buf_i[q * a.cap + pos] = (int)j;
+            }
+          }
+        }
+      }
+      if (has_next) lstore(cur ^ 1);  // cur^1 was read in the previous tile, fenced by its barrier
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+  if (MODE == 0 && q_ok) {
+    const int64_t base = ((q * a.nsplit + split) * 2 + h) * T;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      a.cand_s[base + t] = ts[t];
+      a.cand_i[base + t] = ti[t];
+    }
+  }
+}
+
+// bitonic sort of NC (score, idx) pairs in LDS by (score desc, idx asc)
+template <int NC>
+__device__ __forceinline__ void bitonic_desc(float* ss, int* si) {
+  for (int size = 2; size <= NC; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = threadIdx.x; t < NC / 2; t += blockDim.x) {
+        const int lo = 2 * t - (t & (stride - 1));
+        const int hi = lo + stride;
+        const bool desc = ((lo & size) == 0);
+        const float a0 = ss[lo], a1 = ss[hi];
+        const int b0 = si[lo], b1 = si[hi];
+        const bool swap = desc ? better(a1, b1, a0, b0) : better(a0, b0, a1, b1);
+        if (swap) {
+          ss[lo] = a1; ss[hi] = a0;
+          si[lo] = b1; si[hi] = b0;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// K2: t_q = k-th best candidate (or -inf if fewer valid candidates than k); count[q] = 0
+template <int NC>
+__global__ __launch_bounds__(256) void topk_thresh_k(const float* cs, const int* ci, int ncand, int K, float* thresh,
+                                                     int* count) {
+  __shared__ float ss[NC];
+  __shared__ int si[NC];
+  const int64_t q = blockIdx.x;
+  for (int t = threadIdx.x; t < NC; t += blockDim.x) {
+    const bool ok = t < ncand;
+    ss[t] = ok ? cs[q * ncand + t] : -INFINITY;
+    si[t] = ok ? ci[q * ncand + t] : 0x7fffffff;
+  }
+  __syncthreads();
+  bitonic_desc<NC>(ss, si);
+  if (threadIdx.x == 0) {
+    const bool valid = si[K - 1] != 0x7fffffff;
+    thresh[q] = valid ? ss[K - 1] : -INFINITY;
+    count[q] = 0;
+  }
+}
+
+// K4: sort the collected entries and write the top k; overflow -> flag for the fallback
+template <int NC>
+__global__ __launch_bounds__(256) void topk_final_k(const float* bs, const int* bi, const int* count, int cap, int K,
+                                                    float* out_s, int64_t* out_i, int* overflow) {
+  __shared__ float ss[NC];
+  __shared__ int si[NC];
+  const int64_t q = blockIdx.x;
+  const int n = count[q];
+  if (n > cap) {
+    if (threadIdx.x == 0) atomicOr(overflow, 1);
+    return;
+  }
+  for (int t = threadIdx.x; t < NC; t += blockDim.x) {
+    const bool ok = t < n;
+    ss[t] = ok ? bs[q * cap + t] : -INFINITY;
+    si[t] = ok ? bi[q * cap + t] : 0x7fffffff;
+  }
+  __syncthreads();
+  bitonic_desc<NC>(ss, si);
+  for (int t = threadIdx.x; t < K; t += blockDim.x) {
+    out_s[q * K + t] = ss[t];
+    out_i[q * K + t] = (si[t] == 0x7fffffff) ? -1 : (int64_t)si[t];
+  }
+}
+
+constexpr int kFastCap = 2048;
+
+struct FastPlan {
+  bool use;
+  int T, nsplit;
+};
+
+FastPlan fast_plan(int64_t Q, int64_t NI, int64_t k) {
+  FastPlan p;
+  p.T = k <= 128 ? 8 : 16;
+  p.use = NI > 16384 && k <= 512;
+  // enough candidates for a tight threshold (2*ns*T >= 4k), enough workgroups, <= 8192 candidates
+  const int64_t rbs = (Q + kOwnRows - 1) / kOwnRows;
+  int ns = 8;
+  while (ns < 256 && (2 * ns * p.T < 4 * k || rbs * ns < 1024) && NI / (ns * 2) >= 1024 && 2 * ns * 2 * p.T <= 8192)
+    ns *= 2;
+  p.nsplit = ns;
+  if (2 * ns * p.T < k) p.use = false;  // too few candidates for a threshold
+  return p;
+}
+
 int choose_nsplit(int64_t Q, int64_t NI, int kmax) {
   // >= ~1024 workgroups when there are enough items; each split keeps >= 2048 items; the
   // merge sorts at most 8192 candidates per query in LDS (2 * nsplit * kmax <= 8192)
@@ -211,10 +442,70 @@ int choose_nsplit(int64_t Q, int64_t NI, int kmax) {
 
 }  // namespace
 
-RSX_API int64_t rsx_topk_workspace_bytes(int64_t Q, int64_t NI, int64_t k) {
+namespace {
+int64_t old_ws_bytes(int64_t Q, int64_t NI, int64_t k) {
   const int kmax = k <= 128 ? 128 : 512;
   const int ns = choose_nsplit(Q, NI, kmax);
-  return Q * ns * 2 * (int64_t)kmax * 8 + 256;
+  return Q * ns * 2 * (int64_t)kmax * 8;
+}
+int64_t align256(int64_t x) { return (x + 255) / 256 * 256; }
+struct FastLayout {
+  int64_t thresh, count, cand_s, cand_i, buf_s, buf_i, fallback, total;
+};
+FastLayout fast_layout(int64_t Q, int64_t NI, int64_t k, const FastPlan& p) {
+  FastLayout L;
+  L.thresh = 256;
+  L.count = L.thresh + align256(Q * 4);
+  L.cand_s = L.count + align256(Q * 4);
+  const int64_t nc = Q * p.nsplit * 2 * (int64_t)p.T;
+  L.cand_i = L.cand_s + align256(nc * 4);
+  L.buf_s = L.cand_i + align256(nc * 4);
+  L.buf_i = L.buf_s + align256(Q * (int64_t)kFastCap * 4);
+  const int64_t fast_end = L.buf_i + align256(Q * (int64_t)kFastCap * 4);
+  L.fallback = L.cand_s;  // the exact fallback reuses the candidate/buffer region after K4
+  const int64_t fb_end = L.fallback + old_ws_bytes(Q, NI, k);
+  L.total = (fast_end > fb_end ? fast_end : fb_end) + 256;
+  return L;
+}
+
+int launch_old(const float* U, int64_t ldu, const float* I, int64_t ldi, int64_t Q, int64_t NI, int64_t k,
+               char* ws, float* out_scores, int64_t* out_idx, const int* gate, hipStream_t st) {
+  const int kmax = k <= 128 ? 128 : 512;
+  ScanArgs a;
+  a.gate = gate;
+  a.U = U; a.I = I; a.Q = Q; a.NI = NI; a.ldu = ldu; a.ldi = ldi;
+  a.nsplit = choose_nsplit(Q, NI, kmax);
+  a.span = ((NI + a.nsplit - 1) / a.nsplit + kTile - 1) / kTile * kTile;
+  if (a.span < kTile) a.span = kTile;
+  a.K = (int)k;
+  a.cs = reinterpret_cast<float*>(ws);
+  a.ci = reinterpret_cast<int*>(ws + Q * a.nsplit * 2 * (int64_t)kmax * 4);
+  const int blocks = (int)(((Q + kOwnRows - 1) / kOwnRows) * a.nsplit);
+  if (kmax == 128) hipLaunchKernelGGL(topk_scan_k<128>, dim3(blocks), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(topk_scan_k<512>, dim3(blocks), dim3(256), 0, st, a);
+  RSX_LAUNCHED();
+  const int ncand = a.nsplit * 2 * kmax;
+  if (ncand <= 2048)
+    hipLaunchKernelGGL(topk_merge_k<2048>, dim3((unsigned)Q), dim3(256), 0, st, a.cs, a.ci, Q, ncand, (int)k,
+                       out_scores, out_idx, gate);
+  else
+    hipLaunchKernelGGL(topk_merge_k<8192>, dim3((unsigned)Q), dim3(256), 0, st, a.cs, a.ci, Q, ncand, (int)k,
+                       out_scores, out_idx, gate);
+  RSX_LAUNCHED();
+  return 0;
+}
+
+template <int T>
+void launch_fast_scans(FastArgs f, int blocks, int mode, hipStream_t st) {
+  if (mode == 0) hipLaunchKernelGGL((topk_fast_scan_k<0, T>), dim3(blocks), dim3(256), 0, st, f);
+  else hipLaunchKernelGGL((topk_fast_scan_k<1, T>), dim3(blocks), dim3(256), 0, st, f);
+}
+}  // namespace
+
+RSX_API int64_t rsx_topk_workspace_bytes(int64_t Q, int64_t NI, int64_t k) {
+  const FastPlan p = fast_plan(Q, NI, k);
+  if (!p.use) return old_ws_bytes(Q, NI, k) + 256;
+  return fast_layout(Q, NI, k, p).total;
 }
 
 // scores [Q, k] (desc), idx [Q, k] int64 (-1 where fewer than k items exist).
@@ -226,26 +517,44 @@ RSX_API int rsx_retrieve_topk(const float* U, int64_t ldu, const float* I, int64
   RSX_ARG(NI < 0x7fffffff, "item count must fit int32");
   if (Q == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  const int kmax = k <= 128 ? 128 : 512;
-  ScanArgs a;
-  a.U = U; a.I = I; a.Q = Q; a.NI = NI; a.ldu = ldu; a.ldi = ldi;
-  a.nsplit = choose_nsplit(Q, NI, kmax);
-  a.span = ((NI + a.nsplit - 1) / a.nsplit + kTile - 1) / kTile * kTile;
-  if (a.span < kTile) a.span = kTile;
-  a.K = (int)k;
-  a.cs = reinterpret_cast<float*>(ws);
-  a.ci = reinterpret_cast<int*>(reinterpret_cast<char*>(ws) + Q * a.nsplit * 2 * (int64_t)kmax * 4);
-  const int blocks = (int)(((Q + kOwnRows - 1) / kOwnRows) * a.nsplit);
-  if (kmax == 128) hipLaunchKernelGGL(topk_scan_k<128>, dim3(blocks), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(topk_scan_k<512>, dim3(blocks), dim3(256), 0, st, a);
+  char* w = reinterpret_cast<char*>(ws);
+  const FastPlan p = fast_plan(Q, NI, k);
+  if (!p.use) return launch_old(U, ldu, I, ldi, Q, NI, k, w, out_scores, out_idx, nullptr, st);
+  const FastLayout L = fast_layout(Q, NI, k, p);
+  int* flag = reinterpret_cast<int*>(w);
+  (void)hipMemsetAsync(flag, 0, sizeof(int), st);
+  FastArgs f;
+  f.U = U; f.I = I; f.Q = Q; f.NI = NI; f.ldu = ldu; f.ldi = ldi;
+  f.nsplit = p.nsplit;
+  f.span = ((NI + p.nsplit - 1) / p.nsplit + kTile - 1) / kTile * kTile;
+  if (f.span < kTile) f.span = kTile;
+  f.K = (int)k;
+  f.cap = kFastCap;
+  f.cand_s = reinterpret_cast<float*>(w + L.cand_s);
+  f.cand_i = reinterpret_cast<int*>(w + L.cand_i);
+  f.thresh = reinterpret_cast<const float*>(w + L.thresh);
+  f.count = reinterpret_cast<int*>(w + L.count);
+  f.buf_s = reinterpret_cast<float*>(w + L.buf_s);
+  f.buf_i = reinterpret_cast<int*>(w + L.buf_i);
+  const int blocks = (int)(((Q + kOwnRows - 1) / kOwnRows) * p.nsplit);
+  if (p.T == 8) launch_fast_scans<8>(f, blocks, 0, st);
+  else launch_fast_scans<16>(f, blocks, 0, st);
   RSX_LAUNCHED();
-  const int ncand = a.nsplit * 2 * kmax;
+  const int ncand = p.nsplit * 2 * p.T;
+  float* th = reinterpret_cast<float*>(w + L.thresh);
   if (ncand <= 2048)
-    hipLaunchKernelGGL(topk_merge_k<2048>, dim3((unsigned)Q), dim3(256), 0, st, a.cs, a.ci, Q, ncand, (int)k,
-                       out_scores, out_idx);
+    hipLaunchKernelGGL(topk_thresh_k<2048>, dim3((unsigned)Q), dim3(256), 0, st, f.cand_s, f.cand_i, ncand, (int)k,
+                       th, f.count);
   else
-    hipLaunchKernelGGL(topk_merge_k<8192>, dim3((unsigned)Q), dim3(256), 0, st, a.cs, a.ci, Q, ncand, (int)k,
-                       out_scores, out_idx);
+    hipLaunchKernelGGL(topk_thresh_k<8192>, dim3((unsigned)Q), dim3(256), 0, st, f.cand_s, f.cand_i, ncand, (int)k,
+                       th, f.count);
   RSX_LAUNCHED();
-  return 0;
+  if (p.T == 8) launch_fast_scans<8>(f, blocks, 1, st);
+  else launch_fast_scans<16>(f, blocks, 1, st);
+  RSX_LAUNCHED();
+  hipLaunchKernelGGL(topk_final_k<kFastCap>, dim3((unsigned)Q), dim3(256), 0, st, f.buf_s, f.buf_i, f.count,
+                     kFastCap, (int)k, out_scores, out_idx, flag);
+  RSX_LAUNCHED();
+  // exact fallback for the whole batch, a no-op unless some query overflowed its buffer
+  return launch_old(U, ldu, I, ldi, Q, NI, k, w + L.fallback, out_scores, out_idx, flag, st);
 }

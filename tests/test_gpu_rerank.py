@@ -89,3 +89,29 @@ def test_reranking_system_deepfm(gpu):
     assert len(recs) == 10
     scores = [r["final_score"] for r in recs]
     assert scores == sorted(scores, reverse=True)
+
+
+@pytest.mark.parametrize("Q,NI,k", [(130, 100003, 100), (70, 60000, 500), (257, 40000, 7)])
+def test_retrieve_topk_fast_path_bit_exact(gpu, Q, NI, k):
+    """Large corpora take the candidate -> threshold -> collect path: on dyadic inputs (exact
+    dot products, many exact ties) the result must equal the oracle's (score desc, index asc)."""
+    g = torch.Generator().manual_seed(Q * 7 + k)
+    U = torch.randint(-4, 5, (Q, 128), generator=g).float() / 8.0
+    I = torch.randint(-4, 5, (NI, 128), generator=g).float() / 8.0
+    s, i = ops.retrieve_topk(U.to(gpu), I.to(gpu), k)
+    rs, ri = OR.retrieve_topk(U, I, k)
+    assert torch.equal(i.cpu(), ri)
+    assert torch.equal(s.cpu().double(), rs)
+
+
+def test_retrieve_topk_fast_path_overflow_fallback(gpu):
+    """Massive exact ties at the threshold (a corpus of 40k copies of a few rows) overflow the
+    per-query buffers; the gated exact fallback must still return the oracle's result."""
+    g = torch.Generator().manual_seed(11)
+    base = torch.randint(-4, 5, (5, 128), generator=g).float() / 8.0
+    I = base[torch.randint(0, 5, (40000,), generator=g)]
+    U = torch.randint(-4, 5, (33, 128), generator=g).float() / 8.0
+    s, i = ops.retrieve_topk(U.to(gpu), I.to(gpu), 100)
+    rs, ri = OR.retrieve_topk(U, I, 100)
+    assert torch.equal(i.cpu(), ri)
+    assert torch.equal(s.cpu().double(), rs)
