@@ -108,18 +108,25 @@ _SEQ_ID_KEYS = ("item_ids", "time_bucket_ids", "type_ids", "color_ids", "graphic
 
 
 def packed_views(model, batch, pretrained_vecs=None, pretrained_lookup=None):
-    """Both dropout views (reference :788-789) on the packed token set of the step.
-    Returns (packed tokens, out_1 [T, D], out_2 [T, D])."""
-    pk = PackedTokens(batch["padding_mask"])
-    tok_ids = [pk.take(batch[k]) for k in _SEQ_ID_KEYS]
+    """Both dropout views (reference :788-789) on the packed token set of the step, run as ONE
+    packed pass over the doubled batch: users b and B + b carry the same inputs, so view 1 is
+    tokens [0, T) and view 2 tokens [T, 2T) of the output. The views still draw independent
+    dropout masks (the kernels key their masks by token row; torch dropout is per element), and
+    every kernel launch covers both views (half the launches, no per-parameter gradient adds).
+    Returns (packed tokens of one view, out_1 [T, D], out_2 [T, D])."""
+    pm = batch["padding_mask"]
+    pk = PackedTokens(pm)
+    pk2 = PackedTokens(torch.cat([pm, pm]))
+    T = pk.flat.numel()
+    tok_ids = [torch.cat([t, t]) for t in (pk.take(batch[k]) for k in _SEQ_ID_KEYS)]
     if pretrained_vecs is not None:
         pv_tok = pk.take(pretrained_vecs)
     else:
-        pv_tok = ops.gather_rows(pretrained_lookup, tok_ids[0])
-    static = [batch[k] for k in _STATIC_KEYS]
-    out1 = model.forward_packed(pk, pv_tok, tok_ids, *static)
-    out2 = model.forward_packed(pk, pv_tok, tok_ids, *static)
-    return pk, out1, out2
+        pv_tok = ops.gather_rows(pretrained_lookup, tok_ids[0][:T])
+    pv_tok = torch.cat([pv_tok, pv_tok])
+    static = [torch.cat([batch[k], batch[k]]) for k in _STATIC_KEYS]
+    out = model.forward_packed(pk2, pv_tok, tok_ids, *static)
+    return pk, out[:T], out[T:]
 
 
 def contrastive_losses(model, item_tower, log_q_tensor, batch, cfg, pretrained_vecs=None, pretrained_lookup=None):
