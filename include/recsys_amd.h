@@ -135,6 +135,19 @@ int rsx_nce_grouped_bwd(const float* A, const float* B, const float* bias, const
                         int nsplit, const float* gout, float* ws, float* dA, float* dB, int accumulate,
                         void* stream);
 
+/* ---- static-profile embeddings: gated lookups of several tiny tables, concatenated ------
+ * out[b, off_j + c] = E_j[ids_j[b]][c] * gate[j]; backward accumulates dE_j (padding_idx rows
+ * skipped) and dgate[j] (both added into). Replaces the nine nn.Embedding lookups x u_g of
+ * tower_code/v1_refine_usertower.py:472-494 (and their sort-based embedding backward).
+ * <= 16 tables, <= 256 columns, <= 4096 table floats in total. */
+int rsx_static_embed_fwd(const int64_t* const* ids, const float* const* tables, const int64_t* table_rows,
+                         const int64_t* dims, int ntab, const float* gate, int64_t B, float* out, int64_t ld_out,
+                         void* stream);
+int rsx_static_embed_bwd(const int64_t* const* ids, const float* const* tables, const int64_t* table_rows,
+                         const int64_t* dims, const int64_t* padding_idx, int ntab, const float* gate,
+                         const float* dout, int64_t ld_dout, int64_t B, float* const* dtables, float* dgate,
+                         void* stream);
+
 /* ---- LayerNorm fused with the preceding residual add + dropout and a following GELU ----
  * s = x + dropout(res) (res nullable), y = act(LN(s) * w + b), act 0 none / 2 GELU(erf).
  * Replaces norm1/norm2 and the residual adds of the norm_first TransformerEncoderLayer and the

@@ -398,6 +398,53 @@ def nce_grouped_sum(A, B_distinct, bias, groups: TargetGroups, tau=0.1, tag="nce
 
 
 # ----------------------------------------------------------------------------------------
+# Static-profile embeddings (several tiny gated tables, concatenated): rsx_static_embed_*
+class _StaticEmbed(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gate, ids, padding_idx, *tables):
+        N.ensure_device(gate)
+        ids = [_c(t) for t in ids]
+        tables = [_c(t) for t in tables]
+        B = ids[0].shape[0]
+        dims = [t.shape[1] for t in tables]
+        out = torch.empty(B, sum(dims), device=gate.device, dtype=torch.float32)
+        gate = _c(gate)
+        rc = N.lib().rsx_static_embed_fwd(N.ptr_array(ids), N.ptr_array(tables),
+                                          N.i64_array([t.shape[0] for t in tables]), N.i64_array(dims), len(tables),
+                                          N.ptr(gate), B, N.ptr(out), out.stride(0), N.stream())
+        N.check(rc, "static_embed_fwd")
+        ctx.save_for_backward(gate, *ids, *tables)
+        ctx.cfg = (len(tables), list(padding_idx))
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        nt, pad = ctx.cfg
+        saved = ctx.saved_tensors
+        gate, ids, tables = saved[0], list(saved[1:1 + nt]), list(saved[1 + nt:1 + 2 * nt])
+        need = ctx.needs_input_grad
+        dgate = torch.zeros_like(gate) if need[0] else None
+        dtabs = [torch.zeros_like(t) if need[3 + j] else None for j, t in enumerate(tables)]
+        dout = _c(dout)
+        rc = N.lib().rsx_static_embed_bwd(N.ptr_array(ids), N.ptr_array(tables),
+                                          N.i64_array([t.shape[0] for t in tables]),
+                                          N.i64_array([t.shape[1] for t in tables]), N.i64_array(pad), nt,
+                                          N.ptr(gate), N.ptr(dout), dout.stride(0), ids[0].shape[0],
+                                          N.ptr_array(dtabs), N.ptr(dgate), N.stream())
+        N.check(rc, "static_embed_bwd")
+        return (dgate, None, None, *dtabs)
+
+
+def static_embed(ids, tables, gate, padding_idx=None):
+    """cat_j(tables[j][ids[j]] * gate[j]) -> [B, sum_j dim_j] (nn.Embedding padding_idx
+    semantics for the gradient)."""
+    if padding_idx is None:
+        padding_idx = [-1] * len(tables)
+    padding_idx = [(-1 if p is None else int(p)) for p in padding_idx]
+    return _StaticEmbed.apply(gate, list(ids), padding_idx, *tables)
+
+
+# ----------------------------------------------------------------------------------------
 # LayerNorm (+ residual add + dropout before it, + GELU after it): rsx_ln_fwd / rsx_ln_bwd
 ACT_GELU_ERF = 2
 

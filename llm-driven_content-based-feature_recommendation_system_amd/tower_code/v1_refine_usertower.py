@@ -183,13 +183,14 @@ class SASRecUserTower(nn.Module):
 
     def _static_profile(self, age_bucket, price_bucket, cnt_bucket, recency_bucket, channel_ids, club_status_ids,
                         news_freq_ids, fn_ids, active_ids, cont_feats, u_g):
-        # Phase 2: static encoding (reference :472-494)
-        static_input = torch.cat([
-            self.age_emb(age_bucket) * u_g[0], self.price_emb(price_bucket) * u_g[1],
-            self.cnt_emb(cnt_bucket) * u_g[2], self.recency_emb(recency_bucket) * u_g[3],
-            self.channel_emb(channel_ids) * u_g[4], self.club_status_emb(club_status_ids) * u_g[5],
-            self.news_freq_emb(news_freq_ids) * u_g[6], self.fn_emb(fn_ids) * u_g[7],
-            self.active_emb(active_ids) * u_g[8], F.relu(self.cont_proj(cont_feats)) * u_g[9]], dim=1)
+        # Phase 2: static encoding (reference :472-494): the nine gated lookups in one kernel
+        # (rsx_static_embed), then relu(cont_proj(cont)) * u_g[9], static_mlp.
+        embs = [self.age_emb, self.price_emb, self.cnt_emb, self.recency_emb, self.channel_emb,
+                self.club_status_emb, self.news_freq_emb, self.fn_emb, self.active_emb]
+        ids = [age_bucket, price_bucket, cnt_bucket, recency_bucket, channel_ids, club_status_ids, news_freq_ids,
+               fn_ids, active_ids]
+        looked = ops.static_embed(ids, [e.weight for e in embs], u_g[:9], [e.padding_idx for e in embs])
+        static_input = torch.cat([looked, F.relu(self.cont_proj(cont_feats)) * u_g[9]], dim=1)
         return self.static_mlp(static_input)
 
     def forward_packed(self, packed, pretrained_tok, tok_ids, age_bucket, price_bucket, cnt_bucket, recency_bucket,
