@@ -8,8 +8,11 @@ all-time-steps LogQ in-batch loss (N ~ 75.7k valid positions, N x N implicit log
 (InfoNCE + SupCon), backward, clip_grad_norm_(5.0), AdamW (item matrix unfrozen, lr x 0.05:
 the reference's epoch >= 2 steady state). Inputs are resident in HBM before timing.
 
-Multi-GPU (torchrun, one process per GPU, RCCL): the global batch stays fixed (strong
-scaling) and is split by users across ranks; see dist.py. Prints ONE JSON line on rank 0.
+Multi-GPU (torchrun, one process per GPU, RCCL): by default every GPU holds 4096 users, so the
+global batch is 4096 x N (weak scaling; N=8 is configs[3], global batch 32 768 with the
+all-gathered negative pool). ``--batch G`` fixes the global batch instead (strong scaling; the
+N=1 run at G=32768 is the single-GPU end of configs[3]). Users are split by rank; see dist.py.
+Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
@@ -37,7 +40,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=4096, help="global batch (users)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="fixed global batch (users) for every N: strong scaling. Default: --batch-per-gpu x N")
+    ap.add_argument("--batch-per-gpu", type=int, default=4096,
+                    help="users per GPU when --batch is not given (weak scaling; N=8 -> 32768 = configs[3])")
     ap.add_argument("--items", type=int, default=47_062)
     ap.add_argument("--dropout", type=float, default=0.2)
     ap.add_argument("--freeze-items", action="store_true", help="epoch-1 regime (item matrix frozen)")
@@ -217,6 +223,9 @@ def bench_item_tower(args, device):
 def main():
     args = parse()
     rank, world, device = setup_dist(args)
+    scaling = "strong" if args.batch is not None else "weak"
+    if args.batch is None:
+        args.batch = args.batch_per_gpu * world
     if args.blas == "rocblas":
         torch.backends.cuda.preferred_blas_library("hipblas")
     elif args.blas == "hipblaslt":
@@ -320,13 +329,15 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(1e3 * elapsed / args.steps, 3),
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "fp32+bf16x3" if x3 else "fp32",
         "data": "synthetic (seeded H&M-shaped users/items: sample-calibrated lengths, Zipf(1.0) items; "
                 "random-init weights)",
         "config": {"workload": "user-tower two-view contrastive train step (fwd x2 + LogQ in-batch loss + "
-                               "DuoRec + bwd + clip + AdamW), BASELINE configs[1]",
+                               "DuoRec + bwd + clip + AdamW), BASELINE configs[1] at N=1 (global batch 4096), "
+                               "configs[3] at N=8 (global batch 32768, all-gathered negatives)",
+                   "users_per_gpu": args.batch // world,
                    "global_batch": args.batch, "seq_len": 50, "d_model": 128, "items": args.items,
                    "valid_positions_per_batch": [sum(c) for c in n_glob],
                    "distinct_targets_per_batch": n_dist, "dropout": args.dropout,
