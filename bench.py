@@ -31,7 +31,7 @@ FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32-input MFMA (= f
 BF16_MFMA_PEAK_TFLOPS = 16 * FP32_MFMA_PEAK_TFLOPS  # 2516.8: dense bf16 MFMA (16x the f32 rate, same guide)
 # bf16x3: every fp32-equivalent FLOP is three bf16 MFMA products (hi*hi + hi*lo + lo*hi)
 BF16X3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 3
-TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_nce_bwd_rows_traffic.json")
+TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_nce_fwdg_traffic.json")
 HBM_PEAK_GBS = 8000.0
 
 
@@ -298,25 +298,30 @@ def main():
     elapsed = float(elapsed.item())
     total_loss = float(losses[0].item())
 
-    # roofline of the dominant kernel: the main-loss InfoNCE backward, row-owned pass (grouped
-    # form: S recompute + dU product over N_local x D distinct-target columns). Algorithmic
-    # FLOPs per launch = 4 * N_local * D * 128 (2 * N * D * d per product; SURVEY.md 8d counts
-    # 2 N^2 d per product for the ungrouped reference formulation). Peak: the MFMA rate of the
-    # arithmetic used — fp32 MFMA, or bf16 MFMA / 3 for the bf16x3 split products.
+    # roofline of the dominant kernel. bf16x3 (default): the main loss's forward fused with the
+    # row gradient (nce_grouped_fwdg_x3_k: S plus the P x B product over N_local x D
+    # distinct-target columns); fp32: the backward's row-owned pass (S recompute + dU product).
+    # Algorithmic FLOPs per launch = 4 * N_local * D * 128 either way (2 * N * D * d per
+    # product; SURVEY.md 8d counts 2 N^2 d per product for the ungrouped reference formulation).
+    # Peak: the MFMA rate of the arithmetic used: fp32 MFMA, or bf16 MFMA / 3 for the bf16x3
+    # split products. The timed window is the op's launches (fused kernel + B split + merge).
     flops = 0.0
     for i in range(args.steps):
         cnts = n_glob[i % 2]
         flops += 4.0 * cnts[rank] * n_dist[i % 2] * 128
-    launches, ms = kernel_times.get("main/nce_bwd_rows", (0, 0.0))
+    x3 = args.nce_precision == "bf16x3"
+    fused = x3 and ops._NCE_FUSED_ROWGRAD
+    timer = "main/nce_fwd" if fused else "main/nce_bwd_rows"
+    launches, ms = kernel_times.get(timer, (0, 0.0))
     avg_s = (ms / 1e3) / max(launches, 1)
     achieved = (flops / max(launches, 1)) / avg_s / 1e12 if launches else None
-    x3 = args.nce_precision == "bf16x3"
     peak = BF16X3_PEAK_TFLOPS if x3 else FP32_MFMA_PEAK_TFLOPS
     traffic = None
     if os.path.exists(TRAFFIC_FILE):
         with open(TRAFFIC_FILE) as f:
             tr = json.load(f)
-        if tr.get("precision") == args.nce_precision and tr.get("global_batch") == args.batch and world == 1:
+        if (tr.get("precision") == args.nce_precision and tr.get("global_batch") == args.batch and world == 1
+                and fused):
             traffic = tr.get("hbm_bytes_per_launch")
 
     kt = {k: {"launches": n, "avg_ms": round(t / max(n, 1), 4)} for k, (n, t) in sorted(kernel_times.items())}
@@ -344,8 +349,10 @@ def main():
                    "item_matrix": "frozen" if args.freeze_items else "unfrozen (lr x0.05)",
                    "parallelism": f"dp{world} (users split by rank, RCCL all-gather of ids/z, grad all-reduce)",
                    "dense_projection_blas": args.blas, "nce_logit_precision": args.nce_precision},
-        "roofline": {"kernel": ("nce_grouped_bwd_x3_k<true>" if x3 else "nce_grouped_bwd_k<true>")
-                     + " (main LogQ loss backward, row-owned)", "bound": "mfma",
+        "roofline": {"kernel": ("nce_grouped_fwdg_x3_k (main LogQ loss forward fused with the row gradient)"
+                                if fused else ("nce_grouped_bwd_x3_k<true>" if x3 else "nce_grouped_bwd_k<true>")
+                                + " (main LogQ loss backward, row-owned)"),
+                     "timer": timer, "bound": "mfma",
                      "achieved": round(achieved, 2) if achieved else None, "peak": round(peak, 1),
                      "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
                      "traffic": traffic, "traffic_source": os.path.basename(TRAFFIC_FILE) if traffic else None,

@@ -116,8 +116,8 @@ int rsx_nce_bwd(const float* A, const float* B, const float* bias, const int* k1
  * Rows of one user must be contiguous (flat (b, t) order). FLOPs: N*D instead of N*N.
  * precision: RSX_NCE_FP32 (0) = logits on the fp32-input MFMA (exact fp32 products);
  *            RSX_NCE_BF16X3 (1) = logits as hi*hi + hi*lo + lo*hi of a bf16 hi/lo split
- *            (fp32 accumulate, max |dot error| ~3e-6 on unit vectors), 5.3x fewer MFMA cycles.
- * The gradient product (dS x rows) is fp32 MFMA in both modes. */
+ *            (fp32 accumulate, max |dot error| ~3e-6 on unit vectors), 5.3x fewer MFMA cycles;
+ *            the gradient products (dS x rows) use the same split. */
 #define RSX_NCE_FP32 0
 #define RSX_NCE_BF16X3 1
 /* ws for the grouped pair: >= rsx_nce_grouped_workspace_floats(N, D, nsplit_fwd, 8, precision)
@@ -128,6 +128,17 @@ int rsx_nce_grouped_fwd(const float* A, const float* B, const float* bias, const
                         const int* row_beg, const int* row_end, const int* exc_cols, int64_t N, int64_t D,
                         int64_t lda, int64_t ldb, float tau, int precision, int nsplit, float* ws, float* out2,
                         void* stream);
+/* Forward fused with the row-side gradient (bf16x3 only): same loss as rsx_nce_grouped_fwd
+ * (out2, and lse in ws for a later column pass), plus ga [N][128] = d(sum of row losses)/dA
+ * per unit upstream gradient, i.e. dA = gout * ga. The row gradient is a softmax-weighted sum
+ * of B's rows (an attention output), accumulated in the same sweep over S as the loss, so the
+ * backward runs only the column pass (rsx_nce_grouped_bwd with dA = NULL). nsplit in
+ * {1, 2, 4, 8}. Replaces the forward of the reference's live loss
+ * (tower_code/v1_usertower_train.py:787-845) plus the row half of its autograd backward. */
+int rsx_nce_grouped_fwd_grad(const float* A, const float* B, const float* bias, const float* colcnt,
+                             const int* row_col, const int* row_beg, const int* row_end, const int* exc_cols,
+                             int64_t N, int64_t D, int64_t lda, int64_t ldb, float tau, int nsplit, float* ws,
+                             float* out2, float* ga, void* stream);
 int rsx_nce_grouped_bwd(const float* A, const float* B, const float* bias, const float* colcnt, const int* row_col,
                         const int* row_beg, const int* row_end, const int* exc_cols, const int* col_beg,
                         const int* col_end, const int* exc_s, const int* exc_e, const int* exc_n, int64_t N,

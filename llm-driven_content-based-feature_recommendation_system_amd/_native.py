@@ -12,7 +12,7 @@ import threading
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librecsys_amd.so")
+LIB_PATH = os.environ.get("RSX_LIB_PATH") or os.path.join(_HERE, "librecsys_amd.so")  # override: A/B builds
 
 _lock = threading.Lock()
 _lib = None
@@ -43,6 +43,8 @@ _SIGS = {
     "rsx_nce_grouped_workspace_floats": (c_i64, [c_i64, c_i64, c_i, c_i, c_i]),
     "rsx_nce_grouped_fwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_f, c_i, c_i,
                                   c_p, c_p, c_p]),
+    "rsx_nce_grouped_fwd_grad": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_f, c_i,
+                                       c_p, c_p, c_p, c_p]),
     "rsx_nce_grouped_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64,
                                   c_i64, c_i64, c_f, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_i, c_p]),
     "rsx_deepfm_embed": (c_i, [c_p, c_i64, c_i, c_i, c_p, c_p, c_f, c_p, c_p, c_p]),

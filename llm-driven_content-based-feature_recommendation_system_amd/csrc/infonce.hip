@@ -1015,6 +1015,8 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
+// s_waitcnt vmcnt(0) (expcnt, lgkmcnt left at their maxima): gfx9 encoding
+constexpr int kVmcnt0 = 0x0F70;
 
 // [32][128] bf16 image: 320-B rows plus a 16-B skew per 8-row group, i.e. byte offset
 // 320*row + 16*(row>>3) + 2*col. Conflict-free for the row reads (ds_read_b128, lane (c,h)
@@ -1125,22 +1127,13 @@ __device__ __forceinline__ f32x16 dots_x3(const X3Tile& t, int c, int h, const b
   return acc;
 }
 
-// gacc[nb] += G^T X over the tile: G = the 32x32 gradient tile (acc layout: streamed row
-// tile_row(r,h) in register r, owner on the lane). k-step ks takes registers 8ks..8ks+7, i.e.
-// streamed rows 16ks + 8(j>>2) + 4h + (j&3); the B fragment is those rows of dims 32nb + c,
-// two transposed 4-row reads per image. Steps (ks, nb) are software-pipelined by one.
-__device__ __forceinline__ void grad_x3(f32x16 (&gacc)[4], const f32x16& g, const X3Tile& t, int lane) {
+// gacc[nb] += G^T X over the tile, G given as its hi/lo bf16 fragments (acc layout: streamed
+// row tile_row(r,h) in register r, owner on the lane; k-step ks takes registers 8ks..8ks+7,
+// i.e. streamed rows 16ks + 8(j>>2) + 4h + (j&3)). The B fragment is those rows of dims
+// 32nb + c, two transposed 4-row reads per image. Steps (ks, nb) are software-pipelined by one.
+__device__ __forceinline__ void grad_x3s(f32x16 (&gacc)[4], const bf16x8 (&gh)[2], const bf16x8 (&gl)[2],
+                                         const X3Tile& t, int lane) {
   const int q = (lane >> 2) & 3, p = lane & 3, h = lane >> 5, cb = (lane >> 4) & 1;
-  bf16x8 gh[2], gl[2];
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float x = g[8 * ks + j];
-      const __bf16 hj = (__bf16)x;
-      gh[ks][j] = hj;
-      gl[ks][j] = (__bf16)(x - (float)hj);
-    }
   const int base = img_off(4 * h + q, 16 * cb + 4 * p);  // + img_off(16ks + 8half, 32nb) - img_off(0,0)
   auto rd = [&](const __bf16* img, int step, bf16x8& out) {
     const int ks = step >> 2, nb = step & 3;
@@ -1167,6 +1160,77 @@ __device__ __forceinline__ void grad_x3(f32x16 (&gacc)[4], const f32x16& g, cons
     bh = nh;
     bl = nl;
   }
+}
+
+__device__ __forceinline__ void split_tile(const f32x16& g, bf16x8 (&gh)[2], bf16x8 (&gl)[2]) {
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float x = g[8 * ks + j];
+      const __bf16 hj = (__bf16)x;
+      gh[ks][j] = hj;
+      gl[ks][j] = (__bf16)(x - (float)hj);
+    }
+}
+
+// The backward's software pipeline: the S tile of the NEXT streamed tile (MFMA, returned) runs
+// interleaved with the gradient tile of the CURRENT one (VALU), so the exp/split work of a
+// wave fills its own MFMA issue gaps instead of waiting for the S chain to drain:
+//   g_r = f_r * 2^(S_r * it2 - (m0[tr] + o_m2)),  f_r = ROW ? fo * m1[tr] : fo,  tr = tile_row(r, h)
+// split to hi/lo fragments, two rows of G per k-step. The tile's metadata comes in as b128
+// reads two k-steps ahead of use. MFMA = false: the G half alone (the last tile of a split).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+template <bool ROW, bool MFMA>
+__device__ __forceinline__ f32x16 dots_g_x3(const X3Tile& t, int c, int h, const bf16x8 (&uh)[8],
+                                            const bf16x8 (&ul)[8], const f32x16& S, const float* m0,
+                                            const float* m1, float o_m2, float it2, float fo, bf16x8 (&gh)[2],
+                                            bf16x8 (&gl)[2]) {
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+  const int base = img_off(c, 64 * h);
+  bf16x8 ah, al;
+  if (MFMA) {
+    ah = *reinterpret_cast<const bf16x8*>(&t.hi[base]);
+    al = *reinterpret_cast<const bf16x8*>(&t.lo[base]);
+  }
+  f32x4 q0 = *reinterpret_cast<const f32x4*>(m0 + 4 * h), q1 = q0, n0 = q0, n1 = q0;
+  if (ROW) q1 = *reinterpret_cast<const f32x4*>(m1 + 4 * h);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    bf16x8 nh = ah, nl = al;
+    if (MFMA && s < 7) {
+      nh = *reinterpret_cast<const bf16x8*>(&t.hi[base + 8 * (s + 1)]);
+      nl = *reinterpret_cast<const bf16x8*>(&t.lo[base + 8 * (s + 1)]);
+    }
+    if ((s & 1) == 0 && s < 6) {  // rows of k-steps s+2, s+3
+      n0 = *reinterpret_cast<const f32x4*>(m0 + 8 * ((s >> 1) + 1) + 4 * h);
+      if (ROW) n1 = *reinterpret_cast<const f32x4*>(m1 + 8 * ((s >> 1) + 1) + 4 * h);
+    }
+    if (MFMA) {
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, uh[s], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, ul[s], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, uh[s], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      const int r = 2 * s + rr, e = r & 3;
+      const float f = ROW ? fo * q1[e] : fo;
+      const float g = f * __builtin_amdgcn_exp2f(fmaf(S[r], it2, -(q0[e] + o_m2)));
+      const __bf16 hi = (__bf16)g;
+      gh[r >> 3][r & 7] = hi;
+      gl[r >> 3][r & 7] = (__bf16)(g - (float)hi);
+    }
+    if (s & 1) {
+      q0 = n0;
+      q1 = n1;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    ah = nh;
+    al = nl;
+  }
+  return acc;
 }
 
 __global__ __launch_bounds__(256, 2) void nce_grouped_fwd_x3_k(GArgs a) {
@@ -1293,12 +1357,31 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_fwd_x3_k(GArgs a) {
   }
 }
 
+#ifndef RSX_BWD_X3_OCC
+#define RSX_BWD_X3_OCC 2
+#endif
+#ifndef RSX_BWD_X3_PIPE
+#define RSX_BWD_X3_PIPE 0
+#endif
+#ifndef RSX_BWD_VMCNT0
+#define RSX_BWD_VMCNT0 1
+#endif
+// Backward of the grouped loss (bf16x3). Per streamed tile: S = owner x streamed rows, then
+// G = w * 2^(S log2e / tau - ...) (- 1 on the label), then G^T X into the owner's gradient.
+// Ordering rules that keep the staging loads in flight (vmcnt counts in order, so a wait on
+// any later load drains the prefetch): the per-tile exception flag (and the column pass's
+// window update, which may load) runs BEFORE the prefetch is issued, and an explicit
+// vmcnt(0) before each barrier leaves no load pending at the loop head on any path, so the
+// common path never waits on memory before its LDS store. Only the rare exception tiles
+// load after the prefetch. PIPE: the S tile of tile t+1 runs
+// interleaved with G of tile t (dots_g_x3) over a three-deep LDS ring.
 template <bool ROW_OWNED>
-__global__ __launch_bounds__(256, 2) void nce_grouped_bwd_x3_k(GArgs a) {
-  __shared__ __attribute__((aligned(16))) X3Tile sT[2];
-  __shared__ __attribute__((aligned(16))) float sM0[2][kTile];  // rows: bias_d*log2e | cols: lse_i*log2e (+inf past the split)
-  __shared__ __attribute__((aligned(16))) float sM1[2][kTile];  // rows: c_d (0 past the split) | cols: unused
-  __shared__ __attribute__((aligned(16))) int sM2[2][kTile];    // cols: d(i)
+__global__ __launch_bounds__(256, RSX_BWD_X3_OCC) void nce_grouped_bwd_x3_k(GArgs a) {
+  constexpr int kRing = RSX_BWD_X3_PIPE ? 3 : 2;
+  __shared__ __attribute__((aligned(16))) X3Tile sT[kRing];
+  __shared__ __attribute__((aligned(16))) float sM0[kRing][kTile];  // rows: bias_d*log2e | cols: lse_i*log2e (+inf past the split)
+  __shared__ __attribute__((aligned(16))) float sM1[kRing][kTile];  // rows: c_d (0 past the split) | cols: unused
+  __shared__ __attribute__((aligned(16))) int sM2[kRing][kTile];    // cols: d(i)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, c = lane & 31;
   int split, ob;
@@ -1316,9 +1399,10 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_bwd_x3_k(GArgs a) {
   const int64_t s_begin = (int64_t)split * a.span;
   int64_t s_end = s_begin + a.span;
   if (s_end > n_str) s_end = n_str;
+  constexpr int kNone = 0x7fffffff;
 
   float o_m2 = 0.0f, o_cnt = 0.0f;  // rows: lse_o*log2e | cols: bias_o*log2e, c_o
-  int o_d = -1, p = 0, e = 0, next = 0x7fffffff;
+  int o_d = -1, p = 0, e = 0, next = kNone;
   if (own_ok) {
     if (ROW_OWNED) {
       o_m2 = a.lse[o] * kLog2e;
@@ -1326,7 +1410,7 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_bwd_x3_k(GArgs a) {
       p = a.row_beg[o];
       e = a.row_end[o];
       p = lower_bound_i(a.exc_cols, p, e, s_begin);
-      next = (p < e) ? a.exc_cols[p] : 0x7fffffff;
+      next = (p < e) ? a.exc_cols[p] : kNone;
     } else {
       o_m2 = a.bias ? a.bias[o] * kLog2e : 0.0f;
       o_cnt = a.colcnt[o];
@@ -1335,9 +1419,11 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_bwd_x3_k(GArgs a) {
       p = lower_bound_i(a.exc_e, p, e, s_begin + 1);  // first user range ending after s_begin
     }
   }
+  const float gso = own_ok ? gs : 0.0f;  // the owner's factor of every G entry
+  const float fo = ROW_OWNED ? gso : gso * o_cnt;
   // cols: ranges [p, q) intersect the current tile; e_first = end of range p (if p < q),
   // s_next = start of range q: the per-tile window update is register compares only
-  int q = p, e_first = 0, s_next = 0x7fffffff;
+  int q = p, e_first = 0, s_next = kNone;
   if (!ROW_OWNED && own_ok && q < e) s_next = a.exc_s[q];
 
   f32x16 gacc[4];
@@ -1374,91 +1460,138 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_bwd_x3_k(GArgs a) {
       sM2[buf][tid] = stg2;
     }
   };
+  // exception flag of tile s0 (before the tile prefetch is issued: the column pass's window
+  // update may load, and a wait on it must not drain the prefetch): rows: the user's own
+  // target columns; cols: user row ranges [p, q) holding target o that intersect the tile
+  auto exc_flag = [&](int64_t s0) -> bool {
+    if (ROW_OWNED) return (int64_t)next < s0 + kTile;
+    while (p < q && (int64_t)e_first <= s0) {
+      ++p;
+      if (p < q) e_first = a.exc_e[p];
+    }
+    while ((int64_t)s_next < s0 + kTile) {
+      if (p == q) e_first = a.exc_e[q];
+      ++q;
+      s_next = (q < e) ? a.exc_s[q] : kNone;
+    }
+    return q != p;
+  };
+  // per-lane multiplicities n[r] of the owner's exceptions among the tile's streamed rows
+  // and the row label column tl (rare: called when some lane of the wave has exceptions)
+  auto exc_counts = [&](int64_t s0, bool exc, float (&n)[16], int& tl) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) n[r] = 0.0f;
+    tl = -1;
+    if (!exc) return;
+    if (ROW_OWNED) {
+      int k = p;
+      for (; k < e && (int64_t)a.exc_cols[k] < s0 + kTile; ++k) {  // sorted, with repeats
+        const int tk = (int)(a.exc_cols[k] - s0);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) n[r] += (tk == tile_row(r, h)) ? 1.0f : 0.0f;
+      }
+      p = k;
+      next = (p < e) ? a.exc_cols[p] : kNone;
+      tl = ((int64_t)o_d < s_end) ? (int)(o_d - s0) : -1;  // label column, if this split owns it
+    } else {
+      for (int k = p; k < q; ++k) {
+        const int ks = (int)(a.exc_s[k] - s0), ke = (int)(a.exc_e[k] - s0);
+        const float nk = (float)a.exc_n[k];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) n[r] += (tile_row(r, h) >= ks && tile_row(r, h) < ke) ? nk : 0.0f;
+      }
+    }
+  };
+  // G of tile buffer cb from its S tile (in place), exception form: per-lane multiplicities
+  // and labels; lanes without exceptions take the common form
+  auto g_exc = [&](f32x16& acc, int cb, bool exc, const float (&n)[16], int tl) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int tr = tile_row(r, h);
+      const float x = fmaf(acc[r], it2, -(sM0[cb][tr] + o_m2));
+      bool lab;
+      float wr;
+      if (ROW_OWNED) {
+        lab = exc && tr == tl;
+        wr = lab ? 1.0f : sM1[cb][tr] - n[r];
+      } else {
+        lab = exc && sM2[cb][tr] == (int)o;
+        wr = lab ? 1.0f : o_cnt - n[r];
+      }
+      const float g = (wr > 0.0f ? wr * __builtin_amdgcn_exp2f(x) : 0.0f) - (lab ? 1.0f : 0.0f);
+      acc[r] = gso * g;
+    }
+  };
 
   if (s_begin < s_end) {
+    const int ntile = (int)((s_end - s_begin + kTile - 1) / kTile);
     gload(s_begin);
     lstore(0);
+#if RSX_BWD_X3_PIPE
+    if (ntile > 1) {
+      gload(s_begin + kTile);
+      lstore(1);
+    }
+    __syncthreads();
+    f32x16 acc = dots_x3(sT[0], c, h, uh, ul);
+    int cur = 0;
+    for (int t = 0; t < ntile; ++t) {
+      const int64_t s0 = s_begin + (int64_t)t * kTile;
+      const int nxt = cur == 2 ? 0 : cur + 1;
+      const int fut = nxt == 2 ? 0 : nxt + 1;
+      const bool has_next = t + 1 < ntile, has_fut = t + 2 < ntile;
+      const bool exc = exc_flag(s0);
+      if (has_fut) gload(s0 + 2 * kTile);
+      bf16x8 gh[2], gl[2];
+      f32x16 accn;
+      if (__any(exc)) {
+        float n[16];
+        int tl;
+        exc_counts(s0, exc, n, tl);
+        g_exc(acc, cur, exc, n, tl);
+        split_tile(acc, gh, gl);
+        accn = has_next ? dots_x3(sT[nxt], c, h, uh, ul) : acc;
+      } else if (has_next) {
+        accn = dots_g_x3<ROW_OWNED, true>(sT[nxt], c, h, uh, ul, acc, sM0[cur], sM1[cur], o_m2, it2, fo, gh, gl);
+      } else {
+        accn = dots_g_x3<ROW_OWNED, false>(sT[nxt], c, h, uh, ul, acc, sM0[cur], sM1[cur], o_m2, it2, fo, gh, gl);
+      }
+      grad_x3s(gacc, gh, gl, sT[cur], lane);
+      // sT[fut] was last read in tile t-1, which every wave finished before that tile's barrier
+      if (has_fut) lstore(fut);
+      __builtin_amdgcn_s_waitcnt(kVmcnt0);  // nothing pending at the loop head on any path
+      __syncthreads();
+      acc = accn;
+      cur = nxt;
+    }
+#else
     __syncthreads();
     int cur = 0;
-    for (int64_t s0 = s_begin; s0 < s_end; s0 += kTile) {
-      const bool has_next = s0 + kTile < s_end;
+    for (int t = 0; t < ntile; ++t) {
+      const int64_t s0 = s_begin + (int64_t)t * kTile;
+      const bool has_next = t + 1 < ntile;
+      const bool exc = exc_flag(s0);
       if (has_next) gload(s0 + kTile);
       f32x16 acc = dots_x3(sT[cur], c, h, uh, ul);
-      // acc -> g = w * 2^(S*log2e - (bias + lse)*log2e) (- 1 on the label), in place
-      if (ROW_OWNED) {
-        if ((int64_t)next >= s0 + kTile) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int tr = tile_row(r, h);
-            acc[r] = sM1[cur][tr] * __builtin_amdgcn_exp2f(fmaf(acc[r], it2, -(sM0[cur][tr] + o_m2)));
-          }
-        } else {  // rare: the user's own targets (d(o) among them) fall in this tile
-          int q = p;
-          while (q < e && (int64_t)a.exc_cols[q] < s0 + kTile) ++q;
-          float n[16];
-#pragma unroll
-          for (int r = 0; r < 16; ++r) n[r] = 0.0f;
-          for (int k = p; k < q; ++k) {
-            const int tk = (int)(a.exc_cols[k] - s0);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) n[r] += (tk == tile_row(r, h)) ? 1.0f : 0.0f;
-          }
-          const int tl = ((int64_t)o_d < s_end) ? (int)(o_d - s0) : -1;  // label column, if this split owns it
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int tr = tile_row(r, h);
-            const bool lab = tr == tl;
-            const float wr = lab ? 1.0f : sM1[cur][tr] - n[r];
-            const float x = fmaf(acc[r], it2, -(sM0[cur][tr] + o_m2));
-            acc[r] = (wr > 0.0f ? wr * __builtin_amdgcn_exp2f(x) : 0.0f) - (lab ? 1.0f : 0.0f);
-          }
-          p = q;
-          next = (p < e) ? a.exc_cols[p] : 0x7fffffff;
-        }
+      bf16x8 gh[2], gl[2];
+      if (__any(exc)) {
+        float n[16];
+        int tl;
+        exc_counts(s0, exc, n, tl);
+        g_exc(acc, cur, exc, n, tl);
+        split_tile(acc, gh, gl);
       } else {
-        // user row ranges holding target o that intersect this tile: [p, q)
-        while (p < q && (int64_t)e_first <= s0) {
-          ++p;
-          if (p < q) e_first = a.exc_e[p];
-        }
-        while ((int64_t)s_next < s0 + kTile) {
-          if (p == q) e_first = a.exc_e[q];
-          ++q;
-          s_next = (q < e) ? a.exc_s[q] : 0x7fffffff;
-        }
-        if (q == p) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int tr = tile_row(r, h);
-            acc[r] = o_cnt * __builtin_amdgcn_exp2f(fmaf(acc[r], it2, -(o_m2 + sM0[cur][tr])));
-          }
-        } else {
-          float n[16];
-#pragma unroll
-          for (int r = 0; r < 16; ++r) n[r] = 0.0f;
-          for (int k = p; k < q; ++k) {
-            const int ks = (int)(a.exc_s[k] - s0), ke = (int)(a.exc_e[k] - s0);
-            const float nk = (float)a.exc_n[k];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) n[r] += (tile_row(r, h) >= ks && tile_row(r, h) < ke) ? nk : 0.0f;
-          }
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int tr = tile_row(r, h);
-            const bool lab = sM2[cur][tr] == (int)o;
-            const float wr = lab ? 1.0f : o_cnt - n[r];
-            const float x = fmaf(acc[r], it2, -(o_m2 + sM0[cur][tr]));
-            acc[r] = (wr > 0.0f ? wr * __builtin_amdgcn_exp2f(x) : 0.0f) - (lab ? 1.0f : 0.0f);
-          }
-        }
+        dots_g_x3<ROW_OWNED, false>(sT[cur], c, h, uh, ul, acc, sM0[cur], sM1[cur], o_m2, it2, fo, gh, gl);
       }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = own_ok ? gs * acc[r] : 0.0f;
-      grad_x3(gacc, acc, sT[cur], lane);
+      grad_x3s(gacc, gh, gl, sT[cur], lane);
       if (has_next) lstore(cur ^ 1);  // cur^1: read in the previous tile, fenced by its barrier
+#if RSX_BWD_VMCNT0
+      __builtin_amdgcn_s_waitcnt(kVmcnt0);  // nothing pending at the loop head on any path
+#endif
       __syncthreads();
       cur ^= 1;
     }
+#endif
   }
   const int64_t own_base = (int64_t)ob * kOwnRows + wave * 32;
   float* dst = a.dout + (int64_t)split * n_own * kD;
@@ -1469,6 +1602,213 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_bwd_x3_k(GArgs a) {
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) dst[orow * kD + kb * 32 + c] = gacc[kb][r];
     }
+  }
+}
+
+// Forward of the grouped loss fused with the row-side gradient (bf16x3). The row gradient
+//   dA_i = gout/tau * (sum_j p_ij B_j - B_d(i)),  p_ij = w_ij 2^(x_ij) / sum_j w_ij 2^(x_ij)
+// is a softmax-weighted sum of the streamed rows, i.e. an attention output with V = B: it is
+// accumulated during the forward sweep, unnormalised, against a lazily raised running max
+// (rescaled only when a tile max exceeds it by more than 2^8, so almost never after the first
+// tiles), and normalised in the merge. This replaces the forward plus the backward's row pass
+// (two sweeps of S) with one sweep; the backward keeps only the column pass.
+// Per split: part = (m ln2, l) per row as the plain forward, dpart[split][row][128] = O.
+constexpr float kLazyLog2 = 8.0f;
+__global__ __launch_bounds__(256, 2) void nce_grouped_fwdg_x3_k(GArgs a) {
+  __shared__ __attribute__((aligned(16))) X3Tile sT[2];
+  __shared__ __attribute__((aligned(16))) float sB2[2][kTile];   // bias_d * log2e (+inf past the split)
+  __shared__ __attribute__((aligned(16))) float sCnt[2][kTile];  // c_d (0 past the split)
+  __shared__ __attribute__((aligned(16))) float sAlpha[kWaves][32];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, c = lane & 31;
+  int split, rb;
+  remap_block(a.nsplit, split, rb);
+  const int64_t i = (int64_t)rb * kOwnRows + wave * 32 + c;
+  const bool row_ok = i < a.N;
+  bf16x8 uh[8], ul[8];
+  load_owner_x3(uh, ul, a.A, i, a.lda, row_ok, h);
+  const int64_t j_begin = (int64_t)split * a.span;
+  int64_t j_end = j_begin + a.span;
+  if (j_end > a.M) j_end = a.M;
+  constexpr int kNone = 0x7fffffff;
+  int di = -1, p = 0, e = 0, next = kNone;
+  if (row_ok) {
+    di = a.row_col[i];
+    p = a.row_beg[i];
+    e = a.row_end[i];
+    p = lower_bound_i(a.exc_cols, p, e, j_begin);
+    next = (p < e) ? a.exc_cols[p] : kNone;
+  }
+  const float it2 = a.inv_tau * kLog2e;
+  float m = -INFINITY, l = 0.0f;  // base 2; m is the same on both lane halves
+  f32x16 gacc[4];
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) gacc[kb][r] = 0.0f;
+  X3Stage stg;
+  float stg_b = 0.0f, stg_c = 0.0f;
+  auto gload = [&](int64_t j0) {
+    const int64_t j = j0 + (tid >> 3);
+    stg.load(a.bhi, a.blo, j, j < j_end, tid);
+    if (tid < kTile) {
+      const int64_t jj = j0 + tid;
+      const bool ok = jj < j_end;
+      stg_b = ok ? (a.bias ? a.bias[jj] : 0.0f) : INFINITY;
+      stg_c = ok ? a.colcnt[jj] : 0.0f;
+    }
+  };
+  auto lstore = [&](int buf) {
+    stg.store(sT[buf], tid);
+    if (tid < kTile) {
+      sB2[buf][tid] = stg_b * kLog2e;
+      sCnt[buf][tid] = stg_c;
+    }
+  };
+  if (j_begin < j_end) {
+    gload(j_begin);
+    lstore(0);
+    __syncthreads();
+    int cur = 0;
+    for (int64_t j0 = j_begin; j0 < j_end; j0 += kTile) {
+      const bool has_next = j0 + kTile < j_end;
+      const bool exc = (int64_t)next < j0 + kTile;  // before the prefetch (see the backward)
+      if (has_next) gload(j0 + kTile);
+      f32x16 acc = dots_x3(sT[cur], c, h, uh, ul);
+      float w[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int tr = tile_row(r, h);
+        w[r] = sCnt[cur][tr];
+        acc[r] = fmaf(acc[r], it2, -sB2[cur][tr]);  // x = S/tau - bias, base 2 (-inf past the split)
+      }
+      if (__any(exc)) {
+        if (exc) {
+          int q = p;
+          while (q < e && (int64_t)a.exc_cols[q] < j0 + kTile) ++q;
+          float n[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) n[r] = 0.0f;
+          for (int k = p; k < q; ++k) {
+            const int tk = (int)(a.exc_cols[k] - j0);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) n[r] += (tk == tile_row(r, h)) ? 1.0f : 0.0f;
+          }
+          const int tl = ((int64_t)di < j_end) ? (int)(di - j0) : -1;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) w[r] = (tile_row(r, h) == tl) ? 1.0f : w[r] - n[r];
+          p = q;
+          next = (p < e) ? a.exc_cols[p] : kNone;
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (!(w[r] > 0.0f)) acc[r] = -INFINITY;  // multiplicity 0: masked
+      }
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, acc[r]);
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      if (!row_ok) tmax = -INFINITY;
+      const bool raise = tmax > m + kLazyLog2;  // m = -inf: the first finite tile
+      if (__any(raise)) {
+        // rescale this lane's l and, through LDS, the accumulator rows of every raised owner
+        const float alpha = raise ? ((m == -INFINITY) ? 0.0f : __builtin_amdgcn_exp2f(m - tmax)) : 1.0f;
+        if (raise) {
+          l *= alpha;
+          m = tmax;
+        }
+        if (h == 0) sAlpha[wave][c] = alpha;
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float al = sAlpha[wave][tile_row(r, h)];
+#pragma unroll
+          for (int kb = 0; kb < 4; ++kb) gacc[kb][r] *= al;
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+      const float ms = (m == -INFINITY) ? 0.0f : m;
+      float ls = 0.0f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        acc[r] = w[r] * __builtin_amdgcn_exp2f(acc[r] - ms);  // w >= 0 where acc is finite
+        ls += acc[r];
+      }
+      l += ls;
+      bf16x8 gh[2], gl[2];
+      split_tile(acc, gh, gl);
+      grad_x3s(gacc, gh, gl, sT[cur], lane);
+      if (has_next) lstore(cur ^ 1);
+      __builtin_amdgcn_s_waitcnt(kVmcnt0);  // nothing pending at the loop head on any path
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+  const float lt = l + __shfl_xor(l, 32, 64);
+  if (h == 0 && row_ok) {
+    const int64_t stride = (int64_t)a.nsplit * a.N;
+    const int64_t o = (int64_t)split * a.N + i;
+    a.part[o] = (m == -INFINITY) ? -INFINITY : m * kLn2;
+    a.part[stride + o] = lt;
+    a.part[2 * stride + o] = 0.0f;
+    a.part[3 * stride + o] = 0.0f;
+  }
+  const int64_t own_base = (int64_t)rb * kOwnRows + wave * 32;
+  float* dst = a.dout + (int64_t)split * a.N * kD;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int64_t orow = own_base + tile_row(r, h);
+    if (orow < a.N) {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) dst[orow * kD + kb * 32 + c] = gacc[kb][r];
+    }
+  }
+}
+
+// merge of the fused forward: lse / row loss as nce_grouped_merge_k, plus the row gradient
+// per unit upstream gradient  ga_i = (sum_s O_s e^(m_s - M) / sum_s l_s e^(m_s - M) - B_d(i)) / tau
+__global__ __launch_bounds__(256) void nce_grouped_merge_g_k(const float* A, const float* B, const float* bias,
+                                                             const int* row_col, int64_t N, int64_t lda,
+                                                             int64_t ldb, float inv_tau, int nsplit,
+                                                             const float* part, const float* opart,
+                                                             float* lse_out, float* row_loss, float* row_valid,
+                                                             float* ga) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= N) return;
+  const int64_t stride = (int64_t)nsplit * N;
+  float m = -INFINITY, l = 0.0f;
+  if (lane < nsplit) {
+    m = part[(int64_t)lane * N + i];
+    l = part[stride + (int64_t)lane * N + i];
+  }
+  float mm = m;
+  for (int o = 32; o > 0; o >>= 1) mm = fmaxf(mm, __shfl_xor(mm, o, 64));
+  const float f = (m == -INFINITY) ? 0.0f : __expf(m - mm);
+  float t = l * f;
+  for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+  const float lse = (mm == -INFINITY) ? -INFINITY : mm + logf(t);
+  const int d = row_col[i];
+  const float2 x = reinterpret_cast<const float2*>(A + i * lda)[lane];
+  const float2 y = reinterpret_cast<const float2*>(B + (int64_t)d * ldb)[lane];
+  float dd = x.x * y.x + x.y * y.y;
+  for (int o = 32; o > 0; o >>= 1) dd += __shfl_xor(dd, o, 64);
+  const float sii = dd * inv_tau - (bias ? bias[d] : 0.0f);
+  const float inv_t = (t > 0.0f) ? 1.0f / t : 0.0f;
+  float2 acc = make_float2(0.0f, 0.0f);
+  for (int s = 0; s < nsplit; ++s) {
+    const float fs = __shfl(f, s, 64) * inv_t;
+    if (fs != 0.0f) {
+      const float2 v = reinterpret_cast<const float2*>(opart + ((int64_t)s * N + i) * kD)[lane];
+      acc.x = fmaf(fs, v.x, acc.x);
+      acc.y = fmaf(fs, v.y, acc.y);
+    }
+  }
+  reinterpret_cast<float2*>(ga + i * kD)[lane] = make_float2((acc.x - y.x) * inv_tau, (acc.y - y.y) * inv_tau);
+  if (lane == 0) {
+    lse_out[i] = lse;
+    row_loss[i] = lse - sii;
+    row_valid[i] = 1.0f;
   }
 }
 
@@ -1663,6 +2003,51 @@ RSX_API int rsx_nce_grouped_fwd(const float* A, const float* B, const float* bia
   RSX_LAUNCHED();
   hipLaunchKernelGGL(nce_grouped_merge_k, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, A, B, bias, row_col, N,
                      lda, ldb, g.inv_tau, nsplit, part, lse, row_loss, row_valid);
+  RSX_LAUNCHED();
+  hipLaunchKernelGGL(nce_reduce_k, dim3(1), dim3(1024), 0, st, row_loss, row_valid, N, out2);
+  RSX_LAUNCHED();
+  return 0;
+}
+
+RSX_API int rsx_nce_grouped_fwd_grad(const float* A, const float* B, const float* bias, const float* colcnt,
+                                     const int* row_col, const int* row_beg, const int* row_end,
+                                     const int* exc_cols, int64_t N, int64_t D, int64_t lda, int64_t ldb, float tau,
+                                     int nsplit, float* ws, float* out2, float* ga, void* stream) {
+  RSX_ARG(A && B && colcnt && row_col && row_beg && row_end && exc_cols && ws && out2 && ga, "null tensor");
+  RSX_ARG(nsplit == 1 || nsplit == 2 || nsplit == 4 || nsplit == 8, "nsplit must be 1, 2, 4 or 8");
+  RSX_ARG(lda % 4 == 0 && ldb % 4 == 0 && lda >= kD && ldb >= kD, "row strides must be >=128 and multiples of 4");
+  RSX_ARG(((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0, "A/B must be 16-byte aligned");
+  hipStream_t st = (hipStream_t)stream;
+  if (N == 0) {
+    (void)hipMemsetAsync(out2, 0, 2 * sizeof(float), st);
+    RSX_LAUNCHED();
+    return 0;
+  }
+  float* part = ws;
+  float* lse = part + 4 * (int64_t)nsplit * N;
+  float* row_loss = lse + N;
+  float* row_valid = row_loss + N;
+  float* opart = lse + 4 * N;  // the backward's split-partial region (>= nsplit x N x 128)
+  GArgs g = {};
+  g.A = A; g.B = B; g.bias = bias; g.colcnt = colcnt;
+  g.row_col = row_col; g.row_beg = row_beg; g.row_end = row_end; g.exc_cols = exc_cols;
+  g.N = N; g.M = D; g.lda = lda; g.ldb = ldb;
+  g.inv_tau = 1.0f / tau;
+  g.nsplit = nsplit;
+  g.span = round_up((D + nsplit - 1) / nsplit, kTile);
+  if (g.span < kTile) g.span = kTile;
+  g.part = part;
+  g.dout = opart;
+  const Images im = grouped_images(ws, N, D, nsplit, kNsplitBwdGrouped);
+  g.bhi = im.bhi;
+  g.blo = im.blo;
+  launch_split(B, ldb, D, im.bhi, im.blo, st);
+  RSX_LAUNCHED();
+  const int blocks = (int)(((N + kOwnRows - 1) / kOwnRows) * nsplit);
+  hipLaunchKernelGGL(nce_grouped_fwdg_x3_k, dim3(blocks), dim3(256), 0, st, g);
+  RSX_LAUNCHED();
+  hipLaunchKernelGGL(nce_grouped_merge_g_k, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, A, B, bias, row_col,
+                     N, lda, ldb, g.inv_tau, nsplit, part, opart, lse, row_loss, row_valid, ga);
   RSX_LAUNCHED();
   hipLaunchKernelGGL(nce_reduce_k, dim3(1), dim3(1024), 0, st, row_loss, row_valid, N, out2);
   RSX_LAUNCHED();

@@ -339,6 +339,12 @@ class TargetGroups:
         self.n_cols = D
 
 
+# bf16x3 + the rows need a gradient: the forward also produces the row gradient (one sweep of
+# S instead of two; rsx_nce_grouped_fwd_grad). RSX_NCE_FUSED_ROWGRAD=0 restores the separate
+# backward row pass.
+_NCE_FUSED_ROWGRAD = os.environ.get("RSX_NCE_FUSED_ROWGRAD", "1") != "0"
+
+
 class _NCEGrouped(torch.autograd.Function):
     @staticmethod
     def forward(ctx, A, B, bias, grp, tau, tag, prec):
@@ -349,13 +355,22 @@ class _NCEGrouped(torch.autograd.Function):
         nws = N.lib().rsx_nce_grouped_workspace_floats(n, d, _NSPLIT_FWD_GROUPED, _NSPLIT_BWD, prec)
         ws = torch.empty(nws, device=A.device, dtype=torch.float32)
         out2 = torch.empty(2, device=A.device, dtype=torch.float32)
+        fused = _NCE_FUSED_ROWGRAD and prec == NCE_PRECISIONS["bf16x3"] and ctx.needs_input_grad[0]
+        ga = None
         with timed(f"{tag}/nce_fwd"):
-            rc = N.lib().rsx_nce_grouped_fwd(N.ptr(A), N.ptr(B), N.ptr(bias), N.ptr(grp.colcnt), N.ptr(grp.row_col),
-                                             N.ptr(grp.row_beg), N.ptr(grp.row_end), N.ptr(grp.exc_cols), n, d,
-                                             A.stride(0), B.stride(0), tau, prec, _NSPLIT_FWD_GROUPED, N.ptr(ws),
-                                             N.ptr(out2), N.stream())
+            if fused:
+                ga = torch.empty(n, 128, device=A.device, dtype=torch.float32)
+                rc = N.lib().rsx_nce_grouped_fwd_grad(
+                    N.ptr(A), N.ptr(B), N.ptr(bias), N.ptr(grp.colcnt), N.ptr(grp.row_col), N.ptr(grp.row_beg),
+                    N.ptr(grp.row_end), N.ptr(grp.exc_cols), n, d, A.stride(0), B.stride(0), tau,
+                    _NSPLIT_FWD_GROUPED, N.ptr(ws), N.ptr(out2), N.ptr(ga), N.stream())
+            else:
+                rc = N.lib().rsx_nce_grouped_fwd(
+                    N.ptr(A), N.ptr(B), N.ptr(bias), N.ptr(grp.colcnt), N.ptr(grp.row_col), N.ptr(grp.row_beg),
+                    N.ptr(grp.row_end), N.ptr(grp.exc_cols), n, d, A.stride(0), B.stride(0), tau, prec,
+                    _NSPLIT_FWD_GROUPED, N.ptr(ws), N.ptr(out2), N.stream())
         N.check(rc, "nce_grouped_fwd")
-        ctx.save_for_backward(A, B, bias, ws)
+        ctx.save_for_backward(A, B, bias, ws, ga)
         ctx.grp = grp
         ctx.cfg = (n, d, tau, tag, prec)
         cnt = out2[1]
@@ -364,7 +379,7 @@ class _NCEGrouped(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g, _gcnt):
-        A, B, bias, ws = ctx.saved_tensors
+        A, B, bias, ws, ga = ctx.saved_tensors
         grp = ctx.grp
         n, d, tau, tag, prec = ctx.cfg
         g = _c(g.reshape(1).to(torch.float32))
@@ -375,10 +390,13 @@ class _NCEGrouped(torch.autograd.Function):
                 N.ptr(g), N.ptr(ws))
         dA = dB = None
         if ctx.needs_input_grad[0]:
-            dA = torch.empty_like(A)
-            with timed(f"{tag}/nce_bwd_rows"):
-                rc = N.lib().rsx_nce_grouped_bwd(*args, N.ptr(dA), None, 0, N.stream())
-            N.check(rc, "nce_grouped_bwd(rows)")
+            if ga is not None:  # the forward's row gradient, per unit upstream gradient
+                dA = ga * g
+            else:
+                dA = torch.empty_like(A)
+                with timed(f"{tag}/nce_bwd_rows"):
+                    rc = N.lib().rsx_nce_grouped_bwd(*args, N.ptr(dA), None, 0, N.stream())
+                N.check(rc, "nce_grouped_bwd(rows)")
         if ctx.needs_input_grad[1]:
             dB = torch.empty_like(B)
             with timed(f"{tag}/nce_bwd_cols"):

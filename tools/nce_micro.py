@@ -28,18 +28,24 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "fp32"])
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="emulate one rank of a DP run: rows of the first --batch users, columns = the "
+                         "distinct targets of a global batch of this many users")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     items = synth.make_items(seed=args.seed)
-    b = synth.make_batch(items, args.batch, seed=args.seed + 100)
+    gb = max(args.global_batch, args.batch)
+    b = synth.make_batch(items, gb, seed=args.seed + 100)
     valid = ~b["padding_mask"]
-    t = b["target_ids"][valid].to(dev)
+    t_all = b["target_ids"][valid].to(dev)
+    valid = valid[:args.batch]
+    t = b["target_ids"][:args.batch][valid].to(dev)
     users = torch.arange(args.batch).unsqueeze(1).expand_as(valid)[valid].to(dev)
     n = t.numel()
     g = torch.Generator(device="cpu").manual_seed(args.seed)
     U = F.normalize(torch.randn(n, 128, generator=g), dim=1).to(dev).requires_grad_()
     W = items.pretrained.to(dev)
-    grp = ops.TargetGroups(t, users)
+    grp = ops.TargetGroups(t, users, t_cols=t_all) if gb > args.batch else ops.TargetGroups(t, users)
     B = W[grp.uniq].contiguous().requires_grad_()
     bias = items.log_q.to(dev)[grp.uniq].contiguous()
     for i in range(3):
