@@ -183,6 +183,22 @@ int rsx_ln_bwd(const float* s, const float* mean, const float* rstd, const float
 int64_t rsx_linear_wgrad_workspace_floats(int64_t T, int64_t N, int64_t K);
 int rsx_linear_wgrad(const float* dY, int64_t ldy, const float* X, int64_t ldx, int64_t T, int64_t N, int64_t K,
                      float* dW, int64_t ldw, float* db, int accumulate, float* ws, int64_t ws_floats, void* stream);
+/* Same contract in bf16x3 split precision (hi*hi + hi*lo + lo*hi on the bf16 MFMA, fp32
+ * accumulate; db summed in fp32): the default of the training step. */
+int rsx_linear_wgrad_x3(const float* dY, int64_t ldy, const float* X, int64_t ldx, int64_t T, int64_t N,
+                        int64_t K, float* dW, int64_t ldw, float* db, int accumulate, float* ws, int64_t ws_floats,
+                        void* stream);
+
+/* ---- forward / input-gradient GEMMs of the token-level linear layers (bf16x3) ------------
+ * C[M, N] = epi(A[M, K] . B[N, K]^T + bias): the forward Y = X W^T + b (B = W) and the input
+ * gradient dX = dY W (B = W^T) of the same per-token nn.Linear layers as rsx_linear_wgrad,
+ * replacing autograd's library GEMMs. epi: 0 bias; 1 z = acc + bias, C = dropout_p(gelu_erf(z))
+ * (keep-mask hash(seed, m*N + n)), aux = gelu_erf'(z); 2 C = acc * keep / (1-p) * aux, its
+ * backward (same seed, aux from epi 1). Epilogues 1/2 fuse nn.TransformerEncoderLayer's feed-forward
+ * dropout(gelu(linear1(x))) (v1_refine_usertower.py:343-352) into its GEMMs.
+ * N % 128 == 0, K % 32 == 0, A/B 16-byte aligned, leading dimensions multiples of 4. */
+int rsx_gemm_x3(const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias, int64_t M, int N, int K,
+                int epi, float* aux, int64_t ldaux, float p_drop, uint64_t seed, float* C, int64_t ldc, void* stream);
 
 /* ---- A14: retrieval top-k ------------------------------------------------------------
  * scores = U I^T (fp32 MFMA, never materialised), per query the k best items sorted by

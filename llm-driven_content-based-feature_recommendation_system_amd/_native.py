@@ -58,6 +58,8 @@ _SIGS = {
                          c_i64, c_p]),
     "rsx_linear_wgrad_workspace_floats": (c_i64, [c_i64, c_i64, c_i64]),
     "rsx_linear_wgrad": (c_i, [c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i, c_p, c_i64, c_p]),
+    "rsx_linear_wgrad_x3": (c_i, [c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i, c_p, c_i64, c_p]),
+    "rsx_gemm_x3": (c_i, [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_i, c_i, c_i, c_p, c_i64, c_f, c_u64, c_p, c_i64, c_p]),
     "rsx_topk_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64]),
     "rsx_retrieve_topk": (c_i, [c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p]),
     "rsx_gather_rows": (c_i, [c_p, c_i64, c_p, c_i64, c_i64, c_i, c_f, c_p, c_p, c_p]),

@@ -135,6 +135,185 @@ __global__ __launch_bounds__(256, 2) void wgrad_k(WArgs a) {
   if (do_db && tid < kTile && n0 + tid < a.N) a.part[split * pstride + (int64_t)a.N * a.K + n0 + tid] = dbsum;
 }
 
+// bf16x3 form (rsx_linear_wgrad_x3): the staged dY / X stages are split into hi/lo bf16
+// images (x = hi + lo) as they are written to LDS, and every product is hi*hi' + hi*lo' +
+// lo*hi' on v_mfma_f32_32x32x16_bf16 (fp32 accumulate; the arithmetic of infonce.hip's
+// bf16x3 loss). Both MFMA operands have the token axis as their k index, so both come from
+// ds_read_b64_tr_b16 transposed reads of the token-major images: lane (c, h) element j of
+// k-step ks is token 16ks + 8(j>>2) + 4h + (j&3), column c of the 32-wide block. Image
+// layout (as infonce.hip): 320-B rows + a 16-B skew per 8 rows, conflict-free for the
+// transposed reads. db is summed in fp32 from the staged registers.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kImgRow = 160;
+constexpr int kImgElems = 5120;
+__device__ __forceinline__ int img_off(int row, int col) { return row * kImgRow + 8 * (row >> 3) + col; }
+struct X3Img {
+  __bf16 hi[kImgElems];
+  __bf16 lo[kImgElems];
+};
+
+__device__ __forceinline__ void split8(const float4& a, const float4& b, u32x4& hi, u32x4& lo) {
+  const float f[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  bf16x8 h, l;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const __bf16 hk = (__bf16)f[k];
+    h[k] = hk;
+    l[k] = (__bf16)(f[k] - (float)hk);
+  }
+  hi = __builtin_bit_cast(u32x4, h);
+  lo = __builtin_bit_cast(u32x4, l);
+}
+
+__global__ __launch_bounds__(256, 2) void wgrad_x3_k(WArgs a) {
+  __shared__ __attribute__((aligned(16))) X3Img sY[2];
+  __shared__ __attribute__((aligned(16))) X3Img sX[2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, c = lane & 31;
+  const int total = a.tiles_n * a.tiles_k * a.nsplit;
+  const int flat = (blockIdx.x & 7) * (total >> 3) + (blockIdx.x >> 3);
+  const int tiles = a.tiles_n * a.tiles_k;
+  const int split = flat / tiles, tile = flat % tiles;
+  const int n0 = (tile / a.tiles_k) * kTile, k0 = (tile % a.tiles_k) * kTile;
+  const int64_t t_begin = (int64_t)split * a.span;
+  int64_t t_end = t_begin + a.span;
+  if (t_end > a.T) t_end = a.T;
+  const int wn = wave >> 1, wk = wave & 1;
+  const bool live = (n0 + wn * 64 < a.N) && (k0 + wk * 64 < a.K);  // wave-uniform
+  const bool do_db = a.with_db && k0 == 0;
+  const int64_t pstride = (int64_t)a.N * a.K + a.N;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+  float dbp[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) dbp[q] = 0.0f;
+
+  const int srow = tid >> 3, scol = (tid & 7) * 16;
+  float4 py[4], px[4];
+  auto gload = [&](int64_t t0) {
+    const int64_t t = t0 + srow;
+    const bool ok = t < t_end;
+    const bool oky = ok && n0 + scol < a.N;
+    const bool okx = ok && k0 + scol < a.K;
+    const float4* ys = reinterpret_cast<const float4*>(a.dY + (oky ? t : 0) * a.ldy + n0 + scol);
+    const float4* xs = reinterpret_cast<const float4*>(a.X + (okx ? t : 0) * a.ldx + k0 + scol);
+    // unconditional loads (from row 0 when out of range), zeroed by a select afterwards: a
+    // predicated load is a branch per load
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 vy = ys[q], vx = xs[q];
+      py[q] = oky ? vy : z;
+      px[q] = okx ? vx : z;
+    }
+  };
+  auto lstore = [&](int buf) {
+    const int o0 = img_off(srow, scol), o1 = img_off(srow, scol + 8);
+    u32x4 hi, lo;
+    split8(py[0], py[1], hi, lo);
+    *reinterpret_cast<u32x4*>(&sY[buf].hi[o0]) = hi;
+    *reinterpret_cast<u32x4*>(&sY[buf].lo[o0]) = lo;
+    split8(py[2], py[3], hi, lo);
+    *reinterpret_cast<u32x4*>(&sY[buf].hi[o1]) = hi;
+    *reinterpret_cast<u32x4*>(&sY[buf].lo[o1]) = lo;
+    split8(px[0], px[1], hi, lo);
+    *reinterpret_cast<u32x4*>(&sX[buf].hi[o0]) = hi;
+    *reinterpret_cast<u32x4*>(&sX[buf].lo[o0]) = lo;
+    split8(px[2], px[3], hi, lo);
+    *reinterpret_cast<u32x4*>(&sX[buf].hi[o1]) = hi;
+    *reinterpret_cast<u32x4*>(&sX[buf].lo[o1]) = lo;
+    if (do_db) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        dbp[4 * q] += py[q].x;
+        dbp[4 * q + 1] += py[q].y;
+        dbp[4 * q + 2] += py[q].z;
+        dbp[4 * q + 3] += py[q].w;
+      }
+    }
+  };
+  // transposed fragment reads: lane (c, h) gets column 32nb + c of tokens 16ks + 8(j>>2) + 4h + (j&3)
+  const int q4 = (lane >> 2) & 3, p4 = lane & 3, cb = (lane >> 4) & 1;
+  const int tbase = img_off(4 * h + q4, 16 * cb + 4 * p4);
+  auto rd = [&](const __bf16* img, int ks, int nb) -> bf16x8 {
+    const int o0 = tbase + img_off(16 * ks, 32 * nb), o1 = tbase + img_off(16 * ks + 8, 32 * nb);
+    const bf16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(&img[o0]));
+    const bf16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(&img[o1]));
+    return __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+
+  if (t_begin < t_end) {
+    gload(t_begin);
+    lstore(0);
+    __syncthreads();
+    int cur = 0;
+    for (int64_t t0 = t_begin; t0 < t_end; t0 += kStage) {
+      const bool has_next = t0 + kStage < t_end;
+      if (has_next) gload(t0 + kStage);
+      if (live) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          bf16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            ah[i] = rd(sY[cur].hi, ks, 2 * wn + i);
+            al[i] = rd(sY[cur].lo, ks, 2 * wn + i);
+            bh[i] = rd(sX[cur].hi, ks, 2 * wk + i);
+            bl[i] = rd(sX[cur].lo, ks, 2 * wk + i);
+          }
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+            }
+        }
+      }
+      if (has_next) lstore(cur ^ 1);  // cur^1 was read in the previous stage, fenced by its barrier
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+  if (live) {
+    float* dst = a.part + split * pstride;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int k = k0 + wk * 64 + j * 32 + c;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int n = n0 + wn * 64 + i * 32 + tile_row(r, h);
+          if (n < a.N && k < a.K) dst[(int64_t)n * a.K + k] = acc[i][j][r];
+        }
+      }
+  }
+  if (do_db) {
+    // column sums of the 32 token rows: threads with equal tid&7 hold the same 16 columns
+    float* red = reinterpret_cast<float*>(&sY[0]);  // free after the loop's last barrier
+#pragma unroll
+    for (int q = 0; q < 16; ++q) red[srow * kTile + scol + q] = dbp[q];
+    __syncthreads();
+    if (tid < kTile) {
+      float s = 0.0f;
+#pragma unroll 8
+      for (int t = 0; t < 32; ++t) s += red[t * kTile + tid];
+      if (n0 + tid < a.N) a.part[split * pstride + (int64_t)a.N * a.K + n0 + tid] = s;
+    }
+  }
+}
+
 // Deterministic split reduction. A workgroup owns 16 consecutive float4 granules of the
 // per-split vector [dW (N*K) | db (N)]; its 16 thread groups each sum the splits g, g+16, ...
 // (many independent loads in flight per thread), then group 0 adds the 16 group sums in
@@ -193,7 +372,8 @@ RSX_API int64_t rsx_linear_wgrad_workspace_floats(int64_t T, int64_t N, int64_t 
   return (int64_t)ns * (N * K + N) + 64;
 }
 
-RSX_API int rsx_linear_wgrad(const float* dY, int64_t ldy, const float* X, int64_t ldx, int64_t T, int64_t N,
+namespace {
+int wgrad_launch(bool x3, const float* dY, int64_t ldy, const float* X, int64_t ldx, int64_t T, int64_t N,
                              int64_t K, float* dW, int64_t ldw, float* db, int accumulate, float* ws,
                              int64_t ws_floats, void* stream) {
   RSX_ARG(((dY && X) || T == 0) && dW && ws, "null tensor");
@@ -217,7 +397,8 @@ RSX_API int rsx_linear_wgrad(const float* dY, int64_t ldy, const float* X, int64
   a.part = ws;
   a.with_db = db != nullptr;
   const int blocks = a.tiles_n * a.tiles_k * a.nsplit;
-  hipLaunchKernelGGL(wgrad_k, dim3(blocks), dim3(256), 0, st, a);
+  if (x3) hipLaunchKernelGGL(wgrad_x3_k, dim3(blocks), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(wgrad_k, dim3(blocks), dim3(256), 0, st, a);
   RSX_LAUNCHED();
   const int64_t pstride4 = (N * K + N) / 4;
   const int64_t n4 = db ? pstride4 : N * K / 4;
@@ -225,4 +406,17 @@ RSX_API int rsx_linear_wgrad(const float* dY, int64_t ldy, const float* X, int64
                      pstride4, (int)N, (int)K, dW, ldw, db, accumulate);
   RSX_LAUNCHED();
   return 0;
+}
+}  // namespace
+
+RSX_API int rsx_linear_wgrad(const float* dY, int64_t ldy, const float* X, int64_t ldx, int64_t T, int64_t N,
+                             int64_t K, float* dW, int64_t ldw, float* db, int accumulate, float* ws,
+                             int64_t ws_floats, void* stream) {
+  return wgrad_launch(false, dY, ldy, X, ldx, T, N, K, dW, ldw, db, accumulate, ws, ws_floats, stream);
+}
+
+RSX_API int rsx_linear_wgrad_x3(const float* dY, int64_t ldy, const float* X, int64_t ldx, int64_t T, int64_t N,
+                                int64_t K, float* dW, int64_t ldw, float* db, int accumulate, float* ws,
+                                int64_t ws_floats, void* stream) {
+  return wgrad_launch(true, dY, ldy, X, ldx, T, N, K, dW, ldw, db, accumulate, ws, ws_floats, stream);
 }

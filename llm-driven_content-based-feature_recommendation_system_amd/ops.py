@@ -557,9 +557,46 @@ def add_layer_norm(x, res, weight, bias, eps=1e-5, p_drop=0.0):
 
 
 # ----------------------------------------------------------------------------------------
-# Token-level linear layer: forward/dX on the BLAS GEMM, dW/db on rsx_linear_wgrad (split-K)
-def linear_wgrad(dy, x, weight_shape, need_bias, tag="wgrad"):
-    """(dW [N, K], db [N] or None) for dy [T, N], x [T, K] (fp32, contiguous)."""
+# Token-level linear layers: forward / dX on rsx_gemm_x3, dW / db on rsx_linear_wgrad(_x3)
+# Token-linear GEMM precision: "bf16x3" = rsx_gemm_x3 / rsx_linear_wgrad_x3 (hi/lo bf16 split
+# on the bf16 MFMA, ~2^-17 relative error per product), "fp32" = the library fp32 GEMM for the
+# forward / input gradient and the fp32-MFMA rsx_linear_wgrad. RSX_GEMM_PRECISION selects.
+GEMM_PRECISIONS = ("fp32", "bf16x3")
+_gemm_precision = os.environ.get("RSX_GEMM_PRECISION", "bf16x3")
+EPI_BIAS, EPI_GELU_DROP, EPI_DGELU_DROP = 0, 1, 2
+
+
+def set_gemm_precision(p: str) -> None:
+    global _gemm_precision
+    assert p in GEMM_PRECISIONS, p
+    _gemm_precision = p
+
+
+def _x3_ok(m_out: int, k_in: int) -> bool:
+    return _gemm_precision == "bf16x3" and m_out % 128 == 0 and k_in % 32 == 0
+
+
+def gemm_x3(a, b, bias=None, epi=EPI_BIAS, aux=None, p_drop=0.0, seed=0, tag=None):
+    """epi(a [M, K] @ b [N, K]^T + bias) on rsx_gemm_x3 (N % 128 == 0, K % 32 == 0).
+    EPI_GELU_DROP returns dropout(gelu(pre)) and writes gelu'(pre) into aux;
+    EPI_DGELU_DROP returns (a @ b^T) * keep / (1 - p) * aux."""
+    a = _c(a)
+    b = _c(b)
+    M, K = a.shape
+    n = b.shape[0]
+    out = torch.empty(M, n, device=a.device, dtype=torch.float32)
+    if M == 0:
+        return out
+    with timed(tag or "gemm_x3"):
+        rc = N.lib().rsx_gemm_x3(N.ptr(a), a.stride(0), N.ptr(b), b.stride(0), N.ptr(None if bias is None else _c(bias)),
+                                 M, n, K, epi, N.ptr(aux), 0 if aux is None else aux.stride(0), float(p_drop),
+                                 int(seed), N.ptr(out), out.stride(0), N.stream())
+    N.check(rc, "gemm_x3")
+    return out
+
+
+def linear_wgrad(dy, x, weight_shape, need_bias, tag="linear_wgrad"):
+    """(dW, db) of y = x W^T + b over the token axis: split-K over tokens, deterministic."""
     N.ensure_device(dy)
     dy = _c(dy)
     x = _c(x)
@@ -570,9 +607,10 @@ def linear_wgrad(dy, x, weight_shape, need_bias, tag="wgrad"):
     ws = torch.empty(nws, device=dy.device, dtype=torch.float32)
     dw = torch.empty(n, k, device=dy.device, dtype=torch.float32)
     db = torch.empty(n, device=dy.device, dtype=torch.float32) if need_bias else None
+    fn = N.lib().rsx_linear_wgrad_x3 if _gemm_precision == "bf16x3" else N.lib().rsx_linear_wgrad
     with timed(tag):
-        rc = N.lib().rsx_linear_wgrad(N.ptr(dy), dy.stride(0), N.ptr(x), x.stride(0), t, n, k, N.ptr(dw), dw.stride(0),
-                                      N.ptr(db), 0, N.ptr(ws), nws, N.stream())
+        rc = fn(N.ptr(dy), dy.stride(0), N.ptr(x), x.stride(0), t, n, k, N.ptr(dw), dw.stride(0), N.ptr(db), 0,
+                N.ptr(ws), nws, N.stream())
     N.check(rc, "linear_wgrad")
     return dw, db
 
@@ -582,13 +620,20 @@ class _TokLinear(torch.autograd.Function):
     def forward(ctx, x, weight, bias):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
+        if _x3_ok(weight.shape[0], weight.shape[1]):
+            return gemm_x3(x, weight, bias, tag="tok_linear_fwd")
         return torch.nn.functional.linear(x, weight, bias)
 
     @staticmethod
     def backward(ctx, dy):
         x, weight = ctx.saved_tensors
         dy = _c(dy)
-        dx = dy @ weight if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if _x3_ok(weight.shape[1], weight.shape[0]):
+                dx = gemm_x3(dy, weight.t(), tag="tok_linear_dx")
+            else:
+                dx = dy @ weight
         dw = db = None
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             dw, db = linear_wgrad(dy, x, weight.shape, ctx.has_bias and ctx.needs_input_grad[2])
@@ -597,13 +642,60 @@ class _TokLinear(torch.autograd.Function):
 
 def linear_tok(x, weight, bias=None):
     """F.linear over a token axis (x [..., K]) whose weight/bias gradients come from the
-    split-K rsx_linear_wgrad kernel instead of the library GEMM (T >> N, K)."""
+    split-K rsx_linear_wgrad kernel instead of the library GEMM (T >> N, K); forward and
+    input gradient on rsx_gemm_x3 when the shapes allow (bf16x3 mode)."""
     shp = x.shape
     x2 = _c(x.reshape(-1, shp[-1]))
     if x2.shape[0] == 0 or shp[-1] % 16 or weight.shape[0] % 16:
         return torch.nn.functional.linear(x, weight, bias)
     y = _TokLinear.apply(x2, weight, bias)
     return y.reshape(*shp[:-1], weight.shape[0])
+
+
+class _FFN(torch.autograd.Function):
+    """linear2(dropout(gelu(linear1(h)))) with the GELU and the dropout in the GEMM epilogues
+    (rsx_gemm_x3 EPI_GELU_DROP forward, EPI_DGELU_DROP for the backward through them)."""
+
+    @staticmethod
+    def forward(ctx, h, w1, b1, w2, b2, p_drop, seed):
+        h = _c(h)
+        ggrad = torch.empty(h.shape[0], w1.shape[0], device=h.device, dtype=torch.float32)  # gelu'(pre)
+        act = gemm_x3(h, w1, b1, EPI_GELU_DROP, ggrad, p_drop, seed, tag="ffn_fwd1")
+        f = gemm_x3(act, w2, b2, tag="ffn_fwd2")
+        ctx.save_for_backward(h, w1, w2, ggrad, act)
+        ctx.cfg = (p_drop, seed, b1 is not None, b2 is not None)
+        return f
+
+    @staticmethod
+    def backward(ctx, df):
+        h, w1, w2, ggrad, act = ctx.saved_tensors
+        p_drop, seed, has_b1, has_b2 = ctx.cfg
+        df = _c(df)
+        need = ctx.needs_input_grad
+        dpre = gemm_x3(df, w2.t(), None, EPI_DGELU_DROP, ggrad, p_drop, seed, tag="ffn_dpre")
+        dw2 = db2 = dw1 = db1 = None
+        if need[3] or need[4]:
+            dw2, db2 = linear_wgrad(df, act, w2.shape, has_b2 and need[4])
+        if need[1] or need[2]:
+            dw1, db1 = linear_wgrad(dpre, h, w1.shape, has_b1 and need[2])
+        dh = gemm_x3(dpre, w1.t(), tag="ffn_dh") if need[0] else None
+        return dh, dw1, db1, dw2, db2, None, None
+
+
+def ffn(h, w1, b1, w2, b2, p_drop=0.0, training=True):
+    """linear2(dropout(gelu(linear1(h)))) over a token axis (nn.TransformerEncoderLayer's
+    feed-forward block, activation="gelu"). bf16x3 mode with GEMM-shaped widths: two fused
+    GEMM launches forward, three plus two weight gradients backward; otherwise the unfused ops."""
+    p = float(p_drop) if training else 0.0
+    shp = h.shape
+    h2 = h.reshape(-1, shp[-1])
+    if (h2.is_cuda and h2.shape[0] > 0 and _x3_ok(w1.shape[0], w1.shape[1]) and _x3_ok(w2.shape[0], w2.shape[1])
+            and _x3_ok(w2.shape[1], w2.shape[0]) and _x3_ok(w1.shape[1], w1.shape[0])):
+        seed = next_seed() if p > 0 else 0
+        f = _FFN.apply(h2, w1, b1, w2, b2, p, seed)
+        return f.reshape(*shp[:-1], w2.shape[0])
+    return linear_tok(torch.nn.functional.dropout(torch.nn.functional.gelu(linear_tok(h, w1, b1)), p, training),
+                      w2, b2)
 
 
 # ----------------------------------------------------------------------------------------

@@ -52,7 +52,8 @@ def encoder_stack(layers, x, key_pad, p, training, causal=True, seg_off=None):
     (v1_refine_usertower.py:343-352, item_tower.py:169-182):
       x = x + drop(out_proj(mha(norm1(x)))) ; x = x + drop(linear2(drop(gelu(linear1(norm2(x))))))
     Each residual add is fused with the LayerNorm that follows it (ops.add_layer_norm); the
-    token linears take their weight gradients from rsx_linear_wgrad (ops.linear_tok)."""
+    token linears run on the bf16x3 GEMMs (ops.linear_tok), the feed-forward's GELU and dropout
+    in their epilogues (ops.ffn)."""
     layers = list(layers)
     h = ops.layer_norm(x, layers[0].norm1.weight, layers[0].norm1.bias, layers[0].norm1.eps)
     for i, layer in enumerate(layers):
@@ -61,8 +62,8 @@ def encoder_stack(layers, x, key_pad, p, training, causal=True, seg_off=None):
         a = ops.mha(qkv, key_pad, sa.num_heads, causal=causal, p_drop=p, seg_off=seg_off)
         a = ops.linear_tok(a, sa.out_proj.weight, sa.out_proj.bias)
         x, h = ops.add_layer_norm(x, a, layer.norm2.weight, layer.norm2.bias, layer.norm2.eps, p)
-        f = ops.linear_tok(F.dropout(F.gelu(ops.linear_tok(h, layer.linear1.weight, layer.linear1.bias)), p,
-                                     training), layer.linear2.weight, layer.linear2.bias)
+        f = ops.ffn(h, layer.linear1.weight, layer.linear1.bias, layer.linear2.weight, layer.linear2.bias, p,
+                    training)
         if i + 1 < len(layers):
             nxt = layers[i + 1].norm1
             x, h = ops.add_layer_norm(x, f, nxt.weight, nxt.bias, nxt.eps, p)

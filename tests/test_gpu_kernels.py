@@ -349,11 +349,20 @@ def test_nce_grouped_sharded_rows(gpu, precision):
     assert abs(tot - ref.sum().item()) < 2e-3
 
 
+@pytest.fixture(params=["bf16x3", "fp32"])
+def gemm_precision(request):
+    prev = ops._gemm_precision
+    ops.set_gemm_precision(request.param)
+    yield request.param
+    ops.set_gemm_precision(prev)
+
+
 @pytest.mark.parametrize("T,N,K", [(80001, 384, 128), (4133, 128, 256), (37, 64, 48), (5, 16, 16), (0, 32, 32),
                                    (70000, 256, 128)])
-def test_linear_wgrad_against_float64(gpu, T, N, K):
-    """dW = dY^T X and db = sum_t dY (split-K fp32 MFMA) vs a float64 product: max error
-    <= 1e-5 * (sum_t |dY||X| scale) — fp32 accumulation over T terms."""
+def test_linear_wgrad_against_float64(gpu, gemm_precision, T, N, K):
+    """dW = dY^T X and db = sum_t dY (split-K; fp32 MFMA or bf16x3) vs a float64 product: max
+    error <= 2e-5 * sqrt(T) — fp32 accumulation over T terms (bf16x3 adds <= 2^-17 |dy x| per
+    product, random in sign)."""
     g = torch.Generator().manual_seed(T + N + K)
     dy = torch.randn(T, N, generator=g)
     x = torch.randn(T, K, generator=g)
@@ -361,8 +370,90 @@ def test_linear_wgrad_against_float64(gpu, T, N, K):
     ref_w = dy.double().t() @ x.double()
     ref_b = dy.double().sum(0)
     scale = max(1.0, math.sqrt(max(T, 1)))
-    assert (dw.cpu().double() - ref_w).abs().max().item() <= 2e-5 * scale
+    if gemm_precision == "bf16x3":  # per-element bound: each product within 2^-17 (+ fp32 sums)
+        bound = 2e-5 * (dy.double().abs().t() @ x.double().abs()) + 2e-5 * scale
+        assert ((dw.cpu().double() - ref_w).abs() <= bound).all()
+    else:
+        assert (dw.cpu().double() - ref_w).abs().max().item() <= 2e-5 * scale
     assert (db.cpu().double() - ref_b).abs().max().item() <= 2e-5 * scale
+
+
+def _absprod(a, b):
+    return a.double().abs() @ b.double().abs().t()
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 384, 128), (777, 128, 256), (5, 256, 384), (129, 128, 32), (0, 128, 32)])
+def test_gemm_x3_against_float64(gpu, M, N, K):
+    """rsx_gemm_x3 (bf16x3 products, fp32 accumulate) vs float64: |C - ref| <= 2e-5 * sum_k
+    |a_mk b_nk| + 1e-6 per element (each bf16x3 product is within 2^-17 of exact)."""
+    g = torch.Generator().manual_seed(M + N + K)
+    a = torch.randn(M, K, generator=g)
+    b = torch.randn(N, K, generator=g)
+    bias = torch.randn(N, generator=g)
+    c = ops.gemm_x3(a.to(gpu), b.to(gpu), bias.to(gpu)).cpu().double()
+    ref = a.double() @ b.double().t() + bias.double()
+    assert c.shape == (M, N)
+    if M:
+        assert ((c - ref).abs() <= 2e-5 * _absprod(a, b) + 1e-6).all()
+
+
+def test_gemm_x3_gelu_dropout_epilogues(gpu):
+    """EPI_GELU_DROP: C = dropout(gelu(pre)) (kept entries gelu(pre) / (1 - p), drop rate ~p)
+    and aux = gelu'(pre), both against float64 from the inputs (bound 2e-5 * sum|a||b| on pre,
+    propagated through |gelu'| <= 1.13 and |gelu''| <= 0.6); EPI_DGELU_DROP with the same seed:
+    zero exactly where the forward dropped, (dY W) / (1 - p) * aux elsewhere."""
+    g = torch.Generator().manual_seed(11)
+    M, N, K, p, seed = 1031, 256, 128, 0.2, 12345
+    x = torch.randn(M, K, generator=g)
+    w1 = torch.randn(N, K, generator=g) / math.sqrt(K)
+    b1 = torch.randn(N, generator=g)
+    aux = torch.empty(M, N, device=gpu)
+    act = ops.gemm_x3(x.to(gpu), w1.to(gpu), b1.to(gpu), ops.EPI_GELU_DROP, aux, p, seed).cpu().double()
+    aux = aux.cpu().double()
+    pre = x.double() @ w1.double().t() + b1.double()
+    bnd = 2e-5 * _absprod(x, w1)
+    cdf = 0.5 * (1 + torch.erf(pre / math.sqrt(2.0)))
+    gel = pre * cdf
+    ggrad = cdf + pre * torch.exp(-0.5 * pre ** 2) / math.sqrt(2 * math.pi)
+    assert ((aux - ggrad).abs() <= 0.6 * bnd + 2e-6).all()
+    kept = act != 0
+    assert ((act - gel / (1 - p)).abs()[kept] <= (1.13 * bnd / (1 - p) + 2e-6)[kept]).all()
+    frac = 1.0 - kept.double().mean().item()
+    assert abs(frac - p) < 0.01
+    w2 = torch.randn(128, N, generator=g) / math.sqrt(N)
+    dy = torch.randn(M, 128, generator=g)
+    dpre = ops.gemm_x3(dy.to(gpu), w2.t().to(gpu), None, ops.EPI_DGELU_DROP, aux.float().to(gpu), p,
+                       seed).cpu().double()
+    dact = dy.double() @ w2.double()
+    ref = torch.where(kept, dact / (1 - p) * aux, torch.zeros_like(aux))
+    dropped = (~kept) & (gel.abs() > 1e-6)
+    assert (dpre[dropped] == 0).all()
+    assert ((dpre - ref).abs() <= 2e-5 * _absprod(dy, w2.t()) / (1 - p) * aux.abs() + 1e-6).all()
+
+
+def test_ffn_matches_torch(gpu):
+    """ops.ffn (fused GELU epilogues, bf16x3 GEMMs) == linear2(gelu(linear1(h))) in float64
+    at p = 0, in value and in all gradients: |err| <= 2e-4 + 2e-5 * max|ref| (bf16x3 products
+    carry ~2^-17 relative error each; the weight gradients sum ~2k token products)."""
+    g = torch.Generator().manual_seed(5)
+    h = torch.randn(2, 999, 128, generator=g).to(gpu)
+    w1 = (torch.randn(256, 128, generator=g) / 11).to(gpu)
+    b1 = torch.randn(256, generator=g).to(gpu)
+    w2 = (torch.randn(128, 256, generator=g) / 16).to(gpu)
+    b2 = torch.randn(128, generator=g).to(gpu)
+    gy = torch.randn(2, 999, 128, generator=g).to(gpu)
+    outs = []
+    for impl in ("rsx", "torch64"):
+        ts = (h, w1, b1, w2, b2) if impl == "rsx" else tuple(t.double() for t in (h, w1, b1, w2, b2))
+        hh, a1, c1, a2, c2 = (t.clone().requires_grad_() for t in ts)
+        if impl == "rsx":
+            y = ops.ffn(hh, a1, c1, a2, c2, 0.0, True)
+        else:
+            y = F.linear(F.gelu(F.linear(hh, a1, c1)), a2, c2)
+        (y * (gy if impl == "rsx" else gy.double())).sum().backward()
+        outs.append((y.detach(), hh.grad, a1.grad, c1.grad, a2.grad, c2.grad))
+    for a, r in zip(*outs):
+        assert (a.double() - r).abs().max().item() <= 2e-4 + 2e-5 * r.abs().max().item()
 
 
 def test_linear_tok_autograd_matches_linear(gpu):
