@@ -104,6 +104,19 @@ int rsx_nce_bwd(const float* A, const float* B, const float* bias, const int* k1
                 int flags, int nsplit_fwd, int nsplit, const float* gout, float* ws, float* dA, float* dB,
                 int accumulate, void* stream);
 
+/* bf16x3 form of the two calls above (same flags, objective and outputs; products as
+ * hi*hi + hi*lo + lo*hi on the bf16 MFMA, see RSX_NCE_BF16X3 below). The split counts are
+ * chosen by the library (enough workgroups for the chip at any N, M); the workspace is
+ * rsx_nce_x3_workspace_floats(N, M) floats and carries the hi/lo images between the calls. */
+int64_t rsx_nce_x3_workspace_floats(int64_t N, int64_t M);
+int rsx_nce_fwd_x3(const float* A, const float* B, const float* bias, const int* k1a, const int* k1b,
+                   const int* k2a, const int* k2b, int64_t N, int64_t M, int64_t lda, int64_t ldb,
+                   int64_t diag_offset, float tau, int flags, float* ws, float* out2, void* stream);
+int rsx_nce_bwd_x3(const float* A, const float* B, const float* bias, const int* k1a, const int* k1b,
+                   const int* k2a, const int* k2b, int64_t N, int64_t M, int64_t lda, int64_t ldb,
+                   int64_t diag_offset, float tau, int flags, const float* gout, float* ws, float* dA, float* dB,
+                   int accumulate, void* stream);
+
 /* ---- A6 grouped: the live LogQ loss over the batch's DISTINCT targets ------------------
  * Same objective as rsx_nce_fwd flags 6 on columns normalize(item_matrix)[t_j], evaluated
  * over the D distinct targets (B[d] = normalised item uniq[d], bias[d] = logQ*lambda) with

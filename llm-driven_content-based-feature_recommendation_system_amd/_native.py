@@ -40,6 +40,11 @@ _SIGS = {
                           c_p, c_p]),
     "rsx_nce_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_f, c_i, c_i, c_i,
                           c_p, c_p, c_p, c_p, c_i, c_p]),
+    "rsx_nce_x3_workspace_floats": (c_i64, [c_i64, c_i64]),
+    "rsx_nce_fwd_x3": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_f, c_i, c_p, c_p,
+                             c_p]),
+    "rsx_nce_bwd_x3": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_f, c_i, c_p, c_p,
+                             c_p, c_p, c_i, c_p]),
     "rsx_nce_grouped_workspace_floats": (c_i64, [c_i64, c_i64, c_i, c_i, c_i]),
     "rsx_nce_grouped_fwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_f, c_i, c_i,
                                   c_p, c_p, c_p]),

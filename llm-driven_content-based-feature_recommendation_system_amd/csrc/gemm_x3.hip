@@ -35,6 +35,9 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kBM = 128, kBN = 128, kBK = 32;
 constexpr int kRow = 40;  // bf16 per LDS row
 constexpr int EPI_BIAS = 0, EPI_GELU_DROP = 1, EPI_DGELU_DROP = 2;
+#ifndef RSX_GEMM_BLOCKS
+#define RSX_GEMM_BLOCKS 512
+#endif
 
 __device__ __forceinline__ int tile_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
@@ -62,7 +65,7 @@ struct GArgs {
   float* C;           // [M, ldc]
   float* aux;         // [M, ldaux]: gelu'(pre) (written by EPI_GELU_DROP, read by EPI_DGELU_DROP)
   int64_t lda, ldb, ldc, ldaux, M;
-  int N, K, epi, tiles_n, tiles;
+  int N, K, epi, tiles_n, tiles, per;
   rsx::Dropout drop;
 };
 
@@ -85,93 +88,11 @@ __device__ __forceinline__ void split16(const float4 (&v)[4], u32x4 (&hi)[2], u3
 }
 
 template <int EPI>
-__global__ __launch_bounds__(256, 2) void gemm_x3_nt_k(GArgs a) {
-  __shared__ __attribute__((aligned(16))) Img sA[2];
-  __shared__ __attribute__((aligned(16))) Img sB[2];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int h = lane >> 5, c = lane & 31;
-  const int wm = wave >> 1, wn = wave & 1;
-  // XCD-aware flat order (the grid is padded to a multiple of 8)
-  const int flat = (blockIdx.x & 7) * ((int)gridDim.x >> 3) + (blockIdx.x >> 3);
-  if (flat >= a.tiles) return;
-  const int64_t m0 = (int64_t)(flat / a.tiles_n) * kBM;
-  const int n0 = (flat % a.tiles_n) * kBN;
-
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-
-  // staging: thread -> row tid>>1 of both tiles, 16 floats at column (tid&1)*16 of the stage.
-  // Rows past M load row m0 instead (unconditional loads: a predicated load would make the
-  // compiler wait on each one); their C rows are never stored and no other row depends on them.
-  const int srow = tid >> 1, scol = (tid & 1) * 16;
-  const float* a_src = a.A + (m0 + srow < a.M ? m0 + srow : m0) * a.lda + scol;
-  const float* b_src = a.B + (int64_t)(n0 + srow) * a.ldb + scol;
-  float4 pa[4], pb[4];
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      pa[q] = *reinterpret_cast<const float4*>(a_src + k0 + 4 * q);
-      pb[q] = *reinterpret_cast<const float4*>(b_src + k0 + 4 * q);
-    }
-  };
-  auto lstore = [&](int buf) {
-    u32x4 hi[2], lo[2];
-    const int o = srow * kRow + scol;
-    split16(pa, hi, lo);
-    *reinterpret_cast<u32x4*>(&sA[buf].hi[o]) = hi[0];
-    *reinterpret_cast<u32x4*>(&sA[buf].hi[o + 8]) = hi[1];
-    *reinterpret_cast<u32x4*>(&sA[buf].lo[o]) = lo[0];
-    *reinterpret_cast<u32x4*>(&sA[buf].lo[o + 8]) = lo[1];
-    split16(pb, hi, lo);
-    *reinterpret_cast<u32x4*>(&sB[buf].hi[o]) = hi[0];
-    *reinterpret_cast<u32x4*>(&sB[buf].hi[o + 8]) = hi[1];
-    *reinterpret_cast<u32x4*>(&sB[buf].lo[o]) = lo[0];
-    *reinterpret_cast<u32x4*>(&sB[buf].lo[o + 8]) = lo[1];
-  };
-
-  gload(0);
-  lstore(0);
-  __syncthreads();
-  int cur = 0;
-  for (int k0 = 0; k0 < a.K; k0 += kBK) {
-    const bool has_next = k0 + kBK < a.K;
-    if (has_next) gload(k0 + kBK);
-    const Img& ta = sA[cur];
-    const Img& tb = sB[cur];
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 ah[2], al[2], bh[2], bl[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int oa = (wm * 64 + 32 * i + c) * kRow + 16 * ks + 8 * h;
-        const int ob = (wn * 64 + 32 * i + c) * kRow + 16 * ks + 8 * h;
-        ah[i] = *reinterpret_cast<const bf16x8*>(&ta.hi[oa]);
-        al[i] = *reinterpret_cast<const bf16x8*>(&ta.lo[oa]);
-        bh[i] = *reinterpret_cast<const bf16x8*>(&tb.hi[ob]);
-        bl[i] = *reinterpret_cast<const bf16x8*>(&tb.lo[ob]);
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-        }
-    }
-    if (has_next) lstore(cur ^ 1);  // cur^1 was read in the previous stage, fenced by its barrier
-    __syncthreads();
-    cur ^= 1;
-  }
-
-  // epilogue: row m0 + wm*64 + 32i + tile_row(r,h), column n0 + wn*64 + 32j + c.
-  // EPI_DGELU_DROP loads the tile's saved GELU derivatives 16 at a time (rows past M read row
-  // M-1), so the loads overlap instead of each waiting in turn.
+__device__ __forceinline__ void epilogue(const GArgs& a, f32x16 (&acc)[2][2], int64_t m0, int n0, int wm, int wn,
+                                         int h, int c) {
+  // row m0 + wm*64 + 32i + tile_row(r,h), column n0 + wn*64 + 32j + c. EPI_DGELU_DROP loads
+  // the tile's saved GELU derivatives 16 at a time (rows past M read row M-1), so the loads
+  // overlap instead of each waiting in turn.
   if (EPI == EPI_DGELU_DROP) {
 #pragma unroll
     for (int j = 0; j < 2; ++j)
@@ -197,8 +118,9 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_k(GArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int64_t m = m0 + wm * 64 + 32 * i + tile_row(r, h);
-        if (m >= a.M) continue;
         float v = acc[i][j][r];
+        acc[i][j][r] = 0.0f;
+        if (m >= a.M) continue;
         if (EPI == EPI_BIAS) {
           v += bn;
         } else if (EPI == EPI_GELU_DROP) {
@@ -212,6 +134,106 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_k(GArgs a) {
         }
         a.C[m * a.ldc + n] = v;
       }
+  }
+}
+
+// Each workgroup walks `per` consecutive output tiles (same XCD; consecutive tiles share the
+// M block) as one continuous stream of K stages: the prefetch of the next stage (possibly
+// the next tile's first) overlaps the current stage's MFMAs and the finished tile's epilogue,
+// so the load pipeline never drains between tiles.
+template <int EPI>
+__global__ __launch_bounds__(256, 2) void gemm_x3_nt_k(GArgs a) {
+  __shared__ __attribute__((aligned(16))) Img sA[2];
+  __shared__ __attribute__((aligned(16))) Img sB[2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, c = lane & 31;
+  const int wm = wave >> 1, wn = wave & 1;
+  // XCD-aware block order (the grid is padded to a multiple of 8)
+  const int bflat = (blockIdx.x & 7) * ((int)gridDim.x >> 3) + (blockIdx.x >> 3);
+  const int t_begin = bflat * a.per;
+  int t_end = t_begin + a.per;
+  if (t_end > a.tiles) t_end = a.tiles;
+  if (t_begin >= t_end) return;
+  const int nk = a.K / kBK;
+  const int nstage = (t_end - t_begin) * nk;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+  // staging: thread -> row tid>>1 of both tiles, 16 floats at column (tid&1)*16 of the stage.
+  // Rows past M load row m0 instead (unconditional loads: a predicated load would make the
+  // compiler wait on each one); their C rows are never stored and no other row depends on them.
+  const int srow = tid >> 1, scol = (tid & 1) * 16;
+  float4 pa[4], pb[4];
+  auto gload = [&](int st) {
+    const int t = t_begin + st / nk, k0 = (st % nk) * kBK;
+    const int64_t m0 = (int64_t)(t / a.tiles_n) * kBM;
+    const int n0 = (t % a.tiles_n) * kBN;
+    const float* a_src = a.A + (m0 + srow < a.M ? m0 + srow : m0) * a.lda + scol + k0;
+    const float* b_src = a.B + (int64_t)(n0 + srow) * a.ldb + scol + k0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      pa[q] = *reinterpret_cast<const float4*>(a_src + 4 * q);
+      pb[q] = *reinterpret_cast<const float4*>(b_src + 4 * q);
+    }
+  };
+  auto lstore = [&](int buf) {
+    u32x4 hi[2], lo[2];
+    const int o = srow * kRow + scol;
+    split16(pa, hi, lo);
+    *reinterpret_cast<u32x4*>(&sA[buf].hi[o]) = hi[0];
+    *reinterpret_cast<u32x4*>(&sA[buf].hi[o + 8]) = hi[1];
+    *reinterpret_cast<u32x4*>(&sA[buf].lo[o]) = lo[0];
+    *reinterpret_cast<u32x4*>(&sA[buf].lo[o + 8]) = lo[1];
+    split16(pb, hi, lo);
+    *reinterpret_cast<u32x4*>(&sB[buf].hi[o]) = hi[0];
+    *reinterpret_cast<u32x4*>(&sB[buf].hi[o + 8]) = hi[1];
+    *reinterpret_cast<u32x4*>(&sB[buf].lo[o]) = lo[0];
+    *reinterpret_cast<u32x4*>(&sB[buf].lo[o + 8]) = lo[1];
+  };
+
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  int cur = 0;
+  for (int st = 0; st < nstage; ++st) {
+    const bool has_next = st + 1 < nstage;
+    if (has_next) gload(st + 1);
+    const Img& ta = sA[cur];
+    const Img& tb = sB[cur];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int oa = (wm * 64 + 32 * i + c) * kRow + 16 * ks + 8 * h;
+        const int ob = (wn * 64 + 32 * i + c) * kRow + 16 * ks + 8 * h;
+        ah[i] = *reinterpret_cast<const bf16x8*>(&ta.hi[oa]);
+        al[i] = *reinterpret_cast<const bf16x8*>(&ta.lo[oa]);
+        bh[i] = *reinterpret_cast<const bf16x8*>(&tb.hi[ob]);
+        bl[i] = *reinterpret_cast<const bf16x8*>(&tb.lo[ob]);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+    }
+    if (st % nk == nk - 1) {  // tile finished: epilogue (resets acc) while the next stage loads
+      const int t = t_begin + st / nk;
+      epilogue<EPI>(a, acc, (int64_t)(t / a.tiles_n) * kBM, (t % a.tiles_n) * kBN, wm, wn, h, c);
+    }
+    if (has_next) lstore(cur ^ 1);  // cur^1 was read in the previous stage, fenced by its barrier
+    __syncthreads();
+    cur ^= 1;
   }
 }
 
@@ -238,7 +260,10 @@ RSX_API int rsx_gemm_x3(const float* A, int64_t lda, const float* B, int64_t ldb
   RSX_ARG(tiles < (1LL << 30), "too many tiles");
   g.tiles = (int)tiles;
   g.drop = rsx::make_dropout(epi == EPI_BIAS ? 0.0f : p_drop, seed);
-  const int grid = (int)((tiles + 7) / 8 * 8);
+  // tiles per workgroup: enough workgroups for two per CU, each a continuous stage stream
+  g.per = (int)((tiles + RSX_GEMM_BLOCKS - 1) / RSX_GEMM_BLOCKS);
+  const int64_t blocks = (tiles + g.per - 1) / g.per;
+  const int grid = (int)((blocks + 7) / 8 * 8);
   hipStream_t st = (hipStream_t)stream;
   if (epi == EPI_BIAS) hipLaunchKernelGGL(gemm_x3_nt_k<EPI_BIAS>, dim3(grid), dim3(256), 0, st, g);
   else if (epi == EPI_GELU_DROP) hipLaunchKernelGGL(gemm_x3_nt_k<EPI_GELU_DROP>, dim3(grid), dim3(256), 0, st, g);

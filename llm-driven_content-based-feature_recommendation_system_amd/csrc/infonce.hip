@@ -1605,6 +1605,285 @@ __global__ __launch_bounds__(256, RSX_BWD_X3_OCC) void nce_grouped_bwd_x3_k(GArg
   }
 }
 
+// ---- plain (ungrouped) InfoNCE in bf16x3: DuoRec unsup/sup, SimCSE -------------------
+// The objective, flags and partial layout of nce_fwd_k / nce_bwd_k; the products as in the
+// grouped bf16x3 kernels (streamed hi/lo images copied from ws into LDS, owner fragments in
+// registers, S tile on dots_x3, gradient tile split and fed to grad_x3s), one barrier per tile.
+struct X3Args {
+  const __bf16* shi;  // streamed operand's hi/lo images [rows][128]
+  const __bf16* slo;
+};
+
+template <int FL>
+__global__ __launch_bounds__(256, 2) void nce_fwd_x3_k(FwdArgs a, X3Args x) {
+  __shared__ __attribute__((aligned(16))) X3Tile sT[2];
+  __shared__ __attribute__((aligned(16))) float sBias[2][kTile];
+  __shared__ __attribute__((aligned(16))) int sK1[2][kTile];
+  __shared__ __attribute__((aligned(16))) int sK2[2][kTile];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, c = lane & 31;
+  int split, rb;
+  remap_block(a.nsplit, split, rb);
+  const int64_t i = (int64_t)rb * kOwnRows + wave * 32 + c;
+  const bool row_ok = i < a.N;
+  bf16x8 uh[8], ul[8];
+  load_owner_x3(uh, ul, a.A, i, a.lda, row_ok, h);
+  int k1i = 0, k2i = 0;
+  if (row_ok) {
+    if ((FL & (F_MASK_K1 | F_POS)) && a.k1a) k1i = a.k1a[i];
+    if ((FL & F_MASK_K2) && a.k2a) k2i = a.k2a[i];
+  }
+  const int64_t j_begin = (int64_t)split * a.cols_per_split;
+  int64_t j_end = j_begin + a.cols_per_split;
+  if (j_end > a.M) j_end = a.M;
+  float m = -INFINITY, l = 0.0f, ps = 0.0f, pc = 0.0f;
+  X3Stage stg;
+  float stg_bias = 0.0f;
+  int stg_k1 = 0, stg_k2 = 0;
+  auto gload = [&](int64_t j0) {
+    const int64_t j = j0 + (tid >> 3);
+    stg.load(x.shi, x.slo, j, j < j_end, tid);
+    if (tid < kTile) {
+      const int64_t jj = j0 + tid;
+      const bool ok = jj < j_end;
+      stg_bias = (ok && a.bias) ? a.bias[jj] : 0.0f;
+      stg_k1 = (ok && a.k1b) ? a.k1b[jj] : 0;
+      stg_k2 = (ok && a.k2b) ? a.k2b[jj] : 0;
+    }
+  };
+  auto lstore = [&](int buf) {
+    stg.store(sT[buf], tid);
+    if (tid < kTile) {
+      sBias[buf][tid] = stg_bias;
+      sK1[buf][tid] = stg_k1;
+      sK2[buf][tid] = stg_k2;
+    }
+  };
+  if (j_begin < j_end) {
+    gload(j_begin);
+    lstore(0);
+    __syncthreads();
+    int cur = 0;
+    for (int64_t j0 = j_begin; j0 < j_end; j0 += kTile) {
+      const bool has_next = j0 + kTile < j_end;
+      if (has_next) gload(j0 + kTile);
+      const f32x16 acc = dots_x3(sT[cur], c, h, uh, ul);
+      float v[16];
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        const int rbase = 8 * q4 + 4 * h;
+        const float4 bi4 = *reinterpret_cast<const float4*>(&sBias[cur][rbase]);
+        const int4 k14 = *reinterpret_cast<const int4*>(&sK1[cur][rbase]);
+        const int4 k24 = *reinterpret_cast<const int4*>(&sK2[cur][rbase]);
+        const float bia[4] = {bi4.x, bi4.y, bi4.z, bi4.w};
+        const int kk1[4] = {k14.x, k14.y, k14.z, k14.w};
+        const int kk2[4] = {k24.x, k24.y, k24.z, k24.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * q4 + e;
+          const int64_t j = j0 + rbase + e;
+          const float sv = acc[r] * a.inv_tau - bia[e];
+          bool excl = (j >= j_end) || !row_ok;
+          const bool offdiag = (j != i + a.diag_off);
+          if (FL & F_EXCL_DIAG) excl = excl || !offdiag;
+          if (FL & F_MASK_K1) excl = excl || (offdiag && kk1[e] == k1i);
+          if (FL & F_MASK_K2) excl = excl || (offdiag && kk2[e] == k2i);
+          if (FL & F_POS) {
+            if (!excl && offdiag && kk1[e] == k1i && k1i != 0) {
+              ps += sv;
+              pc += 1.0f;
+            }
+          }
+          v[r] = excl ? -INFINITY : sv;
+          tmax = fmaxf(tmax, v[r]);
+        }
+      }
+      if (tmax > m) {
+        l = (m == -INFINITY) ? 0.0f : l * __expf(m - tmax);
+        m = tmax;
+      }
+      if (m != -INFINITY) {
+        float t = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t += __expf(v[r] - m);
+        l += t;
+      }
+      if (has_next) lstore(cur ^ 1);  // cur^1: read in the previous tile, fenced by its barrier
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+  const float m2 = __shfl_xor(m, 32, 64);
+  const float l2 = __shfl_xor(l, 32, 64);
+  const float ps2 = __shfl_xor(ps, 32, 64);
+  const float pc2 = __shfl_xor(pc, 32, 64);
+  const float mm = fmaxf(m, m2);
+  float ll = 0.0f;
+  if (mm != -INFINITY) {
+    if (m != -INFINITY) ll += l * __expf(m - mm);
+    if (m2 != -INFINITY) ll += l2 * __expf(m2 - mm);
+  }
+  if (h == 0 && row_ok) {
+    const int64_t stride = (int64_t)a.nsplit * a.N;
+    const int64_t o = (int64_t)split * a.N + i;
+    a.part[o] = mm;
+    a.part[stride + o] = ll;
+    a.part[2 * stride + o] = ps + ps2;
+    a.part[3 * stride + o] = pc + pc2;
+  }
+}
+
+template <int FL, bool ROW_OWNED>
+__global__ __launch_bounds__(256, 2) void nce_bwd_x3_k(BwdArgs a, X3Args x) {
+  __shared__ __attribute__((aligned(16))) X3Tile sT[2];
+  __shared__ __attribute__((aligned(16))) float sM0[2][kTile];  // row side: lse_i | col side: bias_j
+  __shared__ __attribute__((aligned(16))) float sM1[2][kTile];  // row side: w_i
+  __shared__ __attribute__((aligned(16))) float sM2[2][kTile];  // row side: inv_cnt_i
+  __shared__ __attribute__((aligned(16))) int sK1[2][kTile];
+  __shared__ __attribute__((aligned(16))) int sK2[2][kTile];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, c = lane & 31;
+  int split, ob;
+  remap_block(a.nsplit, split, ob);
+  const int64_t n_own = ROW_OWNED ? a.N : a.M;
+  const int64_t n_str = ROW_OWNED ? a.M : a.N;
+  const float* own = ROW_OWNED ? a.A : a.B;
+  const int64_t ld_own = ROW_OWNED ? a.lda : a.ldb;
+  const float g_scale = a.gout[0] * a.inv_tau;
+  const int64_t o = (int64_t)ob * kOwnRows + wave * 32 + c;
+  const bool own_ok = o < n_own;
+  bf16x8 uh[8], ul[8];
+  load_owner_x3(uh, ul, own, o, ld_own, own_ok, h);
+  float o_lse = 0.0f, o_w = 0.0f, o_icnt = 0.0f, o_bias = 0.0f;
+  int o_k1 = 0, o_k2 = 0;
+  if (own_ok) {
+    if (ROW_OWNED) {
+      o_lse = a.lse[o];
+      o_w = a.row_valid[o] * g_scale;
+      if ((FL & F_POS) && a.inv_cnt) o_icnt = a.inv_cnt[o];
+      if ((FL & (F_MASK_K1 | F_POS)) && a.k1a) o_k1 = a.k1a[o];
+      if ((FL & F_MASK_K2) && a.k2a) o_k2 = a.k2a[o];
+    } else {
+      o_bias = a.bias ? a.bias[o] : 0.0f;
+      if ((FL & (F_MASK_K1 | F_POS)) && a.k1b) o_k1 = a.k1b[o];
+      if ((FL & F_MASK_K2) && a.k2b) o_k2 = a.k2b[o];
+    }
+  }
+  const int64_t s_begin = (int64_t)split * a.span_per_split;
+  int64_t s_end = s_begin + a.span_per_split;
+  if (s_end > n_str) s_end = n_str;
+  f32x16 gacc[4];
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) gacc[kb][r] = 0.0f;
+  X3Stage stg;
+  float stg0 = 0.0f, stg1 = 0.0f, stg2 = 0.0f;
+  int stg_k1 = 0, stg_k2 = 0;
+  auto gload = [&](int64_t s0) {
+    const int64_t sidx = s0 + (tid >> 3);
+    stg.load(x.shi, x.slo, sidx, sidx < s_end, tid);
+    if (tid < kTile) {
+      const int64_t ss = s0 + tid;
+      const bool ok = ss < s_end;
+      if (ROW_OWNED) {
+        stg0 = (ok && a.bias) ? a.bias[ss] : 0.0f;
+        stg_k1 = (ok && a.k1b) ? a.k1b[ss] : 0;
+        stg_k2 = (ok && a.k2b) ? a.k2b[ss] : 0;
+      } else {
+        stg0 = ok ? a.lse[ss] : 0.0f;
+        stg1 = ok ? a.row_valid[ss] * g_scale : 0.0f;
+        stg2 = (ok && a.inv_cnt) ? a.inv_cnt[ss] : 0.0f;
+        stg_k1 = (ok && a.k1a) ? a.k1a[ss] : 0;
+        stg_k2 = (ok && a.k2a) ? a.k2a[ss] : 0;
+      }
+    }
+  };
+  auto lstore = [&](int buf) {
+    stg.store(sT[buf], tid);
+    if (tid < kTile) {
+      sM0[buf][tid] = stg0;
+      sM1[buf][tid] = stg1;
+      sM2[buf][tid] = stg2;
+      sK1[buf][tid] = stg_k1;
+      sK2[buf][tid] = stg_k2;
+    }
+  };
+  if (s_begin < s_end) {
+    gload(s_begin);
+    lstore(0);
+    __syncthreads();
+    int cur = 0;
+    for (int64_t s0 = s_begin; s0 < s_end; s0 += kTile) {
+      const bool has_next = s0 + kTile < s_end;
+      if (has_next) gload(s0 + kTile);
+      f32x16 acc = dots_x3(sT[cur], c, h, uh, ul);
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        const int rbase = 8 * q4 + 4 * h;
+        const float4 m04 = *reinterpret_cast<const float4*>(&sM0[cur][rbase]);
+        const float4 m14 = *reinterpret_cast<const float4*>(&sM1[cur][rbase]);
+        const float4 m24 = *reinterpret_cast<const float4*>(&sM2[cur][rbase]);
+        const int4 k14 = *reinterpret_cast<const int4*>(&sK1[cur][rbase]);
+        const int4 k24 = *reinterpret_cast<const int4*>(&sK2[cur][rbase]);
+        const float mm0[4] = {m04.x, m04.y, m04.z, m04.w};
+        const float mm1[4] = {m14.x, m14.y, m14.z, m14.w};
+        const float mm2[4] = {m24.x, m24.y, m24.z, m24.w};
+        const int kk1[4] = {k14.x, k14.y, k14.z, k14.w};
+        const int kk2[4] = {k24.x, k24.y, k24.z, k24.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * q4 + e;
+          const int64_t sidx = s0 + rbase + e;
+          int64_t ii, jj;
+          float lse_i, w_i, icnt_i, bias_j;
+          int k1_i, k1_j, k2_i, k2_j;
+          if (ROW_OWNED) {
+            ii = o; jj = sidx;
+            lse_i = o_lse; w_i = o_w; icnt_i = o_icnt; bias_j = mm0[e];
+            k1_i = o_k1; k1_j = kk1[e]; k2_i = o_k2; k2_j = kk2[e];
+          } else {
+            ii = sidx; jj = o;
+            lse_i = mm0[e]; w_i = mm1[e]; icnt_i = mm2[e]; bias_j = o_bias;
+            k1_i = kk1[e]; k1_j = o_k1; k2_i = kk2[e]; k2_j = o_k2;
+          }
+          const float sv = acc[r] * a.inv_tau - bias_j;
+          bool excl = (sidx >= s_end) || !own_ok;
+          const bool offdiag = (jj != ii + a.diag_off);
+          if (FL & F_EXCL_DIAG) excl = excl || !offdiag;
+          if (FL & F_MASK_K1) excl = excl || (offdiag && k1_i == k1_j);
+          if (FL & F_MASK_K2) excl = excl || (offdiag && k2_i == k2_j);
+          float y = 0.0f;
+          if (FL & F_POS) {
+            if (!excl && offdiag && k1_i == k1_j && k1_i != 0) y = icnt_i;
+          } else {
+            y = offdiag ? 0.0f : 1.0f;
+          }
+          const float p = (excl || lse_i == -INFINITY) ? 0.0f : __expf(sv - lse_i);
+          acc[r] = excl ? 0.0f : w_i * (p - y);
+        }
+      }
+      bf16x8 gh[2], gl[2];
+      split_tile(acc, gh, gl);
+      grad_x3s(gacc, gh, gl, sT[cur], lane);
+      if (has_next) lstore(cur ^ 1);  // cur^1: read in the previous tile, fenced by its barrier
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+  const int64_t own_base = (int64_t)ob * kOwnRows + wave * 32;
+  float* dst = a.dout + (int64_t)split * n_own * kD;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int64_t orow = own_base + tile_row(r, h);
+    if (orow < n_own) {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) dst[orow * kD + kb * 32 + c] = gacc[kb][r];
+    }
+  }
+}
+
 // Forward of the grouped loss fused with the row-side gradient (bf16x3). The row gradient
 //   dA_i = gout/tau * (sum_j p_ij B_j - B_d(i)),  p_ij = w_ij 2^(x_ij) / sum_j w_ij 2^(x_ij)
 // is a softmax-weighted sum of the streamed rows, i.e. an attention output with V = B: it is
@@ -1959,6 +2238,171 @@ RSX_API int rsx_nce_bwd(const float* A, const float* B, const float* bias, const
   return 0;
 }
 
+
+// ---- plain InfoNCE, bf16x3 ------------------------------------------------------------
+namespace {
+// split count of one pass: the smallest power of two (<= 64) that gives the owner side >= 1024
+// workgroups while every split keeps >= 2 streamed tiles
+int plain_split(int64_t n_own, int64_t n_str) {
+  const int64_t ob = (n_own + kOwnRows - 1) / kOwnRows;
+  int ps = 1;
+  while (ps < 64 && ob * ps < 1024 && n_str >= (int64_t)ps * 4 * kTile) ps *= 2;
+  return ps;
+}
+struct X3Plan {
+  int nf, pr, pc;            // forward / row-pass / column-pass splits
+  int64_t img, dpart, total;  // float offsets of the images and the split partials; total size
+};
+X3Plan plain_plan(int64_t N, int64_t M) {
+  X3Plan p;
+  p.nf = plain_split(N, M);
+  p.pr = plain_split(N, M);
+  p.pc = plain_split(M, N);
+  p.img = (4 * (int64_t)p.nf * N + 4 * N + 63) / 64 * 64;  // after part [4][nf][N] and lse/loss/valid/icnt
+  p.dpart = p.img + (N + M) * kD;                          // hi+lo bf16 of A and B = 1 float per element
+  const int64_t a = (int64_t)p.pr * N, b = (int64_t)p.pc * M;
+  p.total = p.dpart + (a > b ? a : b) * kD + 16;
+  return p;
+}
+Images plain_images(float* ws, const X3Plan& p, int64_t N, int64_t M) {
+  __bf16* q = reinterpret_cast<__bf16*>(ws + p.img);
+  Images im;
+  im.ahi = q;
+  im.alo = q + N * kD;
+  im.bhi = q + 2 * N * kD;
+  im.blo = q + 2 * N * kD + M * kD;
+  return im;
+}
+template <int FL>
+void launch_fwd_x3_t(const FwdArgs& a, const X3Args& x, int blocks, hipStream_t st) {
+  hipLaunchKernelGGL(nce_fwd_x3_k<FL>, dim3(blocks), dim3(256), 0, st, a, x);
+}
+template <int FL>
+void launch_bwd_x3_t(const BwdArgs& a, const X3Args& x, bool row_owned, int blocks, hipStream_t st) {
+  if (row_owned) hipLaunchKernelGGL((nce_bwd_x3_k<FL, true>), dim3(blocks), dim3(256), 0, st, a, x);
+  else hipLaunchKernelGGL((nce_bwd_x3_k<FL, false>), dim3(blocks), dim3(256), 0, st, a, x);
+}
+}  // namespace
+
+RSX_API int64_t rsx_nce_x3_workspace_floats(int64_t N, int64_t M) { return plain_plan(N, M).total; }
+
+RSX_API int rsx_nce_fwd_x3(const float* A, const float* B, const float* bias, const int* k1a, const int* k1b,
+                           const int* k2a, const int* k2b, int64_t N, int64_t M, int64_t lda, int64_t ldb,
+                           int64_t diag_offset, float tau, int flags, float* ws, float* out2, void* stream) {
+  RSX_ARG(valid_flags(flags), "unsupported flag combination");
+  RSX_ARG(N >= 0 && M >= 0, "negative size");
+  RSX_ARG(lda % 4 == 0 && ldb % 4 == 0 && lda >= kD && ldb >= kD, "row strides must be >=128 and multiples of 4");
+  RSX_ARG(((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0, "A/B must be 16-byte aligned");
+  RSX_ARG(diag_offset >= 0 && diag_offset + N <= M, "need 0 <= diag_offset and diag_offset + N <= M");
+  RSX_ARG(!(flags & (F_MASK_K1 | F_POS)) || (k1a && k1b), "k1 keys required");
+  RSX_ARG(!(flags & F_MASK_K2) || (k2a && k2b), "k2 keys required");
+  RSX_ARG(ws && out2, "null workspace / output");
+  hipStream_t st = (hipStream_t)stream;
+  if (N == 0) {
+    (void)hipMemsetAsync(out2, 0, 2 * sizeof(float), st);
+    RSX_LAUNCHED();
+    return 0;
+  }
+  const X3Plan pl = plain_plan(N, M);
+  float* part = ws;
+  float* lse = part + 4 * (int64_t)pl.nf * N;
+  float* row_loss = lse + N;
+  float* row_valid = row_loss + N;
+  float* inv_cnt = row_valid + N;
+  const Images im = plain_images(ws, pl, N, M);
+  launch_split(B, ldb, M, im.bhi, im.blo, st);  // kept in ws for the backward's row pass
+  RSX_LAUNCHED();
+  FwdArgs fa;
+  fa.A = A; fa.B = B; fa.bias = bias;
+  fa.k1a = k1a; fa.k1b = k1b; fa.k2a = k2a; fa.k2b = k2b;
+  fa.N = N; fa.M = M; fa.lda = lda; fa.ldb = ldb;
+  fa.diag_off = diag_offset;
+  fa.inv_tau = 1.0f / tau;
+  fa.nsplit = pl.nf;
+  fa.cols_per_split = round_up((M + pl.nf - 1) / pl.nf, kTile);
+  if (fa.cols_per_split < kTile) fa.cols_per_split = kTile;
+  fa.part = part;
+  X3Args x = {im.bhi, im.blo};
+  const int blocks = (int)(((N + kOwnRows - 1) / kOwnRows) * pl.nf);
+  switch (flags) {
+    case 0: launch_fwd_x3_t<0>(fa, x, blocks, st); break;
+    case F_MASK_K1: launch_fwd_x3_t<F_MASK_K1>(fa, x, blocks, st); break;
+    case F_MASK_K1 | F_MASK_K2: launch_fwd_x3_t<F_MASK_K1 | F_MASK_K2>(fa, x, blocks, st); break;
+    default: launch_fwd_x3_t<F_EXCL_DIAG | F_POS>(fa, x, blocks, st); break;
+  }
+  RSX_LAUNCHED();
+  MergeArgs ma;
+  ma.A = A; ma.B = B; ma.bias = bias;
+  ma.N = N; ma.lda = lda; ma.ldb = ldb;
+  ma.diag_off = diag_offset;
+  ma.inv_tau = fa.inv_tau;
+  ma.nsplit = pl.nf;
+  ma.part = part;
+  ma.pos_mode = (flags & F_POS) ? 1 : 0;
+  ma.lse = lse; ma.row_loss = row_loss; ma.row_valid = row_valid; ma.inv_cnt = inv_cnt;
+  hipLaunchKernelGGL(nce_merge_k, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, ma);
+  RSX_LAUNCHED();
+  hipLaunchKernelGGL(nce_reduce_k, dim3(1), dim3(1024), 0, st, row_loss, row_valid, N, out2);
+  RSX_LAUNCHED();
+  return 0;
+}
+
+RSX_API int rsx_nce_bwd_x3(const float* A, const float* B, const float* bias, const int* k1a, const int* k1b,
+                           const int* k2a, const int* k2b, int64_t N, int64_t M, int64_t lda, int64_t ldb,
+                           int64_t diag_offset, float tau, int flags, const float* gout, float* ws, float* dA,
+                           float* dB, int accumulate, void* stream) {
+  RSX_ARG(valid_flags(flags), "unsupported flag combination");
+  RSX_ARG(gout != nullptr && ws != nullptr, "gout/ws required");
+  RSX_ARG(diag_offset >= 0 && diag_offset + N <= M, "need 0 <= diag_offset and diag_offset + N <= M");
+  hipStream_t st = (hipStream_t)stream;
+  if (N == 0) return 0;
+  const X3Plan pl = plain_plan(N, M);
+  float* part = ws;
+  float* lse = part + 4 * (int64_t)pl.nf * N;
+  float* row_valid = lse + 2 * N;
+  float* inv_cnt = row_valid + N;
+  float* dpart = ws + pl.dpart;
+  const Images im = plain_images(ws, pl, N, M);
+  BwdArgs ba;
+  ba.A = A; ba.B = B; ba.bias = bias;
+  ba.k1a = k1a; ba.k1b = k1b; ba.k2a = k2a; ba.k2b = k2b;
+  ba.N = N; ba.M = M; ba.lda = lda; ba.ldb = ldb;
+  ba.diag_off = diag_offset;
+  ba.inv_tau = 1.0f / tau;
+  ba.lse = lse; ba.row_valid = row_valid; ba.inv_cnt = inv_cnt;
+  ba.gout = gout;
+  for (int pass = 0; pass < 2; ++pass) {
+    const bool row_owned = pass == 0;
+    float* target = row_owned ? dA : dB;
+    if (!target) continue;
+    const int64_t n_own = row_owned ? N : M;
+    const int64_t n_str = row_owned ? M : N;
+    if (n_own == 0) continue;
+    const int ps = row_owned ? pl.pr : pl.pc;
+    ba.nsplit = ps;
+    ba.span_per_split = round_up((n_str + ps - 1) / ps, kTile);
+    if (ba.span_per_split < kTile) ba.span_per_split = kTile;
+    ba.dout = dpart;
+    if (!row_owned) {  // B's images come from the forward; A's are made here, for the column pass
+      launch_split(A, lda, N, im.ahi, im.alo, st);
+      RSX_LAUNCHED();
+    }
+    const X3Args x = row_owned ? X3Args{im.bhi, im.blo} : X3Args{im.ahi, im.alo};
+    const int blocks = (int)(((n_own + kOwnRows - 1) / kOwnRows) * ps);
+    switch (flags) {
+      case 0: launch_bwd_x3_t<0>(ba, x, row_owned, blocks, st); break;
+      case F_MASK_K1: launch_bwd_x3_t<F_MASK_K1>(ba, x, row_owned, blocks, st); break;
+      case F_MASK_K1 | F_MASK_K2: launch_bwd_x3_t<F_MASK_K1 | F_MASK_K2>(ba, x, row_owned, blocks, st); break;
+      default: launch_bwd_x3_t<F_EXCL_DIAG | F_POS>(ba, x, row_owned, blocks, st); break;
+    }
+    RSX_LAUNCHED();
+    const int64_t total4 = n_own * kD / 4;
+    hipLaunchKernelGGL(nce_sum_splits_k, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, st, dpart, ps,
+                       n_own, target, accumulate);
+    RSX_LAUNCHED();
+  }
+  return 0;
+}
 
 RSX_API int rsx_nce_grouped_fwd(const float* A, const float* B, const float* bias, const float* colcnt,
                                 const int* row_col, const int* row_beg, const int* row_end, const int* exc_cols,

@@ -232,7 +232,9 @@ def l2_normalize(x, eps=1e-12):
 # ----------------------------------------------------------------------------------------
 # A6 / A7 / A12: fused contrastive cross-entropy
 class _NCE(torch.autograd.Function):
-    """Returns (sum of row losses over valid rows, number of valid rows)."""
+    """Returns (sum of row losses over valid rows, number of valid rows). bf16x3 precision
+    (default) runs rsx_nce_fwd_x3 / rsx_nce_bwd_x3 (split counts chosen by the library), fp32
+    the fp32-MFMA rsx_nce_fwd / rsx_nce_bwd."""
 
     @staticmethod
     def forward(ctx, A, B, bias, k1a, k1b, k2a, k2b, tau, flags, diag_offset, tag):
@@ -240,17 +242,24 @@ class _NCE(torch.autograd.Function):
         A = _c(A)
         B = _c(B)
         n, m = A.shape[0], B.shape[0]
-        nws = N.lib().rsx_nce_workspace_floats(n, m, _NSPLIT_FWD, _NSPLIT_BWD)
+        x3 = _nce_precision == "bf16x3"
+        nws = (N.lib().rsx_nce_x3_workspace_floats(n, m) if x3
+               else N.lib().rsx_nce_workspace_floats(n, m, _NSPLIT_FWD, _NSPLIT_BWD))
         ws = torch.empty(nws, device=A.device, dtype=torch.float32)
         out2 = torch.empty(2, device=A.device, dtype=torch.float32)
         keys = [_c(k) for k in (k1a, k1b, k2a, k2b)]
         with timed(f"{tag}/nce_fwd"):
-            rc = N.lib().rsx_nce_fwd(N.ptr(A), N.ptr(B), N.ptr(bias), *[N.ptr(k) for k in keys], n, m, A.stride(0),
-                                     B.stride(0), diag_offset, tau, flags, _NSPLIT_FWD, N.ptr(ws), N.ptr(out2),
-                                     N.stream())
+            if x3:
+                rc = N.lib().rsx_nce_fwd_x3(N.ptr(A), N.ptr(B), N.ptr(bias), *[N.ptr(k) for k in keys], n, m,
+                                            A.stride(0), B.stride(0), diag_offset, tau, flags, N.ptr(ws), N.ptr(out2),
+                                            N.stream())
+            else:
+                rc = N.lib().rsx_nce_fwd(N.ptr(A), N.ptr(B), N.ptr(bias), *[N.ptr(k) for k in keys], n, m,
+                                         A.stride(0), B.stride(0), diag_offset, tau, flags, _NSPLIT_FWD, N.ptr(ws),
+                                         N.ptr(out2), N.stream())
         N.check(rc, "nce_fwd")
         ctx.save_for_backward(A, B, bias, *keys, ws)
-        ctx.cfg = (n, m, tau, flags, diag_offset, tag)
+        ctx.cfg = (n, m, tau, flags, diag_offset, tag, x3)
         cnt = out2[1]
         ctx.mark_non_differentiable(cnt)
         return out2[0], cnt
@@ -258,20 +267,24 @@ class _NCE(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g, _gcnt):
         A, B, bias, k1a, k1b, k2a, k2b, ws = ctx.saved_tensors
-        n, m, tau, flags, off, tag = ctx.cfg
+        n, m, tau, flags, off, tag, x3 = ctx.cfg
         g = _c(g.reshape(1).to(torch.float32))
-        args = (N.ptr(A), N.ptr(B), N.ptr(bias), N.ptr(k1a), N.ptr(k1b), N.ptr(k2a), N.ptr(k2b), n, m, A.stride(0),
-                B.stride(0), off, tau, flags, _NSPLIT_FWD, _NSPLIT_BWD, N.ptr(g), N.ptr(ws))
+        head = (N.ptr(A), N.ptr(B), N.ptr(bias), N.ptr(k1a), N.ptr(k1b), N.ptr(k2a), N.ptr(k2b), n, m, A.stride(0),
+                B.stride(0), off, tau, flags)
+        if x3:
+            fn, args = N.lib().rsx_nce_bwd_x3, head + (N.ptr(g), N.ptr(ws))
+        else:
+            fn, args = N.lib().rsx_nce_bwd, head + (_NSPLIT_FWD, _NSPLIT_BWD, N.ptr(g), N.ptr(ws))
         dA = dB = None
         if ctx.needs_input_grad[0]:
             dA = torch.empty_like(A)
             with timed(f"{tag}/nce_bwd_rows"):
-                rc = N.lib().rsx_nce_bwd(*args, N.ptr(dA), None, 0, N.stream())
+                rc = fn(*args, N.ptr(dA), None, 0, N.stream())
             N.check(rc, "nce_bwd(rows)")
         if ctx.needs_input_grad[1]:
             dB = torch.empty_like(B)
             with timed(f"{tag}/nce_bwd_cols"):
-                rc = N.lib().rsx_nce_bwd(*args, None, N.ptr(dB), 0, N.stream())
+                rc = fn(*args, None, N.ptr(dB), 0, N.stream())
             N.check(rc, "nce_bwd(cols)")
         return dA, dB, None, None, None, None, None, None, None, None, None
 
