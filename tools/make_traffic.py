@@ -1,0 +1,52 @@
+"""profiles/r01_nce_fwdg_traffic.json from the FETCH_SIZE / WRITE_SIZE passes of
+tools/nce_micro.py (rocprofv3 --pmc, separate passes; see tools/steps_final_r01.txt).
+
+FETCH_SIZE is doubled (gfx950 reports half the bytes of 16-B/lane streaming reads,
+MI355X_MICROARCH.md HBM section); WRITE_SIZE is taken as reported.
+  python tools/make_traffic.py gpurun_out/pmcf gpurun_out/pmcw out.json"""
+import csv
+import glob
+import json
+import sys
+
+KERNEL = "nce_grouped_fwdg_x3_k"
+
+
+def vals(d, counter):
+    out = []
+    for f in glob.glob(d + "/*counter_collection.csv"):
+        for r in csv.DictReader(open(f)):
+            if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                out.append(float(r["Counter_Value"]))
+    return out
+
+
+def main():
+    fetch = vals(sys.argv[1], "FETCH_SIZE")
+    write = vals(sys.argv[2], "WRITE_SIZE")
+    N, D = 76850, 16363  # tools/nce_micro.py batch 4096 (bench batch 0 shapes)
+    f = sum(fetch) / len(fetch)
+    w = sum(write) / len(write)
+    hbm = int((2 * f + w) * 1024)
+    # algorithmic: A and B rows (fp32) read once, the row-gradient partials [4][N][128] written
+    # once, the per-row (m, l) partials; images of B (hi/lo bf16) are written by the split
+    # kernel outside this launch
+    alg = 4 * (N + D) * 128 + 4 * 4 * N * 128 + 4 * 4 * 4 * N
+    out = {
+        "kernel": "nce_grouped_fwdg_x3_k (grouped LogQ forward fused with the row gradient)",
+        "precision": "bf16x3", "global_batch": 4096, "rows_N": N, "distinct_targets_D": D,
+        "fetch_size_kb_raw": round(f, 1), "write_size_kb": round(w, 1),
+        "hbm_bytes_per_launch": hbm,
+        "correction": "FETCH_SIZE doubled (gfx950 reports half the bytes of 16-B/lane streaming reads, "
+                      "MI355X_MICROARCH.md HBM section); WRITE_SIZE as reported",
+        "algorithmic_bytes_per_launch": alg,
+        "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) over tools/nce_micro.py "
+                  "--iters 3 (bench batch 0 shapes)",
+        "samples": {"fetch_kb": fetch, "write_kb": write},
+    }
+    json.dump(out, open(sys.argv[3], "w"), indent=1)
+    print(json.dumps({k: out[k] for k in ("hbm_bytes_per_launch", "algorithmic_bytes_per_launch")}))
+
+
+if __name__ == "__main__":
+    main()
