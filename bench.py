@@ -59,6 +59,9 @@ def parse():
     ap.add_argument("--no-item-tower", action="store_true", help="skip the item-tower secondary metric")
     ap.add_argument("--nce-precision", default="bf16x3", choices=["bf16x3", "fp32"],
                     help="logit precision of the grouped LogQ loss kernels (ops.set_nce_precision)")
+    ap.add_argument("--no-prefetch-index", action="store_true",
+                    help="build each batch's index inside its own step (host syncs mid-step)")
+    ap.add_argument("--unfused-adamw", action="store_true", help="torch's foreach AdamW instead of fused")
     ap.add_argument("--blas", default="default", choices=["default", "hipblaslt", "rocblas", "ck"],
                     help="library torch uses for the tower's dense projections")
     return ap.parse_args()
@@ -251,7 +254,9 @@ def main():
     item_tower = TT.SASRecItemTower(args.items, cfg.d_model, items.log_q.clone()).to(device)
     item_tower.init_from_pretrained(items.pretrained.to(device))
     item_tower.set_freeze_state(args.freeze_items)
-    opt = torch.optim.AdamW(model.parameters(), lr=cfg.lr, weight_decay=cfg.weight_decay)
+    # fused AdamW: one multi-tensor kernel per group instead of the foreach chain (same update)
+    opt = torch.optim.AdamW(model.parameters(), lr=cfg.lr, weight_decay=cfg.weight_decay,
+                            fused=not args.unfused_adamw)
     if not args.freeze_items:
         opt.add_param_group({"params": list(item_tower.parameters()), "lr": cfg.lr * 0.05})
     bucket = D.GradBucket(list(model.parameters()) + list(item_tower.parameters()))
@@ -273,8 +278,19 @@ def main():
         n_dist.append(int(torch.unique(g["target_ids"][~g["padding_mask"]]).numel()))
     torch.cuda.synchronize()
 
+    # Each step enqueues its work, then builds the NEXT batch's data-dependent index (packed
+    # tokens, grouped targets: the host-synchronising size queries) on a side stream while the
+    # GPU runs the step (dist.prepare_step_index_async). Every timed step still builds one index.
+    pending = {}
+
     def step(i):
-        return D.contrastive_step_dp(model, item_tower, log_q, batches[i % 2], opt, cfg, lookup, bucket)
+        ix = pending.pop(i, None)
+        if ix is None:
+            ix = D.prepare_step_index(batches[i % 2], pretrained_lookup=lookup)
+        out = D.contrastive_step_dp(model, item_tower, log_q, batches[i % 2], opt, cfg, lookup, bucket, index=ix)
+        if not args.no_prefetch_index:
+            pending[i + 1] = D.prepare_step_index_async(batches[(i + 1) % 2], pretrained_lookup=lookup)
+        return out
 
     for i in range(args.warmup):
         step(i)
@@ -286,7 +302,7 @@ def main():
     t0 = time.perf_counter()
     losses = None
     for i in range(args.steps):
-        losses = step(i)
+        losses = step(args.warmup + i)  # continues the warm-up's step numbering (pending index)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -306,7 +322,7 @@ def main():
     # Peak: the MFMA rate of the arithmetic used: fp32 MFMA, or bf16 MFMA / 3 for the bf16x3
     # split products. The timed window is the op's launches (fused kernel + B split + merge).
     flops = 0.0
-    for i in range(args.steps):
+    for i in range(args.warmup, args.warmup + args.steps):
         cnts = n_glob[i % 2]
         flops += 4.0 * cnts[rank] * n_dist[i % 2] * 128
     x3 = args.nce_precision == "bf16x3"

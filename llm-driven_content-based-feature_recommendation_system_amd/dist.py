@@ -122,31 +122,109 @@ class GradBucket:
             o += n
 
 
+class StepIndex:
+    """Every data-dependent structure of one DP step (nothing depends on model state): the
+    packed token sets and per-token inputs (v1_usertower_train.pack_inputs), the global row
+    counts, the main loss's grouped-target index and the DuoRec keys."""
+
+
+def prepare_step_index(batch, pretrained_vecs=None, pretrained_lookup=None) -> StepIndex:
+    """Builds the StepIndex of `batch` on the current stream. Its size queries (nonzero /
+    unique / the count all-gather) synchronise the host with that stream."""
+    from .tower_code.v1_usertower_train import pack_inputs
+
+    rank, ws = world()
+    device = batch["item_ids"].device
+    B = batch["item_ids"].shape[0]
+    target_ids = batch["target_ids"]
+    ix = StepIndex()
+    ix.packed = pack_inputs(batch, pretrained_vecs, pretrained_lookup)
+    pk = ix.packed[0]
+    ix.B = B
+    ix.counts = all_gather_counts(pk.valid_tok.numel(), device)
+    ix.n_glob = sum(ix.counts)
+    ix.groups = None
+    if ix.n_glob > 0:
+        t_loc = target_ids.reshape(-1)[pk.flat[pk.valid_tok]]
+        user_loc = pk.tok_user[pk.valid_tok] + rank * B
+        t_glob = all_gather_var(t_loc, ix.counts)
+        ix.groups = ops.TargetGroups(t_loc, user_loc, t_cols=t_glob)
+    ix.last_t = target_ids.reshape(-1)[pk.flat[pk.last_tok]]
+    ix.t_glob_last = all_gather_var(ix.last_t, [B] * ws)
+    return ix
+
+
+def _tensors_of(obj, seen=None):
+    seen = set() if seen is None else seen
+    if id(obj) in seen:
+        return
+    seen.add(id(obj))
+    if torch.is_tensor(obj):
+        yield obj
+    elif isinstance(obj, (list, tuple)):
+        for x in obj:
+            yield from _tensors_of(x, seen)
+    elif hasattr(obj, "__dict__"):
+        for x in vars(obj).values():
+            yield from _tensors_of(x, seen)
+
+
+_PREP_STREAM = None
+
+
+def prepare_step_index_async(batch, pretrained_vecs=None, pretrained_lookup=None):
+    """prepare_step_index on a high-priority side stream: its host synchronisations wait only
+    for that stream's few small kernels, so calling it right after a step has been enqueued
+    overlaps the next batch's index building (and its size queries) with the running step.
+    The batch tensors must not be written by pending work. Pass the result to
+    contrastive_step_dp(..., index=...), which orders the main stream after it."""
+    global _PREP_STREAM
+    if _PREP_STREAM is None:
+        _PREP_STREAM = torch.cuda.Stream(priority=-1)
+    with torch.cuda.stream(_PREP_STREAM):
+        ix = prepare_step_index(batch, pretrained_vecs, pretrained_lookup)
+        ix.ready = torch.cuda.Event()
+        ix.ready.record(_PREP_STREAM)
+    return ix
+
+
+def _adopt(ix):
+    """Order the current stream after an async-prepared index and keep its memory alive for it."""
+    ev = getattr(ix, "ready", None)
+    if ev is None:
+        return
+    cur = torch.cuda.current_stream()
+    cur.wait_event(ev)
+    for t in _tensors_of(ix):
+        if t.is_cuda:
+            t.record_stream(cur)
+    ix.ready = None
+
+
 def contrastive_objective_dp(model, item_tower, log_q_tensor, batch, cfg, pretrained_lookup=None,
-                             pretrained_vecs=None, temperature=0.1):
+                             pretrained_vecs=None, temperature=0.1, index=None):
     """This rank's share of the global objective (reference :787-845 on the global batch).
 
-    batch holds this rank's users (global user index = rank * B_local + b).
+    batch holds this rank's users (global user index = rank * B_local + b). index: a
+    StepIndex of this batch prepared ahead (prepare_step_index[_async]); built here if None.
     Returns (local objective to backward, global total / main / cl for logging; the
     logging values are all-reduced and detached)."""
     from .tower_code.v1_usertower_train import packed_views
 
     rank, ws = world()
     device = batch["item_ids"].device
-    B, L = batch["item_ids"].shape
-    target_ids = batch["target_ids"]
-    pk, out1, out2 = packed_views(model, batch, pretrained_vecs, pretrained_lookup)
+    if index is None:
+        index = prepare_step_index(batch, pretrained_vecs, pretrained_lookup)
+    else:
+        _adopt(index)
+    B = index.B
+    pk, out1, out2 = packed_views(model, batch, pretrained_vecs, pretrained_lookup, packed=index.packed)
 
     # ---- main LogQ loss over all valid steps of the global batch
-    n_loc = pk.valid_tok.numel()
-    counts = all_gather_counts(n_loc, device)
-    n_glob = sum(counts)
+    n_glob = index.n_glob
     if n_glob > 0:
         u_loc = ops.gather_rows(out1, pk.valid_tok, normalize=True, unique=True)
-        t_loc = target_ids.reshape(-1)[pk.flat[pk.valid_tok]]
-        user_loc = pk.tok_user[pk.valid_tok] + rank * B
-        t_glob = all_gather_var(t_loc, counts)
-        groups = ops.TargetGroups(t_loc, user_loc, t_cols=t_glob)
+        groups = index.groups
         items_d = ops.gather_rows(item_tower.get_all_embeddings(), groups.uniq, normalize=True, unique=True)
         bias = log_q_tensor[groups.uniq] * cfg.lambda_logq if cfg.lambda_logq > 0.0 else None
         main_sum, _ = ops.nce_grouped_sum(u_loc, items_d, bias, groups, tau=temperature, tag="main")
@@ -157,12 +235,12 @@ def contrastive_objective_dp(model, item_tower, log_q_tensor, batch, cfg, pretra
     # ---- DuoRec on the bug-compatible "last" index (count_valid - 1), global B x B
     z1 = ops.l2_normalize(ops.gather_rows(out1, pk.last_tok, unique=True))
     z2 = ops.l2_normalize(ops.gather_rows(out2, pk.last_tok, unique=True))
-    last_t = target_ids.reshape(-1)[pk.flat[pk.last_tok]]
+    last_t = index.last_t
     bcounts = [B] * ws
     b_glob = B * ws
     z1_glob = all_gather_rows(z1, bcounts)
     z2_glob = all_gather_rows(z2, bcounts)
-    t_glob_last = all_gather_var(last_t, bcounts)
+    t_glob_last = index.t_glob_last
     un_sum, _ = ops.nce_sum(z1, z2_glob, tau=temperature, flags=ops.NCE_PLAIN, diag_offset=rank * B,
                             tag="duorec")
     unsup_local = un_sum / float(b_glob)
@@ -182,12 +260,14 @@ def contrastive_objective_dp(model, item_tower, log_q_tensor, batch, cfg, pretra
 
 
 def contrastive_step_dp(model, item_tower, log_q_tensor, batch, optimizer, cfg, pretrained_lookup, bucket,
-                        max_norm=5.0):
+                        max_norm=5.0, index=None):
     """Full data-parallel step: local forward/loss/backward, one gradient all-reduce,
-    clip_grad_norm_(5.0) on the summed gradients, AdamW (replicated, identical on all ranks)."""
+    clip_grad_norm_(5.0) on the summed gradients, AdamW (replicated, identical on all ranks).
+    index: the batch's StepIndex prepared ahead (e.g. prepare_step_index_async while the
+    previous step runs); built inline if None."""
     optimizer.zero_grad(set_to_none=True)
     objective, total, main, cl = contrastive_objective_dp(model, item_tower, log_q_tensor, batch, cfg,
-                                                          pretrained_lookup=pretrained_lookup)
+                                                          pretrained_lookup=pretrained_lookup, index=index)
     objective.backward()
     bucket()
     torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=max_norm)

@@ -107,13 +107,10 @@ _STATIC_KEYS = ("age_bucket", "price_bucket", "cnt_bucket", "recency_bucket", "c
 _SEQ_ID_KEYS = ("item_ids", "time_bucket_ids", "type_ids", "color_ids", "graphic_ids", "section_ids")
 
 
-def packed_views(model, batch, pretrained_vecs=None, pretrained_lookup=None):
-    """Both dropout views (reference :788-789) on the packed token set of the step, run as ONE
-    packed pass over the doubled batch: users b and B + b carry the same inputs, so view 1 is
-    tokens [0, T) and view 2 tokens [T, 2T) of the output. The views still draw independent
-    dropout masks (the kernels key their masks by token row; torch dropout is per element), and
-    every kernel launch covers both views (half the launches, no per-parameter gradient adds).
-    Returns (packed tokens of one view, out_1 [T, D], out_2 [T, D])."""
+def pack_inputs(batch, pretrained_vecs=None, pretrained_lookup=None):
+    """The data-dependent half of packed_views (no model state): packed token sets of one view
+    and of the doubled batch, and the per-token inputs of the doubled batch. Its size queries
+    synchronise the host with the stream it runs on (see dist.prepare_step_index_async)."""
     pm = batch["padding_mask"]
     pk = PackedTokens(pm)
     pk2 = PackedTokens(torch.cat([pm, pm]))
@@ -125,6 +122,21 @@ def packed_views(model, batch, pretrained_vecs=None, pretrained_lookup=None):
         pv_tok = ops.gather_rows(pretrained_lookup, tok_ids[0][:T])
     pv_tok = torch.cat([pv_tok, pv_tok])
     static = [torch.cat([batch[k], batch[k]]) for k in _STATIC_KEYS]
+    return pk, pk2, tok_ids, pv_tok, static
+
+
+def packed_views(model, batch, pretrained_vecs=None, pretrained_lookup=None, packed=None):
+    """Both dropout views (reference :788-789) on the packed token set of the step, run as ONE
+    packed pass over the doubled batch: users b and B + b carry the same inputs, so view 1 is
+    tokens [0, T) and view 2 tokens [T, 2T) of the output. The views still draw independent
+    dropout masks (the kernels key their masks by token row; torch dropout is per element), and
+    every kernel launch covers both views (half the launches, no per-parameter gradient adds).
+    packed: pack_inputs(batch, ...) computed ahead (else computed here).
+    Returns (packed tokens of one view, out_1 [T, D], out_2 [T, D])."""
+    if packed is None:
+        packed = pack_inputs(batch, pretrained_vecs, pretrained_lookup)
+    pk, pk2, tok_ids, pv_tok, static = packed
+    T = pk.flat.numel()
     out = model.forward_packed(pk2, pv_tok, tok_ids, *static)
     return pk, out[:T], out[T:]
 
