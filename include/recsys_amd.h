@@ -252,6 +252,14 @@ int rsx_gather_rows(const float* src, int64_t ld_src, const int64_t* idx, int64_
  * Rows whose index equals skip_idx are dropped (nn.Embedding padding_idx), -1 = none. */
 int rsx_scatter_rows(const float* dy, const float* y, const float* nrm, const int64_t* idx, int64_t n, int64_t D,
                      int normalize, float eps, int mode, int64_t skip_idx, float* dst, int64_t ld_dst, void* stream);
+/* Segmented row sums, the atomic-free scatter-add when the sort by destination is known:
+ * dst[rows[u]] (+)= scale[0] * sum_{k in [seg_off[u], seg_off[u+1])} src[perm[k]] (scale
+ * nullable = 1; rows[u] == skip_row untouched; rows unique). Used for the user tower's item-id
+ * embedding gradient (v1_refine_usertower.py:447-459, nn.Embedding backward) with the sort
+ * built ahead of the step; deterministic. */
+int rsx_segment_sum_rows(const float* src, int64_t ld_src, const int64_t* perm, const int64_t* seg_off,
+                         const int64_t* rows, int64_t nseg, int64_t D, const float* scale, int64_t skip_row,
+                         float* dst, int64_t ld_dst, int accumulate, void* stream);
 
 #ifdef __cplusplus
 }

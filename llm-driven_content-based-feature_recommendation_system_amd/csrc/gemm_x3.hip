@@ -32,8 +32,12 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kBM = 128, kBN = 128, kBK = 32;
-constexpr int kRow = 40;  // bf16 per LDS row
+#ifndef RSX_GEMM_BK
+#define RSX_GEMM_BK 32
+#endif
+constexpr int kBM = 128, kBN = 128, kBK = RSX_GEMM_BK;
+constexpr int kRow = kBK + 8;  // bf16 per LDS row (80 B at BK 32, 48 B at BK 16: conflict-free b128 reads)
+constexpr int kF4 = kBK / 8;   // float4 loads per thread and operand per stage (two threads per row)
 constexpr int EPI_BIAS = 0, EPI_GELU_DROP = 1, EPI_DGELU_DROP = 2;
 #ifndef RSX_GEMM_BLOCKS
 #define RSX_GEMM_BLOCKS 512
@@ -69,22 +73,18 @@ struct GArgs {
   rsx::Dropout drop;
 };
 
-// 16 fp32 -> 16 hi + 16 lo bf16 (two 16-B chunks each)
-__device__ __forceinline__ void split16(const float4 (&v)[4], u32x4 (&hi)[2], u32x4 (&lo)[2]) {
+// 8 fp32 -> 8 hi + 8 lo bf16 (one 16-B chunk each)
+__device__ __forceinline__ void split8(const float4& x, const float4& y, u32x4& hi, u32x4& lo) {
+  const float f[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+  bf16x8 h, l;
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const float f[8] = {v[2 * q].x, v[2 * q].y, v[2 * q].z, v[2 * q].w,
-                        v[2 * q + 1].x, v[2 * q + 1].y, v[2 * q + 1].z, v[2 * q + 1].w};
-    bf16x8 h, l;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const __bf16 hk = (__bf16)f[k];
-      h[k] = hk;
-      l[k] = (__bf16)(f[k] - (float)hk);
-    }
-    hi[q] = __builtin_bit_cast(u32x4, h);
-    lo[q] = __builtin_bit_cast(u32x4, l);
+  for (int k = 0; k < 8; ++k) {
+    const __bf16 hk = (__bf16)f[k];
+    h[k] = hk;
+    l[k] = (__bf16)(f[k] - (float)hk);
   }
+  hi = __builtin_bit_cast(u32x4, h);
+  lo = __builtin_bit_cast(u32x4, l);
 }
 
 template <int EPI>
@@ -168,8 +168,8 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_k(GArgs a) {
   // staging: thread -> row tid>>1 of both tiles, 16 floats at column (tid&1)*16 of the stage.
   // Rows past M load row m0 instead (unconditional loads: a predicated load would make the
   // compiler wait on each one); their C rows are never stored and no other row depends on them.
-  const int srow = tid >> 1, scol = (tid & 1) * 16;
-  float4 pa[4], pb[4];
+  const int srow = tid >> 1, scol = (tid & 1) * (kBK / 2);
+  float4 pa[kF4], pb[kF4];
   auto gload = [&](int st) {
     const int t = t_begin + st / nk, k0 = (st % nk) * kBK;
     const int64_t m0 = (int64_t)(t / a.tiles_n) * kBM;
@@ -177,24 +177,23 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_k(GArgs a) {
     const float* a_src = a.A + (m0 + srow < a.M ? m0 + srow : m0) * a.lda + scol + k0;
     const float* b_src = a.B + (int64_t)(n0 + srow) * a.ldb + scol + k0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < kF4; ++q) {
       pa[q] = *reinterpret_cast<const float4*>(a_src + 4 * q);
       pb[q] = *reinterpret_cast<const float4*>(b_src + 4 * q);
     }
   };
   auto lstore = [&](int buf) {
-    u32x4 hi[2], lo[2];
     const int o = srow * kRow + scol;
-    split16(pa, hi, lo);
-    *reinterpret_cast<u32x4*>(&sA[buf].hi[o]) = hi[0];
-    *reinterpret_cast<u32x4*>(&sA[buf].hi[o + 8]) = hi[1];
-    *reinterpret_cast<u32x4*>(&sA[buf].lo[o]) = lo[0];
-    *reinterpret_cast<u32x4*>(&sA[buf].lo[o + 8]) = lo[1];
-    split16(pb, hi, lo);
-    *reinterpret_cast<u32x4*>(&sB[buf].hi[o]) = hi[0];
-    *reinterpret_cast<u32x4*>(&sB[buf].hi[o + 8]) = hi[1];
-    *reinterpret_cast<u32x4*>(&sB[buf].lo[o]) = lo[0];
-    *reinterpret_cast<u32x4*>(&sB[buf].lo[o + 8]) = lo[1];
+#pragma unroll
+    for (int q = 0; q < kF4 / 2; ++q) {
+      u32x4 hi, lo;
+      split8(pa[2 * q], pa[2 * q + 1], hi, lo);
+      *reinterpret_cast<u32x4*>(&sA[buf].hi[o + 8 * q]) = hi;
+      *reinterpret_cast<u32x4*>(&sA[buf].lo[o + 8 * q]) = lo;
+      split8(pb[2 * q], pb[2 * q + 1], hi, lo);
+      *reinterpret_cast<u32x4*>(&sB[buf].hi[o + 8 * q]) = hi;
+      *reinterpret_cast<u32x4*>(&sB[buf].lo[o + 8 * q]) = lo;
+    }
   };
 
   gload(0);
@@ -207,7 +206,7 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_k(GArgs a) {
     const Img& ta = sA[cur];
     const Img& tb = sB[cur];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < kBK / 16; ++ks) {
       bf16x8 ah[2], al[2], bh[2], bl[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
@@ -244,6 +243,7 @@ RSX_API int rsx_gemm_x3(const float* A, int64_t lda, const float* B, int64_t ldb
                         int64_t ldc, void* stream) {
   RSX_ARG(A && B && C, "null tensor");
   RSX_ARG(M >= 0 && N > 0 && K > 0 && N % kBN == 0 && K % kBK == 0, "N must be a multiple of 128, K of 32");
+  static_assert(kBK == 16 || kBK == 32, "stage depth 16 or 32");
   RSX_ARG(lda >= K && ldb >= K && ldc >= N && lda % 4 == 0 && ldb % 4 == 0, "bad leading dimensions");
   RSX_ARG(((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0, "A/B must be 16-byte aligned");
   RSX_ARG(epi == EPI_BIAS || epi == EPI_GELU_DROP || epi == EPI_DGELU_DROP, "epi must be 0, 1 or 2");

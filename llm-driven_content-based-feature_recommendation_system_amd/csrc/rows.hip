@@ -117,6 +117,44 @@ unsigned grid_for(int64_t n, int D) {
   return (unsigned)b;
 }
 
+// Segmented row sums: dst[rows[u]] (+)= scale * sum_{k in [seg[u], seg[u+1])} src[perm[k]].
+// The deterministic, atomic-free form of a scatter-add with repeated indices when the sort by
+// destination row is known (the embedding-table gradient of the user tower's item ids, whose
+// Zipf-hot rows made the atomic form contend): one row group of lanes per segment, summed in
+// segment order. rows[u] == skip (padding_idx) is left untouched; scale: device scalar.
+template <int D>
+__global__ __launch_bounds__(256) void segsum_rows_k(const float* __restrict__ src, int64_t ld_src,
+                                                    const int64_t* __restrict__ perm,
+                                                    const int64_t* __restrict__ seg,
+                                                    const int64_t* __restrict__ rows, int64_t nseg,
+                                                    const float* __restrict__ scale, int64_t skip,
+                                                    float* __restrict__ dst, int64_t ld_dst, int accumulate) {
+  constexpr int LPR = RowGeo<D>::LPR, RPW = RowGeo<D>::RPW;
+  const int lane = threadIdx.x & 63, sub = lane / LPR, c = lane % LPR;
+  const int64_t wave_g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const float sc = scale ? scale[0] : 1.0f;
+  for (int64_t u0 = wave_g * RPW; u0 < nseg; u0 += nw * RPW) {
+    const int64_t u = u0 + sub;
+    if (u >= nseg) continue;
+    const int64_t row = rows[u];
+    if (row == skip) continue;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int64_t k1 = seg[u + 1];
+    for (int64_t k = seg[u]; k < k1; ++k) {
+      const float4 x = reinterpret_cast<const float4*>(src + perm[k] * ld_src)[c];
+      acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
+    }
+    float4* d = reinterpret_cast<float4*>(dst + row * ld_dst) + c;
+    float4 v = make_float4(sc * acc.x, sc * acc.y, sc * acc.z, sc * acc.w);
+    if (accumulate) {
+      const float4 o = *d;
+      v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+    }
+    *d = v;
+  }
+}
+
 }  // namespace
 
 RSX_API int rsx_gather_rows(const float* src, int64_t ld_src, const int64_t* idx, int64_t n, int64_t D, int normalize,
@@ -163,6 +201,25 @@ RSX_API int rsx_scatter_rows(const float* dy, const float* y, const float* nrm, 
   RSX_SD(64) RSX_SD(128) RSX_SD(256)
 #undef RSX_SD
 #undef RSX_S
+  RSX_LAUNCHED();
+  return 0;
+}
+
+RSX_API int rsx_segment_sum_rows(const float* src, int64_t ld_src, const int64_t* perm, const int64_t* seg_off,
+                                 const int64_t* rows, int64_t nseg, int64_t D, const float* scale, int64_t skip_row,
+                                 float* dst, int64_t ld_dst, int accumulate, void* stream) {
+  RSX_ARG(src && perm && seg_off && rows && dst, "null tensor");
+  RSX_ARG(D == 64 || D == 128 || D == 256, "D must be 64, 128 or 256");
+  RSX_ARG(ld_src >= D && ld_dst >= D && ld_src % 4 == 0 && ld_dst % 4 == 0, "bad leading dimensions");
+  if (nseg == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned g = grid_for(nseg, (int)D);
+#define RSX_SS(DD)                                                                                            \
+  if (D == DD)                                                                                                \
+    hipLaunchKernelGGL(segsum_rows_k<DD>, dim3(g), dim3(256), 0, st, src, ld_src, perm, seg_off, rows, nseg, \
+                       scale, skip_row, dst, ld_dst, accumulate);
+  RSX_SS(64) RSX_SS(128) RSX_SS(256)
+#undef RSX_SS
   RSX_LAUNCHED();
   return 0;
 }

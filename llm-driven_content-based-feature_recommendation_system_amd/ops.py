@@ -56,7 +56,7 @@ def _c(t):
 class _SeqEmbed(torch.autograd.Function):
     @staticmethod
     def forward(ctx, base, gate, pos, ln_w, ln_b, ids, cfg, tok_pos, *tables):
-        eps, p_drop, seed, padding_idx, L = cfg
+        eps, p_drop, seed, padding_idx, L, tab0_seg = cfg
         N.ensure_device(base)
         D = base.shape[-1]
         T = base.numel() // D
@@ -74,6 +74,7 @@ class _SeqEmbed(torch.autograd.Function):
         N.check(rc, "seq_embed_fwd")
         ctx.save_for_backward(base, gate, pos, ln_w, mean, rstd, tok_pos, *ids, *tables)
         ctx.cfg = (eps, p_drop, seed, padding_idx, len(tables), T, L, D)
+        ctx.tab0_seg = tab0_seg
         return out
 
     @staticmethod
@@ -92,22 +93,69 @@ class _SeqEmbed(torch.autograd.Function):
         dlnb = torch.zeros_like(ln_w) if need[4] else None
         dtabs = [torch.zeros_like(t) if need[8 + j] else None for j, t in enumerate(tables)]
         rows = N.i64_array([t.shape[0] for t in tables])
+        # table 0 with a prepared sort by id: segmented sums of dx (= dbase) instead of atomics
+        seg0 = ctx.tab0_seg if (nt > 0 and dtabs[0] is not None) else None
+        if seg0 is not None and dbase is None:
+            dbase = torch.empty_like(base)
+        kern_tabs = ([None] + dtabs[1:]) if seg0 is not None else dtabs
         rc = N.lib().rsx_seq_embed_bwd(
             N.ptr(base), N.ptr_array(ids), N.ptr_array(tables), rows,
             N.i64_array(padding_idx), nt, N.ptr(gate), N.ptr(pos), N.ptr(tok_pos), N.ptr(ln_w), N.ptr(mean),
-            N.ptr(rstd), eps, T, L, D, p_drop, seed, N.ptr(dout), N.ptr(dbase), N.ptr_array(dtabs), N.ptr(dgate),
-            N.ptr(dpos), N.ptr(dlnw), N.ptr(dlnb), N.stream())
+            N.ptr(rstd), eps, T, L, D, p_drop, seed, N.ptr(dout), N.ptr(dbase), N.ptr_array(kern_tabs),
+            N.ptr(dgate), N.ptr(dpos), N.ptr(dlnw), N.ptr(dlnb), N.stream())
         N.check(rc, "seq_embed_bwd")
+        if seg0 is not None:  # chunk partials, then per-id sums of its chunks (both deterministic)
+            perm, cb, chunk_ids, ch_off, uniq = seg0
+            part = torch.empty(chunk_ids.numel(), D, device=base.device, dtype=torch.float32)
+            rc = N.lib().rsx_segment_sum_rows(N.ptr(dbase), D, N.ptr(perm), N.ptr(cb), N.ptr(chunk_ids),
+                                              chunk_ids.numel(), D, None, -1, N.ptr(part), D, 0, N.stream())
+            N.check(rc, "segment_sum_rows(chunks)")
+            rc = N.lib().rsx_segment_sum_rows(N.ptr(part), D, N.ptr(chunk_ids), N.ptr(ch_off), N.ptr(uniq),
+                                              uniq.numel(), D, N.ptr(gate), padding_idx[0], N.ptr(dtabs[0]),
+                                              dtabs[0].stride(0), 1, N.stream())
+            N.check(rc, "segment_sum_rows(ids)")
+        if not need[0]:
+            dbase = None
         return (dbase, dgate, dpos, dlnw, dlnb, None, None, None, *dtabs)
 
 
-def seq_embed(base, ids, tables, gate, pos, ln_w, ln_b, eps=1e-5, p_drop=0.0, padding_idx=None, tok_pos=None):
+_SEG_CHUNK = 64
+
+
+def sort_segments(ids):
+    """Two-level plan for the sorted segmented sums of table 0's gradient (seq_embed tab0_seg):
+    ids[perm] sorted (stable); the sorted tokens are cut into chunks of <= 64 tokens that never
+    straddle two ids (chunk c = [cb[c], cb[c+1])), so a Zipf-hot id's thousands of tokens are
+    summed by many chunks in parallel; segment u (id uniq[u]) owns chunks [ch_off[u],
+    ch_off[u+1]). Its size queries synchronise the host (build it ahead, e.g. in
+    dist.prepare_step_index_async). Returns (perm, cb, chunk_ids, ch_off, uniq)."""
+    ids = ids.reshape(-1)
+    dev = ids.device
+    srt, perm = torch.sort(ids, stable=True)
+    uniq, cnt = torch.unique_consecutive(srt, return_counts=True)
+    seg_off = torch.zeros(uniq.numel() + 1, device=dev, dtype=torch.int64)
+    seg_off[1:] = torch.cumsum(cnt, 0)
+    nch = (cnt + _SEG_CHUNK - 1) // _SEG_CHUNK
+    ch_off = torch.zeros(uniq.numel() + 1, device=dev, dtype=torch.int64)
+    ch_off[1:] = torch.cumsum(nch, 0)
+    total = int(ch_off[-1])
+    ch_seg = torch.repeat_interleave(torch.arange(uniq.numel(), device=dev), nch, output_size=total)
+    k = torch.arange(total, device=dev)
+    cb = torch.empty(total + 1, device=dev, dtype=torch.int64)
+    cb[:-1] = seg_off[ch_seg] + _SEG_CHUNK * (k - ch_off[ch_seg])
+    cb[-1] = ids.numel()
+    return perm, cb, k, ch_off, uniq
+
+
+def seq_embed(base, ids, tables, gate, pos, ln_w, ln_b, eps=1e-5, p_drop=0.0, padding_idx=None, tok_pos=None,
+              tab0_seg=None):
     """x = base + sum_j tables[j][ids[j]] * gate[j] + pos[l] ; LayerNorm ; dropout.
 
     Dense: base [B, L, D], ids [B, L], pos [>= L, D] (position = token % L).
     Packed: base [T, D], ids [T], tok_pos [T] int64 positions, pos [L, D].
     gate [ntab]; ln_w/ln_b [D]. padding_idx: per-table row excluded from the table gradient
-    (nn.Embedding semantics).
+    (nn.Embedding semantics). tab0_seg: sort_segments(ids[0]) — table 0's gradient then comes
+    from rsx_segment_sum_rows (deterministic, no atomics) instead of the kernel's scatter-add.
     """
     if padding_idx is None:
         padding_idx = [-1] * len(tables)
@@ -119,7 +167,7 @@ def seq_embed(base, ids, tables, gate, pos, ln_w, ln_b, eps=1e-5, p_drop=0.0, pa
     else:
         L = pos.shape[0]
         tok_pos = _c(tok_pos)
-    cfg = (float(eps), float(p_drop), seed, padding_idx, int(L))
+    cfg = (float(eps), float(p_drop), seed, padding_idx, int(L), tab0_seg)
     return _SeqEmbed.apply(base, gate, pos, ln_w, ln_b, list(ids), cfg, tok_pos, *tables)
 
 

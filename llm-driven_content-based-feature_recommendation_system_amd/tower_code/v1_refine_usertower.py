@@ -213,7 +213,7 @@ class SASRecUserTower(nn.Module):
             [self.item_id_emb.weight, self.time_emb.weight, self.type_emb.weight, self.color_emb.weight,
              self.graphic_emb.weight, self.section_emb.weight],
             s_g, self.pos_emb.weight, self.emb_ln.weight, self.emb_ln.bias, eps=self.emb_ln.eps, p_drop=p,
-            padding_idx=[0, 0, 0, 0, 0, 0], tok_pos=packed.tok_pos)
+            padding_idx=[0, 0, 0, 0, 0, 0], tok_pos=packed.tok_pos, tab0_seg=getattr(packed, "item_seg", None))
         x = self._encoder_stack(x, packed.tok_pad, p, seg_off=packed.seg_off)
         profile = self._static_profile(age_bucket, price_bucket, cnt_bucket, recency_bucket, channel_ids,
                                        club_status_ids, news_freq_ids, fn_ids, active_ids, cont_feats, u_g)

@@ -116,6 +116,8 @@ def pack_inputs(batch, pretrained_vecs=None, pretrained_lookup=None):
     pk2 = PackedTokens(torch.cat([pm, pm]))
     T = pk.flat.numel()
     tok_ids = [torch.cat([t, t]) for t in (pk.take(batch[k]) for k in _SEQ_ID_KEYS)]
+    if tok_ids[0].is_cuda:
+        pk2.item_seg = ops.sort_segments(tok_ids[0])  # item-id embedding gradient without atomics
     if pretrained_vecs is not None:
         pv_tok = pk.take(pretrained_vecs)
     else:

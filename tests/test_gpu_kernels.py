@@ -48,7 +48,10 @@ def test_seq_embed_gather_bit_exact(gpu):
     assert torch.equal(out.cpu(), ref), (out.cpu() - ref).abs().max()
 
 
-def test_seq_embed_layernorm_and_backward(gpu):
+@pytest.mark.parametrize("seg", [False, True])
+def test_seq_embed_layernorm_and_backward(gpu, seg):
+    """Forward (atol 2e-6) and every gradient (atol 2e-5 / rtol 1e-4) vs float64; seg=True
+    takes table 0's gradient from the sorted segmented sums (rsx_segment_sum_rows)."""
     base, tables, ids, gate, pos, lw, lb = _embed_inputs(seed=1)
     leaves = [t.clone().double().requires_grad_() for t in [base, *tables, gate, pos, lw, lb]]
     b64, t64, g64, p64, w64, bb64 = leaves[0], leaves[1:7], leaves[7], leaves[8], leaves[9], leaves[10]
@@ -62,7 +65,8 @@ def test_seq_embed_layernorm_and_backward(gpu):
 
     dev = [t.clone().to(gpu).requires_grad_() for t in [base, *tables, gate, pos, lw, lb]]
     out = ops.seq_embed(dev[0], [i.to(gpu) for i in ids], dev[1:7], dev[7], dev[8], dev[9], dev[10],
-                        eps=1e-5, padding_idx=[0] * 6)
+                        eps=1e-5, padding_idx=[0] * 6,
+                        tab0_seg=ops.sort_segments(ids[0].to(gpu)) if seg else None)
     torch.testing.assert_close(out.cpu().double(), ref.detach(), atol=2e-6, rtol=0)
     (out * dout.float().to(gpu)).sum().backward()
     names = ["base"] + [f"table{j}" for j in range(6)] + ["gate", "pos", "ln_w", "ln_b"]
