@@ -20,9 +20,10 @@
 //                  acc = dAct = dY2 . W2)
 //
 // Tiling: 128 x 128 output tile per 256-thread workgroup (four waves of 64 x 64 = 2 x 2
-// MFMA tiles), K staged 32 at a time, double-buffered in LDS with register prefetch and one
-// barrier per stage. LDS rows are 32 bf16 + 8 pad (80 B): the fragment reads (ds_read_b128,
-// 32 rows x 16 B per lane half) are bank-conflict free. XCD-aware order: the N tiles of one
+// MFMA tiles), K staged 16 at a time, double-buffered in LDS with register prefetch and one
+// barrier per stage. LDS rows are 16 bf16 + 8 pad (48 B): the fragment reads (ds_read_b128,
+// 32 rows x 16 B per lane half) are bank-conflict free, and 48 KB per workgroup leaves room
+// for three workgroups per CU (the GEMMs are latency-bound at two). XCD-aware order: the N tiles of one
 // M block run back to back on one XCD, so A's rows are re-read from that XCD's L2.
 #include "rsx_common.h"
 
@@ -33,14 +34,14 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 #ifndef RSX_GEMM_BK
-#define RSX_GEMM_BK 32
+#define RSX_GEMM_BK 16  // measured (tools/gemm_micro.py): 16 beats 32 by 10-15 % (48 KB LDS: 3 workgroups/CU)
 #endif
 constexpr int kBM = 128, kBN = 128, kBK = RSX_GEMM_BK;
 constexpr int kRow = kBK + 8;  // bf16 per LDS row (80 B at BK 32, 48 B at BK 16: conflict-free b128 reads)
 constexpr int kF4 = kBK / 8;   // float4 loads per thread and operand per stage (two threads per row)
 constexpr int EPI_BIAS = 0, EPI_GELU_DROP = 1, EPI_DGELU_DROP = 2;
 #ifndef RSX_GEMM_BLOCKS
-#define RSX_GEMM_BLOCKS 512
+#define RSX_GEMM_BLOCKS (1 << 30)  // workgroup budget of the multi-tile stream: at BK 16 one tile each measured best
 #endif
 
 __device__ __forceinline__ int tile_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
