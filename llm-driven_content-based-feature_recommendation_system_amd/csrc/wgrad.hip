@@ -148,11 +148,14 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kImgRow = 160;
-constexpr int kImgElems = 5120;
 __device__ __forceinline__ int img_off(int row, int col) { return row * kImgRow + 8 * (row >> 3) + col; }
+// One staged operand: STAGE tokens x 128 columns as bf16 hi/lo images (row stride 160 + 8 per 8 rows).
+template <int STAGE>
 struct X3Img {
-  __bf16 hi[kImgElems];
-  __bf16 lo[kImgElems];
+  static constexpr int kElems = STAGE * kImgRow;  // covers img_off(STAGE - 1, 127)
+  static_assert((STAGE - 1) * kImgRow + 8 * ((STAGE - 1) >> 3) + 128 <= kElems, "image size");
+  __bf16 hi[kElems];
+  __bf16 lo[kElems];
 };
 
 __device__ __forceinline__ void split8(const float4& a, const float4& b, u32x4& hi, u32x4& lo) {
@@ -168,9 +171,13 @@ __device__ __forceinline__ void split8(const float4& a, const float4& b, u32x4& 
   lo = __builtin_bit_cast(u32x4, l);
 }
 
+// STAGE = tokens per LDS stage: 32 (80 KB LDS, two workgroups per CU) or 16 (40 KB, three).
+template <int STAGE>
 __global__ __launch_bounds__(256, 2) void wgrad_x3_k(WArgs a) {
-  __shared__ __attribute__((aligned(16))) X3Img sY[2];
-  __shared__ __attribute__((aligned(16))) X3Img sX[2];
+  constexpr int kStageX3 = STAGE;
+  constexpr int kFpt = STAGE / 2;  // floats per thread and operand per stage (256 threads, 128 columns)
+  __shared__ __attribute__((aligned(16))) X3Img<STAGE> sY[2];
+  __shared__ __attribute__((aligned(16))) X3Img<STAGE> sX[2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, c = lane & 31;
   const int total = a.tiles_n * a.tiles_k * a.nsplit;
@@ -193,12 +200,12 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_k(WArgs a) {
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-  float dbp[16];
+  float dbp[kFpt];
 #pragma unroll
-  for (int q = 0; q < 16; ++q) dbp[q] = 0.0f;
+  for (int q = 0; q < kFpt; ++q) dbp[q] = 0.0f;
 
-  const int srow = tid >> 3, scol = (tid & 7) * 16;
-  float4 py[4], px[4];
+  const int srow = tid / (kTile / kFpt), scol = (tid % (kTile / kFpt)) * kFpt;
+  float4 py[kFpt / 4], px[kFpt / 4];
   auto gload = [&](int64_t t0) {
     const int64_t t = t0 + srow;
     const bool ok = t < t_end;
@@ -210,30 +217,27 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_k(WArgs a) {
     // predicated load is a branch per load
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < kFpt / 4; ++q) {
       const float4 vy = ys[q], vx = xs[q];
       py[q] = oky ? vy : z;
       px[q] = okx ? vx : z;
     }
   };
   auto lstore = [&](int buf) {
-    const int o0 = img_off(srow, scol), o1 = img_off(srow, scol + 8);
-    u32x4 hi, lo;
-    split8(py[0], py[1], hi, lo);
-    *reinterpret_cast<u32x4*>(&sY[buf].hi[o0]) = hi;
-    *reinterpret_cast<u32x4*>(&sY[buf].lo[o0]) = lo;
-    split8(py[2], py[3], hi, lo);
-    *reinterpret_cast<u32x4*>(&sY[buf].hi[o1]) = hi;
-    *reinterpret_cast<u32x4*>(&sY[buf].lo[o1]) = lo;
-    split8(px[0], px[1], hi, lo);
-    *reinterpret_cast<u32x4*>(&sX[buf].hi[o0]) = hi;
-    *reinterpret_cast<u32x4*>(&sX[buf].lo[o0]) = lo;
-    split8(px[2], px[3], hi, lo);
-    *reinterpret_cast<u32x4*>(&sX[buf].hi[o1]) = hi;
-    *reinterpret_cast<u32x4*>(&sX[buf].lo[o1]) = lo;
+#pragma unroll
+    for (int q = 0; q < kFpt / 8; ++q) {
+      const int o = img_off(srow, scol + 8 * q);
+      u32x4 hi, lo;
+      split8(py[2 * q], py[2 * q + 1], hi, lo);
+      *reinterpret_cast<u32x4*>(&sY[buf].hi[o]) = hi;
+      *reinterpret_cast<u32x4*>(&sY[buf].lo[o]) = lo;
+      split8(px[2 * q], px[2 * q + 1], hi, lo);
+      *reinterpret_cast<u32x4*>(&sX[buf].hi[o]) = hi;
+      *reinterpret_cast<u32x4*>(&sX[buf].lo[o]) = lo;
+    }
     if (do_db) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < kFpt / 4; ++q) {
         dbp[4 * q] += py[q].x;
         dbp[4 * q + 1] += py[q].y;
         dbp[4 * q + 2] += py[q].z;
@@ -256,12 +260,12 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_k(WArgs a) {
     lstore(0);
     __syncthreads();
     int cur = 0;
-    for (int64_t t0 = t_begin; t0 < t_end; t0 += kStage) {
-      const bool has_next = t0 + kStage < t_end;
-      if (has_next) gload(t0 + kStage);
+    for (int64_t t0 = t_begin; t0 < t_end; t0 += kStageX3) {
+      const bool has_next = t0 + kStageX3 < t_end;
+      if (has_next) gload(t0 + kStageX3);
       if (live) {
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
+        for (int ks = 0; ks < kStageX3 / 16; ++ks) {
           bf16x8 ah[2], al[2], bh[2], bl[2];
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
@@ -301,14 +305,14 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_k(WArgs a) {
   }
   if (do_db) {
     // column sums of the 32 token rows: threads with equal tid&7 hold the same 16 columns
-    float* red = reinterpret_cast<float*>(&sY[0]);  // free after the loop's last barrier
+    float* red = reinterpret_cast<float*>(&sY[0]);  // free after the loop's last barrier (>= kStageX3 x 128 floats)
 #pragma unroll
-    for (int q = 0; q < 16; ++q) red[srow * kTile + scol + q] = dbp[q];
+    for (int q = 0; q < kFpt; ++q) red[srow * kTile + scol + q] = dbp[q];
     __syncthreads();
     if (tid < kTile) {
       float s = 0.0f;
 #pragma unroll 8
-      for (int t = 0; t < 32; ++t) s += red[t * kTile + tid];
+      for (int t = 0; t < kStageX3; ++t) s += red[t * kTile + tid];
       if (n0 + tid < a.N) a.part[split * pstride + (int64_t)a.N * a.K + n0 + tid] = s;
     }
   }
@@ -397,7 +401,10 @@ int wgrad_launch(bool x3, const float* dY, int64_t ldy, const float* X, int64_t 
   a.part = ws;
   a.with_db = db != nullptr;
   const int blocks = a.tiles_n * a.tiles_k * a.nsplit;
-  if (x3) hipLaunchKernelGGL(wgrad_x3_k, dim3(blocks), dim3(256), 0, st, a);
+  // 16-token stages measured faster for three or more output row tiles (tools/gemm_micro.py wgrad_384x128:
+  // 0.119 vs 0.146 ms) and slower for fewer (wgrad_128x256: 0.075 vs 0.068 ms).
+  if (x3 && a.tiles_n >= 3) hipLaunchKernelGGL(wgrad_x3_k<16>, dim3(blocks), dim3(256), 0, st, a);
+  else if (x3) hipLaunchKernelGGL(wgrad_x3_k<32>, dim3(blocks), dim3(256), 0, st, a);
   else hipLaunchKernelGGL(wgrad_k, dim3(blocks), dim3(256), 0, st, a);
   RSX_LAUNCHED();
   const int64_t pstride4 = (N * K + N) / 4;
