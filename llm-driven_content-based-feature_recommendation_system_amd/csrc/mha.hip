@@ -394,7 +394,7 @@ __global__ __launch_bounds__(256) void mha_bwd_mfma_k(BwdArgs a) {
     f32x16 dkT, dvT;
 #pragma unroll
     for (int r = 0; r < 16; ++r) { dkT[r] = 0.0f; dvT[r] = 0.0f; }
-    for (int qb = kb; qb < nb; ++qb) {
+    for (int qb = a.causal ? kb : 0; qb < nb; ++qb) {  // non-causal: every query block
       float qr[16], gr[16];
       const int iq = 32 * qb + c;
       load_row16(qr, Qb, ld, iq, iq < L, h);
@@ -463,6 +463,312 @@ __global__ __launch_bounds__(256) void mha_bwd_mfma_k(BwdArgs a) {
   }
 }
 
+// ---- bf16x3 forward and backward (head dim 32) ------------------------------------------
+// Same semantics, masks, dropout hash and lse as the kernels above, on 16x16 tiles of the bf16
+// MFMA: every fp32 operand x is split x = hi + lo (hi = bf16(x), lo = bf16(x - hi)) and a
+// product is hi*hi' + hi*lo' + lo*hi' with fp32 accumulation (~2^-17 relative error per term,
+// the precision of the bf16x3 InfoNCE and token GEMMs).
+//   score tiles  S = Q K^T, dP = dO V^T over the 32 head dims: one v_mfma_f32_16x16x32_bf16
+//                per split product (lane (c,g) holds row c, dims 8g..8g+7 of each operand);
+//   token sums   O = P V, dV = Pd^T dO, dK = dS^T Q, dQ = dS K over 16 tokens:
+//                v_mfma_f32_16x16x16_bf16 with the A operand taken straight from the score
+//                accumulator (lane (c,g) register r holds tile row 4g+r, column c = exactly the
+//                A fragment of the transposed product) and the B operand gathered as columns
+//                (4 rows x 1 float per lane, L1/L2 hits of rows this wave just read).
+// One wave per (sequence, head), four per workgroup, no LDS; 16-token blocks waste less of
+// the tile than 32 on the H&M lengths (mean ~19 tokens). MFMA cycles per 16x16 block pair:
+// fwd 3x16 + 6x8, bwd (two passes) 12x16 + 18x8, against 8x(16x4 f32) = 256 per product on
+// the fp32 MFMA.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct Row8 {  // dims 8g .. 8g+7 of one token row, split
+  bf16x8 hi, lo;
+};
+struct Col4 {  // 4 consecutive token rows of one column, split
+  s16x4 hi, lo;
+};
+
+__device__ __forceinline__ Row8 load_row8(const float* base, int64_t ld, int row, bool ok, int g) {
+  float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
+  if (ok) {
+    const float4* p = reinterpret_cast<const float4*>(base + (int64_t)row * ld + 8 * g);
+    v0 = p[0];
+    v1 = p[1];
+  }
+  const float f[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+  Row8 r;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const __bf16 h = (__bf16)f[k];
+    r.hi[k] = h;
+    r.lo[k] = (__bf16)(f[k] - (float)h);
+  }
+  return r;
+}
+
+__device__ __forceinline__ Col4 split4(const float (&f)[4]) {
+  bf16x4 h, l;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const __bf16 hk = (__bf16)f[k];
+    h[k] = hk;
+    l[k] = (__bf16)(f[k] - (float)hk);
+  }
+  Col4 c;
+  c.hi = __builtin_bit_cast(s16x4, h);
+  c.lo = __builtin_bit_cast(s16x4, l);
+  return c;
+}
+
+// column col of rows row0 .. row0+3 (zero past L)
+__device__ __forceinline__ Col4 load_col4(const float* base, int64_t ld, int row0, int L, int col) {
+  float f[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) f[t] = (row0 + t < L) ? base[(int64_t)(row0 + t) * ld + col] : 0.0f;
+  return split4(f);
+}
+
+__device__ __forceinline__ f32x4 dot16_x3(const Row8& a, const Row8& b) {
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.lo, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.lo, b.hi, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.hi, acc, 0, 0, 0);
+  return acc;
+}
+
+__device__ __forceinline__ f32x4 sum16_x3(const Col4& a, const Col4& b, f32x4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a.hi, b.lo, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a.lo, b.hi, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a.hi, b.hi, acc, 0, 0, 0);
+  return acc;
+}
+
+__global__ __launch_bounds__(256) void mha_fwd_x3_k(FwdArgs a) {
+  constexpr int DH = 32;
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int64_t unit = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (unit >= (int64_t)a.B * a.H) return;  // whole wave exits together
+  const int b = (int)(unit / a.H), hd = (int)(unit % a.H);
+  const int D = a.H * DH;
+  const int64_t ld = 3 * (int64_t)D;
+  const int64_t tok0 = a.seg ? (int64_t)a.seg[b] : (int64_t)b * a.L;
+  int L = a.seg ? (a.seg[b + 1] - a.seg[b]) : a.L;
+  if (L > kLMax) L = kLMax;
+  if (L <= 0) return;
+  const int nb = (L + 15) >> 4;
+  const float* Qb = a.qkv + tok0 * ld + hd * DH;
+  const float* Kb = Qb + D;
+  const float* Vb = Qb + 2 * D;
+  float* Ob = a.out + tok0 * D + hd * DH;
+  const int my_pad = (lane < L) ? (a.kpad ? (int)a.kpad[tok0 + lane] : 0) : 1;
+
+  for (int qb = 0; qb < nb; ++qb) {
+    const int i = 16 * qb + c;  // query of this lane's score column
+    const bool iok = i < L;
+    const Row8 qx = load_row8(Qb, ld, i, iok, g);
+    const int kb_end = a.causal ? qb : nb - 1;
+    f32x4 s[4];
+    float m = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      if (kb <= kb_end) {
+        const Row8 kx = load_row8(Kb, ld, 16 * kb + c, 16 * kb + c < L, g);
+        s[kb] = dot16_x3(kx, qx);  // S^T: [key 16kb+4g+r][query i]
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int j = 16 * kb + 4 * g + r;
+          const int jpad = __shfl(my_pad, j & 63, 64);
+          const bool allowed = iok && j < L && !jpad && (!a.causal || j <= i);
+          s[kb][r] = allowed ? s[kb][r] * a.scale : -INFINITY;
+          m = fmaxf(m, s[kb][r]);
+        }
+      }
+    }
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float l = 0.0f;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      if (kb <= kb_end) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = (s[kb][r] == -INFINITY) ? 0.0f : __expf(s[kb][r] - m);
+          s[kb][r] = p;
+          l += p;
+        }
+      }
+    }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = (l > 0.0f) ? 1.0f / l : 0.0f;
+    f32x4 o[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    const uint64_t rowidx = ((uint64_t)(tok0 + i) * a.H + hd) * kLMax;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      if (kb <= kb_end) {
+        float p[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) p[r] = a.drop.apply(s[kb][r] * inv, rowidx + 16 * kb + 4 * g + r);
+        const Col4 pa = split4(p);
+#pragma unroll
+        for (int et = 0; et < 2; ++et) o[et] = sum16_x3(pa, load_col4(Vb, ld, 16 * kb + 4 * g, L, 16 * et + c), o[et]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * qb + 4 * g + r;
+      if (row < L) {
+        Ob[(int64_t)row * D + c] = o[0][r];
+        Ob[(int64_t)row * D + 16 + c] = o[1][r];
+      }
+    }
+    if (a.lse && g == 0 && iok) a.lse[(tok0 + i) * a.H + hd] = (l > 0.0f) ? m + logf(l) : -INFINITY;
+  }
+}
+
+__global__ __launch_bounds__(256) void mha_bwd_x3_k(BwdArgs a) {
+  constexpr int DH = 32;
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int64_t unit = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (unit >= (int64_t)a.B * a.H) return;  // whole wave exits together
+  const int b = (int)(unit / a.H), hd = (int)(unit % a.H);
+  const int D = a.H * DH;
+  const int64_t ld = 3 * (int64_t)D;
+  const int64_t tok0 = a.seg ? (int64_t)a.seg[b] : (int64_t)b * a.L;
+  int L = a.seg ? (a.seg[b + 1] - a.seg[b]) : a.L;
+  if (L > kLMax) L = kLMax;
+  if (L <= 0) return;
+  const int nb = (L + 15) >> 4;
+  const float* Qb = a.qkv + tok0 * ld + hd * DH;
+  const float* Kb = Qb + D;
+  const float* Vb = Qb + 2 * D;
+  const float* dOb = a.dout + tok0 * D + hd * DH;
+  const float* Ob = a.out + tok0 * D + hd * DH;
+  float* dQb = a.dqkv + tok0 * ld + hd * DH;
+  float* dKb = dQb + D;
+  float* dVb = dQb + 2 * D;
+  const float sc = a.scale;
+
+  // per-token softmax statistics (token t < L on lane t): lse_t, delta_t = dO_t . O_t, key pad
+  float my_lse = -INFINITY, my_delta = 0.0f;
+  int my_pad = 1;
+  if (lane < L) {
+    my_lse = a.lse[(tok0 + lane) * a.H + hd];
+    const float4* op = reinterpret_cast<const float4*>(Ob + (int64_t)lane * D);
+    const float4* gp = reinterpret_cast<const float4*>(dOb + (int64_t)lane * D);
+    float d = 0.0f;
+#pragma unroll
+    for (int t = 0; t < DH / 4; ++t) {
+      const float4 x = op[t], y = gp[t];
+      d += x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
+    }
+    my_delta = d;
+    my_pad = a.kpad ? (int)a.kpad[tok0 + lane] : 0;
+  }
+  // dS_ij and the dropped-out probability Pd_ij of one score element (mha_bwd_k's formulas)
+  auto grad_elem = [&](int i, int j, float s, float dp, float lse_i, float delta_i, bool allowed, float& pd_out) {
+    pd_out = 0.0f;
+    if (!allowed) return 0.0f;
+    const float p = __expf(s * sc - lse_i);
+    float pd = p, dpd = dp;
+    if (a.drop.active()) {
+      const uint64_t idx = ((uint64_t)(tok0 + i) * a.H + hd) * kLMax + j;
+      const bool keep = rsx::hash_u32(a.drop.seed, idx) >= a.drop.thresh;
+      pd = keep ? p * a.drop.scale : 0.0f;
+      dpd = keep ? dp * a.drop.scale : 0.0f;
+    }
+    pd_out = pd;
+    return p * (dpd - delta_i) * sc;
+  };
+
+  // ---- pass 1: key block on the score columns (j = 16kb + c): dK, dV ----
+  for (int kb = 0; kb < nb; ++kb) {
+    const int j = 16 * kb + c;
+    const bool jok = j < L;
+    const int jpad = __shfl(my_pad, j & 63, 64);
+    const Row8 kx = load_row8(Kb, ld, j, jok, g);
+    const Row8 vx = load_row8(Vb, ld, j, jok, g);
+    f32x4 dk[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    f32x4 dv[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    for (int qb = a.causal ? kb : 0; qb < nb; ++qb) {
+      const int iq = 16 * qb + c;
+      const Row8 qx = load_row8(Qb, ld, iq, iq < L, g);
+      const Row8 gx = load_row8(dOb, D, iq, iq < L, g);
+      f32x4 S = dot16_x3(qx, kx);   // [query 16qb+4g+r][key j]
+      f32x4 dP = dot16_x3(gx, vx);  // [query][key]
+      float ds[4], pd[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 16 * qb + 4 * g + r;
+        const float lse_i = __shfl(my_lse, i & 63, 64);
+        const float del_i = __shfl(my_delta, i & 63, 64);
+        const bool allowed = jok && i < L && !jpad && (!a.causal || j <= i) && lse_i != -INFINITY;
+        ds[r] = grad_elem(i, j, S[r], dP[r], lse_i, del_i, allowed, pd[r]);
+      }
+      const Col4 pa = split4(pd), sa = split4(ds);
+#pragma unroll
+      for (int et = 0; et < 2; ++et) {
+        dv[et] = sum16_x3(pa, load_col4(dOb, D, 16 * qb + 4 * g, L, 16 * et + c), dv[et]);  // dV[j][e]
+        dk[et] = sum16_x3(sa, load_col4(Qb, ld, 16 * qb + 4 * g, L, 16 * et + c), dk[et]);  // dK[j][e]
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * kb + 4 * g + r;
+      if (row < L) {
+#pragma unroll
+        for (int et = 0; et < 2; ++et) {
+          dKb[(int64_t)row * ld + 16 * et + c] = dk[et][r];
+          dVb[(int64_t)row * ld + 16 * et + c] = dv[et][r];
+        }
+      }
+    }
+  }
+
+  // ---- pass 2: query block on the score columns (i = 16qb + c): dQ ----
+  for (int qb = 0; qb < nb; ++qb) {
+    const int i = 16 * qb + c;
+    const bool iok = i < L;
+    const float lse_i = __shfl(my_lse, i & 63, 64);
+    const float del_i = __shfl(my_delta, i & 63, 64);
+    const Row8 qx = load_row8(Qb, ld, i, iok, g);
+    const Row8 gx = load_row8(dOb, D, i, iok, g);
+    f32x4 dq[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    const int kb_end = a.causal ? qb : nb - 1;
+    for (int kb = 0; kb <= kb_end; ++kb) {
+      const int jr = 16 * kb + c;
+      const Row8 kx = load_row8(Kb, ld, jr, jr < L, g);
+      const Row8 vx = load_row8(Vb, ld, jr, jr < L, g);
+      f32x4 St = dot16_x3(kx, qx);   // [key 16kb+4g+r][query i]
+      f32x4 dPt = dot16_x3(vx, gx);  // [key][query]
+      float ds[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = 16 * kb + 4 * g + r;
+        const int jpad = __shfl(my_pad, j & 63, 64);
+        const bool allowed = iok && j < L && !jpad && (!a.causal || j <= i) && lse_i != -INFINITY;
+        float pd;
+        ds[r] = grad_elem(i, j, St[r], dPt[r], lse_i, del_i, allowed, pd);
+      }
+      const Col4 sa = split4(ds);
+#pragma unroll
+      for (int et = 0; et < 2; ++et)
+        dq[et] = sum16_x3(sa, load_col4(Kb, ld, 16 * kb + 4 * g, L, 16 * et + c), dq[et]);  // dQ[i][e]
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * qb + 4 * g + r;
+      if (row < L) {
+        dQb[(int64_t)row * ld + c] = dq[0][r];
+        dQb[(int64_t)row * ld + 16 + c] = dq[1][r];
+      }
+    }
+  }
+}
+
 }  // namespace
 
 RSX_API int rsx_mha_fwd(const float* qkv, const uint8_t* key_pad, const int* seg_off, int64_t B, int64_t L,
@@ -505,6 +811,43 @@ RSX_API int rsx_mha_bwd(const float* qkv, const uint8_t* key_pad, const int* seg
   const dim3 grid((unsigned)(B * H));
   if (Dh == 16) hipLaunchKernelGGL(mha_bwd_k<16>, grid, dim3(64), 0, st, a);
   else hipLaunchKernelGGL(mha_bwd_mfma_k, dim3((unsigned)((B * H + 3) / 4)), dim3(256), 0, st, a);
+  RSX_LAUNCHED();
+  return 0;
+}
+
+RSX_API int rsx_mha_fwd_x3(const float* qkv, const uint8_t* key_pad, const int* seg_off, int64_t B, int64_t L,
+                           int64_t H, int64_t Dh, int causal, float p_drop, uint64_t seed, float* out, float* lse,
+                           void* stream) {
+  RSX_ARG(qkv && out, "null tensor");
+  RSX_ARG(L >= 1 && L <= kLMax, "L must be in [1,64]");
+  RSX_ARG(Dh == 32, "bf16x3 attention head dim must be 32");
+  RSX_ARG(H >= 1, "H must be >= 1");
+  RSX_ARG(p_drop >= 0.0f && p_drop < 1.0f, "p_drop must be in [0,1)");
+  if (B == 0) return 0;
+  FwdArgs a;
+  a.qkv = qkv; a.kpad = key_pad; a.seg = seg_off; a.out = out; a.lse = lse;
+  a.B = (int)B; a.L = (int)L; a.H = (int)H; a.causal = causal;
+  a.scale = 1.0f / sqrtf((float)Dh);
+  a.drop = rsx::make_dropout(p_drop, seed);
+  hipLaunchKernelGGL(mha_fwd_x3_k, dim3((unsigned)((B * H + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a);
+  RSX_LAUNCHED();
+  return 0;
+}
+
+RSX_API int rsx_mha_bwd_x3(const float* qkv, const uint8_t* key_pad, const int* seg_off, const float* out,
+                           const float* lse, const float* dout, int64_t B, int64_t L, int64_t H, int64_t Dh,
+                           int causal, float p_drop, uint64_t seed, float* dqkv, void* stream) {
+  RSX_ARG(qkv && out && lse && dout && dqkv, "null tensor");
+  RSX_ARG(L >= 1 && L <= kLMax, "L must be in [1,64]");
+  RSX_ARG(Dh == 32, "bf16x3 attention head dim must be 32");
+  RSX_ARG(p_drop >= 0.0f && p_drop < 1.0f, "p_drop must be in [0,1)");
+  if (B == 0) return 0;
+  BwdArgs a;
+  a.qkv = qkv; a.kpad = key_pad; a.seg = seg_off; a.out = out; a.lse = lse; a.dout = dout; a.dqkv = dqkv;
+  a.B = (int)B; a.L = (int)L; a.H = (int)H; a.causal = causal;
+  a.scale = 1.0f / sqrtf((float)Dh);
+  a.drop = rsx::make_dropout(p_drop, seed);
+  hipLaunchKernelGGL(mha_bwd_x3_k, dim3((unsigned)((B * H + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a);
   RSX_LAUNCHED();
   return 0;
 }

@@ -173,6 +173,27 @@ def seq_embed(base, ids, tables, gate, pos, ln_w, ln_b, eps=1e-5, p_drop=0.0, pa
 
 # ----------------------------------------------------------------------------------------
 # A3 / A9: masked MHA core
+# "bf16x3" (default): head dim 32 runs mha_fwd_x3_k / mha_bwd_x3_k (split-bf16 MFMA, ~2^-17
+# relative error per product); other head dims and "fp32" run the fp32 kernels.
+MHA_PRECISIONS = ("fp32", "bf16x3")
+_mha_precision = os.environ.get("RSX_MHA_PRECISION", "bf16x3")
+assert _mha_precision in MHA_PRECISIONS, _mha_precision
+
+
+def set_mha_precision(p: str) -> None:
+    global _mha_precision
+    assert p in MHA_PRECISIONS, p
+    _mha_precision = p
+
+
+def mha_precision() -> str:
+    return _mha_precision
+
+
+def _mha_x3(Dh):
+    return _mha_precision == "bf16x3" and Dh == 32
+
+
 class _MHA(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, key_pad, seg_off, H, causal, p_drop, seed):
@@ -191,8 +212,9 @@ class _MHA(torch.autograd.Function):
         kp = None
         if key_pad is not None:
             kp = _c(key_pad.to(torch.uint8)) if key_pad.dtype != torch.uint8 else _c(key_pad)
-        rc = N.lib().rsx_mha_fwd(N.ptr(qkv), N.ptr(kp), N.ptr(seg_off), B, L, H, Dh, int(causal), p_drop, seed,
-                                 N.ptr(out), N.ptr(lse), N.stream())
+        fn = N.lib().rsx_mha_fwd_x3 if _mha_x3(Dh) else N.lib().rsx_mha_fwd
+        rc = fn(N.ptr(qkv), N.ptr(kp), N.ptr(seg_off), B, L, H, Dh, int(causal), p_drop, seed, N.ptr(out), N.ptr(lse),
+                N.stream())
         N.check(rc, "mha_fwd")
         ctx.save_for_backward(qkv, kp, seg_off, out, lse)
         ctx.cfg = (B, L, H, Dh, int(causal), p_drop, seed)
@@ -204,8 +226,9 @@ class _MHA(torch.autograd.Function):
         qkv, kp, seg_off, out, lse = ctx.saved_tensors
         dout = _c(dout)
         dqkv = torch.empty_like(qkv)
-        rc = N.lib().rsx_mha_bwd(N.ptr(qkv), N.ptr(kp), N.ptr(seg_off), N.ptr(out), N.ptr(lse), N.ptr(dout), B, L, H,
-                                 Dh, causal, p_drop, seed, N.ptr(dqkv), N.stream())
+        fn = N.lib().rsx_mha_bwd_x3 if _mha_x3(Dh) else N.lib().rsx_mha_bwd
+        rc = fn(N.ptr(qkv), N.ptr(kp), N.ptr(seg_off), N.ptr(out), N.ptr(lse), N.ptr(dout), B, L, H, Dh, causal,
+                p_drop, seed, N.ptr(dqkv), N.stream())
         N.check(rc, "mha_bwd")
         return dqkv, None, None, None, None, None, None
 
