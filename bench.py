@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-batch8192", action="store_true",
+                    help="skip the secondary line at global batch 8192 (the batch BASELINE.json's metric names)")
+    ap.add_argument("--steps8192", type=int, default=5)
     ap.add_argument("--no-deepfm", action="store_true", help="skip the DeepFM rerank secondary metric")
     ap.add_argument("--deepfm-rows", type=int, default=65536)
     ap.add_argument("--deepfm-vocab", type=int, default=1_000_000)
@@ -223,6 +226,69 @@ def bench_item_tower(args, device):
             "data": "synthetic std/RE/text ids (SURVEY.md 8d config 1), random BERT weights"}
 
 
+def train_bench(args, global_batch, steps, warmup, items, cfg, model, item_tower, opt, bucket, rank, world,
+                device):
+    """Times `steps` full train steps (after `warmup`) on this rank's slice of two seeded global
+    batches of `global_batch` users. -> (max-over-ranks seconds, per-op HIP-event times,
+    last losses, per-batch valid counts per rank, per-batch distinct targets)."""
+    from recsys_amd import dist as D
+    from recsys_amd import ops, synth
+    b_loc = global_batch // world
+    lookup = items.pretrained.to(device)
+    log_q = item_tower.log_q
+    batches = []
+    n_dist = []
+    for s in range(2):
+        g = synth.make_batch(items, global_batch, seed=args.seed + 100 + s)
+        # distinct targets of each global batch = the grouped loss's column count
+        n_dist.append(int(torch.unique(g["target_ids"][~g["padding_mask"]]).numel()))
+        sl = {k: (v[rank * b_loc:(rank + 1) * b_loc] if torch.is_tensor(v) else v) for k, v in g.items()}
+        batches.append({k: (v.to(device) if torch.is_tensor(v) else v) for k, v in sl.items()})
+    n_valid = [int((~b["padding_mask"]).sum()) for b in batches]
+    n_glob = [D.all_gather_counts(n, device) for n in n_valid]
+    # packed tokens per view (valid steps + the DuoRec slot of users whose count-1 is a pad)
+    n_tok = [int(D.prepare_step_index(b, pretrained_lookup=lookup).packed[0].flat.numel()) for b in batches]
+    torch.cuda.synchronize()
+
+    # Each step enqueues its work, then builds the NEXT batch's data-dependent index (packed
+    # tokens, grouped targets: the host-synchronising size queries) on a side stream while the
+    # GPU runs the step (dist.prepare_step_index_async). Every timed step still builds one index.
+    pending = {}
+
+    def step(i):
+        ix = pending.pop(i, None)
+        if ix is None:
+            ix = D.prepare_step_index(batches[i % 2], pretrained_lookup=lookup)
+        out = D.contrastive_step_dp(model, item_tower, log_q, batches[i % 2], opt, cfg, lookup, bucket, index=ix)
+        if not args.no_prefetch_index:
+            pending[i + 1] = D.prepare_step_index_async(batches[(i + 1) % 2], pretrained_lookup=lookup)
+        return out
+
+    for i in range(warmup):
+        step(i)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    ops.timing_start()
+    t0 = time.perf_counter()
+    losses = None
+    for i in range(steps):
+        losses = step(warmup + i)  # continues the warm-up's step numbering (pending index)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    kernel_times = ops.timing_stop()
+    # drain the prefetched index of the step that never ran
+    pending.clear()
+    torch.cuda.synchronize()
+    elapsed = torch.tensor([t1 - t0], device=device, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    return float(elapsed.item()), kernel_times, losses, n_glob, n_dist, n_tok
+
+
 def main():
     args = parse()
     rank, world, device = setup_dist(args)
@@ -243,7 +309,6 @@ def main():
     ops.set_nce_precision(args.nce_precision)
 
     assert args.batch % world == 0, "global batch must divide by the number of GPUs"
-    b_loc = args.batch // world
     hs = synth.HASH_SIZE
     cfg = TT.PipelineConfig(num_items=args.items, num_prod_types=hs, num_colors=hs, num_graphics=hs,
                             num_sections=hs, dropout=args.dropout)
@@ -260,58 +325,10 @@ def main():
     if not args.freeze_items:
         opt.add_param_group({"params": list(item_tower.parameters()), "lr": cfg.lr * 0.05})
     bucket = D.GradBucket(list(model.parameters()) + list(item_tower.parameters()))
-    lookup = items.pretrained.to(device)
-    log_q = item_tower.log_q
 
     # two distinct global batches, this rank's user slice of each, resident in HBM
-    batches = []
-    for s in range(2):
-        g = synth.make_batch(items, args.batch, seed=args.seed + 100 + s)
-        sl = {k: (v[rank * b_loc:(rank + 1) * b_loc] if torch.is_tensor(v) else v) for k, v in g.items()}
-        batches.append({k: (v.to(device) if torch.is_tensor(v) else v) for k, v in sl.items()})
-    n_valid = [int((~b["padding_mask"]).sum()) for b in batches]
-    n_glob = [D.all_gather_counts(n, device) for n in n_valid]
-    # distinct targets of each global batch = the grouped loss's column count
-    n_dist = []
-    for s in range(2):
-        g = synth.make_batch(items, args.batch, seed=args.seed + 100 + s)
-        n_dist.append(int(torch.unique(g["target_ids"][~g["padding_mask"]]).numel()))
-    torch.cuda.synchronize()
-
-    # Each step enqueues its work, then builds the NEXT batch's data-dependent index (packed
-    # tokens, grouped targets: the host-synchronising size queries) on a side stream while the
-    # GPU runs the step (dist.prepare_step_index_async). Every timed step still builds one index.
-    pending = {}
-
-    def step(i):
-        ix = pending.pop(i, None)
-        if ix is None:
-            ix = D.prepare_step_index(batches[i % 2], pretrained_lookup=lookup)
-        out = D.contrastive_step_dp(model, item_tower, log_q, batches[i % 2], opt, cfg, lookup, bucket, index=ix)
-        if not args.no_prefetch_index:
-            pending[i + 1] = D.prepare_step_index_async(batches[(i + 1) % 2], pretrained_lookup=lookup)
-        return out
-
-    for i in range(args.warmup):
-        step(i)
-    if world > 1:
-        import torch.distributed as dist
-        dist.barrier()
-    torch.cuda.synchronize()
-    ops.timing_start()
-    t0 = time.perf_counter()
-    losses = None
-    for i in range(args.steps):
-        losses = step(args.warmup + i)  # continues the warm-up's step numbering (pending index)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    kernel_times = ops.timing_stop()
-    elapsed = torch.tensor([t1 - t0], device=device, dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    elapsed = float(elapsed.item())
+    (elapsed, kernel_times, losses, n_glob, n_dist, n_tok) = train_bench(
+        args, args.batch, args.steps, args.warmup, items, cfg, model, item_tower, opt, bucket, rank, world, device)
     total_loss = float(losses[0].item())
 
     # roofline of the dominant kernel. bf16x3 (default): the main loss's forward fused with the
@@ -341,6 +358,20 @@ def main():
             traffic = tr.get("hbm_bytes_per_launch")
 
     kt = {k: {"launches": n, "avg_ms": round(t / max(n, 1), 4)} for k, (n, t) in sorted(kernel_times.items())}
+    # embedding gather (north_star: >= 40 % of HBM): the fused seq-embed forward
+    # (seq_embed_fwd_k, both dropout views in one packed launch). Algorithmic bytes per token
+    # (SURVEY.md 8d): 3 live 512-B rows read (projected pretrained row, item-id row, time row;
+    # the gate-0 tables are skipped), the 512-B output row written, 16 B of ids.
+    g_n, g_ms = kernel_times.get("seq_embed_fwd", (0, 0.0))
+    gather = None
+    if g_n:
+        tok = sum(2 * n_tok[i % 2] for i in range(args.warmup, args.warmup + args.steps))  # two views
+        bpl = 2064.0 * tok / g_n
+        gs = g_ms / 1e3 / g_n
+        gather = {"kernel": "seq_embed_fwd_k", "bound": "hbm", "bytes_per_token": 2064,
+                  "tokens_per_launch": int(tok / g_n), "avg_launch_ms": round(gs * 1e3, 4),
+                  "achieved": round(bpl / gs / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                  "frac": round(bpl / gs / 1e9 / HBM_PEAK_GBS, 4)}
     result = {
         "metric": "SimCSE train-step pairs/sec at d=128 (global batch %d)" % args.batch,
         "value": round(args.batch * args.steps / elapsed, 2),
@@ -375,11 +406,23 @@ def main():
                      "avg_launch_ms": round(avg_s * 1e3, 4),
                      "peak_note": ("bf16 dense MFMA 2516.8 TF / 3 split products" if x3
                                    else "fp32-input MFMA dense")},
+        "gather_roofline": gather,
         "kernels": kt,
         "final_loss": round(total_loss, 5),
     }
+    if world == 1 and not args.no_batch8192 and args.batch != 8192:
+        # BASELINE.json's metric string names batch 8192 (configs[1] says 4096): same step, same
+        # model and optimiser state, global batch 8192 on this GPU.
+        el8, kt8, _, ng8, nd8, _ = train_bench(args, 8192, args.steps8192, 2, items, cfg, model, item_tower, opt,
+                                            bucket, rank, world, device)
+        result["secondary_batch8192"] = {
+            "metric": "SimCSE train-step pairs/sec at d=128 (global batch 8192)",
+            "value": round(8192 * args.steps8192 / el8, 2), "unit": "pairs/s", "steps": args.steps8192,
+            "warmup": 2, "ms_per_step": round(1e3 * el8 / args.steps8192, 3),
+            "valid_positions_per_batch": [sum(c) for c in ng8], "distinct_targets_per_batch": nd8,
+            "main_loss_fwd_ms": round(kt8.get("main/nce_fwd", (1, 0.0))[1] / max(kt8.get("main/nce_fwd", (1, 0))[0], 1), 4)}
+        torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_deepfm:
-        del batches
         torch.cuda.empty_cache()
         deepfm, result["secondary"] = bench_deepfm(args, device)
         if not args.no_rerank:

@@ -31,22 +31,45 @@ struct EmbedArgs {
   float* lin;                     // [R] bias + first order + FM
 };
 
-// E = 16: a row is owned by 4 lanes (one float4 of every field each).
+// E = 16: a row is owned by 4 lanes (one float4 of every field each). The fields are walked
+// in batches of kFB: all ids of a batch first, then all its embedding rows and first-order
+// weights, then the sums and the DNN-row stores, so every lane keeps kFB independent random
+// row reads in flight instead of one id -> row dependency chain per field.
+constexpr int kFB = 13;  // 39 fields = 3 batches
 __global__ __launch_bounds__(256) void deepfm_embed_k(EmbedArgs a) {
   const int64_t r = (int64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
   const int q = threadIdx.x & 3;
   if (r >= a.R) return;
-  const int64_t* xr = a.x + r * a.F;
+  const int64_t* __restrict__ xr = a.x + r * a.F;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f), ss = make_float4(0.f, 0.f, 0.f, 0.f);
   float first = 0.0f;
-  float* er = a.emb ? a.emb + r * (int64_t)a.F * 16 : nullptr;
-  for (int f = 0; f < a.F; ++f) {
-    const int64_t id = xr[f];
-    const float4 v = reinterpret_cast<const float4*>(a.V[f] + id * 16)[q];
-    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-    ss.x += v.x * v.x; ss.y += v.y * v.y; ss.z += v.z * v.z; ss.w += v.w * v.w;
-    if (er) reinterpret_cast<float4*>(er + f * 16)[q] = v;
-    if (q == (f & 3) && a.W[f]) first += a.W[f][id];
+  float* __restrict__ er = a.emb ? a.emb + r * (int64_t)a.F * 16 : nullptr;
+  for (int f0 = 0; f0 < a.F; f0 += kFB) {
+    int64_t id[kFB];
+    float4 v[kFB];
+    float w[kFB];
+#pragma unroll
+    for (int j = 0; j < kFB; ++j) id[j] = (f0 + j < a.F) ? __builtin_nontemporal_load(xr + f0 + j) : 0;
+#pragma unroll
+    for (int j = 0; j < kFB; ++j) {
+      const int f = f0 + j;
+      v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      w[j] = 0.0f;
+      if (f < a.F) {
+        v[j] = reinterpret_cast<const float4*>(a.V[f] + id[j] * 16)[q];
+        if (q == (f & 3) && a.W[f]) w[j] = a.W[f][id[j]];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kFB; ++j) {
+      const int f = f0 + j;
+      if (f < a.F) {
+        s.x += v[j].x; s.y += v[j].y; s.z += v[j].z; s.w += v[j].w;
+        ss.x += v[j].x * v[j].x; ss.y += v[j].y * v[j].y; ss.z += v[j].z * v[j].z; ss.w += v[j].w * v[j].w;
+        if (er) reinterpret_cast<float4*>(er + f * 16)[q] = v[j];
+        first += w[j];
+      }
+    }
   }
   float fm = (s.x * s.x - ss.x) + (s.y * s.y - ss.y) + (s.z * s.z - ss.z) + (s.w * s.w - ss.w);
   fm += __shfl_xor(fm, 1, 64);

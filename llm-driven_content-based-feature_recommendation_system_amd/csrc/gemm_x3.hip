@@ -26,6 +26,7 @@
 // for three workgroups per CU (the GEMMs are latency-bound at two). XCD-aware order: the N tiles of one
 // M block run back to back on one XCD, so A's rows are re-read from that XCD's L2.
 #include "rsx_common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -237,6 +238,222 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_k(GArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Weight-stationary form (used whenever K is 128, 256 or 384 and N a multiple of the column
+// block): the GEMMs here have M ~ 160k and tiny N, K, so the whole column block of B (N_blk x
+// K, hi and lo) is split ONCE per workgroup into LDS in MFMA-fragment order, and the
+// activations never touch LDS: each wave streams 32-row strips of A straight from HBM into
+// registers (a 128-k chunk per strip = 64 fp32 per lane: lane (c, h) reads row c, 16 B at a
+// time at k = 8i + 4h), double-buffered across strips so one chunk is always in flight per
+// wave (~128 KB per CU with eight waves; the two-stage LDS pipeline above kept ~24 KB of A in
+// flight per CU and was latency-bound at 2-3.4 TB/s).
+// The summation order over k is a fixed permutation (k-step s of a chunk takes k = 16s + 4h
+// + {0..3} and 16s + 8 + 4h + {0..3}); B's fragments use the same permutation, so each
+// product is the plain sum over k. Same epilogues and dropout hash as gemm_x3_nt_k.
+constexpr int kWsThreads = 256;  // 4 waves: one per SIMD with the whole 512-register file
+constexpr int kWsWaves = kWsThreads / 64;
+constexpr int kWsBufs = 3;       // A chunks per wave: one being computed, two in flight
+
+struct WsArgs {
+  GArgs g;
+  int nblk;     // column blocks
+  int groups;   // workgroups per column block
+};
+
+template <int KC, int NBW, int EPI>
+__global__ __launch_bounds__(kWsThreads, 1) void gemm_ws_k(WsArgs w) {
+  static_assert(kWsBufs == 3, "the main loop below is written for three buffers");
+  constexpr int NT = NBW / 32;
+  __shared__ __attribute__((aligned(16))) u32x4 sW[KC * 8 * NT * 2 * 64];
+  const GArgs& a = w.g;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, c = lane & 31;
+  const int bflat = (blockIdx.x & 7) * ((int)gridDim.x >> 3) + (blockIdx.x >> 3);
+  const int nb = bflat % w.nblk, grp = bflat / w.nblk;
+  if (grp >= w.groups) return;  // whole workgroup: no barrier is skipped by part of it
+  const int n0 = nb * NBW;
+
+  // B column block -> LDS fragments: slot (step st = 16-k step over all chunks, tile j, lane l)
+  // holds B[n0 + 32j + (l & 31)][k-set(st, l >> 5)] as 8 hi and 8 lo bf16.
+  for (int slot = tid; slot < KC * 8 * NT * 64; slot += kWsThreads) {
+    const int l = slot & 63, rest = slot >> 6;
+    const int j = rest % NT, st = rest / NT;
+    const float* src = a.B + (int64_t)(n0 + 32 * j + (l & 31)) * a.ldb + (st >> 3) * 128 + 16 * (st & 7) +
+                       4 * (l >> 5);
+    u32x4 hi, lo;
+    split8(*reinterpret_cast<const float4*>(src), *reinterpret_cast<const float4*>(src + 8), hi, lo);
+    sW[(rest * 2 + 0) * 64 + l] = hi;
+    sW[(rest * 2 + 1) * 64 + l] = lo;
+  }
+  __shared__ __attribute__((aligned(16))) float sBias[NBW];
+  for (int n = tid; n < NBW; n += kWsThreads) sBias[n] = (EPI != EPI_DGELU_DROP && a.bias) ? a.bias[n0 + n] : 0.0f;
+  __syncthreads();
+
+  // this wave's strips: (grp + groups * it) * kWsWaves + wave, it = 0, 1, ...
+  const int64_t nstrips = (a.M + 31) >> 5;
+  const int64_t s_first = (int64_t)grp * kWsWaves + wave, s_step = (int64_t)w.groups * kWsWaves;
+  const int nmine = s_first < nstrips ? (int)((nstrips - 1 - s_first) / s_step + 1) : 0;
+  const int nitems = nmine * KC;
+
+  f32x16 acc[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
+
+  auto load = [&](int t, float4 (&buf)[16]) {
+    const int64_t strip = s_first + (int64_t)(t / KC) * s_step;
+    int64_t row = strip * 32 + c;
+    if (row >= a.M) row = a.M - 1;  // tail rows re-read the last row; never stored
+    const float* src = a.A + row * a.lda + (t % KC) * 128 + 4 * h;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) buf[i] = *reinterpret_cast<const float4*>(src + 8 * i);
+  };
+
+  // acc[j] = B_j . A^T (the B fragment is the MFMA's A operand): lane (c, h), register
+  // 4g + e holds C[strip*32 + c][n0 + 32j + 8g + 4h + e], so the epilogue moves float4s.
+  auto compute = [&](int t, const float4 (&buf)[16]) {
+    const int q = t % KC;
+    int64_t m = (s_first + (int64_t)(t / KC) * s_step) * 32 + c;
+    if (m >= a.M) m = a.M - 1;
+    float* crow = a.C + m * a.ldc + n0 + 4 * h;
+    float* xrow = (EPI != EPI_BIAS) ? a.aux + m * a.ldaux + n0 + 4 * h : nullptr;
+    // EPI_DGELU_DROP: the strip's saved GELU derivatives are loaded before its MFMAs (vmcnt
+    // retires in order, so a load issued at the epilogue would drain the prefetched strips)
+    float4 z[NT][4];
+    if (EPI == EPI_DGELU_DROP && q == KC - 1) {
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) z[j][g] = *reinterpret_cast<const float4*>(xrow + 32 * j + 8 * g);
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      u32x4 hi, lo;
+      split8(buf[2 * s], buf[2 * s + 1], hi, lo);
+      const bf16x8 xh = __builtin_bit_cast(bf16x8, hi), xl = __builtin_bit_cast(bf16x8, lo);
+      const u32x4* wp = sW + ((q * 8 + s) * NT) * 128 + lane;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const bf16x8 wh = __builtin_bit_cast(bf16x8, wp[j * 128]);
+        const bf16x8 wl = __builtin_bit_cast(bf16x8, wp[j * 128 + 64]);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, xh, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xl, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xh, acc[j], 0, 0, 0);
+      }
+    }
+    if (q != KC - 1) return;
+    // epilogue. Rows past M loaded A row M-1 and computed exactly row M-1's values; they are
+    // written to row M-1 again (same values, dropout hashed on the clamped row), so the stores
+    // need no branch.
+    const uint32_t e0 = (uint32_t)m * (uint32_t)a.N + (uint32_t)(n0 + 4 * h);
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int o = 32 * j + 8 * g;
+        float v[4] = {acc[j][4 * g], acc[j][4 * g + 1], acc[j][4 * g + 2], acc[j][4 * g + 3]};
+        if (EPI == EPI_DGELU_DROP) {
+          v[0] *= z[j][g].x; v[1] *= z[j][g].y; v[2] *= z[j][g].z; v[3] *= z[j][g].w;
+        } else {
+          const float4 bb = *reinterpret_cast<const float4*>(&sBias[o + 4 * h]);
+          v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+        }
+        if (EPI == EPI_GELU_DROP) {
+          float d[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float x = v[e];
+            const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+            d[e] = cdf + x * 0.3989422804014327f * __expf(-0.5f * x * x);  // gelu'(x)
+            v[e] = x * cdf;
+          }
+          *reinterpret_cast<float4*>(xrow + o) = make_float4(d[0], d[1], d[2], d[3]);
+        }
+        if (EPI != EPI_BIAS && a.drop.active()) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = keep(a.drop, e0 + o + e) ? v[e] * a.drop.scale : 0.0f;
+        }
+        *reinterpret_cast<float4*>(crow + o) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
+  };
+
+  // sched_barrier fences keep the compiler from hoisting one buffer's conversions into another
+  // phase (which raised the register demand past the file and forced early vmcnt waits).
+#define WS_FENCE __builtin_amdgcn_sched_barrier(0)
+  float4 b0[16], b1[16], b2[16];
+  if (nitems == 0) return;  // wave-uniform; no barrier follows
+  // every load is unconditional (item index clamped to the last item): all paths into the
+  // loop then carry the same outstanding-load pattern, so the compiler's vmcnt waits stay
+  // per buffer instead of draining the prefetches. The trailing re-loads are never used.
+  const int last = nitems - 1;
+  load(0, b0);
+  load(last < 1 ? last : 1, b1);
+  load(last < 2 ? last : 2, b2);
+  for (int t = 0;; t += 3) {
+    WS_FENCE;
+    compute(t, b0);
+    WS_FENCE;
+    load(t + 3 < last ? t + 3 : last, b0);
+    if (t + 1 > last) break;
+    WS_FENCE;
+    compute(t + 1, b1);
+    WS_FENCE;
+    load(t + 4 < last ? t + 4 : last, b1);
+    if (t + 2 > last) break;
+    WS_FENCE;
+    compute(t + 2, b2);
+    WS_FENCE;
+    load(t + 5 < last ? t + 5 : last, b2);
+    if (t + 3 > last) break;
+  }
+#undef WS_FENCE
+}
+
+int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) ==
+                                                 hipSuccess && v > 0)
+      n = v;
+    else
+      n = 256;
+  }
+  return n;
+}
+
+bool ws_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("RSX_GEMM_WS");
+    on = (e && e[0] == '0') ? 0 : 1;
+  }
+  return on == 1;
+}
+
+template <int KC, int NBW>
+void launch_ws(const GArgs& g, hipStream_t st) {
+  WsArgs w;
+  w.g = g;
+  w.nblk = g.N / NBW;
+  const int64_t strips = (g.M + 31) / 32;
+  const int64_t blocks_rows = (strips + kWsWaves - 1) / kWsWaves;  // strips per workgroup round
+  int groups = num_cus() / w.nblk;
+  if (groups < 1) groups = 1;
+  if (groups > blocks_rows) groups = (int)blocks_rows;
+  w.groups = groups;
+  const int grid = (w.nblk * groups + 7) / 8 * 8;
+  if (g.epi == EPI_BIAS) hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_BIAS>), dim3(grid), dim3(kWsThreads), 0, st, w);
+  else if (g.epi == EPI_GELU_DROP)
+    hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_GELU_DROP>), dim3(grid), dim3(kWsThreads), 0, st, w);
+  else hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_DGELU_DROP>), dim3(grid), dim3(kWsThreads), 0, st, w);
+}
+
 }  // namespace
 
 RSX_API int rsx_gemm_x3(const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias, int64_t M,
@@ -261,11 +478,16 @@ RSX_API int rsx_gemm_x3(const float* A, int64_t lda, const float* B, int64_t ldb
   RSX_ARG(tiles < (1LL << 30), "too many tiles");
   g.tiles = (int)tiles;
   g.drop = rsx::make_dropout(epi == EPI_BIAS ? 0.0f : p_drop, seed);
+  hipStream_t st = (hipStream_t)stream;
+  if (ws_enabled() && ldb % 4 == 0) {
+    if (K == 128) { launch_ws<1, 128>(g, st); RSX_LAUNCHED(); return 0; }
+    if (K == 256) { launch_ws<2, 128>(g, st); RSX_LAUNCHED(); return 0; }
+    if (K == 384) { launch_ws<3, 64>(g, st); RSX_LAUNCHED(); return 0; }
+  }
   // tiles per workgroup: enough workgroups for two per CU, each a continuous stage stream
   g.per = (int)((tiles + RSX_GEMM_BLOCKS - 1) / RSX_GEMM_BLOCKS);
   const int64_t blocks = (tiles + g.per - 1) / g.per;
   const int grid = (int)((blocks + 7) / 8 * 8);
-  hipStream_t st = (hipStream_t)stream;
   if (epi == EPI_BIAS) hipLaunchKernelGGL(gemm_x3_nt_k<EPI_BIAS>, dim3(grid), dim3(256), 0, st, g);
   else if (epi == EPI_GELU_DROP) hipLaunchKernelGGL(gemm_x3_nt_k<EPI_GELU_DROP>, dim3(grid), dim3(256), 0, st, g);
   else hipLaunchKernelGGL(gemm_x3_nt_k<EPI_DGELU_DROP>, dim3(grid), dim3(256), 0, st, g);

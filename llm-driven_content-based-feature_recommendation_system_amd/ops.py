@@ -67,10 +67,11 @@ class _SeqEmbed(torch.autograd.Function):
         mean = torch.empty(T, device=base.device, dtype=torch.float32)
         rstd = torch.empty_like(mean)
         gate = _c(gate)
-        rc = N.lib().rsx_seq_embed_fwd(
-            N.ptr(base), N.ptr_array(ids), N.ptr_array(tables), len(tables), N.ptr(gate), N.ptr(pos),
-            N.ptr(tok_pos), N.ptr(ln_w), N.ptr(ln_b), eps, T, L, D, p_drop, seed, N.ptr(out), N.ptr(mean),
-            N.ptr(rstd), N.stream())
+        with timed("seq_embed_fwd"):
+            rc = N.lib().rsx_seq_embed_fwd(
+                N.ptr(base), N.ptr_array(ids), N.ptr_array(tables), len(tables), N.ptr(gate), N.ptr(pos),
+                N.ptr(tok_pos), N.ptr(ln_w), N.ptr(ln_b), eps, T, L, D, p_drop, seed, N.ptr(out), N.ptr(mean),
+                N.ptr(rstd), N.stream())
         N.check(rc, "seq_embed_fwd")
         ctx.save_for_backward(base, gate, pos, ln_w, mean, rstd, tok_pos, *ids, *tables)
         ctx.cfg = (eps, p_drop, seed, padding_idx, len(tables), T, L, D)
@@ -650,10 +651,13 @@ _gemm_precision = os.environ.get("RSX_GEMM_PRECISION", "bf16x3")
 EPI_BIAS, EPI_GELU_DROP, EPI_DGELU_DROP = 0, 1, 2
 
 
-def set_gemm_precision(p: str) -> None:
+def set_gemm_precision(p: str) -> str:
+    """Set the token-linear GEMM precision ("fp32" | "bf16x3"); returns the previous mode."""
     global _gemm_precision
-    assert p in GEMM_PRECISIONS, p
-    _gemm_precision = p
+    if p not in GEMM_PRECISIONS:
+        raise ValueError(f"precision must be one of {sorted(GEMM_PRECISIONS)}")
+    prev, _gemm_precision = _gemm_precision, p
+    return prev
 
 
 def _x3_ok(m_out: int, k_in: int) -> bool:
