@@ -14,17 +14,20 @@ Differences by design:
   * forward runs the token work on this package's kernels: fused LayerNorm(+GELU), the
     token linears with split-K weight gradients, the MHA kernel (no mask, 16 field tokens)
     and the InfoNCE kernel for the loss. BERT itself stays on PyTorch (hipBLASLt GEMMs).
-The DB-backed training driver (train_simcse_from_db :887+) needs PostgreSQL/pgvector and is
-out of scope; ``simcse_train_step`` is its per-batch GPU step.
+``train_simcse_from_db`` keeps the reference driver's signature and loop; its ``db_session`` is
+any product source with ``fetch_products()`` (item_data.py; PostgreSQL itself is out of scope)
+and ``simcse_train_step`` is its per-batch GPU step.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import _native as N
 from . import ops
 from .tower_code.v1_refine_usertower import encoder_stack
 
@@ -36,15 +39,17 @@ OUTPUT_DIM_PROJECTOR = 128
 
 
 def _ln(x, ln: nn.LayerNorm, gelu: bool = False):
-    """LayerNorm (+ exact GELU) on the fused kernel where the width fits it, else PyTorch."""
-    if x.is_cuda and x.shape[-1] in (64, 128, 256):
+    """LayerNorm (+ exact GELU) on the fused kernel where the width fits it; wider rows (the
+    SE blocks' 16d LayerNorm) use torch's ROCm LayerNorm kernel. GPU only: no CPU path."""
+    N.ensure_device(x)
+    if x.shape[-1] in (64, 128, 256):
         return ops.layer_norm(x, ln.weight, ln.bias, ln.eps, act=ops.ACT_GELU_ERF if gelu else 0)
     y = F.layer_norm(x, (x.shape[-1],), ln.weight, ln.bias, ln.eps)
     return F.gelu(y) if gelu else y
 
 
 def _lin(x, layer: nn.Linear):
-    return ops.linear_tok(x, layer.weight, layer.bias) if x.is_cuda else layer(x)
+    return ops.linear_tok(x, layer.weight, layer.bias)
 
 
 class SEResidualBlock(nn.Module):
@@ -149,12 +154,9 @@ class HybridItemTower(nn.Module):
         text_vec = _ln(_lin(cls, t[0]), t[1], gelu=True).unsqueeze(1)                         # :269-271
         seq = torch.cat([std_emb, re_vec, text_vec], dim=1)                                   # [B, 16, d]
         p = self.transformer.layers[0].dropout.p if self.training else 0.0
-        if seq.is_cuda:
-            ctx = encoder_stack(self.transformer.layers, seq.contiguous(), None, p, self.training, causal=False)
-        else:
-            ctx = self.transformer(seq)
+        ctx = encoder_stack(self.transformer.layers, seq.contiguous(), None, p, self.training, causal=False)
         out = self.head(ctx.mean(dim=1))
-        return ops.l2_normalize(out) if out.is_cuda else F.normalize(out, p=2, dim=1)
+        return ops.l2_normalize(out)
 
 
 class OptimizedItemTower(nn.Module):
@@ -168,7 +170,7 @@ class OptimizedItemTower(nn.Module):
     def forward(self, x):
         L = self.layer
         y = _lin(_ln(_lin(x, L[0]), L[1], gelu=True), L[3])
-        return ops.l2_normalize(y) if y.is_cuda else F.normalize(y, p=2, dim=1)
+        return ops.l2_normalize(y)
 
 
 class SimCSEModelWrapper(nn.Module):
@@ -214,3 +216,74 @@ def simcse_train_step(model, inputs_v1, inputs_v2, optimizer, temperature: float
     if scheduler is not None:
         scheduler.step()
     return loss.detach(), emb1.detach(), emb2.detach()
+
+
+def train_simcse_from_db(encoder: nn.Module, projector: nn.Module, db_session, batch_size: int, epochs: int,
+                         lr: float, checkpoint_path: Optional[str] = None, collator=None, model_dir: str = "models",
+                         dropout_prob: float = 0.2, temperature: float = 0.08, seed: Optional[int] = None,
+                         check_interval: int = 50):
+    """item_tower.py:887-1126: SimCSE training of encoder + projector over every product of the
+    source. Products -> TrainingItems with the RAW name (:898-950); the encoder optionally
+    resumes from an encoder-only checkpoint (strict, then non-strict, :966-983); AdamW with the
+    BERT parameters at lr 1e-5 and the rest at ``lr`` (:995-1018); two corrupted views per
+    product (SimCSERecSysDataset, p = 0.2), shuffled, drop_last; linear warm-up schedule over
+    10 % of the steps (:1033-1038); per batch ``simcse_train_step`` (both views, symmetric
+    loss at tau 0.08 on the fused InfoNCE kernel); alignment / uniformity every
+    ``check_interval`` steps; the encoder's state_dict saved per epoch as
+    ``encoder_ep{NN}_loss{L:.4f}.pth`` (:1113-1118). fp32 throughout (the reference's CUDA
+    path runs fp16 AMP with a GradScaler). Returns the per-epoch average losses."""
+    import random
+
+    from transformers import get_linear_schedule_with_warmup
+
+    from .item_data import SimCSECollator, SimCSERecSysDataset, build_std_vocab, rows_to_items
+
+    rows = db_session.fetch_products()
+    if not rows:
+        print("[Error] No data found.")
+        return []
+    products = rows_to_items(rows)
+    model = SimCSEModelWrapper(encoder, projector)
+    device = next(encoder.parameters()).device
+    N.ensure_device(next(encoder.parameters()))
+    if checkpoint_path:
+        if not os.path.exists(checkpoint_path):
+            print(f"Checkpoint file not found: {checkpoint_path}")
+            return []
+        state = torch.load(checkpoint_path, map_location="cpu", weights_only=True)
+        try:
+            model.encoder.load_state_dict(state)
+        except RuntimeError:
+            model.encoder.load_state_dict(state, strict=False)
+    model = model.to(device)
+    model.train()
+    bert_params = [p for n, p in model.named_parameters() if p.requires_grad and "bert_model" in n]
+    other_params = [p for n, p in model.named_parameters() if p.requires_grad and "bert_model" not in n]
+    optimizer = torch.optim.AdamW([{"params": bert_params, "lr": 1e-5}, {"params": other_params, "lr": lr}])
+    rng = random.Random(seed)
+    dataset = SimCSERecSysDataset(products, dropout_prob=dropout_prob, rng=rng)
+    if collator is None:
+        collator = SimCSECollator(std_vocab=build_std_vocab(products))
+    gen = torch.Generator().manual_seed(seed) if seed is not None else None
+    loader = torch.utils.data.DataLoader(dataset, batch_size=batch_size, shuffle=True, collate_fn=collator,
+                                         drop_last=True, num_workers=0, generator=gen)
+    total_steps = len(loader) * epochs
+    scheduler = get_linear_schedule_with_warmup(optimizer, num_warmup_steps=int(total_steps * 0.1),
+                                                num_training_steps=total_steps)
+    os.makedirs(model_dir, exist_ok=True)
+    history = []
+    for epoch in range(epochs):
+        total, step = 0.0, 0
+        for v1, v2 in loader:
+            v1 = [t.to(device, non_blocking=True) for t in v1]
+            v2 = [t.to(device, non_blocking=True) for t in v2]
+            loss, e1, e2 = simcse_train_step(model, v1, v2, optimizer, temperature, scheduler)
+            if step % check_interval == 0:
+                align, uni = calculate_metrics(e1, e2)
+                print(f"epoch {epoch + 1} step {step} loss {loss.item():.4f} align {align:.4f} uni {uni:.4f}")
+            total += float(loss.item())
+            step += 1
+        avg = total / step if step else float("nan")
+        history.append(avg)
+        torch.save(encoder.state_dict(), os.path.join(model_dir, f"encoder_ep{epoch + 1:02d}_loss{avg:.4f}.pth"))
+    return history

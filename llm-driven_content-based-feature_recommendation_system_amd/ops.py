@@ -731,7 +731,8 @@ class _TokLinear(torch.autograd.Function):
 def linear_tok(x, weight, bias=None):
     """F.linear over a token axis (x [..., K]) whose weight/bias gradients come from the
     split-K rsx_linear_wgrad kernel instead of the library GEMM (T >> N, K); forward and
-    input gradient on rsx_gemm_x3 when the shapes allow (bf16x3 mode)."""
+    input gradient on rsx_gemm_x3 when the shapes allow (bf16x3 mode). GPU tensors only."""
+    N.ensure_device(x)
     shp = x.shape
     x2 = _c(x.reshape(-1, shp[-1]))
     if x2.shape[0] == 0 or shp[-1] % 16 or weight.shape[0] % 16:
