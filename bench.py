@@ -130,24 +130,48 @@ def bench_deepfm(args, device):
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / iters
     kt = ops.timing_stop()
-    emb_n, emb_ms = kt.get("deepfm/embed", (1, 0.0))
-    lin_n, lin_ms = kt.get("deepfm/linear", (1, 0.0))
-    dot_n, dot_ms = kt.get("deepfm/linear_dot", (1, 0.0))
-    # algorithmic bytes per row of the gather kernel: 39 ids (8 B) + 39 x (16 + 1) fp32 reads +
-    # the 624-float DNN input row written + 4 B linear/FM term
-    bytes_row = F * 8 + F * 17 * 4 + F * 16 * 4 + 4
-    emb_s = emb_ms / 1e3 / emb_n
+    # the fused kernel (gather + FM + DNN in one launch): algorithmic HBM bytes per row =
+    # SURVEY.md 8d's 39 x (64 B embedding row + 4 B first-order weight + 8 B id) + 4 B output =
+    # 2,968 B; DNN FLOPs per row 2 (624*256 + 256*128 + 128), priced at the bf16x3 MFMA peak
+    f_n, f_ms = kt.get("deepfm/fused", (0, 0.0))
+    bytes_row = F * (64 + 4 + 8) + 4
     dnn_flops = 2.0 * R * (F * 16 * 256 + 256 * 128 + 128)
-    dnn_s = (lin_ms / lin_n + dot_ms / dot_n) / 1e3
-    return model, {"metric": "DeepFM rerank rows/sec (forward, 39 fields, d=16, vocab 1e6/field)",
-            "value": round(R / dt, 1), "unit": "rows/s", "rows": R, "ms_per_batch": round(dt * 1e3, 4),
-            "data": "synthetic Zipf(1.1) ids, deepctr-style N(0,1e-4) init",
-            "gather_fm": {"avg_ms": round(emb_s * 1e3, 4), "bytes_per_row": bytes_row,
-                          "achieved_GBs": round(bytes_row * R / emb_s / 1e9, 1), "peak_GBs": HBM_PEAK_GBS,
-                          "frac": round(bytes_row * R / emb_s / 1e9 / HBM_PEAK_GBS, 4)},
-            "dnn": {"avg_ms": round(dnn_s * 1e3, 4), "achieved_TFLOPs": round(dnn_flops / dnn_s / 1e12, 2),
-                    "peak_TFLOPs": FP32_MFMA_PEAK_TFLOPS,
-                    "frac": round(dnn_flops / dnn_s / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)}}
+    out = {"metric": "DeepFM rerank rows/sec (forward, 39 fields, d=16, vocab 1e6/field)",
+           "value": round(R / dt, 1), "unit": "rows/s", "rows": R, "ms_per_batch": round(dt * 1e3, 4),
+           "data": "synthetic Zipf(1.1) ids, deepctr-style N(0,1e-4) init"}
+    if f_n:
+        fs = f_ms / 1e3 / f_n
+        out["fused"] = {"kernel": "deepfm_fused_k (+ deepfm_prep_k weight images)", "avg_ms": round(fs * 1e3, 4),
+                        "bytes_per_row": bytes_row,
+                        "gather_achieved_GBs": round(bytes_row * R / fs / 1e9, 1), "hbm_peak_GBs": HBM_PEAK_GBS,
+                        "gather_frac": round(bytes_row * R / fs / 1e9 / HBM_PEAK_GBS, 4),
+                        "dnn_achieved_TFLOPs": round(dnn_flops / fs / 1e12, 2),
+                        "dnn_peak_TFLOPs": round(BF16X3_PEAK_TFLOPS, 1),
+                        "dnn_frac": round(dnn_flops / fs / 1e12 / BF16X3_PEAK_TFLOPS, 4)}
+    else:
+        emb_n, emb_ms = kt.get("deepfm/embed", (1, 0.0))
+        lin_n, lin_ms = kt.get("deepfm/linear", (1, 0.0))
+        dot_n, dot_ms = kt.get("deepfm/linear_dot", (1, 0.0))
+        eb = F * 8 + F * 17 * 4 + F * 16 * 4 + 4   # + the 624-float DNN input row written
+        emb_s = emb_ms / 1e3 / emb_n
+        dnn_s = (lin_ms / lin_n + dot_ms / dot_n) / 1e3
+        out["gather_fm"] = {"avg_ms": round(emb_s * 1e3, 4), "bytes_per_row": eb,
+                            "achieved_GBs": round(eb * R / emb_s / 1e9, 1), "peak_GBs": HBM_PEAK_GBS,
+                            "frac": round(eb * R / emb_s / 1e9 / HBM_PEAK_GBS, 4)}
+        out["dnn"] = {"avg_ms": round(dnn_s * 1e3, 4), "achieved_TFLOPs": round(dnn_flops / dnn_s / 1e12, 2),
+                      "peak_TFLOPs": FP32_MFMA_PEAK_TFLOPS,
+                      "frac": round(dnn_flops / dnn_s / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)}
+    # uniform-id stress variant: every row gathers cold table lines
+    xu = torch.randint(0, V, (R, F), device=device, generator=torch.Generator(device=device).manual_seed(9))
+    for _ in range(3):
+        model.forward_logits(xu)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        model.forward_logits(xu)
+    torch.cuda.synchronize()
+    out["uniform_ids_rows_per_s"] = round(R / ((time.perf_counter() - t0) / iters), 1)
+    return model, out
 
 
 def bench_retrieve_rerank(args, device, deepfm):

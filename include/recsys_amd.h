@@ -248,6 +248,17 @@ int rsx_linear_fwd(const float* X, int64_t ldx, const float* W, const float* b, 
 int rsx_linear_dot_fwd(const float* X, int64_t ldx, const float* W, const float* b, int64_t M, int64_t N, int64_t K,
                        int act, const float* wo, const float* add, float* logit, float* prob, void* stream);
 
+/* rsx_deepfm_fused: the whole forward in one kernel (gather + first-order + FM + the
+ *   (256, 128) ReLU DNN on bf16x3 MFMA + final dot + sigmoid); the [R, F*16] DNN input never
+ *   reaches HBM. Same arguments as the three calls above with w1 [256, F*16], b1 [256],
+ *   w2 [128, 256], b2 [128], wo [128] (torch Linear layouts; dnn_hidden_units = (256, 128),
+ *   embed_dim 16). ws: rsx_deepfm_fused_workspace_bytes(F) (per-call bf16 weight images).
+ *   Replaces the same deepctr-torch DeepFM forward. */
+int64_t rsx_deepfm_fused_workspace_bytes(int F);
+int rsx_deepfm_fused(const int64_t* x, int64_t R, int F, const float* const* V, const float* const* W, float bias,
+                     const float* w1, const float* b1, const float* w2, const float* b2, const float* wo, void* ws,
+                     float* logit, float* prob, void* stream);
+
 /* ---- row gather / scatter / L2 normalise ---------------------------------------------
  * out[r] = src[idx[r]] (idx NULL => r), optionally F.normalize'd (eps) with norms saved:
  *   pretrained_lookup[item_ids]            tower_code/v1_usertower_train.py:760

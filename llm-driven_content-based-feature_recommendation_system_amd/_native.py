@@ -55,6 +55,8 @@ _SIGS = {
     "rsx_nce_grouped_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64,
                                   c_i64, c_i64, c_f, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_i, c_p]),
     "rsx_deepfm_embed": (c_i, [c_p, c_i64, c_i, c_i, c_p, c_p, c_f, c_p, c_p, c_p]),
+    "rsx_deepfm_fused_workspace_bytes": (c_i64, [c_i]),
+    "rsx_deepfm_fused": (c_i, [c_p, c_i64, c_i, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "rsx_linear_fwd": (c_i, [c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i64, c_i, c_p, c_p]),
     "rsx_linear_dot_fwd": (c_i, [c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i64, c_i, c_p, c_p, c_p, c_p, c_p]),
     "rsx_static_embed_fwd": (c_i, [c_p, c_p, c_p, c_p, c_i, c_p, c_i64, c_p, c_i64, c_p]),

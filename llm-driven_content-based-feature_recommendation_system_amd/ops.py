@@ -806,17 +806,35 @@ def linear(x, weight, bias=None, act=ACT_NONE):
     return y
 
 
+# RSX_DEEPFM_FUSED=0 selects the three-kernel path (gather+FM, fp32-MFMA linears) for A/B runs
+_DEEPFM_FUSED = os.environ.get("RSX_DEEPFM_FUSED", "1") != "0"
+
+
 def deepfm_forward(x, emb_tables, lin_tables, out_bias, dnn_weights, dnn_biases, w_out):
     """DeepFM logits/probabilities for x [R, F] int64 (see csrc/deepfm.hip).
 
     emb_tables: F tensors [vocab_f, 16]; lin_tables: F tensors [vocab_f] (or [vocab_f, 1]);
     dnn_weights/dnn_biases: torch Linear layout, ReLU between layers; w_out [H_last].
-    Returns (logit [R], prob [R])."""
+    Config-3 shapes (E 16, DNN (256, 128)) run the single fused kernel (rsx_deepfm_fused, bf16x3
+    DNN products); other shapes the gather + fp32-MFMA linear kernels. Returns (logit [R], prob [R])."""
     N.ensure_device(x)
     x = _c(x)
     R, F = x.shape
     E = emb_tables[0].shape[1]
     dev = x.device
+    if (_DEEPFM_FUSED and E == 16 and F <= 64 and len(dnn_weights) == 2 and tuple(dnn_weights[0].shape) == (256, F * 16)
+            and tuple(dnn_weights[1].shape) == (128, 256)):
+        logit = torch.empty(R, device=dev, dtype=torch.float32)
+        prob = torch.empty(R, device=dev, dtype=torch.float32)
+        ws = torch.empty(N.lib().rsx_deepfm_fused_workspace_bytes(F), device=dev, dtype=torch.uint8)
+        b1, b2 = dnn_biases
+        with timed("deepfm/fused"):
+            rc = N.lib().rsx_deepfm_fused(
+                N.ptr(x), R, F, N.ptr_array([_c(t) for t in emb_tables]), N.ptr_array([_c(t) for t in lin_tables]),
+                float(out_bias), N.ptr(_c(dnn_weights[0])), N.ptr(_c(b1)), N.ptr(_c(dnn_weights[1])), N.ptr(_c(b2)),
+                N.ptr(_c(w_out.reshape(-1))), N.ptr(ws), N.ptr(logit), N.ptr(prob), N.stream())
+        N.check(rc, "deepfm_fused")
+        return logit, prob
     emb = torch.empty(R, F * E, device=dev, dtype=torch.float32)
     lin = torch.empty(R, device=dev, dtype=torch.float32)
     with timed("deepfm/embed"):

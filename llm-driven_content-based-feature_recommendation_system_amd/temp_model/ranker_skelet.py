@@ -57,11 +57,18 @@ class DeepFM(nn.Module):
         _, prob = self.forward_logits(X)
         return prob.unsqueeze(1)
 
+    def _bias_value(self) -> float:
+        """out.bias as a host float, read once per parameter version (no sync per forward)."""
+        v = self.out.bias._version
+        if getattr(self, "_bias_cache", (None, 0.0))[0] != v:
+            self._bias_cache = (v, float(self.out.bias.item()))
+        return self._bias_cache[1]
+
     @torch.no_grad()
     def forward_logits(self, X):
         return ops.deepfm_forward(
             X, [self.embedding_dict[n].weight for n in self.field_names],
-            [self.linear_model.embedding_dict[n].weight for n in self.field_names], float(self.out.bias.item()),
+            [self.linear_model.embedding_dict[n].weight for n in self.field_names], self._bias_value(),
             [l.weight for l in self.dnn.linears], [l.bias for l in self.dnn.linears], self.dnn_linear.weight)
 
     def predict_proba(self, X) -> np.ndarray:

@@ -33,6 +33,29 @@ def test_deepfm_forward_matches_oracle(gpu, R, F, vocab):
     assert out.shape == (R, 1)
 
 
+@pytest.mark.parametrize("R,F", [(4099, 39), (64, 13), (200, 40)])
+def test_deepfm_fused_matches_unfused(gpu, R, F):
+    """The fused kernel (bf16x3 DNN) against the three-kernel path (fp32-MFMA DNN) on the same
+    model: logits within 1e-4 (north_star's fp32-logit bound), including the F % 13 != 0 tail
+    and rows past the last 64-row block."""
+    model = DeepFM([3000] * F, init_std=0.05, device=gpu)
+    with torch.no_grad():
+        model.out.bias.fill_(-0.3)
+        for l in model.dnn.linears:
+            l.bias.normal_(0, 0.05)
+    g = torch.Generator().manual_seed(R + F)
+    x = torch.randint(0, 3000, (R, F), generator=g).to(gpu)
+    assert ops._DEEPFM_FUSED
+    lf, pf = model.forward_logits(x)
+    ops._DEEPFM_FUSED = False
+    try:
+        lu, pu = model.forward_logits(x)
+    finally:
+        ops._DEEPFM_FUSED = True
+    torch.testing.assert_close(lf, lu, atol=1e-4, rtol=0)
+    torch.testing.assert_close(pf, pu, atol=2.5e-5, rtol=0)
+
+
 def test_linear_act_variants(gpu):
     g = torch.Generator().manual_seed(3)
     x = torch.randn(300, 96, generator=g)
