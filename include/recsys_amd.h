@@ -221,6 +221,13 @@ int rsx_linear_wgrad_x3(const float* dY, int64_t ldy, const float* X, int64_t ld
  * N % 128 == 0, K % 32 == 0, A/B 16-byte aligned, leading dimensions multiples of 4. */
 int rsx_gemm_x3(const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias, int64_t M, int N, int K,
                 int epi, float* aux, int64_t ldaux, float p_drop, uint64_t seed, float* C, int64_t ldc, void* stream);
+/* C[m] = A[m] . B^T + bias + R[ridx[m]]: a per-row table added in the epilogue. Replaces
+ * output_proj[0](cat(enc_out, profile.expand)) of SASRecUserTower.forward
+ * (v1_refine_usertower.py:498-505) over the packed tokens: A = encoder output, B = the token
+ * half of output_proj[0].weight (ldb = 256), R = profile half + bias per user, ridx = user of
+ * each token. K 128 or 256, N % 128 == 0, every pointer 16-byte aligned. */
+int rsx_gemm_x3_rowadd(const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias, int64_t M, int N,
+                       int K, const float* R, int64_t ldr, const int64_t* ridx, float* C, int64_t ldc, void* stream);
 
 /* ---- A14: retrieval top-k ------------------------------------------------------------
  * scores = U I^T (fp32 MFMA, never materialised), per query the k best items sorted by
@@ -274,9 +281,11 @@ int rsx_scatter_rows(const float* dy, const float* y, const float* nrm, const in
                      int normalize, float eps, int mode, int64_t skip_idx, float* dst, int64_t ld_dst, void* stream);
 /* Segmented row sums, the atomic-free scatter-add when the sort by destination is known:
  * dst[rows[u]] (+)= scale[0] * sum_{k in [seg_off[u], seg_off[u+1])} src[perm[k]] (scale
- * nullable = 1; rows[u] == skip_row untouched; rows unique). Used for the user tower's item-id
- * embedding gradient (v1_refine_usertower.py:447-459, nn.Embedding backward) with the sort
- * built ahead of the step; deterministic. */
+ * nullable = 1; perm nullable = identity; rows nullable = u; rows[u] == skip_row untouched;
+ * rows unique). Used for the user tower's item-id embedding gradient
+ * (v1_refine_usertower.py:447-459, nn.Embedding backward) with the sort built ahead of the
+ * step, and for the per-user profile gradient (the broadcast of :498-505 over each user's
+ * contiguous packed tokens); deterministic. */
 int rsx_segment_sum_rows(const float* src, int64_t ld_src, const int64_t* perm, const int64_t* seg_off,
                          const int64_t* rows, int64_t nseg, int64_t D, const float* scale, int64_t skip_row,
                          float* dst, int64_t ld_dst, int accumulate, void* stream);

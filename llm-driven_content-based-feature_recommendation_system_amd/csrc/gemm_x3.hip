@@ -40,7 +40,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kBM = 128, kBN = 128, kBK = RSX_GEMM_BK;
 constexpr int kRow = kBK + 8;  // bf16 per LDS row (80 B at BK 32, 48 B at BK 16: conflict-free b128 reads)
 constexpr int kF4 = kBK / 8;   // float4 loads per thread and operand per stage (two threads per row)
-constexpr int EPI_BIAS = 0, EPI_GELU_DROP = 1, EPI_DGELU_DROP = 2;
+constexpr int EPI_BIAS = 0, EPI_GELU_DROP = 1, EPI_DGELU_DROP = 2, EPI_ROWADD = 3;
 #ifndef RSX_GEMM_BLOCKS
 #define RSX_GEMM_BLOCKS (1 << 30)  // workgroup budget of the multi-tile stream: at BK 16 one tile each measured best
 #endif
@@ -69,7 +69,9 @@ struct GArgs {
   const float* B;     // [N, ldb]
   const float* bias;  // [N] (nullable)
   float* C;           // [M, ldc]
-  float* aux;         // [M, ldaux]: gelu'(pre) (written by EPI_GELU_DROP, read by EPI_DGELU_DROP)
+  float* aux;         // [M, ldaux]: gelu'(pre) (written by EPI_GELU_DROP, read by EPI_DGELU_DROP);
+                      // EPI_ROWADD: the row table R [*, ldaux]
+  const int64_t* ridx;  // EPI_ROWADD: C[m] += R[ridx[m]]
   int64_t lda, ldb, ldc, ldaux, M;
   int N, K, epi, tiles_n, tiles, per;
   rsx::Dropout drop;
@@ -317,11 +319,13 @@ __global__ __launch_bounds__(kWsThreads, 1) void gemm_ws_k(WsArgs w) {
     int64_t m = (s_first + (int64_t)(t / KC) * s_step) * 32 + c;
     if (m >= a.M) m = a.M - 1;
     float* crow = a.C + m * a.ldc + n0 + 4 * h;
-    float* xrow = (EPI != EPI_BIAS) ? a.aux + m * a.ldaux + n0 + 4 * h : nullptr;
-    // EPI_DGELU_DROP: the strip's saved GELU derivatives are loaded before its MFMAs (vmcnt
-    // retires in order, so a load issued at the epilogue would drain the prefetched strips)
+    float* xrow = (EPI == EPI_GELU_DROP || EPI == EPI_DGELU_DROP) ? a.aux + m * a.ldaux + n0 + 4 * h : nullptr;
+    // EPI_DGELU_DROP / EPI_ROWADD: the strip's saved GELU derivatives / added table rows are
+    // loaded before its MFMAs (vmcnt retires in order, so a load issued at the epilogue
+    // would drain the prefetched strips)
+    if (EPI == EPI_ROWADD) xrow = a.aux + a.ridx[m] * a.ldaux + n0 + 4 * h;
     float4 z[NT][4];
-    if (EPI == EPI_DGELU_DROP && q == KC - 1) {
+    if ((EPI == EPI_DGELU_DROP || EPI == EPI_ROWADD) && q == KC - 1) {
 #pragma unroll
       for (int j = 0; j < NT; ++j)
 #pragma unroll
@@ -358,6 +362,9 @@ __global__ __launch_bounds__(kWsThreads, 1) void gemm_ws_k(WsArgs w) {
         } else {
           const float4 bb = *reinterpret_cast<const float4*>(&sBias[o + 4 * h]);
           v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+          if (EPI == EPI_ROWADD) {
+            v[0] += z[j][g].x; v[1] += z[j][g].y; v[2] += z[j][g].z; v[3] += z[j][g].w;
+          }
         }
         if (EPI == EPI_GELU_DROP) {
           float d[4];
@@ -370,7 +377,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void gemm_ws_k(WsArgs w) {
           }
           *reinterpret_cast<float4*>(xrow + o) = make_float4(d[0], d[1], d[2], d[3]);
         }
-        if (EPI != EPI_BIAS && a.drop.active()) {
+        if ((EPI == EPI_GELU_DROP || EPI == EPI_DGELU_DROP) && a.drop.active()) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = keep(a.drop, e0 + o + e) ? v[e] * a.drop.scale : 0.0f;
         }
@@ -449,6 +456,8 @@ void launch_ws(const GArgs& g, hipStream_t st) {
   w.groups = groups;
   const int grid = (w.nblk * groups + 7) / 8 * 8;
   if (g.epi == EPI_BIAS) hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_BIAS>), dim3(grid), dim3(kWsThreads), 0, st, w);
+  else if (g.epi == EPI_ROWADD)
+    hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_ROWADD>), dim3(grid), dim3(kWsThreads), 0, st, w);
   else if (g.epi == EPI_GELU_DROP)
     hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_GELU_DROP>), dim3(grid), dim3(kWsThreads), 0, st, w);
   else hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_DGELU_DROP>), dim3(grid), dim3(kWsThreads), 0, st, w);
@@ -470,7 +479,7 @@ RSX_API int rsx_gemm_x3(const float* A, int64_t lda, const float* B, int64_t ldb
   RSX_ARG(M * (int64_t)N < (1LL << 32), "M * N must be < 2^32 (dropout element index)");
   if (M == 0) return 0;
   GArgs g;
-  g.A = A; g.B = B; g.bias = bias; g.C = C; g.aux = aux;
+  g.A = A; g.B = B; g.bias = bias; g.C = C; g.aux = aux; g.ridx = nullptr;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.ldaux = ldaux; g.M = M;
   g.N = N; g.K = K; g.epi = epi;
   g.tiles_n = N / kBN;
@@ -491,6 +500,31 @@ RSX_API int rsx_gemm_x3(const float* A, int64_t lda, const float* B, int64_t ldb
   if (epi == EPI_BIAS) hipLaunchKernelGGL(gemm_x3_nt_k<EPI_BIAS>, dim3(grid), dim3(256), 0, st, g);
   else if (epi == EPI_GELU_DROP) hipLaunchKernelGGL(gemm_x3_nt_k<EPI_GELU_DROP>, dim3(grid), dim3(256), 0, st, g);
   else hipLaunchKernelGGL(gemm_x3_nt_k<EPI_DGELU_DROP>, dim3(grid), dim3(256), 0, st, g);
+  RSX_LAUNCHED();
+  return 0;
+}
+
+// C[m] = A[m] . B^T + bias + R[ridx[m]]  (a per-row table added in the epilogue: the user
+// tower's output_proj[0] over the packed tokens plus its per-user profile half,
+// v1_refine_usertower.py:498-505). K in {128, 256} (weight-stationary path), N % 128 == 0.
+RSX_API int rsx_gemm_x3_rowadd(const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias,
+                               int64_t M, int N, int K, const float* R, int64_t ldr, const int64_t* ridx, float* C,
+                               int64_t ldc, void* stream) {
+  RSX_ARG(A && B && C && R && ridx, "null tensor");
+  RSX_ARG(M >= 0 && N > 0 && N % 128 == 0 && (K == 128 || K == 256), "N must be a multiple of 128, K 128 or 256");
+  RSX_ARG(lda >= K && ldb >= K && ldc >= N && ldr >= N && lda % 4 == 0 && ldb % 4 == 0 && ldr % 4 == 0 &&
+              ldc % 4 == 0, "bad leading dimensions");
+  RSX_ARG(((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0 && ((uintptr_t)R % 16) == 0 &&
+              ((uintptr_t)C % 16) == 0, "A/B/R/C must be 16-byte aligned");
+  if (M == 0) return 0;
+  GArgs g = {};
+  g.A = A; g.B = B; g.bias = bias; g.C = C; g.aux = const_cast<float*>(R); g.ridx = ridx;
+  g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.ldaux = ldr; g.M = M;
+  g.N = N; g.K = K; g.epi = EPI_ROWADD;
+  g.drop = rsx::make_dropout(0.0f, 0);
+  hipStream_t st = (hipStream_t)stream;
+  if (K == 128) launch_ws<1, 128>(g, st);
+  else launch_ws<2, 128>(g, st);
   RSX_LAUNCHED();
   return 0;
 }

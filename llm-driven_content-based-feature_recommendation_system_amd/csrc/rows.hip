@@ -137,12 +137,12 @@ __global__ __launch_bounds__(256) void segsum_rows_k(const float* __restrict__ s
   for (int64_t u0 = wave_g * RPW; u0 < nseg; u0 += nw * RPW) {
     const int64_t u = u0 + sub;
     if (u >= nseg) continue;
-    const int64_t row = rows[u];
+    const int64_t row = rows ? rows[u] : u;
     if (row == skip) continue;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     const int64_t k1 = seg[u + 1];
     for (int64_t k = seg[u]; k < k1; ++k) {
-      const float4 x = reinterpret_cast<const float4*>(src + perm[k] * ld_src)[c];
+      const float4 x = reinterpret_cast<const float4*>(src + (perm ? perm[k] : k) * ld_src)[c];
       acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
     }
     float4* d = reinterpret_cast<float4*>(dst + row * ld_dst) + c;
@@ -208,7 +208,7 @@ RSX_API int rsx_scatter_rows(const float* dy, const float* y, const float* nrm, 
 RSX_API int rsx_segment_sum_rows(const float* src, int64_t ld_src, const int64_t* perm, const int64_t* seg_off,
                                  const int64_t* rows, int64_t nseg, int64_t D, const float* scale, int64_t skip_row,
                                  float* dst, int64_t ld_dst, int accumulate, void* stream) {
-  RSX_ARG(src && perm && seg_off && rows && dst, "null tensor");
+  RSX_ARG(src && seg_off && dst, "null tensor");  // perm NULL: identity; rows NULL: row u
   RSX_ARG(D == 64 || D == 128 || D == 256, "D must be 64, 128 or 256");
   RSX_ARG(ld_src >= D && ld_dst >= D && ld_src % 4 == 0 && ld_dst % 4 == 0, "bad leading dimensions");
   if (nseg == 0) return 0;

@@ -741,6 +741,82 @@ def linear_tok(x, weight, bias=None):
     return y.reshape(*shp[:-1], weight.shape[0])
 
 
+class _ProfileLinear(torch.autograd.Function):
+    """h[t] = x[t] W[:, :D]^T + (profile W[:, D:]^T + b)[user(t)]: nn.Linear(2D -> N) applied
+    to cat(x_tok, profile[user]) without materialising the concatenation or the broadcast
+    (v1_refine_usertower.py:498-505, output_proj[0] on the packed tokens). Forward: the small
+    per-user GEMM, then the token GEMM with the per-user rows added in its epilogue
+    (rsx_gemm_x3_rowadd). Backward: dX on rsx_gemm_x3; the per-user gradient is a segmented
+    sum over each user's contiguous tokens (rsx_segment_sum_rows, no atomics); both weight
+    halves and the bias from the split-K weight-gradient kernel, written into one [N, 2D]
+    gradient (no slice / concatenation kernels)."""
+
+    @staticmethod
+    def forward(ctx, x, profile, weight, bias, tok_user, seg):
+        D = x.shape[1]
+        n = weight.shape[0]
+        wp = weight[:, D:]
+        prof = gemm_x3(profile, wp, bias, tag="tok_linear_fwd") if _x3_ok(n, D) else \
+            torch.addmm(bias, profile, wp.t())
+        h = torch.empty(x.shape[0], n, device=x.device, dtype=torch.float32)
+        with timed("tok_linear_fwd"):
+            rc = N.lib().rsx_gemm_x3_rowadd(N.ptr(x), x.stride(0), N.ptr(weight), weight.stride(0), None,
+                                            x.shape[0], n, D, N.ptr(prof), prof.stride(0), N.ptr(tok_user),
+                                            N.ptr(h), h.stride(0), N.stream())
+        N.check(rc, "gemm_x3_rowadd")
+        ctx.save_for_backward(x, profile, weight, seg)
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        x, profile, weight, seg = ctx.saved_tensors
+        dh = _c(dh)
+        D = x.shape[1]
+        n = weight.shape[0]
+        U = profile.shape[0]
+        dprof = torch.empty(U, n, device=dh.device, dtype=torch.float32)
+        rc = N.lib().rsx_segment_sum_rows(N.ptr(dh), dh.stride(0), None, N.ptr(seg), None, U, n, None, -1,
+                                          N.ptr(dprof), dprof.stride(0), 0, N.stream())
+        N.check(rc, "segment_sum_rows(profile)")
+        dx = dprofile = None
+        if ctx.needs_input_grad[0]:
+            dx = gemm_x3(dh, weight[:, :D].t(), tag="tok_linear_dx")
+        if ctx.needs_input_grad[1]:
+            dprofile = gemm_x3(dprof, weight[:, D:].t(), tag="tok_linear_dx") if _x3_ok(D, n) else \
+                dprof @ weight[:, D:]
+        dw = torch.empty_like(weight)
+        db = torch.empty(n, device=dh.device, dtype=torch.float32)
+        _wgrad_into(dh, x, dw[:, :D], None)
+        _wgrad_into(dprof, profile, dw[:, D:], db)
+        return dx, dprofile, dw, db, None, None
+
+
+def _wgrad_into(dy, x, dw_view, db):
+    """dW (+ db) of y = x W^T + b written into a (row-strided) view: rsx_linear_wgrad(_x3)."""
+    t, n = dy.shape
+    k = x.shape[1]
+    nws = N.lib().rsx_linear_wgrad_workspace_floats(t, n, k)
+    ws = torch.empty(nws, device=dy.device, dtype=torch.float32)
+    fn = N.lib().rsx_linear_wgrad_x3 if _gemm_precision == "bf16x3" else N.lib().rsx_linear_wgrad
+    with timed("linear_wgrad"):
+        rc = fn(N.ptr(dy), dy.stride(0), N.ptr(_c(x)), x.stride(0), t, n, k, N.ptr(dw_view), dw_view.stride(0),
+                N.ptr(db), 0, N.ptr(ws), nws, N.stream())
+    N.check(rc, "linear_wgrad")
+
+
+def profile_linear(x, profile, weight, bias, tok_user, seg):
+    """x [T, D] packed tokens, profile [U, D] per user, weight [N, 2D], bias [N], tok_user [T]
+    int64 (user of each token, non-decreasing), seg [U + 1] int64 token offsets of the users.
+    Returns [T, N] = F.linear(cat(x, profile[tok_user]), weight, bias)."""
+    N.ensure_device(x)
+    D = x.shape[1]
+    n = weight.shape[0]
+    if (x.shape[0] == 0 or weight.shape[1] != 2 * D or D not in (128, 256) or n % 128 or weight.stride(1) != 1
+            or weight.stride(0) % 4 or _gemm_precision != "bf16x3"):
+        return linear_tok(x, weight[:, :D]) + torch.nn.functional.linear(profile, weight[:, D:], bias)[tok_user]
+    return _ProfileLinear.apply(_c(x), _c(profile), weight, bias, _c(tok_user), _c(seg))
+
+
 class _FFN(torch.autograd.Function):
     """linear2(dropout(gelu(linear1(h)))) with the GELU and the dropout in the GEMM epilogues
     (rsx_gemm_x3 EPI_GELU_DROP forward, EPI_DGELU_DROP for the backward through them)."""

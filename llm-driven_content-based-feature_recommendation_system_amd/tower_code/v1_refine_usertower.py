@@ -219,8 +219,7 @@ class SASRecUserTower(nn.Module):
                                        club_status_ids, news_freq_ids, fn_ids, active_ids, cont_feats, u_g)
         lin0, ln, lin3 = self.output_proj[0], self.output_proj[1], self.output_proj[3]
         D = self.d_model
-        prof = F.linear(profile, lin0.weight[:, D:], lin0.bias)
-        h = ops.linear_tok(x, lin0.weight[:, :D]) + ops.gather_rows(prof, packed.tok_user)
+        h = ops.profile_linear(x, profile, lin0.weight, lin0.bias, packed.tok_user, packed.seg_off64)
         h = ops.layer_norm(h, ln.weight, ln.bias, ln.eps, act=ops.ACT_GELU_ERF)
         return ops.l2_normalize(ops.linear_tok(h, lin3.weight, lin3.bias))
 
@@ -247,6 +246,7 @@ class PackedTokens:
         seg = torch.zeros(B + 1, device=dev, dtype=torch.int64)
         seg[1:] = torch.cumsum(torch.bincount(self.tok_user, minlength=B), 0)
         self.seg_off = seg.to(torch.int32)
+        self.seg_off64 = seg
         self.valid_tok = (self.tok_pad == 0).nonzero().squeeze(1)   # loss rows (valid steps, flat order)
         pad_len = L - cnt
         self.last_tok = seg[:-1] + torch.where(need_extra, torch.zeros_like(last), last - pad_len)

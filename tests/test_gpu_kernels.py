@@ -644,3 +644,36 @@ def test_static_embed_against_torch(gpu):
     torch.testing.assert_close(outs[0][1], outs[1][1], atol=1e-3, rtol=1e-5)
     for a, r in zip(outs[0][2], outs[1][2]):
         torch.testing.assert_close(a, r, atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("users,n", [(37, 128), (300, 256)])
+def test_profile_linear_matches_concat_linear(gpu, users, n):
+    """ops.profile_linear == F.linear(cat(x, profile[tok_user]), W, b) in float64, value and
+    all gradients: the row-add GEMM epilogue, the segmented per-user gradient and both weight
+    halves written into one [N, 2D] gradient. Users with 0 tokens included."""
+    g = torch.Generator().manual_seed(users)
+    counts = torch.randint(0, 40, (users,), generator=g)
+    counts[3] = 0
+    tok_user = torch.repeat_interleave(torch.arange(users), counts)
+    seg = torch.zeros(users + 1, dtype=torch.int64)
+    seg[1:] = torch.cumsum(counts, 0)
+    T, D = tok_user.numel(), 128
+    x = torch.randn(T, D, generator=g)
+    prof = torch.randn(users, D, generator=g)
+    w = torch.randn(n, 2 * D, generator=g) / 16
+    b = torch.randn(n, generator=g)
+    gy = torch.randn(T, n, generator=g)
+    outs = []
+    for impl in ("rsx", "torch64"):
+        if impl == "rsx":
+            ts = [t.to(gpu).requires_grad_() for t in (x, prof, w, b)]
+            y = ops.profile_linear(ts[0], ts[1], ts[2], ts[3], tok_user.to(gpu), seg.to(gpu))
+            (y * gy.to(gpu)).sum().backward()
+        else:
+            ts = [t.double().requires_grad_() for t in (x, prof, w, b)]
+            y = F.linear(torch.cat([ts[0], ts[1][tok_user]], 1), ts[2], ts[3])
+            (y * gy.double()).sum().backward()
+        outs.append([y.detach()] + [t.grad for t in ts])
+    for a, r in zip(*outs):
+        a = a.double().cpu()
+        assert (a - r).abs().max().item() <= 2e-4 + 2e-5 * r.abs().max().item()
