@@ -191,6 +191,10 @@ int rsx_static_embed_bwd(const int64_t* const* ids, const float* const* tables, 
 int rsx_ln_fwd(const float* x, const float* res, float p_drop, uint64_t seed, const float* w, const float* b,
                float eps, int act, int64_t T, int64_t D, float* sum_out, float* y, float* mean, float* rstd,
                void* stream);
+/* Backward of the add-only form of rsx_ln_fwd (y = NULL: s = x + dropout_p(res), as after the
+ * encoder's last layer, v1_refine_usertower.py:343-352): dres = the forward's keep-mask / (1 - p)
+ * applied to ds (flat index row*D + col); dx is ds itself. */
+int rsx_dropout_bwd(const float* ds, int64_t T, int64_t D, float p_drop, uint64_t seed, float* dres, void* stream);
 int64_t rsx_ln_bwd_workspace_floats(int64_t T, int64_t D);
 int rsx_ln_bwd(const float* s, const float* mean, const float* rstd, const float* w, const float* b, int act,
                const float* dy, const float* ds_in, float p_drop, uint64_t seed, int64_t T, int64_t D, float* ds_out,

@@ -1162,16 +1162,33 @@ __device__ __forceinline__ void grad_x3s(f32x16 (&gacc)[4], const bf16x8 (&gh)[2
   }
 }
 
+// (a, b) -> packed bf16 hi pair and lo pair (x = hi + lo, hi = RNE bf16(x), lo = bf16(x - hi)):
+// one pair conversion for hi, its two halves unpacked as fp32 by a shift and a mask, two
+// subtractions and one pair conversion for lo (the per-element form converted every element
+// twice and re-packed).
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void split_pair(float a, float b, uint32_t& hi, uint32_t& lo) {
+  const bf16x2 h = {(__bf16)a, (__bf16)b};
+  hi = __builtin_bit_cast(uint32_t, h);
+  const float ha = __uint_as_float(hi << 16), hb = __uint_as_float(hi & 0xffff0000u);
+  const bf16x2 l = {(__bf16)(a - ha), (__bf16)(b - hb)};
+  lo = __builtin_bit_cast(uint32_t, l);
+}
+
 __device__ __forceinline__ void split_tile(const f32x16& g, bf16x8 (&gh)[2], bf16x8 (&gl)[2]) {
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks)
+  for (int ks = 0; ks < 2; ++ks) {
+    u32x4 h, l;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float x = g[8 * ks + j];
-      const __bf16 hj = (__bf16)x;
-      gh[ks][j] = hj;
-      gl[ks][j] = (__bf16)(x - (float)hj);
+    for (int q = 0; q < 4; ++q) {
+      uint32_t hq, lq;
+      split_pair(g[8 * ks + 2 * q], g[8 * ks + 2 * q + 1], hq, lq);
+      h[q] = hq;
+      l[q] = lq;
     }
+    gh[ks] = __builtin_bit_cast(bf16x8, h);
+    gl[ks] = __builtin_bit_cast(bf16x8, l);
+  }
 }
 
 // The backward's software pipeline: the S tile of the NEXT streamed tile (MFMA, returned) runs
@@ -1213,14 +1230,21 @@ __device__ __forceinline__ f32x16 dots_g_x3(const X3Tile& t, int c, int h, const
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, ul[s], acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, uh[s], acc, 0, 0, 0);
     }
+    float gp[2];
 #pragma unroll
     for (int rr = 0; rr < 2; ++rr) {
       const int r = 2 * s + rr, e = r & 3;
       const float f = ROW ? fo * q1[e] : fo;
-      const float g = f * __builtin_amdgcn_exp2f(fmaf(S[r], it2, -(q0[e] + o_m2)));
-      const __bf16 hi = (__bf16)g;
-      gh[r >> 3][r & 7] = hi;
-      gl[r >> 3][r & 7] = (__bf16)(g - (float)hi);
+      gp[rr] = f * __builtin_amdgcn_exp2f(fmaf(S[r], it2, -(q0[e] + o_m2)));
+    }
+    {  // rows 2s, 2s+1 = dword s & 3 of fragment s >> 2
+      uint32_t hp, lp;
+      split_pair(gp[0], gp[1], hp, lp);
+      u32x4 hv = __builtin_bit_cast(u32x4, gh[s >> 2]), lv = __builtin_bit_cast(u32x4, gl[s >> 2]);
+      hv[s & 3] = hp;
+      lv[s & 3] = lp;
+      gh[s >> 2] = __builtin_bit_cast(bf16x8, hv);
+      gl[s >> 2] = __builtin_bit_cast(bf16x8, lv);
     }
     if (s & 1) {
       q0 = n0;
@@ -1895,7 +1919,7 @@ __global__ __launch_bounds__(256, 2) void nce_bwd_x3_k(BwdArgs a, X3Args x) {
 constexpr float kLazyLog2 = 8.0f;
 __global__ __launch_bounds__(256, 2) void nce_grouped_fwdg_x3_k(GArgs a) {
   __shared__ __attribute__((aligned(16))) X3Tile sT[2];
-  __shared__ __attribute__((aligned(16))) float sB2[2][kTile];   // bias_d * log2e (+inf past the split)
+  __shared__ __attribute__((aligned(16))) float sB2[2][kTile];   // -bias_d * log2e (-inf past the split)
   __shared__ __attribute__((aligned(16))) float sCnt[2][kTile];  // c_d (0 past the split)
   __shared__ __attribute__((aligned(16))) float sAlpha[kWaves][32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1940,7 +1964,7 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_fwdg_x3_k(GArgs a) {
   auto lstore = [&](int buf) {
     stg.store(sT[buf], tid);
     if (tid < kTile) {
-      sB2[buf][tid] = stg_b * kLog2e;
+      sB2[buf][tid] = -(stg_b * kLog2e);  // negated here: one fma per logit, no negation
       sCnt[buf][tid] = stg_c;
     }
   };
@@ -1954,12 +1978,18 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_fwdg_x3_k(GArgs a) {
       const bool exc = (int64_t)next < j0 + kTile;  // before the prefetch (see the backward)
       if (has_next) gload(j0 + kTile);
       f32x16 acc = dots_x3(sT[cur], c, h, uh, ul);
+      // registers 4g..4g+3 hold tile rows 8g + 4h + 0..3: one b128 read per group and array
+      // (an immediate offset from a per-lane base) instead of 16 scalar reads with 32 address ops
       float w[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int tr = tile_row(r, h);
-        w[r] = sCnt[cur][tr];
-        acc[r] = fmaf(acc[r], it2, -sB2[cur][tr]);  // x = S/tau - bias, base 2 (-inf past the split)
+      for (int g = 0; g < 4; ++g) {
+        const float4 cw = *reinterpret_cast<const float4*>(&sCnt[cur][8 * g + 4 * h]);
+        const float4 nb = *reinterpret_cast<const float4*>(&sB2[cur][8 * g + 4 * h]);
+        w[4 * g + 0] = cw.x; w[4 * g + 1] = cw.y; w[4 * g + 2] = cw.z; w[4 * g + 3] = cw.w;
+        acc[4 * g + 0] = fmaf(acc[4 * g + 0], it2, nb.x);  // x = S/tau - bias, base 2 (-inf past the split)
+        acc[4 * g + 1] = fmaf(acc[4 * g + 1], it2, nb.y);
+        acc[4 * g + 2] = fmaf(acc[4 * g + 2], it2, nb.z);
+        acc[4 * g + 3] = fmaf(acc[4 * g + 3], it2, nb.w);
       }
       if (__any(exc)) {
         if (exc) {

@@ -68,6 +68,7 @@ __global__ __launch_bounds__(256) void ln_fwd_k(FArgs a) {
       s.x += q.x; s.y += q.y; s.z += q.z; s.w += q.w;
       if (a.sum_out) reinterpret_cast<float4*>(a.sum_out + r * D)[c] = s;
     }
+    if (!a.y) continue;  // residual add + dropout only (the encoder's last residual)
     const float mu = rsx::wave_sum_width((s.x + s.y) + (s.z + s.w), LPR) * (1.0f / D);
     const float4 d = make_float4(s.x - mu, s.y - mu, s.z - mu, s.w - mu);
     const float var = rsx::wave_sum_width(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w, LPR) * (1.0f / D);
@@ -194,12 +195,26 @@ int64_t bwd_blocks(int64_t T, int64_t D, int64_t& rpb) {
   return (T + rpb - 1) / rpb;
 }
 
+// dres = dropout mask (the forward's hash of (seed, i)) applied to ds, flat over T x D
+__global__ __launch_bounds__(256) void dropout_bwd_k(const float* __restrict__ ds, int64_t n4, rsx::Dropout drop,
+                                                     float* __restrict__ dres) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    float4 g = reinterpret_cast<const float4*>(ds)[i];
+    const uint64_t bi = (uint64_t)i * 4;
+    g.x = drop.apply(g.x, bi + 0);
+    g.y = drop.apply(g.y, bi + 1);
+    g.z = drop.apply(g.z, bi + 2);
+    g.w = drop.apply(g.w, bi + 3);
+    reinterpret_cast<float4*>(dres)[i] = g;
+  }
+}
+
 }  // namespace
 
 RSX_API int rsx_ln_fwd(const float* x, const float* res, float p_drop, uint64_t seed, const float* w, const float* b,
                        float eps, int act, int64_t T, int64_t D, float* sum_out, float* y, float* mean, float* rstd,
                        void* stream) {
-  RSX_ARG(x && y, "null tensor");
+  RSX_ARG(x && (y || (res && sum_out)), "null tensor (y may be null only for the add-only form)");
   RSX_ARG(D == 64 || D == 128 || D == 256, "D must be 64, 128 or 256");
   RSX_ARG(act == 0 || act == 2, "act must be 0 (none) or 2 (gelu)");
   RSX_ARG(p_drop >= 0.0f && p_drop < 1.0f, "p_drop must be in [0,1)");
@@ -254,5 +269,23 @@ RSX_API int rsx_ln_bwd(const float* s, const float* mean, const float* rstd, con
                        (int)D);
     RSX_LAUNCHED();
   }
+  return 0;
+}
+
+// Backward of s = x + dropout(res) (rsx_ln_fwd with y = NULL): dres = mask(ds) with the same
+// (seed, row*D + col) hash; ds itself is dx. Replaces the autograd of
+// `x + F.dropout(f, p)` after the encoder's last layer (v1_refine_usertower.py:343-352).
+RSX_API int rsx_dropout_bwd(const float* ds, int64_t T, int64_t D, float p_drop, uint64_t seed, float* dres,
+                            void* stream) {
+  RSX_ARG(ds && dres, "null tensor");
+  RSX_ARG(D % 4 == 0, "D must be a multiple of 4");
+  RSX_ARG(p_drop >= 0.0f && p_drop < 1.0f, "p_drop must be in [0,1)");
+  if (T == 0) return 0;
+  const int64_t n4 = T * D / 4;
+  int64_t blocks = (n4 + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(dropout_bwd_k, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, ds, n4,
+                     rsx::make_dropout(p_drop, seed), dres);
+  RSX_LAUNCHED();
   return 0;
 }

@@ -624,6 +624,78 @@ class _AddLayerNorm(torch.autograd.Function):
         return dx, dres, dw, db, None, None, None
 
 
+class _LayerNormPass(torch.autograd.Function):
+    """(x, LayerNorm(x)): the first norm1 of a norm_first encoder, whose input also feeds the
+    residual. The backward adds the residual-path gradient inside the LayerNorm backward
+    (ds_in) instead of autograd's separate add of two [T, D] gradients."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        N.ensure_device(x)
+        T, D = x.shape
+        y = torch.empty_like(x)
+        mean = torch.empty(T, device=x.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        with timed("ln_fwd"):
+            rc = N.lib().rsx_ln_fwd(N.ptr(x), None, 0.0, 0, N.ptr(w), N.ptr(b), eps, 0, T, D, None, N.ptr(y),
+                                    N.ptr(mean), N.ptr(rstd), N.stream())
+        N.check(rc, "ln_fwd")
+        ctx.save_for_backward(x, mean, rstd, w, b)
+        return x.view_as(x), y
+
+    @staticmethod
+    def backward(ctx, dx_pass, dy):
+        x, mean, rstd, w, b = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        if dy is None:
+            return dx_pass, None, None, None
+        dx, _, dw, db = _ln_bwd(x, mean, rstd, w, b, 0, dy, dx_pass, 0.0, 0, need[0], False, need[1], need[2])
+        return dx, dw, db, None
+
+
+def layer_norm_pass(x, weight, bias, eps=1e-5):
+    """(x, LayerNorm(x)) with the residual gradient of x folded into the LayerNorm backward."""
+    shp = x.shape
+    x2, y = _LayerNormPass.apply(_c(x.reshape(-1, shp[-1])), weight, bias, float(eps))
+    return x2.reshape(shp), y.reshape(shp)
+
+
+class _AddDropout(torch.autograd.Function):
+    """s = x + dropout_p(res) in one pass (rsx_ln_fwd's add-only form); backward dx = ds,
+    dres = mask(ds) (rsx_dropout_bwd, the same counter hash)."""
+
+    @staticmethod
+    def forward(ctx, x, res, p_drop, seed):
+        N.ensure_device(x)
+        T, D = x.shape
+        s = torch.empty_like(x)
+        rc = N.lib().rsx_ln_fwd(N.ptr(x), N.ptr(res), p_drop, seed, None, None, 0.0, 0, T, D, N.ptr(s), None,
+                                None, None, N.stream())
+        N.check(rc, "ln_fwd(add)")
+        ctx.cfg = (p_drop, seed, T, D)
+        return s
+
+    @staticmethod
+    def backward(ctx, ds):
+        p_drop, seed, T, D = ctx.cfg
+        ds = _c(ds)
+        dres = None
+        if ctx.needs_input_grad[1]:
+            dres = torch.empty_like(ds)
+            rc = N.lib().rsx_dropout_bwd(N.ptr(ds), T, D, p_drop, seed, N.ptr(dres), N.stream())
+            N.check(rc, "dropout_bwd")
+        return ds, dres, None, None
+
+
+def add_dropout(x, res, p_drop=0.0, training=True):
+    """x + F.dropout(res, p_drop, training) as one kernel (counter-hash mask; p = 0 in eval)."""
+    p = float(p_drop) if training else 0.0
+    shp = x.shape
+    seed = next_seed() if p > 0 else 0
+    s = _AddDropout.apply(_c(x.reshape(-1, shp[-1])), _c(res.reshape(-1, shp[-1])), p, seed)
+    return s.reshape(shp)
+
+
 def layer_norm(x, weight, bias, eps=1e-5, act=0):
     """act(LayerNorm(x)) over the last dim (act 0 none / ACT_GELU_ERF)."""
     shp = x.shape

@@ -51,11 +51,18 @@ def encoder_stack(layers, x, key_pad, p, training, causal=True, seg_off=None):
     """norm_first nn.TransformerEncoderLayer stack (gelu), reference semantics
     (v1_refine_usertower.py:343-352, item_tower.py:169-182):
       x = x + drop(out_proj(mha(norm1(x)))) ; x = x + drop(linear2(drop(gelu(linear1(norm2(x))))))
-    Each residual add is fused with the LayerNorm that follows it (ops.add_layer_norm); the
-    token linears run on the bf16x3 GEMMs (ops.linear_tok), the feed-forward's GELU and dropout
-    in their epilogues (ops.ffn)."""
+    Each residual add is fused with the LayerNorm that follows it (ops.add_layer_norm), the
+    first norm1 folds the residual path's gradient into its backward (ops.layer_norm_pass), the
+    last residual add + dropout is one pass (ops.add_dropout); the token linears run on the
+    bf16x3 GEMMs (ops.linear_tok), the feed-forward's GELU and dropout in their epilogues
+    (ops.ffn)."""
     layers = list(layers)
-    h = ops.layer_norm(x, layers[0].norm1.weight, layers[0].norm1.bias, layers[0].norm1.eps)
+    D = x.shape[-1]
+    fused = D in (64, 128, 256)
+    if fused:
+        x, h = ops.layer_norm_pass(x, layers[0].norm1.weight, layers[0].norm1.bias, layers[0].norm1.eps)
+    else:
+        h = ops.layer_norm(x, layers[0].norm1.weight, layers[0].norm1.bias, layers[0].norm1.eps)
     for i, layer in enumerate(layers):
         sa = layer.self_attn
         qkv = ops.linear_tok(h, sa.in_proj_weight, sa.in_proj_bias)
@@ -67,6 +74,8 @@ def encoder_stack(layers, x, key_pad, p, training, causal=True, seg_off=None):
         if i + 1 < len(layers):
             nxt = layers[i + 1].norm1
             x, h = ops.add_layer_norm(x, f, nxt.weight, nxt.bias, nxt.eps, p)
+        elif fused:
+            x = ops.add_dropout(x, f, p, training)
         else:
             x = x + F.dropout(f, p, training)
     return x
