@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--no-batch8192", action="store_true",
                     help="skip the secondary line at global batch 8192 (the batch BASELINE.json's metric names)")
     ap.add_argument("--steps8192", type=int, default=5)
+    ap.add_argument("--no-batch32768", action="store_true",
+                    help="skip the N=1 run of configs[3]'s global batch 32768 (the strong-scaling baseline)")
+    ap.add_argument("--steps32768", type=int, default=3)
     ap.add_argument("--no-deepfm", action="store_true", help="skip the DeepFM rerank secondary metric")
     ap.add_argument("--deepfm-rows", type=int, default=65536)
     ap.add_argument("--deepfm-vocab", type=int, default=1_000_000)
@@ -445,6 +448,18 @@ def main():
             "warmup": 2, "ms_per_step": round(1e3 * el8 / args.steps8192, 3),
             "valid_positions_per_batch": [sum(c) for c in ng8], "distinct_targets_per_batch": nd8,
             "main_loss_fwd_ms": round(kt8.get("main/nce_fwd", (1, 0.0))[1] / max(kt8.get("main/nce_fwd", (1, 0))[0], 1), 4)}
+        torch.cuda.empty_cache()
+    if world == 1 and not args.no_batch32768 and args.batch != 32768:
+        # configs[3]'s global batch (32,768 users, all negatives in one pool) on ONE GPU: the
+        # strong-scaling baseline for the N = 8 run (4,096 users per GPU, same global batch)
+        el32, kt32, _, ng32, nd32, _ = train_bench(args, 32768, args.steps32768, 1, items, cfg, model, item_tower,
+                                                   opt, bucket, rank, world, device)
+        result["secondary_batch32768"] = {
+            "metric": "SimCSE train-step pairs/sec at d=128 (global batch 32768 on one GPU: strong-scaling baseline "
+                      "of configs[3])",
+            "value": round(32768 * args.steps32768 / el32, 2), "unit": "pairs/s", "steps": args.steps32768,
+            "warmup": 1, "ms_per_step": round(1e3 * el32 / args.steps32768, 3),
+            "valid_positions_per_batch": [sum(c) for c in ng32], "distinct_targets_per_batch": nd32}
         torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_deepfm:
         torch.cuda.empty_cache()
