@@ -222,6 +222,39 @@ def bench_retrieve_rerank(args, device, deepfm):
                           "frac": round(flops / rs / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)}}
 
 
+def bench_item_refresh(args, device):
+    """refresh-item-vectors (utils/inference_utils.py:74-207) on one GPU: the
+    endpoint's eval forward over batches of 4 x 192 = 768 products, d = 128 (the serving
+    defaults), bert-base-shaped local BERT, synthetic tokenised products. items/s."""
+    import numpy as np
+    from recsys_amd import item_tower as IT
+    B, R, S = 768, 32, 32
+    torch.manual_seed(args.seed)
+    model = IT.HybridItemTower(384, 6, 128, 128, bert_model=IT.build_local_bert()).to(device).eval()
+    rng = np.random.default_rng(args.seed + 11)
+    std = torch.from_numpy(rng.integers(0, 384, (B, 6))).to(device)
+    lens = rng.integers(2, R + 1, (B, 9))
+    re_mask = torch.from_numpy((np.arange(R)[None, None, :] < lens[..., None]).astype(np.int64)).to(device)
+    re_ids = torch.from_numpy(rng.integers(1000, 30521, (B, 9, R))).to(device) * re_mask
+    tl = rng.integers(2, S + 1, (B,))
+    txt_mask = torch.from_numpy((np.arange(S)[None, :] < tl[:, None]).astype(np.int64)).to(device)
+    txt = torch.from_numpy(rng.integers(1000, 30521, (B, S))).to(device) * txt_mask
+    with torch.no_grad():
+        for _ in range(2):
+            model(std, re_ids, re_mask, txt, txt_mask)
+        torch.cuda.synchronize()
+        iters = 5
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            model(std, re_ids, re_mask, txt, txt_mask)
+        torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / iters
+    return {"metric": "refresh-item-vectors HybridItemTower forward items/sec (batches of 768, d=128, "
+                      "bert-base-shaped local BERT)",
+            "value": round(B / dt, 1), "unit": "items/s", "ms_per_batch": round(dt * 1e3, 3),
+            "data": "synthetic std/RE/text ids, RE field lengths U{2..32}, random BERT weights"}
+
+
 def bench_item_tower(args, device):
     """BASELINE configs[0] shape on the GPU: HybridItemTower forward (eval) for 256 items,
     d=64, with a locally built bert-base-shaped BERT (random weights). items/s."""
@@ -470,6 +503,7 @@ def main():
         torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_item_tower:
         result["secondary_item_tower"] = bench_item_tower(args, device)
+        result["secondary_item_refresh"] = bench_item_refresh(args, device)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, items, cfg)
     if rank == 0:

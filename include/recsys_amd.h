@@ -270,6 +270,15 @@ int rsx_deepfm_fused(const int64_t* x, int64_t R, int F, const float* const* V, 
                      const float* w1, const float* b1, const float* w2, const float* b2, const float* wo, void* ws,
                      float* logit, float* prob, void* stream);
 
+/* ---- A9: item-tower RE path ------------------------------------------------------------
+ * out[t] = LayerNorm((word[ids[t]] + type_row) + pos[tok_pos[t]]) * ln_w + ln_b over packed
+ * tokens: BertEmbeddings (word + token type 0 + absolute position, LayerNorm, eval) for the
+ * valid tokens of the RE fields only (HybridItemTower.forward, item_tower.py:247-262; their
+ * masked mean ignores the padded ones). D in {256, 512, 768, 1024}. */
+int rsx_embed3_ln(const float* word, int64_t ld_word, const float* pos, const float* type_row, const float* ln_w,
+                  const float* ln_b, float eps, const int64_t* ids, const int64_t* tok_pos, int64_t T, int64_t D,
+                  float* out, void* stream);
+
 /* ---- row gather / scatter / L2 normalise ---------------------------------------------
  * out[r] = src[idx[r]] (idx NULL => r), optionally F.normalize'd (eps) with norms saved:
  *   pretrained_lookup[item_ids]            tower_code/v1_usertower_train.py:760

@@ -134,11 +134,34 @@ class HybridItemTower(nn.Module):
 
     def re_vectors(self, re_input_ids, re_attn_mask):
         """RE fields: BERT word embeddings (no grad) -> re_proj -> masked mean over the field's
-        tokens (count clamped at 1e-9) -> + field position -> LayerNorm  (:247-262)."""
+        tokens (count clamped at 1e-9) -> + field position -> LayerNorm  (:247-262).
+
+        Only the valid tokens enter the masked mean, so they are packed first: BertEmbeddings on
+        the packed ids (rsx_embed3_ln, no [B*9, 32, 768] activation), re_proj + LayerNorm/GELU on
+        the packed rows, and the mean as a segmented sum over each field's contiguous tokens.
+        Same sums as the reference's (feats * m).sum(1) without the zero terms."""
         B, nf, R = re_input_ids.shape
-        flat_ids = re_input_ids.reshape(-1, R)
+        emb = self.bert_model.embeddings
+        m = re_attn_mask.reshape(-1, R)
+        if (emb.word_embeddings.weight.shape[1] % 256 or getattr(emb, "position_embedding_type", "absolute")
+                != "absolute"):
+            return self._re_vectors_dense(re_input_ids, re_attn_mask)
+        flat = (m.reshape(-1) != 0).nonzero().squeeze(1)                     # packed valid tokens
+        tok_seg = torch.div(flat, R, rounding_mode="floor")
+        counts = m.to(torch.float32).sum(dim=1)                              # [B*9]
+        seg = torch.zeros(m.shape[0] + 1, device=m.device, dtype=torch.int64)
+        seg[1:] = torch.cumsum((m != 0).sum(dim=1), 0)
+        word = ops.bert_embed_packed(emb, re_input_ids.reshape(-1)[flat], flat % R)
+        p = self.re_proj
+        feats = _ln(_lin(word, p[0]), p[1], gelu=True)                      # [T_valid, d]
+        vec = ops.segment_mean(feats, seg, tok_seg, counts)
+        vec = vec.reshape(B, nf, -1) + self.re_field_position
+        return _ln(vec, self.re_ln)
+
+    def _re_vectors_dense(self, re_input_ids, re_attn_mask):
+        B, nf, R = re_input_ids.shape
         with torch.no_grad():
-            word = self.bert_model.embeddings(input_ids=flat_ids)
+            word = self.bert_model.embeddings(input_ids=re_input_ids.reshape(-1, R))
         p = self.re_proj
         feats = _ln(_lin(word, p[0]), p[1], gelu=True)                      # [B*9, R, d]
         m = re_attn_mask.reshape(-1, R, 1).to(feats.dtype)

@@ -936,6 +936,56 @@ def ffn(h, w1, b1, w2, b2, p_drop=0.0, training=True):
 
 
 # ----------------------------------------------------------------------------------------
+# A9: item-tower RE fields over packed (valid) tokens
+@torch.no_grad()
+def bert_embed_packed(embeddings, ids, tok_pos):
+    """BertEmbeddings(input_ids) rows for a packed token list (ids [T], positions tok_pos [T],
+    token type 0) via rsx_embed3_ln; dropout as the module's (active only in training)."""
+    N.ensure_device(ids)
+    word = embeddings.word_embeddings.weight
+    D = word.shape[1]
+    T = ids.numel()
+    out = torch.empty(T, D, device=ids.device, dtype=torch.float32)
+    ln = embeddings.LayerNorm
+    rc = N.lib().rsx_embed3_ln(N.ptr(word), word.stride(0), N.ptr(_c(embeddings.position_embeddings.weight)),
+                               N.ptr(_c(embeddings.token_type_embeddings.weight[0])), N.ptr(ln.weight),
+                               N.ptr(ln.bias), float(ln.eps), N.ptr(_c(ids)), N.ptr(_c(tok_pos)), T, D, N.ptr(out),
+                               N.stream())
+    N.check(rc, "embed3_ln")
+    if embeddings.training and embeddings.dropout.p > 0:
+        out = torch.nn.functional.dropout(out, embeddings.dropout.p, True)
+    return out
+
+
+class _SegmentMean(torch.autograd.Function):
+    """vec[u] = sum_{t in [seg[u], seg[u+1])} x[t] / max(cnt[u], 1e-9): the masked mean of the
+    reference's (feats * m).sum(1) / clamp(m.sum(1), 1e-9) over packed valid tokens."""
+
+    @staticmethod
+    def forward(ctx, x, seg, tok_seg, inv):
+        U = inv.numel()
+        D = x.shape[1]
+        s = torch.empty(U, D, device=x.device, dtype=torch.float32)
+        rc = N.lib().rsx_segment_sum_rows(N.ptr(x), x.stride(0), None, N.ptr(seg), None, U, D, None, -1, N.ptr(s),
+                                          s.stride(0), 0, N.stream())
+        N.check(rc, "segment_sum_rows(mean)")
+        ctx.save_for_backward(tok_seg, inv)
+        return s * inv.unsqueeze(1)
+
+    @staticmethod
+    def backward(ctx, dv):
+        tok_seg, inv = ctx.saved_tensors
+        return gather_rows(_c(dv * inv.unsqueeze(1)), tok_seg), None, None, None
+
+
+def segment_mean(x, seg, tok_seg, counts):
+    """x [T, D] packed rows (segments contiguous), seg [U+1] int64 offsets, tok_seg [T] int64,
+    counts [U] float -> [U, D] means (a zero-count segment gives 0, as the clamp does)."""
+    inv = 1.0 / torch.clamp(counts, min=1e-9)
+    return _SegmentMean.apply(_c(x), _c(seg), _c(tok_seg), inv.float())
+
+
+# ----------------------------------------------------------------------------------------
 # A16: DeepFM forward (inference)
 ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
 
