@@ -222,6 +222,32 @@ def bench_retrieve_rerank(args, device, deepfm):
                           "frac": round(flops / rs / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)}}
 
 
+def bench_dcn(args, device):
+    """The reference's DCN-V2 RankingModel (temp_model/ranker_skelet.py:274-357; SURVEY.md 8f
+    #3) scoring 4,096 queries x 100 retrieved candidates (user 128 + item 128 + context 20).
+    rows/s with inputs resident in HBM."""
+    from recsys_amd.temp_model.ranker_skelet import RankingModel
+    R = 4096 * 100
+    torch.manual_seed(args.seed)
+    model = RankingModel(128, 128, 20).to(device).eval()
+    g = torch.Generator(device="cpu").manual_seed(13)
+    u = torch.nn.functional.normalize(torch.randn(R, 128, generator=g), dim=1).to(device)
+    it = torch.nn.functional.normalize(torch.randn(R, 128, generator=g), dim=1).to(device)
+    c = torch.randn(R, 20, generator=g).to(device)
+    for _ in range(3):
+        model(u, it, c)
+    torch.cuda.synchronize()
+    iters = 10
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        model(u, it, c)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / iters
+    return {"metric": "DCN-V2 RankingModel rerank rows/sec (user 128 + item 128 + context 20, 409,600 rows)",
+            "value": round(R / dt, 1), "unit": "rows/s", "ms_per_batch": round(dt * 1e3, 4),
+            "data": "synthetic normalised vectors, random-init model"}
+
+
 def bench_item_refresh(args, device):
     """refresh-item-vectors (utils/inference_utils.py:74-207) on one GPU: the
     endpoint's eval forward over batches of 4 x 192 = 768 products, d = 128 (the serving
@@ -499,6 +525,7 @@ def main():
         deepfm, result["secondary"] = bench_deepfm(args, device)
         if not args.no_rerank:
             result["secondary_retrieve_rerank"] = bench_retrieve_rerank(args, device, deepfm)
+            result["secondary_dcn_rerank"] = bench_dcn(args, device)
         del deepfm
         torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_item_tower:

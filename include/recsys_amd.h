@@ -279,6 +279,13 @@ int rsx_embed3_ln(const float* word, int64_t ld_word, const float* pos, const fl
                   const float* ln_b, float eps, const int64_t* ids, const int64_t* tok_pos, int64_t T, int64_t D,
                   float* out, void* stream);
 
+/* ---- DCN-V2 reranker ------------------------------------------------
+ * CrossNet (temp_model/ranker_skelet.py:239-272): x_{l+1} = x_0 * (x_l . k_l + b_l) + x_l for L
+ * layers (k_l [D], b_l [D]); writes x_L (x_out, nullable) and/or head_part[b] = x_L . w_head
+ * (the cross half of RankingModel.final_head, :313-338). D % 4 == 0, D <= 512, L <= 8. */
+int rsx_crossnet(const float* x, int64_t ldx, int64_t B, int D, int L, const float* const* kernels,
+                 const float* const* biases, const float* w_head, float* x_out, float* head_part, void* stream);
+
 /* ---- row gather / scatter / L2 normalise ---------------------------------------------
  * out[r] = src[idx[r]] (idx NULL => r), optionally F.normalize'd (eps) with norms saved:
  *   pretrained_lookup[item_ids]            tower_code/v1_usertower_train.py:760

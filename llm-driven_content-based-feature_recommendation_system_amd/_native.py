@@ -75,6 +75,7 @@ _SIGS = {
     "rsx_retrieve_topk": (c_i, [c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p]),
     "rsx_gather_rows": (c_i, [c_p, c_i64, c_p, c_i64, c_i64, c_i, c_f, c_p, c_p, c_p]),
     "rsx_embed3_ln": (c_i, [c_p, c_i64, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_i64, c_i64, c_p, c_p]),
+    "rsx_crossnet": (c_i, [c_p, c_i64, c_i64, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p]),
     "rsx_segment_sum_rows": (c_i, [c_p, c_i64, c_p, c_p, c_p, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_i, c_p]),
     "rsx_scatter_rows": (c_i, [c_p, c_p, c_p, c_p, c_i64, c_i64, c_i, c_f, c_i, c_i64, c_p, c_i64, c_p]),
 }

@@ -986,6 +986,24 @@ def segment_mean(x, seg, tok_seg, counts):
 
 
 # ----------------------------------------------------------------------------------------
+# DCN-V2 reranker: cross network + the cross half of the final head
+def crossnet(x, kernels, biases, w_head=None, want_x=False):
+    """rsx_crossnet: x [B, D] -> (x_L [B, D] or None, head_part [B] = x_L . w_head or None)."""
+    N.ensure_device(x)
+    x = _c(x)
+    B, D = x.shape
+    x_out = torch.empty(B, D, device=x.device, dtype=torch.float32) if want_x else None
+    part = torch.empty(B, device=x.device, dtype=torch.float32) if w_head is not None else None
+    rc = N.lib().rsx_crossnet(N.ptr(x), x.stride(0), B, D, len(kernels),
+                              N.ptr_array([_c(k.reshape(-1)) for k in kernels]),
+                              N.ptr_array([_c(b.reshape(-1)) for b in biases]),
+                              N.ptr(None if w_head is None else _c(w_head.reshape(-1))), N.ptr(x_out), N.ptr(part),
+                              N.stream())
+    N.check(rc, "crossnet")
+    return x_out, part
+
+
+# ----------------------------------------------------------------------------------------
 # A16: DeepFM forward (inference)
 ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
 

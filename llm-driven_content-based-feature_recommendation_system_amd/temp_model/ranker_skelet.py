@@ -5,6 +5,8 @@ Reference (temp_model/ranker_skelet.py):
   * the neural ranker the north star asks for (DeepFM) does not exist in the reference; it
     is specified by deepctr-torch 0.2.9 (pinned in requirements.txt:41, never imported) and
     lives here as `DeepFM`, with a CatBoost-compatible `predict_proba` wrapper.
+  * CrossNet :239-272 and RankingModel (DCN-V2) :274-357 — dead code in the reference, kept
+    as a second neural reranker with the same parameter names and init.
 Compute: DeepFM forward = rsx_deepfm_embed + rsx_linear_fwd + rsx_linear_dot_fwd; retrieval
 (user_vec @ item_vectors.T -> topk, :193-196) = rsx_retrieve_topk (see ops.retrieve_topk).
 """
@@ -165,3 +167,65 @@ class ReRankingSystem:
         sc_cpu = top_scores[0].cpu().numpy()
         return [{"product_id": int(idx_cpu[o]), "two_tower_score": float(sc_cpu[o]), "final_score": float(probs[o])}
                 for o in order]
+
+
+class CrossNet(nn.Module):
+    """Reference :239-272: x_{l+1} = x_0 * (x_l @ k_l + b_l) + x_l, k_l [D, 1] (xavier normal),
+    b_l [D] (zeros). GPU forward on rsx_crossnet (one wave per row, the row in registers)."""
+
+    def __init__(self, input_dim, num_layers=3):
+        super().__init__()
+        self.num_layers = num_layers
+        self.kernels = nn.ParameterList([nn.Parameter(torch.nn.init.xavier_normal_(torch.empty(input_dim, 1)))
+                                         for _ in range(num_layers)])
+        self.biases = nn.ParameterList([nn.Parameter(torch.zeros(input_dim)) for _ in range(num_layers)])
+
+    @torch.no_grad()
+    def forward(self, x):
+        x_out, _ = ops.crossnet(x, list(self.kernels), list(self.biases), want_x=True)
+        return x_out
+
+
+class RankingModel(nn.Module):
+    """Reference :274-357 (DCN-V2 re-ranker): x = cat(user, item[, context]); cross =
+    CrossNet(x, 3); deep = GELU(LN(Linear(GELU(LN(Linear(x, 256))), 128))); sigmoid(final_head(
+    cat(cross, deep))). Inference on the GPU: the cross network fused with the cross half of
+    final_head (rsx_crossnet: neither cross_out nor the concatenation is materialised), the deep
+    linears on the fp32-MFMA kernel (rsx_linear_fwd) with the LayerNorm+GELU kernel between;
+    dropout is inactive (inference)."""
+
+    def __init__(self, user_dim=128, item_dim=128, context_dim=20):
+        super().__init__()
+        total_input_dim = user_dim + item_dim + context_dim
+        self.cross_net = CrossNet(total_input_dim, num_layers=3)
+        self.deep_net = nn.Sequential(nn.Linear(total_input_dim, 256), nn.LayerNorm(256), nn.GELU(), nn.Dropout(0.2),
+                                      nn.Linear(256, 128), nn.LayerNorm(128), nn.GELU())
+        self.final_head = nn.Linear(total_input_dim + 128, 1)
+
+    @torch.no_grad()
+    def forward(self, user_emb, item_emb, context_emb=None):
+        parts = [user_emb, item_emb] + ([context_emb] if context_emb is not None else [])
+        x = torch.cat(parts, dim=1).float().contiguous()
+        D = x.shape[1]
+        lin1, ln1, lin2, ln2 = self.deep_net[0], self.deep_net[1], self.deep_net[4], self.deep_net[5]
+        if lin1.in_features != D:
+            raise ValueError(f"input width {D} != the model's {lin1.in_features} (context given / omitted?)")
+        wh = self.final_head.weight.reshape(-1)
+        _, head_part = ops.crossnet(x, list(self.cross_net.kernels), list(self.cross_net.biases), w_head=wh[:D])
+        h = ops.layer_norm(ops.linear(x, lin1.weight, lin1.bias), ln1.weight, ln1.bias, ln1.eps,
+                           act=ops.ACT_GELU_ERF)
+        h = ops.layer_norm(ops.linear(h, lin2.weight, lin2.bias), ln2.weight, ln2.bias, ln2.eps,
+                           act=ops.ACT_GELU_ERF)
+        logits = head_part + h @ wh[D:] + self.final_head.bias
+        return torch.sigmoid(logits).unsqueeze(1)
+
+    @torch.no_grad()
+    def predict_for_user(self, user_vec, item_vecs, context_vec=None):
+        """Reference :327-357: one user (and context) broadcast over N candidate items -> [N]."""
+        if user_vec.dim() == 1:
+            user_vec = user_vec.unsqueeze(0)
+        n = item_vecs.size(0)
+        ctx = None
+        if context_vec is not None:
+            ctx = (context_vec.unsqueeze(0) if context_vec.dim() == 1 else context_vec).expand(n, -1)
+        return self.forward(user_vec.expand(n, -1), item_vecs, ctx).squeeze()
