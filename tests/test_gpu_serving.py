@@ -67,3 +67,34 @@ def test_train_item_tower_endpoint(app_client):
     ok = client.post("/ai-api/serving/bg/inference/refresh-item-vectors",
                      params={"save_dir": str(tmp / "m3"), "checkpoint_path": str(tmp / "ckpt" / ck[0])})
     assert ok.status_code == 200, ok.text
+
+
+def test_similarity_endpoint_exact_top50(gpu):
+    """GET /similarity/pgvector/{id} on the GPU index: the 50 nearest other items by exact cosine
+    (the reference asks pgvector's approximate HNSW), in the reference's response shape."""
+    from fastapi import FastAPI
+    from fastapi.testclient import TestClient
+    from recsys_amd.APIController import controller as C
+    g = torch.Generator().manual_seed(5)
+    ids = list(range(1000, 1000 + 3000))
+    vecs = torch.randn(3000, 128, generator=g)
+    C.set_vector_index(C.ItemVectorIndex(ids, vecs, {i: f"cat{i % 7}" for i in ids}, device=gpu))
+    app = FastAPI()
+    app.include_router(C.controller_router, prefix="/ai-api/controller")
+    cl = TestClient(app)
+    try:
+        r = cl.get("/ai-api/controller/similarity/pgvector/1234")
+        assert r.status_code == 200, r.text
+        body = r.json()
+        hits = body["top_5_similar"]
+        assert len(hits) == 50 and body["query_item"] == {"id": 1234, "category": "cat2"}
+        vn = torch.nn.functional.normalize(vecs.double(), dim=1)
+        sim = vn @ vn[234]
+        sim[234] = -2
+        ref = torch.argsort(-sim, stable=True)[:50]
+        assert [h["id"] for h in hits] == [ids[int(i)] for i in ref]
+        assert abs(hits[0]["rank_score"] - round(float(sim[ref[0]]), 4)) < 1e-4
+        assert abs(hits[0]["raw_distance"] - round(1 - float(sim[ref[0]]), 4)) < 1e-4
+        assert cl.get("/ai-api/controller/similarity/pgvector/7").status_code == 404
+    finally:
+        C.set_vector_index(None)

@@ -94,3 +94,26 @@ def test_product_path_refuses_cpu_tensors():
         ops.l2_normalize(torch.randn(3, 128))
     with pytest.raises(RuntimeError, match="ROCm GPU tensor"):
         ops.retrieve_topk(torch.randn(3, 128), torch.randn(10, 128), 2)
+
+
+def test_controller_ingest_and_routes():
+    from fastapi import FastAPI
+    from fastapi.testclient import TestClient
+    from recsys_amd.APIController import controller as C
+    from recsys_amd.utils import dependencies as deps
+    routes = {(r.path, tuple(sorted(r.methods))) for r in C.controller_router.routes}
+    assert ("/products/ingest", ("POST",)) in routes and ("/similarity/pgvector/{item_id}", ("GET",)) in routes
+    store = D.InMemoryProductStore(D.synthetic_product_rows(3))
+    saved = deps.global_product_store
+    deps.set_product_store(store)
+    app = FastAPI()
+    app.include_router(C.controller_router)
+    try:
+        r = TestClient(app).post("/products/ingest", json=[{"product_id": 2, "feature_data": {"a": 1}},
+                                                           {"product_id": 9, "product_name": "x", "feature_data": {}}])
+        assert r.status_code == 200
+        got = {int(x["product_id"]): x for x in store.fetch_products()}
+        assert sorted(got) == [1, 2, 3, 9] and got[2]["feature_data"] == {"a": 1}
+        assert TestClient(app).get("/similarity/pgvector/1").status_code == 404  # no index loaded
+    finally:
+        deps.set_product_store(saved)
