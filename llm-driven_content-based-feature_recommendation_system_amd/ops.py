@@ -1096,6 +1096,33 @@ def retrieve_topk(queries, items, k):
     return sc, ix
 
 
+def hnm_mine(u_norm, i_norm, target_ids, k, hnm_threshold=0.90, temperature=1.0):
+    """Hard-negative mining (v1_refine_usertower.py:641-669, 705-728, 776-790) in one kernel:
+    per row the k largest of (u_norm @ i_norm.T) / temperature with same-target columns and
+    columns whose item-item cosine exceeds hnm_threshold (off the diagonal) set to -inf.
+    Returns (top_idx [N, k] int64, value desc then column asc; top_cos [N, k] raw cosines;
+    avail [N] int32 = columns not ignored). No autograd (the reference mines under no_grad)."""
+    N.ensure_device(u_norm)
+    u = _c(u_norm.detach().to(torch.float32))
+    it = _c(i_norm.detach().to(torch.float32))
+    tg = _c(target_ids.to(torch.int64))
+    n, d = u.shape
+    if it.shape != u.shape or tg.shape != (n,):
+        raise ValueError(f"hnm_mine: shapes {tuple(u.shape)} / {tuple(it.shape)} / {tuple(tg.shape)} disagree")
+    if not 1 <= k <= n:
+        raise ValueError(f"hnm_mine: k={k} out of range for N={n} (torch.topk would fail too)")
+    if n > N.lib().rsx_hnm_max_rows():
+        raise ValueError(f"hnm_mine: N={n} exceeds the LDS-resident row limit {N.lib().rsx_hnm_max_rows()}")
+    idx = torch.empty(n, k, device=u.device, dtype=torch.int64)
+    cos = torch.empty(n, k, device=u.device, dtype=torch.float32)
+    avail = torch.empty(n, device=u.device, dtype=torch.int32)
+    with timed("hnm_mine"):
+        rc = N.lib().rsx_hnm_mine(N.ptr(u), N.ptr(it), N.ptr(tg), n, d, k, float(hnm_threshold), float(temperature),
+                                  N.ptr(idx), N.ptr(cos), N.ptr(avail), N.stream())
+    N.check(rc, "hnm_mine")
+    return idx, cos, avail
+
+
 # ----------------------------------------------------------------------------------------
 # Optional per-op device timing (bench.py): HIP events on the launching (current) stream.
 _TIMING = {"on": False, "events": {}}

@@ -310,34 +310,96 @@ def duorec_loss_refined(user_emb_1, user_emb_2, target_ids, temperature=0.1, lam
     return loss_unsup + lambda_sup * torch.zeros((), device=z_i.device)
 
 
+def _hnm_rows(user_emb, item_tower_emb, target_ids):
+    """u_norm, normalize(item_tower_emb[target_ids]) (reference :642-643, 706-707, 777-778)."""
+    return ops.l2_normalize(user_emb), ops.gather_rows(item_tower_emb, target_ids, normalize=True)
+
+
+def _hnm_logits(u, it, cols, target_ids, log_q_tensor, temperature, lambda_logq):
+    """logits[i, c] = cos(u_i, it_cols[i, c]) / tau - lambda_logq * logQ[target[cols[i, c]]]
+    for a [N, C] column-index table (the reference's torch.gather over the N x N logits,
+    :675-680, 735-741): only the N x C gathered entries are formed, with autograd to u and it."""
+    cos = torch.einsum("nd,ncd->nc", u, it[cols])
+    logits = cos / temperature
+    if lambda_logq > 0.0:
+        logits = logits - log_q_tensor[target_ids][cols] * lambda_logq
+    return logits
+
+
+def inbatch_hnm_corrected_loss_with_stats(user_emb, item_tower_emb, target_ids, log_q_tensor, top_k_percent=0.01,
+                                          hnm_threshold=0.90, temperature=0.1, lambda_logq=0.7, lambda_cl=0.2):
+    """Reference :632-692. Hard negatives mined on the masked cosines / tau by rsx_hnm_mine
+    (no N x N tensors); k = max(1, min(floor((N-1) * top_k_percent), min_i available_i)) —
+    the kernel returns the sorted top floor((N-1) p) and the per-row available counts, so the
+    reference's host sync on available_negs.min() becomes a slice. Loss = CE over
+    [positive, k hard negatives] with the LogQ correction applied after selection.
+    lambda_cl is accepted and unused, as in the reference."""
+    N = user_emb.size(0)
+    device = user_emb.device
+    tgt = target_ids.reshape(-1)
+    u, it = _hnm_rows(user_emb, item_tower_emb, tgt)
+    k_cap = int((N - 1) * top_k_percent)
+    top_idx, top_cos, avail = ops.hnm_mine(u, it, tgt, max(1, min(k_cap, N)), hnm_threshold, temperature)
+    num_k = max(1, min(k_cap, int(avail.min().item())))
+    top_idx, top_cos = top_idx[:, :num_k], top_cos[:, :num_k]
+    diag = torch.arange(N, device=device).unsqueeze(1)
+    final_logits = _hnm_logits(u, it, torch.cat([diag, top_idx], dim=1), tgt, log_q_tensor, temperature,
+                               lambda_logq)
+    loss = F.cross_entropy(final_logits, torch.zeros(N, dtype=torch.long, device=device))
+    return loss, {"avg_hn_similarity": top_cos.mean().item(), "num_active_hard_negs": num_k}
+
+
+def inbatch_mixed_hnm_loss_with_stats(user_emb, item_tower_emb, target_ids, log_q_tensor, top_k_percent=0.01,
+                                      random_sample_size=100, hnm_threshold=0.90, temperature=0.1, lambda_logq=0.7):
+    """Reference :695-757: k = max(1, floor((N-1) p)) mined hard negatives (rsx_hnm_mine) plus
+    random_sample_size uniform column draws per row (torch.randint(0, N, (N, M)) on the same
+    device, so the same generator state draws the same columns), random draws that hit an
+    ignored column (same target, or item cosine > hnm_threshold off the diagonal) get -1e9.
+    Rows with fewer than k available negatives pick -inf-valued columns in ascending index
+    order (torch.topk leaves that order unspecified)."""
+    N = user_emb.size(0)
+    device = user_emb.device
+    tgt = target_ids.reshape(-1)
+    u, it = _hnm_rows(user_emb, item_tower_emb, tgt)
+    num_k = max(1, int((N - 1) * top_k_percent))
+    top_idx, top_cos, _ = ops.hnm_mine(u, it, tgt, num_k, hnm_threshold, temperature)
+    random_indices = torch.randint(0, N, (N, random_sample_size), device=device)
+    diag = torch.arange(N, device=device).unsqueeze(1)
+    cols = torch.cat([diag, top_idx, random_indices], dim=1)
+    final_logits = _hnm_logits(u, it, cols, tgt, log_q_tensor, temperature, lambda_logq)
+    with torch.no_grad():
+        item_sim = torch.einsum("nd,nmd->nm", it, it[random_indices])
+        random_mask = (tgt[random_indices] == tgt.unsqueeze(1)) | ((item_sim > hnm_threshold) & (random_indices != diag))
+        fill = torch.zeros_like(final_logits, dtype=torch.bool)
+        fill[:, 1 + num_k:] = random_mask
+    final_logits = final_logits.masked_fill(fill, -1e9)
+    loss = F.cross_entropy(final_logits, torch.zeros(N, dtype=torch.long, device=device))
+    return loss, {"avg_hn_similarity": top_cos.mean().item(), "num_hard": num_k, "num_random": random_sample_size}
+
+
 def full_batch_hard_emphasis_loss(user_emb, item_tower_emb, target_ids, log_q_tensor, top_k_percent=0.01,
                                   hard_margin=0.2, hnm_threshold=0.90, temperature=0.1, lambda_logq=1.0):
     """Reference :762-822 (the loss of train_user_tower, v1_usertower_train.py:459-469).
     N x N over the batch (N <= a few thousand last-step rows): cosine logits, ignore mask
     (same item, or item-item cosine > hnm_threshold off the diagonal), top-k hard negatives
     (k = max(1, floor((N-1) * top_k_percent))) mined on the masked cosines get +margin/tau,
-    same-item off-diagonal columns -> -inf, CE against the diagonal. The column rows are
-    gathered + L2-normalised by rsx_gather_rows; the N x N products and top-k are PyTorch
-    (hipBLASLt / rocPRIM) — this is the secondary (resume) path, not the step's hot loop.
+    same-item off-diagonal columns -> -inf, CE against the diagonal. Column rows are gathered +
+    L2-normalised by rsx_gather_rows and the mining (both products, mask, top-k) is the fused
+    rsx_hnm_mine kernel; the N x N logits for the full-batch CE are one GEMM.
     Returns (loss, {"avg_hn_similarity", "num_hard"})."""
     N = user_emb.size(0)
     device = user_emb.device
-    u = ops.l2_normalize(user_emb)
-    it = ops.gather_rows(item_tower_emb, target_ids, normalize=True)
+    tgt = target_ids.reshape(-1)
+    u, it = _hnm_rows(user_emb, item_tower_emb, tgt)
+    num_k = max(1, int((N - 1) * top_k_percent))
+    top_idx, top_cos, _ = ops.hnm_mine(u, it, tgt, num_k, hnm_threshold, 1.0)
     cos = u @ it.T
-    same = target_ids.unsqueeze(1) == target_ids.unsqueeze(0)
+    same = tgt.unsqueeze(1) == tgt.unsqueeze(0)
     diag = torch.eye(N, dtype=torch.bool, device=device)
-    with torch.no_grad():
-        ignore = same | (((it @ it.T) > hnm_threshold) & ~diag)
-        mining = cos.detach().masked_fill(ignore, float("-inf"))
-        num_k = max(1, int((N - 1) * top_k_percent))
-        _, top_idx = torch.topk(mining, k=num_k, dim=1)
     logits = cos / temperature
     if lambda_logq > 0.0:
-        logits = logits - log_q_tensor[target_ids].view(1, -1) * lambda_logq
+        logits = logits - log_q_tensor[tgt].view(1, -1) * lambda_logq
     emphasis = torch.zeros_like(logits).scatter_(1, top_idx, hard_margin / temperature)
     logits = (logits + emphasis).masked_fill(same & ~diag, float("-inf"))
     loss = F.cross_entropy(logits, torch.arange(N, device=device))
-    with torch.no_grad():
-        avg_hn = torch.gather(cos, 1, top_idx).mean().item()
-    return loss, {"avg_hn_similarity": avg_hn, "num_hard": num_k}
+    return loss, {"avg_hn_similarity": top_cos.mean().item(), "num_hard": num_k}

@@ -14,8 +14,9 @@ import torch
 import torch.nn as nn
 
 from .. import ops
-from .v1_refine_usertower import (PackedTokens, SASRecUserTower, duorec_loss_refined, full_batch_hard_emphasis_loss,
-                                  inbatch_corrected_logq_loss)
+from .v1_refine_usertower import (PackedTokens, SASRecUserTower, duorec_loss_refined, full_batch_hard_emphasis_loss,  # noqa: F401
+                                  inbatch_corrected_logq_loss, inbatch_hnm_corrected_loss_with_stats,
+                                  inbatch_mixed_hnm_loss_with_stats)
 
 try:  # the reference hard-imports wandb (v1_usertower_train.py:14); here it is optional
     import wandb  # type: ignore

@@ -270,3 +270,76 @@ def full_batch_hard_emphasis_loss(user_emb, item_tower_emb, target_ids, log_q_te
     loss = F.cross_entropy(logits, torch.arange(N))
     avg = torch.gather(cos_sim, 1, top_k_indices).mean().item()
     return loss, {"avg_hn_similarity": avg, "num_hard": num_k}
+
+
+def inbatch_hnm_corrected_loss_with_stats(user_emb, item_tower_emb, target_ids, log_q_tensor, top_k_percent=0.01,
+                                          hnm_threshold=0.90, temperature=0.1, lambda_logq=0.7, lambda_cl=0.2):
+    """v1_refine_usertower.py:632-692, restated (CPU fp32)."""
+    N = user_emb.size(0)
+    u_norm = F.normalize(user_emb, p=2, dim=1)
+    i_norm = F.normalize(item_tower_emb[target_ids], p=2, dim=1)
+    cos_sim = u_norm @ i_norm.T
+    same = target_ids.unsqueeze(1) == target_ids.unsqueeze(0)
+    diag = torch.eye(N, dtype=torch.bool)
+    with torch.no_grad():
+        too_similar = (i_norm @ i_norm.T > hnm_threshold) & ~diag
+    ignore = same | too_similar
+    mining = (cos_sim / temperature).detach().clone().masked_fill_(ignore, float("-inf"))
+    available = (~ignore).sum(dim=1)
+    num_k = max(1, min(int((N - 1) * top_k_percent), available.min().item()))
+    _, top_k_indices = torch.topk(mining, k=num_k, dim=1)
+    logits = cos_sim / temperature
+    if lambda_logq > 0.0:
+        logits = logits - log_q_tensor[target_ids].view(1, -1) * lambda_logq
+    final = torch.cat([torch.diagonal(logits).unsqueeze(1), torch.gather(logits, 1, top_k_indices)], dim=1)
+    loss = F.cross_entropy(final, torch.zeros(N, dtype=torch.long))
+    with torch.no_grad():
+        avg = torch.gather(cos_sim, 1, top_k_indices).mean().item()
+    return loss, {"avg_hn_similarity": avg, "num_active_hard_negs": num_k}
+
+
+def inbatch_mixed_hnm_loss_with_stats(user_emb, item_tower_emb, target_ids, log_q_tensor, top_k_percent=0.01,
+                                      random_sample_size=100, hnm_threshold=0.90, temperature=0.1, lambda_logq=0.7,
+                                      random_indices=None):
+    """v1_refine_usertower.py:695-757, restated (CPU fp32). random_indices: the [N, M] draws of
+    :730 (the reference draws them with torch.randint on its device; tests replay the GPU
+    draw and pass it here)."""
+    N = user_emb.size(0)
+    u_norm = F.normalize(user_emb, p=2, dim=1)
+    i_norm = F.normalize(item_tower_emb[target_ids], p=2, dim=1)
+    cos_sim = u_norm @ i_norm.T
+    same = target_ids.unsqueeze(1) == target_ids.unsqueeze(0)
+    diag = torch.eye(N, dtype=torch.bool)
+    with torch.no_grad():
+        too_similar = (i_norm @ i_norm.T > hnm_threshold) & ~diag
+    ignore = same | too_similar
+    mining = (cos_sim / temperature).detach().clone().masked_fill_(ignore, float("-inf"))
+    num_k = max(1, int((N - 1) * top_k_percent))
+    _, top_k_indices = torch.topk(mining, k=num_k, dim=1)
+    if random_indices is None:
+        random_indices = torch.randint(0, N, (N, random_sample_size))
+    logits = cos_sim / temperature
+    if lambda_logq > 0.0:
+        logits = logits - log_q_tensor[target_ids].view(1, -1) * lambda_logq
+    pos = torch.diagonal(logits).unsqueeze(1)
+    hard = torch.gather(logits, 1, top_k_indices)
+    rnd = torch.gather(logits, 1, random_indices).masked_fill(torch.gather(ignore, 1, random_indices), -1e9)
+    loss = F.cross_entropy(torch.cat([pos, hard, rnd], dim=1), torch.zeros(N, dtype=torch.long))
+    with torch.no_grad():
+        avg = torch.gather(cos_sim, 1, top_k_indices).mean().item()
+    return loss, {"avg_hn_similarity": avg, "num_hard": num_k, "num_random": random_sample_size}
+
+
+def hnm_mine(u_norm, i_norm, target_ids, k, hnm_threshold=0.90, temperature=1.0):
+    """The mining step shared by :641-669, :705-728, :776-790 in float64, with the total order
+    the kernel promises (mining value desc, then column index asc): (top_idx, avail)."""
+    u = u_norm.double()
+    it = i_norm.double()
+    N = u.shape[0]
+    same = target_ids.unsqueeze(1) == target_ids.unsqueeze(0)
+    diag = torch.eye(N, dtype=torch.bool)
+    ignore = same | ((it @ it.T > hnm_threshold) & ~diag)
+    mining = (u @ it.T / temperature).masked_fill(ignore, float("-inf"))
+    # a stable descending sort keeps equal values in ascending column order
+    order = torch.argsort(mining, dim=1, descending=True, stable=True)
+    return order[:, :k], (~ignore).sum(dim=1)

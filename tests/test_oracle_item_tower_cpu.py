@@ -1,6 +1,7 @@
 """CPU checks of the item-tower oracle (test infrastructure): shapes, normalisation, the
 SimCSE loss identity on a symmetric case, and the hard-emphasis loss's mining count."""
 import torch
+import torch.nn.functional as F
 
 from oracle import item_tower as OIT
 from oracle import user_tower as O
@@ -57,3 +58,28 @@ def test_feature_processor_logq():
     exp = synth.logq_from_probs(probs)
     assert torch.equal(lq, exp)
     assert fp.item2id[13] == 3 and lq[0].item() == -20.0
+
+
+def test_oracle_hnm_losses_num_k_and_mining():
+    """inbatch_hnm_corrected (:632-692): k is capped by the fewest available negatives; both HNM
+    losses mine the same columns as the ordered hnm_mine restatement the kernel is checked on."""
+    g = torch.Generator().manual_seed(5)
+    N = 60
+    u = torch.randn(N, 128, generator=g)
+    w = torch.randn(40, 128, generator=g)
+    t = torch.randint(1, 40, (N,), generator=g)
+    t[:55] = 7  # row 0 has only 5 targets that differ from its own
+    loss, st = O.inbatch_hnm_corrected_loss_with_stats(u, w, t, torch.zeros(40), top_k_percent=0.5)
+    assert st["num_active_hard_negs"] == 5 and torch.isfinite(loss)
+    un = F.normalize(u, dim=1)
+    itn = F.normalize(w[t], dim=1)
+    idx, avail = O.hnm_mine(un, itn, t, 5, 0.9, 0.1)
+    assert int(avail.min()) == 5
+    cos = un @ itn.T
+    expect = torch.gather(cos, 1, idx).mean().item()
+    assert abs(st["avg_hn_similarity"] - expect) < 1e-6
+    ri = torch.randint(0, N, (N, 7), generator=g)
+    loss2, st2 = O.inbatch_mixed_hnm_loss_with_stats(u, w, t, torch.zeros(40), top_k_percent=0.05,
+                                                      random_sample_size=7, random_indices=ri)
+    assert st2 == {"avg_hn_similarity": st2["avg_hn_similarity"], "num_hard": 2, "num_random": 7}
+    assert torch.isfinite(loss2)
