@@ -310,18 +310,22 @@ int rsx_segment_sum_rows(const float* src, int64_t ld_src, const int64_t* perm, 
                          const int64_t* rows, int64_t nseg, int64_t D, const float* scale, int64_t skip_row,
                          float* dst, int64_t ld_dst, int accumulate, void* stream);
 
-/* Hard-negative mining, one fused kernel: for each row i of u_norm [N,D]
- * against the columns i_norm [N,D] (both already L2-normalised), ignore column j when
- * target_ids[j] == target_ids[i] or (i_norm[i].i_norm[j] > hnm_threshold and j != i); mining
- * value = (u_norm[i].i_norm[j]) / temperature (-inf when ignored). Writes the k largest per row
- * (value desc, column asc) as top_idx [N,k] int64 with their raw cosines top_cos [N,k], and
- * avail [N] int32 = number of columns not ignored. Replaces the N x N cos / item_sim / mask
- * tensors and torch.topk of v1_refine_usertower.py:641-669 (inbatch_hnm_corrected_loss_with_stats),
- * :705-728 (inbatch_mixed_hnm_loss_with_stats), :776-790 (full_batch_hard_emphasis_loss).
+/* Hard-negative mining: for each row i of u_norm [N,D] against the columns
+ * i_norm [N,D] (both already L2-normalised), ignore column j when target_ids[j] ==
+ * target_ids[i] or (i_norm[i].i_norm[j] > hnm_threshold and j != i); mining value =
+ * (u_norm[i].i_norm[j]) / temperature (-inf when ignored). Writes the k largest per row (value
+ * desc, column asc) as top_idx [N,k] int64 with their raw cosines top_cos [N,k], and avail [N]
+ * int32 = number of columns not ignored. Two kernels: both products on the fp32 MFMA with the
+ * mask applied in registers -> ONE masked N x ld fp32 workspace (ws, 16-B aligned,
+ * >= rsx_hnm_workspace_bytes(N)) -> per-row radix select + sort in LDS. Replaces the N x N
+ * cos / item_sim / mask tensors and torch.topk of v1_refine_usertower.py:641-669
+ * (inbatch_hnm_corrected_loss_with_stats), :705-728 (inbatch_mixed_hnm_loss_with_stats),
+ * :776-790 (full_batch_hard_emphasis_loss).
  * D in {64,128}; 1 <= k <= min(N, 4096); N <= rsx_hnm_max_rows() (one row's values live in LDS). */
 int rsx_hnm_mine(const float* u_norm, const float* i_norm, const int64_t* target_ids, int64_t N, int64_t D,
-                 int64_t k, float hnm_threshold, float temperature, int64_t* top_idx, float* top_cos,
-                 int32_t* avail, void* stream);
+                 int64_t k, float hnm_threshold, float temperature, void* ws, size_t ws_bytes, int64_t* top_idx,
+                 float* top_cos, int32_t* avail, void* stream);
+int64_t rsx_hnm_workspace_bytes(int64_t N);
 int64_t rsx_hnm_max_rows(void);
 
 #ifdef __cplusplus

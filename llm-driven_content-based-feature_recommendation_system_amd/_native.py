@@ -78,7 +78,8 @@ _SIGS = {
     "rsx_crossnet": (c_i, [c_p, c_i64, c_i64, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p]),
     "rsx_segment_sum_rows": (c_i, [c_p, c_i64, c_p, c_p, c_p, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_i, c_p]),
     "rsx_scatter_rows": (c_i, [c_p, c_p, c_p, c_p, c_i64, c_i64, c_i, c_f, c_i, c_i64, c_p, c_i64, c_p]),
-    "rsx_hnm_mine": (c_i, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_f, c_f, c_p, c_p, c_p, c_p]),
+    "rsx_hnm_mine": (c_i, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_f, c_f, c_p, ctypes.c_size_t, c_p, c_p, c_p, c_p]),
+    "rsx_hnm_workspace_bytes": (c_i64, [c_i64]),
     "rsx_hnm_max_rows": (c_i64, []),
 }
 

@@ -1116,9 +1116,11 @@ def hnm_mine(u_norm, i_norm, target_ids, k, hnm_threshold=0.90, temperature=1.0)
     idx = torch.empty(n, k, device=u.device, dtype=torch.int64)
     cos = torch.empty(n, k, device=u.device, dtype=torch.float32)
     avail = torch.empty(n, device=u.device, dtype=torch.int32)
+    nws = N.lib().rsx_hnm_workspace_bytes(n)
+    ws = torch.empty(nws, device=u.device, dtype=torch.uint8)
     with timed("hnm_mine"):
         rc = N.lib().rsx_hnm_mine(N.ptr(u), N.ptr(it), N.ptr(tg), n, d, k, float(hnm_threshold), float(temperature),
-                                  N.ptr(idx), N.ptr(cos), N.ptr(avail), N.stream())
+                                  N.ptr(ws), nws, N.ptr(idx), N.ptr(cos), N.ptr(avail), N.stream())
     N.check(rc, "hnm_mine")
     return idx, cos, avail
 

@@ -132,3 +132,21 @@ def test_mixed_hnm_loss_parity(gpu, N, M):
     assert abs(s_dut["avg_hn_similarity"] - s_ref["avg_hn_similarity"]) < 1e-5
     torch.testing.assert_close(u2.grad.cpu(), u1.grad, atol=1e-6, rtol=1e-4)
     torch.testing.assert_close(w2.grad.cpu(), w1.grad, atol=1e-6, rtol=1e-4)
+
+
+@pytest.mark.parametrize("N,k,levels", [(3000, 100, 2), (2000, 37, 1), (5000, 1000, 3)])
+def test_hnm_mine_massive_ties(gpu, N, k, levels):
+    """Few distinct products: the boundary bin overflows the sort buffer (or min == max), so the
+    exact radix-select path runs; ties must resolve to the lowest columns exactly."""
+    g = torch.Generator().manual_seed(N)
+    u = torch.zeros(N, 128)
+    u[:, 0] = 1.0
+    it = torch.zeros(N, 128)
+    it[:, 0] = torch.randint(0, levels, (N,), generator=g).float() + 1.0
+    it[:, 1 + torch.arange(N) % 100] = 0.5  # off-axis part: item-item products vary, none > thr
+    t = torch.arange(N)  # distinct targets: only the diagonal is ignored (same target)
+    idx, cos, avail = ops.hnm_mine(u.to(gpu), it.to(gpu), t.to(gpu), k, 1e9, 1.0)
+    r_idx, r_avail = O.hnm_mine(u, it, t, k, 1e9, 1.0)
+    assert torch.equal(avail.cpu().long(), r_avail)
+    assert torch.equal(idx.cpu(), r_idx)
+    assert torch.equal(cos.cpu(), (u.double() @ it.double().T).gather(1, r_idx).float())

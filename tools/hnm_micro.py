@@ -6,7 +6,7 @@ import sys
 import torch
 import torch.nn.functional as F
 
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 import recsys_amd  # noqa: F401,E402
 from recsys_amd import ops  # noqa: E402
 
