@@ -248,6 +248,50 @@ def bench_dcn(args, device):
             "data": "synthetic normalised vectors, random-init model"}
 
 
+def bench_hnm(args, device):
+    """Hard-negative-mined LogQ loss (inbatch_hnm_corrected_loss_with_stats,
+    tower_code/v1_refine_usertower.py:632-692) forward + backward over
+    N = 4,096 user rows (one per user of the configs[1] batch), d = 128, 47,063-item table.
+    rows/s; the mining kernels (products on the fp32 MFMA + select) timed separately."""
+    from recsys_amd import ops
+    from recsys_amd.tower_code import v1_refine_usertower as T
+    N, I = 4096, 47063
+    g = torch.Generator(device="cpu").manual_seed(17)
+    W = torch.nn.functional.normalize(torch.randn(I, 128, generator=g), dim=1).to(device).requires_grad_()
+    lq = torch.log_softmax(torch.randn(I, generator=g), 0).to(device)
+    t = torch.randint(1, I, (N,), generator=g).to(device)
+    U = torch.randn(N, 128, generator=g).to(device).requires_grad_()
+
+    def step():
+        loss, _ = T.inbatch_hnm_corrected_loss_with_stats(U, W, t, lq)
+        loss.backward()
+
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    iters = 20
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        step()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / iters
+    un = torch.nn.functional.normalize(U.detach(), dim=1)
+    itn = torch.nn.functional.normalize(W.detach()[t], dim=1)
+    k = int((N - 1) * 0.01)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        ops.hnm_mine(un, itn, t, k, 0.9, 0.1)
+    b.record()
+    torch.cuda.synchronize()
+    mine_ms = a.elapsed_time(b) / iters
+    return {"metric": "HNM LogQ loss fwd+bwd rows/sec (inbatch_hnm_corrected_loss_with_stats, N=4096, d=128)",
+            "value": round(N / dt, 1), "unit": "rows/s", "ms_per_step": round(dt * 1e3, 4),
+            "mining_ms": round(mine_ms, 4), "k": k,
+            "mining_tflops_fp32": round(4.0 * N * N * 128 / mine_ms / 1e9, 2),
+            "data": "synthetic normalised item table, Gaussian user rows, uniform targets"}
+
+
 def bench_item_refresh(args, device):
     """refresh-item-vectors (utils/inference_utils.py:74-207) on one GPU: the
     endpoint's eval forward over batches of 4 x 192 = 768 products, d = 128 (the serving
@@ -531,6 +575,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_item_tower:
         result["secondary_item_tower"] = bench_item_tower(args, device)
         result["secondary_item_refresh"] = bench_item_refresh(args, device)
+        result["secondary_hnm"] = bench_hnm(args, device)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, items, cfg)
     if rank == 0:
