@@ -137,3 +137,28 @@ def _packed_vs_dense(gpu, atol, rtol):
     pk, o1, _ = TT.packed_views(dut, bd, pretrained_vecs=pv)
     assert (pk.tok_pad == 1).sum() > 0  # some users' last index falls on padding
     torch.testing.assert_close(o1, dense.reshape(-1, dense.shape[-1])[pk.flat], atol=atol, rtol=rtol)
+
+
+def test_gated_off_tables_still_decay(gpu):
+    """Appendix B trap 4: s_mask zeroes the gates of the type/color/graphic/section tables
+    (v1_refine_usertower.py:437-438), but the reference still gathers them, so their gradients
+    are zero TENSORS (not None) and AdamW's decoupled weight decay shrinks them every step:
+    p <- p * (1 - lr * wd) exactly (the Adam update of a zero gradient is 0)."""
+    cfg = small_cfg(num_items=500, dropout=0.0)
+    items = small_universe(500)
+    batch = to_dev(synth.make_batch(items, 32, seed=3), gpu)
+    torch.manual_seed(0)
+    model = T.SASRecUserTower(cfg).to(gpu)
+    item_tower = TT.SASRecItemTower(500, 128, items.log_q.clone()).to(gpu)
+    item_tower.init_from_pretrained(items.pretrained.to(gpu))
+    opt = torch.optim.AdamW(model.parameters(), lr=cfg.lr, weight_decay=cfg.weight_decay)
+    names = ["type_emb.weight", "color_emb.weight", "graphic_emb.weight", "section_emb.weight"]
+    params = dict(model.named_parameters())
+    before = {n: params[n].detach().clone() for n in names}
+    TT.contrastive_step(model, item_tower, item_tower.log_q, batch, opt, None, cfg,
+                        pretrained_lookup=items.pretrained.to(gpu))
+    for n in names:
+        g = params[n].grad
+        assert g is not None and torch.count_nonzero(g) == 0, n
+        torch.testing.assert_close(params[n].detach(), before[n] * (1 - cfg.lr * cfg.weight_decay),
+                                   atol=0, rtol=1e-6)
