@@ -194,6 +194,28 @@ def retrieval_fixture():
            "items": "in.items_x16 / 16"})
 
 
+def hnm_fixture():
+    """Hard-negative mining (v1_refine_usertower.py:641-669, 705-728, 776-790) on integer inputs
+    (every product exact in fp32): duplicated item rows give exact ties and item-similarity hits,
+    repeated targets give same-item masks; expected (value desc, column asc) top-k and the
+    available counts, plus the inbatch_hnm_corrected loss on the normalised rows."""
+    g = torch.Generator().manual_seed(71)
+    N, D, k, thr = 600, 128, 12, 30.0
+    u = torch.randint(-2, 3, (N, D), generator=g).to(torch.int8)
+    it = torch.randint(-2, 3, (N, D), generator=g).to(torch.int8)
+    it[1::5] = it[0::5]
+    tgt = torch.randint(1, 150, (N,), generator=g)
+    idx, avail = O.hnm_mine(u.float(), it.float(), tgt, k, thr, 1.0)
+    W = torch.randn(150, D, generator=g)
+    lq = torch.log_softmax(torch.randn(150, generator=g), 0)
+    U = torch.randn(N, D, generator=g)
+    loss, st = O.inbatch_hnm_corrected_loss_with_stats(U, W, tgt, lq, top_k_percent=0.02)
+    _save("hnm_n600", {"in.u": u, "in.items": it, "in.target_ids": tgt, "out.top_idx": idx, "out.avail": avail,
+                       "in.user": U, "in.table": W, "in.log_q": lq, "out.loss": loss.detach().reshape(1)},
+          {"k": k, "hnm_threshold": thr, "temperature_mining": 1.0, "order": "value desc, column asc",
+           "loss_top_k_percent": 0.02, "num_active_hard_negs": st["num_active_hard_negs"]})
+
+
 def main():
     torch.set_num_threads(1)
     user_tower_fixture()
@@ -202,6 +224,7 @@ def main():
     simcse_fixture()
     deepfm_fixture()
     retrieval_fixture()
+    hnm_fixture()
 
 
 if __name__ == "__main__":

@@ -226,3 +226,34 @@ def test_golden_gpu_retrieval_bit_exact(gpu, k):
     sc, idx = ops.retrieve_topk(q, it, k)
     assert torch.equal(idx.cpu(), t["out.index"][:, :k])       # bit-exact indices, ties by index
     assert torch.equal(sc.cpu().double(), t["out.scores"][:, :k])
+
+
+def test_golden_oracle_hnm():
+    """The HNM golden re-derived by the oracle (mining order and counts exact; loss 1e-6)."""
+    from oracle import user_tower as OU
+    t, meta = load("hnm_n600")
+    idx, avail = OU.hnm_mine(t["in.u"].float(), t["in.items"].float(), t["in.target_ids"], meta["k"],
+                             meta["hnm_threshold"], meta["temperature_mining"])
+    assert torch.equal(idx, t["out.top_idx"]) and torch.equal(avail, t["out.avail"])
+    loss, st = OU.inbatch_hnm_corrected_loss_with_stats(t["in.user"], t["in.table"], t["in.target_ids"],
+                                                        t["in.log_q"], top_k_percent=meta["loss_top_k_percent"])
+    assert st["num_active_hard_negs"] == meta["num_active_hard_negs"]
+    torch.testing.assert_close(loss.reshape(1), t["out.loss"], atol=1e-6, rtol=1e-6)
+
+
+@pytest.mark.gpu
+def test_golden_gpu_hnm(gpu):
+    """rsx_hnm_mine bit-exact on the golden's integer inputs; the HNM loss within 1e-5."""
+    from recsys_amd import ops
+    from recsys_amd.tower_code import v1_refine_usertower as T
+    t, meta = load("hnm_n600")
+    idx, cos, avail = ops.hnm_mine(t["in.u"].float().to(gpu), t["in.items"].float().to(gpu),
+                                   t["in.target_ids"].to(gpu), meta["k"], meta["hnm_threshold"],
+                                   meta["temperature_mining"])
+    assert torch.equal(idx.cpu(), t["out.top_idx"])
+    assert torch.equal(avail.cpu().long(), t["out.avail"])
+    loss, st = T.inbatch_hnm_corrected_loss_with_stats(t["in.user"].to(gpu), t["in.table"].to(gpu),
+                                                       t["in.target_ids"].to(gpu), t["in.log_q"].to(gpu),
+                                                       top_k_percent=meta["loss_top_k_percent"])
+    assert st["num_active_hard_negs"] == meta["num_active_hard_negs"]
+    assert abs(loss.item() - t["out.loss"].item()) <= 1e-5 * abs(t["out.loss"].item())
