@@ -1,18 +1,22 @@
 #!/usr/bin/env python
-"""Headline benchmark: SimCSE/DuoRec contrastive train step of the user tower (BASELINE.json
-configs[1]: two-tower forward + in-batch contrastive loss, batch 4096, d=128, 1 x MI355X).
+"""Headline benchmark: SimCSE/DuoRec contrastive train step of the user tower at the batch
+BASELINE.json's metric names ("SimCSE train-step pairs/sec at d=128, batch 8192"), 1 x MI355X.
 
 A step = one full training step of tower_code/v1_usertower_train.py:717-893 on one global
 batch of synthetic H&M-shaped users: two dropout views (p=0.2) of SASRecUserTower, the
-all-time-steps LogQ in-batch loss (N ~ 75.7k valid positions, N x N implicit logits), DuoRec
-(InfoNCE + SupCon), backward, clip_grad_norm_(5.0), AdamW (item matrix unfrozen, lr x 0.05:
-the reference's epoch >= 2 steady state). Inputs are resident in HBM before timing.
+all-time-steps LogQ in-batch loss (N ~ 153k valid positions at 8192 users, N x N implicit
+logits), DuoRec (InfoNCE + SupCon), backward, clip_grad_norm_(5.0), AdamW (item matrix
+unfrozen, lr x 0.05: the reference's epoch >= 2 steady state). Inputs are resident in HBM
+before timing. Secondary lines: batch 4096 (configs[1]), the fp32 parity mode, batch 32768 on
+one GPU, DeepFM (configs[2]), retrieve->rerank (configs[4] on one GPU), the item tower
+(configs[0] shape), HNM; the CPU oracle on the headline's own batch (cpu_baseline).
 
-Multi-GPU (torchrun, one process per GPU, RCCL): by default every GPU holds 4096 users, so the
-global batch is 4096 x N (weak scaling; N=8 is configs[3], global batch 32 768 with the
-all-gathered negative pool). ``--batch G`` fixes the global batch instead (strong scaling; the
-N=1 run at G=32768 is the single-GPU end of configs[3]). Users are split by rank; see dist.py.
-Prints ONE JSON line on rank 0.
+Multi-GPU (one process per GPU, RCCL): ``--gpus N`` without torchrun's environment starts
+``torch.distributed.run --nproc-per-node N`` as a child process (this parent never touches
+the GPU); under torchrun each rank holds 8192 users by default, so the global batch is
+8192 x N (weak scaling; N=4 is configs[3]'s global batch 32768, negatives all-gathered).
+``--batch G`` fixes the global batch instead (strong scaling). Users are split by rank; see
+dist.py. Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
@@ -37,26 +41,34 @@ HBM_PEAK_GBS = 8000.0
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one process per GPU, RCCL). Without torchrun's env this process starts "
+                         "`torch.distributed.run --nproc-per-node N` as a child and exits with its code")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=None,
                     help="fixed global batch (users) for every N: strong scaling. Default: --batch-per-gpu x N")
-    ap.add_argument("--batch-per-gpu", type=int, default=4096,
-                    help="users per GPU when --batch is not given (weak scaling; N=8 -> 32768 = configs[3])")
+    ap.add_argument("--batch-per-gpu", type=int, default=8192,
+                    help="users per GPU when --batch is not given (weak scaling). N=1: the 8192-user batch "
+                         "BASELINE.json's metric names; N=4: configs[3]'s global batch 32768")
     ap.add_argument("--items", type=int, default=47_062)
     ap.add_argument("--dropout", type=float, default=0.2)
     ap.add_argument("--freeze-items", action="store_true", help="epoch-1 regime (item matrix frozen)")
-    ap.add_argument("--cpu-sample-batch", type=int, default=384)
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-loss-chunk", type=int, default=64,
+                    help="row chunk of the CPU oracle's N x N main loss (same arithmetic, bounded RAM)")
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="CPU baseline threads (capped at the physical cores; 16 = one GPU's CPU share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--no-batch8192", action="store_true",
-                    help="skip the secondary line at global batch 8192 (the batch BASELINE.json's metric names)")
-    ap.add_argument("--steps8192", type=int, default=5)
+    ap.add_argument("--no-batch4096", action="store_true",
+                    help="skip the secondary line at global batch 4096 (BASELINE configs[1])")
+    ap.add_argument("--steps4096", type=int, default=10)
     ap.add_argument("--no-batch32768", action="store_true",
                     help="skip the N=1 run of configs[3]'s global batch 32768 (the strong-scaling baseline)")
     ap.add_argument("--steps32768", type=int, default=3)
+    ap.add_argument("--no-fp32-line", action="store_true",
+                    help="skip the secondary line in the fp32 parity mode (fp32 MFMA loss, fp32 GEMMs/attention)")
+    ap.add_argument("--steps-fp32", type=int, default=3)
     ap.add_argument("--no-deepfm", action="store_true", help="skip the DeepFM rerank secondary metric")
     ap.add_argument("--deepfm-rows", type=int, default=65536)
     ap.add_argument("--deepfm-vocab", type=int, default=1_000_000)
@@ -70,46 +82,122 @@ def parse():
     ap.add_argument("--unfused-adamw", action="store_true", help="torch's foreach AdamW instead of fused")
     ap.add_argument("--blas", default="default", choices=["default", "hipblaslt", "rocblas", "ck"],
                     help="library torch uses for the tower's dense projections")
+    ap.add_argument("--master-port", type=int, default=29531, help="rendezvous port when spawning ranks")
     return ap.parse_args()
+
+
+def launch_ranks(args) -> int:
+    """--gpus N > 1 without torchrun's environment: start torchrun as a CHILD process (one rank per
+    GPU, rendezvous on 127.0.0.1) and return its exit code. This parent never touches the GPU."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={args.master_port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group(backend="nccl", init_method="env://", rank=rank, world_size=world,
                                 device_id=torch.device("cuda", local))
+        assert dist.get_world_size() == args.gpus
     else:
         torch.cuda.set_device(0)
     return rank, world, torch.device("cuda", local if world > 1 else 0)
 
 
-def cpu_baseline(args, items, cfg):
-    """The oracle (CPU PyTorch fp32 restatement of the reference step) on a bounded sample."""
+def host_cpu_info():
+    """os.cpu_count(), the lscpu model name and the physical core count of this host."""
+    info = {"os_cpu_count": os.cpu_count(), "model": None, "physical_cores": None}
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        kv = {}
+        for line in out.splitlines():
+            if ":" in line:
+                k, v = line.split(":", 1)
+                kv[k.strip()] = v.strip()
+        info["model"] = kv.get("Model name")
+        cps, sock = kv.get("Core(s) per socket"), kv.get("Socket(s)")
+        if cps and sock and cps.isdigit() and sock.isdigit():
+            info["physical_cores"] = int(cps) * int(sock)
+    except (OSError, ValueError):
+        pass
+    try:
+        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        pass
+    return info
+
+
+class _Heartbeat:
+    """Prints a progress line to stderr every `every` seconds while a long host-only phase runs
+    (the GPU box takes a command that is silent for minutes to be hung)."""
+
+    def __init__(self, what, every=20.0):
+        import threading
+        self.what, self.every, self.t0 = what, every, time.perf_counter()
+        self.stop = threading.Event()
+        self.th = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        while not self.stop.wait(self.every):
+            print(f"[bench] {self.what}: {time.perf_counter() - self.t0:.0f} s", file=sys.stderr, flush=True)
+
+    def __enter__(self):
+        self.th.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.stop.set()
+        self.th.join()
+        return False
+
+
+def cpu_baseline(args, items, cfg, batch_size, batch_seed):
+    """The oracle (CPU PyTorch fp32 restatement of tower_code/v1_usertower_train.py:717-893) on
+    the SAME global batch the GPU headline runs (same generator, same seed): one timed step
+    after a small warm-up step; the main loss row-chunked (same arithmetic, bounded RAM)."""
     from oracle import user_tower as O
     from recsys_amd import synth
+    info = host_cpu_info()
+    phys = info.get("physical_cores") or os.cpu_count() or 1
+    avail = info.get("affinity_cpus") or phys
+    threads = max(1, min(args.cpu_threads, phys, avail))
+    prev_threads = torch.get_num_threads()
+    torch.set_num_threads(threads)
     torch.manual_seed(args.seed)
     model = O.OracleUserTower(cfg)
     model.train()
     W = torch.nn.Parameter(items.pretrained.clone())
     opt = torch.optim.AdamW(model.parameters(), lr=cfg.lr, weight_decay=cfg.weight_decay)
     opt.add_param_group({"params": [W], "lr": cfg.lr * 0.05})
-    batch = synth.make_batch(items, args.cpu_sample_batch, seed=args.seed + 7)
-    O.contrastive_step(model, W, items.log_q, batch, opt, items.pretrained)  # warm-up
-    t0 = time.perf_counter()
-    for _ in range(args.cpu_steps):
-        O.contrastive_step(model, W, items.log_q, batch, opt, items.pretrained)
-    dt = (time.perf_counter() - t0) / args.cpu_steps
+    warm = synth.make_batch(items, 64, seed=args.seed + 7)
+    O.contrastive_step(model, W, items.log_q, warm, opt, items.pretrained, loss_chunk=args.cpu_loss_chunk)
+    batch = synth.make_batch(items, batch_size, seed=batch_seed)
     n_valid = int((~batch["padding_mask"]).sum())
-    return {"value": round(args.cpu_sample_batch / dt, 2), "unit": "pairs/s", "cores": torch.get_num_threads(),
+    with _Heartbeat(f"cpu_baseline step ({batch_size} users, {n_valid} valid steps)"):
+        t0 = time.perf_counter()
+        O.contrastive_step(model, W, items.log_q, batch, opt, items.pretrained, loss_chunk=args.cpu_loss_chunk)
+        dt = time.perf_counter() - t0
+    torch.set_num_threads(prev_threads)
+    return {"value": round(batch_size / dt, 3), "unit": "pairs/s", "cores": threads,
             "kind": "port",
-            "sample": (f"oracle/user_tower.py contrastive_step (fp32 PyTorch CPU, dropout 0.2, AdamW) on "
-                       f"{args.cpu_sample_batch} users ({n_valid} valid steps), mean of {args.cpu_steps} steps "
-                       f"after 1 warm-up, {dt:.2f} s/step; smaller batch than the GPU run (CPU loss cost "
-                       f"grows with N^2)")}
+            "host": info,
+            "sample": (f"oracle/user_tower.py contrastive_step (fp32 PyTorch CPU, dropout 0.2, AdamW) on the GPU "
+                       f"headline's first global batch ({batch_size} users, {n_valid} valid steps, same seed); "
+                       f"ONE timed step ({dt:.1f} s) after a 64-user warm-up step; main loss evaluated over "
+                       f"{args.cpu_loss_chunk}-row chunks of the N x N logits under activation checkpointing "
+                       f"(same per-element arithmetic; the one-shot N x N tensors would need ~{4 * n_valid ** 2 / 1e9:.0f} GB)"),
+            "seconds_per_step": round(dt, 2)}
 
 
 def bench_deepfm(args, device):
@@ -175,6 +263,54 @@ def bench_deepfm(args, device):
     torch.cuda.synchronize()
     out["uniform_ids_rows_per_s"] = round(R / ((time.perf_counter() - t0) / iters), 1)
     return model, out
+
+
+def bench_gather_1m(device, T=316_372, rows=1_000_000, iters=10, flush_mb=1024):
+    """The embedding gather on DRAM-resident rows (SURVEY.md 7 "cache effects"): the fused
+    seq-embed forward (seq_embed_fwd_k, the north star's ">= 40 % of HBM on embedding gather")
+    over T packed tokens (the headline launch's size: both dropout views of the 8192-user batch)
+    with a 1M-row item-id table (512 MB, past the 256 MB Infinity Cache) and uniform ids, a fresh
+    projected-pretrained base per token, the reference's gates (s_mask: item-id and time tables
+    live, side tables 0), position add, LayerNorm and dropout 0.2. A 1 GiB buffer is written
+    before every launch so neither the table, the base nor the output stays cache-resident, and
+    each launch is timed alone with HIP events on its stream. Algorithmic bytes per token: base
+    row 512 + item row 512 + output row 512 + ids/position 24 + mean/rstd 8 = 1,568 B; the
+    12-row time table is read too but credited with nothing (it is cache-resident by nature)."""
+    from recsys_amd import ops
+    D, L = 128, 50
+    g = torch.Generator(device="cpu").manual_seed(21)
+    base = torch.randn(T, D, generator=g).to(device)
+    item_ids = torch.randint(1, rows, (T,), generator=g).to(device)
+    time_ids = torch.randint(1, 10, (T,), generator=g).to(device)
+    side = [torch.randint(1, 1001, (T,), generator=g).to(device) for _ in range(4)]
+    tok_pos = torch.randint(0, L, (T,), generator=g).to(device)
+    item_tab = (0.02 * torch.randn(rows, D, generator=g)).to(device)
+    time_tab = (0.02 * torch.randn(12, D, generator=g)).to(device)
+    side_tab = [(0.02 * torch.randn(1001, D, generator=g)).to(device) for _ in range(4)]
+    gate = torch.tensor([0.5, 0.5, 0.0, 0.0, 0.0, 0.0], device=device)
+    pos = (0.02 * torch.randn(L, D, generator=g)).to(device)
+    ln_w, ln_b = torch.ones(D, device=device), torch.zeros(D, device=device)
+    scratch = torch.empty(flush_mb << 18, device=device, dtype=torch.float32)
+    ids = [item_ids, time_ids] + side
+    tabs = [item_tab, time_tab] + side_tab
+    ms = []
+    with torch.no_grad():
+        for i in range(iters + 2):
+            scratch.zero_()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            ops.seq_embed(base, ids, tabs, gate, pos, ln_w, ln_b, p_drop=0.2, padding_idx=[0] * 6, tok_pos=tok_pos)
+            b.record()
+            torch.cuda.synchronize()
+            if i >= 2:
+                ms.append(a.elapsed_time(b))
+    avg = sum(ms) / len(ms)
+    bpt = 512 * 3 + 24 + 8
+    ach = bpt * T / (avg / 1e3) / 1e9
+    return {"kernel": "seq_embed_fwd_k", "bound": "hbm", "tokens_per_launch": T, "table_rows": rows,
+            "bytes_per_token": bpt, "avg_launch_ms": round(avg, 4), "achieved": round(ach, 1),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+            "note": "uniform ids over a 512 MB table, 1 GiB cache flush before each launch, time table uncredited"}
 
 
 def bench_retrieve_rerank(args, device, deepfm):
@@ -359,8 +495,9 @@ def bench_item_tower(args, device):
 def train_bench(args, global_batch, steps, warmup, items, cfg, model, item_tower, opt, bucket, rank, world,
                 device):
     """Times `steps` full train steps (after `warmup`) on this rank's slice of two seeded global
-    batches of `global_batch` users. -> (max-over-ranks seconds, per-op HIP-event times,
-    last losses, per-batch valid counts per rank, per-batch distinct targets)."""
+    batches of `global_batch` users (seeds args.seed + 100, + 101). -> dict with the max-over-ranks
+    seconds, per-op HIP-event times, last losses, per-batch valid counts per rank, per-batch distinct
+    targets, packed tokens per view, host enqueue time per step and allocator retry counts."""
     from recsys_amd import dist as D
     from recsys_amd import ops, synth
     b_loc = global_batch // world
@@ -384,12 +521,15 @@ def train_bench(args, global_batch, steps, warmup, items, cfg, model, item_tower
     # tokens, grouped targets: the host-synchronising size queries) on a side stream while the
     # GPU runs the step (dist.prepare_step_index_async). Every timed step still builds one index.
     pending = {}
+    enqueue = []
 
     def step(i):
+        h0 = time.perf_counter()
         ix = pending.pop(i, None)
         if ix is None:
             ix = D.prepare_step_index(batches[i % 2], pretrained_lookup=lookup)
         out = D.contrastive_step_dp(model, item_tower, log_q, batches[i % 2], opt, cfg, lookup, bucket, index=ix)
+        enqueue.append(time.perf_counter() - h0)
         if not args.no_prefetch_index:
             pending[i + 1] = D.prepare_step_index_async(batches[(i + 1) % 2], pretrained_lookup=lookup)
         return out
@@ -397,9 +537,10 @@ def train_bench(args, global_batch, steps, warmup, items, cfg, model, item_tower
     for i in range(warmup):
         step(i)
     if world > 1:
-        import torch.distributed as dist
-        dist.barrier()
+        torch.distributed.barrier()
     torch.cuda.synchronize()
+    retries0 = torch.cuda.memory_stats().get("num_alloc_retries", 0)
+    enqueue.clear()
     ops.timing_start()
     t0 = time.perf_counter()
     losses = None
@@ -407,20 +548,93 @@ def train_bench(args, global_batch, steps, warmup, items, cfg, model, item_tower
         losses = step(warmup + i)  # continues the warm-up's step numbering (pending index)
     torch.cuda.synchronize()
     if world > 1:
-        dist.barrier()
+        torch.distributed.barrier()
     t1 = time.perf_counter()
     kernel_times = ops.timing_stop()
+    retries = torch.cuda.memory_stats().get("num_alloc_retries", 0) - retries0
     # drain the prefetched index of the step that never ran
     pending.clear()
     torch.cuda.synchronize()
     elapsed = torch.tensor([t1 - t0], device=device, dtype=torch.float64)
     if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    return float(elapsed.item()), kernel_times, losses, n_glob, n_dist, n_tok
+        torch.distributed.all_reduce(elapsed, op=torch.distributed.ReduceOp.MAX)
+    return {"elapsed": float(elapsed.item()), "kernel_times": kernel_times, "losses": losses, "n_glob": n_glob,
+            "n_dist": n_dist, "n_tok": n_tok, "host_enqueue_ms": round(1e3 * sum(enqueue) / max(len(enqueue), 1), 3),
+            "alloc_retries": int(retries)}
+
+
+def nce_roofline(args, tb, global_batch, rank, world, precision):
+    """Roofline of the dominant kernel from the run's own HIP events. bf16x3: the main loss's
+    forward fused with the row gradient (nce_grouped_fwdg_x3_k: S plus the P x B product over
+    N_local x D distinct-target columns); fp32: the backward's row-owned pass (S recompute + dU).
+    Algorithmic FLOPs per launch = 4 * N_local * D * 128 either way (2 * N * D * d per product;
+    SURVEY.md 8d counts 2 N^2 d per product for the ungrouped reference formulation). Peak: the
+    MFMA rate of the arithmetic used (fp32 MFMA, or bf16 MFMA / 3 for the bf16x3 split products).
+    The timed window is the op's launches (fused kernel + B split + merge) on the launching stream."""
+    from recsys_amd import ops
+    kernel_times, n_glob, n_dist = tb["kernel_times"], tb["n_glob"], tb["n_dist"]
+    flops = 0.0
+    for i in range(args.warmup, args.warmup + args.steps):
+        flops += 4.0 * n_glob[i % 2][rank] * n_dist[i % 2] * 128
+    x3 = precision == "bf16x3"
+    fused = x3 and ops._NCE_FUSED_ROWGRAD
+    timer = "main/nce_fwd" if fused else "main/nce_bwd_rows"
+    launches, ms = kernel_times.get(timer, (0, 0.0))
+    avg_s = (ms / 1e3) / max(launches, 1)
+    achieved = (flops / max(launches, 1)) / avg_s / 1e12 if launches else None
+    peak = BF16X3_PEAK_TFLOPS if x3 else FP32_MFMA_PEAK_TFLOPS
+    traffic, traffic_src = None, None
+    if os.path.exists(TRAFFIC_FILE):
+        with open(TRAFFIC_FILE) as f:
+            tr = json.load(f)
+        if tr.get("precision") == precision and tr.get("global_batch") == global_batch and world == 1 and fused:
+            traffic, traffic_src = tr.get("hbm_bytes_per_launch"), os.path.basename(TRAFFIC_FILE)
+    return {"kernel": ("nce_grouped_fwdg_x3_k (main LogQ loss forward fused with the row gradient)"
+                       if fused else ("nce_grouped_bwd_x3_k<true>" if x3 else "nce_grouped_bwd_k<true>")
+                       + " (main LogQ loss backward, row-owned)"),
+            "timer": timer, "bound": "mfma",
+            "achieved": round(achieved, 2) if achieved else None, "peak": round(peak, 1),
+            "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
+            "traffic": traffic, "traffic_source": traffic_src,
+            "flops_per_launch": round(flops / max(launches, 1)), "avg_launch_ms": round(avg_s * 1e3, 4),
+            "peak_note": ("bf16 dense MFMA 2516.8 TF / 3 split products" if x3 else "fp32-input MFMA dense")}
+
+
+def gather_roofline(args, tb):
+    """Embedding gather (north_star: >= 40 % of HBM): the fused seq-embed forward
+    (seq_embed_fwd_k, both dropout views in one packed launch). Algorithmic bytes per token
+    (SURVEY.md 8d): 3 live 512-B rows read (projected pretrained row, item-id row, time row; the
+    gate-0 tables are skipped), the 512-B output row written, 16 B of ids. NB: the 47k-row item
+    table (24 MB) and the 12-row time table are L2/MALL-resident at this size, so this figure
+    credits cache hits as HBM bytes; see secondary_gather_1m for DRAM-resident rows."""
+    kernel_times, n_tok = tb["kernel_times"], tb["n_tok"]
+    g_n, g_ms = kernel_times.get("seq_embed_fwd", (0, 0.0))
+    if not g_n:
+        return None
+    tok = sum(2 * n_tok[i % 2] for i in range(args.warmup, args.warmup + args.steps))  # two views
+    bpl = 2064.0 * tok / g_n
+    gs = g_ms / 1e3 / g_n
+    return {"kernel": "seq_embed_fwd_k", "bound": "hbm", "bytes_per_token": 2064,
+            "tokens_per_launch": int(tok / g_n), "avg_launch_ms": round(gs * 1e3, 4),
+            "achieved": round(bpl / gs / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(bpl / gs / 1e9 / HBM_PEAK_GBS, 4), "cache_note": "item/time tables cache-resident"}
+
+
+def train_line(args, tb, global_batch, steps, warmup):
+    kt = tb["kernel_times"]
+    nf = kt.get("main/nce_fwd", (0, 0.0))
+    return {"metric": "SimCSE train-step pairs/sec at d=128 (global batch %d)" % global_batch,
+            "value": round(global_batch * steps / tb["elapsed"], 2), "unit": "pairs/s", "steps": steps,
+            "warmup": warmup, "ms_per_step": round(1e3 * tb["elapsed"] / steps, 3),
+            "valid_positions_per_batch": [sum(c) for c in tb["n_glob"]], "distinct_targets_per_batch": tb["n_dist"],
+            "main_loss_fwd_ms": round(nf[1] / max(nf[0], 1), 4), "host_enqueue_ms_per_step": tb["host_enqueue_ms"],
+            "alloc_retries": tb["alloc_retries"]}
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     rank, world, device = setup_dist(args)
     scaling = "strong" if args.batch is not None else "weak"
     if args.batch is None:
@@ -457,112 +671,79 @@ def main():
     bucket = D.GradBucket(list(model.parameters()) + list(item_tower.parameters()))
 
     # two distinct global batches, this rank's user slice of each, resident in HBM
-    (elapsed, kernel_times, losses, n_glob, n_dist, n_tok) = train_bench(
-        args, args.batch, args.steps, args.warmup, items, cfg, model, item_tower, opt, bucket, rank, world, device)
-    total_loss = float(losses[0].item())
-
-    # roofline of the dominant kernel. bf16x3 (default): the main loss's forward fused with the
-    # row gradient (nce_grouped_fwdg_x3_k: S plus the P x B product over N_local x D
-    # distinct-target columns); fp32: the backward's row-owned pass (S recompute + dU product).
-    # Algorithmic FLOPs per launch = 4 * N_local * D * 128 either way (2 * N * D * d per
-    # product; SURVEY.md 8d counts 2 N^2 d per product for the ungrouped reference formulation).
-    # Peak: the MFMA rate of the arithmetic used: fp32 MFMA, or bf16 MFMA / 3 for the bf16x3
-    # split products. The timed window is the op's launches (fused kernel + B split + merge).
-    flops = 0.0
-    for i in range(args.warmup, args.warmup + args.steps):
-        cnts = n_glob[i % 2]
-        flops += 4.0 * cnts[rank] * n_dist[i % 2] * 128
-    x3 = args.nce_precision == "bf16x3"
-    fused = x3 and ops._NCE_FUSED_ROWGRAD
-    timer = "main/nce_fwd" if fused else "main/nce_bwd_rows"
-    launches, ms = kernel_times.get(timer, (0, 0.0))
-    avg_s = (ms / 1e3) / max(launches, 1)
-    achieved = (flops / max(launches, 1)) / avg_s / 1e12 if launches else None
-    peak = BF16X3_PEAK_TFLOPS if x3 else FP32_MFMA_PEAK_TFLOPS
-    traffic = None
-    if os.path.exists(TRAFFIC_FILE):
-        with open(TRAFFIC_FILE) as f:
-            tr = json.load(f)
-        if (tr.get("precision") == args.nce_precision and tr.get("global_batch") == args.batch and world == 1
-                and fused):
-            traffic = tr.get("hbm_bytes_per_launch")
-
-    kt = {k: {"launches": n, "avg_ms": round(t / max(n, 1), 4)} for k, (n, t) in sorted(kernel_times.items())}
-    # embedding gather (north_star: >= 40 % of HBM): the fused seq-embed forward
-    # (seq_embed_fwd_k, both dropout views in one packed launch). Algorithmic bytes per token
-    # (SURVEY.md 8d): 3 live 512-B rows read (projected pretrained row, item-id row, time row;
-    # the gate-0 tables are skipped), the 512-B output row written, 16 B of ids.
-    g_n, g_ms = kernel_times.get("seq_embed_fwd", (0, 0.0))
-    gather = None
-    if g_n:
-        tok = sum(2 * n_tok[i % 2] for i in range(args.warmup, args.warmup + args.steps))  # two views
-        bpl = 2064.0 * tok / g_n
-        gs = g_ms / 1e3 / g_n
-        gather = {"kernel": "seq_embed_fwd_k", "bound": "hbm", "bytes_per_token": 2064,
-                  "tokens_per_launch": int(tok / g_n), "avg_launch_ms": round(gs * 1e3, 4),
-                  "achieved": round(bpl / gs / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                  "frac": round(bpl / gs / 1e9 / HBM_PEAK_GBS, 4)}
+    tb = train_bench(args, args.batch, args.steps, args.warmup, items, cfg, model, item_tower, opt, bucket, rank,
+                     world, device)
+    total_loss = float(tb["losses"][0].item())
+    kt = {k: {"launches": n, "avg_ms": round(t / max(n, 1), 4)} for k, (n, t) in sorted(tb["kernel_times"].items())}
     result = {
-        "metric": "SimCSE train-step pairs/sec at d=128 (global batch %d)" % args.batch,
-        "value": round(args.batch * args.steps / elapsed, 2),
+        "metric": "SimCSE train-step pairs/sec at d=128, batch %d" % args.batch,
+        "value": round(args.batch * args.steps / tb["elapsed"], 2),
         "unit": "pairs/s",
         "n_gpus": world,
+        "rccl_world_size": (torch.distributed.get_world_size() if world > 1 else 1),
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "ms_per_step": round(1e3 * tb["elapsed"] / args.steps, 3),
         "higher_is_better": True,
         "scaling": scaling,
         "vs_baseline": None,
-        "dtype": "fp32+bf16x3" if x3 else "fp32",
+        "dtype": "fp32+bf16x3" if args.nce_precision == "bf16x3" else "fp32",
         "data": "synthetic (seeded H&M-shaped users/items: sample-calibrated lengths, Zipf(1.0) items; "
                 "random-init weights)",
         "config": {"workload": "user-tower two-view contrastive train step (fwd x2 + LogQ in-batch loss + "
-                               "DuoRec + bwd + clip + AdamW), BASELINE configs[1] at N=1 (global batch 4096), "
-                               "configs[3] at N=8 (global batch 32768, all-gathered negatives)",
+                               "DuoRec + bwd + clip + AdamW); N=1: global batch 8192 (BASELINE.json metric); "
+                               "weak scaling at 8192 users/GPU (N=4: configs[3]'s global batch 32768), "
+                               "negatives all-gathered over ranks",
                    "users_per_gpu": args.batch // world,
                    "global_batch": args.batch, "seq_len": 50, "d_model": 128, "items": args.items,
-                   "valid_positions_per_batch": [sum(c) for c in n_glob],
-                   "distinct_targets_per_batch": n_dist, "dropout": args.dropout,
+                   "valid_positions_per_batch": [sum(c) for c in tb["n_glob"]],
+                   "distinct_targets_per_batch": tb["n_dist"], "dropout": args.dropout,
                    "item_matrix": "frozen" if args.freeze_items else "unfrozen (lr x0.05)",
-                   "parallelism": f"dp{world} (users split by rank, RCCL all-gather of ids/z, grad all-reduce)",
+                   "parallelism": f"dp{world} (users split by rank, RCCL all-gather of ids/z, bucketed grad "
+                                  f"all-reduce overlapped with backward)",
                    "dense_projection_blas": args.blas, "nce_logit_precision": args.nce_precision},
-        "roofline": {"kernel": ("nce_grouped_fwdg_x3_k (main LogQ loss forward fused with the row gradient)"
-                                if fused else ("nce_grouped_bwd_x3_k<true>" if x3 else "nce_grouped_bwd_k<true>")
-                                + " (main LogQ loss backward, row-owned)"),
-                     "timer": timer, "bound": "mfma",
-                     "achieved": round(achieved, 2) if achieved else None, "peak": round(peak, 1),
-                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
-                     "traffic": traffic, "traffic_source": os.path.basename(TRAFFIC_FILE) if traffic else None,
-                     "avg_launch_ms": round(avg_s * 1e3, 4),
-                     "peak_note": ("bf16 dense MFMA 2516.8 TF / 3 split products" if x3
-                                   else "fp32-input MFMA dense")},
-        "gather_roofline": gather,
+        "roofline": nce_roofline(args, tb, args.batch, rank, world, args.nce_precision),
+        "gather_roofline": gather_roofline(args, tb),
+        "host_enqueue_ms_per_step": tb["host_enqueue_ms"],
+        "alloc_retries": tb["alloc_retries"],
         "kernels": kt,
         "final_loss": round(total_loss, 5),
     }
-    if world == 1 and not args.no_batch8192 and args.batch != 8192:
-        # BASELINE.json's metric string names batch 8192 (configs[1] says 4096): same step, same
-        # model and optimiser state, global batch 8192 on this GPU.
-        el8, kt8, _, ng8, nd8, _ = train_bench(args, 8192, args.steps8192, 2, items, cfg, model, item_tower, opt,
-                                            bucket, rank, world, device)
-        result["secondary_batch8192"] = {
-            "metric": "SimCSE train-step pairs/sec at d=128 (global batch 8192)",
-            "value": round(8192 * args.steps8192 / el8, 2), "unit": "pairs/s", "steps": args.steps8192,
-            "warmup": 2, "ms_per_step": round(1e3 * el8 / args.steps8192, 3),
-            "valid_positions_per_batch": [sum(c) for c in ng8], "distinct_targets_per_batch": nd8,
-            "main_loss_fwd_ms": round(kt8.get("main/nce_fwd", (1, 0.0))[1] / max(kt8.get("main/nce_fwd", (1, 0))[0], 1), 4)}
+    del tb
+    if world == 1 and not args.no_batch4096 and args.batch != 4096:
+        # BASELINE configs[1]: same step, same model and optimiser state, global batch 4096
+        t4 = train_bench(args, 4096, args.steps4096, 3, items, cfg, model, item_tower, opt, bucket, rank, world,
+                         device)
+        result["secondary_batch4096"] = train_line(args, t4, 4096, args.steps4096, 3)
+        del t4
+        torch.cuda.empty_cache()
+    if world == 1 and not args.no_fp32_line:
+        # the fp32 parity mode: loss products on the fp32 MFMA, token GEMMs / attention
+        # in fp32, at the headline's batch
+        prev = (ops.set_nce_precision("fp32"), ops.set_gemm_precision("fp32"), ops.mha_precision())
+        ops.set_mha_precision("fp32")
+        tf = train_bench(args, args.batch, args.steps_fp32, 2, items, cfg, model, item_tower, opt, bucket, rank,
+                         world, device)
+        line = train_line(args, tf, args.batch, args.steps_fp32, 2)
+        line["metric"] += " [fp32 parity mode: fp32-MFMA loss kernels, fp32 token GEMMs and attention]"
+        result["secondary_fp32_mode"] = line
+        ops.set_nce_precision(prev[0])
+        ops.set_gemm_precision(prev[1])
+        ops.set_mha_precision(prev[2])
+        del tf
         torch.cuda.empty_cache()
     if world == 1 and not args.no_batch32768 and args.batch != 32768:
         # configs[3]'s global batch (32,768 users, all negatives in one pool) on ONE GPU: the
-        # strong-scaling baseline for the N = 8 run (4,096 users per GPU, same global batch)
-        el32, kt32, _, ng32, nd32, _ = train_bench(args, 32768, args.steps32768, 1, items, cfg, model, item_tower,
-                                                   opt, bucket, rank, world, device)
-        result["secondary_batch32768"] = {
-            "metric": "SimCSE train-step pairs/sec at d=128 (global batch 32768 on one GPU: strong-scaling baseline "
-                      "of configs[3])",
-            "value": round(32768 * args.steps32768 / el32, 2), "unit": "pairs/s", "steps": args.steps32768,
-            "warmup": 1, "ms_per_step": round(1e3 * el32 / args.steps32768, 3),
-            "valid_positions_per_batch": [sum(c) for c in ng32], "distinct_targets_per_batch": nd32}
+        # strong-scaling baseline for a multi-GPU run at the same global batch
+        t32 = train_bench(args, 32768, args.steps32768, 2, items, cfg, model, item_tower, opt, bucket, rank, world,
+                          device)
+        line = train_line(args, t32, 32768, args.steps32768, 2)
+        line["metric"] += " [configs[3]'s global batch on ONE GPU: strong-scaling baseline]"
+        result["secondary_batch32768"] = line
+        del t32
+        torch.cuda.empty_cache()
+    if rank == 0 and world == 1:
+        result["secondary_gather_1m"] = bench_gather_1m(device)
         torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_deepfm:
         torch.cuda.empty_cache()
@@ -577,11 +758,12 @@ def main():
         result["secondary_item_refresh"] = bench_item_refresh(args, device)
         result["secondary_hnm"] = bench_hnm(args, device)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args, items, cfg)
+        result["cpu_baseline"] = cpu_baseline(args, items, cfg, args.batch, args.seed + 100)
+        result["gpu_over_cpu"] = round(result["value"] / result["cpu_baseline"]["value"], 1)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
-        dist.destroy_process_group()
+        torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -52,14 +52,17 @@ int rsx_seq_embed_fwd(const float* base, const int64_t* const* ids, const float*
 /* Backward of rsx_seq_embed_fwd. dbase [T,D] written; dtables[j], dgate [ntab], dpos [L,D],
  * dln_w/dln_b [D] accumulated (nullable). padding_idx[j]: rows excluded from the table
  * gradient exactly like nn.Embedding(padding_idx=...) (-1 = none). table_rows[j] lets small
- * tables (time buckets) accumulate in LDS; position and small-table gradients are flushed
- * once per workgroup (float atomics: summation order varies run to run in the last bits). */
+ * tables (time buckets) accumulate in LDS. Position, small-table, LN and gate gradients are
+ * per-workgroup LDS sums; with a workspace (>= rsx_seq_embed_bwd_workspace_floats floats) they
+ * are stored per workgroup and folded in block order by a second kernel (deterministic);
+ * workspace NULL flushes them with global float atomics (last bits vary run to run). */
+int64_t rsx_seq_embed_bwd_workspace_floats(int64_t T, int64_t L, int64_t D);
 int rsx_seq_embed_bwd(const float* base, const int64_t* const* ids, const float* const* tables,
                       const int64_t* table_rows, const int64_t* padding_idx, int ntab, const float* gate,
                       const float* pos, const int64_t* tok_pos, const float* ln_w, const float* mean,
                       const float* rstd, float eps, int64_t T, int64_t L, int64_t D, float p_drop, uint64_t seed,
                       const float* dout, float* dbase, float* const* dtables, float* dgate, float* dpos,
-                      float* dln_w, float* dln_b, void* stream);
+                      float* dln_w, float* dln_b, float* workspace, int64_t ws_floats, void* stream);
 
 /* ---- A3 / A9: masked multi-head self-attention core (L <= 64) -----------------------
  * Replaces the attention inside nn.TransformerEncoderLayer (norm_first, batch_first) at

@@ -24,6 +24,8 @@ c_i = ctypes.c_int
 c_f = ctypes.c_float
 c_u64 = ctypes.c_uint64
 
+ABI_VERSION = 2  # rsx_abi_version() of the library these signatures describe
+
 # name -> (restype, argtypes)
 _SIGS = {
     "rsx_last_error": (ctypes.c_char_p, []),
@@ -31,8 +33,9 @@ _SIGS = {
     "rsx_target_arch": (ctypes.c_char_p, []),
     "rsx_seq_embed_fwd": (c_i, [c_p, c_p, c_p, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_i64, c_i64, c_i64, c_f, c_u64,
                                 c_p, c_p, c_p, c_p]),
+    "rsx_seq_embed_bwd_workspace_floats": (c_i64, [c_i64, c_i64, c_i64]),
     "rsx_seq_embed_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_i64, c_i64,
-                                c_i64, c_f, c_u64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+                                c_i64, c_f, c_u64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p]),
     "rsx_mha_fwd": (c_i, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i, c_f, c_u64, c_p, c_p, c_p]),
     "rsx_mha_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i, c_f, c_u64, c_p, c_p]),
     "rsx_mha_fwd_x3": (c_i, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i, c_f, c_u64, c_p, c_p, c_p]),
@@ -101,6 +104,9 @@ def load(path: str = LIB_PATH):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        if lib.rsx_abi_version() != ABI_VERSION:
+            raise RuntimeError(f"recsys_amd: {path} has ABI {lib.rsx_abi_version()}, this binding expects "
+                               f"{ABI_VERSION}; rebuild with __graft_entry__.build()")
         _lib = lib
         return lib
 

@@ -71,7 +71,90 @@ __device__ __forceinline__ float4 build_row(const FwdArgs& a, int64_t r, int c, 
   return x;
 }
 
+// Forward. The gather is latency-bound (each row is an id load followed by a dependent row
+// load), so each wave owns U row groups (RPW rows each) per iteration and issues every id load,
+// then every row load of all U groups before the first use: U independent id -> row chains per
+// lane in flight. Tables whose gate is exactly 0 contribute exactly nothing (x + e*0 == x), so
+// the wave first compacts the live tables (gate != 0; the reference's s_mask leaves item-id and
+// time live) into NL <= 2 slots, which keeps the register budget at U x 2 rows; more than two
+// live tables take the one-row-at-a-time path. Per element the op order is unchanged: base,
+// + E_j[id_j] * g_j for the live j in increasing order, + pos, then LayerNorm and dropout.
 template <int D>
+__device__ __forceinline__ void ln_drop_store(const FwdArgs& a, float4 x, int64_t r, bool ok, int c, float4 w,
+                                              float4 bb, bool do_ln) {
+  constexpr int LPR = D / 4;
+  float4 y = x;
+  if (do_ln) {
+    float s = (x.x + x.y) + (x.z + x.w);
+    s = rsx::wave_sum_width(s, LPR);
+    const float mu = s / (float)D;
+    const float4 d = make_float4(x.x - mu, x.y - mu, x.z - mu, x.w - mu);
+    float v = d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w;
+    v = rsx::wave_sum_width(v, LPR);
+    const float rs = 1.0f / sqrtf(v / (float)D + a.eps);
+    y.x = d.x * rs * w.x + bb.x;
+    y.y = d.y * rs * w.y + bb.y;
+    y.z = d.z * rs * w.z + bb.z;
+    y.w = d.w * rs * w.w + bb.w;
+    if (ok && c == 0) {
+      if (a.mean) a.mean[r] = mu;
+      if (a.rstd) a.rstd[r] = rs;
+    }
+  }
+  if (ok) {
+    if (a.drop.active()) {
+      const uint64_t base_idx = (uint64_t)r * D + 4 * c;
+      y.x = a.drop.apply(y.x, base_idx + 0);
+      y.y = a.drop.apply(y.y, base_idx + 1);
+      y.z = a.drop.apply(y.z, base_idx + 2);
+      y.w = a.drop.apply(y.w, base_idx + 3);
+    }
+    reinterpret_cast<float4*>(a.out + r * D)[c] = y;
+  }
+}
+
+template <int D, int U, int NL>
+__device__ __forceinline__ void fwd_groups(const FwdArgs& a, const int64_t* const* ids_l, const float* const* tab_l,
+                                           const float* g_l, int64_t r0, int sub, int c, float4 w, float4 bb,
+                                           bool do_ln) {
+  constexpr int RPW = 64 / (D / 4);
+  int64_t rr[U];
+  int64_t id[U][NL > 0 ? NL : 1];
+  int lp[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t r = r0 + u * RPW + sub;
+    rr[u] = r < a.T ? r : a.T - 1;  // clamped: out-of-range slots recompute the last row, store nothing
+#pragma unroll
+    for (int k = 0; k < NL; ++k) id[u][k] = ids_l[k][rr[u]];
+    lp[u] = a.pos ? (a.tok_pos ? (int)a.tok_pos[rr[u]] : (int)(rr[u] % a.L)) : 0;
+  }
+  float4 x[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    x[u] = a.base ? reinterpret_cast<const float4*>(a.base + rr[u] * D)[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 e[U][NL > 0 ? NL : 1];
+#pragma unroll
+  for (int k = 0; k < NL; ++k)
+#pragma unroll
+    for (int u = 0; u < U; ++u) e[u][k] = reinterpret_cast<const float4*>(tab_l[k] + id[u][k] * D)[c];
+#pragma unroll
+  for (int k = 0; k < NL; ++k)
+#pragma unroll
+    for (int u = 0; u < U; ++u) x[u] = f4_axpy_rn(x[u], e[u][k], g_l[k]);
+  if (a.pos) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      x[u] = f4_add_rn(x[u], reinterpret_cast<const float4*>(a.pos + (int64_t)lp[u] * D)[c]);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t r = r0 + u * RPW + sub;
+    ln_drop_store<D>(a, x[u], r, r < a.T, c, w, bb, do_ln);
+  }
+}
+
+template <int D, int U>
 __global__ __launch_bounds__(256) void seq_embed_fwd_k(FwdArgs a) {
   constexpr int LPR = D / 4;
   constexpr int RPW = 64 / LPR;
@@ -82,45 +165,38 @@ __global__ __launch_bounds__(256) void seq_embed_fwd_k(FwdArgs a) {
   float g[kMaxTab];
 #pragma unroll
   for (int j = 0; j < kMaxTab; ++j) g[j] = (j < a.ntab) ? (a.gate ? a.gate[j] : 1.0f) : 0.0f;
+  // compact the live tables (wave-uniform selects over the kernarg pointers: no dynamic indexing)
+  const int64_t* ids_l[2] = {nullptr, nullptr};
+  const float* tab_l[2] = {nullptr, nullptr};
+  float g_l[2] = {0.0f, 0.0f};
+  int nl = 0;
+#pragma unroll
+  for (int j = 0; j < kMaxTab; ++j) {
+    if (g[j] != 0.0f) {
+      if (nl == 0) { ids_l[0] = a.ids[j]; tab_l[0] = a.tab[j]; g_l[0] = g[j]; }
+      else if (nl == 1) { ids_l[1] = a.ids[j]; tab_l[1] = a.tab[j]; g_l[1] = g[j]; }
+      ++nl;
+    }
+  }
   const bool do_ln = a.ln_w != nullptr;
   float4 w = make_float4(1.f, 1.f, 1.f, 1.f), bb = make_float4(0.f, 0.f, 0.f, 0.f);
   if (do_ln) {
     w = reinterpret_cast<const float4*>(a.ln_w)[c];
     bb = reinterpret_cast<const float4*>(a.ln_b)[c];
   }
-  for (int64_t r0 = wave_g * RPW; r0 < a.T; r0 += nwaves * RPW) {
-    const int64_t r = r0 + sub;
-    const bool ok = r < a.T;
-    float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (ok) x = build_row<D>(a, r, c, g);
-    float4 y = x;
-    if (do_ln) {
-      float s = (x.x + x.y) + (x.z + x.w);
-      s = rsx::wave_sum_width(s, LPR);
-      const float mu = s / (float)D;
-      const float4 d = make_float4(x.x - mu, x.y - mu, x.z - mu, x.w - mu);
-      float v = d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w;
-      v = rsx::wave_sum_width(v, LPR);
-      const float rs = 1.0f / sqrtf(v / (float)D + a.eps);
-      y.x = d.x * rs * w.x + bb.x;
-      y.y = d.y * rs * w.y + bb.y;
-      y.z = d.z * rs * w.z + bb.z;
-      y.w = d.w * rs * w.w + bb.w;
-      if (ok && c == 0) {
-        if (a.mean) a.mean[r] = mu;
-        if (a.rstd) a.rstd[r] = rs;
-      }
+  if (nl > 2) {  // generic: one row group per iteration, every table
+    for (int64_t r0 = wave_g * RPW; r0 < a.T; r0 += nwaves * RPW) {
+      const int64_t r = r0 + sub;
+      const bool ok = r < a.T;
+      const float4 x = build_row<D>(a, ok ? r : a.T - 1, c, g);
+      ln_drop_store<D>(a, x, r, ok, c, w, bb, do_ln);
     }
-    if (ok) {
-      if (a.drop.active()) {
-        const uint64_t base_idx = (uint64_t)r * D + 4 * c;
-        y.x = a.drop.apply(y.x, base_idx + 0);
-        y.y = a.drop.apply(y.y, base_idx + 1);
-        y.z = a.drop.apply(y.z, base_idx + 2);
-        y.w = a.drop.apply(y.w, base_idx + 3);
-      }
-      reinterpret_cast<float4*>(a.out + r * D)[c] = y;
-    }
+    return;
+  }
+  for (int64_t r0 = wave_g * (RPW * U); r0 < a.T; r0 += nwaves * (RPW * U)) {
+    if (nl == 2) fwd_groups<D, U, 2>(a, ids_l, tab_l, g_l, r0, sub, c, w, bb, do_ln);
+    else if (nl == 1) fwd_groups<D, U, 1>(a, ids_l, tab_l, g_l, r0, sub, c, w, bb, do_ln);
+    else fwd_groups<D, U, 0>(a, ids_l, tab_l, g_l, r0, sub, c, w, bb, do_ln);
   }
 }
 
@@ -138,6 +214,8 @@ struct BwdArgs {
   float* dln_b;
   int64_t rows_per_block;
   int small_total;        // floats of LDS for small tables
+  float* partials;        // [blocks][part_w] per-block sums (then seq_embed_bwd_reduce_k), or nullptr => atomics
+  int part_w;             // L*D + small_total + 2*D + kMaxTab
 };
 
 constexpr int kSmallMax = 8192;  // floats (32 KiB)
@@ -280,6 +358,27 @@ __global__ __launch_bounds__(256) void seq_embed_bwd_k(BwdArgs a) {
     for (int j = 0; j < kMaxTab; ++j) s_gate[wave][j] = acc_g[j];
   }
   __syncthreads();
+  if (a.partials) {
+    // deterministic two-pass reduction: this block's sums in its own workspace row (plain
+    // stores, zeros included), folded over blocks in a fixed order by seq_embed_bwd_reduce_k
+    float* prow = a.partials + (int64_t)blockIdx.x * a.part_w;
+    const int nlds = f.L * D + a.small_total;
+    for (int i = tid; i < nlds; i += blockDim.x) prow[i] = s_dyn[i];
+    for (int i = tid; i < 2 * D; i += blockDim.x) {
+      const int which = i / D, col = i % D;
+      float v = 0.0f;
+#pragma unroll
+      for (int wv = 0; wv < NW; ++wv) v += s_red[wv][which][col];
+      prow[nlds + i] = v;
+    }
+    if (tid < kMaxTab) {
+      float v = 0.0f;
+#pragma unroll
+      for (int wv = 0; wv < NW; ++wv) v += s_gate[wv][tid];
+      prow[nlds + 2 * D + tid] = v;
+    }
+    return;
+  }
   if (do_ln) {
     for (int i = tid; i < 2 * D; i += blockDim.x) {
       const int which = i / D, col = i % D;
@@ -312,13 +411,94 @@ __global__ __launch_bounds__(256) void seq_embed_bwd_k(BwdArgs a) {
   }
 }
 
+// Fold of the per-block partial rows: column j of [blocks][part_w] summed over blocks in block
+// order, then added to its destination (positions, LDS-resident small tables, LN weight / bias,
+// gates). One workgroup per 64 columns; its 4 waves take every 4th block row, 64 lanes read 256
+// contiguous bytes of a row; the 4 wave sums are combined in LDS in wave order.
+struct ReduceArgs {
+  const float* partials;
+  int64_t blocks;
+  int part_w;
+  int L, D, ntab;
+  int small_total;
+  int small_off[kMaxTab];
+  int small_rows[kMaxTab];
+  float* dtab[kMaxTab];
+  float* dpos;
+  float* dln_w;
+  float* dln_b;
+  float* dgate;
+};
+
+__global__ __launch_bounds__(256) void seq_embed_bwd_reduce_k(ReduceArgs a) {
+  __shared__ float s_part[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + lane;
+  float v = 0.0f;
+  if (j < a.part_w) {
+    const float* p = a.partials + j;
+    int64_t b = wave;
+    for (; b + 12 < a.blocks; b += 16) {
+      const float x0 = p[b * a.part_w], x1 = p[(b + 4) * a.part_w];
+      const float x2 = p[(b + 8) * a.part_w], x3 = p[(b + 12) * a.part_w];
+      v += x0; v += x1; v += x2; v += x3;
+    }
+    for (; b < a.blocks; b += 4) v += p[b * a.part_w];
+  }
+  s_part[wave][lane] = v;
+  __syncthreads();
+  if (wave != 0 || j >= a.part_w) return;
+  v = ((s_part[0][lane] + s_part[1][lane]) + s_part[2][lane]) + s_part[3][lane];
+  const int npos = a.L * a.D;
+  const int nlds = npos + a.small_total;
+  float* dst = nullptr;
+  if (j < npos) {
+    dst = a.dpos ? a.dpos + j : nullptr;
+  } else if (j < nlds) {
+    const int o = j - npos;
+    for (int t = 0; t < a.ntab; ++t) {
+      if (a.small_off[t] >= 0 && o >= a.small_off[t] && o < a.small_off[t] + a.small_rows[t] * a.D)
+        dst = a.dtab[t] ? a.dtab[t] + (o - a.small_off[t]) : nullptr;
+    }
+  } else if (j < nlds + a.D) {
+    dst = a.dln_w ? a.dln_w + (j - nlds) : nullptr;
+  } else if (j < nlds + 2 * a.D) {
+    dst = a.dln_b ? a.dln_b + (j - nlds - a.D) : nullptr;
+  } else if (j - nlds - 2 * a.D < a.ntab) {
+    dst = a.dgate ? a.dgate + (j - nlds - 2 * a.D) : nullptr;
+  }
+  if (dst) *dst += v;
+}
+
+// row groups per wave iteration (seq_embed_fwd_k U); RSX_SEQ_EMBED_FWD_U in {1,2,4,8} overrides
+// (tuning experiments)
+int fwd_groups_setting() {
+  static int u = [] {
+    const char* s = getenv("RSX_SEQ_EMBED_FWD_U");
+    const int v = s ? atoi(s) : 2;
+    return (v == 1 || v == 2 || v == 4 || v == 8) ? v : 2;
+  }();
+  return u;
+}
+
+template <int D, int U>
+void launch_fwd_u(const FwdArgs& a, hipStream_t st) {
+  const int64_t rows_per_block = 4 * (64 / (D / 4)) * U;
+  int64_t blocks = (a.T + rows_per_block - 1) / rows_per_block;
+  if (blocks > 16384) blocks = 16384;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL((seq_embed_fwd_k<D, U>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+}
+
 template <int D>
 int launch_fwd(const FwdArgs& a, hipStream_t st) {
-  const int64_t rows_per_block = 4 * (64 / (D / 4));
-  int64_t blocks = (a.T + rows_per_block - 1) / rows_per_block;
-  if (blocks > 8192) blocks = 8192;
-  if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(seq_embed_fwd_k<D>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  switch (fwd_groups_setting()) {
+    case 1: launch_fwd_u<D, 1>(a, st); break;
+    case 2: launch_fwd_u<D, 2>(a, st); break;
+    case 8: launch_fwd_u<D, 8>(a, st); break;
+    case 4: launch_fwd_u<D, 4>(a, st); break;
+    default: launch_fwd_u<D, 2>(a, st); break;
+  }
   return 0;
 }
 
@@ -330,9 +510,9 @@ int launch_bwd(const BwdArgs& a, hipStream_t st) {
   return 0;
 }
 
-int64_t bwd_rows_per_block(int64_t T, int64_t D) {
-  // ~2 workgroups per CU, each owning a contiguous token chunk
-  int64_t rpb = (T + 511) / 512;
+int64_t bwd_rows_per_block(int64_t T, int64_t D, int64_t target_blocks) {
+  // target_blocks workgroups, each owning a contiguous token chunk
+  int64_t rpb = (T + target_blocks - 1) / target_blocks;
   const int64_t quantum = 4 * (64 / (D / 4));
   rpb = (rpb + quantum - 1) / quantum * quantum;
   if (rpb < quantum) rpb = quantum;
@@ -403,12 +583,27 @@ RSX_API int rsx_seq_embed_fwd(const float* base, const int64_t* const* ids, cons
   return 0;
 }
 
+// With a workspace the backward runs kBwdBlocksWs workgroups (4 per CU: the gathers of the
+// LayerNorm recompute need the occupancy) that store per-block partial sums, folded by
+// seq_embed_bwd_reduce_k (deterministic, no global atomics); without one, ~2 workgroups per CU
+// flush their LDS sums with global float atomics.
+constexpr int64_t kBwdBlocksWs = 1024;
+constexpr int64_t kBwdBlocksAtomic = 512;
+
+RSX_API int64_t rsx_seq_embed_bwd_workspace_floats(int64_t T, int64_t L, int64_t D) {
+  if (T <= 0 || D <= 0) return 0;
+  const int64_t rpb = bwd_rows_per_block(T, D, kBwdBlocksWs);
+  const int64_t blocks = (T + rpb - 1) / rpb;
+  return blocks * (L * D + kSmallMax + 2 * D + kMaxTab);
+}
+
 RSX_API int rsx_seq_embed_bwd(const float* base, const int64_t* const* ids, const float* const* tables,
                               const int64_t* table_rows, const int64_t* padding_idx, int ntab, const float* gate,
                               const float* pos, const int64_t* tok_pos, const float* ln_w, const float* mean,
                               const float* rstd, float eps, int64_t T, int64_t L, int64_t D, float p_drop,
                               uint64_t seed, const float* dout, float* dbase, float* const* dtables, float* dgate,
-                              float* dpos, float* dln_w, float* dln_b, void* stream) {
+                              float* dpos, float* dln_w, float* dln_b, float* workspace, int64_t ws_floats,
+                              void* stream) {
   RSX_ARG(dout != nullptr, "dout is null");
   RSX_ARG(D == 64 || D == 128 || D == 256, "D must be 64, 128 or 256");
   RSX_ARG(ntab >= 0 && ntab <= kMaxTab, "ntab must be in [0,6]");
@@ -432,11 +627,37 @@ RSX_API int rsx_seq_embed_bwd(const float* base, const int64_t* const* ids, cons
   a.dpos = dpos;
   a.dln_w = dln_w;
   a.dln_b = dln_b;
-  a.rows_per_block = bwd_rows_per_block(T, D);
+  const bool use_ws = workspace != nullptr;
+  if (use_ws)
+    RSX_ARG(ws_floats >= rsx_seq_embed_bwd_workspace_floats(T, L, D), "workspace too small");
+  a.rows_per_block = bwd_rows_per_block(T, D, use_ws ? kBwdBlocksWs : kBwdBlocksAtomic);
+  const int64_t blocks = (T + a.rows_per_block - 1) / a.rows_per_block;
+  a.partials = use_ws ? workspace : nullptr;
+  a.part_w = (int)(L * D + a.small_total + 2 * D + kMaxTab);
   hipStream_t st = (hipStream_t)stream;
   if (D == 64) launch_bwd<64>(a, st);
   else if (D == 128) launch_bwd<128>(a, st);
   else launch_bwd<256>(a, st);
+  if (use_ws) {
+    ReduceArgs r;
+    r.partials = workspace;
+    r.blocks = blocks;
+    r.part_w = a.part_w;
+    r.L = (int)L;
+    r.D = (int)D;
+    r.ntab = ntab;
+    r.small_total = a.small_total;
+    for (int j = 0; j < kMaxTab; ++j) {
+      r.small_off[j] = a.small_off[j];
+      r.small_rows[j] = a.small_rows[j];
+      r.dtab[j] = a.dtab[j];
+    }
+    r.dpos = dpos;
+    r.dln_w = dln_w;
+    r.dln_b = dln_b;
+    r.dgate = dgate;
+    hipLaunchKernelGGL(seq_embed_bwd_reduce_k, dim3((unsigned)((a.part_w + 63) / 64)), dim3(256), 0, st, r);
+  }
   RSX_LAUNCHED();
   return 0;
 }

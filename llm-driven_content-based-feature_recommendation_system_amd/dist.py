@@ -13,7 +13,10 @@ single-GPU step on the rank-major concatenated global batch:
     are all-gathered (autograd-aware: their gradients are all-reduced back to the owners);
   * every loss is a sum over local rows divided by the GLOBAL row count, so the per-rank
     objectives add up to the single-GPU objective, and the replicated parameters' gradients
-    are summed with one bucketed all-reduce before clipping.
+    are summed by bucketed all-reduces launched from gradient hooks during backward
+    (GradBucket), finished before clipping;
+  * the data-dependent step index (row counts, target ids) is exchanged over a second
+    communicator (index_group) from the prefetch stream, ahead of the step that uses it.
 Only the collective helpers here are device-agnostic (gloo-tested on CPU); the losses call
 the HIP kernels through ops.
 """
@@ -31,18 +34,61 @@ def world():
     return 0, 1
 
 
-def all_gather_counts(n: int, device) -> list:
-    """Every rank's local row count (one tiny all-gather + host read)."""
+def _host_staged(t: torch.Tensor, group=None) -> bool:
+    """gloo carries device tensors only for some collectives: stage them through host memory
+    (the CPU test transport; production runs use RCCL, which takes device pointers)."""
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
+def all_gather_into(bufs, t: torch.Tensor, group=None) -> None:
+    if _host_staged(t, group):
+        cb = [torch.empty(t.shape, dtype=t.dtype) for _ in bufs]
+        dist.all_gather(cb, t.cpu(), group=group)
+        for b, c in zip(bufs, cb):
+            b.copy_(c)
+        return
+    dist.all_gather(bufs, t, group=group)
+
+
+def all_reduce_(t: torch.Tensor, op=None, group=None, async_op=False):
+    """In-place all-reduce (sum by default). Returns the work handle when async_op and the
+    transport is asynchronous, else None."""
+    op = dist.ReduceOp.SUM if op is None else op
+    if _host_staged(t, group):
+        c = t.cpu()
+        dist.all_reduce(c, op=op, group=group)
+        t.copy_(c)
+        return None
+    return dist.all_reduce(t, op=op, group=group, async_op=async_op)
+
+
+_INDEX_GROUP = None
+
+
+def index_group():
+    """A second communicator for the step-index exchanges (row counts, target ids). Under RCCL
+    each communicator has its own stream, so the next batch's index exchange, issued from the
+    prefetch side stream while the current step runs, never queues behind that step's gradient
+    all-reduce. Created lazily; every rank reaches the first call at the same point."""
+    global _INDEX_GROUP
+    if _INDEX_GROUP is None:
+        _INDEX_GROUP = dist.new_group(backend=dist.get_backend())
+    return _INDEX_GROUP
+
+
+def all_gather_counts(n: int, device, group=None) -> list:
+    """Every rank's local row count (one tiny all-gather + host read). Called only while a
+    StepIndex is built (ahead of the step, on the prefetch stream, over index_group())."""
     rank, ws = world()
     if ws == 1:
         return [int(n)]
     t = torch.tensor([int(n)], device=device, dtype=torch.int64)
     out = [torch.empty_like(t) for _ in range(ws)]
-    dist.all_gather(out, t)
-    return [int(x.item()) for x in out]
+    all_gather_into(out, t, group=group)
+    return torch.cat(out).tolist()
 
 
-def all_gather_var(x: torch.Tensor, counts: list) -> torch.Tensor:
+def all_gather_var(x: torch.Tensor, counts: list, group=None) -> torch.Tensor:
     """Concatenate every rank's x[:counts[r]] (rank-major). Not differentiable."""
     rank, ws = world()
     if ws == 1:
@@ -51,7 +97,7 @@ def all_gather_var(x: torch.Tensor, counts: list) -> torch.Tensor:
     pad = torch.zeros((mx,) + tuple(x.shape[1:]), device=x.device, dtype=x.dtype)
     pad[: x.shape[0]] = x
     bufs = [torch.empty_like(pad) for _ in range(ws)]
-    dist.all_gather(bufs, pad)
+    all_gather_into(bufs, pad, group=group)
     return torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0)
 
 
@@ -70,7 +116,7 @@ class _AllGatherRows(torch.autograd.Function):
     def backward(ctx, g):
         g = g.contiguous()
         if world()[1] > 1:
-            dist.all_reduce(g)
+            all_reduce_(g)
         return g[ctx.lo: ctx.lo + ctx.n], None
 
 
@@ -82,44 +128,116 @@ def all_gather_rows(x: torch.Tensor, counts: list) -> torch.Tensor:
 
 def all_reduce_sum_(t: torch.Tensor) -> torch.Tensor:
     if world()[1] > 1:
-        dist.all_reduce(t)
+        all_reduce_(t)
     return t
 
 
 class GradBucket:
-    """One flat fp32 all-reduce over every replicated parameter's gradient (DDP semantics,
-    sum over ranks). Parameters without a gradient contribute zeros, so every rank issues
-    the same collective."""
+    """Sum of the replicated parameters' gradients over ranks (DDP semantics), overlapped with
+    backward. Parameters are grouped into ~bucket_mb buckets in reverse registration order (the
+    order backward produces them); a post-accumulate-grad hook copies each gradient into its
+    bucket's flat fp32 buffer, and a bucket's all-reduce is launched (asynchronously, on the
+    communicator's stream) as soon as it and every earlier bucket are complete, so the
+    exchange runs under the rest of backward. Launch order is the bucket index on every rank.
+    Each bucket carries one has-gradient flag per parameter in the same buffer: after the
+    exchange a parameter whose gradient is None on EVERY rank stays None (the single-GPU step's
+    AdamW skips it), otherwise its gradient becomes the summed slice (a view of the bucket).
+    Call the bucket after backward to launch what is left and wait."""
 
-    def __init__(self, params):
+    def __init__(self, params, bucket_mb: float = 16.0):
         self.params = [p for p in params if p.requires_grad]
         self.numel = sum(p.numel() for p in self.params)
+        cap = max(1, int(bucket_mb * (1 << 20) / 4))
+        self.buckets = []          # [[param index, ...], ...]
+        cur, size = [], 0
+        for i in reversed(range(len(self.params))):
+            n = self.params[i].numel()
+            if cur and size + n > cap:
+                self.buckets.append(cur)
+                cur, size = [], 0
+            cur.append(i)
+            size += n
+        if cur:
+            self.buckets.append(cur)
+        self.where = {}            # param index -> (bucket, offset, slot)
+        self.sizes = []
+        for b, idx in enumerate(self.buckets):
+            o = 0
+            for s, i in enumerate(idx):
+                self.where[i] = (b, o, s)
+                o += self.params[i].numel()
+            self.sizes.append(o)
         self.flat = None
+        self.by_id = {id(p): i for i, p in enumerate(self.params)}
+        self.handles = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
+        self._reset()
+
+    def _reset(self):
+        self.filled = [0] * len(self.buckets)
+        self.work = [None] * len(self.buckets)
+        self.launched = 0
+        self.active = False
+
+    def _buffers(self, dev):
+        if self.flat is None or self.flat[0].device != dev:
+            # [bucket values..., one has-grad flag per parameter]
+            self.flat = [torch.empty(n + len(idx), device=dev, dtype=torch.float32)
+                         for n, idx in zip(self.sizes, self.buckets)]
+        return self.flat
+
+    def _on_grad(self, p):
+        if world()[1] == 1:
+            return
+        i = self.by_id[id(p)]
+        b, o, s = self.where[i]
+        if not self.active:
+            self.active = True
+            bufs = self._buffers(p.device)
+            for f, n in zip(bufs, self.sizes):
+                f[n:].zero_()
+        f = self.flat[b]
+        f[o:o + p.numel()].copy_(p.grad.reshape(-1))
+        f[self.sizes[b] + s].fill_(1.0)
+        self.filled[b] += 1
+        while self.launched < len(self.buckets) and self.filled[self.launched] == len(self.buckets[self.launched]):
+            self._launch(self.launched)
+
+    def _launch(self, b):
+        self.work[b] = all_reduce_(self.flat[b], async_op=True)
+        self.launched += 1
 
     def __call__(self):
         if world()[1] == 1 or not self.params:
             return
-        dev = self.params[0].device
-        if self.flat is None or self.flat.device != dev:
-            self.flat = torch.empty(self.numel, device=dev, dtype=torch.float32)
-        o = 0
-        for p in self.params:
-            n = p.numel()
-            if p.grad is None:
-                self.flat[o:o + n].zero_()
-            else:
-                self.flat[o:o + n].copy_(p.grad.reshape(-1))
-            o += n
-        dist.all_reduce(self.flat)
-        o = 0
-        for p in self.params:
-            n = p.numel()
-            g = self.flat[o:o + n].view_as(p)
-            if p.grad is None:
-                p.grad = g.clone()
-            else:
-                p.grad.copy_(g)
-            o += n
+        if not self.active:
+            self.active = True
+            bufs = self._buffers(self.params[0].device)
+            for f, n in zip(bufs, self.sizes):
+                f[n:].zero_()
+        # buckets still open: parameters without a gradient on this rank contribute zeros
+        for b in range(self.launched, len(self.buckets)):
+            f = self.flat[b]
+            for i in self.buckets[b]:
+                p = self.params[i]
+                if p.grad is None:
+                    _, o, _ = self.where[i]
+                    f[o:o + p.numel()].zero_()
+        while self.launched < len(self.buckets):
+            self._launch(self.launched)
+        for b, w in enumerate(self.work):
+            if w is not None:
+                w.wait()
+        for b, idx in enumerate(self.buckets):
+            f = self.flat[b]
+            flags = f[self.sizes[b]:]
+            has = (flags > 0).tolist() if any(self.params[i].grad is None for i in idx) else None
+            for s, i in enumerate(idx):
+                p = self.params[i]
+                _, o, _ = self.where[i]
+                if p.grad is None and not (has and has[s]):
+                    continue
+                p.grad = f[o:o + p.numel()].view_as(p)
+        self._reset()
 
 
 class StepIndex:
@@ -141,16 +259,17 @@ def prepare_step_index(batch, pretrained_vecs=None, pretrained_lookup=None) -> S
     ix.packed = pack_inputs(batch, pretrained_vecs, pretrained_lookup)
     pk = ix.packed[0]
     ix.B = B
-    ix.counts = all_gather_counts(pk.valid_tok.numel(), device)
+    grp = index_group() if ws > 1 else None
+    ix.counts = all_gather_counts(pk.valid_tok.numel(), device, group=grp)
     ix.n_glob = sum(ix.counts)
     ix.groups = None
     if ix.n_glob > 0:
         t_loc = target_ids.reshape(-1)[pk.flat[pk.valid_tok]]
         user_loc = pk.tok_user[pk.valid_tok] + rank * B
-        t_glob = all_gather_var(t_loc, ix.counts)
+        t_glob = all_gather_var(t_loc, ix.counts, group=grp)
         ix.groups = ops.TargetGroups(t_loc, user_loc, t_cols=t_glob)
     ix.last_t = target_ids.reshape(-1)[pk.flat[pk.last_tok]]
-    ix.t_glob_last = all_gather_var(ix.last_t, [B] * ws)
+    ix.t_glob_last = all_gather_var(ix.last_t, [B] * ws, group=grp)
     return ix
 
 
@@ -309,8 +428,8 @@ def retrieve_topk_sharded(queries, item_shard, shard_offset, k, local_topk=None,
     if ws > 1:
         ss = [torch.empty_like(s) for _ in range(ws)]
         ii = [torch.empty_like(i) for _ in range(ws)]
-        dist.all_gather(ss, s.contiguous(), group=group)
-        dist.all_gather(ii, i.contiguous(), group=group)
+        all_gather_into(ss, s.contiguous(), group=group)
+        all_gather_into(ii, i.contiguous(), group=group)
         s = torch.cat(ss, 1)
         i = torch.cat(ii, 1)
     s, i = merge_topk(s, i, k)

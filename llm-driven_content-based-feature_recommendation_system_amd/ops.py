@@ -114,11 +114,14 @@ class _SeqEmbed(torch.autograd.Function):
         if seg0 is not None and dbase is None:
             dbase = torch.empty_like(base)
         kern_tabs = ([None] + dtabs[1:]) if seg0 is not None else dtabs
-        rc = N.lib().rsx_seq_embed_bwd(
-            N.ptr(base), N.ptr_array(ids), N.ptr_array(tables), rows,
-            N.i64_array(padding_idx), nt, N.ptr(gate), N.ptr(pos), N.ptr(tok_pos), N.ptr(ln_w), N.ptr(mean),
-            N.ptr(rstd), eps, T, L, D, p_drop, seed, N.ptr(dout), N.ptr(dbase), N.ptr_array(kern_tabs),
-            N.ptr(dgate), N.ptr(dpos), N.ptr(dlnw), N.ptr(dlnb), N.stream())
+        nws = N.lib().rsx_seq_embed_bwd_workspace_floats(T, L, D)
+        ws = torch.empty(nws, device=base.device, dtype=torch.float32)
+        with timed("seq_embed_bwd"):
+            rc = N.lib().rsx_seq_embed_bwd(
+                N.ptr(base), N.ptr_array(ids), N.ptr_array(tables), rows,
+                N.i64_array(padding_idx), nt, N.ptr(gate), N.ptr(pos), N.ptr(tok_pos), N.ptr(ln_w), N.ptr(mean),
+                N.ptr(rstd), eps, T, L, D, p_drop, seed, N.ptr(dout), N.ptr(dbase), N.ptr_array(kern_tabs),
+                N.ptr(dgate), N.ptr(dpos), N.ptr(dlnw), N.ptr(dlnb), N.ptr(ws), nws, N.stream())
         N.check(rc, "seq_embed_bwd")
         if seg0 is not None:  # chunk partials, then per-id sums of its chunks (both deterministic)
             perm, cb, chunk_ids, ch_off, uniq = seg0

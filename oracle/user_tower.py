@@ -162,6 +162,37 @@ def inbatch_corrected_logq_loss(user_emb, item_tower_emb, target_ids, user_ids, 
     return F.cross_entropy(logits, torch.arange(n))
 
 
+def inbatch_corrected_logq_loss_chunked(user_emb, item_tower_emb, target_ids, user_ids, log_q_tensor,
+                                        temperature=0.1, lambda_logq=1.0, chunk=2048):
+    """inbatch_corrected_logq_loss (v1_refine_usertower.py:826-861) over row chunks of the N x N
+    logits, each chunk under activation checkpointing: the same per-element arithmetic (matmul,
+    /tau, - logQ per column, -inf off-diagonal same-item / same-user mask, CE), with the mean taken
+    as the sum of chunk sums / N. Bounded RAM (chunk x N floats) at the sizes where the reference's
+    one-shot N x N tensors do not fit (N ~ 153k valid steps at batch 8192)."""
+    from torch.utils.checkpoint import checkpoint
+    n = user_emb.size(0)
+    cols = item_tower_emb[target_ids]
+    bias = log_q_tensor[target_ids].view(1, -1) * lambda_logq if lambda_logq > 0.0 else None
+
+    def part(u, c, r0):
+        r1 = r0 + u.size(0)
+        logits = torch.matmul(u, c.T)
+        logits.div_(temperature)
+        if bias is not None:
+            logits = logits - bias
+        mask = (target_ids[r0:r1].unsqueeze(1) == target_ids.unsqueeze(0)) | \
+               (user_ids[r0:r1].unsqueeze(1) == user_ids.unsqueeze(0))
+        rows = torch.arange(r1 - r0, device=u.device)
+        mask[rows, rows + r0] = False
+        logits.masked_fill_(mask, float("-inf"))
+        return F.cross_entropy(logits, rows + r0, reduction="sum")
+
+    total = user_emb.new_zeros(())
+    for r0 in range(0, n, chunk):
+        total = total + checkpoint(part, user_emb[r0:r0 + chunk], cols, r0, use_reentrant=False)
+    return total / n
+
+
 def inbatch_corrected_logq_loss_no_user(user_emb, item_tower_emb, target_ids, log_q_tensor, temperature=0.1,
                                         lambda_logq=1.0):
     """Shadowed first definition, v1_refine_usertower.py:520-573."""
@@ -211,8 +242,9 @@ _FWD_KEYS = ("item_ids", "time_bucket_ids", "type_ids", "color_ids", "graphic_id
 
 
 def contrastive_losses(model, item_matrix, log_q_tensor, batch, pretrained_lookup, lambda_logq=1.0,
-                       lambda_sup=0.1, lambda_cl=0.2):
-    """Forward part of train_user_tower_all_time, v1_usertower_train.py:757-845 (fp32, no AMP)."""
+                       lambda_sup=0.1, lambda_cl=0.2, loss_chunk=None):
+    """Forward part of train_user_tower_all_time, v1_usertower_train.py:757-845 (fp32, no AMP).
+    loss_chunk: evaluate the main loss row-chunked (inbatch_corrected_logq_loss_chunked)."""
     kw = {k: batch[k] for k in _FWD_KEYS}
     kw["pretrained_vecs"] = pretrained_lookup[batch["item_ids"]]                  # :760
     kw["training_mode"] = True
@@ -225,9 +257,10 @@ def contrastive_losses(model, item_matrix, log_q_tensor, batch, pretrained_looku
     flat_targets = target_ids[valid]
     flat_user_ids = torch.arange(bsz).unsqueeze(1).expand(-1, seq_len)[valid]      # :803-804
     if flat_output.size(0) > 0:
-        main = inbatch_corrected_logq_loss(F.normalize(flat_output, p=2, dim=1),
-                                           F.normalize(item_matrix, p=2, dim=1), flat_targets, flat_user_ids,
-                                           log_q_tensor, temperature=0.1, lambda_logq=lambda_logq)
+        kw = {"chunk": loss_chunk} if loss_chunk else {}
+        fn = inbatch_corrected_logq_loss_chunked if loss_chunk else inbatch_corrected_logq_loss
+        main = fn(F.normalize(flat_output, p=2, dim=1), F.normalize(item_matrix, p=2, dim=1), flat_targets,
+                  flat_user_ids, log_q_tensor, temperature=0.1, lambda_logq=lambda_logq, **kw)
     else:
         main = torch.tensor(0.0)
     last = (valid.sum(dim=1) - 1).clamp(min=0)                                     # :830
@@ -236,10 +269,12 @@ def contrastive_losses(model, item_matrix, log_q_tensor, batch, pretrained_looku
     return main + lambda_cl * cl, main, cl
 
 
-def contrastive_step(model, item_matrix_param, log_q_tensor, batch, optimizer, pretrained_lookup, max_norm=5.0):
+def contrastive_step(model, item_matrix_param, log_q_tensor, batch, optimizer, pretrained_lookup, max_norm=5.0,
+                     loss_chunk=None):
     """One optimiser step (:850-854, without GradScaler: fp32 on CPU)."""
     optimizer.zero_grad()
-    total, main, cl = contrastive_losses(model, item_matrix_param, log_q_tensor, batch, pretrained_lookup)
+    total, main, cl = contrastive_losses(model, item_matrix_param, log_q_tensor, batch, pretrained_lookup,
+                                         loss_chunk=loss_chunk)
     total.backward()
     torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=max_norm)
     optimizer.step()

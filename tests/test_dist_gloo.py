@@ -50,21 +50,37 @@ def _worker(rank, world, port, q):
         X2 = X1 + 0.1 * torch.randn(8, 16, generator=g)
         b = 8 // world
         w_loc = Wt.clone().requires_grad_()
-        z1 = F.normalize(X1[rank * b:(rank + 1) * b] @ w_loc, dim=1)
-        z2 = F.normalize(X2[rank * b:(rank + 1) * b] @ w_loc, dim=1)
-        z2_glob = D.all_gather_rows(z2, [b] * world)
-        obj = _dense_rows_loss(z1, z2_glob, rank * b) / 8.0
-        obj.backward()
-        bucket = D.GradBucket([w_loc])
-        bucket()
+        # hook-driven buckets (~1 KB each: several buckets, launched during backward); `unused`
+        # gets no gradient on any rank (stays None), `partial` only on rank 0 (summed anyway)
+        unused = torch.zeros(5, requires_grad=True)
+        partial = torch.ones(300, requires_grad=True)
+        bias = torch.zeros(128, requires_grad=True)
+        bucket = D.GradBucket([w_loc, unused, partial, bias], bucket_mb=1e-3)
+        assert len(bucket.buckets) > 2
+        for step in range(2):   # the second step reuses the buckets
+            for p in (w_loc, unused, partial, bias):
+                p.grad = None
+            z1 = F.normalize(X1[rank * b:(rank + 1) * b] @ w_loc + bias, dim=1)
+            z2 = F.normalize(X2[rank * b:(rank + 1) * b] @ w_loc + bias, dim=1)
+            z2_glob = D.all_gather_rows(z2, [b] * world)
+            obj = _dense_rows_loss(z1, z2_glob, rank * b) / 8.0
+            if rank == 0:
+                obj = obj + partial.square().sum()
+            obj.backward()
+            bucket()
         total = obj.detach().clone()
         D.all_reduce_sum_(total)
         # single-process reference
         w_ref = Wt.clone().requires_grad_()
-        ref = _dense_rows_loss(F.normalize(X1 @ w_ref, dim=1), F.normalize(X2 @ w_ref, dim=1), 0) / 8.0
+        b_ref = torch.zeros(128, requires_grad=True)
+        ref = _dense_rows_loss(F.normalize(X1 @ w_ref + b_ref, dim=1), F.normalize(X2 @ w_ref + b_ref, dim=1),
+                               0) / 8.0
         ref.backward()
-        torch.testing.assert_close(total, ref.detach(), atol=1e-6, rtol=1e-6)
+        torch.testing.assert_close(total, ref.detach() + 300.0, atol=1e-5, rtol=1e-6)
         torch.testing.assert_close(w_loc.grad, w_ref.grad, atol=1e-6, rtol=1e-5)
+        torch.testing.assert_close(bias.grad, b_ref.grad, atol=1e-6, rtol=1e-5)
+        assert unused.grad is None
+        torch.testing.assert_close(partial.grad, torch.full((300,), 2.0))
         q.put((rank, "ok"))
     except Exception as e:  # pragma: no cover - reported to the parent
         q.put((rank, repr(e)))

@@ -35,6 +35,24 @@ def test_library_exports_every_declared_symbol():
     assert lib.rsx_target_arch() == b"gfx950"
 
 
+def _prototypes():
+    """{name: parameter count} of every prototype in the header."""
+    text = open(HEADER).read()
+    out = {}
+    for m in re.finditer(r"^(?:int64_t|int|const char\*)\s+(rsx_\w+)\(([^;]*?)\);", text, flags=re.M | re.S):
+        params = m.group(2).strip()
+        out[m.group(1)] = 0 if params in ("", "void") else params.count(",") + 1
+    return out
+
+
+def test_ctypes_signatures_match_header_arity():
+    protos = _prototypes()
+    assert set(protos) == set(_declared())
+    for name, n in protos.items():
+        assert name in _native._SIGS, name
+        assert len(_native._SIGS[name][1]) == n, f"{name}: header has {n} parameters, ctypes {len(_native._SIGS[name][1])}"
+
+
 def test_argument_errors_are_reported_without_a_gpu():
     if not os.path.exists(_native.LIB_PATH):
         pytest.skip("library not built")
