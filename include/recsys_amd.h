@@ -272,6 +272,19 @@ int64_t rsx_deepfm_fused_workspace_bytes(int F);
 int rsx_deepfm_fused(const int64_t* x, int64_t R, int F, const float* const* V, const float* const* W, float bias,
                      const float* w1, const float* b1, const float* w2, const float* b2, const float* wo, void* ws,
                      float* logit, float* prob, void* stream);
+/* The two halves of rsx_deepfm_fused, for callers that keep ws across calls (the weight images
+ * are a function of w1/w2 only: rebuild them with rsx_deepfm_fused_prep after an update).
+ * F in [25, 48] runs the persistent kernel (one workgroup per CU looping over 64-row blocks). */
+int rsx_deepfm_fused_prep(int F, const float* w1, const float* w2, void* ws, void* stream);
+/* packed: nullable per-field tables from rsx_deepfm_pack, read by the persistent kernel (F in
+ * [25, 48]: rsx_deepfm_fused_uses_packed(F) == 1) instead of V/W: a field's V row and first-order
+ * weight then share one 128-B line, halving the lines fetched per (row, field) on random ids. */
+int rsx_deepfm_fused_run(const int64_t* x, int64_t R, int F, const float* const* V, const float* const* W,
+                         const float* const* packed, float bias, const float* b1, const float* b2, const float* wo,
+                         const void* ws, float* logit, float* prob, void* stream);
+/* packed [vocab][32] = (V [vocab][16] row, W [vocab] (0 if NULL), 15 zeros): one field's table. */
+int rsx_deepfm_pack(const float* V, const float* W, int64_t vocab, float* packed, void* stream);
+int rsx_deepfm_fused_uses_packed(int F);
 
 /* ---- A9: item-tower RE path ------------------------------------------------------------
  * out[t] = LayerNorm((word[ids[t]] + type_row) + pos[tok_pos[t]]) * ln_w + ln_b over packed

@@ -321,12 +321,458 @@ __global__ __launch_bounds__(256) void deepfm_prep_k(const float* w1, int F, int
   }
 }
 
+// ---- persistent form (F in [25, 48]) ------------------------------------------------------
+// One 512-thread workgroup per CU loops over 64-row blocks; fields in chunks of 8. The per-block
+// latency chain of deepfm_fused_k (id staging, W1 ring prologue, the layer-2 barriers at one
+// workgroup per CU: 0.11 ms of its 0.19 ms with the gathers disabled) overlaps with useful work:
+//  * loader waves stage the next block's ids during chunk 0, its first two chunks during the
+//    compute waves' layer-1 tail and epilogue, so every chunk is in LDS before it is needed;
+//  * the compute waves' W1 fragment ring runs on across block boundaries (no prologue);
+//  * layer 2 is split by n2 (each compute wave 32 outputs over all k) from relu(H1 + b1)
+//    exchanged through LDS in bf16 hi/lo, so it needs no cross-wave partial sums; the four
+//    waves' per-row dot products with w_o meet in LDS, the loaders add bias + first + FM.
+// Barrier sequence per block (both roles, same order): A_0 .. A_{C-1} (chunk j staged),
+// E1 (layer 1 done: its buffers free), E2 (h1 written), E3 (per-row partials written).
+constexpr int kFC2 = 8;                   // fields per chunk
+constexpr int kChunk2 = kFC2 * kBM * 16;  // bf16 per image per chunk
+constexpr int kH1Stride = kN1 + 8;        // bf16 per h1 row (528 B: conflict-free row reads)
+constexpr int kPersistMaxF = 48;
+constexpr int kRing2 = 6;  // W1 fragment ring depth of the persistent kernel (fields ahead)
+
+struct PArgs {
+  const int64_t* x;
+  const float* V[kMaxF];
+  const float* W[kMaxF];
+  const float* P[kMaxF];     // packed [vocab_f][32] (V row, W, pad: one 128-B line per id) or nullptr
+  int64_t R;
+  int F, nchunk, id_stride;
+  int64_t nrb;               // row blocks
+  float bias;
+  const __bf16* w1hi;        // [nchunk*8][256][16]
+  const __bf16* w1lo;
+  const float* b1;
+  const __bf16* w2hi;        // [128][256] natural k order
+  const __bf16* w2lo;
+  const float* b2;
+  const float* wo;
+  float* logit;
+  float* prob;
+};
+
+__global__ __launch_bounds__(512, 1) void deepfm_persist_k(PArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __bf16* xhi = reinterpret_cast<__bf16*>(smem);                  // [2][8][64][16]
+  __bf16* xlo = xhi + 2 * kChunk2;
+  __bf16* h1hi = xlo + 2 * kChunk2;                               // [64][264]
+  __bf16* h1lo = h1hi + kBM * kH1Stride;
+  float* red = reinterpret_cast<float*>(h1lo + kBM * kH1Stride);  // [4][64]
+  int* ids = reinterpret_cast<int*>(red + 4 * kBM);               // [2][64][id_stride]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, c = lane & 31;
+  const int C = a.nchunk, nf = C * kFC2;
+  const int64_t nit = (a.nrb - blockIdx.x + gridDim.x - 1) / gridDim.x;
+  auto rb_of = [&](int64_t it) -> int64_t { return blockIdx.x + it * (int64_t)gridDim.x; };
+
+  if (wave >= 4) {
+    // ---------------- loaders: row gr, quarter q (floats 4q..4q+3 of every field)
+    const int lt = tid - 256, gr = lt >> 2, q = lt & 3;
+    float4 vA[kFC2], vB[kFC2], vC[kFC2];  // three register sets: global chunk g uses set g % 3
+    float wA[kFC2], wB[kFC2], wC[kFC2];
+    float4 fs = make_float4(0.f, 0.f, 0.f, 0.f), fss = fs;
+    float first = 0.0f;
+    auto load_ids = [&](int64_t it) {  // ids of block it -> ids[it & 1] (int32), coalesced
+      const int64_t m0 = rb_of(it) * kBM;
+      int* dst = ids + (it & 1) * kBM * a.id_stride;
+      for (int i = lt; i < kBM * a.F; i += 256) {
+        const int r = i / a.F, f = i - r * a.F;
+        const int64_t row = m0 + r < a.R ? m0 + r : a.R - 1;  // tail rows re-read the last row; never stored
+        dst[r * a.id_stride + f] = (int)a.x[row * a.F + f];
+      }
+    };
+    auto issue_set = [&](int64_t it, int j, float4 (&vb)[kFC2], float (&wv)[kFC2]) {
+      const int* idr = ids + (it & 1) * kBM * a.id_stride + gr * a.id_stride;
+#pragma unroll
+      for (int k = 0; k < kFC2; ++k) {
+        const int f = j * kFC2 + k;
+        vb[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        wv[k] = 0.0f;
+        if (f < a.F) {
+          const int id = idr[f];
+          if (a.P[0]) {  // packed: the V row and W of one id share a 128-B line
+            const float* pr = a.P[f] + (int64_t)id * 32;
+            vb[k] = reinterpret_cast<const float4*>(pr)[q];
+            if (q == (f & 3)) wv[k] = pr[16];
+          } else {
+            vb[k] = reinterpret_cast<const float4*>(a.V[f] + (int64_t)id * 16)[q];
+            if (q == (f & 3) && a.W[f]) wv[k] = a.W[f][id];
+          }
+        }
+      }
+    };
+    auto consume_set = [&](int buf, const float4 (&vb)[kFC2], const float (&wv)[kFC2]) {
+#pragma unroll
+      for (int k = 0; k < kFC2; ++k) {
+        const float4 v = vb[k];
+        fs.x += v.x; fs.y += v.y; fs.z += v.z; fs.w += v.w;
+        fss.x += v.x * v.x; fss.y += v.y * v.y; fss.z += v.z * v.z; fss.w += v.w * v.w;
+        first += wv[k];
+        bf16x4 hi, lo;
+        split4(v, hi, lo);
+        const int o = buf * kChunk2 + (k * kBM + gr) * 16 + 4 * q;
+        *reinterpret_cast<u32x2*>(&xhi[o]) = __builtin_bit_cast(u32x2, hi);
+        *reinterpret_cast<u32x2*>(&xlo[o]) = __builtin_bit_cast(u32x2, lo);
+      }
+    };
+    float fm_out = 0.0f, first_out = 0.0f;
+    auto finalize_fm = [&]() {  // the block's FM / first terms per row (4 quarters summed)
+      float fm = (fs.x * fs.x - fss.x) + (fs.y * fs.y - fss.y) + (fs.z * fs.z - fss.z) + (fs.w * fs.w - fss.w);
+      fm += __shfl_xor(fm, 1, 64);
+      fm += __shfl_xor(fm, 2, 64);
+      float fi = first + __shfl_xor(first, 1, 64);
+      fi += __shfl_xor(fi, 2, 64);
+      fm_out = fm;
+      first_out = fi;
+      fs = make_float4(0.f, 0.f, 0.f, 0.f);
+      fss = fs;
+      first = 0.0f;
+    };
+    auto write_logits = [&](int64_t it) {  // after E3(it): the compute waves' per-row partials
+      const int64_t row = rb_of(it) * kBM + gr;
+      if (q == 0 && row < a.R) {
+        const float dnn = ((red[gr] + red[kBM + gr]) + red[2 * kBM + gr]) + red[3 * kBM + gr];
+        const float v = a.bias + first_out + 0.5f * fm_out + dnn;
+        a.logit[row] = v;
+        if (a.prob) a.prob[row] = 1.0f / (1.0f + expf(-v));
+      }
+    };
+    // One step per global chunk g = (it, j) = (g / C, g % C): rows of chunk g+2 issued into the
+    // third register set (two chunks of gathers in flight), chunk g consumed into LDS buffer
+    // g & 1, then the barriers that separate staging chunk g from staging chunk g+1 (see the
+    // sequence above): chunks (it, 0) and (it, 1) are staged during block it-1's layer-1 tail /
+    // epilogue, chunk (it, j >= 2) between A_{j-1} and A_j; the next block's ids are loaded
+    // between A_0 and A_1 (C >= 4: they are visible before chunk (it+1, 0) is issued at step
+    // (it, C-2), which follows A_{C-3}).
+    const int64_t G = nit * C;
+    auto step = [&](int64_t g, float4 (&vc)[kFC2], float (&wc)[kFC2], float4 (&vn)[kFC2], float (&wn)[kFC2]) {
+      const int64_t it = g / C;
+      const int j = (int)(g - it * C);
+      if (j == 0 && it > 0) finalize_fm();
+      if (g + 2 < G) issue_set((g + 2) / C, (int)((g + 2) % C), vn, wn);
+      consume_set((int)(g & 1), vc, wc);
+      if (j == 0) {
+        if (it > 0) __syncthreads();  // E1(it-1)
+      } else if (j == 1) {
+        if (it > 0) {
+          __syncthreads();  // E2(it-1)
+          __syncthreads();  // E3(it-1)
+          write_logits(it - 1);
+        }
+        __syncthreads();  // A_0(it)
+        if (it + 1 < nit) load_ids(it + 1);
+        __syncthreads();  // A_1(it)
+      } else {
+        __syncthreads();  // A_j(it)
+      }
+    };
+    if (nit > 0) load_ids(0);
+    __syncthreads();  // P
+    if (G > 0) issue_set(0, 0, vA, wA);
+    if (G > 1) issue_set(1 / C, 1 % C, vB, wB);
+    for (int64_t g = 0; g < G; g += 3) {
+      step(g, vA, wA, vC, wC);
+      if (g + 1 < G) step(g + 1, vB, wB, vA, wA);
+      if (g + 2 < G) step(g + 2, vC, wC, vB, wB);
+    }
+    if (nit > 0) {
+      finalize_fm();
+      __syncthreads();  // E1(last)
+      __syncthreads();  // E2(last)
+      __syncthreads();  // E3(last)
+      write_logits(nit - 1);
+    }
+    return;
+  }
+
+  // ---------------- compute waves
+  const int nw0 = 64 * wave;
+  const __bf16* w1h = a.w1hi + ((int64_t)nw0 + c) * 16 + 8 * h;
+  const __bf16* w1l = a.w1lo + ((int64_t)nw0 + c) * 16 + 8 * h;
+  auto wload = [&](int f, bf16x8 (&wh)[2], bf16x8 (&wl)[2]) {
+    const int ff = f % nf;  // the ring runs on into the next block's fields
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      wh[j] = *reinterpret_cast<const bf16x8*>(w1h + ((int64_t)ff * kN1 + 32 * j) * 16);
+      wl[j] = *reinterpret_cast<const bf16x8*>(w1l + ((int64_t)ff * kN1 + 32 * j) * 16);
+    }
+  };
+  bf16x8 rh[kRing2][2], rl[kRing2][2];
+#pragma unroll
+  for (int d = 0; d < kRing2; ++d) wload(d, rh[d], rl[d]);
+  __syncthreads();  // P
+  for (int64_t it = 0; it < nit; ++it) {
+    f32x16 acc[2][2];  // [m-tile i][n-tile j]: D[n = nw0 + 32j + tile_row][m = 32i + c]
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+    for (int ch = 0; ch < C; ++ch) {
+      __syncthreads();  // A_ch
+      const int buf = (int)((it * C + ch) & 1);
+#pragma unroll
+      for (int f = 0; f < kFC2; ++f) {
+        bf16x8 xh[2], xl[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int o = buf * kChunk2 + (f * kBM + 32 * i + c) * 16 + 8 * h;
+          xh[i] = *reinterpret_cast<const bf16x8*>(&xhi[o]);
+          xl[i] = *reinterpret_cast<const bf16x8*>(&xlo[o]);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rl[0][j], xh[i], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rh[0][j], xl[i], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rh[0][j], xh[i], acc[i][j], 0, 0, 0);
+          }
+#pragma unroll
+        for (int d = 0; d + 1 < kRing2; ++d)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            rh[d][j] = rh[d + 1][j];
+            rl[d][j] = rl[d + 1][j];
+          }
+        wload(ch * kFC2 + f + kRing2, rh[kRing2 - 1], rl[kRing2 - 1]);
+      }
+    }
+    __syncthreads();  // E1
+    // h1 = relu(H1 + b1) -> LDS hi/lo: lane (c, h) holds rows 32i + c, n = nw0 + 32j + 8g + 4h + e
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 bb = *reinterpret_cast<const float4*>(a.b1 + nw0 + 32 * j + 8 * g + 4 * h);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const float4 v = make_float4(fmaxf(acc[i][j][4 * g + 0] + bb.x, 0.0f), fmaxf(acc[i][j][4 * g + 1] + bb.y, 0.0f),
+                                       fmaxf(acc[i][j][4 * g + 2] + bb.z, 0.0f), fmaxf(acc[i][j][4 * g + 3] + bb.w, 0.0f));
+          bf16x4 hi, lo;
+          split4(v, hi, lo);
+          const int o = (32 * i + c) * kH1Stride + nw0 + 32 * j + 8 * g + 4 * h;
+          *reinterpret_cast<u32x2*>(&h1hi[o]) = __builtin_bit_cast(u32x2, hi);
+          *reinterpret_cast<u32x2*>(&h1lo[o]) = __builtin_bit_cast(u32x2, lo);
+        }
+      }
+    __syncthreads();  // E2
+    // layer 2, n2 in [32 wave, 32 wave + 32): D[n2][m] = sum_k W2[n2][k] h1[m][k]
+    f32x16 acc2[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc2[i][r] = 0.0f;
+    const int n2 = 32 * wave + c;
+    const __bf16* w2h = a.w2hi + (int64_t)n2 * kN1 + 8 * h;
+    const __bf16* w2l = a.w2lo + (int64_t)n2 * kN1 + 8 * h;
+#pragma unroll 4
+    for (int s = 0; s < kN1 / 16; ++s) {
+      const bf16x8 ah = *reinterpret_cast<const bf16x8*>(w2h + 16 * s);
+      const bf16x8 al = *reinterpret_cast<const bf16x8*>(w2l + 16 * s);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int o = (32 * i + c) * kH1Stride + 16 * s + 8 * h;
+        const bf16x8 bh = *reinterpret_cast<const bf16x8*>(&h1hi[o]);
+        const bf16x8 bl = *reinterpret_cast<const bf16x8*>(&h1lo[o]);
+        acc2[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc2[i], 0, 0, 0);
+        acc2[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc2[i], 0, 0, 0);
+        acc2[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc2[i], 0, 0, 0);
+      }
+    }
+    // relu(H2 + b2) . w_o over this wave's 32 n2 (register r: n2 = 32 wave + tile_row(r, h))
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      float sdot = 0.0f;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int nb = 32 * wave + 8 * g + 4 * h;
+        const float4 bb = *reinterpret_cast<const float4*>(a.b2 + nb);
+        const float4 ww = *reinterpret_cast<const float4*>(a.wo + nb);
+        sdot += fmaxf(acc2[i][4 * g + 0] + bb.x, 0.0f) * ww.x;
+        sdot += fmaxf(acc2[i][4 * g + 1] + bb.y, 0.0f) * ww.y;
+        sdot += fmaxf(acc2[i][4 * g + 2] + bb.z, 0.0f) * ww.z;
+        sdot += fmaxf(acc2[i][4 * g + 3] + bb.w, 0.0f) * ww.w;
+      }
+      sdot += __shfl_xor(sdot, 32, 64);
+      if (h == 0) red[wave * kBM + 32 * i + c] = sdot;
+    }
+    __syncthreads();  // E3
+  }
+}
+
+// Weight images of the persistent form: W1 [256][F*16] -> [nchunk*8][256][16] hi/lo (zero past
+// F); W2 [128][256] -> [128][256] hi/lo (natural k order).
+__global__ __launch_bounds__(256) void deepfm_prep2_k(const float* w1, int F, int nchunk, const float* w2,
+                                                      __bf16* w1hi, __bf16* w1lo, __bf16* w2hi, __bf16* w2lo) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n1 = (int64_t)nchunk * kFC2 * kN1 * 16;
+  float v;
+  __bf16 *dh, *dl;
+  if (i < n1) {
+    const int k = (int)(i % 16), n = (int)((i / 16) % kN1), f = (int)(i / (16 * kN1));
+    v = f < F ? w1[(int64_t)n * F * 16 + f * 16 + k] : 0.0f;
+    dh = w1hi + i;
+    dl = w1lo + i;
+  } else if (i - n1 < (int64_t)kN2 * kN1) {
+    v = w2[i - n1];
+    dh = w2hi + (i - n1);
+    dl = w2lo + (i - n1);
+  } else {
+    return;
+  }
+  const __bf16 hv = (__bf16)v;
+  *dh = hv;
+  *dl = (__bf16)(v - (float)hv);
+}
+
+// packed table of one field: out[id][0..15] = V[id], out[id][16] = W[id] (0 if W is null),
+// out[id][17..31] = 0; one thread per 16-B chunk
+__global__ __launch_bounds__(256) void deepfm_pack_k(const float* V, const float* W, int64_t vocab, float* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (id, chunk 0..7)
+  if (i >= vocab * 8) return;
+  const int64_t id = i >> 3;
+  const int ch = (int)(i & 7);
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (ch < 4) v = reinterpret_cast<const float4*>(V + id * 16)[ch];
+  else if (ch == 4 && W) v.x = W[id];
+  reinterpret_cast<float4*>(out + id * 32)[ch] = v;
+}
+
+size_t persist_lds_bytes(int id_stride) {
+  return (size_t)4 * kChunk2 * sizeof(__bf16) + 2 * (size_t)kBM * kH1Stride * sizeof(__bf16) +
+         4 * kBM * sizeof(float) + 2 * (size_t)kBM * id_stride * sizeof(int);
+}
+
+int cu_count() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return v > 0 ? v : 256;
+  }();
+  return n;
+}
+
+bool persist_ok(int F) { return F >= 3 * kFC2 + 1 && F <= kPersistMaxF && getenv("RSX_DEEPFM_PERSIST") == nullptr; }
+
 }  // namespace
 
 RSX_API int64_t rsx_deepfm_fused_workspace_bytes(int F) {
   if (F < 1 || F > kMaxF) return -1;
-  const int64_t nchunk = (F + kFC - 1) / kFC;
-  return 2 * (nchunk * kFC * kN1 * 16 + 16 * kN2 * 16) * (int64_t)sizeof(__bf16);
+  const int64_t nchunk = (F + kFC - 1) / kFC, nchunk2 = (F + kFC2 - 1) / kFC2;
+  const int64_t w1 = nchunk * kFC * kN1 * 16 > nchunk2 * kFC2 * kN1 * 16 ? nchunk * kFC * kN1 * 16
+                                                                          : nchunk2 * kFC2 * kN1 * 16;
+  return 2 * (w1 + 16 * kN2 * 16) * (int64_t)sizeof(__bf16);
+}
+
+namespace {
+// Builds the weight images of the kernel form rsx_deepfm_fused_run takes for F fields.
+int deepfm_prep_images(int F, const float* w1, const float* w2, __bf16* wsb, hipStream_t st) {
+  if (persist_ok(F)) {
+    const int nchunk = (F + kFC2 - 1) / kFC2;
+    const int64_t m1 = (int64_t)nchunk * kFC2 * kN1 * 16, m2 = (int64_t)kN2 * kN1;
+    hipLaunchKernelGGL(deepfm_prep2_k, dim3((unsigned)((m1 + m2 + 255) / 256)), dim3(256), 0, st, w1, F, nchunk,
+                       w2, wsb, wsb + m1, wsb + 2 * m1, wsb + 2 * m1 + m2);
+  } else {
+    const int nchunk = (F + kFC - 1) / kFC;
+    const int64_t n1 = (int64_t)nchunk * kFC * kN1 * 16, n2 = 16 * kN2 * 16;
+    hipLaunchKernelGGL(deepfm_prep_k, dim3((unsigned)((n1 + n2 + 255) / 256)), dim3(256), 0, st, w1, F, nchunk, w2,
+                       wsb, wsb + n1, wsb + 2 * n1, wsb + 2 * n1 + n2);
+  }
+  return 0;
+}
+}  // namespace
+
+RSX_API int rsx_deepfm_fused_prep(int F, const float* w1, const float* w2, void* ws, void* stream) {
+  RSX_ARG(w1 && w2 && ws, "null tensor");
+  RSX_ARG(F >= 1 && F <= kMaxF, "F must be in [1,64]");
+  deepfm_prep_images(F, w1, w2, reinterpret_cast<__bf16*>(ws), (hipStream_t)stream);
+  RSX_LAUNCHED();
+  return 0;
+}
+
+RSX_API int rsx_deepfm_pack(const float* V, const float* W, int64_t vocab, float* packed, void* stream) {
+  RSX_ARG(V && packed, "null tensor");
+  RSX_ARG(vocab >= 0, "vocab must be >= 0");
+  if (vocab == 0) return 0;
+  hipLaunchKernelGGL(deepfm_pack_k, dim3((unsigned)((vocab * 8 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, V, W,
+                     vocab, packed);
+  RSX_LAUNCHED();
+  return 0;
+}
+
+RSX_API int rsx_deepfm_fused_uses_packed(int F) { return persist_ok(F) ? 1 : 0; }
+
+RSX_API int rsx_deepfm_fused_run(const int64_t* x, int64_t R, int F, const float* const* V, const float* const* W,
+                                 const float* const* packed, float bias, const float* b1, const float* b2,
+                                 const float* wo, const void* ws, float* logit, float* prob, void* stream) {
+  RSX_ARG(x && V && b1 && b2 && wo && ws && logit, "null tensor");
+  RSX_ARG(F >= 1 && F <= kMaxF, "F must be in [1,64]");
+  if (R == 0) return 0;
+  for (int f = 0; f < F; ++f) RSX_ARG(V[f] != nullptr, "null field table");
+  const __bf16* wsb = reinterpret_cast<const __bf16*>(ws);
+  hipStream_t st = (hipStream_t)stream;
+  if (persist_ok(F)) {
+    PArgs p;
+    p.x = x;
+    for (int f = 0; f < kMaxF; ++f) {
+      p.V[f] = f < F ? V[f] : nullptr;
+      p.W[f] = (f < F && W) ? W[f] : nullptr;
+      p.P[f] = (f < F && packed) ? packed[f] : nullptr;
+    }
+    if (packed)
+      for (int f = 0; f < F; ++f) RSX_ARG(packed[f] != nullptr, "null packed table");
+    p.R = R;
+    p.F = F;
+    p.nchunk = (F + kFC2 - 1) / kFC2;
+    p.id_stride = F | 1;  // odd: the loaders' per-row id reads fall on distinct banks
+    p.nrb = (R + kBM - 1) / kBM;
+    p.bias = bias;
+    const int64_t m1 = (int64_t)p.nchunk * kFC2 * kN1 * 16, m2 = (int64_t)kN2 * kN1;
+    p.w1hi = wsb;
+    p.w1lo = wsb + m1;
+    p.w2hi = wsb + 2 * m1;
+    p.w2lo = wsb + 2 * m1 + m2;
+    p.b1 = b1; p.b2 = b2; p.wo = wo; p.logit = logit; p.prob = prob;
+    const int64_t grid = p.nrb < cu_count() ? p.nrb : cu_count();
+    static const bool attr = [] {  // > 64 KB of dynamic LDS per workgroup
+      return hipFuncSetAttribute(reinterpret_cast<const void*>(&deepfm_persist_k),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+    }();
+    (void)attr;
+    hipLaunchKernelGGL(deepfm_persist_k, dim3((unsigned)grid), dim3(512), persist_lds_bytes(p.id_stride), st, p);
+    RSX_LAUNCHED();
+    return 0;
+  }
+  FArgs a;
+  a.x = x;
+  for (int f = 0; f < kMaxF; ++f) {
+    a.V[f] = f < F ? V[f] : nullptr;
+    a.W[f] = (f < F && W) ? W[f] : nullptr;
+  }
+  a.R = R;
+  a.F = F;
+  a.nchunk = (F + kFC - 1) / kFC;
+  a.bias = bias;
+  const int64_t n1 = (int64_t)a.nchunk * kFC * kN1 * 16, n2 = 16 * kN2 * 16;
+  a.w1hi = wsb;
+  a.w1lo = wsb + n1;
+  a.w2hi = wsb + 2 * n1;
+  a.w2lo = wsb + 2 * n1 + n2;
+  a.b1 = b1; a.b2 = b2; a.wo = wo; a.logit = logit; a.prob = prob;
+  hipLaunchKernelGGL(deepfm_fused_k, dim3((unsigned)((R + kBM - 1) / kBM)), dim3(512), 0, st, a);
+  RSX_LAUNCHED();
+  return 0;
 }
 
 RSX_API int rsx_deepfm_fused(const int64_t* x, int64_t R, int F, const float* const* V, const float* const* W,
@@ -335,29 +781,7 @@ RSX_API int rsx_deepfm_fused(const int64_t* x, int64_t R, int F, const float* co
   RSX_ARG(x && V && w1 && b1 && w2 && b2 && wo && ws && logit, "null tensor");
   RSX_ARG(F >= 1 && F <= kMaxF, "F must be in [1,64]");
   if (R == 0) return 0;
-  FArgs a;
-  a.x = x;
-  for (int f = 0; f < kMaxF; ++f) {
-    a.V[f] = f < F ? V[f] : nullptr;
-    a.W[f] = (f < F && W) ? W[f] : nullptr;
-  }
-  for (int f = 0; f < F; ++f) RSX_ARG(a.V[f] != nullptr, "null field table");
-  a.R = R;
-  a.F = F;
-  a.nchunk = (F + kFC - 1) / kFC;
-  a.bias = bias;
-  __bf16* wsb = reinterpret_cast<__bf16*>(ws);
-  const int64_t n1 = (int64_t)a.nchunk * kFC * kN1 * 16, n2 = 16 * kN2 * 16;
-  a.w1hi = wsb;
-  a.w1lo = wsb + n1;
-  a.w2hi = wsb + 2 * n1;
-  a.w2lo = wsb + 2 * n1 + n2;
-  a.b1 = b1; a.b2 = b2; a.wo = wo; a.logit = logit; a.prob = prob;
-  hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(deepfm_prep_k, dim3((unsigned)((n1 + n2 + 255) / 256)), dim3(256), 0, st, w1, F, a.nchunk, w2,
-                     wsb, wsb + n1, wsb + 2 * n1, wsb + 2 * n1 + n2);
-  RSX_LAUNCHED();
-  hipLaunchKernelGGL(deepfm_fused_k, dim3((unsigned)((R + kBM - 1) / kBM)), dim3(512), 0, st, a);
-  RSX_LAUNCHED();
-  return 0;
+  const int rc = rsx_deepfm_fused_prep(F, w1, w2, ws, stream);
+  if (rc != 0) return rc;
+  return rsx_deepfm_fused_run(x, R, F, V, W, nullptr, bias, b1, b2, wo, ws, logit, prob, stream);
 }

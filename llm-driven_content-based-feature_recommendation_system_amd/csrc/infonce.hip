@@ -1917,6 +1917,7 @@ __global__ __launch_bounds__(256, 2) void nce_bwd_x3_k(BwdArgs a, X3Args x) {
 // (two sweeps of S) with one sweep; the backward keeps only the column pass.
 // Per split: part = (m ln2, l) per row as the plain forward, dpart[split][row][128] = O.
 constexpr float kLazyLog2 = 8.0f;
+template <int PRIO>
 __global__ __launch_bounds__(256, 2) void nce_grouped_fwdg_x3_k(GArgs a) {
   __shared__ __attribute__((aligned(16))) X3Tile sT[2];
   __shared__ __attribute__((aligned(16))) float sB2[2][kTile];   // -bias_d * log2e (-inf past the split)
@@ -1978,6 +1979,7 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_fwdg_x3_k(GArgs a) {
       const bool exc = (int64_t)next < j0 + kTile;  // before the prefetch (see the backward)
       if (has_next) gload(j0 + kTile);
       f32x16 acc = dots_x3(sT[cur], c, h, uh, ul);
+      if (PRIO) __builtin_amdgcn_s_setprio(PRIO);  // experiment: the softmax's VALU ahead of the partner wave
       // registers 4g..4g+3 hold tile rows 8g + 4h + 0..3: one b128 read per group and array
       // (an immediate offset from a per-lane base) instead of 16 scalar reads with 32 address ops
       float w[16];
@@ -2016,7 +2018,10 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_fwdg_x3_k(GArgs a) {
       float tmax = -INFINITY;
 #pragma unroll
       for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, acc[r]);
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      {  // max with the partner lane c ^ 32: v_permlane32_swap (VALU) instead of an LDS permute
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(tmax), __float_as_uint(tmax), false, false);
+        tmax = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+      }
       if (!row_ok) tmax = -INFINITY;
       const bool raise = tmax > m + kLazyLog2;  // m = -inf: the first finite tile
       if (__any(raise)) {
@@ -2046,6 +2051,7 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_fwdg_x3_k(GArgs a) {
       l += ls;
       bf16x8 gh[2], gl[2];
       split_tile(acc, gh, gl);
+      if (PRIO) __builtin_amdgcn_s_setprio(0);
       grad_x3s(gacc, gh, gl, sT[cur], lane);
       if (has_next) lstore(cur ^ 1);
       __builtin_amdgcn_s_waitcnt(kVmcnt0);  // nothing pending at the loop head on any path
@@ -2070,369 +2076,6 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_fwdg_x3_k(GArgs a) {
     if (orow < a.N) {
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) dst[orow * kD + kb * 32 + c] = gacc[kb][r];
-    }
-  }
-}
-
-// ---- v2 of the fused forward: 64 owner rows per wave, two 32-row sub-tiles pipelined ------
-// One wave per SIMD (occupancy 1). Per streamed tile the wave runs
-//     S_a | S_b + softmax_a | G_a + softmax_b | G_b
-// (S_x: the 24 MFMAs of sub-tile x's logit tile, G_x: the 24 MFMAs of its row-gradient
-// product, softmax_x: its logits -> max / lazy raise / exp / split on the VALU), so the vector
-// work of one sub-tile fills the MFMA issue gaps of the other's chain (an MFMA blocks vector
-// issue for 8 of its 32 cycles; MI355X_MICROARCH.md constants table). Both sub-tiles share
-// every tile fragment read and the per-tile barrier. Register budget: sub-tile a's owner
-// fragments and both gradient accumulators in registers, sub-tile b's owner fragments in LDS
-// (16 KB per wave, lane-contiguous: conflict-free ds_read_b128). The user's own targets
-// (exception columns) enter as a per-lane weight adjustment wadj (column weight c_d - wadj;
-// the label column gets weight 1), formed before the sub-tile's softmax starts.
-// Per element the arithmetic is that of nce_grouped_fwdg_x3_k (same products, same lazy max,
-// same split); part / dout are written in the same layout and merged by nce_grouped_merge_g_k.
-constexpr int kOwnRows2 = 64 * kWaves;  // owner rows per workgroup
-
-__device__ __forceinline__ float pair_max(float v) {  // max over lanes c and c ^ 32
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
-}
-
-// per-sub-tile softmax state
-struct SmState {
-  float m, l;       // running max (base 2, same on both lane halves) and this lane's partial sum
-  float alpha;      // rescale factor of the sub-tile's gradient rows for this tile (1: none)
-  bool raise_any;   // some lane of the wave raised its max on this tile
-  bool ok;          // owner row in range
-};
-
-// Piece k (0..7) of one sub-tile's softmax: x (its S accumulator, rewritten in place) ->
-// e = w * 2^(x - m), split into hi/lo fragments gh/gl. Pieces 0-1 form x (biases read from
-// LDS per piece; EXC: columns whose adjusted weight is 0 masked) and the tile max, piece 2
-// combines it across the lane halves and decides the lazy raise (the caller rescales the
-// gradient rows after the chain: st.alpha / st.raise_any), pieces 3-7 exponentiate and split.
-template <bool EXC>
-__device__ __forceinline__ void softmax_piece(int k, f32x16& x, const float (&wadj)[16], const float* scnt,
-                                              const float* snb, float it2, float& tmax, SmState& st, int h,
-                                              bf16x8 (&gh)[2], bf16x8 (&gl)[2], float& ls) {
-  if (k < 2) {
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
-      const int r = 8 * k + 4 * g;
-      const float4 bv = *reinterpret_cast<const float4*>(&snb[8 * (2 * k + g) + 4 * h]);
-      x[r + 0] = fmaf(x[r + 0], it2, bv.x);
-      x[r + 1] = fmaf(x[r + 1], it2, bv.y);
-      x[r + 2] = fmaf(x[r + 2], it2, bv.z);
-      x[r + 3] = fmaf(x[r + 3], it2, bv.w);
-      if (EXC) {
-        const float4 cw = *reinterpret_cast<const float4*>(&scnt[8 * (2 * k + g) + 4 * h]);
-        if (!(cw.x - wadj[r + 0] > 0.0f)) x[r + 0] = -INFINITY;
-        if (!(cw.y - wadj[r + 1] > 0.0f)) x[r + 1] = -INFINITY;
-        if (!(cw.z - wadj[r + 2] > 0.0f)) x[r + 2] = -INFINITY;
-        if (!(cw.w - wadj[r + 3] > 0.0f)) x[r + 3] = -INFINITY;
-      }
-    }
-    float t = k == 0 ? -INFINITY : tmax;
-#pragma unroll
-    for (int j = 0; j < 8; j += 2) t = fmaxf(t, fmaxf(x[8 * k + j], x[8 * k + j + 1]));
-    tmax = t;
-  } else if (k == 2) {
-    float t = pair_max(tmax);
-    if (!st.ok) t = -INFINITY;
-    const bool raise = t > st.m + kLazyLog2;  // m = -inf: the first finite tile
-    st.alpha = raise ? ((st.m == -INFINITY) ? 0.0f : __builtin_amdgcn_exp2f(st.m - t)) : 1.0f;
-    st.raise_any = __any(raise);
-    if (raise) {
-      st.l *= st.alpha;
-      st.m = t;
-    }
-    tmax = (st.m == -INFINITY) ? 0.0f : st.m;  // from here on: the exponent offset
-    ls = 0.0f;
-  } else {
-    // pieces 3..7: rows [lo, hi) = [0,2) [2,6) [6,10) [10,14) [14,16) (even bounds: each row
-    // pair is exponentiated and split within one piece)
-    const int lo = k == 3 ? 0 : 4 * (k - 3) - 2, hi = k == 7 ? 16 : 4 * (k - 2) - 2;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      if (r >= lo && r < hi) {
-        float wr = scnt[tile_row(r, h)];
-        if (EXC) wr -= wadj[r];
-        x[r] = wr * __builtin_amdgcn_exp2f(x[r] - tmax);  // wr >= 0 where x is finite
-        ls += x[r];
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      if (2 * q >= lo && 2 * q < hi) {
-        uint32_t hp, lp;
-        split_pair(x[2 * q], x[2 * q + 1], hp, lp);
-        u32x4 hv = __builtin_bit_cast(u32x4, gh[q >> 2]), lv = __builtin_bit_cast(u32x4, gl[q >> 2]);
-        hv[q & 3] = hp;
-        lv[q & 3] = lp;
-        gh[q >> 2] = __builtin_bit_cast(bf16x8, hv);
-        gl[q >> 2] = __builtin_bit_cast(bf16x8, lv);
-      }
-    }
-    if (k == 7) st.l += ls;
-  }
-}
-
-// rows of a sub-tile's gradient accumulator scaled by their owners' alpha (lazy raise),
-// exchanged through the wave's LDS row
-__device__ __forceinline__ void rescale_rows(f32x16 (&gacc)[4], const SmState& st, float* salpha, int c, int h) {
-  if (!st.raise_any) return;
-  if (h == 0) salpha[c] = st.alpha;
-  __builtin_amdgcn_wave_barrier();
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const float al = salpha[tile_row(r, h)];
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb) gacc[kb][r] *= al;
-  }
-  __builtin_amdgcn_wave_barrier();
-}
-
-// S chain of sub-tile b (owner fragments in LDS: own[s][lane] hi, own[8 + s][lane] lo, 16 B
-// each) on the tile image t, with the softmax pieces of sub-tile a interleaved per k-step.
-template <bool EXC>
-__device__ __forceinline__ f32x16 dots_lds_sm_x3(const X3Tile& t, int c, int h, int lane, const bf16x8* own,
-                                                 f32x16& x, const float (&wadj)[16], const float* scnt,
-                                                 const float* snb, float it2, SmState& st, bf16x8 (&gh)[2],
-                                                 bf16x8 (&gl)[2]) {
-  f32x16 acc;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-  const int base = img_off(c, 64 * h);
-  bf16x8 ah = *reinterpret_cast<const bf16x8*>(&t.hi[base]);
-  bf16x8 al = *reinterpret_cast<const bf16x8*>(&t.lo[base]);
-  bf16x8 uh = own[lane], ul = own[8 * 64 + lane];
-  float tmax = 0.0f, ls = 0.0f;
-#pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    bf16x8 nh = ah, nl = al, nuh = uh, nul = ul;
-    if (s < 7) {
-      nh = *reinterpret_cast<const bf16x8*>(&t.hi[base + 8 * (s + 1)]);
-      nl = *reinterpret_cast<const bf16x8*>(&t.lo[base + 8 * (s + 1)]);
-      nuh = own[(s + 1) * 64 + lane];
-      nul = own[(8 + s + 1) * 64 + lane];
-    }
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, uh, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, ul, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, uh, acc, 0, 0, 0);
-    softmax_piece<EXC>(s, x, wadj, scnt, snb, it2, tmax, st, h, gh, gl, ls);
-    __builtin_amdgcn_sched_barrier(0);
-    ah = nh;
-    al = nl;
-    uh = nuh;
-    ul = nul;
-  }
-  return acc;
-}
-
-// G chain of sub-tile a (gacc += G^T X, as grad_x3s) with the softmax pieces of sub-tile b
-// interleaved per step.
-template <bool EXC>
-__device__ __forceinline__ void grad_sm_x3(f32x16 (&gacc)[4], const bf16x8 (&gh)[2], const bf16x8 (&gl)[2],
-                                           const X3Tile& t, int lane, f32x16& x, const float (&wadj)[16],
-                                           const float* scnt, const float* snb, float it2, SmState& st,
-                                           bf16x8 (&gh2)[2], bf16x8 (&gl2)[2]) {
-  const int q = (lane >> 2) & 3, p = lane & 3, h = lane >> 5, cb = (lane >> 4) & 1;
-  const int base = img_off(4 * h + q, 16 * cb + 4 * p);
-  auto rd = [&](const __bf16* img, int step, bf16x8& out) {
-    const int ks = step >> 2, nb2 = step & 3;
-    const int o0 = base + img_off(16 * ks, 32 * nb2), o1 = base + img_off(16 * ks + 8, 32 * nb2);
-    const bf16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(&img[o0]));
-    const bf16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(&img[o1]));
-    out = __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
-  };
-  bf16x8 bh, bl;
-  rd(t.hi, 0, bh);
-  rd(t.lo, 0, bl);
-  float tmax = 0.0f, ls = 0.0f;
-#pragma unroll
-  for (int step = 0; step < 8; ++step) {
-    bf16x8 nh = bh, nl = bl;
-    if (step < 7) {
-      rd(t.hi, step + 1, nh);
-      rd(t.lo, step + 1, nl);
-    }
-    const int ks = step >> 2, nbk = step & 3;
-    gacc[nbk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gl[ks], bh, gacc[nbk], 0, 0, 0);
-    gacc[nbk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gh[ks], bl, gacc[nbk], 0, 0, 0);
-    gacc[nbk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gh[ks], bh, gacc[nbk], 0, 0, 0);
-    softmax_piece<EXC>(step, x, wadj, scnt, snb, it2, tmax, st, h, gh2, gl2, ls);
-    __builtin_amdgcn_sched_barrier(0);
-    bh = nh;
-    bl = nl;
-  }
-}
-
-// per-lane weight adjustment of one sub-tile for the tile [j0, j0 + 32): wadj[r] = number of
-// the row user's own columns equal to tile column tile_row(r, h) (removed by the same-user
-// mask), and c_d - 1 on the row's label column (its weight is 1). Walks the sorted exception
-// list with the lane's monotone pointer.
-__device__ __forceinline__ void exc_adjust(float (&wadj)[16], const float* scnt, const int* exc_cols, int64_t j0,
-                                           int64_t j_end, int h, int di, int& p, int e, int& next) {
-  constexpr int kNone = 0x7fffffff;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) wadj[r] = 0.0f;
-  if (!((int64_t)next < j0 + kTile)) return;
-  int q = p;
-  for (; q < e && (int64_t)exc_cols[q] < j0 + kTile; ++q) {
-    const int tk = (int)(exc_cols[q] - j0);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) wadj[r] += (tk == tile_row(r, h)) ? 1.0f : 0.0f;
-  }
-  const int tl = ((int64_t)di < j_end && (int64_t)di >= j0) ? (int)(di - j0) : -1;
-#pragma unroll
-  for (int r = 0; r < 16; ++r)
-    if (tile_row(r, h) == tl) wadj[r] = scnt[tl] - 1.0f;
-  p = q;
-  next = (p < e) ? exc_cols[p] : kNone;
-}
-
-__global__ __launch_bounds__(256, 1) void nce_grouped_fwdg2_x3_k(GArgs a) {
-  __shared__ __attribute__((aligned(16))) X3Tile sT[2];
-  __shared__ __attribute__((aligned(16))) bf16x8 sOwn[kWaves][16 * 64];  // sub-tile b owner fragments
-  __shared__ __attribute__((aligned(16))) float sB2[2][kTile];   // -bias_d * log2e (-inf past the split)
-  __shared__ __attribute__((aligned(16))) float sCnt[2][kTile];  // c_d (0 past the split)
-  __shared__ __attribute__((aligned(16))) float sAlpha[kWaves][2][32];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int h = lane >> 5, c = lane & 31;
-  int split, rb;
-  remap_block(a.nsplit, split, rb);
-  const int64_t ia = (int64_t)rb * kOwnRows2 + wave * 64 + c, ib = ia + 32;
-  SmState sa, sb;
-  sa.ok = ia < a.N;
-  sb.ok = ib < a.N;
-  sa.m = sb.m = -INFINITY;
-  sa.l = sb.l = 0.0f;
-  sa.alpha = sb.alpha = 1.0f;
-  sa.raise_any = sb.raise_any = false;
-  bf16x8 uha[8], ula[8];
-  {
-    bf16x8 uhb[8], ulb[8];
-    load_owner_x3(uhb, ulb, a.A, ib, a.lda, sb.ok, h);
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      sOwn[wave][s * 64 + lane] = uhb[s];
-      sOwn[wave][(8 + s) * 64 + lane] = ulb[s];
-    }
-  }
-  load_owner_x3(uha, ula, a.A, ia, a.lda, sa.ok, h);
-  const bf16x8* own_b = &sOwn[wave][0];
-  const int64_t j_begin = (int64_t)split * a.span;
-  int64_t j_end = j_begin + a.span;
-  if (j_end > a.M) j_end = a.M;
-  constexpr int kNone = 0x7fffffff;
-  int dia = -1, pa = 0, ea = 0, nexta = kNone;
-  int dib = -1, pb = 0, eb = 0, nextb = kNone;
-  if (sa.ok) {
-    dia = a.row_col[ia];
-    ea = a.row_end[ia];
-    pa = lower_bound_i(a.exc_cols, a.row_beg[ia], ea, j_begin);
-    nexta = (pa < ea) ? a.exc_cols[pa] : kNone;
-  }
-  if (sb.ok) {
-    dib = a.row_col[ib];
-    eb = a.row_end[ib];
-    pb = lower_bound_i(a.exc_cols, a.row_beg[ib], eb, j_begin);
-    nextb = (pb < eb) ? a.exc_cols[pb] : kNone;
-  }
-  const float it2 = a.inv_tau * kLog2e;
-  f32x16 gacca[4], gaccb[4];
-#pragma unroll
-  for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      gacca[kb][r] = 0.0f;
-      gaccb[kb][r] = 0.0f;
-    }
-  X3Stage stg;
-  float stg_b = 0.0f, stg_c = 0.0f;
-  auto gload = [&](int64_t j0) {
-    const int64_t j = j0 + (tid >> 3);
-    stg.load(a.bhi, a.blo, j, j < j_end, tid);
-    if (tid < kTile) {
-      const int64_t jj = j0 + tid;
-      const bool ok = jj < j_end;
-      stg_b = ok ? (a.bias ? a.bias[jj] : 0.0f) : INFINITY;
-      stg_c = ok ? a.colcnt[jj] : 0.0f;
-    }
-  };
-  auto lstore = [&](int buf) {
-    stg.store(sT[buf], tid);
-    if (tid < kTile) {
-      sB2[buf][tid] = -(stg_b * kLog2e);
-      sCnt[buf][tid] = stg_c;
-    }
-  };
-  if (j_begin < j_end) {
-    gload(j_begin);
-    lstore(0);
-    __syncthreads();
-    int cur = 0;
-    float* salpha_a = &sAlpha[wave][0][0];
-    float* salpha_b = &sAlpha[wave][1][0];
-    for (int64_t j0 = j_begin; j0 < j_end; j0 += kTile) {
-      const bool has_next = j0 + kTile < j_end;
-      // exception flags before the prefetch is issued (their walks load; a wait on those must
-      // not drain the prefetch)
-      const bool exca = __any((int64_t)nexta < j0 + kTile), excb = __any((int64_t)nextb < j0 + kTile);
-      const float* scnt = sCnt[cur];
-      const float* snb = sB2[cur];
-      float wadj[16];
-      if (exca) exc_adjust(wadj, scnt, a.exc_cols, j0, j_end, h, dia, pa, ea, nexta);
-      if (has_next) gload(j0 + kTile);
-      bf16x8 gha[2], gla[2], ghb[2], glb[2];
-      f32x16 xa = dots_x3(sT[cur], c, h, uha, ula);  // S_a
-      f32x16 xb;
-      if (exca)  // S_b + softmax_a
-        xb = dots_lds_sm_x3<true>(sT[cur], c, h, lane, own_b, xa, wadj, scnt, snb, it2, sa, gha, gla);
-      else
-        xb = dots_lds_sm_x3<false>(sT[cur], c, h, lane, own_b, xa, wadj, scnt, snb, it2, sa, gha, gla);
-      rescale_rows(gacca, sa, salpha_a, c, h);
-      if (excb) {  // G_a + softmax_b
-        exc_adjust(wadj, scnt, a.exc_cols, j0, j_end, h, dib, pb, eb, nextb);
-        grad_sm_x3<true>(gacca, gha, gla, sT[cur], lane, xb, wadj, scnt, snb, it2, sb, ghb, glb);
-      } else {
-        grad_sm_x3<false>(gacca, gha, gla, sT[cur], lane, xb, wadj, scnt, snb, it2, sb, ghb, glb);
-      }
-      rescale_rows(gaccb, sb, salpha_b, c, h);
-      grad_x3s(gaccb, ghb, glb, sT[cur], lane);  // G_b
-      if (has_next) lstore(cur ^ 1);
-      __builtin_amdgcn_s_waitcnt(kVmcnt0);  // nothing pending at the loop head on any path
-      __syncthreads();
-      cur ^= 1;
-    }
-  }
-  const int64_t stride = (int64_t)a.nsplit * a.N;
-  const float lta = sa.l + __shfl_xor(sa.l, 32, 64), ltb = sb.l + __shfl_xor(sb.l, 32, 64);
-  if (h == 0) {
-    if (sa.ok) {
-      const int64_t o = (int64_t)split * a.N + ia;
-      a.part[o] = (sa.m == -INFINITY) ? -INFINITY : sa.m * kLn2;
-      a.part[stride + o] = lta;
-      a.part[2 * stride + o] = 0.0f;
-      a.part[3 * stride + o] = 0.0f;
-    }
-    if (sb.ok) {
-      const int64_t o = (int64_t)split * a.N + ib;
-      a.part[o] = (sb.m == -INFINITY) ? -INFINITY : sb.m * kLn2;
-      a.part[stride + o] = ltb;
-      a.part[2 * stride + o] = 0.0f;
-      a.part[3 * stride + o] = 0.0f;
-    }
-  }
-  const int64_t own_base = (int64_t)rb * kOwnRows2 + wave * 64;
-  float* dst = a.dout + (int64_t)split * a.N * kD;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int64_t oa = own_base + tile_row(r, h), ob = oa + 32;
-    if (oa < a.N) {
-#pragma unroll
-      for (int kb = 0; kb < 4; ++kb) dst[oa * kD + kb * 32 + c] = gacca[kb][r];
-    }
-    if (ob < a.N) {
-#pragma unroll
-      for (int kb = 0; kb < 4; ++kb) dst[ob * kD + kb * 32 + c] = gaccb[kb][r];
     }
   }
 }
@@ -2846,18 +2489,6 @@ RSX_API int rsx_nce_grouped_fwd(const float* A, const float* B, const float* bia
   return 0;
 }
 
-namespace {
-// RSX_NCE_FWDG2=1 selects the experimental pipelined 64-row forward (nce_grouped_fwdg2_x3_k;
-// 1.6x slower than nce_grouped_fwdg_x3_k on MI355X at batch 8192)
-bool fwdg_pipelined() {
-  static const bool on = [] {
-    const char* s = getenv("RSX_NCE_FWDG2");
-    return s && s[0] == '1';
-  }();
-  return on;
-}
-}  // namespace
-
 RSX_API int rsx_nce_grouped_fwd_grad(const float* A, const float* B, const float* bias, const float* colcnt,
                                      const int* row_col, const int* row_beg, const int* row_end,
                                      const int* exc_cols, int64_t N, int64_t D, int64_t lda, int64_t ldb, float tau,
@@ -2892,13 +2523,14 @@ RSX_API int rsx_nce_grouped_fwd_grad(const float* A, const float* B, const float
   g.blo = im.blo;
   launch_split(B, ldb, D, im.bhi, im.blo, st);
   RSX_LAUNCHED();
-  if (fwdg_pipelined()) {
-    const int blocks = (int)(((N + kOwnRows2 - 1) / kOwnRows2) * nsplit);
-    hipLaunchKernelGGL(nce_grouped_fwdg2_x3_k, dim3(blocks), dim3(256), 0, st, g);
-  } else {
-    const int blocks = (int)(((N + kOwnRows - 1) / kOwnRows) * nsplit);
-    hipLaunchKernelGGL(nce_grouped_fwdg_x3_k, dim3(blocks), dim3(256), 0, st, g);
-  }
+  const int blocks = (int)(((N + kOwnRows - 1) / kOwnRows) * nsplit);
+  static const int prio = [] {
+    const char* e = getenv("RSX_NCE_FWDG_PRIO");  // experiment knob (default 0: off)
+    return e ? atoi(e) : 0;
+  }();
+  if (prio == 1) hipLaunchKernelGGL(nce_grouped_fwdg_x3_k<1>, dim3(blocks), dim3(256), 0, st, g);
+  else if (prio == 2) hipLaunchKernelGGL(nce_grouped_fwdg_x3_k<2>, dim3(blocks), dim3(256), 0, st, g);
+  else hipLaunchKernelGGL(nce_grouped_fwdg_x3_k<0>, dim3(blocks), dim3(256), 0, st, g);
   RSX_LAUNCHED();
   hipLaunchKernelGGL(nce_grouped_merge_g_k, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, A, B, bias, row_col,
                      N, lda, ldb, g.inv_tau, nsplit, part, opart, lse, row_loss, row_valid, ga);

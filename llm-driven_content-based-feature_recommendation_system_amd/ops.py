@@ -1042,15 +1042,19 @@ def linear(x, weight, bias=None, act=ACT_NONE):
 
 # RSX_DEEPFM_FUSED=0 selects the three-kernel path (gather+FM, fp32-MFMA linears) for A/B runs
 _DEEPFM_FUSED = os.environ.get("RSX_DEEPFM_FUSED", "1") != "0"
+# packed inference tables for the persistent DeepFM kernel (RSX_DEEPFM_PACK=0: read V / W directly)
+_DEEPFM_PACK = os.environ.get("RSX_DEEPFM_PACK", "1") != "0"
 
 
-def deepfm_forward(x, emb_tables, lin_tables, out_bias, dnn_weights, dnn_biases, w_out):
+def deepfm_forward(x, emb_tables, lin_tables, out_bias, dnn_weights, dnn_biases, w_out, cache=None):
     """DeepFM logits/probabilities for x [R, F] int64 (see csrc/deepfm.hip).
 
     emb_tables: F tensors [vocab_f, 16]; lin_tables: F tensors [vocab_f] (or [vocab_f, 1]);
     dnn_weights/dnn_biases: torch Linear layout, ReLU between layers; w_out [H_last].
     Config-3 shapes (E 16, DNN (256, 128)) run the single fused kernel (rsx_deepfm_fused, bf16x3
-    DNN products); other shapes the gather + fp32-MFMA linear kernels. Returns (logit [R], prob [R])."""
+    DNN products); other shapes the gather + fp32-MFMA linear kernels. cache: a dict owned by the
+    caller (the DeepFM module) that keeps the fused kernel's bf16 weight images between calls,
+    rebuilt when either DNN weight changes (storage or in-place version). Returns (logit [R], prob [R])."""
     N.ensure_device(x)
     x = _c(x)
     R, F = x.shape
@@ -1060,12 +1064,33 @@ def deepfm_forward(x, emb_tables, lin_tables, out_bias, dnn_weights, dnn_biases,
             and tuple(dnn_weights[1].shape) == (128, 256)):
         logit = torch.empty(R, device=dev, dtype=torch.float32)
         prob = torch.empty(R, device=dev, dtype=torch.float32)
-        ws = torch.empty(N.lib().rsx_deepfm_fused_workspace_bytes(F), device=dev, dtype=torch.uint8)
+        w1, w2 = _c(dnn_weights[0]), _c(dnn_weights[1])
+        key = (F, w1.data_ptr(), w1._version, w2.data_ptr(), w2._version, dev)
         b1, b2 = dnn_biases
         with timed("deepfm/fused"):
-            rc = N.lib().rsx_deepfm_fused(
+            if cache is not None and cache.get("key") == key:
+                ws = cache["ws"]
+            else:
+                ws = torch.empty(N.lib().rsx_deepfm_fused_workspace_bytes(F), device=dev, dtype=torch.uint8)
+                N.check(N.lib().rsx_deepfm_fused_prep(F, N.ptr(w1), N.ptr(w2), N.ptr(ws), N.stream()), "deepfm_prep")
+                if cache is not None:
+                    cache["key"], cache["ws"] = key, ws
+            packed = None
+            if cache is not None and _DEEPFM_PACK and N.lib().rsx_deepfm_fused_uses_packed(F):
+                # inference images of the tables: [vocab][32] per field (V row, W, pad), rebuilt when
+                # any table changes; one 128-B line per (row, field) instead of two
+                tkey = tuple((t.data_ptr(), t._version) for t in list(emb_tables) + list(lin_tables))
+                if cache.get("tkey") != tkey:
+                    cache.pop("packed", None)
+                    packed = [torch.empty(v.shape[0], 32, device=dev, dtype=torch.float32) for v in emb_tables]
+                    for v, w, p in zip(emb_tables, lin_tables, packed):
+                        N.check(N.lib().rsx_deepfm_pack(N.ptr(_c(v)), N.ptr(_c(w)), v.shape[0], N.ptr(p), N.stream()),
+                                "deepfm_pack")
+                    cache["tkey"], cache["packed"] = tkey, packed
+                packed = cache["packed"]
+            rc = N.lib().rsx_deepfm_fused_run(
                 N.ptr(x), R, F, N.ptr_array([_c(t) for t in emb_tables]), N.ptr_array([_c(t) for t in lin_tables]),
-                float(out_bias), N.ptr(_c(dnn_weights[0])), N.ptr(_c(b1)), N.ptr(_c(dnn_weights[1])), N.ptr(_c(b2)),
+                N.ptr_array(packed) if packed is not None else None, float(out_bias), N.ptr(_c(b1)), N.ptr(_c(b2)),
                 N.ptr(_c(w_out.reshape(-1))), N.ptr(ws), N.ptr(logit), N.ptr(prob), N.stream())
         N.check(rc, "deepfm_fused")
         return logit, prob

@@ -71,7 +71,8 @@ class DeepFM(nn.Module):
         return ops.deepfm_forward(
             X, [self.embedding_dict[n].weight for n in self.field_names],
             [self.linear_model.embedding_dict[n].weight for n in self.field_names], self._bias_value(),
-            [l.weight for l in self.dnn.linears], [l.bias for l in self.dnn.linears], self.dnn_linear.weight)
+            [l.weight for l in self.dnn.linears], [l.bias for l in self.dnn.linears], self.dnn_linear.weight,
+            cache=self.__dict__.setdefault("_fused_cache", {}))
 
     def predict_proba(self, X) -> np.ndarray:
         """CatBoost-compatible: probability of class 1 (RecommendationRanker.predict_proba :148-149)."""

@@ -171,3 +171,29 @@ def test_dcn_ranking_model_matches_oracle(gpu, B, ctx):
     ref1 = ORK.ranking_model_forward(model.cpu(), u[:1].expand(B, -1), it,
                                      c[:1].expand(B, -1) if ctx else None).squeeze()
     torch.testing.assert_close(s, ref1, atol=2e-6, rtol=0)
+
+
+def test_deepfm_weight_image_cache_follows_updates(gpu):
+    """The module keeps the fused kernel's bf16 weight images between calls; an in-place update
+    of a DNN weight (new version) or a replaced Parameter (new storage) must rebuild them."""
+    R, F, vocab = 3000, 39, 5000
+    model = DeepFM([vocab] * F, init_std=0.05, device=gpu)
+    g = torch.Generator().manual_seed(11)
+    x = torch.randint(0, vocab, (R, F), generator=g)
+
+    def check():
+        logit, _ = model.forward_logits(x.to(gpu))
+        names = model.field_names
+        ref_l, _ = OD.deepfm_forward(
+            x, [model.embedding_dict[n].weight.cpu() for n in names],
+            [model.linear_model.embedding_dict[n].weight.cpu() for n in names], float(model.out.bias.item()),
+            [l.weight.cpu() for l in model.dnn.linears], [l.bias.cpu() for l in model.dnn.linears],
+            model.dnn_linear.weight.cpu())
+        torch.testing.assert_close(logit.cpu().double(), ref_l, atol=1e-4, rtol=1e-5)
+
+    check()
+    with torch.no_grad():
+        model.dnn.linears[0].weight.mul_(-1.5)
+    check()
+    model.dnn.linears[1].weight = torch.nn.Parameter(torch.randn(128, 256, device=gpu) * 0.05)
+    check()

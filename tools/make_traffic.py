@@ -3,7 +3,7 @@ tools/nce_micro.py (rocprofv3 --pmc, separate passes; see tools/steps_final_r01.
 
 FETCH_SIZE is doubled (gfx950 reports half the bytes of 16-B/lane streaming reads,
 MI355X_MICROARCH.md HBM section); WRITE_SIZE is taken as reported.
-  python tools/make_traffic.py gpurun_out/pmcf gpurun_out/pmcw out.json"""
+  python tools/make_traffic.py gpurun_out/pmcf gpurun_out/pmcw out.json [global_batch N D]"""
 import csv
 import glob
 import json
@@ -24,7 +24,8 @@ def vals(d, counter):
 def main():
     fetch = vals(sys.argv[1], "FETCH_SIZE")
     write = vals(sys.argv[2], "WRITE_SIZE")
-    N, D = 76850, 16363  # tools/nce_micro.py batch 4096 (bench batch 0 shapes)
+    # tools/nce_micro.py --batch B shapes (bench batch 0): 4096 -> N 76850, D 16363
+    batch, N, D = (int(sys.argv[4]), int(sys.argv[5]), int(sys.argv[6])) if len(sys.argv) > 6 else (4096, 76850, 16363)
     f = sum(fetch) / len(fetch)
     w = sum(write) / len(write)
     hbm = int((2 * f + w) * 1024)
@@ -34,14 +35,14 @@ def main():
     alg = 4 * (N + D) * 128 + 4 * 4 * N * 128 + 4 * 4 * 4 * N
     out = {
         "kernel": "nce_grouped_fwdg_x3_k (grouped LogQ forward fused with the row gradient)",
-        "precision": "bf16x3", "global_batch": 4096, "rows_N": N, "distinct_targets_D": D,
+        "precision": "bf16x3", "global_batch": batch, "rows_N": N, "distinct_targets_D": D,
         "fetch_size_kb_raw": round(f, 1), "write_size_kb": round(w, 1),
         "hbm_bytes_per_launch": hbm,
         "correction": "FETCH_SIZE doubled (gfx950 reports half the bytes of 16-B/lane streaming reads, "
                       "MI355X_MICROARCH.md HBM section); WRITE_SIZE as reported",
         "algorithmic_bytes_per_launch": alg,
         "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) over tools/nce_micro.py "
-                  "--iters 3 (bench batch 0 shapes)",
+                  "--batch %d (bench batch 0 shapes)" % batch,
         "samples": {"fetch_kb": fetch, "write_kb": write},
     }
     json.dump(out, open(sys.argv[3], "w"), indent=1)
