@@ -286,6 +286,23 @@ int rsx_deepfm_fused_run(const int64_t* x, int64_t R, int F, const float* const*
 int rsx_deepfm_pack(const float* V, const float* W, int64_t vocab, float* packed, void* stream);
 int rsx_deepfm_fused_uses_packed(int F);
 
+/* ---- §8f #3: GDCN reranker batch (utils/data_preprocessing/feature_processor.py:144-195) ----
+ * rsx_reranker_batch replaces RerankerDataset.__getitem__ (:156-181) + reranker_collate_fn
+ * (:184-191) for a batch of (user row uidx[b], item row iidx[b]) on device tables:
+ *   dense [B, 12] = user_scaled[u] (3) | item_scaled[i] (6) | price gap, trend 1w, trend 1m
+ *     (cross features in float64 from u_raw [U, 2] = (user_avg_price_log, total_cnt_log) and
+ *     i_raw [I, 3] = (avg_item_price_log, velocity_1w, velocity_1m), rounded to fp32 once);
+ *   cat [B] = u_cat[u]; target [B] = i_num[i];
+ *   seq/mask [B, L]: the last min(len, max_len) ids of the user's CSR sequence (seq_off [U+1],
+ *     seq_ids), right-padded with 0; mask = seq != 0. L = the batch maximum of min(len, max_len)
+ *     (rsx_reranker_seq_lens gives the per-row lengths). */
+int rsx_reranker_seq_lens(const int64_t* uidx, const int64_t* seq_off, int64_t B, int max_len, int64_t* lens,
+                          void* stream);
+int rsx_reranker_batch(const int64_t* uidx, const int64_t* iidx, int64_t B, const float* u_scaled, const double* u_raw,
+                       const int64_t* u_cat, const float* i_scaled, const double* i_raw, const int64_t* i_num,
+                       const int64_t* seq_off, const int64_t* seq_ids, int max_len, int64_t L, float* dense,
+                       int64_t* cat, int64_t* target, int64_t* seq, int64_t* mask, void* stream);
+
 /* ---- A9: item-tower RE path ------------------------------------------------------------
  * out[t] = LayerNorm((word[ids[t]] + type_row) + pos[tok_pos[t]]) * ln_w + ln_b over packed
  * tokens: BertEmbeddings (word + token type 0 + absolute position, LayerNorm, eval) for the

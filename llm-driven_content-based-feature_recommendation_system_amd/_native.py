@@ -63,6 +63,9 @@ _SIGS = {
     "rsx_deepfm_fused_prep": (c_i, [c_i, c_p, c_p, c_p, c_p]),
     "rsx_deepfm_fused_run": (c_i, [c_p, c_i64, c_i, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "rsx_deepfm_pack": (c_i, [c_p, c_p, c_i64, c_p, c_p]),
+    "rsx_reranker_seq_lens": (c_i, [c_p, c_p, c_i64, c_i, c_p, c_p]),
+    "rsx_reranker_batch": (c_i, [c_p, c_p, c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i64, c_p, c_p, c_p,
+                                 c_p, c_p, c_p]),
     "rsx_deepfm_fused_uses_packed": (c_i, [c_i]),
     "rsx_linear_fwd": (c_i, [c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i64, c_i, c_p, c_p]),
     "rsx_linear_dot_fwd": (c_i, [c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i64, c_i, c_p, c_p, c_p, c_p, c_p]),

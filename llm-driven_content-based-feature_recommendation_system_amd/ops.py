@@ -1121,6 +1121,36 @@ def deepfm_forward(x, emb_tables, lin_tables, out_bias, dnn_weights, dnn_biases,
 
 
 # ----------------------------------------------------------------------------------------
+# §8f #3: GDCN reranker batch (utils/data_preprocessing/feature_processor.py:144-195)
+def reranker_batch(uidx, iidx, tables, max_len=50):
+    """(dense [B,12] f32, cat [B], seq_ids [B,L], seq_mask [B,L], target [B]) of the batch rows
+    uidx / iidx (int64 device row indices) from device tables (a dict: u_scaled [U,3] f32,
+    u_raw [U,2] f64, u_cat [U], i_scaled [I,6] f32, i_raw [I,3] f64, i_num [I], seq_off [U+1],
+    seq_ids [nnz]) on rsx_reranker_batch. L = the batch's longest min(len, max_len) (one host
+    read of the per-row lengths: pad_sequence pads to the batch maximum)."""
+    N.ensure_device(uidx)
+    uidx, iidx = _c(uidx), _c(iidx)
+    B = uidx.numel()
+    dev = uidx.device
+    t = tables
+    lens = torch.empty(B, device=dev, dtype=torch.int64)
+    N.check(N.lib().rsx_reranker_seq_lens(N.ptr(uidx), N.ptr(t["seq_off"]), B, int(max_len), N.ptr(lens), N.stream()),
+            "reranker_seq_lens")
+    L = int(lens.max().item()) if B > 0 else 0
+    dense = torch.empty(B, 12, device=dev, dtype=torch.float32)
+    cat = torch.empty(B, device=dev, dtype=torch.int64)
+    target = torch.empty(B, device=dev, dtype=torch.int64)
+    seq = torch.empty(B, L, device=dev, dtype=torch.int64)
+    mask = torch.empty(B, L, device=dev, dtype=torch.int64)
+    rc = N.lib().rsx_reranker_batch(
+        N.ptr(uidx), N.ptr(iidx), B, N.ptr(t["u_scaled"]), N.ptr(t["u_raw"]), N.ptr(t["u_cat"]), N.ptr(t["i_scaled"]),
+        N.ptr(t["i_raw"]), N.ptr(t["i_num"]), N.ptr(t["seq_off"]), N.ptr(t["seq_ids"]), int(max_len), L, N.ptr(dense),
+        N.ptr(cat), N.ptr(target), N.ptr(seq), N.ptr(mask), N.stream())
+    N.check(rc, "reranker_batch")
+    return dense, cat, seq, mask, target
+
+
+# ----------------------------------------------------------------------------------------
 # A14: retrieval top-k
 def retrieve_topk(queries, items, k):
     """(scores [Q, k] desc, indices [Q, k] int64) of queries @ items.T without materialising
@@ -1139,12 +1169,15 @@ def retrieve_topk(queries, items, k):
     return sc, ix
 
 
-def hnm_mine(u_norm, i_norm, target_ids, k, hnm_threshold=0.90, temperature=1.0):
+def hnm_mine(u_norm, i_norm, target_ids, k, hnm_threshold=0.90, temperature=1.0, ignored_at=None):
     """Hard-negative mining (v1_refine_usertower.py:641-669, 705-728, 776-790) in one kernel:
     per row the k largest of (u_norm @ i_norm.T) / temperature with same-target columns and
     columns whose item-item cosine exceeds hnm_threshold (off the diagonal) set to -inf.
     Returns (top_idx [N, k] int64, value desc then column asc; top_cos [N, k] raw cosines;
-    avail [N] int32 = columns not ignored). No autograd (the reference mines under no_grad)."""
+    avail [N] int32 = columns not ignored). No autograd (the reference mines under no_grad).
+    ignored_at: optional [N, M] int64 column indices; then a 4th output [N, M] bool tells
+    whether column ignored_at[i, m] is ignored for row i, read from the kernel's own masked
+    workspace (the same item-item products and threshold test the mining used)."""
     N.ensure_device(u_norm)
     u = _c(u_norm.detach().to(torch.float32))
     it = _c(i_norm.detach().to(torch.float32))
@@ -1165,7 +1198,11 @@ def hnm_mine(u_norm, i_norm, target_ids, k, hnm_threshold=0.90, temperature=1.0)
         rc = N.lib().rsx_hnm_mine(N.ptr(u), N.ptr(it), N.ptr(tg), n, d, k, float(hnm_threshold), float(temperature),
                                   N.ptr(ws), nws, N.ptr(idx), N.ptr(cos), N.ptr(avail), N.stream())
     N.check(rc, "hnm_mine")
-    return idx, cos, avail
+    if ignored_at is None:
+        return idx, cos, avail
+    ldw = nws // (4 * n)
+    masked = ws.view(torch.float32)[: n * ldw].view(n, ldw)
+    return idx, cos, avail, torch.gather(masked, 1, ignored_at) == float("-inf")
 
 
 # ----------------------------------------------------------------------------------------

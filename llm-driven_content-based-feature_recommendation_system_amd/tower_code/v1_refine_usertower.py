@@ -362,14 +362,17 @@ def inbatch_mixed_hnm_loss_with_stats(user_emb, item_tower_emb, target_ids, log_
     tgt = target_ids.reshape(-1)
     u, it = _hnm_rows(user_emb, item_tower_emb, tgt)
     num_k = max(1, int((N - 1) * top_k_percent))
-    top_idx, top_cos, _ = ops.hnm_mine(u, it, tgt, num_k, hnm_threshold, temperature)
+    # the random draws first (same generator use as the reference: randint after mining does
+    # not consume from the GPU generator in between), so the mining kernel can also report its
+    # ignore decision at exactly those columns: the reference derives both masks from one
+    # ignore_mask (:719, :746), so a draw is masked iff the miner ignores that column
     random_indices = torch.randint(0, N, (N, random_sample_size), device=device)
+    top_idx, top_cos, _, random_mask = ops.hnm_mine(u, it, tgt, num_k, hnm_threshold, temperature,
+                                                    ignored_at=random_indices)
     diag = torch.arange(N, device=device).unsqueeze(1)
     cols = torch.cat([diag, top_idx, random_indices], dim=1)
     final_logits = _hnm_logits(u, it, cols, tgt, log_q_tensor, temperature, lambda_logq)
     with torch.no_grad():
-        item_sim = torch.einsum("nd,nmd->nm", it, it[random_indices])
-        random_mask = (tgt[random_indices] == tgt.unsqueeze(1)) | ((item_sim > hnm_threshold) & (random_indices != diag))
         fill = torch.zeros_like(final_logits, dtype=torch.bool)
         fill[:, 1 + num_k:] = random_mask
     final_logits = final_logits.masked_fill(fill, -1e9)

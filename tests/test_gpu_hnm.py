@@ -150,3 +150,39 @@ def test_hnm_mine_massive_ties(gpu, N, k, levels):
     assert torch.equal(avail.cpu().long(), r_avail)
     assert torch.equal(idx.cpu(), r_idx)
     assert torch.equal(cos.cpu(), (u.double() @ it.double().T).gather(1, r_idx).float())
+
+
+@pytest.mark.parametrize("planted", [False, True])
+def test_hnm_ignore_mask_export_matches_mining(gpu, planted):
+    """The mixed loss masks its random draws with the miner's own ignore decisions
+    (ops.hnm_mine(..., ignored_at=)), as the reference derives both from one ignore_mask
+    (v1_refine_usertower.py:719, 746). With the threshold planted exactly at pair similarities
+    (borderline pairs whose comparison can flip with the summation order), the exported mask is
+    still consistent with the mining: avail = number of columns not ignored, mined columns are
+    never ignored, and the exported mask equals the reference formula on the integer case."""
+    N, k = 700, 9
+    g = torch.Generator().manual_seed(7)
+    it = F.normalize(torch.randn(N, 128, generator=g), dim=1)
+    it[1::9] = F.normalize(it[0::9][: it[1::9].shape[0]] + 0.3 * torch.randn(it[1::9].shape[0], 128, generator=g),
+                           dim=1)
+    u = F.normalize(torch.randn(N, 128, generator=g), dim=1)
+    t = torch.randint(1, N // 3, (N,), generator=g)
+    thr = 0.9
+    if planted:
+        sims = (it[0::9][:10] * it[1::9][:10]).sum(1)
+        thr = float(sims.median())  # several pairs sit exactly at the threshold in fp32
+    d = lambda x: x.to(gpu)  # noqa: E731
+    cols = torch.arange(N).repeat(N, 1)
+    idx, cos, avail, ign = ops.hnm_mine(d(u), d(it), d(t), k, thr, 0.1, ignored_at=d(cols))
+    ign = ign.cpu()
+    assert torch.equal((~ign).sum(1).int(), avail.cpu())
+    full = avail.cpu() >= k
+    assert not ign.gather(1, idx.cpu())[full].any()
+    assert ign.diagonal().all()  # same target as itself
+    # integer vectors: exact products, so the exported mask equals the reference formula
+    ui, ii, ti = _int_case(300, 128, 3, n_tgt=60)
+    cols = torch.randint(0, 300, (300, 50), generator=g)
+    *_, ign2 = ops.hnm_mine(d(ui), d(ii), d(ti), 5, 30.0, 1.0, ignored_at=d(cols))
+    sim = ii @ ii.T
+    ref = (ti[cols] == ti.unsqueeze(1)) | ((sim.gather(1, cols) > 30.0) & (cols != torch.arange(300).unsqueeze(1)))
+    assert torch.equal(ign2.cpu(), ref)
