@@ -2077,227 +2077,6 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_fwdg_x3_k(GArgs a) {
   }
 }
 
-// ---- ping-pong form of the fused forward ------------------------------------------------
-// 512-thread workgroup, 2 waves per SIMD from the SAME workgroup: group A (waves 0-3) and group B
-// (waves 4-7, the partner of wave w - 4 on its SIMD) each own 32 rows per wave and sweep the
-// same column tiles, but B runs half a tile behind. In barrier interval k:
-//     A:  S(k) [MFMA]           | softmax(k) [VALU]    | G(k) [MFMA]
-//     B:  softmax(k-1) [VALU]   | G(k-1) [MFMA]        | S(k) [MFMA]
-// so on every SIMD one wave's softmax runs beside the other's MFMA chain instead of both
-// waves reaching the same phase together (the 2-workgroups-per-CU form's partners come from
-// different workgroups with unrelated phases, and each per-tile barrier waits for the slowest
-// of its four). B's G(k-1) reads tile k-1, so the column tiles rotate through a 3-slot LDS ring;
-// one barrier per interval; B holds its S(k) accumulator across it.
-// Per element: the arithmetic of nce_grouped_fwdg_x3_k (same products, lazy max, split, merge).
-constexpr int kPPWaves = 8;
-constexpr int kPPRows = 32 * kPPWaves;  // owner rows per workgroup
-
-// softmax of one wave's S tile (acc, rewritten in place) -> split fragments gh / gl. The tile's
-// column offsets snb already hold -bias_d * log2e + log2(c_d) (the multiplicity folded into the
-// exponent: sum_d c_d 2^x = sum_d 2^(x + log2 c_d)), so the common path has no weight multiply;
-// the row user's own columns (exceptions) add log2(w_eff / c_d) (-inf when w_eff = 0) and the
-// label column log2(1 / c_d). A lazy raise rescales l and the gradient rows through LDS.
-__device__ __forceinline__ void fwdg_softmax(f32x16& acc, const float* scnt, const float* snb, float it2,
-                                             int64_t j0, int64_t j_end, bool exc, int& p, int e, int& next, int di,
-                                             const int* exc_cols, bool row_ok, float& m, float& l,
-                                             f32x16 (&gacc)[4], float* salpha, int c, int h, bf16x8 (&gh)[2],
-                                             bf16x8 (&gl)[2]) {
-  constexpr int kNone = 0x7fffffff;
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const float4 nb = *reinterpret_cast<const float4*>(&snb[8 * g + 4 * h]);
-    acc[4 * g + 0] = fmaf(acc[4 * g + 0], it2, nb.x);
-    acc[4 * g + 1] = fmaf(acc[4 * g + 1], it2, nb.y);
-    acc[4 * g + 2] = fmaf(acc[4 * g + 2], it2, nb.z);
-    acc[4 * g + 3] = fmaf(acc[4 * g + 3], it2, nb.w);
-  }
-  if (__any(exc) && exc) {
-    int q = p;
-    while (q < e && (int64_t)exc_cols[q] < j0 + kTile) ++q;
-    const int tl = ((int64_t)di < j_end) ? (int)(di - j0) : -1;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int tr = tile_row(r, h);
-      float n = 0.0f;
-      for (int k = p; k < q; ++k) n += ((int)(exc_cols[k] - j0) == tr) ? 1.0f : 0.0f;
-      if (tr == tl || n != 0.0f) {
-        const float cd = scnt[tr];
-        const float weff = (tr == tl) ? 1.0f : cd - n;
-        acc[r] = (weff > 0.0f) ? acc[r] + (__log2f(weff) - __log2f(cd)) : -INFINITY;
-      }
-    }
-    p = q;
-    next = (p < e) ? exc_cols[p] : kNone;
-  }
-  float tmax = -INFINITY;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, acc[r]);
-  {
-    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(tmax), __float_as_uint(tmax), false, false);
-    tmax = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
-  }
-  if (!row_ok) tmax = -INFINITY;
-  const bool raise = tmax > m + kLazyLog2;
-  if (__any(raise)) {
-    const float alpha = raise ? ((m == -INFINITY) ? 0.0f : __builtin_amdgcn_exp2f(m - tmax)) : 1.0f;
-    if (raise) {
-      l *= alpha;
-      m = tmax;
-    }
-    if (h == 0) salpha[c] = alpha;
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float al = salpha[tile_row(r, h)];
-#pragma unroll
-      for (int kb = 0; kb < 4; ++kb) gacc[kb][r] *= al;
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-  const float ms = (m == -INFINITY) ? 0.0f : m;
-  float ls = 0.0f;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    acc[r] = __builtin_amdgcn_exp2f(acc[r] - ms);
-    ls += acc[r];
-  }
-  l += ls;
-  split_tile(acc, gh, gl);
-}
-
-__global__ __launch_bounds__(512, 1) void nce_grouped_fwdg_pp_x3_k(GArgs a) {
-  __shared__ __attribute__((aligned(16))) X3Tile sT[3];
-  __shared__ __attribute__((aligned(16))) float sB2[3][kTile];
-  __shared__ __attribute__((aligned(16))) float sCnt[3][kTile];
-  __shared__ __attribute__((aligned(16))) float sAlpha[kPPWaves][32];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int h = lane >> 5, c = lane & 31;
-  const bool groupB = wave >= 4;
-  int split, rb;
-  remap_block(a.nsplit, split, rb);
-  const int64_t i = (int64_t)rb * kPPRows + wave * 32 + c;
-  const bool row_ok = i < a.N;
-  bf16x8 uh[8], ul[8];
-  load_owner_x3(uh, ul, a.A, i, a.lda, row_ok, h);
-  const int64_t j_begin = (int64_t)split * a.span;
-  int64_t j_end = j_begin + a.span;
-  if (j_end > a.M) j_end = a.M;
-  constexpr int kNone = 0x7fffffff;
-  int di = -1, p = 0, e = 0, next = kNone;
-  if (row_ok) {
-    di = a.row_col[i];
-    p = a.row_beg[i];
-    e = a.row_end[i];
-    p = lower_bound_i(a.exc_cols, p, e, j_begin);
-    next = (p < e) ? a.exc_cols[p] : kNone;
-  }
-  const float it2 = a.inv_tau * kLog2e;
-  float m = -INFINITY, l = 0.0f;
-  f32x16 gacc[4];
-#pragma unroll
-  for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) gacc[kb][r] = 0.0f;
-  // staging: 512 threads, thread t moves 16-B chunk t & 15 of row t >> 4 in both images
-  u32x4 sth, stl;
-  float stg_b = 0.0f, stg_c = 0.0f;
-  auto gload = [&](int64_t j0) {
-    const int64_t j = j0 + (tid >> 4);
-    if (j < j_end) {
-      const int64_t o = j * kD + (tid & 15) * 8;
-      sth = *reinterpret_cast<const u32x4*>(a.bhi + o);
-      stl = *reinterpret_cast<const u32x4*>(a.blo + o);
-    } else {
-      sth = u32x4{0u, 0u, 0u, 0u};
-      stl = sth;
-    }
-    if (tid < kTile) {
-      const int64_t jj = j0 + tid;
-      const bool ok = jj < j_end;
-      stg_b = ok ? (a.bias ? a.bias[jj] : 0.0f) : INFINITY;
-      stg_c = ok ? a.colcnt[jj] : 0.0f;
-    }
-  };
-  auto lstore = [&](int buf) {
-    const int o = img_off(tid >> 4, 8 * (tid & 15));
-    *reinterpret_cast<u32x4*>(&sT[buf].hi[o]) = sth;
-    *reinterpret_cast<u32x4*>(&sT[buf].lo[o]) = stl;
-    if (tid < kTile) {
-      sB2[buf][tid] = -(stg_b * kLog2e) + __log2f(stg_c);  // past the split: -inf
-      sCnt[buf][tid] = stg_c;
-    }
-  };
-  const int64_t ntile = (j_end - j_begin + kTile - 1) / kTile;  // <= 0 when the split is empty
-  if (ntile > 0) {
-    gload(j_begin);
-    lstore(0);
-    __syncthreads();
-    // the two groups run separate loops (accB is live only in B's) with the same barrier
-    // sequence: ntile + 1 intervals each
-    if (!groupB) {
-      for (int64_t k = 0; k <= ntile; ++k) {
-        const int cur = (int)(k % 3), nxt = (int)((k + 1) % 3);
-        const int64_t j0 = j_begin + k * kTile;
-        const bool has_next = k + 1 < ntile;
-        // exception flag before the prefetch is issued (its walk may load)
-        const bool exc = k < ntile && (int64_t)next < j0 + kTile;
-        if (has_next) gload(j0 + kTile);
-        if (k < ntile) {
-          f32x16 acc = dots_x3(sT[cur], c, h, uh, ul);
-          bf16x8 gh[2], gl[2];
-          fwdg_softmax(acc, sCnt[cur], sB2[cur], it2, j0, j_end, exc, p, e, next, di, a.exc_cols, row_ok, m, l,
-                       gacc, sAlpha[wave], c, h, gh, gl);
-          grad_x3s(gacc, gh, gl, sT[cur], lane);
-        }
-        if (has_next) lstore(nxt);  // slot of tile k-2: B's G(k-2) ran in interval k-1
-        __builtin_amdgcn_s_waitcnt(kVmcnt0);
-        __syncthreads();
-      }
-    } else {
-      f32x16 accB;  // S of the previous tile, carried across the barrier
-      bool excB = false;
-      for (int64_t k = 0; k <= ntile; ++k) {
-        const int cur = (int)(k % 3), prv = (int)((k + 2) % 3), nxt = (int)((k + 1) % 3);
-        const int64_t j0 = j_begin + k * kTile;
-        const bool has_next = k + 1 < ntile;
-        if (has_next) gload(j0 + kTile);
-        if (k > 0) {
-          bf16x8 gh[2], gl[2];
-          fwdg_softmax(accB, sCnt[prv], sB2[prv], it2, j0 - kTile, j_end, excB, p, e, next, di, a.exc_cols,
-                       row_ok, m, l, gacc, sAlpha[wave], c, h, gh, gl);
-          grad_x3s(gacc, gh, gl, sT[prv], lane);
-        }
-        if (k < ntile) {
-          excB = (int64_t)next < j0 + kTile;  // tile k's flag (the pointer is past tile k-1 now)
-          accB = dots_x3(sT[cur], c, h, uh, ul);
-        }
-        if (has_next) lstore(nxt);
-        __builtin_amdgcn_s_waitcnt(kVmcnt0);
-        __syncthreads();
-      }
-    }
-  }
-  const float lt = l + __shfl_xor(l, 32, 64);
-  if (h == 0 && row_ok) {
-    const int64_t stride = (int64_t)a.nsplit * a.N;
-    const int64_t o = (int64_t)split * a.N + i;
-    a.part[o] = (m == -INFINITY) ? -INFINITY : m * kLn2;
-    a.part[stride + o] = lt;
-    a.part[2 * stride + o] = 0.0f;
-    a.part[3 * stride + o] = 0.0f;
-  }
-  const int64_t own_base = (int64_t)rb * kPPRows + wave * 32;
-  float* dst = a.dout + (int64_t)split * a.N * kD;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int64_t orow = own_base + tile_row(r, h);
-    if (orow < a.N) {
-#pragma unroll
-      for (int kb = 0; kb < 4; ++kb) dst[orow * kD + kb * 32 + c] = gacc[kb][r];
-    }
-  }
-}
-
 // merge of the fused forward: lse / row loss as nce_grouped_merge_k, plus the row gradient
 // per unit upstream gradient  ga_i = (sum_s O_s e^(m_s - M) / sum_s l_s e^(m_s - M) - B_d(i)) / tau
 __global__ __launch_bounds__(256) void nce_grouped_merge_g_k(const float* A, const float* B, const float* bias,
@@ -2741,17 +2520,8 @@ RSX_API int rsx_nce_grouped_fwd_grad(const float* A, const float* B, const float
   g.blo = im.blo;
   launch_split(B, ldb, D, im.bhi, im.blo, st);
   RSX_LAUNCHED();
-  static const int pp = [] {  // RSX_NCE_FWDG_PP=0: the 2-workgroups-per-CU form
-    const char* v = getenv("RSX_NCE_FWDG_PP");
-    return v ? atoi(v) : 1;
-  }();
-  if (pp) {
-    const int blocks = (int)(((N + kPPRows - 1) / kPPRows) * nsplit);
-    hipLaunchKernelGGL(nce_grouped_fwdg_pp_x3_k, dim3(blocks), dim3(512), 0, st, g);
-  } else {
-    const int blocks = (int)(((N + kOwnRows - 1) / kOwnRows) * nsplit);
-    hipLaunchKernelGGL(nce_grouped_fwdg_x3_k, dim3(blocks), dim3(256), 0, st, g);
-  }
+  const int blocks = (int)(((N + kOwnRows - 1) / kOwnRows) * nsplit);
+  hipLaunchKernelGGL(nce_grouped_fwdg_x3_k, dim3(blocks), dim3(256), 0, st, g);
   RSX_LAUNCHED();
   hipLaunchKernelGGL(nce_grouped_merge_g_k, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, A, B, bias, row_col,
                      N, lda, ldb, g.inv_tau, nsplit, part, opart, lse, row_loss, row_valid, ga);
