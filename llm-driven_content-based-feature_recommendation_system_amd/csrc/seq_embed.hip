@@ -218,6 +218,161 @@ struct BwdArgs {
   int part_w;             // L*D + small_total + 2*D + kMaxTab
 };
 
+struct BwdLive {
+  const int64_t* ids[kMaxTab];
+  const float* tab[kMaxTab];
+  float* dtab[kMaxTab];
+  float g[kMaxTab];
+  int64_t pad[kMaxTab];
+  int soff[kMaxTab];
+  int j[kMaxTab];
+  int n;
+};
+
+struct BwdCtx {
+  float* xr;        // this row slot's LDS exchange row
+  float* s_pos;
+  float* s_small;
+  int64_t r_begin, r_end;
+  int wave, sub, c;
+  float4 w;
+  bool do_ln;
+};
+
+// U row groups of one wave: every independent load of all U groups is issued before the first
+// use — token position and live-table ids, then dout / mean / rstd / base and the dependent
+// position and table rows (the LN recompute and the gate dot reuse the same table rows) — so a
+// lane has U x (1 + NL) id -> row chains in flight instead of one at a time. NL = kMaxTab is the
+// generic more-than-two-live-tables form (slots guarded by lv.n).
+template <int D, int U, int NL>
+__device__ __forceinline__ void bwd_groups(const BwdArgs& a, const BwdLive& lv, const BwdCtx& cx, int64_t r00,
+                                           float4& acc_w, float4& acc_b, float* acc_l) {
+  constexpr int LPR = D / 4;
+  constexpr int RPW = 64 / LPR;
+  constexpr int NW = 4;
+  constexpr int NS = NL > 0 ? NL : 1;
+  const FwdArgs& f = a.f;
+  const int c = cx.c;
+  const bool need_e = cx.do_ln || a.dgate;
+  const bool need_l = (f.pos && cx.do_ln) || a.dpos;
+  int64_t rc[U];
+  int lp[U];
+  int64_t id[U][NS];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t ru = r00 + (u * NW + cx.wave) * RPW + cx.sub;
+    rc[u] = ru < cx.r_end ? ru : cx.r_begin;  // out-of-range slots re-read a valid row, store nothing
+    lp[u] = need_l ? (f.tok_pos ? (int)f.tok_pos[rc[u]] : (int)(rc[u] % f.L)) : 0;
+#pragma unroll
+    for (int k = 0; k < NS; ++k)
+      id[u][k] = (NL > 0 && (NL != kMaxTab || k < lv.n)) ? lv.ids[k][rc[u]] : 0;
+  }
+  float4 dyv[U], xv[U];
+  float muv[U], rsv[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    dyv[u] = reinterpret_cast<const float4*>(a.dout + rc[u] * D)[c];
+    xv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    muv[u] = 0.0f; rsv[u] = 0.0f;
+    if (cx.do_ln) {
+      if (f.base) xv[u] = reinterpret_cast<const float4*>(f.base + rc[u] * D)[c];
+      muv[u] = f.mean[rc[u]];
+      rsv[u] = f.rstd[rc[u]];
+    }
+  }
+  float4 ev[U][NS];
+#pragma unroll
+  for (int k = 0; k < NS; ++k)
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      ev[u][k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (NL > 0 && (NL != kMaxTab || k < lv.n) && need_e)
+        ev[u][k] = reinterpret_cast<const float4*>(lv.tab[k] + id[u][k] * D)[c];
+    }
+  if (cx.do_ln) {  // recompute x in the forward's op order: base, + E_j[id] * g_j (j ascending), + pos
+#pragma unroll
+    for (int k = 0; k < NS; ++k)
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (NL > 0 && (NL != kMaxTab || k < lv.n)) xv[u] = f4_axpy_rn(xv[u], ev[u][k], lv.g[k]);
+    if (f.pos) {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        xv[u] = f4_add_rn(xv[u], reinterpret_cast<const float4*>(f.pos + (int64_t)lp[u] * D)[c]);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t r = r00 + (u * NW + cx.wave) * RPW + cx.sub;
+    if (r >= cx.r_end) continue;  // row groups are lane-aligned: shuffles below stay inside active groups
+    float4 dy = dyv[u];
+    if (f.drop.active()) {
+      const uint64_t bi = (uint64_t)r * D + 4 * c;
+      dy.x = f.drop.apply(dy.x, bi + 0);
+      dy.y = f.drop.apply(dy.y, bi + 1);
+      dy.z = f.drop.apply(dy.z, bi + 2);
+      dy.w = f.drop.apply(dy.w, bi + 3);
+    }
+    float4 dx = dy;
+    if (cx.do_ln) {
+      const float4 x = xv[u];
+      const float mu = muv[u], rs = rsv[u];
+      const float4 w = cx.w;
+      const float4 xh = make_float4((x.x - mu) * rs, (x.y - mu) * rs, (x.z - mu) * rs, (x.w - mu) * rs);
+      acc_w.x += dy.x * xh.x; acc_w.y += dy.y * xh.y; acc_w.z += dy.z * xh.z; acc_w.w += dy.w * xh.w;
+      acc_b.x += dy.x; acc_b.y += dy.y; acc_b.z += dy.z; acc_b.w += dy.w;
+      const float4 dh = make_float4(dy.x * w.x, dy.y * w.y, dy.z * w.z, dy.w * w.w);
+      float c1 = (dh.x + dh.y) + (dh.z + dh.w);
+      float c2 = dh.x * xh.x + dh.y * xh.y + dh.z * xh.z + dh.w * xh.w;
+      c1 = rsx::wave_sum_width(c1, LPR) / (float)D;
+      c2 = rsx::wave_sum_width(c2, LPR) / (float)D;
+      dx.x = (dh.x - c1 - xh.x * c2) * rs;
+      dx.y = (dh.y - c1 - xh.y * c2) * rs;
+      dx.z = (dh.z - c1 - xh.z * c2) * rs;
+      dx.w = (dh.w - c1 - xh.w * c2) * rs;
+    }
+    if (a.dbase) reinterpret_cast<float4*>(a.dbase + r * D)[c] = dx;
+    // Scatter-adds take the row in lane-strided order (lane c holds elements c + LPR*k): each
+    // atomic instruction then covers LPR consecutive floats (one 128-B line per row at D=128)
+    // instead of LPR 16-B pieces over four lines — 4x fewer lines per L2 atomic and
+    // conflict-free LDS adds. The exchange goes through a per-wave LDS row (same wave: LDS
+    // operations complete in order, no barrier).
+    float xs[4];
+    reinterpret_cast<float4*>(cx.xr)[c] = dx;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) xs[k] = cx.xr[c + LPR * k];
+    __builtin_amdgcn_wave_barrier();
+    if (a.dpos) {
+      float* dst = cx.s_pos + lp[u] * D + c;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) atomicAdd(dst + LPR * k, xs[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      if (!(NL > 0 && (NL != kMaxTab || k < lv.n))) continue;
+      if (a.dgate) {
+        const float4 e = ev[u][k];
+        acc_l[k] += dx.x * e.x + dx.y * e.y + dx.z * e.z + dx.w * e.w;
+      }
+      const int64_t i = id[u][k];
+      if (lv.dtab[k] && i != lv.pad[k]) {
+        const float gk = lv.g[k];
+        if (lv.soff[k] >= 0) {
+          float* dst = cx.s_small + lv.soff[k] + i * D + c;
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            __hip_atomic_fetch_add(dst + LPR * q, xs[q] * gk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
+          float* dst = lv.dtab[k] + i * D + c;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) atomicAdd(dst + LPR * q, xs[q] * gk);
+        }
+      }
+    }
+  }
+}
+
 constexpr int kSmallMax = 8192;  // floats (32 KiB)
 
 // One workgroup per contiguous chunk of tokens (~2 per CU). Position and small-table
@@ -261,78 +416,48 @@ __global__ __launch_bounds__(256) void seq_embed_bwd_k(BwdArgs a) {
   const int64_t r_begin = (int64_t)blockIdx.x * a.rows_per_block;
   int64_t r_end = r_begin + a.rows_per_block;
   if (r_end > f.T) r_end = f.T;
-  for (int64_t r0 = r_begin; r0 < r_end; r0 += NW * RPW) {
-    const int64_t r = r0 + wave * RPW + sub;
-    const bool ok = r < r_end;
-    if (!ok) continue;  // row groups are lane-aligned: shuffles below stay inside active groups
-    float4 dy = reinterpret_cast<const float4*>(a.dout + r * D)[c];
-    if (f.drop.active()) {
-      const uint64_t bi = (uint64_t)r * D + 4 * c;
-      dy.x = f.drop.apply(dy.x, bi + 0);
-      dy.y = f.drop.apply(dy.y, bi + 1);
-      dy.z = f.drop.apply(dy.z, bi + 2);
-      dy.w = f.drop.apply(dy.w, bi + 3);
-    }
-    float4 dx = dy;
-    if (do_ln) {
-      const float4 x = build_row<D>(f, r, c, g);
-      const float mu = f.mean[r], rs = f.rstd[r];
-      const float4 xh = make_float4((x.x - mu) * rs, (x.y - mu) * rs, (x.z - mu) * rs, (x.w - mu) * rs);
-      acc_w.x += dy.x * xh.x; acc_w.y += dy.y * xh.y; acc_w.z += dy.z * xh.z; acc_w.w += dy.w * xh.w;
-      acc_b.x += dy.x; acc_b.y += dy.y; acc_b.z += dy.z; acc_b.w += dy.w;
-      const float4 dh = make_float4(dy.x * w.x, dy.y * w.y, dy.z * w.z, dy.w * w.w);
-      float c1 = (dh.x + dh.y) + (dh.z + dh.w);
-      float c2 = dh.x * xh.x + dh.y * xh.y + dh.z * xh.z + dh.w * xh.w;
-      c1 = rsx::wave_sum_width(c1, LPR) / (float)D;
-      c2 = rsx::wave_sum_width(c2, LPR) / (float)D;
-      dx.x = (dh.x - c1 - xh.x * c2) * rs;
-      dx.y = (dh.y - c1 - xh.y * c2) * rs;
-      dx.z = (dh.z - c1 - xh.z * c2) * rs;
-      dx.w = (dh.w - c1 - xh.w * c2) * rs;
-    }
-    if (a.dbase) reinterpret_cast<float4*>(a.dbase + r * D)[c] = dx;
-    // Scatter-adds take the row in lane-strided order (lane c holds elements c + LPR*k): each
-    // atomic instruction then covers LPR consecutive floats (one 128-B line per row at D=128)
-    // instead of LPR 16-B pieces over four lines — 4x fewer lines per L2 atomic and
-    // conflict-free LDS adds. The exchange goes through a per-wave LDS row (same wave: LDS
-    // operations complete in order, no barrier).
-    float xs[4];
-    {
-      float* xr = &s_xr[wave][sub][0];
-      reinterpret_cast<float4*>(xr)[c] = dx;
-      __builtin_amdgcn_wave_barrier();
+  // live tables (gate != 0) compacted into slots by wave-uniform selects over the kernarg fields,
+  // so every register array below is indexed by compile-time slot numbers only
+  BwdLive lv;
+  lv.n = 0;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) xs[k] = xr[c + LPR * k];
-      __builtin_amdgcn_wave_barrier();
-    }
-    if (a.dpos) {
-      const int l = f.tok_pos ? (int)f.tok_pos[r] : (int)(r % f.L);
-      float* dst = s_pos + l * D + c;
+  for (int k = 0; k < kMaxTab; ++k) {
+    lv.ids[k] = nullptr; lv.tab[k] = nullptr; lv.dtab[k] = nullptr;
+    lv.g[k] = 0.0f; lv.pad[k] = 0; lv.soff[k] = -1; lv.j[k] = -1;
+  }
 #pragma unroll
-      for (int k = 0; k < 4; ++k) atomicAdd(dst + LPR * k, xs[k]);
-    }
+  for (int j = 0; j < kMaxTab; ++j) {
+    if (g[j] != 0.0f) {
 #pragma unroll
-    for (int j = 0; j < kMaxTab; ++j) {
-      if (j < f.ntab && g[j] != 0.0f) {
-        const int64_t id = f.ids[j][r];
-        if (a.dgate) {
-          const float4 e = reinterpret_cast<const float4*>(f.tab[j] + id * D)[c];
-          acc_g[j] += dx.x * e.x + dx.y * e.y + dx.z * e.z + dx.w * e.w;
-        }
-        if (a.dtab[j] && id != a.pad_idx[j]) {
-          if (a.small_off[j] >= 0) {
-            float* dst = s_small + a.small_off[j] + id * D + c;
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-              __hip_atomic_fetch_add(dst + LPR * k, xs[k] * g[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          } else {
-            float* dst = a.dtab[j] + id * D + c;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) atomicAdd(dst + LPR * k, xs[k] * g[j]);
-          }
+      for (int k = 0; k < kMaxTab; ++k) {
+        if (k == lv.n) {
+          lv.ids[k] = f.ids[j]; lv.tab[k] = f.tab[j]; lv.dtab[k] = a.dtab[j];
+          lv.g[k] = g[j]; lv.pad[k] = a.pad_idx[j]; lv.soff[k] = a.small_off[j]; lv.j[k] = j;
         }
       }
+      ++lv.n;
     }
+  }
+  float acc_l[kMaxTab];
+#pragma unroll
+  for (int k = 0; k < kMaxTab; ++k) acc_l[k] = 0.0f;
+  BwdCtx cx{&s_xr[wave][sub][0], s_pos, s_small, r_begin, r_end, wave, sub, c, w, do_ln};
+  if (lv.n <= 2) {
+    constexpr int U = 2;
+    for (int64_t r00 = r_begin; r00 < r_end; r00 += U * NW * RPW) {
+      if (lv.n == 2) bwd_groups<D, U, 2>(a, lv, cx, r00, acc_w, acc_b, acc_l);
+      else if (lv.n == 1) bwd_groups<D, U, 1>(a, lv, cx, r00, acc_w, acc_b, acc_l);
+      else bwd_groups<D, U, 0>(a, lv, cx, r00, acc_w, acc_b, acc_l);
+    }
+  } else {
+    for (int64_t r00 = r_begin; r00 < r_end; r00 += NW * RPW)
+      bwd_groups<D, 1, kMaxTab>(a, lv, cx, r00, acc_w, acc_b, acc_l);
+  }
+#pragma unroll
+  for (int j = 0; j < kMaxTab; ++j) {
+#pragma unroll
+    for (int k = 0; k < kMaxTab; ++k)
+      if (lv.j[k] == j) acc_g[j] = acc_l[k];
   }
 
   // ---- block reductions: fold the RPW row slots of each wave, then the waves ----
@@ -513,7 +638,7 @@ int launch_bwd(const BwdArgs& a, hipStream_t st) {
 int64_t bwd_rows_per_block(int64_t T, int64_t D, int64_t target_blocks) {
   // target_blocks workgroups, each owning a contiguous token chunk
   int64_t rpb = (T + target_blocks - 1) / target_blocks;
-  const int64_t quantum = 4 * (64 / (D / 4));
+  const int64_t quantum = 2 * 4 * (64 / (D / 4));  // two row groups per wave iteration
   rpb = (rpb + quantum - 1) / quantum * quantum;
   if (rpb < quantum) rpb = quantum;
   return rpb;
@@ -583,11 +708,11 @@ RSX_API int rsx_seq_embed_fwd(const float* base, const int64_t* const* ids, cons
   return 0;
 }
 
-// With a workspace the backward runs kBwdBlocksWs workgroups (4 per CU: the gathers of the
+// With a workspace the backward runs kBwdBlocksWs workgroups (3 per CU: the gathers of the
 // LayerNorm recompute need the occupancy) that store per-block partial sums, folded by
 // seq_embed_bwd_reduce_k (deterministic, no global atomics); without one, ~2 workgroups per CU
 // flush their LDS sums with global float atomics.
-constexpr int64_t kBwdBlocksWs = 1024;
+constexpr int64_t kBwdBlocksWs = 768;  // 3 per CU: the two-group loop runs at 3 waves per SIMD
 constexpr int64_t kBwdBlocksAtomic = 512;
 
 RSX_API int64_t rsx_seq_embed_bwd_workspace_floats(int64_t T, int64_t L, int64_t D) {
