@@ -1191,6 +1191,97 @@ __device__ __forceinline__ void split_tile(const f32x16& g, bf16x8 (&gh)[2], bf1
   }
 }
 
+// g = 2^(x - m) per element of the tile, summed into ls and split to hi/lo fragments, two elements
+// per step on packed fp32 ops: one v_pk_add for the exponent arguments, one for the running sum,
+// and a truncation split (hi = top 16 bits: one v_perm packs the pair, two masks give hi as fp32,
+// one v_pk_add the exact residuals x - hi, one pair conversion rounds them to bf16). Truncation
+// leaves |lo| < 2^-7 |x| and an error below 2^-16 |x| after rounding lo (RNE hi: 2^-17), well
+// inside the bf16x3 product's own 2^-16 (the dropped lo*lo' term).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void exp_split_pair(float a, float b, float m, uint32_t& hi, uint32_t& lo, f32x2& sum) {
+  f32x2 v = {a, b};
+  const f32x2 mm = {m, m};
+  v = v - mm;
+  v.x = __builtin_amdgcn_exp2f(v.x);
+  v.y = __builtin_amdgcn_exp2f(v.y);
+  sum = sum + v;
+  const uint32_t ua = __float_as_uint(v.x), ub = __float_as_uint(v.y);
+  hi = __builtin_amdgcn_perm(ub, ua, 0x07060302u);
+  const f32x2 hv = {__uint_as_float(ua & 0xffff0000u), __uint_as_float(ub & 0xffff0000u)};
+  const f32x2 r = v - hv;  // exact
+  const bf16x2 lq = {(__bf16)r.x, (__bf16)r.y};
+  lo = __builtin_bit_cast(uint32_t, lq);
+}
+
+__device__ __forceinline__ void exp_split_tile(const f32x16& x, float m, bf16x8 (&gh)[2], bf16x8 (&gl)[2],
+                                               float& ls) {
+  f32x2 sum = {0.0f, 0.0f};
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    u32x4 h, l;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint32_t hq, lq;
+      exp_split_pair(x[8 * ks + 2 * q], x[8 * ks + 2 * q + 1], m, hq, lq, sum);
+      h[q] = hq;
+      l[q] = lq;
+    }
+    gh[ks] = __builtin_bit_cast(bf16x8, h);
+    gl[ks] = __builtin_bit_cast(bf16x8, l);
+  }
+  ls = sum.x + sum.y;
+}
+
+// One k-step half of the gradient product, gacc[nb] += G_ks^T X (steps nb = 0..3 over tile t,
+// ks fixed), with WORK: the exp/split of pair q of half xh of the next G operand placed under
+// step q's three MFMAs (sched_group_barrier: the VALU fills the MFMA issue gaps of the same wave
+// instead of running as its own phase).
+__device__ __forceinline__ int grad_lane_base(int lane) {
+  const int q = (lane >> 2) & 3, p = lane & 3, h = lane >> 5, cb = (lane >> 4) & 1;
+  return img_off(4 * h + q, 16 * cb + 4 * p);
+}
+
+__device__ __forceinline__ void grad_rd(const __bf16* img, int base, int ks, int nb, bf16x8& out) {
+  const int o0 = base + img_off(16 * ks, 32 * nb), o1 = base + img_off(16 * ks + 8, 32 * nb);
+  const bf16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(&img[o0]));
+  const bf16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(&img[o1]));
+  out = __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+template <bool WORK>
+__device__ __forceinline__ void grad_half_x3(f32x16 (&gacc)[4], const bf16x8& gh, const bf16x8& gl, const X3Tile& t,
+                                             int base, int ks, const f32x16& x, int xh, float m, uint32_t (&oh)[4],
+                                             uint32_t (&ol)[4], f32x2& sum) {
+  bf16x8 bh, bl;
+  grad_rd(t.hi, base, ks, 0, bh);
+  grad_rd(t.lo, base, ks, 0, bl);
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) {
+    bf16x8 nh = bh, nl = bl;
+    if (nb < 3) {
+      grad_rd(t.hi, base, ks, nb + 1, nh);
+      grad_rd(t.lo, base, ks, nb + 1, nl);
+    }
+    gacc[nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gl, bh, gacc[nb], 0, 0, 0);
+    gacc[nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gh, bl, gacc[nb], 0, 0, 0);
+    gacc[nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gh, bh, gacc[nb], 0, 0, 0);
+    if (WORK) {
+      exp_split_pair(x[8 * xh + 2 * nb], x[8 * xh + 2 * nb + 1], m, oh[nb], ol[nb], sum);
+      asm volatile("" : "+v"(oh[nb]), "+v"(ol[nb]));  // pins the work to this step (no sinking)
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);  // next step's transposed reads
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    bh = nh;
+    bl = nl;
+  }
+}
+
 // The backward's software pipeline: the S tile of the NEXT streamed tile (MFMA, returned) runs
 // interleaved with the gradient tile of the CURRENT one (VALU), so the exp/split work of a
 // wave fills its own MFMA issue gaps instead of waiting for the S chain to drain:
@@ -1964,7 +2055,9 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_fwdg_x3_k(GArgs a) {
   auto lstore = [&](int buf) {
     stg.store(sT[buf], tid);
     if (tid < kTile) {
-      sB2[buf][tid] = -(stg_b * kLog2e);  // negated here: one fma per logit, no negation
+      // -bias log2e + log2 c_d: the multiplicity rides in the exponent (one fma per logit, no
+      // multiply); -inf past the split (c = 0, bias = inf)
+      sB2[buf][tid] = -(stg_b * kLog2e) + __log2f(stg_c);
       sCnt[buf][tid] = stg_c;
     }
   };
@@ -1980,38 +2073,39 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_fwdg_x3_k(GArgs a) {
       f32x16 acc = dots_x3(sT[cur], c, h, uh, ul);
       // registers 4g..4g+3 hold tile rows 8g + 4h + 0..3: one b128 read per group and array
       // (an immediate offset from a per-lane base) instead of 16 scalar reads with 32 address ops
-      float w[16];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const float4 cw = *reinterpret_cast<const float4*>(&sCnt[cur][8 * g + 4 * h]);
         const float4 nb = *reinterpret_cast<const float4*>(&sB2[cur][8 * g + 4 * h]);
-        w[4 * g + 0] = cw.x; w[4 * g + 1] = cw.y; w[4 * g + 2] = cw.z; w[4 * g + 3] = cw.w;
-        acc[4 * g + 0] = fmaf(acc[4 * g + 0], it2, nb.x);  // x = S/tau - bias, base 2 (-inf past the split)
+        acc[4 * g + 0] = fmaf(acc[4 * g + 0], it2, nb.x);  // x = S/tau - bias + log2 c, base 2
         acc[4 * g + 1] = fmaf(acc[4 * g + 1], it2, nb.y);
         acc[4 * g + 2] = fmaf(acc[4 * g + 2], it2, nb.z);
         acc[4 * g + 3] = fmaf(acc[4 * g + 3], it2, nb.w);
       }
-      if (__any(exc)) {
-        if (exc) {
-          int q = p;
-          while (q < e && (int64_t)a.exc_cols[q] < j0 + kTile) ++q;
-          float n[16];
+      if (exc) {  // the row's own targets: multiplicity c_d - n_{u,d}, or 1 for d(i)
+        int q = p;
+        while (q < e && (int64_t)a.exc_cols[q] < j0 + kTile) ++q;
+        float n[16];
 #pragma unroll
-          for (int r = 0; r < 16; ++r) n[r] = 0.0f;
-          for (int k = p; k < q; ++k) {
-            const int tk = (int)(a.exc_cols[k] - j0);
+        for (int r = 0; r < 16; ++r) n[r] = 0.0f;
+        for (int k = p; k < q; ++k) {
+          const int tk = (int)(a.exc_cols[k] - j0);
 #pragma unroll
-            for (int r = 0; r < 16; ++r) n[r] += (tk == tile_row(r, h)) ? 1.0f : 0.0f;
-          }
-          const int tl = ((int64_t)di < j_end) ? (int)(di - j0) : -1;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) w[r] = (tile_row(r, h) == tl) ? 1.0f : w[r] - n[r];
-          p = q;
-          next = (p < e) ? a.exc_cols[p] : kNone;
+          for (int r = 0; r < 16; ++r) n[r] += (tk == tile_row(r, h)) ? 1.0f : 0.0f;
         }
+        const int tl = ((int64_t)di < j_end) ? (int)(di - j0) : -1;
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (!(w[r] > 0.0f)) acc[r] = -INFINITY;  // multiplicity 0: masked
+        for (int g = 0; g < 4; ++g) {
+          const float4 cw = *reinterpret_cast<const float4*>(&sCnt[cur][8 * g + 4 * h]);
+          const float cv[4] = {cw.x, cw.y, cw.z, cw.w};
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int r = 4 * g + t;
+            const float wn = (tile_row(r, h) == tl) ? 1.0f : cv[t] - n[r];
+            if (wn != cv[t]) acc[r] = (wn > 0.0f) ? acc[r] + __log2f(wn / cv[t]) : -INFINITY;
+          }
+        }
+        p = q;
+        next = (p < e) ? a.exc_cols[p] : kNone;
       }
       float tmax = -INFINITY;
 #pragma unroll
@@ -2040,20 +2134,209 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_fwdg_x3_k(GArgs a) {
         __builtin_amdgcn_wave_barrier();
       }
       const float ms = (m == -INFINITY) ? 0.0f : m;
-      float ls = 0.0f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        acc[r] = w[r] * __builtin_amdgcn_exp2f(acc[r] - ms);  // w >= 0 where acc is finite
-        ls += acc[r];
-      }
-      l += ls;
+      float ls;
       bf16x8 gh[2], gl[2];
-      split_tile(acc, gh, gl);
+      exp_split_tile(acc, ms, gh, gl, ls);
+      l += ls;
       grad_x3s(gacc, gh, gl, sT[cur], lane);
       if (has_next) lstore(cur ^ 1);
       __builtin_amdgcn_s_waitcnt(kVmcnt0);  // nothing pending at the loop head on any path
       __syncthreads();
       cur ^= 1;
+    }
+  }
+  const float lt = l + __shfl_xor(l, 32, 64);
+  if (h == 0 && row_ok) {
+    const int64_t stride = (int64_t)a.nsplit * a.N;
+    const int64_t o = (int64_t)split * a.N + i;
+    a.part[o] = (m == -INFINITY) ? -INFINITY : m * kLn2;
+    a.part[stride + o] = lt;
+    a.part[2 * stride + o] = 0.0f;
+    a.part[3 * stride + o] = 0.0f;
+  }
+  const int64_t own_base = (int64_t)rb * kOwnRows + wave * 32;
+  float* dst = a.dout + (int64_t)split * a.N * kD;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int64_t orow = own_base + tile_row(r, h);
+    if (orow < a.N) {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) dst[orow * kD + kb * 32 + c] = gacc[kb][r];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void nce_grouped_fwdg_x3p_k(GArgs a) {
+  __shared__ __attribute__((aligned(16))) X3Tile sT[3];  // ring: t-1 (deferred k-step), t, t+1
+  __shared__ __attribute__((aligned(16))) float sB2[3][kTile];   // -bias_d * log2e (-inf past the split)
+  __shared__ __attribute__((aligned(16))) float sCnt[3][kTile];  // c_d (0 past the split)
+  __shared__ __attribute__((aligned(16))) float sAlpha[kWaves][32];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, c = lane & 31;
+  int split, rb;
+  remap_block(a.nsplit, split, rb);
+  const int64_t i = (int64_t)rb * kOwnRows + wave * 32 + c;
+  const bool row_ok = i < a.N;
+  bf16x8 uh[8], ul[8];
+  load_owner_x3(uh, ul, a.A, i, a.lda, row_ok, h);
+  const int64_t j_begin = (int64_t)split * a.span;
+  int64_t j_end = j_begin + a.span;
+  if (j_end > a.M) j_end = a.M;
+  constexpr int kNone = 0x7fffffff;
+  int di = -1, p = 0, e = 0, next = kNone;
+  if (row_ok) {
+    di = a.row_col[i];
+    p = a.row_beg[i];
+    e = a.row_end[i];
+    p = lower_bound_i(a.exc_cols, p, e, j_begin);
+    next = (p < e) ? a.exc_cols[p] : kNone;
+  }
+  const float it2 = a.inv_tau * kLog2e;
+  float m = -INFINITY, l = 0.0f;  // base 2; m is the same on both lane halves
+  f32x16 gacc[4];
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) gacc[kb][r] = 0.0f;
+  X3Stage stg;
+  float stg_b = 0.0f, stg_c = 0.0f;
+  auto gload = [&](int64_t j0) {
+    const int64_t j = j0 + (tid >> 3);
+    stg.load(a.bhi, a.blo, j, j < j_end, tid);
+    if (tid < kTile) {
+      const int64_t jj = j0 + tid;
+      const bool ok = jj < j_end;
+      stg_b = ok ? (a.bias ? a.bias[jj] : 0.0f) : INFINITY;
+      stg_c = ok ? a.colcnt[jj] : 0.0f;
+    }
+  };
+  auto lstore = [&](int buf) {
+    stg.store(sT[buf], tid);
+    if (tid < kTile) {
+      // -bias log2e + log2 c_d: the multiplicity rides in the exponent (one fma per logit, no
+      // multiply); -inf past the split (c = 0, bias = inf)
+      sB2[buf][tid] = -(stg_b * kLog2e) + __log2f(stg_c);
+      sCnt[buf][tid] = stg_c;
+    }
+  };
+  if (j_begin < j_end) {
+    gload(j_begin);
+    lstore(0);
+    __syncthreads();
+    // k-step 1 of the previous tile's gradient product runs in the next iteration (its G
+    // fragments pgh/pgl); zero fragments (first tile, after a flush) add exactly zero
+    int cur = 0, prev = 0;
+    bf16x8 pgh, pgl;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      pgh[k] = (__bf16)0.0f;
+      pgl[k] = (__bf16)0.0f;
+    }
+    const int gbase = grad_lane_base(lane);
+    for (int64_t j0 = j_begin; j0 < j_end; j0 += kTile) {
+      const bool has_next = j0 + kTile < j_end;
+      const bool exc = (int64_t)next < j0 + kTile;  // before the prefetch (see the backward)
+      if (has_next) gload(j0 + kTile);
+      f32x16 acc = dots_x3(sT[cur], c, h, uh, ul);
+      // registers 4g..4g+3 hold tile rows 8g + 4h + 0..3: one b128 read per group and array
+      // (an immediate offset from a per-lane base) instead of 16 scalar reads with 32 address ops
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 nb = *reinterpret_cast<const float4*>(&sB2[cur][8 * g + 4 * h]);
+        acc[4 * g + 0] = fmaf(acc[4 * g + 0], it2, nb.x);  // x = S/tau - bias + log2 c, base 2
+        acc[4 * g + 1] = fmaf(acc[4 * g + 1], it2, nb.y);
+        acc[4 * g + 2] = fmaf(acc[4 * g + 2], it2, nb.z);
+        acc[4 * g + 3] = fmaf(acc[4 * g + 3], it2, nb.w);
+      }
+      if (exc) {  // the row's own targets: multiplicity c_d - n_{u,d}, or 1 for d(i)
+        int q = p;
+        while (q < e && (int64_t)a.exc_cols[q] < j0 + kTile) ++q;
+        float n[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) n[r] = 0.0f;
+        for (int k = p; k < q; ++k) {
+          const int tk = (int)(a.exc_cols[k] - j0);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) n[r] += (tk == tile_row(r, h)) ? 1.0f : 0.0f;
+        }
+        const int tl = ((int64_t)di < j_end) ? (int)(di - j0) : -1;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 cw = *reinterpret_cast<const float4*>(&sCnt[cur][8 * g + 4 * h]);
+          const float cv[4] = {cw.x, cw.y, cw.z, cw.w};
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int r = 4 * g + t;
+            const float wn = (tile_row(r, h) == tl) ? 1.0f : cv[t] - n[r];
+            if (wn != cv[t]) acc[r] = (wn > 0.0f) ? acc[r] + __log2f(wn / cv[t]) : -INFINITY;
+          }
+        }
+        p = q;
+        next = (p < e) ? a.exc_cols[p] : kNone;
+      }
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, acc[r]);
+      {  // max with the partner lane c ^ 32: v_permlane32_swap (VALU) instead of an LDS permute
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(tmax), __float_as_uint(tmax), false, false);
+        tmax = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+      }
+      if (!row_ok) tmax = -INFINITY;
+      const bool raise = tmax > m + kLazyLog2;  // m = -inf: the first finite tile
+      if (__any(raise)) {
+        {  // the deferred product was formed against the old max: add it before rescaling
+          uint32_t dh[4], dl[4];
+          f32x2 ds = {0.0f, 0.0f};
+          grad_half_x3<false>(gacc, pgh, pgl, sT[prev], gbase, 1, acc, 0, 0.0f, dh, dl, ds);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            pgh[k] = (__bf16)0.0f;
+            pgl[k] = (__bf16)0.0f;
+          }
+        }
+        // rescale this lane's l and, through LDS, the accumulator rows of every raised owner
+        const float alpha = raise ? ((m == -INFINITY) ? 0.0f : __builtin_amdgcn_exp2f(m - tmax)) : 1.0f;
+        if (raise) {
+          l *= alpha;
+          m = tmax;
+        }
+        if (h == 0) sAlpha[wave][c] = alpha;
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float al = sAlpha[wave][tile_row(r, h)];
+#pragma unroll
+          for (int kb = 0; kb < 4; ++kb) gacc[kb][r] *= al;
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+      const float ms = (m == -INFINITY) ? 0.0f : m;
+      // G half 0 of this tile under the previous tile's deferred k-step 1, then G half 1 under
+      // this tile's k-step 0; this tile's k-step 1 is deferred to the next iteration
+      uint32_t h0[4], l0[4], h1[4], l1[4];
+      f32x2 sum = {0.0f, 0.0f};
+      grad_half_x3<true>(gacc, pgh, pgl, sT[prev], gbase, 1, acc, 0, ms, h0, l0, sum);
+      const u32x4 h0v = {h0[0], h0[1], h0[2], h0[3]}, l0v = {l0[0], l0[1], l0[2], l0[3]};
+      grad_half_x3<true>(gacc, __builtin_bit_cast(bf16x8, h0v), __builtin_bit_cast(bf16x8, l0v), sT[cur], gbase, 0,
+                         acc, 1, ms, h1, l1, sum);
+      l += sum.x + sum.y;
+      const u32x4 h1v = {h1[0], h1[1], h1[2], h1[3]}, l1v = {l1[0], l1[1], l1[2], l1[3]};
+      pgh = __builtin_bit_cast(bf16x8, h1v);
+      pgl = __builtin_bit_cast(bf16x8, l1v);
+      prev = cur;
+      const int nxt = (cur == 2) ? 0 : cur + 1;
+      if (has_next) lstore(nxt);  // nxt held tile t-2, whose deferred step ran before the last barrier
+      __builtin_amdgcn_s_waitcnt(kVmcnt0);  // nothing pending at the loop head on any path
+      __syncthreads();
+      cur = nxt;
+    }
+    {
+      uint32_t dh[4], dl[4];
+      f32x2 ds = {0.0f, 0.0f};
+      f32x16 z;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) z[r] = 0.0f;
+      grad_half_x3<false>(gacc, pgh, pgl, sT[prev], gbase, 1, z, 0, 0.0f, dh, dl, ds);
     }
   }
   const float lt = l + __shfl_xor(l, 32, 64);
@@ -2486,6 +2769,15 @@ RSX_API int rsx_nce_grouped_fwd(const float* A, const float* B, const float* bia
   return 0;
 }
 
+// RSX_NCE_FWDG=0 selects the unpipelined fused forward (A/B measurements)
+static bool fwdg_pipelined() {
+  static const bool v = [] {
+    const char* e = getenv("RSX_NCE_FWDG");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 RSX_API int rsx_nce_grouped_fwd_grad(const float* A, const float* B, const float* bias, const float* colcnt,
                                      const int* row_col, const int* row_beg, const int* row_end,
                                      const int* exc_cols, int64_t N, int64_t D, int64_t lda, int64_t ldb, float tau,
@@ -2521,7 +2813,10 @@ RSX_API int rsx_nce_grouped_fwd_grad(const float* A, const float* B, const float
   launch_split(B, ldb, D, im.bhi, im.blo, st);
   RSX_LAUNCHED();
   const int blocks = (int)(((N + kOwnRows - 1) / kOwnRows) * nsplit);
-  hipLaunchKernelGGL(nce_grouped_fwdg_x3_k, dim3(blocks), dim3(256), 0, st, g);
+  if (fwdg_pipelined())
+    hipLaunchKernelGGL(nce_grouped_fwdg_x3p_k, dim3(blocks), dim3(256), 0, st, g);
+  else
+    hipLaunchKernelGGL(nce_grouped_fwdg_x3_k, dim3(blocks), dim3(256), 0, st, g);
   RSX_LAUNCHED();
   hipLaunchKernelGGL(nce_grouped_merge_g_k, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, A, B, bias, row_col,
                      N, lda, ldb, g.inv_tau, nsplit, part, opart, lse, row_loss, row_valid, ga);
