@@ -565,7 +565,7 @@ def train_bench(args, global_batch, steps, warmup, items, cfg, model, item_tower
 
 def nce_roofline(args, tb, global_batch, rank, world, precision):
     """Roofline of the dominant kernel from the run's own HIP events. bf16x3: the main loss's
-    forward fused with the row gradient (nce_grouped_fwdg_x3_k: S plus the P x B product over
+    forward fused with the row gradient (nce_grouped_fwdg_x3p_k: S plus the P x B product over
     N_local x D distinct-target columns); fp32: the backward's row-owned pass (S recompute + dU).
     Algorithmic FLOPs per launch = 4 * N_local * D * 128 either way (2 * N * D * d per product;
     SURVEY.md 8d counts 2 N^2 d per product for the ungrouped reference formulation). Peak: the
@@ -589,7 +589,8 @@ def nce_roofline(args, tb, global_batch, rank, world, precision):
             tr = json.load(f)
         if tr.get("precision") == precision and tr.get("global_batch") == global_batch and world == 1 and fused:
             traffic, traffic_src = tr.get("hbm_bytes_per_launch"), os.path.basename(TRAFFIC_FILE)
-    return {"kernel": ("nce_grouped_fwdg_x3_k (main LogQ loss forward fused with the row gradient)"
+    fwdg = "nce_grouped_fwdg_x3_k" if os.environ.get("RSX_NCE_FWDG", "1") == "0" else "nce_grouped_fwdg_x3p_k"
+    return {"kernel": (f"{fwdg} (main LogQ loss forward fused with the row gradient)"
                        if fused else ("nce_grouped_bwd_x3_k<true>" if x3 else "nce_grouped_bwd_k<true>")
                        + " (main LogQ loss backward, row-owned)"),
             "timer": timer, "bound": "mfma",

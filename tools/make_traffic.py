@@ -9,7 +9,7 @@ import glob
 import json
 import sys
 
-KERNEL = "nce_grouped_fwdg_x3_k"
+KERNEL = "nce_grouped_fwdg_x3"  # both forms: x3_k (RSX_NCE_FWDG=0) and the pipelined x3p_k
 
 
 def vals(d, counter):
@@ -34,7 +34,7 @@ def main():
     # kernel outside this launch
     alg = 4 * (N + D) * 128 + 4 * 4 * N * 128 + 4 * 4 * 4 * N
     out = {
-        "kernel": "nce_grouped_fwdg_x3_k (grouped LogQ forward fused with the row gradient)",
+        "kernel": "nce_grouped_fwdg_x3p_k (grouped LogQ forward fused with the row gradient, pipelined)",
         "precision": "bf16x3", "global_batch": batch, "rows_N": N, "distinct_targets_D": D,
         "fetch_size_kb_raw": round(f, 1), "write_size_kb": round(w, 1),
         "hbm_bytes_per_launch": hbm,
