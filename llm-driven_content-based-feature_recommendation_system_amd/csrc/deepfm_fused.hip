@@ -337,6 +337,7 @@ constexpr int kFC2 = 8;                   // fields per chunk
 constexpr int kChunk2 = kFC2 * kBM * 16;  // bf16 per image per chunk
 constexpr int kH1Stride = kN1 + 8;        // bf16 per h1 row (528 B: conflict-free row reads)
 constexpr int kPersistMaxF = 48;
+constexpr int kIdLoads = (kBM * kPersistMaxF + 255) / 256;  // id loads per loader thread per block
 constexpr int kRing2 = 6;  // W1 fragment ring depth of the persistent kernel (fields ahead)
 
 struct PArgs {
@@ -380,13 +381,37 @@ __global__ __launch_bounds__(512, 1) void deepfm_persist_k(PArgs a) {
     float wA[kFC2], wB[kFC2], wC[kFC2];
     float4 fs = make_float4(0.f, 0.f, 0.f, 0.f), fss = fs;
     float first = 0.0f;
-    auto load_ids = [&](int64_t it) {  // ids of block it -> ids[it & 1] (int32), coalesced
+    // ids of block it -> ids[it & 1] (int32), coalesced: the block's [64][F] slice of x is
+    // contiguous, so every load is issued before the first is used (one memory latency per
+    // block instead of one per 256 ids); (row, field) from a float reciprocal (exact: the
+    // quotient of i + 0.5 stays >= 0.5 / F away from an integer)
+    const float invF = 1.0f / (float)a.F;
+    auto load_ids = [&](int64_t it) {
       const int64_t m0 = rb_of(it) * kBM;
       int* dst = ids + (it & 1) * kBM * a.id_stride;
-      for (int i = lt; i < kBM * a.F; i += 256) {
-        const int r = i / a.F, f = i - r * a.F;
-        const int64_t row = m0 + r < a.R ? m0 + r : a.R - 1;  // tail rows re-read the last row; never stored
-        dst[r * a.id_stride + f] = (int)a.x[row * a.F + f];
+      const int n = kBM * a.F;
+      const bool full = m0 + kBM <= a.R;
+      int64_t v[kIdLoads];
+#pragma unroll
+      for (int k = 0; k < kIdLoads; ++k) {
+        const int i = lt + 256 * k;
+        v[k] = 0;
+        if (i < n) {
+          int64_t e = m0 * a.F + i;
+          if (!full) {  // tail rows re-read the last row; never stored
+            const int r = (int)(((float)i + 0.5f) * invF);
+            if (m0 + r >= a.R) e = (a.R - 1) * a.F + (i - r * a.F);
+          }
+          v[k] = a.x[e];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kIdLoads; ++k) {
+        const int i = lt + 256 * k;
+        if (i < n) {
+          const int r = (int)(((float)i + 0.5f) * invF), f = i - r * a.F;
+          dst[r * a.id_stride + f] = (int)v[k];
+        }
       }
     };
     auto issue_set = [&](int64_t it, int j, float4 (&vb)[kFC2], float (&wv)[kFC2]) {

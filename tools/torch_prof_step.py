@@ -29,7 +29,7 @@ def main():
     opt.add_param_group({"params": list(it.parameters()), "lr": cfg.lr * 0.05})
     bucket = D.GradBucket(list(model.parameters()) + list(it.parameters()))
     lookup = items.pretrained.to(dev)
-    batch = {k: (v.to(dev) if torch.is_tensor(v) else v) for k, v in synth.make_batch(items, 4096, seed=100).items()}
+    batch = {k: (v.to(dev) if torch.is_tensor(v) else v) for k, v in synth.make_batch(items, int(os.environ.get("BATCH", "8192")), seed=100).items()}
     ix = D.prepare_step_index(batch, pretrained_lookup=lookup)
     for _ in range(3):
         D.contrastive_step_dp(model, it, it.log_q, batch, opt, cfg, lookup, bucket, index=ix)
@@ -41,6 +41,14 @@ def main():
         torch.cuda.synchronize()
     print(prof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=60,
                                                                max_name_column_width=60, max_shapes_column_width=70))
+    # the small framework ops (fills, copies, cats, index) with their python call sites
+    ka = prof.key_averages(group_by_stack_n=6)
+    small = [e for e in ka if any(k in e.key for k in ("fill_", "zero_", "copy_", "cat", "index", "zeros", "empty"))]
+    small.sort(key=lambda e: -e.device_time_total)
+    for e in small[:40]:
+        print(f"{e.device_time_total / 3:9.1f} us/step  n={e.count // 3:4d}  {e.key}")
+        for fr in e.stack[:6]:
+            print("        ", fr)
 
 
 if __name__ == "__main__":
