@@ -678,15 +678,7 @@ size_t persist_lds_bytes(int id_stride) {
          4 * kBM * sizeof(float) + 2 * (size_t)kBM * id_stride * sizeof(int);
 }
 
-int cu_count() {
-  static int n = [] {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return 256;
-    return v > 0 ? v : 256;
-  }();
-  return n;
-}
+using rsx::cu_count;
 
 bool persist_ok(int F) { return F >= 3 * kFC2 + 1 && F <= kPersistMaxF && getenv("RSX_DEEPFM_PERSIST") == nullptr; }
 

@@ -629,6 +629,10 @@ struct GArgs {
   const __bf16* alo;
   const __bf16* bhi;
   const __bf16* blo;
+  // fused forward, tail-split geometry (fwdg_geometry): row blocks [0, rb1) run nsplit splits of
+  // span columns, the rest nsplit2 splits of span2; partial slots per row: nslots
+  int64_t rb1, span2;
+  int nsplit2, nslots;
 };
 
 __device__ __forceinline__ int lower_bound_i(const int* a, int lo, int hi, int64_t key) {
@@ -637,6 +641,40 @@ __device__ __forceinline__ int lower_bound_i(const int* a, int lo, int hi, int64
     if ((int64_t)a[mid] < key) lo = mid + 1; else hi = mid;
   }
   return lo;
+}
+
+// Block geometry of the fused forward (nce_grouped_fwdg_x3p_k / _x3_k). Row blocks [0, rb1)
+// run a.nsplit column splits, the rest a.nsplit2 (finer: their workgroups are shorter and are
+// dispatched last, so the final round of the grid is filled by short workgroups instead of a
+// third of the chip running long ones). Each region keeps the XCD-aware remap of remap_block.
+__device__ __forceinline__ void fwdg_geometry(const GArgs& a, int& split, int64_t& rb, int64_t& j_begin,
+                                              int64_t& j_end) {
+  const int64_t b = blockIdx.x, n1 = a.rb1 * a.nsplit;
+  int64_t span;
+  if (b < n1) {
+    const int xcd = (int)(b & 7);
+    const int64_t q = b >> 3;
+    if (a.nsplit >= 8) {
+      const int nsub = a.nsplit >> 3;
+      split = xcd + 8 * (int)(q % nsub);
+      rb = q / nsub;
+    } else {
+      split = xcd % a.nsplit;
+      rb = (8 / a.nsplit) * q + xcd / a.nsplit;
+    }
+    span = a.span;
+  } else {  // n1 is a multiple of 8 (host), so b & 7 still names the XCD group
+    const int64_t b2 = b - n1;
+    const int xcd = (int)(b2 & 7);
+    const int64_t q = b2 >> 3;
+    const int nsub = a.nsplit2 >> 3;  // nsplit2 in {8, 16, ...}
+    split = xcd + 8 * (int)(q % nsub);
+    rb = a.rb1 + q / nsub;
+    span = a.span2;
+  }
+  j_begin = (int64_t)split * span;
+  j_end = j_begin + span;
+  if (j_end > a.M) j_end = a.M;
 }
 
 __device__ __forceinline__ void load_owner(float (&u)[64], const float* base, int64_t row, int64_t ld, bool ok,
@@ -2015,15 +2053,13 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_fwdg_x3_k(GArgs a) {
   __shared__ __attribute__((aligned(16))) float sAlpha[kWaves][32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, c = lane & 31;
-  int split, rb;
-  remap_block(a.nsplit, split, rb);
-  const int64_t i = (int64_t)rb * kOwnRows + wave * 32 + c;
+  int split;
+  int64_t rb, j_begin, j_end;
+  fwdg_geometry(a, split, rb, j_begin, j_end);
+  const int64_t i = rb * kOwnRows + wave * 32 + c;
   const bool row_ok = i < a.N;
   bf16x8 uh[8], ul[8];
   load_owner_x3(uh, ul, a.A, i, a.lda, row_ok, h);
-  const int64_t j_begin = (int64_t)split * a.span;
-  int64_t j_end = j_begin + a.span;
-  if (j_end > a.M) j_end = a.M;
   constexpr int kNone = 0x7fffffff;
   int di = -1, p = 0, e = 0, next = kNone;
   if (row_ok) {
@@ -2147,14 +2183,14 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_fwdg_x3_k(GArgs a) {
   }
   const float lt = l + __shfl_xor(l, 32, 64);
   if (h == 0 && row_ok) {
-    const int64_t stride = (int64_t)a.nsplit * a.N;
+    const int64_t stride = (int64_t)a.nslots * a.N;
     const int64_t o = (int64_t)split * a.N + i;
     a.part[o] = (m == -INFINITY) ? -INFINITY : m * kLn2;
     a.part[stride + o] = lt;
     a.part[2 * stride + o] = 0.0f;
     a.part[3 * stride + o] = 0.0f;
   }
-  const int64_t own_base = (int64_t)rb * kOwnRows + wave * 32;
+  const int64_t own_base = rb * kOwnRows + wave * 32;
   float* dst = a.dout + (int64_t)split * a.N * kD;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -2173,15 +2209,13 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_fwdg_x3p_k(GArgs a) {
   __shared__ __attribute__((aligned(16))) float sAlpha[kWaves][32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, c = lane & 31;
-  int split, rb;
-  remap_block(a.nsplit, split, rb);
-  const int64_t i = (int64_t)rb * kOwnRows + wave * 32 + c;
+  int split;
+  int64_t rb, j_begin, j_end;
+  fwdg_geometry(a, split, rb, j_begin, j_end);
+  const int64_t i = rb * kOwnRows + wave * 32 + c;
   const bool row_ok = i < a.N;
   bf16x8 uh[8], ul[8];
   load_owner_x3(uh, ul, a.A, i, a.lda, row_ok, h);
-  const int64_t j_begin = (int64_t)split * a.span;
-  int64_t j_end = j_begin + a.span;
-  if (j_end > a.M) j_end = a.M;
   constexpr int kNone = 0x7fffffff;
   int di = -1, p = 0, e = 0, next = kNone;
   if (row_ok) {
@@ -2341,14 +2375,14 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_fwdg_x3p_k(GArgs a) {
   }
   const float lt = l + __shfl_xor(l, 32, 64);
   if (h == 0 && row_ok) {
-    const int64_t stride = (int64_t)a.nsplit * a.N;
+    const int64_t stride = (int64_t)a.nslots * a.N;
     const int64_t o = (int64_t)split * a.N + i;
     a.part[o] = (m == -INFINITY) ? -INFINITY : m * kLn2;
     a.part[stride + o] = lt;
     a.part[2 * stride + o] = 0.0f;
     a.part[3 * stride + o] = 0.0f;
   }
-  const int64_t own_base = (int64_t)rb * kOwnRows + wave * 32;
+  const int64_t own_base = rb * kOwnRows + wave * 32;
   float* dst = a.dout + (int64_t)split * a.N * kD;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -2367,11 +2401,12 @@ __global__ __launch_bounds__(256) void nce_grouped_merge_g_k(const float* A, con
                                                              int64_t ldb, float inv_tau, int nsplit,
                                                              const float* part, const float* opart,
                                                              float* lse_out, float* row_loss, float* row_valid,
-                                                             float* ga) {
+                                                             float* ga, int64_t rows1, int nsplit2, int nslots) {
   const int lane = threadIdx.x & 63;
   const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= N) return;
-  const int64_t stride = (int64_t)nsplit * N;
+  const int64_t stride = (int64_t)nslots * N;
+  if (i >= rows1) nsplit = nsplit2;  // this row's workgroups ran the tail split count
   float m = -INFINITY, l = 0.0f;
   if (lane < nsplit) {
     m = part[(int64_t)lane * N + i];
@@ -2797,14 +2832,32 @@ RSX_API int rsx_nce_grouped_fwd_grad(const float* A, const float* B, const float
   float* row_loss = lse + N;
   float* row_valid = row_loss + N;
   float* opart = lse + 4 * N;  // the backward's split-partial region (>= nsplit x N x 128)
+  // nsplit = 8 (the partial slots per row): the leading row blocks run 4 column splits, as many
+  // as fill whole rounds of the grid at two workgroups per CU; the remaining row blocks run 8
+  // half-length splits, dispatched last, so the grid's final round is short and full
+  // (batch 8192: 1,152 row blocks x 4 = 9 rounds of 512, then 45 x 8 half-length workgroups)
+  const int64_t rbs = (N + kOwnRows - 1) / kOwnRows;
+  const int ns1 = nsplit == 8 ? 4 : nsplit;
+  int64_t rb1 = rbs;
+  if (nsplit == 8 && !getenv("RSX_NCE_TAIL8_OFF")) {
+    const int64_t slots = 2 * (int64_t)rsx::cu_count();
+    rb1 = (ns1 * rbs / slots) * slots / ns1;  // whole rounds of the 4-split blocks
+  } else if (nsplit == 8) {
+    rb1 = 0;
+  }
   GArgs g = {};
   g.A = A; g.B = B; g.bias = bias; g.colcnt = colcnt;
   g.row_col = row_col; g.row_beg = row_beg; g.row_end = row_end; g.exc_cols = exc_cols;
   g.N = N; g.M = D; g.lda = lda; g.ldb = ldb;
   g.inv_tau = 1.0f / tau;
-  g.nsplit = nsplit;
-  g.span = round_up((D + nsplit - 1) / nsplit, kTile);
+  g.nsplit = ns1;
+  g.span = round_up((D + ns1 - 1) / ns1, kTile);
   if (g.span < kTile) g.span = kTile;
+  g.rb1 = rb1;
+  g.nsplit2 = 8;
+  g.span2 = round_up((D + 7) / 8, kTile);
+  if (g.span2 < kTile) g.span2 = kTile;
+  g.nslots = nsplit;
   g.part = part;
   g.dout = opart;
   const Images im = grouped_images(ws, N, D, nsplit, kNsplitBwdGrouped);
@@ -2812,14 +2865,15 @@ RSX_API int rsx_nce_grouped_fwd_grad(const float* A, const float* B, const float
   g.blo = im.blo;
   launch_split(B, ldb, D, im.bhi, im.blo, st);
   RSX_LAUNCHED();
-  const int blocks = (int)(((N + kOwnRows - 1) / kOwnRows) * nsplit);
+  const int blocks = (int)(rb1 * ns1 + (rbs - rb1) * (nsplit == 8 ? 8 : 0));
   if (fwdg_pipelined())
     hipLaunchKernelGGL(nce_grouped_fwdg_x3p_k, dim3(blocks), dim3(256), 0, st, g);
   else
     hipLaunchKernelGGL(nce_grouped_fwdg_x3_k, dim3(blocks), dim3(256), 0, st, g);
   RSX_LAUNCHED();
   hipLaunchKernelGGL(nce_grouped_merge_g_k, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, A, B, bias, row_col,
-                     N, lda, ldb, g.inv_tau, nsplit, part, opart, lse, row_loss, row_valid, ga);
+                     N, lda, ldb, g.inv_tau, ns1, part, opart, lse, row_loss, row_valid, ga, rb1 * kOwnRows, 8,
+                     nsplit);
   RSX_LAUNCHED();
   hipLaunchKernelGGL(nce_reduce_k, dim3(1), dim3(1024), 0, st, row_loss, row_valid, N, out2);
   RSX_LAUNCHED();

@@ -61,6 +61,17 @@ __device__ __forceinline__ T wave_sum_width(T v, int width) {
 
 __device__ __forceinline__ float fmax_nan(float a, float b) { return a > b ? a : b; }
 
+// compute units of the current device (grid sizing, speed only); 256 when the query fails
+inline int cu_count() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return v > 0 ? v : 256;
+  }();
+  return n;
+}
+
 }  // namespace rsx
 
 #define RSX_ARG(cond, msg)                                   \

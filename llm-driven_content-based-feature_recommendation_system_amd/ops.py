@@ -17,7 +17,7 @@ NCE_MASK_ITEM_USER = 6
 NCE_SUPCON = 9
 
 _NSPLIT_FWD = 8
-_NSPLIT_FWD_GROUPED = int(os.environ.get("RSX_NCE_NSPLIT_FWD", "4"))  # N/128 >= 600 row blocks: 4 splits fill the chip
+_NSPLIT_FWD_GROUPED = int(os.environ.get("RSX_NCE_NSPLIT_FWD", "8"))  # partial slots; the fused forward runs 4 splits on the leading row blocks, 8 on the tail
 _NSPLIT_BWD = 8
 
 # Logit precision of the grouped (live LogQ) loss kernels, include/recsys_amd.h RSX_NCE_*:
