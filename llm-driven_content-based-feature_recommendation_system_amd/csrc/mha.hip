@@ -17,6 +17,7 @@
 // are staged in LDS and read by broadcast; scores live in registers (L <= 64).
 #include "rsx_common.h"
 #include <math.h>
+#include <stdlib.h>
 
 namespace {
 
@@ -629,6 +630,141 @@ __global__ __launch_bounds__(256) void mha_fwd_x3_k(FwdArgs a) {
   }
 }
 
+// Forward with every operand load issued before the first use: the sequence's Q and K rows and
+// V columns of this head for all NB 16-token blocks come in through one buffer resource over the
+// sequence's rows (rows >= L read as zero by the range check: no branches, no per-load waits),
+// so a wave pays one memory latency instead of one or two per query block (mha_fwd_x3_k
+// re-loads K / V per query block behind data-dependent branches). Same arithmetic, masks,
+// dropout hash and lse as mha_fwd_x3_k.
+typedef unsigned int u32x4b __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ Row8 split_row8(const u32x4b& x0, const u32x4b& x1) {
+  const float f[8] = {__uint_as_float(x0.x), __uint_as_float(x0.y), __uint_as_float(x0.z), __uint_as_float(x0.w),
+                      __uint_as_float(x1.x), __uint_as_float(x1.y), __uint_as_float(x1.z), __uint_as_float(x1.w)};
+  Row8 r;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const __bf16 h = (__bf16)f[k];
+    r.hi[k] = h;
+    r.lo[k] = (__bf16)(f[k] - (float)h);
+  }
+  return r;
+}
+template <int NB>
+__device__ __forceinline__ void mha_fwd_x3b_seq(const FwdArgs& a, int hd, int64_t tok0, int L, int lane) {
+  constexpr int DH = 32;
+  const int c = lane & 15, g = lane >> 4;
+  const int D = a.H * DH;
+  const int64_t ld = 3 * (int64_t)D;
+  const uintptr_t bp = (uintptr_t)(a.qkv + tok0 * ld);
+  const unsigned blo = __builtin_amdgcn_readfirstlane((unsigned)bp), bhi = __builtin_amdgcn_readfirstlane((unsigned)(bp >> 32));
+  const unsigned nbytes = __builtin_amdgcn_readfirstlane((unsigned)(L * ld * 4));
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(((uintptr_t)bhi << 32) | blo), 0, (int)nbytes, 0x00020000);
+  u32x4b qr[NB][2], kr[NB][2];
+  unsigned vr[NB][2][4];
+#pragma unroll
+  for (int bb = 0; bb < NB; ++bb) {
+    const unsigned oq = (unsigned)(((16 * bb + c) * ld + hd * DH + 8 * g) * 4);
+    qr[bb][0] = __builtin_amdgcn_raw_buffer_load_b128(rs, oq, 0, 0);
+    qr[bb][1] = __builtin_amdgcn_raw_buffer_load_b128(rs, oq + 16, 0, 0);
+    kr[bb][0] = __builtin_amdgcn_raw_buffer_load_b128(rs, oq + 4 * D, 0, 0);
+    kr[bb][1] = __builtin_amdgcn_raw_buffer_load_b128(rs, oq + 4 * D + 16, 0, 0);
+#pragma unroll
+    for (int et = 0; et < 2; ++et)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        vr[bb][et][t] = __builtin_amdgcn_raw_buffer_load_b32(
+            rs, (unsigned)(((16 * bb + 4 * g + t) * ld + 2 * D + hd * DH + 16 * et + c) * 4), 0, 0);
+  }
+  const int my_pad = (lane < L) ? (a.kpad ? (int)a.kpad[tok0 + lane] : 0) : 1;
+  float* Ob = a.out + tok0 * D + hd * DH;
+  Row8 kx[NB];
+#pragma unroll
+  for (int bb = 0; bb < NB; ++bb) kx[bb] = split_row8(kr[bb][0], kr[bb][1]);
+#pragma unroll
+  for (int qb = 0; qb < NB; ++qb) {
+    const int i = 16 * qb + c;  // query of this lane's score column
+    const bool iok = i < L;
+    const Row8 qx = split_row8(qr[qb][0], qr[qb][1]);
+    const int kb_end = a.causal ? qb : NB - 1;
+    f32x4 sv[NB];
+    float m = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < NB; ++kb) {
+      if (kb <= kb_end) {
+        sv[kb] = dot16_x3(kx[kb], qx);  // S^T: [key 16kb+4g+r][query i]
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int j = 16 * kb + 4 * g + r;
+          const int jpad = __shfl(my_pad, j & 63, 64);
+          const bool allowed = iok && j < L && !jpad && (!a.causal || j <= i);
+          sv[kb][r] = allowed ? sv[kb][r] * a.scale : -INFINITY;
+          m = fmaxf(m, sv[kb][r]);
+        }
+      }
+    }
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float l = 0.0f;
+#pragma unroll
+    for (int kb = 0; kb < NB; ++kb) {
+      if (kb <= kb_end) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = (sv[kb][r] == -INFINITY) ? 0.0f : __expf(sv[kb][r] - m);
+          sv[kb][r] = pv;
+          l += pv;
+        }
+      }
+    }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = (l > 0.0f) ? 1.0f / l : 0.0f;
+    f32x4 o[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    const uint64_t rowidx = ((uint64_t)(tok0 + i) * a.H + hd) * kLMax;
+#pragma unroll
+    for (int kb = 0; kb < NB; ++kb) {
+      if (kb <= kb_end) {
+        float pr[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pr[r] = a.drop.apply(sv[kb][r] * inv, rowidx + 16 * kb + 4 * g + r);
+        const Col4 pa = split4(pr);
+#pragma unroll
+        for (int et = 0; et < 2; ++et) {
+          const float vf[4] = {__uint_as_float(vr[kb][et][0]), __uint_as_float(vr[kb][et][1]),
+                               __uint_as_float(vr[kb][et][2]), __uint_as_float(vr[kb][et][3])};
+          o[et] = sum16_x3(pa, split4(vf), o[et]);
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * qb + 4 * g + r;
+      if (row < L) {
+        Ob[(int64_t)row * D + c] = o[0][r];
+        Ob[(int64_t)row * D + 16 + c] = o[1][r];
+      }
+    }
+    if (a.lse && g == 0 && iok) a.lse[(tok0 + i) * a.H + hd] = (l > 0.0f) ? m + logf(l) : -INFINITY;
+  }
+}
+
+__global__ __launch_bounds__(256) void mha_fwd_x3b_k(FwdArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t unit = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (unit >= (int64_t)a.B * a.H) return;  // whole wave exits together
+  const int b = (int)(unit / a.H), hd = (int)(unit % a.H);
+  const int64_t tok0 = a.seg ? (int64_t)a.seg[b] : (int64_t)b * a.L;
+  int L = a.seg ? (a.seg[b + 1] - a.seg[b]) : a.L;
+  if (L > kLMax) L = kLMax;
+  if (L <= 0) return;
+  const int nb = __builtin_amdgcn_readfirstlane((L + 15) >> 4);
+  if (nb == 1) mha_fwd_x3b_seq<1>(a, hd, tok0, L, lane);
+  else if (nb == 2) mha_fwd_x3b_seq<2>(a, hd, tok0, L, lane);
+  else if (nb == 3) mha_fwd_x3b_seq<3>(a, hd, tok0, L, lane);
+  else mha_fwd_x3b_seq<4>(a, hd, tok0, L, lane);
+}
+
 __global__ __launch_bounds__(256) void mha_bwd_x3_k(BwdArgs a) {
   constexpr int DH = 32;
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
@@ -829,7 +965,11 @@ RSX_API int rsx_mha_fwd_x3(const float* qkv, const uint8_t* key_pad, const int* 
   a.B = (int)B; a.L = (int)L; a.H = (int)H; a.causal = causal;
   a.scale = 1.0f / sqrtf((float)Dh);
   a.drop = rsx::make_dropout(p_drop, seed);
-  hipLaunchKernelGGL(mha_fwd_x3_k, dim3((unsigned)((B * H + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a);
+  static const bool legacy = getenv("RSX_MHA_FWD_LEGACY") != nullptr;  // A/B: the per-block-load kernel
+  if (legacy)
+    hipLaunchKernelGGL(mha_fwd_x3_k, dim3((unsigned)((B * H + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(mha_fwd_x3b_k, dim3((unsigned)((B * H + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a);
   RSX_LAUNCHED();
   return 0;
 }

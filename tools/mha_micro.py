@@ -32,7 +32,7 @@ def bench(fn, n=10):
 def main():
     dev = torch.device("cuda", 0)
     items = synth.make_items(seed=0)
-    b = synth.make_batch(items, 4096, seed=100)
+    b = synth.make_batch(items, int(os.environ.get("BATCH", "8192")), seed=100)
     pk = PackedTokens(b["padding_mask"].to(dev))
     T = pk.flat.numel()
     g = torch.Generator(device="cpu").manual_seed(0)
