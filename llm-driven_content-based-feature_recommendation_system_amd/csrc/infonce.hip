@@ -633,6 +633,7 @@ struct GArgs {
   // span columns, the rest nsplit2 splits of span2; partial slots per row: nslots
   int64_t rb1, span2;
   int nsplit2, nslots;
+  int split_major;       // grouped backward: split-major block order (nce_grouped_bwd_x3_k)
 };
 
 __device__ __forceinline__ int lower_bound_i(const int* a, int lo, int hi, int64_t key) {
@@ -1538,9 +1539,18 @@ __global__ __launch_bounds__(256, RSX_BWD_X3_OCC) void nce_grouped_bwd_x3_k(GArg
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, c = lane & 31;
   int split, ob;
-  remap_block(a.nsplit, split, ob);
   const int64_t n_own = ROW_OWNED ? a.N : a.M;
   const int64_t n_str = ROW_OWNED ? a.M : a.N;
+  if (a.split_major) {
+    // split-major XCD order: an XCD group (b % 8) runs all owner blocks of one split before the
+    // next, so its L2 holds one split's streamed images at a time (speed only)
+    const int b = blockIdx.x, xcd = b & 7, q = b >> 3;
+    const int nob = (int)((n_own + kOwnRows - 1) / kOwnRows);
+    split = xcd + 8 * (q / nob);
+    ob = q % nob;
+  } else {
+    remap_block(a.nsplit, split, ob);
+  }
   const float* own = ROW_OWNED ? a.A : a.B;
   const int64_t ld_own = ROW_OWNED ? a.lda : a.ldb;
   const float gs = a.gout[0] * a.inv_tau;
@@ -2915,7 +2925,27 @@ RSX_API int rsx_nce_grouped_bwd(const float* A, const float* B, const float* bia
     // split count of this pass: fewer splits when the owner side alone fills the chip (>= 1024
     // workgroups), which halves the partial-gradient traffic of the row pass
     const int64_t own_blocks = (n_own + kOwnRows - 1) / kOwnRows;
-    const int ps = (own_blocks * 4 >= 1024) ? 4 : nsplit;
+    int ps = (own_blocks * 4 >= 1024) ? 4 : nsplit;
+    g.split_major = 0;
+    if (!row_owned && precision == RSX_NCE_BF16X3) {
+      // column pass: 32 (else 16) splits in a split-major block order, so each XCD's L2 holds the
+      // one split of A's images it streams (the 8-split span, N/8 rows = 9.8 MB at batch 8192, does
+      // not fit a 4-MB L2): 5.5 -> 5.0-5.1 ms at batch 8192 (profiles/r02_nce_colsplit_ab.json).
+      // Bounded by the partial region (nsplit x max(N, D) rows). RSX_NCE_COLSPLIT=8|16|32 forces one.
+      static const int forced = [] {
+        const char* e = getenv("RSX_NCE_COLSPLIT");
+        return e ? atoi(e) : 0;
+      }();
+      const int64_t cap = (int64_t)nsplit * (N > D ? N : D);
+      for (int want : {32, 16}) {
+        if (forced && want != forced) continue;
+        if ((int64_t)want * n_own <= cap && N >= (int64_t)want * 2 * kTile) {
+          ps = want;
+          g.split_major = 1;
+          break;
+        }
+      }
+    }
     g.nsplit = ps;
     g.span = round_up((n_str + ps - 1) / ps, kTile);
     if (g.span < kTile) g.span = kTile;
