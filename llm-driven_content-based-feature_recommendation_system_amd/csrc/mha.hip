@@ -905,6 +905,225 @@ __global__ __launch_bounds__(256) void mha_bwd_x3_k(BwdArgs a) {
   }
 }
 
+// ---- bf16x3 backward, software-pipelined ----------------------------------------------------
+// mha_bwd_x3_k's wave per (sequence, head) and its two passes, with each pass's (key block,
+// query block) pairs walked as one flat sequence: the operands of pair n+1 are loaded (buffer
+// loads over the sequence's rows: rows past L, and the pair after the last, read as zero by the
+// range check, so no load is predicated) while pair n computes, in two ping-pong register sets
+// so that no in-flight load is copied. mha_bwd_x3_k waits one memory latency per pair.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t seq_rsrc(const void* base, unsigned bytes) {
+  const uintptr_t bp = (uintptr_t)base;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)bp);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(bp >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uintptr_t)hi << 32) | lo), 0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+struct RawRow {  // dims 8g .. 8g+7 of one token row, as loaded
+  u32x4b x0, x1;
+};
+__device__ __forceinline__ RawRow load_rawrow(__amdgpu_buffer_rsrc_t rs, unsigned off) {
+  RawRow r;
+  r.x0 = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+  r.x1 = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 0);
+  return r;
+}
+__device__ __forceinline__ void load_rawcols(__amdgpu_buffer_rsrc_t rs, int row0, int ld, int col,
+                                             unsigned (&v)[2][4]) {
+#pragma unroll
+  for (int et = 0; et < 2; ++et)
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      v[et][t] = __builtin_amdgcn_raw_buffer_load_b32(rs, (unsigned)(((row0 + t) * ld + col + 16 * et) * 4), 0, 0);
+}
+__device__ __forceinline__ Col4 split_col4(const unsigned (&v)[4]) {
+  const float f[4] = {__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3])};
+  return split4(f);
+}
+struct Pair1 {  // pass 1 operands: key block rows (K, V), query block rows (Q, dO) and columns
+  RawRow k, v, q, d;
+  unsigned qc[2][4], dc[2][4];
+};
+struct Pair2 {  // pass 2 operands: query block rows (Q, dO), key block rows (K, V) and K columns
+  RawRow q, d, k, v;
+  unsigned kc[2][4];
+};
+
+__global__ __launch_bounds__(256) void mha_bwd_x3p_k(BwdArgs a) {
+  constexpr int DH = 32;
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int64_t unit = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (unit >= (int64_t)a.B * a.H) return;  // whole wave exits together
+  const int b = (int)(unit / a.H), hd = (int)(unit % a.H);
+  const int D = a.H * DH;
+  const int ld = 3 * D;
+  const int64_t tok0 = a.seg ? (int64_t)a.seg[b] : (int64_t)b * a.L;
+  int L = a.seg ? (a.seg[b + 1] - a.seg[b]) : a.L;
+  if (L > kLMax) L = kLMax;
+  if (L <= 0) return;
+  const int nb = __builtin_amdgcn_readfirstlane((L + 15) >> 4);
+  const auto rq = seq_rsrc(a.qkv + tok0 * ld, (unsigned)(L * ld * 4));
+  const auto rd = seq_rsrc(a.dout + tok0 * D, (unsigned)(L * D * 4));
+  const float sc = a.scale;
+  const int cq = hd * DH, ck = D + hd * DH, cv = 2 * D + hd * DH;  // column offsets in a qkv row
+
+  // per-token softmax statistics (token t < L on lane t): lse_t, delta_t = dO_t . O_t, key pad
+  float my_lse = -INFINITY, my_delta = 0.0f;
+  int my_pad = 1;
+  if (lane < L) {
+    my_lse = a.lse[(tok0 + lane) * a.H + hd];
+    const float4* op = reinterpret_cast<const float4*>(a.out + (tok0 + lane) * D + hd * DH);
+    const float4* gp = reinterpret_cast<const float4*>(a.dout + (tok0 + lane) * D + hd * DH);
+    float d = 0.0f;
+#pragma unroll
+    for (int t = 0; t < DH / 4; ++t) {
+      const float4 x = op[t], y = gp[t];
+      d += x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
+    }
+    my_delta = d;
+    my_pad = a.kpad ? (int)a.kpad[tok0 + lane] : 0;
+  }
+  auto grad_elem = [&](int i, int j, float s, float dp, float lse_i, float delta_i, bool allowed, float& pd_out) {
+    pd_out = 0.0f;
+    if (!allowed) return 0.0f;
+    const float p = __expf(s * sc - lse_i);
+    float pd = p, dpd = dp;
+    if (a.drop.active()) {
+      const uint64_t idx = ((uint64_t)(tok0 + i) * a.H + hd) * kLMax + j;
+      const bool keep = rsx::hash_u32(a.drop.seed, idx) >= a.drop.thresh;
+      pd = keep ? p * a.drop.scale : 0.0f;
+      dpd = keep ? dp * a.drop.scale : 0.0f;
+    }
+    pd_out = pd;
+    return p * (dpd - delta_i) * sc;
+  };
+
+  // ---- pass 1: pairs (kb, qb >= kb) in kb-major order; key j = 16kb + c on the score columns ----
+  {
+    auto load1 = [&](Pair1& P, int kb, int qb) {
+      const int j = 16 * kb + c, iq = 16 * qb + c;
+      P.k = load_rawrow(rq, (unsigned)((j * ld + ck + 8 * g) * 4));
+      P.v = load_rawrow(rq, (unsigned)((j * ld + cv + 8 * g) * 4));
+      P.q = load_rawrow(rq, (unsigned)((iq * ld + cq + 8 * g) * 4));
+      P.d = load_rawrow(rd, (unsigned)((iq * D + hd * DH + 8 * g) * 4));
+      load_rawcols(rq, 16 * qb + 4 * g, ld, cq + c, P.qc);
+      load_rawcols(rd, 16 * qb + 4 * g, D, hd * DH + c, P.dc);
+    };
+    f32x4 dk[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    f32x4 dv[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    int kb = 0, qb = 0;
+    // one pair: prefetch the next one into `fill`, compute this one from `use`; false when done
+    auto step = [&](const Pair1& use, Pair1& fill) -> bool {
+      int nkb = kb, nqb = qb + 1;
+      if (nqb >= nb) { nkb = kb + 1; nqb = a.causal ? nkb : 0; }
+      load1(fill, nkb, nqb);
+      const int j = 16 * kb + c;
+      const bool jok = j < L;
+      const int jpad = __shfl(my_pad, j & 63, 64);
+      const f32x4 S = dot16_x3(split_row8(use.q.x0, use.q.x1), split_row8(use.k.x0, use.k.x1));
+      const f32x4 dP = dot16_x3(split_row8(use.d.x0, use.d.x1), split_row8(use.v.x0, use.v.x1));
+      float ds[4], pd[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 16 * qb + 4 * g + r;
+        const float lse_i = __shfl(my_lse, i & 63, 64);
+        const float del_i = __shfl(my_delta, i & 63, 64);
+        const bool allowed = jok && i < L && !jpad && (!a.causal || j <= i) && lse_i != -INFINITY;
+        ds[r] = grad_elem(i, j, S[r], dP[r], lse_i, del_i, allowed, pd[r]);
+      }
+      const Col4 pa = split4(pd), sa = split4(ds);
+#pragma unroll
+      for (int et = 0; et < 2; ++et) {
+        dv[et] = sum16_x3(pa, split_col4(use.dc[et]), dv[et]);  // dV[j][e]
+        dk[et] = sum16_x3(sa, split_col4(use.qc[et]), dk[et]);  // dK[j][e]
+      }
+      if (nkb != kb) {
+        float* dKb = a.dqkv + tok0 * ld + ck;
+        float* dVb = a.dqkv + tok0 * ld + cv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * kb + 4 * g + r;
+          if (row < L) {
+#pragma unroll
+            for (int et = 0; et < 2; ++et) {
+              dKb[(int64_t)row * ld + 16 * et + c] = dk[et][r];
+              dVb[(int64_t)row * ld + 16 * et + c] = dv[et][r];
+            }
+          }
+        }
+#pragma unroll
+        for (int et = 0; et < 2; ++et) dk[et] = dv[et] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      kb = nkb;
+      qb = nqb;
+      return kb < nb;
+    };
+    Pair1 p0, p1;
+    load1(p0, 0, 0);
+    for (;;) {
+      if (!step(p0, p1)) break;
+      if (!step(p1, p0)) break;
+    }
+  }
+
+  // ---- pass 2: pairs (qb, kb <= qb) in qb-major order; query i = 16qb + c on the score columns ----
+  {
+    auto load2 = [&](Pair2& P, int qb, int kb) {
+      const int i = 16 * qb + c, jr = 16 * kb + c;
+      P.q = load_rawrow(rq, (unsigned)((i * ld + cq + 8 * g) * 4));
+      P.d = load_rawrow(rd, (unsigned)((i * D + hd * DH + 8 * g) * 4));
+      P.k = load_rawrow(rq, (unsigned)((jr * ld + ck + 8 * g) * 4));
+      P.v = load_rawrow(rq, (unsigned)((jr * ld + cv + 8 * g) * 4));
+      load_rawcols(rq, 16 * kb + 4 * g, ld, ck + c, P.kc);
+    };
+    f32x4 dq[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    int qb = 0, kb = 0;
+    auto step = [&](const Pair2& use, Pair2& fill) -> bool {
+      int nqb = qb, nkb = kb + 1;
+      if (nkb > (a.causal ? qb : nb - 1)) { nqb = qb + 1; nkb = 0; }
+      load2(fill, nqb, nkb);
+      const int i = 16 * qb + c;
+      const bool iok = i < L;
+      const float lse_i = __shfl(my_lse, i & 63, 64);
+      const float del_i = __shfl(my_delta, i & 63, 64);
+      const f32x4 St = dot16_x3(split_row8(use.k.x0, use.k.x1), split_row8(use.q.x0, use.q.x1));
+      const f32x4 dPt = dot16_x3(split_row8(use.v.x0, use.v.x1), split_row8(use.d.x0, use.d.x1));
+      float ds[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = 16 * kb + 4 * g + r;
+        const int jpad = __shfl(my_pad, j & 63, 64);
+        const bool allowed = iok && j < L && !jpad && (!a.causal || j <= i) && lse_i != -INFINITY;
+        float pd;
+        ds[r] = grad_elem(i, j, St[r], dPt[r], lse_i, del_i, allowed, pd);
+      }
+      const Col4 sa = split4(ds);
+#pragma unroll
+      for (int et = 0; et < 2; ++et) dq[et] = sum16_x3(sa, split_col4(use.kc[et]), dq[et]);  // dQ[i][e]
+      if (nqb != qb) {
+        float* dQb = a.dqkv + tok0 * ld + cq;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * qb + 4 * g + r;
+          if (row < L) {
+            dQb[(int64_t)row * ld + c] = dq[0][r];
+            dQb[(int64_t)row * ld + 16 + c] = dq[1][r];
+          }
+        }
+        dq[0] = dq[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      qb = nqb;
+      kb = nkb;
+      return qb < nb;
+    };
+    Pair2 p0, p1;
+    load2(p0, 0, 0);
+    for (;;) {
+      if (!step(p0, p1)) break;
+      if (!step(p1, p0)) break;
+    }
+  }
+}
+
 }  // namespace
 
 RSX_API int rsx_mha_fwd(const float* qkv, const uint8_t* key_pad, const int* seg_off, int64_t B, int64_t L,
@@ -987,7 +1206,11 @@ RSX_API int rsx_mha_bwd_x3(const float* qkv, const uint8_t* key_pad, const int* 
   a.B = (int)B; a.L = (int)L; a.H = (int)H; a.causal = causal;
   a.scale = 1.0f / sqrtf((float)Dh);
   a.drop = rsx::make_dropout(p_drop, seed);
-  hipLaunchKernelGGL(mha_bwd_x3_k, dim3((unsigned)((B * H + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a);
+  static const bool legacy = getenv("RSX_MHA_BWD_LEGACY") != nullptr;  // A/B: one latency per pair
+  if (legacy)
+    hipLaunchKernelGGL(mha_bwd_x3_k, dim3((unsigned)((B * H + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(mha_bwd_x3p_k, dim3((unsigned)((B * H + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a);
   RSX_LAUNCHED();
   return 0;
 }
