@@ -190,7 +190,9 @@ int rsx_static_embed_bwd(const int64_t* const* ids, const float* const* tables, 
  * output head LayerNorm+GELU (tower_code/v1_refine_usertower.py:40-50, 68-72, 447-510).
  * sum_out (nullable) receives s when res is given; mean/rstd [T] are saved for the backward.
  * Backward: ds_out = LN-backward(dy) + ds_in (ds_in nullable), dres = dropout-backward(ds_out),
- * dw/db via per-block partials (ws >= rsx_ln_bwd_workspace_floats). D in {64, 128, 256}. */
+ * dw/db via per-block partials (ws >= rsx_ln_bwd_workspace_floats). D in {64, 128, 256}; the
+ * forward also takes D in {512, 768, 1024} (the item tower's BERT LayerNorms, item_tower.py:175,
+ * inference: rsx_ln_bwd stays at D <= 256). */
 int rsx_ln_fwd(const float* x, const float* res, float p_drop, uint64_t seed, const float* w, const float* b,
                float eps, int act, int64_t T, int64_t D, float* sum_out, float* y, float* mean, float* rstd,
                void* stream);
@@ -222,7 +224,8 @@ int rsx_linear_wgrad_x3(const float* dY, int64_t ldy, const float* X, int64_t ld
  * C[M, N] = epi(A[M, K] . B[N, K]^T + bias): the forward Y = X W^T + b (B = W) and the input
  * gradient dX = dY W (B = W^T) of the same per-token nn.Linear layers as rsx_linear_wgrad,
  * replacing autograd's library GEMMs. epi: 0 bias; 1 z = acc + bias, C = dropout_p(gelu_erf(z))
- * (keep-mask hash(seed, m*N + n)), aux = gelu_erf'(z); 2 C = acc * keep / (1-p) * aux, its
+ * (keep-mask hash(seed, m*N + n)), aux = gelu_erf'(z) (aux may be NULL: inference, e.g. the
+ * item tower's BERT intermediate layer, item_tower.py:175); 2 C = acc * keep / (1-p) * aux, its
  * backward (same seed, aux from epi 1). Epilogues 1/2 fuse nn.TransformerEncoderLayer's feed-forward
  * dropout(gelu(linear1(x))) (v1_refine_usertower.py:343-352) into its GEMMs.
  * N % 128 == 0, K % 32 == 0, A/B 16-byte aligned, leading dimensions multiples of 4. */

@@ -130,7 +130,7 @@ __device__ __forceinline__ void epilogue(const GArgs& a, f32x16 (&acc)[2][2], in
         } else if (EPI == EPI_GELU_DROP) {
           v += bn;
           const float cdf = 0.5f * (1.0f + erff(v * 0.70710678118654752f));
-          a.aux[m * a.ldaux + n] = cdf + v * 0.3989422804014327f * __expf(-0.5f * v * v);  // gelu'(v)
+          if (a.aux) a.aux[m * a.ldaux + n] = cdf + v * 0.3989422804014327f * __expf(-0.5f * v * v);  // gelu'(v)
           v *= cdf;  // gelu(v)
           if (a.drop.active()) v = keep(a.drop, (uint32_t)m * (uint32_t)a.N + (uint32_t)n) ? v * a.drop.scale : 0.0f;
         } else if (a.drop.active()) {
@@ -375,7 +375,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void gemm_ws_k(WsArgs w) {
             d[e] = cdf + x * 0.3989422804014327f * __expf(-0.5f * x * x);  // gelu'(x)
             v[e] = x * cdf;
           }
-          *reinterpret_cast<float4*>(xrow + o) = make_float4(d[0], d[1], d[2], d[3]);
+          if (a.aux) *reinterpret_cast<float4*>(xrow + o) = make_float4(d[0], d[1], d[2], d[3]);
         }
         if ((EPI == EPI_GELU_DROP || EPI == EPI_DGELU_DROP) && a.drop.active()) {
 #pragma unroll
@@ -474,7 +474,8 @@ RSX_API int rsx_gemm_x3(const float* A, int64_t lda, const float* B, int64_t ldb
   RSX_ARG(lda >= K && ldb >= K && ldc >= N && lda % 4 == 0 && ldb % 4 == 0, "bad leading dimensions");
   RSX_ARG(((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0, "A/B must be 16-byte aligned");
   RSX_ARG(epi == EPI_BIAS || epi == EPI_GELU_DROP || epi == EPI_DGELU_DROP, "epi must be 0, 1 or 2");
-  RSX_ARG(epi == EPI_BIAS || (aux && ldaux >= N), "the GELU epilogues need aux [M, >=N]");
+  RSX_ARG(epi == EPI_BIAS || (epi == EPI_GELU_DROP && !aux) || (aux && ldaux >= N),
+          "the GELU epilogues need aux [M, >=N] (EPI_GELU_DROP: aux may be null for inference)");
   RSX_ARG(p_drop >= 0.0f && p_drop < 1.0f, "p_drop must be in [0, 1)");
   RSX_ARG(M * (int64_t)N < (1LL << 32), "M * N must be < 2^32 (dropout element index)");
   if (M == 0) return 0;

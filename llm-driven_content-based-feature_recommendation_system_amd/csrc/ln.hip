@@ -83,6 +83,64 @@ __global__ __launch_bounds__(256) void ln_fwd_k(FArgs a) {
   }
 }
 
+// Forward for wide rows (D = 256 NV: 512, 768, 1024 — the BERT hidden sizes of the item
+// tower's text encoder): one wave per row, NV float4 per lane, same formulas as ln_fwd_k.
+template <int NV>
+__global__ __launch_bounds__(256) void ln_fwd_wide_k(FArgs a) {
+  constexpr int D = 256 * NV;
+  const int lane = threadIdx.x & 63;
+  const int64_t wave_g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  float4 w[NV], b[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int c = lane + 64 * v;
+    w[v] = a.w ? reinterpret_cast<const float4*>(a.w)[c] : make_float4(1.f, 1.f, 1.f, 1.f);
+    b[v] = a.b ? reinterpret_cast<const float4*>(a.b)[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  for (int64_t r = wave_g; r < a.T; r += nw) {
+    float4 s[NV];
+    float sum = 0.0f;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int c = lane + 64 * v;
+      s[v] = reinterpret_cast<const float4*>(a.x + r * D)[c];
+      if (a.res) {
+        float4 q = reinterpret_cast<const float4*>(a.res + r * D)[c];
+        const uint64_t bi = (uint64_t)r * D + 4 * c;
+        q.x = a.drop.apply(q.x, bi + 0);
+        q.y = a.drop.apply(q.y, bi + 1);
+        q.z = a.drop.apply(q.z, bi + 2);
+        q.w = a.drop.apply(q.w, bi + 3);
+        s[v].x += q.x; s[v].y += q.y; s[v].z += q.z; s[v].w += q.w;
+        if (a.sum_out) reinterpret_cast<float4*>(a.sum_out + r * D)[c] = s[v];
+      }
+      sum += (s[v].x + s[v].y) + (s[v].z + s[v].w);
+    }
+    if (!a.y) continue;
+    const float mu = rsx::wave_sum_width(sum, 64) * (1.0f / D);
+    float sq = 0.0f;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      s[v] = make_float4(s[v].x - mu, s[v].y - mu, s[v].z - mu, s[v].w - mu);
+      sq += s[v].x * s[v].x + s[v].y * s[v].y + s[v].z * s[v].z + s[v].w * s[v].w;
+    }
+    const float rs = 1.0f / sqrtf(rsx::wave_sum_width(sq, 64) * (1.0f / D) + a.eps);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const float4 d = s[v];
+      float4 z = make_float4(d.x * rs * w[v].x + b[v].x, d.y * rs * w[v].y + b[v].y, d.z * rs * w[v].z + b[v].z,
+                             d.w * rs * w[v].w + b[v].w);
+      if (a.act == 2) z = make_float4(gelu_erf(z.x), gelu_erf(z.y), gelu_erf(z.z), gelu_erf(z.w));
+      reinterpret_cast<float4*>(a.y + r * D)[lane + 64 * v] = z;
+    }
+    if (lane == 0) {
+      if (a.mean) a.mean[r] = mu;
+      if (a.rstd) a.rstd[r] = rs;
+    }
+  }
+}
+
 struct BArgs {
   const float* s;
   const float* mean;
@@ -215,7 +273,8 @@ RSX_API int rsx_ln_fwd(const float* x, const float* res, float p_drop, uint64_t 
                        float eps, int act, int64_t T, int64_t D, float* sum_out, float* y, float* mean, float* rstd,
                        void* stream) {
   RSX_ARG(x && (y || (res && sum_out)), "null tensor (y may be null only for the add-only form)");
-  RSX_ARG(D == 64 || D == 128 || D == 256, "D must be 64, 128 or 256");
+  RSX_ARG(D == 64 || D == 128 || D == 256 || D == 512 || D == 768 || D == 1024,
+          "D must be 64, 128, 256, 512, 768 or 1024");
   RSX_ARG(act == 0 || act == 2, "act must be 0 (none) or 2 (gelu)");
   RSX_ARG(p_drop >= 0.0f && p_drop < 1.0f, "p_drop must be in [0,1)");
   if (T == 0) return 0;
@@ -223,11 +282,14 @@ RSX_API int rsx_ln_fwd(const float* x, const float* res, float p_drop, uint64_t 
   a.x = x; a.res = res; a.w = w; a.b = b; a.sum_out = sum_out; a.y = y; a.mean = mean; a.rstd = rstd;
   a.T = T; a.eps = eps; a.act = act;
   a.drop = rsx::make_dropout(res ? p_drop : 0.0f, seed);
-  const int64_t rows_per_block = 4 * (64 / (D / 4));
+  const int64_t rows_per_block = D > 256 ? 4 : 4 * (64 / (D / 4));
   int64_t blocks = (T + rows_per_block - 1) / rows_per_block;
   if (blocks > 8192) blocks = 8192;
   hipStream_t st = (hipStream_t)stream;
-  if (D == 64) hipLaunchKernelGGL(ln_fwd_k<64>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  if (D == 512) hipLaunchKernelGGL(ln_fwd_wide_k<2>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  else if (D == 768) hipLaunchKernelGGL(ln_fwd_wide_k<3>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  else if (D == 1024) hipLaunchKernelGGL(ln_fwd_wide_k<4>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  else if (D == 64) hipLaunchKernelGGL(ln_fwd_k<64>, dim3((unsigned)blocks), dim3(256), 0, st, a);
   else if (D == 128) hipLaunchKernelGGL(ln_fwd_k<128>, dim3((unsigned)blocks), dim3(256), 0, st, a);
   else hipLaunchKernelGGL(ln_fwd_k<256>, dim3((unsigned)blocks), dim3(256), 0, st, a);
   RSX_LAUNCHED();

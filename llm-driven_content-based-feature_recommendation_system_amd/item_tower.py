@@ -13,7 +13,10 @@ Differences by design:
     downloads ``bert-base-uncased`` by name (:149-150), which has no offline equivalent;
   * forward runs the token work on this package's kernels: fused LayerNorm(+GELU), the
     token linears with split-K weight gradients, the MHA kernel (no mask, 16 field tokens)
-    and the InfoNCE kernel for the loss. BERT itself stays on PyTorch (hipBLASLt GEMMs).
+    and the InfoNCE kernel for the loss. Under no_grad (the refresh-item-vectors inference,
+    utils/inference_utils.py) the text BERT runs over the packed valid tokens
+    (``bert_cls_packed``: bf16x3 GEMMs, the varlen attention kernel, fused residual+LayerNorm,
+    the last layer's feed-forward on the [CLS] rows only); with gradients it stays HF's module.
 ``train_simcse_from_db`` keeps the reference driver's signature and loop; its ``db_session`` is
 any product source with ``fetch_products()`` (item_data.py; PostgreSQL itself is out of scope)
 and ``simcse_train_step`` is its per-batch GPU step.
@@ -108,6 +111,83 @@ def build_local_bert(hidden_size: int = 768, num_layers: int = 12, num_heads: in
     return BertModel(cfg)
 
 
+def _bert_qkv(att_self):
+    """[3D, D] weight / [3D] bias of BertSelfAttention's query, key, value concatenated (the
+    qkv row layout of rsx_mha_fwd: Q | K | V, head h at columns h*dh), rebuilt when one changes."""
+    ps = (att_self.query.weight, att_self.key.weight, att_self.value.weight,
+          att_self.query.bias, att_self.key.bias, att_self.value.bias)
+    key = tuple((p.data_ptr(), p._version) for p in ps)
+    c = att_self.__dict__.get("_rsx_qkv")
+    if c is None or c[0] != key:
+        c = (key, torch.cat(ps[:3], 0).contiguous(), torch.cat(ps[3:], 0).contiguous())
+        att_self.__dict__["_rsx_qkv"] = c
+    return c[1], c[2]
+
+
+def _bert_linear(x, lin, gelu=False):
+    W = lin.weight
+    if ops._x3_ok(W.shape[0], W.shape[1]):
+        return ops.gemm_x3(x, W, lin.bias, epi=ops.EPI_GELU_DROP if gelu else ops.EPI_BIAS, tag="bert_linear")
+    y = F.linear(x, W, lin.bias)
+    return F.gelu(y) if gelu else y
+
+
+def bert_packed_ok(bert, input_ids, attn_mask) -> bool:
+    """Whether bert_cls_packed computes exactly what BertModel does for this call: absolute
+    positions, erf GELU, head dim 16/32/64, hidden a multiple of 256 (<= 1024), sequences of at
+    most 64 tokens, and position 0 ([CLS]) valid in every row (a masked position still produces
+    an output row in BertModel, which packing drops). One host sync (the mask check)."""
+    cfg = bert.config
+    D, H = cfg.hidden_size, cfg.num_attention_heads
+    if (getattr(cfg, "position_embedding_type", "absolute") or "absolute") != "absolute":
+        return False
+    if cfg.hidden_act != "gelu" or D % 256 or D > 1024 or D // H not in (16, 32, 64) or input_ids.shape[1] > 64:
+        return False
+    return bool(attn_mask[:, 0].all().item())
+
+
+@torch.no_grad()
+def bert_cls_packed(bert, input_ids, attn_mask):
+    """BertModel(input_ids, attention_mask).last_hidden_state[:, 0] (item_tower.py:264-268) for
+    inference, over the packed valid tokens only: BertEmbeddings on the packed ids
+    (rsx_embed3_ln, position = column index as BertModel's default position ids), then per layer
+    the fused QKV GEMM, the varlen attention kernel (the mask's padded keys are simply absent
+    from each row's segment), out-proj, residual + LayerNorm, GELU intermediate (in the GEMM
+    epilogue), output GEMM, residual + LayerNorm. The last layer needs every token's K / V but
+    only the [CLS] queries, so its attention output, out-proj and feed-forward run on B rows.
+    Call only when bert_packed_ok(); eval mode (no dropout)."""
+    B, S = input_ids.shape
+    m = attn_mask != 0
+    flat = m.reshape(-1).nonzero().squeeze(1)
+    seg = torch.zeros(B + 1, device=input_ids.device, dtype=torch.int64)
+    seg[1:] = torch.cumsum(m.sum(dim=1), 0)
+    cls_rows = seg[:-1]
+    h = ops.bert_embed_packed(bert.embeddings, input_ids.reshape(-1)[flat], flat % S)
+    H = bert.config.num_attention_heads
+    layers = bert.encoder.layer
+    seg32 = seg.to(torch.int32)
+    for li, layer in enumerate(layers):
+        att = layer.attention
+        wqkv, bqkv = _bert_qkv(att.self)
+        qkv = _bert_linear(h, _Lin(wqkv, bqkv))
+        ctx = ops.mha(qkv, None, H, causal=False, p_drop=0.0, seg_off=seg32)
+        if li == len(layers) - 1:
+            ctx, h = ctx[cls_rows], h[cls_rows]
+        ln = att.output.LayerNorm
+        h = ops.add_layer_norm_infer(_bert_linear(ctx, att.output.dense), h, ln.weight, ln.bias, ln.eps)
+        inter = _bert_linear(h, layer.intermediate.dense, gelu=True)
+        ln = layer.output.LayerNorm
+        h = ops.add_layer_norm_infer(_bert_linear(inter, layer.output.dense), h, ln.weight, ln.bias, ln.eps)
+    if len(layers) == 0:
+        h = h[cls_rows]
+    return h
+
+
+class _Lin:  # weight / bias pair in nn.Linear's attribute names
+    def __init__(self, weight, bias):
+        self.weight, self.bias = weight, bias
+
+
 class HybridItemTower(nn.Module):
     """item_tower.py:131-286. forward(std_input [B,F], re_input_ids [B,9,R], re_attn_mask [B,9,R],
     text_input_ids [B,S], text_attn_mask [B,S]) -> L2-normalised [B, output_dim]."""
@@ -172,7 +252,11 @@ class HybridItemTower(nn.Module):
     def forward(self, std_input, re_input_ids, re_attn_mask, text_input_ids, text_attn_mask):
         std_emb = _ln(self.std_embedding(std_input) + self.std_field_emb, self.std_ln)        # :240-243
         re_vec = self.re_vectors(re_input_ids, re_attn_mask)                                   # :247-262
-        cls = self.bert_model(input_ids=text_input_ids, attention_mask=text_attn_mask).last_hidden_state[:, 0, :]
+        if (not torch.is_grad_enabled() and not self.bert_model.training
+                and bert_packed_ok(self.bert_model, text_input_ids, text_attn_mask)):
+            cls = bert_cls_packed(self.bert_model, text_input_ids, text_attn_mask)       # inference
+        else:
+            cls = self.bert_model(input_ids=text_input_ids, attention_mask=text_attn_mask).last_hidden_state[:, 0, :]
         t = self.text_proj
         text_vec = _ln(_lin(cls, t[0]), t[1], gelu=True).unsqueeze(1)                         # :269-271
         seq = torch.cat([std_emb, re_vec, text_vec], dim=1)                                   # [B, 16, d]

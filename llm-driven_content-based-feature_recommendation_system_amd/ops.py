@@ -721,6 +721,21 @@ def layer_norm(x, weight, bias, eps=1e-5, act=0):
     return y.reshape(shp)
 
 
+@torch.no_grad()
+def add_layer_norm_infer(x, res, weight, bias, eps=1e-5):
+    """LayerNorm(x + res) forward only (no statistics saved, the sum not written): inference,
+    e.g. BERT's post-norm residuals in item_tower.bert_cls_packed. Hidden up to 1024."""
+    N.ensure_device(x)
+    x = _c(x)
+    res = _c(res)
+    T, D = x.shape
+    y = torch.empty_like(x)
+    rc = N.lib().rsx_ln_fwd(N.ptr(x), N.ptr(res), 0.0, 0, N.ptr(weight), N.ptr(bias), float(eps), 0, T, D, None,
+                            N.ptr(y), None, None, N.stream())
+    N.check(rc, "ln_fwd(add, inference)")
+    return y
+
+
 def add_layer_norm(x, res, weight, bias, eps=1e-5, p_drop=0.0):
     """(s, LayerNorm(s)) with s = x + dropout(res): the residual add of a norm_first encoder
     layer fused with the next LayerNorm."""

@@ -224,3 +224,47 @@ def test_evaluate_model_recall_matches_oracle(gpu, tmp_path):
                 hits[k] += int(not actual.isdisjoint(top[r, :k].tolist()))
     for k in hits:
         assert abs(res[f"Recall@{k}"] - hits[k] / n * 100) < 1e-9, (k, res, hits, n)
+
+
+@pytest.mark.parametrize("hidden,heads,layers", [(256, 4, 2), (768, 12, 1)])
+def test_bert_cls_packed_matches_bertmodel(gpu, hidden, heads, layers):
+    """Packed-token BERT inference (item_tower.bert_cls_packed: bf16x3 GEMMs, varlen attention,
+    fused residual+LayerNorm, [CLS]-only last feed-forward) against HF BertModel's dense masked
+    forward, [CLS] row, eval: atol 2e-4 / rtol 1e-4 (the GEMMs are bf16x3, ~2^-17 per product)."""
+    bert = IT.build_local_bert(hidden_size=hidden, num_layers=layers, num_heads=heads, intermediate=4 * hidden,
+                               vocab_size=2000, max_position=64, seed=5).to(gpu).eval()
+    g = torch.Generator().manual_seed(hidden)
+    B, S = 40, 32
+    tl = torch.randint(1, S + 1, (B,), generator=g)
+    tl[0], tl[1] = 1, S                                            # single-token row, full row
+    mask = (torch.arange(S).view(1, S) < tl.unsqueeze(-1)).long()
+    ids = torch.randint(1000, 2000, (B, S), generator=g) * mask
+    ids[:, 0] = 101
+    ids, mask = ids.to(gpu), mask.to(gpu)
+    with torch.no_grad():
+        assert IT.bert_packed_ok(bert, ids, mask)
+        got = IT.bert_cls_packed(bert, ids, mask)
+        want = bert(input_ids=ids, attention_mask=mask).last_hidden_state[:, 0, :]
+    torch.testing.assert_close(got, want, atol=2e-4, rtol=1e-4)
+
+
+def test_item_tower_inference_uses_packed_bert_and_falls_back(gpu):
+    """HybridItemTower under no_grad + eval takes the packed BERT (same vectors as the module
+    path with gradients enabled); a batch whose position 0 is masked in some row is not
+    packable (BertModel still emits that row) and takes BertModel, with the same result."""
+    bert = IT.build_local_bert(hidden_size=256, num_layers=2, num_heads=4, intermediate=1024, vocab_size=2000,
+                               max_position=64, seed=9)
+    torch.manual_seed(1)
+    tower = IT.HybridItemTower(384, 6, 128, 128, bert_model=bert).to(gpu).eval()
+    x = [t.to(gpu) for t in _inputs(32, seed=4)]
+    want = tower(*x).detach()                                      # grad enabled: BertModel
+    with torch.no_grad():
+        got = tower(*x)
+    torch.testing.assert_close(got, want, atol=2e-4, rtol=1e-4)
+    x[4] = x[4].clone()
+    x[4][3, 0] = 0
+    with torch.no_grad():
+        assert not IT.bert_packed_ok(tower.bert_model, x[3], x[4])
+        got2 = tower(*x)
+    want2 = tower(*x).detach()
+    torch.testing.assert_close(got2, want2, atol=1e-5, rtol=1e-5)
