@@ -79,7 +79,8 @@ int rsx_mha_fwd(const float* qkv, const uint8_t* key_pad, const int* seg_off, in
 int rsx_mha_bwd(const float* qkv, const uint8_t* key_pad, const int* seg_off, const float* out, const float* lse,
                 const float* dout, int64_t B, int64_t L, int64_t H, int64_t Dh, int causal, float p_drop,
                 uint64_t seed, float* dqkv, void* stream);
-/* bf16x3 forms (Dh == 32 only; same arguments, masks, dropout stream and lse convention):
+/* bf16x3 forms (Dh == 32; the forward also Dh == 64, the item tower's BERT at inference,
+ * item_tower.py:264-268; same arguments, masks, dropout stream and lse convention):
  * 16x16 score tiles on v_mfma_f32_16x16x32_bf16 and token sums on v_mfma_f32_16x16x16_bf16
  * with every fp32 operand split hi + lo (~2^-17 relative error per product). The forward of
  * one form may be paired with the backward of the other. */

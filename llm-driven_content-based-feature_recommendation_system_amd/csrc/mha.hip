@@ -749,6 +749,125 @@ __device__ __forceinline__ void mha_fwd_x3b_seq(const FwdArgs& a, int hd, int64_
   }
 }
 
+// Head dim 64 (the item tower's BERT, inference): mha_fwd_x3b_seq with each token row in two
+// 32-dim halves — S = Q_a K_a^T + Q_b K_b^T on the same 16x16 tile, four 16-column output groups.
+template <int NB>
+__device__ __forceinline__ void mha_fwd_x3b64_seq(const FwdArgs& a, int hd, int64_t tok0, int L, int lane) {
+  constexpr int DH = 64;
+  const int c = lane & 15, g = lane >> 4;
+  const int D = a.H * DH;
+  const int64_t ld = 3 * (int64_t)D;
+  const uintptr_t bp = (uintptr_t)(a.qkv + tok0 * ld);
+  const unsigned blo = __builtin_amdgcn_readfirstlane((unsigned)bp), bhi = __builtin_amdgcn_readfirstlane((unsigned)(bp >> 32));
+  const unsigned nbytes = __builtin_amdgcn_readfirstlane((unsigned)(L * ld * 4));
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(((uintptr_t)bhi << 32) | blo), 0, (int)nbytes, 0x00020000);
+  u32x4b qr[NB][2][2], kr[NB][2][2];
+  unsigned vr[NB][4][4];
+#pragma unroll
+  for (int bb = 0; bb < NB; ++bb) {
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const unsigned oq = (unsigned)(((16 * bb + c) * ld + hd * DH + 32 * hf + 8 * g) * 4);
+      qr[bb][hf][0] = __builtin_amdgcn_raw_buffer_load_b128(rs, oq, 0, 0);
+      qr[bb][hf][1] = __builtin_amdgcn_raw_buffer_load_b128(rs, oq + 16, 0, 0);
+      kr[bb][hf][0] = __builtin_amdgcn_raw_buffer_load_b128(rs, oq + 4 * D, 0, 0);
+      kr[bb][hf][1] = __builtin_amdgcn_raw_buffer_load_b128(rs, oq + 4 * D + 16, 0, 0);
+    }
+#pragma unroll
+    for (int et = 0; et < 4; ++et)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        vr[bb][et][t] = __builtin_amdgcn_raw_buffer_load_b32(
+            rs, (unsigned)(((16 * bb + 4 * g + t) * ld + 2 * D + hd * DH + 16 * et + c) * 4), 0, 0);
+  }
+  const int my_pad = (lane < L) ? (a.kpad ? (int)a.kpad[tok0 + lane] : 0) : 1;
+  float* Ob = a.out + tok0 * D + hd * DH;
+#pragma unroll
+  for (int qb = 0; qb < NB; ++qb) {
+    const int i = 16 * qb + c;  // query of this lane's score column
+    const bool iok = i < L;
+    const Row8 qa = split_row8(qr[qb][0][0], qr[qb][0][1]), qc = split_row8(qr[qb][1][0], qr[qb][1][1]);
+    const int kb_end = a.causal ? qb : NB - 1;
+    f32x4 sv[NB];
+    float m = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < NB; ++kb) {
+      if (kb <= kb_end) {
+        const f32x4 s0 = dot16_x3(split_row8(kr[kb][0][0], kr[kb][0][1]), qa);  // S^T: [key][query i]
+        const f32x4 s1 = dot16_x3(split_row8(kr[kb][1][0], kr[kb][1][1]), qc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int j = 16 * kb + 4 * g + r;
+          const int jpad = __shfl(my_pad, j & 63, 64);
+          const bool allowed = iok && j < L && !jpad && (!a.causal || j <= i);
+          sv[kb][r] = allowed ? (s0[r] + s1[r]) * a.scale : -INFINITY;
+          m = fmaxf(m, sv[kb][r]);
+        }
+      }
+    }
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float l = 0.0f;
+#pragma unroll
+    for (int kb = 0; kb < NB; ++kb) {
+      if (kb <= kb_end) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = (sv[kb][r] == -INFINITY) ? 0.0f : __expf(sv[kb][r] - m);
+          sv[kb][r] = pv;
+          l += pv;
+        }
+      }
+    }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = (l > 0.0f) ? 1.0f / l : 0.0f;
+    f32x4 o[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    const uint64_t rowidx = ((uint64_t)(tok0 + i) * a.H + hd) * kLMax;
+#pragma unroll
+    for (int kb = 0; kb < NB; ++kb) {
+      if (kb <= kb_end) {
+        float pr[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pr[r] = a.drop.apply(sv[kb][r] * inv, rowidx + 16 * kb + 4 * g + r);
+        const Col4 pa = split4(pr);
+#pragma unroll
+        for (int et = 0; et < 4; ++et) {
+          const float vf[4] = {__uint_as_float(vr[kb][et][0]), __uint_as_float(vr[kb][et][1]),
+                               __uint_as_float(vr[kb][et][2]), __uint_as_float(vr[kb][et][3])};
+          o[et] = sum16_x3(pa, split4(vf), o[et]);
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * qb + 4 * g + r;
+      if (row < L) {
+#pragma unroll
+        for (int et = 0; et < 4; ++et) Ob[(int64_t)row * D + 16 * et + c] = o[et][r];
+      }
+    }
+    if (a.lse && g == 0 && iok) a.lse[(tok0 + i) * a.H + hd] = (l > 0.0f) ? m + logf(l) : -INFINITY;
+  }
+}
+
+__global__ __launch_bounds__(256) void mha_fwd_x3b64_k(FwdArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t unit = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (unit >= (int64_t)a.B * a.H) return;  // whole wave exits together
+  const int b = (int)(unit / a.H), hd = (int)(unit % a.H);
+  const int64_t tok0 = a.seg ? (int64_t)a.seg[b] : (int64_t)b * a.L;
+  int L = a.seg ? (a.seg[b + 1] - a.seg[b]) : a.L;
+  if (L > kLMax) L = kLMax;
+  if (L <= 0) return;
+  const int nb = __builtin_amdgcn_readfirstlane((L + 15) >> 4);
+  if (nb == 1) mha_fwd_x3b64_seq<1>(a, hd, tok0, L, lane);
+  else if (nb == 2) mha_fwd_x3b64_seq<2>(a, hd, tok0, L, lane);
+  else if (nb == 3) mha_fwd_x3b64_seq<3>(a, hd, tok0, L, lane);
+  else mha_fwd_x3b64_seq<4>(a, hd, tok0, L, lane);
+}
+
 __global__ __launch_bounds__(256) void mha_fwd_x3b_k(FwdArgs a) {
   const int lane = threadIdx.x & 63;
   const int64_t unit = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1175,7 +1294,7 @@ RSX_API int rsx_mha_fwd_x3(const float* qkv, const uint8_t* key_pad, const int* 
                            void* stream) {
   RSX_ARG(qkv && out, "null tensor");
   RSX_ARG(L >= 1 && L <= kLMax, "L must be in [1,64]");
-  RSX_ARG(Dh == 32, "bf16x3 attention head dim must be 32");
+  RSX_ARG(Dh == 32 || Dh == 64, "bf16x3 attention forward head dim must be 32 or 64");
   RSX_ARG(H >= 1, "H must be >= 1");
   RSX_ARG(p_drop >= 0.0f && p_drop < 1.0f, "p_drop must be in [0,1)");
   if (B == 0) return 0;
@@ -1185,7 +1304,9 @@ RSX_API int rsx_mha_fwd_x3(const float* qkv, const uint8_t* key_pad, const int* 
   a.scale = 1.0f / sqrtf((float)Dh);
   a.drop = rsx::make_dropout(p_drop, seed);
   static const bool legacy = getenv("RSX_MHA_FWD_LEGACY") != nullptr;  // A/B: the per-block-load kernel
-  if (legacy)
+  if (Dh == 64)
+    hipLaunchKernelGGL(mha_fwd_x3b64_k, dim3((unsigned)((B * H + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a);
+  else if (legacy)
     hipLaunchKernelGGL(mha_fwd_x3_k, dim3((unsigned)((B * H + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a);
   else
     hipLaunchKernelGGL(mha_fwd_x3b_k, dim3((unsigned)((B * H + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a);

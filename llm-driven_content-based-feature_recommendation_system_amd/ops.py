@@ -213,6 +213,10 @@ def _mha_x3(Dh):
     return _mha_precision == "bf16x3" and Dh == 32
 
 
+def _mha_x3_fwd(Dh):  # the bf16x3 forward also covers head dim 64 (BERT inference; no x3 backward)
+    return _mha_precision == "bf16x3" and Dh in (32, 64)
+
+
 class _MHA(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, key_pad, seg_off, H, causal, p_drop, seed):
@@ -231,7 +235,7 @@ class _MHA(torch.autograd.Function):
         kp = None
         if key_pad is not None:
             kp = _c(key_pad.to(torch.uint8)) if key_pad.dtype != torch.uint8 else _c(key_pad)
-        fn = N.lib().rsx_mha_fwd_x3 if _mha_x3(Dh) else N.lib().rsx_mha_fwd
+        fn = N.lib().rsx_mha_fwd_x3 if _mha_x3_fwd(Dh) else N.lib().rsx_mha_fwd
         rc = fn(N.ptr(qkv), N.ptr(kp), N.ptr(seg_off), B, L, H, Dh, int(causal), p_drop, seed, N.ptr(out), N.ptr(lse),
                 N.stream())
         N.check(rc, "mha_fwd")
