@@ -17,9 +17,8 @@ the drop-in endpoints (APIController/serving_controller.py) run end to end offli
     vocabulary file, so the default ``HashingTokenizer`` maps lower-cased words to ids in
     [1000, vocab) by a fixed hash with BERT's special ids (CLS 101, SEP 102, PAD 0). Pass any
     callable with the HF tokenizer's ``(text, max_length) -> (ids, mask)`` contract instead;
-  * the STD vocabulary of utils/vocab.py is a fixed table of H&M values; here it is built with
-    the same rule (sorted union of the values -> ids from 2; 0 PAD, 1 UNK) from the products
-    at hand, or injected;
+  * the STD vocabulary is the reference's fixed table (utils/vocab.py here, restated from
+    utils/vocab.py:5-444: 382 values, ids 2..383, PAD 0, UNK 1), the collator's default;
   * the product source is any object with ``fetch_products() -> list[dict]`` (the rows of
     ``select(ProductInferenceInput.product_id, .feature_data, .product_name)``); a maintainer
     adapts a SQLAlchemy session with a three-line wrapper.
@@ -34,11 +33,11 @@ from typing import Any, Dict, Iterable, List, Optional, Sequence
 import torch
 from pydantic import BaseModel
 
-PAD_ID, UNK_ID = 0, 1
+from .utils.vocab import (PAD_ID, RE_FEATURE_KEYS, STD_TOKEN_TO_ID, STD_VOCAB_CONFIG, UNK_ID,  # noqa: F401
+                          get_std_field_keys, get_std_vocab_size)
+
 CLS_ID, SEP_ID = 101, 102          # bert-base-uncased special ids
-RE_FEATURE_KEYS = ["[CAT]", "[MAT]", "[DET]", "[FIT]", "[FNC]", "[SPC]", "[COL]", "[CTX]", "[LOC]"]
-STD_FIELD_KEYS = ["product_type_name", "graphical_appearance_name", "colour_group_name", "department_name",
-                  "section_name", "perceived_colour_value_name"]
+STD_FIELD_KEYS = get_std_field_keys()
 FIELD_PROMPT_MAP = {"[CAT]": "Clothing Category", "[MAT]": "Fabric Material", "[DET]": "Garment Detail",
                     "[FIT]": "Clothing Fit", "[FNC]": "Apparel Function", "[SPC]": "Product Specification",
                     "[COL]": "Garment Color", "[CTX]": "Occasion", "[LOC]": "Body Part"}
@@ -118,26 +117,21 @@ class HashingTokenizer:
         return ids + [PAD_ID] * pad, mask + [0] * pad
 
 
-def build_std_vocab(items: Iterable[TrainingItem], keys: Sequence[str] = STD_FIELD_KEYS) -> Dict[str, int]:
-    """utils/vocab.py:431-434's rule on the given products: the sorted union of every STD
-    value -> id 2 + index (0 PAD, 1 UNK)."""
-    vals = set()
-    for it in items:
-        for k in keys:
-            v = it.feature_data.get(k)
-            if v:
-                vals.add(str(v))
-    return {tok: i + 2 for i, tok in enumerate(sorted(vals))}
-
-
 class SimCSECollator:
-    """item_tower.py:465-605 with an injectable tokenizer and STD vocabulary."""
+    """item_tower.py:465-605 with an injectable tokenizer. The STD vocabulary defaults to the
+    reference's fixed table (utils/vocab.py: ids 2..383, ``std_vocab_size`` 384); an injected
+    one must keep every id below ``std_vocab_size`` (the embedding's row count): checked here,
+    on the host, before any tensor reaches the GPU gather."""
 
     def __init__(self, tokenizer=None, std_vocab: Optional[Dict[str, int]] = None,
                  std_keys: Sequence[str] = STD_FIELD_KEYS, max_re_len: int = MAX_RE_LEN,
-                 max_txt_len: int = MAX_TXT_LEN):
+                 max_txt_len: int = MAX_TXT_LEN, std_vocab_size: Optional[int] = None):
         self.tokenizer = tokenizer or HashingTokenizer()
-        self.std_vocab = std_vocab or {}
+        self.std_vocab = STD_TOKEN_TO_ID if std_vocab is None else std_vocab
+        self.std_vocab_size = get_std_vocab_size() if std_vocab_size is None else int(std_vocab_size)
+        top = max(self.std_vocab.values(), default=UNK_ID)
+        if top >= self.std_vocab_size or min(self.std_vocab.values(), default=2) < 0:
+            raise ValueError(f"STD vocabulary ids must lie in [0, {self.std_vocab_size}); got max id {top}")
         self.std_keys = list(std_keys)
         self.re_keys = RE_FEATURE_KEYS
         self.max_re_len = max_re_len
@@ -230,10 +224,11 @@ class SimCSERecSysDataset(torch.utils.data.Dataset):
 
 
 def synthetic_product_rows(n: int, seed: int = 0) -> List[Dict[str, Any]]:
-    """H&M-shaped synthetic products (ids 1..n): six STD fields from small value pools, a few
-    RE list fields and a short name. For tests and the offline endpoints."""
+    """H&M-shaped synthetic products (ids 1..n): the six STD fields drawn from the reference's
+    value table (utils/vocab.py; 2 % of values out of vocabulary -> UNK), a few RE list fields
+    and a short name. For tests and the offline endpoints."""
     rng = random.Random(seed)
-    pools = {k: [f"{k}_{i}" for i in range(12)] for k in STD_FIELD_KEYS}
+    pools = {k: list(STD_VOCAB_CONFIG[k]) + [f"unlisted {k} {i}" for i in range(2)] for k in STD_FIELD_KEYS}
     words = [f"w{i}" for i in range(400)]
     rows = []
     for pid in range(1, n + 1):

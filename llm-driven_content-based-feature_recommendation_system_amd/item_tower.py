@@ -34,8 +34,7 @@ from . import _native as N
 from . import ops
 from .tower_code.v1_refine_usertower import encoder_stack
 
-PAD_ID = 0   # utils/vocab.py PAD_ID
-UNK_ID = 1
+from .utils.vocab import PAD_ID, UNK_ID  # noqa: E402,F401
 EMBED_DIM = 128
 OUTPUT_DIM_ENCODER = 128
 OUTPUT_DIM_PROJECTOR = 128
@@ -250,6 +249,9 @@ class HybridItemTower(nn.Module):
         return _ln(vec, self.re_ln)
 
     def forward(self, std_input, re_input_ids, re_attn_mask, text_input_ids, text_attn_mask):
+        n_std = self.std_embedding.num_embeddings
+        if std_input.numel() and (int(std_input.max()) >= n_std or int(std_input.min()) < 0):
+            raise IndexError(f"STD id out of range [0, {n_std}) for std_embedding (utils/vocab.py ids 0..383)")
         std_emb = _ln(self.std_embedding(std_input) + self.std_field_emb, self.std_ln)        # :240-243
         re_vec = self.re_vectors(re_input_ids, re_attn_mask)                                   # :247-262
         if (not torch.is_grad_enabled() and not self.bert_model.training
@@ -343,7 +345,7 @@ def train_simcse_from_db(encoder: nn.Module, projector: nn.Module, db_session, b
 
     from transformers import get_linear_schedule_with_warmup
 
-    from .item_data import SimCSECollator, SimCSERecSysDataset, build_std_vocab, rows_to_items
+    from .item_data import SimCSECollator, SimCSERecSysDataset, rows_to_items
 
     rows = db_session.fetch_products()
     if not rows:
@@ -370,7 +372,7 @@ def train_simcse_from_db(encoder: nn.Module, projector: nn.Module, db_session, b
     rng = random.Random(seed)
     dataset = SimCSERecSysDataset(products, dropout_prob=dropout_prob, rng=rng)
     if collator is None:
-        collator = SimCSECollator(std_vocab=build_std_vocab(products))
+        collator = SimCSECollator(std_vocab_size=encoder.std_embedding.num_embeddings)
     gen = torch.Generator().manual_seed(seed) if seed is not None else None
     loader = torch.utils.data.DataLoader(dataset, batch_size=batch_size, shuffle=True, collate_fn=collator,
                                          drop_last=True, num_workers=0, generator=gen)

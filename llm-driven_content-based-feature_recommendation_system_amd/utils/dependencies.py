@@ -24,12 +24,16 @@ _gpu_lock = threading.Lock()
 DEVICE = torch.device("cuda")
 
 
-def initialize_global_models(std_vocab_size: int = 384, num_std_fields: int = 6, embed_dim: int = 128,
+def initialize_global_models(std_vocab_size: Optional[int] = None, num_std_fields: Optional[int] = None,
+                             embed_dim: int = 128,
                              bert_model=None, batch_size: int = 192, device=None):
     """Builds the encoder / projector on the GPU (the reference's startup hook; its sizes are
     get_std_vocab_size() = 384 and len(get_std_field_keys()) = 6)."""
     from ..item_tower import HybridItemTower, OptimizedItemTower
+    from .vocab import get_std_field_keys, get_std_vocab_size
     global global_encoder, global_projector, global_batch_size
+    std_vocab_size = get_std_vocab_size() if std_vocab_size is None else std_vocab_size
+    num_std_fields = len(get_std_field_keys()) if num_std_fields is None else num_std_fields
     dev = torch.device(device) if device is not None else DEVICE
     global_encoder = HybridItemTower(std_vocab_size, num_std_fields, embed_dim=embed_dim,
                                      output_dim=embed_dim, bert_model=bert_model).to(dev)

@@ -18,7 +18,7 @@ from typing import Optional
 
 import torch
 
-from ..item_data import SimCSECollator, build_std_vocab, parse_db_row
+from ..item_data import SimCSECollator, parse_db_row
 from .dependencies import get_global_batch_size, get_global_encoder, gpu_lock
 
 
@@ -42,7 +42,7 @@ def generate_and_save_item_vectors(db_session, save_dir: str = "models", safe_mo
     items.sort(key=lambda x: x.product_id)       # string order, as the reference (:136-138)
     ordered_ids = [it.product_id for it in items]
     if collator is None:
-        collator = SimCSECollator(std_vocab=build_std_vocab(items))
+        collator = SimCSECollator(std_vocab_size=model.std_embedding.num_embeddings)
     bs = get_global_batch_size() * (1 if safe_mode else 4)
     vecs = []
     with gpu_lock():

@@ -43,7 +43,7 @@ def test_refresh_item_vectors_endpoint(app_client):
     # the same vectors as one direct eval forward over the whole (id-sorted, tagged) set
     rows = deps.global_product_store.fetch_products()
     items = sorted((D.parse_db_row(x) for x in rows), key=lambda x: x.product_id)
-    col = D.SimCSECollator(std_vocab=D.build_std_vocab(items))
+    col = D.SimCSECollator()                       # the fixed reference vocabulary
     enc = deps.get_global_encoder().eval()
     with torch.no_grad():
         ref = enc(*[t.cuda() for t in col.process_batch_items(items)]).cpu()

@@ -2,7 +2,7 @@
 # Run GPU steps in order; each line of the step file is "<timeout_s> <command...>".
 # Stops after a step that faulted, aborted, segfaulted or timed out (rc 124/134/137/139 or >128),
 # continues after ordinary failures (rc 1/2). Logs go to gpurun_out/steps.log.
-# usage: bash tools/gpu_steps.sh stepfile
+# usage: bash tools/gpu_steps.sh .steps/<stepfile> (step lists are untracked scratch under .steps/)
 mkdir -p gpurun_out
 while IFS= read -r line; do
   [ -z "$line" ] && continue
