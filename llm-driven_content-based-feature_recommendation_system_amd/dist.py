@@ -22,6 +22,8 @@ the HIP kernels through ops.
 """
 from __future__ import annotations
 
+import contextlib
+
 import torch
 import torch.distributed as dist
 
@@ -134,18 +136,27 @@ def all_reduce_sum_(t: torch.Tensor) -> torch.Tensor:
 
 class GradBucket:
     """Sum of the replicated parameters' gradients over ranks (DDP semantics), overlapped with
-    backward. Parameters are grouped into ~bucket_mb buckets in reverse registration order (the
-    order backward produces them); a post-accumulate-grad hook copies each gradient into its
-    bucket's flat fp32 buffer, and a bucket's all-reduce is launched (asynchronously, on the
-    communicator's stream) as soon as it and every earlier bucket are complete, so the
-    exchange runs under the rest of backward. Launch order is the bucket index on every rank.
-    Each bucket carries one has-gradient flag per parameter in the same buffer: after the
-    exchange a parameter whose gradient is None on EVERY rank stays None (the single-GPU step's
-    AdamW skips it), otherwise its gradient becomes the summed slice (a view of the bucket).
-    Call the bucket after backward to launch what is left and wait."""
+    backward. Parameters (deduplicated by identity) are grouped into ~bucket_mb buckets in
+    reverse registration order (the order backward produces them); a post-accumulate-grad hook
+    copies each gradient into its bucket's flat fp32 buffer, and a bucket's all-reduce is
+    launched (asynchronously, on the communicator's stream) as soon as it and every earlier
+    bucket are complete, so the exchange runs under the rest of backward. Launch order is the
+    bucket index on every rank. Each bucket carries one has-gradient flag per parameter in the
+    same buffer: after the exchange a parameter whose gradient is None on EVERY rank stays None
+    (the single-GPU step's AdamW skips it), otherwise its gradient becomes the summed slice (a
+    view of the bucket). Call the bucket after backward to launch what is left and wait.
+
+    Contract: ONE synchronising backward per call. A second hook for the same parameter before
+    the call raises (its bucket may already be in flight). Gradient accumulation runs the
+    earlier micro-batches inside ``with bucket.no_sync():`` (hooks idle, p.grad accumulates),
+    then the last backward outside it: its hooks copy the accumulated gradients."""
 
     def __init__(self, params, bucket_mb: float = 16.0):
-        self.params = [p for p in params if p.requires_grad]
+        seen, self.params = set(), []
+        for p in params:
+            if p.requires_grad and id(p) not in seen:
+                seen.add(id(p))
+                self.params.append(p)
         self.numel = sum(p.numel() for p in self.params)
         cap = max(1, int(bucket_mb * (1 << 20) / 4))
         self.buckets = []          # [[param index, ...], ...]
@@ -170,13 +181,24 @@ class GradBucket:
         self.flat = None
         self.by_id = {id(p): i for i, p in enumerate(self.params)}
         self.handles = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
+        self._sync = True
         self._reset()
 
     def _reset(self):
         self.filled = [0] * len(self.buckets)
+        self.got = [False] * len(self.params)
         self.work = [None] * len(self.buckets)
         self.launched = 0
         self.active = False
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Backward passes inside accumulate into p.grad without touching the buckets."""
+        prev, self._sync = self._sync, False
+        try:
+            yield
+        finally:
+            self._sync = prev
 
     def _buffers(self, dev):
         if self.flat is None or self.flat[0].device != dev:
@@ -185,20 +207,30 @@ class GradBucket:
                          for n, idx in zip(self.sizes, self.buckets)]
         return self.flat
 
-    def _on_grad(self, p):
-        if world()[1] == 1:
-            return
-        i = self.by_id[id(p)]
-        b, o, s = self.where[i]
+    def _activate(self, dev):
         if not self.active:
             self.active = True
-            bufs = self._buffers(p.device)
-            for f, n in zip(bufs, self.sizes):
+            for f, n in zip(self._buffers(dev), self.sizes):
                 f[n:].zero_()
+
+    def _copy_in(self, i):
+        p = self.params[i]
+        b, o, s = self.where[i]
         f = self.flat[b]
         f[o:o + p.numel()].copy_(p.grad.reshape(-1))
         f[self.sizes[b] + s].fill_(1.0)
+        self.got[i] = True
         self.filled[b] += 1
+
+    def _on_grad(self, p):
+        if world()[1] == 1 or not self._sync:
+            return
+        i = self.by_id[id(p)]
+        if self.got[i]:
+            raise RuntimeError("GradBucket: a second gradient for one parameter before bucket() was called "
+                               "(two backward passes?); accumulate earlier passes under bucket.no_sync()")
+        self._activate(p.device)
+        self._copy_in(i)
         while self.launched < len(self.buckets) and self.filled[self.launched] == len(self.buckets[self.launched]):
             self._launch(self.launched)
 
@@ -209,17 +241,18 @@ class GradBucket:
     def __call__(self):
         if world()[1] == 1 or not self.params:
             return
-        if not self.active:
-            self.active = True
-            bufs = self._buffers(self.params[0].device)
-            for f, n in zip(bufs, self.sizes):
-                f[n:].zero_()
-        # buckets still open: parameters without a gradient on this rank contribute zeros
+        self._activate(self.params[0].device)
+        # buckets still open: gradients whose hook did not fire in the last backward (made
+        # under no_sync only) are copied now; parameters without a gradient contribute zeros
         for b in range(self.launched, len(self.buckets)):
             f = self.flat[b]
             for i in self.buckets[b]:
+                if self.got[i]:
+                    continue
                 p = self.params[i]
-                if p.grad is None:
+                if p.grad is not None:
+                    self._copy_in(i)
+                else:
                     _, o, _ = self.where[i]
                     f[o:o + p.numel()].zero_()
         while self.launched < len(self.buckets):

@@ -115,9 +115,9 @@ def _bert_qkv(att_self):
     qkv row layout of rsx_mha_fwd: Q | K | V, head h at columns h*dh), rebuilt when one changes."""
     ps = (att_self.query.weight, att_self.key.weight, att_self.value.weight,
           att_self.query.bias, att_self.key.bias, att_self.value.bias)
-    key = tuple((p.data_ptr(), p._version) for p in ps)
+    key = ops._tensor_key(ps)
     c = att_self.__dict__.get("_rsx_qkv")
-    if c is None or c[0] != key:
+    if c is None or not ops._key_eq(c[0], key):
         c = (key, torch.cat(ps[:3], 0).contiguous(), torch.cat(ps[3:], 0).contiguous())
         att_self.__dict__["_rsx_qkv"] = c
     return c[1], c[2]

@@ -17,7 +17,11 @@ NCE_MASK_ITEM_USER = 6
 NCE_SUPCON = 9
 
 _NSPLIT_FWD = 8
-_NSPLIT_FWD_GROUPED = int(os.environ.get("RSX_NCE_NSPLIT_FWD", "8"))  # partial slots; the fused forward runs 4 splits on the leading row blocks, 8 on the tail
+# partial slots of the grouped forward; the fused forward (rsx_nce_grouped_fwd_grad) accepts 1/2/4/8 and
+# runs 4 splits on the leading row blocks, 8 on the tail
+_NSPLIT_FWD_GROUPED = int(os.environ.get("RSX_NCE_NSPLIT_FWD", "8"))
+if _NSPLIT_FWD_GROUPED not in (1, 2, 4, 8):
+    raise ValueError("RSX_NCE_NSPLIT_FWD must be 1, 2, 4 or 8 (the fused forward's supported partial-slot counts)")
 _NSPLIT_BWD = 8
 
 # Logit precision of the grouped (live LogQ) loss kernels, include/recsys_amd.h RSX_NCE_*:
@@ -49,6 +53,25 @@ def next_seed() -> int:
 
 def _c(t):
     return t if t is None or t.is_contiguous() else t.contiguous()
+
+
+def _tensor_key(ts):
+    """Cache key of derived device images: the tensor OBJECTS (held, so their storage cannot be
+    recycled under a stale key), their storage pointers and in-place version counters."""
+    return tuple((t, t.data_ptr(), t._version) for t in ts)
+
+
+def _key_eq(a, b) -> bool:
+    """Key equality with identity for tensors (== on tensors is elementwise)."""
+    if a is None or len(a) != len(b):
+        return False
+    for x, y in zip(a, b):
+        if isinstance(x, tuple):
+            if x[0] is not y[0] or x[1:] != y[1:]:
+                return False
+        elif x != y:
+            return False
+    return True
 
 
 # ----------------------------------------------------------------------------------------
@@ -1084,10 +1107,12 @@ def deepfm_forward(x, emb_tables, lin_tables, out_bias, dnn_weights, dnn_biases,
         logit = torch.empty(R, device=dev, dtype=torch.float32)
         prob = torch.empty(R, device=dev, dtype=torch.float32)
         w1, w2 = _c(dnn_weights[0]), _c(dnn_weights[1])
-        key = (F, w1.data_ptr(), w1._version, w2.data_ptr(), w2._version, dev)
+        if len(emb_tables) != F or len(lin_tables) != F:
+            raise ValueError(f"deepfm: {len(emb_tables)} embedding / {len(lin_tables)} linear tables for {F} fields")
+        key = (F, dev) + _tensor_key((w1, w2))
         b1, b2 = dnn_biases
         with timed("deepfm/fused"):
-            if cache is not None and cache.get("key") == key:
+            if cache is not None and _key_eq(cache.get("key"), key):
                 ws = cache["ws"]
             else:
                 ws = torch.empty(N.lib().rsx_deepfm_fused_workspace_bytes(F), device=dev, dtype=torch.uint8)
@@ -1098,8 +1123,8 @@ def deepfm_forward(x, emb_tables, lin_tables, out_bias, dnn_weights, dnn_biases,
             if cache is not None and _DEEPFM_PACK and N.lib().rsx_deepfm_fused_uses_packed(F):
                 # inference images of the tables: [vocab][32] per field (V row, W, pad), rebuilt when
                 # any table changes; one 128-B line per (row, field) instead of two
-                tkey = tuple((t.data_ptr(), t._version) for t in list(emb_tables) + list(lin_tables))
-                if cache.get("tkey") != tkey:
+                tkey = _tensor_key(list(emb_tables) + list(lin_tables))
+                if not _key_eq(cache.get("tkey"), tkey):
                     cache.pop("packed", None)
                     packed = [torch.empty(v.shape[0], 32, device=dev, dtype=torch.float32) for v in emb_tables]
                     for v, w, p in zip(emb_tables, lin_tables, packed):

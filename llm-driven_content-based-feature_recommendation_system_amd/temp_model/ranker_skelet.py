@@ -61,10 +61,11 @@ class DeepFM(nn.Module):
 
     def _bias_value(self) -> float:
         """out.bias as a host float, read once per parameter version (no sync per forward)."""
-        v = self.out.bias._version
-        if getattr(self, "_bias_cache", (None, 0.0))[0] != v:
-            self._bias_cache = (v, float(self.out.bias.item()))
-        return self._bias_cache[1]
+        b = self.out.bias
+        c = self.__dict__.get("_bias_cache")
+        if c is None or c[0] is not b or c[1] != b._version:
+            c = self.__dict__["_bias_cache"] = (b, b._version, float(b.item()))
+        return c[2]
 
     @torch.no_grad()
     def forward_logits(self, X):

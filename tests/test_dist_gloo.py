@@ -81,6 +81,33 @@ def _worker(rank, world, port, q):
         torch.testing.assert_close(bias.grad, b_ref.grad, atol=1e-6, rtol=1e-5)
         assert unused.grad is None
         torch.testing.assert_close(partial.grad, torch.full((300,), 2.0))
+
+        # gradient accumulation: micro-batch 0 under no_sync, micro-batch 1 synchronising; the
+        # parameter listed twice is bucketed once; `late` gets a gradient only in micro-batch 0
+        # (its hook never fires in the synchronising pass, bucket() copies it in)
+        w2 = Wt.clone().requires_grad_()
+        late = torch.ones(7, requires_grad=True)
+        acc = D.GradBucket([w2, late, w2], bucket_mb=1e-3)
+        assert len(acc.params) == 2
+        Xs = [X1[rank * b:(rank + 1) * b], X2[rank * b:(rank + 1) * b]]
+        with acc.no_sync():
+            (Xs[0] @ w2).square().sum().backward()
+            (late * (rank + 1)).sum().backward()
+        (Xs[1] @ w2).square().sum().backward()
+        acc()
+        w_ref2 = Wt.clone().requires_grad_()
+        ((X1 @ w_ref2).square().sum() + (X2 @ w_ref2).square().sum()).backward()
+        torch.testing.assert_close(w2.grad, w_ref2.grad, atol=1e-4, rtol=1e-5)
+        torch.testing.assert_close(late.grad, torch.full((7,), float(sum(r + 1 for r in range(world)))))
+        # two synchronising backward passes before bucket() is a usage error, not silent divergence
+        w2.grad = None
+        (Xs[0] @ w2).sum().backward()
+        try:
+            (Xs[1] @ w2).sum().backward()
+            raise AssertionError("second backward was accepted")
+        except RuntimeError as e:
+            assert "second gradient" in str(e)
+        acc._reset()
         q.put((rank, "ok"))
     except Exception as e:  # pragma: no cover - reported to the parent
         q.put((rank, repr(e)))
