@@ -182,6 +182,64 @@ def test_mha_packed_segments(gpu, mha_precision, dh):
     torch.testing.assert_close(qd.grad.cpu().double(), q64.grad, atol=_MHA_TOL[mha_precision][1], rtol=1e-4)
 
 
+@pytest.mark.parametrize("L,H,causal,use_pad,packed", [(50, 4, True, True, False), (64, 2, True, True, False),
+                                                       (64, 4, False, False, False), (33, 3, False, True, False),
+                                                       (64, 4, True, True, True), (64, 12, False, False, True)])
+def test_mha_head_dim_64_forward(gpu, mha_precision, L, H, causal, use_pad, packed):
+    """Head dim 64 (BERT's 768 / 12; forward only — the x3 kernel mha_fwd_x3b64_k under bf16x3,
+    mha_fwd_k<64> under fp32): dense [B, L] with left padding / causal, and packed segments of
+    1..64 tokens (bert_packed_ok allows up to 64: NB = 3 / 4 query blocks), against the float64
+    reference at the bf16x3 tolerance."""
+    g = torch.Generator().manual_seed(L * 13 + H)
+    dh = 64
+    if packed:
+        lens = torch.randint(1, L + 1, (29,), generator=g)
+        lens[:3] = torch.tensor([L, 1, 33])
+        seg = torch.cat([torch.zeros(1, dtype=torch.long), torch.cumsum(lens, 0)])
+        qkv = torch.randn(int(seg[-1]), 3 * H * dh, generator=g)
+        pad = torch.zeros(qkv.shape[0], dtype=torch.bool)
+        if use_pad:
+            pad[seg[1:] - 1] = torch.rand(len(lens), generator=g) < 0.3
+        ref = torch.cat([_mha_ref(qkv.double()[int(seg[b]):int(seg[b + 1])][None],
+                                  pad[int(seg[b]):int(seg[b + 1])][None], H, causal)[0] for b in range(len(lens))])
+        out = ops.mha(qkv.to(gpu), pad.to(gpu) if use_pad else None, H, causal, seg_off=seg.to(gpu))
+    else:
+        B = 21
+        qkv = torch.randn(B, L, 3 * H * dh, generator=g)
+        pad = None
+        if use_pad:
+            lens = torch.randint(1, L + 1, (B,), generator=g)
+            lens[0] = L
+            pad = torch.arange(L)[None, :] < (L - lens)[:, None]
+        ref = _mha_ref(qkv.double(), pad, H, causal)
+        out = ops.mha(qkv.to(gpu), pad.to(gpu) if pad is not None else None, H, causal)
+        if use_pad and causal:
+            assert (out[pad.to(gpu)] == 0).all()
+    # 64-dim scores have twice the terms of the 32-dim case: same per-product bound, 2x atol
+    torch.testing.assert_close(out.cpu().double(), ref, atol=2 * _MHA_TOL[mha_precision][0], rtol=1e-5)
+
+
+def test_mha_head_dim_64_dropout_matches_fp32(gpu):
+    """Head dim 64 with dropout: the bf16x3 forward draws the fp32 kernel's keep mask (same hash
+    index), so the outputs agree to the bf16x3 tolerance; about 20 % of probabilities dropped."""
+    g = torch.Generator().manual_seed(64)
+    B, L, H, dh = 12, 64, 4, 64
+    qkv = torch.randn(B, L, 3 * H * dh, generator=g).to(gpu)
+    pad = (torch.arange(L)[None, :] < torch.randint(0, L, (B,), generator=g)[:, None]).to(gpu)
+    res = {}
+    prev = ops.mha_precision()
+    try:
+        for p in ("fp32", "bf16x3"):
+            ops.set_mha_precision(p)
+            with torch.no_grad():
+                res[p] = ops._MHA.apply(qkv, pad, None, H, True, 0.2, 4242)
+                res[p + "_nodrop"] = ops._MHA.apply(qkv, pad, None, H, True, 0.0, 0)
+    finally:
+        ops.set_mha_precision(prev)
+    torch.testing.assert_close(res["bf16x3"], res["fp32"], atol=2 * _MHA_TOL["bf16x3"][0], rtol=1e-5)
+    assert not torch.equal(res["fp32"], res["fp32_nodrop"])
+
+
 def test_mha_precisions_share_dropout_mask(gpu):
     """With dropout the bf16x3 and fp32 kernels draw the same keep mask (same hash index), so
     outputs and gradients agree to the bf16x3 tolerance (_MHA_TOL)."""
