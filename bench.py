@@ -16,7 +16,11 @@ Multi-GPU (one process per GPU, RCCL): ``--gpus N`` without torchrun's environme
 the GPU); under torchrun each rank holds 8192 users by default, so the global batch is
 8192 x N (weak scaling; N=4 is configs[3]'s global batch 32768, negatives all-gathered).
 ``--batch G`` fixes the global batch instead (strong scaling). Users are split by rank; see
-dist.py. Prints ONE JSON line on rank 0.
+dist.py. At every N the JSON also carries ``strong_32768`` (configs[3]: the FIXED global batch
+32768 split over the N ranks; at N > 1 with rank 0's one-GPU run of the same batch in the same
+process and the speedup over it) and, at N > 1, ``retrieve_rerank_sharded`` (configs[4]: the 1M
+corpus sharded by item range, merged top-100 over RCCL, DeepFM rerank sharded by query).
+Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
@@ -56,8 +60,9 @@ def parse():
     ap.add_argument("--freeze-items", action="store_true", help="epoch-1 regime (item matrix frozen)")
     ap.add_argument("--cpu-loss-chunk", type=int, default=64,
                     help="row chunk of the CPU oracle's N x N main loss (same arithmetic, bounded RAM)")
-    ap.add_argument("--cpu-threads", type=int, default=16,
-                    help="CPU baseline threads (capped at the physical cores; 16 = one GPU's CPU share)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads; 0 = the host's physical cores (BASELINE.md), capped by the CPUs "
+                         "this process may use (affinity mask and cgroup CPU quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-batch4096", action="store_true",
@@ -83,6 +88,9 @@ def parse():
     ap.add_argument("--blas", default="default", choices=["default", "hipblaslt", "rocblas", "ck"],
                     help="library torch uses for the tower's dense projections")
     ap.add_argument("--master-port", type=int, default=29531, help="rendezvous port when spawning ranks")
+    ap.add_argument("--rehearse-one-device", action="store_true",
+                    help="rehearsal of the N>1 code path on a 1-GPU box: every rank on cuda:0, gloo transport "
+                         "(numbers are not scaling results)")
     return ap.parse_args()
 
 
@@ -103,6 +111,11 @@ def setup_dist(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+    if world > 1 and args.rehearse_one_device:
+        import torch.distributed as dist
+        torch.cuda.set_device(0)
+        dist.init_process_group(backend="gloo", init_method="env://", rank=rank, world_size=world)
+        return rank, world, torch.device("cuda", 0)
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
@@ -134,6 +147,13 @@ def host_cpu_info():
     try:
         info["affinity_cpus"] = len(os.sched_getaffinity(0))
     except AttributeError:
+        pass
+    try:  # cgroup v2 CPU bandwidth quota ("max 100000" = unlimited)
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            info["cgroup_cpu_quota"] = round(int(quota) / int(period), 2)
+    except (OSError, ValueError):
         pass
     return info
 
@@ -170,8 +190,8 @@ def cpu_baseline(args, items, cfg, batch_size, batch_seed):
     from recsys_amd import synth
     info = host_cpu_info()
     phys = info.get("physical_cores") or os.cpu_count() or 1
-    avail = info.get("affinity_cpus") or phys
-    threads = max(1, min(args.cpu_threads, phys, avail))
+    avail = min(info.get("affinity_cpus") or phys, int(info.get("cgroup_cpu_quota") or phys))
+    threads = max(1, min(args.cpu_threads or phys, phys, avail))
     prev_threads = torch.get_num_threads()
     torch.set_num_threads(threads)
     torch.manual_seed(args.seed)
@@ -191,6 +211,8 @@ def cpu_baseline(args, items, cfg, batch_size, batch_seed):
     torch.set_num_threads(prev_threads)
     return {"value": round(batch_size / dt, 3), "unit": "pairs/s", "cores": threads,
             "kind": "port",
+            "threads_rule": ("physical cores (BASELINE.md), capped by this process's affinity mask / cgroup CPU "
+                             f"quota: physical {phys}, usable {avail}"),
             "host": info,
             "sample": (f"oracle/user_tower.py contrastive_step (fp32 PyTorch CPU, dropout 0.2, AdamW) on the GPU "
                        f"headline's first global batch ({batch_size} users, {n_valid} valid steps, same seed); "
@@ -313,49 +335,77 @@ def bench_gather_1m(device, T=316_372, rows=1_000_000, iters=10, flush_mb=1024):
             "note": "uniform ids over a 512 MB table, 1 GiB cache flush before each launch, time table uncredited"}
 
 
-def bench_retrieve_rerank(args, device, deepfm):
-    """BASELINE configs[4] on one GPU: Q=4096 normalised user vectors against a 1M-item
-    normalised corpus (seed 5), top-100 by rsx_retrieve_topk, 39 hashed (user bucket, item)
-    sparse ids per candidate, DeepFM on the Q x 100 rows, final top-10 per query by
-    probability. queries/s; the retrieval kernel priced at the fp32 MFMA peak."""
+def bench_retrieve_rerank(args, device, deepfm, rank=0, world=1):
+    """BASELINE configs[4]: Q=4096 normalised user vectors against a 1M-item normalised corpus
+    (seed 5), top-100 by rsx_retrieve_topk, 39 hashed (user bucket, item) sparse ids per
+    candidate, DeepFM on the Q x 100 rows, final top-10 per query by probability. queries/s; the
+    retrieval kernel priced at the fp32 MFMA peak.
+
+    world > 1: the corpus is sharded by item range (I/N rows per rank); every rank
+    scores all Q queries against its shard, the [Q, 100] (score, global index) lists are
+    all-gathered over RCCL and merged by (score desc, index asc) (dist.retrieve_topk_sharded);
+    the DeepFM rerank is sharded by query (rank r reranks queries [r Q/N, (r+1) Q/N)). The step
+    time is the max over ranks; value = Q / that time."""
+    from recsys_amd import dist as D
     from recsys_amd import ops
     Q, I, K, F = 4096, args.corpus, 100, 39
     g = torch.Generator(device="cpu").manual_seed(5)
-    corpus = torch.nn.functional.normalize(torch.randn(I, 128, generator=g), dim=1).to(device)
+    corpus_full = torch.nn.functional.normalize(torch.randn(I, 128, generator=g), dim=1)
     users = torch.nn.functional.normalize(torch.randn(Q, 128, generator=g), dim=1).to(device)
+    lo, hi = rank * I // world, (rank + 1) * I // world
+    corpus = corpus_full[lo:hi].to(device)
+    del corpus_full
+    q0, q1 = rank * Q // world, (rank + 1) * Q // world
     V = args.deepfm_vocab
     fld = torch.arange(F, device=device, dtype=torch.int64).view(1, 1, F)
-    ubucket = (torch.arange(Q, device=device, dtype=torch.int64) % 1000).view(Q, 1, 1)
+    ubucket = (torch.arange(q0, q1, device=device, dtype=torch.int64) % 1000).view(q1 - q0, 1, 1)
 
     def step():
-        sc, idx = ops.retrieve_topk(users, corpus, K)
+        if world > 1:
+            sc, idx = D.retrieve_topk_sharded(users, corpus, lo, K)
+        else:
+            sc, idx = ops.retrieve_topk(users, corpus, K)
+        idx = idx[q0:q1]
         h = idx.unsqueeze(-1) * 0x9E3779B1 + ubucket * 0x85EBCA77 + fld * 0xC2B2AE35
         feats = ((h ^ (h >> 29)) & 0x7FFFFFFF) % V
-        _, prob = deepfm.forward_logits(feats.view(Q * K, F))
-        top_p, top_j = torch.topk(prob.view(Q, K), 10, dim=1)
+        _, prob = deepfm.forward_logits(feats.view((q1 - q0) * K, F))
+        top_p, top_j = torch.topk(prob.view(q1 - q0, K), 10, dim=1)
         return torch.gather(idx, 1, top_j), top_p
 
     for _ in range(2):
         step()
     torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
     iters = 5
     ops.timing_start()
     t0 = time.perf_counter()
     for _ in range(iters):
         step()
     torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / iters
+    if world > 1:
+        torch.distributed.barrier()
+    el = torch.tensor([time.perf_counter() - t0], device=device, dtype=torch.float64)
+    if world > 1:
+        D.all_reduce_(el, op=torch.distributed.ReduceOp.MAX)
+    dt = float(el.item()) / iters
     kt = ops.timing_stop()
     n, ms = kt.get("retrieve_topk", (1, 0.0))
     rs = ms / 1e3 / max(n, 1)
-    flops = 2.0 * Q * I * 128  # algorithmic (one score per (query, item)); the exact path scores twice
-    return {"metric": "retrieve->rerank queries/sec (1M-item corpus, top-100, DeepFM rerank, top-10)",
-            "value": round(Q / dt, 1), "unit": "queries/s", "queries": Q, "corpus": I,
-            "ms_per_batch": round(dt * 1e3, 3), "rerank_rows_per_s": round(Q * K / dt, 1),
-            "data": "synthetic normalised N(0,1) corpus / users, hashed rerank ids",
-            "retrieval": {"kernel": "topk_fast_scan_k (candidates + collect passes) + topk_thresh_k + topk_final_k", "avg_ms": round(rs * 1e3, 4),
-                          "achieved_TFLOPs": round(flops / rs / 1e12, 2), "peak_TFLOPs": FP32_MFMA_PEAK_TFLOPS,
-                          "frac": round(flops / rs / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)}}
+    flops = 2.0 * Q * (hi - lo) * 128  # algorithmic (one score per (query, item) of this rank's shard)
+    out = {"metric": "retrieve->rerank queries/sec (1M-item corpus, top-100, DeepFM rerank, top-10)",
+           "value": round(Q / dt, 1), "unit": "queries/s", "queries": Q, "corpus": I, "n_gpus": world,
+           "ms_per_batch": round(dt * 1e3, 3), "rerank_rows_per_s": round(Q * K / dt, 1),
+           "data": "synthetic normalised N(0,1) corpus / users, hashed rerank ids",
+           "retrieval": {"kernel": "rsx_retrieve_topk (exact top-k)", "avg_ms": round(rs * 1e3, 4),
+                         "items_per_rank": hi - lo,
+                         "achieved_TFLOPs": round(flops / rs / 1e12, 2), "peak_TFLOPs": FP32_MFMA_PEAK_TFLOPS,
+                         "frac": round(flops / rs / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)}}
+    if world > 1:
+        out["sharding"] = (f"corpus by item range ({hi - lo} rows on rank {rank}), per-rank top-{K} with global "
+                           f"indices all-gathered over RCCL and merged (score desc, index asc); DeepFM by query "
+                           f"({q1 - q0} queries x {K} rows per rank)")
+    return out
 
 
 def bench_dcn(args, device):
@@ -557,7 +607,7 @@ def train_bench(args, global_batch, steps, warmup, items, cfg, model, item_tower
     torch.cuda.synchronize()
     elapsed = torch.tensor([t1 - t0], device=device, dtype=torch.float64)
     if world > 1:
-        torch.distributed.all_reduce(elapsed, op=torch.distributed.ReduceOp.MAX)
+        D.all_reduce_(elapsed, op=torch.distributed.ReduceOp.MAX)
     return {"elapsed": float(elapsed.item()), "kernel_times": kernel_times, "losses": losses, "n_glob": n_glob,
             "n_dist": n_dist, "n_tok": n_tok, "host_enqueue_ms": round(1e3 * sum(enqueue) / max(len(enqueue), 1), 3),
             "alloc_retries": int(retries)}
@@ -693,8 +743,9 @@ def main():
                 "random-init weights)",
         "config": {"workload": "user-tower two-view contrastive train step (fwd x2 + LogQ in-batch loss + "
                                "DuoRec + bwd + clip + AdamW); N=1: global batch 8192 (BASELINE.json metric); "
-                               "weak scaling at 8192 users/GPU (N=4: configs[3]'s global batch 32768), "
-                               "negatives all-gathered over ranks",
+                               "weak scaling at 8192 users/GPU, negatives all-gathered over ranks; "
+                               "strong_32768 = configs[3] (fixed global batch 32768), retrieve_rerank_sharded = "
+                               "configs[4] at N > 1",
                    "users_per_gpu": args.batch // world,
                    "global_batch": args.batch, "seq_len": 50, "d_model": 128, "items": args.items,
                    "valid_positions_per_batch": [sum(c) for c in tb["n_glob"]],
@@ -733,16 +784,40 @@ def main():
         ops.set_mha_precision(prev[2])
         del tf
         torch.cuda.empty_cache()
-    if world == 1 and not args.no_batch32768 and args.batch != 32768:
-        # configs[3]'s global batch (32,768 users, all negatives in one pool) on ONE GPU: the
-        # strong-scaling baseline for a multi-GPU run at the same global batch
+    if not args.no_batch32768 and (world > 1 or args.batch != 32768):
+        # configs[3]: FIXED global batch 32,768 (all negatives in one pool), users split by rank
+        # (32768 / N each): the strong-scaling line. At N = 1 it is the one-GPU baseline.
         t32 = train_bench(args, 32768, args.steps32768, 2, items, cfg, model, item_tower, opt, bucket, rank, world,
                           device)
         line = train_line(args, t32, 32768, args.steps32768, 2)
-        line["metric"] += " [configs[3]'s global batch on ONE GPU: strong-scaling baseline]"
-        result["secondary_batch32768"] = line
+        line["metric"] += f" [configs[3]: fixed global batch 32768 on {world} GPU(s), strong scaling]"
+        line["n_gpus"] = world
+        line["users_per_gpu"] = 32768 // world
+        line["scaling"] = "strong"
         del t32
         torch.cuda.empty_cache()
+        if world > 1:
+            # the 1-GPU baseline of the same global batch in the same run: rank 0 alone (no
+            # collectives, dist.local_only) while the other ranks wait at the barrier. Last
+            # training line: rank 0's parameters diverge from the others' after it.
+            one = None
+            if rank == 0:
+                with D.local_only():
+                    b1 = D.GradBucket([])
+                    t1 = train_bench(args, 32768, args.steps32768, 2, items, cfg, model, item_tower, opt, b1, 0, 1,
+                                     device)
+                one = train_line(args, t1, 32768, args.steps32768, 2)
+                del t1
+                torch.cuda.empty_cache()
+            torch.distributed.barrier()
+            if one is not None:
+                one["metric"] += " [rank 0 alone, same run: the strong-scaling baseline]"
+                line["one_gpu_baseline"] = one
+                line["speedup_vs_1gpu"] = round(line["value"] / one["value"], 3)
+                line["target_speedup_8gpu"] = 6.0
+        result["strong_32768"] = line
+        if world == 1:
+            result["secondary_batch32768"] = line
     if rank == 0 and world == 1:
         result["secondary_gather_1m"] = bench_gather_1m(device)
         torch.cuda.empty_cache()
@@ -752,6 +827,15 @@ def main():
         if not args.no_rerank:
             result["secondary_retrieve_rerank"] = bench_retrieve_rerank(args, device, deepfm)
             result["secondary_dcn_rerank"] = bench_dcn(args, device)
+        del deepfm
+        torch.cuda.empty_cache()
+    if world > 1 and not args.no_deepfm and not args.no_rerank:
+        # configs[4] on N GPUs: corpus sharded by item range, DeepFM rerank sharded by query
+        from recsys_amd.temp_model.ranker_skelet import DeepFM
+        torch.cuda.empty_cache()
+        torch.manual_seed(args.seed + 3)       # the replicated reranker: identical on every rank
+        deepfm = DeepFM([args.deepfm_vocab] * 39, device=device)
+        result["retrieve_rerank_sharded"] = bench_retrieve_rerank(args, device, deepfm, rank, world)
         del deepfm
         torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_item_tower:

@@ -30,10 +30,26 @@ import torch.distributed as dist
 from . import ops
 
 
+_LOCAL_ONLY = False
+
+
 def world():
-    if dist.is_available() and dist.is_initialized():
+    if not _LOCAL_ONLY and dist.is_available() and dist.is_initialized():
         return dist.get_rank(), dist.get_world_size()
     return 0, 1
+
+
+@contextlib.contextmanager
+def local_only():
+    """Inside, this process behaves as a single-GPU run (world() == (0, 1): no collectives, no
+    bucket exchange) although a process group exists: e.g. one rank timing the 1-GPU baseline of
+    a strong-scaling measurement while the other ranks wait at a barrier."""
+    global _LOCAL_ONLY
+    prev, _LOCAL_ONLY = _LOCAL_ONLY, True
+    try:
+        yield
+    finally:
+        _LOCAL_ONLY = prev
 
 
 def _host_staged(t: torch.Tensor, group=None) -> bool:

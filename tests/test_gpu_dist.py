@@ -122,3 +122,95 @@ def test_dp_objective_grads_and_sharded_topk_world2(gpu):
     for _, _, res in out:
         for precision, (worst, launched) in res.items():
             assert launched >= 1, (precision, launched)
+
+
+def _dp_fullsize_worker(rank, world, port, q):
+    """Global batch 8192 split 2 x 4096 (H&M-shaped lengths, 47,062 items: ~153k valid steps,
+    ~24.4k distinct targets), so the grouped loss's column split, XCD remap and tail split run
+    with FOREIGN columns (the other rank's targets, t_cols = the gathered ids) and user ids
+    offset by rank * 4096 (dist.py prepare_step_index)."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import recsys_amd  # noqa: F401
+        from recsys_amd import dist as D
+        from recsys_amd import ops, synth
+        from recsys_amd.tower_code import v1_usertower_train as TT
+        from recsys_amd.tower_code.v1_refine_usertower import SASRecUserTower
+        from tests.helpers import to_dev
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        hs = synth.HASH_SIZE
+        I = 47_062
+        cfg = TT.PipelineConfig(num_items=I, num_prod_types=hs, num_colors=hs, num_graphics=hs, num_sections=hs,
+                                dropout=0.0)
+        items = synth.make_items(num_items=I, d=128, seed=0)
+        G = 8192
+        b = G // world
+        full = to_dev(synth.make_batch(items, G, seed=100), dev)
+        mine = {k: (v[rank * b:(rank + 1) * b] if torch.is_tensor(v) else v) for k, v in full.items()}
+        lookup = items.pretrained.to(dev)
+        n_dist = int(torch.unique(full["target_ids"][~full["padding_mask"]]).numel())
+        res = {"distinct_targets": n_dist}
+        for precision in ("bf16x3", "fp32"):
+            ops.set_nce_precision(precision)
+
+            def build():
+                torch.manual_seed(0)
+                m = SASRecUserTower(cfg).to(dev)
+                m.train()
+                it = TT.SASRecItemTower(I, 128, items.log_q.clone()).to(dev)
+                it.init_from_pretrained(lookup)
+                it.set_freeze_state(False)
+                return m, it
+
+            m1, it1 = build()
+            tot1, main1, cl1 = TT.contrastive_losses(m1, it1, it1.log_q, full, cfg, pretrained_lookup=lookup)
+            tot1.backward()
+            m2, it2 = build()
+            params = list(m2.parameters()) + list(it2.parameters())
+            bucket = D.GradBucket(params)
+            obj, tot, main, cl = D.contrastive_objective_dp(m2, it2, it2.log_q, mine, cfg, pretrained_lookup=lookup)
+            obj.backward()
+            bucket()
+            for a, r in ((tot, tot1), (main, main1), (cl, cl1)):
+                assert abs(a.item() - r.item()) < 1e-4, (precision, a.item(), r.item())
+            worst = 0.0
+            names = [n for n, _ in m2.named_parameters()] + ["item_matrix.weight"]
+            for name, p_ref, p in zip(names, list(m1.parameters()) + list(it1.parameters()), params):
+                g_ref = p_ref.grad if p_ref.grad is not None else torch.zeros_like(p_ref)
+                assert p.grad is not None, name
+                scale = g_ref.abs().max().item() + 1e-12
+                err = (p.grad - g_ref).abs().max().item()
+                assert err <= 2e-3 * scale + 1e-6, f"{precision} {name}: err {err} vs scale {scale}"
+                worst = max(worst, err / scale)
+            res[precision] = (round(tot.item(), 6), round(tot1.item(), 6), round(worst, 7))
+            del m1, it1, m2, it2, bucket, params, obj, tot1
+            torch.cuda.empty_cache()
+        q.put((rank, "ok", res))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc()[-1500:], None))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_fullsize_world2_equals_single_gpu(gpu):
+    """contrastive_objective_dp summed over 2 ranks (4096 users each) and the bucket-reduced
+    gradients == TT.contrastive_losses / its gradients on the concatenated 8192-user batch
+    (v1_usertower_train.py:794-845): loss 1e-4, every gradient 2e-3 of its scale, both precisions."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_fullsize_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=115) for _ in procs]
+    for p in procs:
+        p.join(timeout=30)
+    status = {r: s for r, s, _ in out}
+    assert status == {0: "ok", 1: "ok"}, status
+    print({r: res for r, _, res in out})
+    assert out[0][2]["distinct_targets"] >= 10_000
