@@ -84,7 +84,8 @@ __global__ __launch_bounds__(256) void ln_fwd_k(FArgs a) {
 }
 
 // Forward for wide rows (D = 256 NV: 512, 768, 1024 — the BERT hidden sizes of the item
-// tower's text encoder): one wave per row, NV float4 per lane, same formulas as ln_fwd_k.
+// tower's text encoder — and 2048, the 16d LayerNorm of the item head's SE blocks at d = 128,
+// item_tower.py:41-75): one wave per row, NV float4 per lane, same formulas as ln_fwd_k.
 template <int NV>
 __global__ __launch_bounds__(256) void ln_fwd_wide_k(FArgs a) {
   constexpr int D = 256 * NV;
@@ -223,6 +224,103 @@ __global__ __launch_bounds__(256) void ln_bwd_k(BArgs a) {
   }
 }
 
+// Backward for wide rows (D = 256 NV): one wave per row, NV float4 per lane; the same
+// formulas as ln_bwd_k. dw/db partials: each wave accumulates its rows in registers, the
+// block's four waves are summed through LDS in a fixed order (deterministic).
+template <int NV>
+__global__ __launch_bounds__(256) void ln_bwd_wide_k(BArgs a) {
+  constexpr int D = 256 * NV;
+  __shared__ __attribute__((aligned(16))) float s_red[2][2][D];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float4 w[NV], b[NV], acc_w[NV], acc_b[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int c = lane + 64 * v;
+    w[v] = a.w ? reinterpret_cast<const float4*>(a.w)[c] : make_float4(1.f, 1.f, 1.f, 1.f);
+    b[v] = a.b ? reinterpret_cast<const float4*>(a.b)[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    acc_w[v] = make_float4(0.f, 0.f, 0.f, 0.f);
+    acc_b[v] = acc_w[v];
+  }
+  const int64_t r_begin = (int64_t)blockIdx.x * a.rows_per_block;
+  int64_t r_end = r_begin + a.rows_per_block;
+  if (r_end > a.T) r_end = a.T;
+  for (int64_t r = r_begin + wave; r < r_end; r += 4) {
+    const float mu = a.mean[r], rs = a.rstd[r];
+    float4 xh[NV], g[NV];
+    float s1 = 0.0f, s2 = 0.0f;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int c = lane + 64 * v;
+      const float4 s = reinterpret_cast<const float4*>(a.s + r * D)[c];
+      g[v] = reinterpret_cast<const float4*>(a.dy + r * D)[c];
+      xh[v] = make_float4((s.x - mu) * rs, (s.y - mu) * rs, (s.z - mu) * rs, (s.w - mu) * rs);
+      if (a.act == 2) {
+        g[v].x *= gelu_erf_grad(xh[v].x * w[v].x + b[v].x);
+        g[v].y *= gelu_erf_grad(xh[v].y * w[v].y + b[v].y);
+        g[v].z *= gelu_erf_grad(xh[v].z * w[v].z + b[v].z);
+        g[v].w *= gelu_erf_grad(xh[v].w * w[v].w + b[v].w);
+      }
+      acc_w[v].x += g[v].x * xh[v].x; acc_w[v].y += g[v].y * xh[v].y;
+      acc_w[v].z += g[v].z * xh[v].z; acc_w[v].w += g[v].w * xh[v].w;
+      acc_b[v].x += g[v].x; acc_b[v].y += g[v].y; acc_b[v].z += g[v].z; acc_b[v].w += g[v].w;
+      const float4 dh = make_float4(g[v].x * w[v].x, g[v].y * w[v].y, g[v].z * w[v].z, g[v].w * w[v].w);
+      g[v] = dh;
+      s1 += (dh.x + dh.y) + (dh.z + dh.w);
+      s2 += dh.x * xh[v].x + dh.y * xh[v].y + dh.z * xh[v].z + dh.w * xh[v].w;
+    }
+    const float c1 = rsx::wave_sum_width(s1, 64) * (1.0f / D);
+    const float c2 = rsx::wave_sum_width(s2, 64) * (1.0f / D);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int c = lane + 64 * v;
+      const float4 dh = g[v];
+      float4 dx = make_float4((dh.x - c1 - xh[v].x * c2) * rs, (dh.y - c1 - xh[v].y * c2) * rs,
+                              (dh.z - c1 - xh[v].z * c2) * rs, (dh.w - c1 - xh[v].w * c2) * rs);
+      if (a.ds_in) {
+        const float4 e = reinterpret_cast<const float4*>(a.ds_in + r * D)[c];
+        dx.x += e.x; dx.y += e.y; dx.z += e.z; dx.w += e.w;
+      }
+      if (a.ds_out) reinterpret_cast<float4*>(a.ds_out + r * D)[c] = dx;
+      if (a.dres) {
+        const uint64_t bi = (uint64_t)r * D + 4 * c;
+        float4 q;
+        q.x = a.drop.apply(dx.x, bi + 0);
+        q.y = a.drop.apply(dx.y, bi + 1);
+        q.z = a.drop.apply(dx.z, bi + 2);
+        q.w = a.drop.apply(dx.w, bi + 3);
+        reinterpret_cast<float4*>(a.dres + r * D)[c] = q;
+      }
+    }
+  }
+  if (!a.part) return;
+  // waves 2, 3 store; waves 0, 1 add theirs; then wave 1's sums are added to wave 0's
+  if (wave >= 2) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      reinterpret_cast<float4*>(&s_red[wave - 2][0][0])[lane + 64 * v] = acc_w[v];
+      reinterpret_cast<float4*>(&s_red[wave - 2][1][0])[lane + 64 * v] = acc_b[v];
+    }
+  }
+  __syncthreads();
+  if (wave < 2) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      float4* pw = reinterpret_cast<float4*>(&s_red[wave][0][0]) + lane + 64 * v;
+      float4* pb = reinterpret_cast<float4*>(&s_red[wave][1][0]) + lane + 64 * v;
+      float4 x = *pw, y = *pb;
+      x.x += acc_w[v].x; x.y += acc_w[v].y; x.z += acc_w[v].z; x.w += acc_w[v].w;
+      y.x += acc_b[v].x; y.y += acc_b[v].y; y.z += acc_b[v].z; y.w += acc_b[v].w;
+      *pw = x;
+      *pb = y;
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < 2 * D; i += blockDim.x) {
+    const float v = s_red[0][0][i] + s_red[1][0][i];
+    a.part[(int64_t)blockIdx.x * 2 * D + i] = v;
+  }
+}
+
 // out[i] = sum_k part[k][i] over nblk rows of width n (fixed order, 16 groups per output)
 __global__ __launch_bounds__(256) void colsum_k(const float* part, int nblk, int n, float* out0, float* out1,
                                                 int split) {
@@ -246,7 +344,7 @@ __global__ __launch_bounds__(256) void colsum_k(const float* part, int nblk, int
 constexpr int kMaxBlocks = 1024;
 
 int64_t bwd_blocks(int64_t T, int64_t D, int64_t& rpb) {
-  const int64_t quantum = 4 * (64 / (D / 4));
+  const int64_t quantum = D > 256 ? 4 : 4 * (64 / (D / 4));  // rows per block-iteration
   rpb = (T + kMaxBlocks - 1) / kMaxBlocks;
   rpb = (rpb + quantum - 1) / quantum * quantum;
   if (rpb < quantum) rpb = quantum;
@@ -273,8 +371,8 @@ RSX_API int rsx_ln_fwd(const float* x, const float* res, float p_drop, uint64_t 
                        float eps, int act, int64_t T, int64_t D, float* sum_out, float* y, float* mean, float* rstd,
                        void* stream) {
   RSX_ARG(x && (y || (res && sum_out)), "null tensor (y may be null only for the add-only form)");
-  RSX_ARG(D == 64 || D == 128 || D == 256 || D == 512 || D == 768 || D == 1024,
-          "D must be 64, 128, 256, 512, 768 or 1024");
+  RSX_ARG(D == 64 || D == 128 || D == 256 || D == 512 || D == 768 || D == 1024 || D == 2048,
+          "D must be 64, 128, 256, 512, 768, 1024 or 2048");
   RSX_ARG(act == 0 || act == 2, "act must be 0 (none) or 2 (gelu)");
   RSX_ARG(p_drop >= 0.0f && p_drop < 1.0f, "p_drop must be in [0,1)");
   if (T == 0) return 0;
@@ -282,13 +380,14 @@ RSX_API int rsx_ln_fwd(const float* x, const float* res, float p_drop, uint64_t 
   a.x = x; a.res = res; a.w = w; a.b = b; a.sum_out = sum_out; a.y = y; a.mean = mean; a.rstd = rstd;
   a.T = T; a.eps = eps; a.act = act;
   a.drop = rsx::make_dropout(res ? p_drop : 0.0f, seed);
-  const int64_t rows_per_block = D > 256 ? 4 : 4 * (64 / (D / 4));
+  const int64_t rows_per_block = D > 256 ? 4 : 4 * (64 / (D / 4));  // wide: one row per wave
   int64_t blocks = (T + rows_per_block - 1) / rows_per_block;
   if (blocks > 8192) blocks = 8192;
   hipStream_t st = (hipStream_t)stream;
   if (D == 512) hipLaunchKernelGGL(ln_fwd_wide_k<2>, dim3((unsigned)blocks), dim3(256), 0, st, a);
   else if (D == 768) hipLaunchKernelGGL(ln_fwd_wide_k<3>, dim3((unsigned)blocks), dim3(256), 0, st, a);
   else if (D == 1024) hipLaunchKernelGGL(ln_fwd_wide_k<4>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  else if (D == 2048) hipLaunchKernelGGL(ln_fwd_wide_k<8>, dim3((unsigned)blocks), dim3(256), 0, st, a);
   else if (D == 64) hipLaunchKernelGGL(ln_fwd_k<64>, dim3((unsigned)blocks), dim3(256), 0, st, a);
   else if (D == 128) hipLaunchKernelGGL(ln_fwd_k<128>, dim3((unsigned)blocks), dim3(256), 0, st, a);
   else hipLaunchKernelGGL(ln_fwd_k<256>, dim3((unsigned)blocks), dim3(256), 0, st, a);
@@ -305,7 +404,8 @@ RSX_API int rsx_ln_bwd(const float* s, const float* mean, const float* rstd, con
                        const float* dy, const float* ds_in, float p_drop, uint64_t seed, int64_t T, int64_t D,
                        float* ds_out, float* dres, float* dw, float* db, float* ws, int64_t ws_floats, void* stream) {
   RSX_ARG(s && mean && rstd && dy, "null tensor");
-  RSX_ARG(D == 64 || D == 128 || D == 256, "D must be 64, 128 or 256");
+  RSX_ARG(D == 64 || D == 128 || D == 256 || D == 512 || D == 768 || D == 1024 || D == 2048,
+          "D must be 64, 128, 256, 512, 768, 1024 or 2048");
   RSX_ARG(act == 0 || act == 2, "act must be 0 (none) or 2 (gelu)");
   RSX_ARG(!(dw || db) || (ws && ws_floats >= rsx_ln_bwd_workspace_floats(T, D)), "workspace too small");
   RSX_ARG(act == 0 || w, "gelu needs the LayerNorm weight");
@@ -323,7 +423,11 @@ RSX_API int rsx_ln_bwd(const float* s, const float* mean, const float* rstd, con
   const int64_t blocks = bwd_blocks(T, D, a.rows_per_block);
   if (D == 64) hipLaunchKernelGGL(ln_bwd_k<64>, dim3((unsigned)blocks), dim3(256), 0, st, a);
   else if (D == 128) hipLaunchKernelGGL(ln_bwd_k<128>, dim3((unsigned)blocks), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(ln_bwd_k<256>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  else if (D == 256) hipLaunchKernelGGL(ln_bwd_k<256>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  else if (D == 512) hipLaunchKernelGGL(ln_bwd_wide_k<2>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  else if (D == 768) hipLaunchKernelGGL(ln_bwd_wide_k<3>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  else if (D == 1024) hipLaunchKernelGGL(ln_bwd_wide_k<4>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(ln_bwd_wide_k<8>, dim3((unsigned)blocks), dim3(256), 0, st, a);
   RSX_LAUNCHED();
   if (dw || db) {
     const int n = (int)(2 * D);

@@ -40,11 +40,15 @@ OUTPUT_DIM_ENCODER = 128
 OUTPUT_DIM_PROJECTOR = 128
 
 
+_LN_WIDTHS = (64, 128, 256, 512, 768, 1024, 2048)
+
+
 def _ln(x, ln: nn.LayerNorm, gelu: bool = False):
-    """LayerNorm (+ exact GELU) on the fused kernel where the width fits it; wider rows (the
-    SE blocks' 16d LayerNorm) use torch's ROCm LayerNorm kernel. GPU only: no CPU path."""
+    """LayerNorm (+ exact GELU) on the fused kernel (rsx_ln_fwd / rsx_ln_bwd: every width the
+    item tower uses at d = 64 / 128, including the head's 2d, 4d and the SE blocks' 16d rows);
+    another width would fall to torch's ROCm LayerNorm. GPU only: no CPU path."""
     N.ensure_device(x)
-    if x.shape[-1] in (64, 128, 256):
+    if x.shape[-1] in _LN_WIDTHS:
         return ops.layer_norm(x, ln.weight, ln.bias, ln.eps, act=ops.ACT_GELU_ERF if gelu else 0)
     y = F.layer_norm(x, (x.shape[-1],), ln.weight, ln.bias, ln.eps)
     return F.gelu(y) if gelu else y
