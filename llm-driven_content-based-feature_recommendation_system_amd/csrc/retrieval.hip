@@ -409,6 +409,268 @@ __global__ __launch_bounds__(256) void topk_final_k(const float* bs, const int* 
   }
 }
 
+
+// ---- single-scan path (large corpora): bf16 scores once, exact fp32 rescoring of a margin set ----
+// P0 (topk_bf16_prep_k): the corpus as a bf16 image (RNE) and max_j ||w_j|| (one pass, 1.5 x the
+//     fp32 corpus bytes).
+// P1 (topk_bf16_scan_k): the only pass over the corpus. 128 G queries per workgroup (4 waves x G
+//     32-query groups, query bf16 images in registers), 32-item tiles of the image staged through
+//     LDS, a(q, j) = bf16(u) . bf16(w) on v_mfma_f32_32x32x16_bf16. Each lane owns one query's
+//     stream of 16 items per tile and keeps its best T approximate scores in registers.
+// P2 (topk_select_k): per query, sort the 2*nsplit*T candidates by approximate score; a_k = k-th.
+//     Rounding bound: |a - e| <= delta_q = ||u|| max||w|| (2^-7 + 2^-12) (bf16 RNE products
+//     2^-7 + 2^-16, fp32 accumulation of both a and the exact score e < 2^-15). Every candidate
+//     with a >= a_k - 2 delta is rescored exactly in fp32 (the others cannot reach the exact k-th
+//     of the candidates), sorted by (e desc, index asc), and the first k written. Exactness
+//     check: an item a stream did not keep has a <= m (that stream's T-th kept score), so
+//     e <= m + delta; if max over full streams of m + delta < the k-th exact score, no dropped
+//     item can be in the true top-k (ties included). Otherwise (or if the margin set exceeds its
+//     buffer) a device flag gates the exact list-based kernels above for the whole batch.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kImgStride = 272;   // bytes per staged item row: 256 + 16 (conflict-free ds_read_b128)
+constexpr int kSelCap = 2048;     // margin-set buffer per query (entries)
+constexpr float kDeltaRel = 0.0078125f + 0.000244140625f;  // 2^-7 + 2^-12
+
+__global__ __launch_bounds__(256) void topk_bf16_prep_k(const float* __restrict__ I, int64_t ldi, int64_t NI,
+                                                        __bf16* __restrict__ img, unsigned* wmax_bits) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave_g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  float mx = 0.0f;
+  for (int64_t j = wave_g; j < NI; j += nw) {
+    const float2 v = reinterpret_cast<const float2*>(I + j * ldi)[lane];
+    const float ss = rsx::wave_sum_width(v.x * v.x + v.y * v.y, 64);
+    mx = fmaxf(mx, sqrtf(ss));
+    __bf16 h[2] = {(__bf16)v.x, (__bf16)v.y};
+    reinterpret_cast<unsigned*>(img + j * kD)[lane] = *reinterpret_cast<unsigned*>(h);
+  }
+  // non-negative floats order like their bit patterns
+  if (lane == 0 && mx > 0.0f) atomicMax(wmax_bits, __float_as_uint(mx * 1.0000001f));
+}
+
+struct BfArgs {
+  const __bf16* img;   // [NI][128]
+  const float* U;      // [Q, ldu]
+  int64_t Q, NI, ldu;
+  int nsplit, nqb;
+  int64_t span;
+  float* cand_s;       // [Q][nsplit][2][T], each stream's list sorted desc
+  int* cand_i;
+};
+
+template <int G, int T>
+__global__ __launch_bounds__(256, 2) void topk_bf16_scan_k(BfArgs a) {
+  __shared__ __attribute__((aligned(16))) unsigned char sI[2][kTile * kImgStride];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, c = lane & 31;
+  // XCD-aware order: the nqb query blocks of one split sit 8 block ids apart, i.e. on one XCD
+  const int b = blockIdx.x, x = b & 7, y = b >> 3;
+  const int qb = y % a.nqb;
+  const int split = (y / a.nqb) * 8 + x;
+  const int64_t q0 = (int64_t)qb * (128 * G) + wave * (32 * G) + c;
+  bf16x8 ub[G][8];
+  bool q_ok[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int64_t q = q0 + 32 * g;
+    q_ok[g] = q < a.Q;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
+      if (q_ok[g]) {
+        const float4* src = reinterpret_cast<const float4*>(a.U + q * a.ldu + 16 * ks + 8 * h);
+        v0 = src[0];
+        v1 = src[1];
+      }
+      ub[g][ks][0] = (__bf16)v0.x; ub[g][ks][1] = (__bf16)v0.y; ub[g][ks][2] = (__bf16)v0.z; ub[g][ks][3] = (__bf16)v0.w;
+      ub[g][ks][4] = (__bf16)v1.x; ub[g][ks][5] = (__bf16)v1.y; ub[g][ks][6] = (__bf16)v1.z; ub[g][ks][7] = (__bf16)v1.w;
+    }
+  }
+  const int64_t j_begin = (int64_t)split * a.span;
+  int64_t j_end = j_begin + a.span;
+  if (j_end > a.NI) j_end = a.NI;
+
+  float ts[G][T];
+  int ti[G][T];
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int t = 0; t < T; ++t) { ts[g][t] = -INFINITY; ti[g][t] = 0x7fffffff; }
+
+  // staging: 8 threads per item row, 32 B each
+  const int srow = tid >> 3, sb = (tid & 7) * 32;
+  u32x4 stg[2];
+  auto gload = [&](int64_t j0) {
+    const int64_t j = j0 + srow;
+    if (j < j_end) {
+      const u32x4* src = reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(a.img + j * kD) + sb);
+      stg[0] = src[0];
+      stg[1] = src[1];
+    } else {
+      stg[0] = u32x4{0u, 0u, 0u, 0u};
+      stg[1] = stg[0];
+    }
+  };
+  auto lstore = [&](int buf) {
+    u32x4* dst = reinterpret_cast<u32x4*>(&sI[buf][srow * kImgStride + sb]);
+    dst[0] = stg[0];
+    dst[1] = stg[1];
+  };
+  if (j_begin < j_end) {
+    gload(j_begin);
+    lstore(0);
+    __syncthreads();
+    int cur = 0;
+    for (int64_t j0 = j_begin; j0 < j_end; j0 += kTile) {
+      const bool has_next = j0 + kTile < j_end;
+      if (has_next) gload(j0 + kTile);
+      f32x16 acc[G];
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[g][r] = 0.0f;
+      const unsigned char* xrow = &sI[cur][c * kImgStride + 16 * h];
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        const bf16x8 av = *reinterpret_cast<const bf16x8*>(xrow + 32 * ks);
+#pragma unroll
+        for (int g = 0; g < G; ++g) acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, ub[g][ks], acc[g], 0, 0, 0);
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        if (!q_ok[g]) continue;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int64_t j = j0 + tile_row(r, h);
+          const float sc = acc[g][r];
+          if (sc > ts[g][T - 1] && j < j_end) {  // rare after the first T items of the stream
+            ts[g][T - 1] = sc;
+            ti[g][T - 1] = (int)j;
+#pragma unroll
+            for (int t = T - 1; t > 0; --t) {
+              if (ts[g][t] > ts[g][t - 1]) {
+                const float fs = ts[g][t]; ts[g][t] = ts[g][t - 1]; ts[g][t - 1] = fs;
+                const int fi = ti[g][t]; ti[g][t] = ti[g][t - 1]; ti[g][t - 1] = fi;
+              }
+            }
+          }
+        }
+      }
+      if (has_next) lstore(cur ^ 1);  // cur^1 was read in the previous tile, fenced by its barrier
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    if (!q_ok[g]) continue;
+    const int64_t base = (((q0 + 32 * g) * a.nsplit + split) * 2 + h) * T;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      a.cand_s[base + t] = ts[g][t];
+      a.cand_i[base + t] = ti[g][t];
+    }
+  }
+}
+
+// bitonic sort of the first P (power of two) entries, (score desc, idx asc)
+__device__ __forceinline__ void bitonic_desc_n(float* ss, int* si, int P) {
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = threadIdx.x; t < P / 2; t += blockDim.x) {
+        const int lo = 2 * t - (t & (stride - 1));
+        const int hi = lo + stride;
+        const bool desc = ((lo & size) == 0);
+        const float a0 = ss[lo], a1 = ss[hi];
+        const int b0 = si[lo], b1 = si[hi];
+        const bool swap = desc ? better(a1, b1, a0, b0) : better(a0, b0, a1, b1);
+        if (swap) {
+          ss[lo] = a1; ss[hi] = a0;
+          si[lo] = b1; si[hi] = b0;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+template <int NC, int T>
+__global__ __launch_bounds__(256) void topk_select_k(const float* __restrict__ cs, const int* __restrict__ ci, int ncand,
+                                                     const float* __restrict__ U, int64_t ldu, const float* __restrict__ I,
+                                                     int64_t ldi, int K, const unsigned* wmax_bits, float* out_s,
+                                                     int64_t* out_i, int* flag) {
+  __shared__ float ss[NC];
+  __shared__ int si[NC];
+  __shared__ float red[4];
+  __shared__ int nsel_s;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t q = blockIdx.x;
+  // the query's norm (fixed-order reduction) and its stream minima
+  const float2 uv = reinterpret_cast<const float2*>(U + q * ldu)[lane];
+  const float unorm = sqrtf(rsx::wave_sum_width(uv.x * uv.x + uv.y * uv.y, 64)) * 1.0000001f;
+  float mloc = -INFINITY;
+  for (int t = tid; t < NC; t += 256) {
+    const bool ok = t < ncand;
+    const float sv = ok ? cs[q * ncand + t] : -INFINITY;
+    const int iv = ok ? ci[q * ncand + t] : 0x7fffffff;
+    ss[t] = sv;
+    si[t] = iv;
+    if (ok && (t % T) == T - 1 && iv != 0x7fffffff) mloc = fmaxf(mloc, sv);  // a full stream's T-th
+  }
+  for (int o = 32; o > 0; o >>= 1) mloc = fmaxf(mloc, __shfl_xor(mloc, o, 64));
+  if (lane == 0) red[wave] = mloc;
+  if (tid == 0) nsel_s = 0;
+  __syncthreads();
+  const float mfull = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const float delta = unorm * __uint_as_float(*wmax_bits) * kDeltaRel + 1e-30f;
+  bitonic_desc_n(ss, si, NC);
+  const bool have_k = si[K - 1] != 0x7fffffff;
+  const float thr = have_k ? ss[K - 1] - 2.0f * delta : -INFINITY;
+  // margin set = the sorted prefix with a >= thr (valid entries only)
+  int cnt = 0;
+  for (int t = tid; t < NC; t += 256) cnt += (si[t] != 0x7fffffff && ss[t] >= thr) ? 1 : 0;
+  cnt = rsx::wave_sum_width(cnt, 64);
+  if (lane == 0) atomicAdd(&nsel_s, cnt);
+  __syncthreads();
+  const int n = nsel_s;
+  if (n > kSelCap) {
+    if (tid == 0) atomicOr(flag, 1);
+    return;
+  }
+  // exact fp32 rescoring: 32 lanes per item, float4 per lane, fixed-order shuffle reduction
+  const int sub = lane >> 5, c = lane & 31;
+  const float4 u4 = reinterpret_cast<const float4*>(U + q * ldu)[c];
+  for (int t0 = 0; t0 < n; t0 += 8) {
+    const int t = t0 + wave * 2 + sub;
+    float e = 0.0f;
+    if (t < n) {
+      const float4 w4 = reinterpret_cast<const float4*>(I + (int64_t)si[t] * ldi)[c];
+      e = u4.x * w4.x + u4.y * w4.y + u4.z * w4.z + u4.w * w4.w;
+    }
+    for (int o = 16; o > 0; o >>= 1) e += __shfl_xor(e, o, 64);
+    __syncthreads();  // every read of ss[t] (threshold count) is done before the overwrite
+    if (t < n && c == 0) ss[t] = e;
+  }
+  int P = 1;
+  while (P < n) P <<= 1;
+  for (int t = n + tid; t < P; t += 256) {
+    ss[t] = -INFINITY;
+    si[t] = 0x7fffffff;
+  }
+  __syncthreads();
+  bitonic_desc_n(ss, si, P);
+  for (int t = tid; t < K; t += 256) {
+    const bool ok = t < n;
+    out_s[q * K + t] = ok ? ss[t] : -INFINITY;
+    out_i[q * K + t] = ok ? (int64_t)si[t] : -1;
+  }
+  if (tid == 0 && mfull > -INFINITY) {
+    // a full stream may have dropped an item whose exact score reaches the k-th
+    if (n < K || !(mfull + delta < ss[K - 1])) atomicOr(flag, 1);
+  }
+}
+
 constexpr int kFastCap = 2048;
 
 struct FastPlan {
@@ -427,6 +689,27 @@ FastPlan fast_plan(int64_t Q, int64_t NI, int64_t k) {
     ns *= 2;
   p.nsplit = ns;
   if (2 * ns * p.T < k) p.use = false;  // too few candidates for a threshold
+  return p;
+}
+
+
+struct BfPlan {
+  bool use;
+  int G, T, nsplit, nqb;
+};
+
+BfPlan bf_plan(int64_t Q, int64_t NI, int64_t k) {
+  BfPlan p;
+  p.T = k <= 128 ? 4 : 8;
+  p.G = Q >= 512 ? 2 : 1;
+  p.nqb = (int)((Q + 128 * p.G - 1) / (128 * p.G));
+  // >= 256 items per stream (2 streams per split), at most 256 splits (<= 4096 candidates/query)
+  int ns = 8;
+  while (ns < 256 && NI / (2 * (int64_t)ns * 2) >= 256) ns *= 2;
+  p.nsplit = ns;
+  p.use = NI > 16384 && k <= 512 && 2 * ns * p.T >= 2 * k;
+  static const bool off = getenv("RSX_TOPK_BF16") != nullptr && getenv("RSX_TOPK_BF16")[0] == '0';
+  if (off) p.use = false;
   return p;
 }
 
@@ -468,6 +751,23 @@ FastLayout fast_layout(int64_t Q, int64_t NI, int64_t k, const FastPlan& p) {
   return L;
 }
 
+
+struct BfLayout {
+  int64_t img, cand_s, cand_i, fallback, total;
+};
+BfLayout bf_layout(int64_t Q, int64_t NI, int64_t k, const BfPlan& p) {
+  BfLayout L;
+  L.img = 256;  // [0] overflow flag, [4] max ||w|| bits
+  const int64_t nc = Q * p.nsplit * 2 * (int64_t)p.T;
+  L.cand_s = L.img + align256(NI * kD * 2);
+  L.cand_i = L.cand_s + align256(nc * 4);
+  const int64_t end = L.cand_i + align256(nc * 4);
+  L.fallback = L.img;  // the exact fallback runs after P2: reuses the image / candidate region
+  const int64_t fb_end = L.fallback + old_ws_bytes(Q, NI, k);
+  L.total = (end > fb_end ? end : fb_end) + 256;
+  return L;
+}
+
 int launch_old(const float* U, int64_t ldu, const float* I, int64_t ldi, int64_t Q, int64_t NI, int64_t k,
                char* ws, float* out_scores, int64_t* out_idx, const int* gate, hipStream_t st) {
   const int kmax = k <= 128 ? 128 : 512;
@@ -503,6 +803,8 @@ void launch_fast_scans(FastArgs f, int blocks, int mode, hipStream_t st) {
 }  // namespace
 
 RSX_API int64_t rsx_topk_workspace_bytes(int64_t Q, int64_t NI, int64_t k) {
+  const BfPlan bp = bf_plan(Q, NI, k);
+  if (bp.use) return bf_layout(Q, NI, k, bp).total;
   const FastPlan p = fast_plan(Q, NI, k);
   if (!p.use) return old_ws_bytes(Q, NI, k) + 256;
   return fast_layout(Q, NI, k, p).total;
@@ -518,6 +820,42 @@ RSX_API int rsx_retrieve_topk(const float* U, int64_t ldu, const float* I, int64
   if (Q == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   char* w = reinterpret_cast<char*>(ws);
+  const BfPlan bp = bf_plan(Q, NI, k);
+  if (bp.use) {
+    const BfLayout L = bf_layout(Q, NI, k, bp);
+    int* flag = reinterpret_cast<int*>(w);
+    unsigned* wmax = reinterpret_cast<unsigned*>(w + 4);
+    (void)hipMemsetAsync(w, 0, 8, st);
+    __bf16* img = reinterpret_cast<__bf16*>(w + L.img);
+    int64_t pb = (NI + 3) / 4;
+    if (pb > 8192) pb = 8192;
+    hipLaunchKernelGGL(topk_bf16_prep_k, dim3((unsigned)pb), dim3(256), 0, st, I, ldi, NI, img, wmax);
+    RSX_LAUNCHED();
+    BfArgs b;
+    b.img = img; b.U = U; b.Q = Q; b.NI = NI; b.ldu = ldu;
+    b.nsplit = bp.nsplit; b.nqb = bp.nqb;
+    b.span = ((NI + bp.nsplit - 1) / bp.nsplit + kTile - 1) / kTile * kTile;
+    b.cand_s = reinterpret_cast<float*>(w + L.cand_s);
+    b.cand_i = reinterpret_cast<int*>(w + L.cand_i);
+    const dim3 grid((unsigned)(bp.nqb * bp.nsplit));
+    if (bp.G == 2 && bp.T == 4) hipLaunchKernelGGL((topk_bf16_scan_k<2, 4>), grid, dim3(256), 0, st, b);
+    else if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_scan_k<2, 8>), grid, dim3(256), 0, st, b);
+    else if (bp.T == 4) hipLaunchKernelGGL((topk_bf16_scan_k<1, 4>), grid, dim3(256), 0, st, b);
+    else hipLaunchKernelGGL((topk_bf16_scan_k<1, 8>), grid, dim3(256), 0, st, b);
+    RSX_LAUNCHED();
+    const int ncand = bp.nsplit * 2 * bp.T;
+    if (bp.T == 4 && ncand <= 1024)
+      hipLaunchKernelGGL((topk_select_k<1024, 4>), dim3((unsigned)Q), dim3(256), 0, st, b.cand_s, b.cand_i, ncand, U,
+                         ldu, I, ldi, (int)k, wmax, out_scores, out_idx, flag);
+    else if (bp.T == 4)
+      hipLaunchKernelGGL((topk_select_k<2048, 4>), dim3((unsigned)Q), dim3(256), 0, st, b.cand_s, b.cand_i, ncand, U,
+                         ldu, I, ldi, (int)k, wmax, out_scores, out_idx, flag);
+    else
+      hipLaunchKernelGGL((topk_select_k<4096, 8>), dim3((unsigned)Q), dim3(256), 0, st, b.cand_s, b.cand_i, ncand, U,
+                         ldu, I, ldi, (int)k, wmax, out_scores, out_idx, flag);
+    RSX_LAUNCHED();
+    return launch_old(U, ldu, I, ldi, Q, NI, k, w + L.fallback, out_scores, out_idx, flag, st);
+  }
   const FastPlan p = fast_plan(Q, NI, k);
   if (!p.use) return launch_old(U, ldu, I, ldi, Q, NI, k, w, out_scores, out_idx, nullptr, st);
   const FastLayout L = fast_layout(Q, NI, k, p);

@@ -1196,9 +1196,11 @@ def reranker_batch(uidx, iidx, tables, max_len=50):
 
 # ----------------------------------------------------------------------------------------
 # A14: retrieval top-k
-def retrieve_topk(queries, items, k):
+def retrieve_topk(queries, items, k, diag=None):
     """(scores [Q, k] desc, indices [Q, k] int64) of queries @ items.T without materialising
-    the score matrix. Ties resolve to the lower item index. D = 128."""
+    the score matrix. Ties resolve to the lower item index. D = 128.
+    diag: optional dict; receives "fallback" (bool: the single-scan path's exactness check sent
+    this batch to the exact list-based kernels; one host sync, for tests / diagnostics)."""
     N.ensure_device(queries)
     q = _c(queries.to(torch.float32))
     it = items if (items.stride(-1) == 1 and items.stride(0) % 4 == 0) else items.contiguous()
@@ -1210,6 +1212,8 @@ def retrieve_topk(queries, items, k):
         rc = N.lib().rsx_retrieve_topk(N.ptr(q), q.stride(0), N.ptr(it), it.stride(0), Q, NI, k, N.ptr(ws),
                                        N.ptr(sc), N.ptr(ix), N.stream())
     N.check(rc, "retrieve_topk")
+    if diag is not None:
+        diag["fallback"] = bool(ws[:4].view(torch.int32).item())
     return sc, ix
 
 

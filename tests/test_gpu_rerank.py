@@ -116,8 +116,9 @@ def test_reranking_system_deepfm(gpu):
 
 @pytest.mark.parametrize("Q,NI,k", [(130, 100003, 100), (70, 60000, 500), (257, 40000, 7)])
 def test_retrieve_topk_fast_path_bit_exact(gpu, Q, NI, k):
-    """Large corpora take the candidate -> threshold -> collect path: on dyadic inputs (exact
-    dot products, many exact ties) the result must equal the oracle's (score desc, index asc)."""
+    """Large corpora take the bf16 single scan + exact rescoring path: on dyadic inputs (exact
+    dot products and exact bf16 images, many exact ties) the result must equal the oracle's
+    (score desc, index asc), whether or not the exactness check falls back."""
     g = torch.Generator().manual_seed(Q * 7 + k)
     U = torch.randint(-4, 5, (Q, 128), generator=g).float() / 8.0
     I = torch.randint(-4, 5, (NI, 128), generator=g).float() / 8.0
@@ -135,6 +136,44 @@ def test_retrieve_topk_fast_path_overflow_fallback(gpu):
     I = base[torch.randint(0, 5, (40000,), generator=g)]
     U = torch.randint(-4, 5, (33, 128), generator=g).float() / 8.0
     s, i = ops.retrieve_topk(U.to(gpu), I.to(gpu), 100)
+    rs, ri = OR.retrieve_topk(U, I, 100)
+    assert torch.equal(i.cpu(), ri)
+    assert torch.equal(s.cpu().double(), rs)
+
+
+@pytest.mark.parametrize("Q,NI,k", [(600, 200_000, 100), (40, 50_000, 300)])
+def test_retrieve_topk_single_scan_no_fallback_on_spread_data(gpu, Q, NI, k):
+    """Realistic normalised data: the bf16 single scan + exact rescoring is exact by its own
+    check (no fallback), and the result equals the float64 oracle up to fp32-noise near-ties."""
+    g = torch.Generator().manual_seed(NI + k)
+    U = torch.nn.functional.normalize(torch.randn(Q, 128, generator=g), dim=1)
+    I = torch.nn.functional.normalize(torch.randn(NI, 128, generator=g), dim=1)
+    diag = {}
+    s, i = ops.retrieve_topk(U.to(gpu), I.to(gpu), k, diag=diag)
+    assert diag["fallback"] is False
+    rs, ri = OR.retrieve_topk(U, I, k)
+    torch.testing.assert_close(s.cpu().double(), rs, atol=2e-6, rtol=0)
+    mism = (i.cpu() != ri)
+    if mism.any():
+        gaps = (rs[:, :-1] - rs[:, 1:]).abs()
+        assert (gaps[mism[:, :-1]] < 2e-6).all()
+
+
+def test_retrieve_topk_single_scan_clustered_falls_back_exactly(gpu):
+    """Adversarial layout: 400 near-copies of query 0 stored contiguously (they land in a few
+    scan streams, each keeping only its best T), dyadic values (exact dot products). The
+    exactness check must detect the possibly dropped items and route the batch to the exact
+    kernels: result bit-identical to the oracle, ties included."""
+    g = torch.Generator().manual_seed(77)
+    Q, NI = 130, 120_000
+    U = torch.randint(-4, 5, (Q, 128), generator=g).float() / 8.0
+    I = torch.randint(-4, 5, (NI, 128), generator=g).float() / 8.0
+    noise = torch.randint(-1, 2, (400, 128), generator=g).float() / 8.0
+    I[60_000:60_400] = U[0] + noise
+    I[60_400:60_410] = U[0]                  # exact ties among the top items
+    diag = {}
+    s, i = ops.retrieve_topk(U.to(gpu), I.to(gpu), 100, diag=diag)
+    assert diag["fallback"] is True
     rs, ri = OR.retrieve_topk(U, I, 100)
     assert torch.equal(i.cpu(), ri)
     assert torch.equal(s.cpu().double(), rs)
