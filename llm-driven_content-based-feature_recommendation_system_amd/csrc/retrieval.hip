@@ -29,6 +29,8 @@ __device__ __forceinline__ int tile_row(int r, int h) { return (r & 3) + 8 * (r 
 
 struct ScanArgs {
   const int* gate;  // nullptr, or: run only if *gate != 0 (the exact fallback of the fast path)
+  const int* qmap;  // nullptr, or: logical row r is query qmap[r], for r < *qcount (per-query fallback)
+  const int* qcount;
   const float* U;  // [Q, ldu]
   const float* I;  // [NI, ldi]
   int64_t Q, NI, ldu, ldi;
@@ -47,6 +49,7 @@ __device__ __forceinline__ bool better(float sa, int ia, float sb, int ib) {
 template <int KMAX>
 __global__ __launch_bounds__(256, 2) void topk_scan_k(ScanArgs a) {
   if (a.gate && *a.gate == 0) return;
+  const int64_t nq = a.qcount ? (int64_t)*a.qcount : a.Q;
   __shared__ __attribute__((aligned(16))) float sI[2][kTile][kLdsStride];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, c = lane & 31;
@@ -54,8 +57,10 @@ __global__ __launch_bounds__(256, 2) void topk_scan_k(ScanArgs a) {
   const int nsub = a.nsplit >> 3;
   const int split = (b & 7) + 8 * ((b >> 3) % nsub);
   const int rb = (b >> 3) / nsub;
-  const int64_t q = (int64_t)rb * kOwnRows + wave * 32 + c;
-  const bool q_ok = q < a.Q;
+  if ((int64_t)rb * kOwnRows >= nq) return;  // whole workgroup: no logical rows here
+  const int64_t ql = (int64_t)rb * kOwnRows + wave * 32 + c;  // logical row (workspace index)
+  const bool q_ok = ql < nq;
+  const int64_t q = (q_ok && a.qmap) ? (int64_t)a.qmap[ql] : ql;
   float u[64];
   if (q_ok) {
     const float4* src = reinterpret_cast<const float4*>(a.U + q * a.ldu + h * 64);
@@ -72,7 +77,7 @@ __global__ __launch_bounds__(256, 2) void topk_scan_k(ScanArgs a) {
   int64_t j_end = j_begin + a.span;
   if (j_end > a.NI) j_end = a.NI;
 
-  const int64_t lbase = ((q_ok ? q : 0) * a.nsplit + split) * 2 + h;
+  const int64_t lbase = ((q_ok ? ql : 0) * a.nsplit + split) * 2 + h;
   float* ls = a.cs + lbase * KMAX;
   int* li = a.ci + lbase * KMAX;
   const int K = a.K;
@@ -165,13 +170,16 @@ __global__ __launch_bounds__(256, 2) void topk_scan_k(ScanArgs a) {
 // One workgroup per query: bitonic sort of NC = 2*nsplit*KMAX candidates, descending.
 template <int NC>
 __global__ __launch_bounds__(256) void topk_merge_k(const float* cs, const int* ci, int64_t Q, int ncand, int K,
-                                                    float* out_s, int64_t* out_i, const int* gate) {
+                                                    float* out_s, int64_t* out_i, const int* gate, const int* qmap,
+                                                    const int* qcount) {
   if (gate && *gate == 0) return;
   __shared__ float ss[NC];
   __shared__ int si[NC];
-  const int64_t q = blockIdx.x;
-  const float* s = cs + q * ncand;
-  const int* ii = ci + q * ncand;
+  const int64_t ql = blockIdx.x;
+  if (qcount && ql >= *qcount) return;
+  const int64_t q = qmap ? (int64_t)qmap[ql] : ql;
+  const float* s = cs + ql * ncand;
+  const int* ii = ci + ql * ncand;
   for (int t = threadIdx.x; t < NC; t += blockDim.x) {
     if (t < ncand) {
       ss[t] = s[t];
@@ -410,41 +418,66 @@ __global__ __launch_bounds__(256) void topk_final_k(const float* bs, const int* 
 }
 
 
-// ---- single-scan path (large corpora): bf16 scores once, exact fp32 rescoring of a margin set ----
-// P0 (topk_bf16_prep_k): the corpus as a bf16 image (RNE) and max_j ||w_j|| (one pass, 1.5 x the
-//     fp32 corpus bytes).
-// P1 (topk_bf16_scan_k): the only pass over the corpus. 128 G queries per workgroup (4 waves x G
-//     32-query groups, query bf16 images in registers), 32-item tiles of the image staged through
-//     LDS, a(q, j) = bf16(u) . bf16(w) on v_mfma_f32_32x32x16_bf16. Each lane owns one query's
-//     stream of 16 items per tile and keeps its best T approximate scores in registers.
-// P2 (topk_select_k): per query, sort the 2*nsplit*T candidates by approximate score; a_k = k-th.
-//     Rounding bound: |a - e| <= delta_q = ||u|| max||w|| (2^-7 + 2^-12) (bf16 RNE products
-//     2^-7 + 2^-16, fp32 accumulation of both a and the exact score e < 2^-15). Every candidate
-//     with a >= a_k - 2 delta is rescored exactly in fp32 (the others cannot reach the exact k-th
-//     of the candidates), sorted by (e desc, index asc), and the first k written. Exactness
-//     check: an item a stream did not keep has a <= m (that stream's T-th kept score), so
-//     e <= m + delta; if max over full streams of m + delta < the k-th exact score, no dropped
-//     item can be in the true top-k (ties included). Otherwise (or if the margin set exceeds its
-//     buffer) a device flag gates the exact list-based kernels above for the whole batch.
+// ---- bf16 path (large corpora): one full scan at bf16 MFMA rate, exact fp32 rescoring ----------
+// P0 (topk_bf16_prep_k): the corpus as a bf16 image (RNE) and max_j ||w_j||.
+// Rounding bound: |a - e| <= delta_q = ||u|| max||w|| (2^-7 + 2^-12) between the bf16 score a
+//     (bf16 RNE operands: 2^-7 + 2^-16 relative per product, fp32 accumulation) and the fp32
+//     score e of the rescoring (fp32 accumulation; both accumulations < 2^-16 relative).
+// P1 (topk_bf16_scan_k<MODE 0>): a strided sample of the corpus (every S-th 32-item tile of each
+//     split, S ~ 8 nsplit / k so that ~4 collected entries per stream are expected in P3); each
+//     lane keeps its best T sample scores in registers.
+// P2 (topk_bf16_thresh_k): per query, c_k = k-th best of the sampled candidates. The k sampled
+//     items with a >= c_k have e >= c_k - delta, so the true k-th best exact score e_k >= c_k -
+//     delta, and every true top-k item has a >= e_k - delta >= c_k - 2 delta =: t_q.
+// P3 (topk_bf16_scan_k<MODE 1>): the one full scan; every (a, j) with a >= t_q is appended to
+//     its lane's stream buffer (cap kStreamCap; ~0.25 % of the items on spread data).
+// P4 (topk_bf16_select_k): per query, gather the appended entries, sort by a; a_k = k-th; every
+//     entry with a >= a_k - 2 delta (the only ones that can reach the exact k-th) is rescored in
+//     fp32 and sorted by (e desc, index asc); the first k are written. A stream buffer overflow or
+//     more than kSelMax entries sends the query to the exact list-based kernels above (a device
+//     list of query ids; their grid exits past its count: no host sync).
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kImgStride = 272;   // bytes per staged item row: 256 + 16 (conflict-free ds_read_b128)
-constexpr int kSelCap = 2048;     // margin-set buffer per query (entries)
+constexpr int kStreamCap = 32;    // P3 entries per lane stream
+constexpr int kSelMax = 8192;     // P4 entries per query (LDS sort)
 constexpr float kDeltaRel = 0.0078125f + 0.000244140625f;  // 2^-7 + 2^-12
 
+// 16 threads per row, 8 floats each; 4 rows per wave per step
 __global__ __launch_bounds__(256) void topk_bf16_prep_k(const float* __restrict__ I, int64_t ldi, int64_t NI,
                                                         __bf16* __restrict__ img, unsigned* wmax_bits) {
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63, sub = lane >> 4, c = lane & 15;
   const int64_t wave_g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t nw = (int64_t)gridDim.x * 4;
   float mx = 0.0f;
-  for (int64_t j = wave_g; j < NI; j += nw) {
-    const float2 v = reinterpret_cast<const float2*>(I + j * ldi)[lane];
-    const float ss = rsx::wave_sum_width(v.x * v.x + v.y * v.y, 64);
-    mx = fmaxf(mx, sqrtf(ss));
-    __bf16 h[2] = {(__bf16)v.x, (__bf16)v.y};
-    reinterpret_cast<unsigned*>(img + j * kD)[lane] = *reinterpret_cast<unsigned*>(h);
+  for (int64_t j0 = wave_g * 8; j0 < NI; j0 += nw * 8) {
+    float4 v[2][2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int64_t j = j0 + 4 * u + sub;
+      if (j < NI) {
+        const float4* src = reinterpret_cast<const float4*>(I + j * ldi) + 2 * c;
+        v[u][0] = src[0];
+        v[u][1] = src[1];
+      } else {
+        v[u][0] = make_float4(0.f, 0.f, 0.f, 0.f);
+        v[u][1] = v[u][0];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int64_t j = j0 + 4 * u + sub;
+      const float4 a = v[u][0], b = v[u][1];
+      const float ss = rsx::wave_sum_width(a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w +
+                                           b.x * b.x + b.y * b.y + b.z * b.z + b.w * b.w, 16);
+      mx = fmaxf(mx, sqrtf(ss));
+      bf16x8 h;
+      h[0] = (__bf16)a.x; h[1] = (__bf16)a.y; h[2] = (__bf16)a.z; h[3] = (__bf16)a.w;
+      h[4] = (__bf16)b.x; h[5] = (__bf16)b.y; h[6] = (__bf16)b.z; h[7] = (__bf16)b.w;
+      if (j < NI) *reinterpret_cast<bf16x8*>(img + j * kD + 8 * c) = h;
+    }
   }
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
   // non-negative floats order like their bit patterns
   if (lane == 0 && mx > 0.0f) atomicMax(wmax_bits, __float_as_uint(mx * 1.0000001f));
 }
@@ -453,13 +486,17 @@ struct BfArgs {
   const __bf16* img;   // [NI][128]
   const float* U;      // [Q, ldu]
   int64_t Q, NI, ldu;
-  int nsplit, nqb;
+  int nsplit, nqb, sample;
   int64_t span;
-  float* cand_s;       // [Q][nsplit][2][T], each stream's list sorted desc
+  float* cand_s;       // MODE 0: [Q][nsplit][2][T], each stream's list sorted desc
   int* cand_i;
+  const float* thr;    // MODE 1: [Q] collection threshold t_q
+  float* buf_s;        // MODE 1: [Q][nsplit][2][kStreamCap]
+  int* buf_i;
+  int* buf_n;          // MODE 1: [Q][nsplit][2] appended count (may exceed the cap: overflow)
 };
 
-template <int G, int T>
+template <int G, int T, int MODE>
 __global__ __launch_bounds__(256, 2) void topk_bf16_scan_k(BfArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned char sI[2][kTile * kImgStride];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -471,10 +508,12 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_scan_k(BfArgs a) {
   const int64_t q0 = (int64_t)qb * (128 * G) + wave * (32 * G) + c;
   bf16x8 ub[G][8];
   bool q_ok[G];
+  float thr[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     const int64_t q = q0 + 32 * g;
     q_ok[g] = q < a.Q;
+    thr[g] = (MODE == 1 && q_ok[g]) ? a.thr[q] : INFINITY;
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
       float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
@@ -490,13 +529,20 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_scan_k(BfArgs a) {
   const int64_t j_begin = (int64_t)split * a.span;
   int64_t j_end = j_begin + a.span;
   if (j_end > a.NI) j_end = a.NI;
+  const int64_t step = MODE == 0 ? (int64_t)kTile * a.sample : kTile;
 
   float ts[G][T];
   int ti[G][T];
+  int cnt[G];
 #pragma unroll
-  for (int g = 0; g < G; ++g)
+  for (int g = 0; g < G; ++g) {
+    cnt[g] = 0;
 #pragma unroll
     for (int t = 0; t < T; ++t) { ts[g][t] = -INFINITY; ti[g][t] = 0x7fffffff; }
+  }
+  int64_t sbase[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) sbase[g] = ((q0 + 32 * g) * a.nsplit + split) * 2 + h;
 
   // staging: 8 threads per item row, 32 B each
   const int srow = tid >> 3, sb = (tid & 7) * 32;
@@ -522,9 +568,9 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_scan_k(BfArgs a) {
     lstore(0);
     __syncthreads();
     int cur = 0;
-    for (int64_t j0 = j_begin; j0 < j_end; j0 += kTile) {
-      const bool has_next = j0 + kTile < j_end;
-      if (has_next) gload(j0 + kTile);
+    for (int64_t j0 = j_begin; j0 < j_end; j0 += step) {
+      const bool has_next = j0 + step < j_end;
+      if (has_next) gload(j0 + step);
       f32x16 acc[G];
 #pragma unroll
       for (int g = 0; g < G; ++g)
@@ -544,16 +590,24 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_scan_k(BfArgs a) {
         for (int r = 0; r < 16; ++r) {
           const int64_t j = j0 + tile_row(r, h);
           const float sc = acc[g][r];
-          if (sc > ts[g][T - 1] && j < j_end) {  // rare after the first T items of the stream
-            ts[g][T - 1] = sc;
-            ti[g][T - 1] = (int)j;
+          if (MODE == 0) {
+            if (sc > ts[g][T - 1] && j < j_end) {
+              ts[g][T - 1] = sc;
+              ti[g][T - 1] = (int)j;
 #pragma unroll
-            for (int t = T - 1; t > 0; --t) {
-              if (ts[g][t] > ts[g][t - 1]) {
-                const float fs = ts[g][t]; ts[g][t] = ts[g][t - 1]; ts[g][t - 1] = fs;
-                const int fi = ti[g][t]; ti[g][t] = ti[g][t - 1]; ti[g][t - 1] = fi;
+              for (int t = T - 1; t > 0; --t) {
+                if (ts[g][t] > ts[g][t - 1]) {
+                  const float fs = ts[g][t]; ts[g][t] = ts[g][t - 1]; ts[g][t - 1] = fs;
+                  const int fi = ti[g][t]; ti[g][t] = ti[g][t - 1]; ti[g][t - 1] = fi;
+                }
               }
             }
+          } else if (sc >= thr[g] && j < j_end) {
+            if (cnt[g] < kStreamCap) {
+              a.buf_s[sbase[g] * kStreamCap + cnt[g]] = sc;
+              a.buf_i[sbase[g] * kStreamCap + cnt[g]] = (int)j;
+            }
+            ++cnt[g];
           }
         }
       }
@@ -565,11 +619,14 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_scan_k(BfArgs a) {
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     if (!q_ok[g]) continue;
-    const int64_t base = (((q0 + 32 * g) * a.nsplit + split) * 2 + h) * T;
+    if (MODE == 0) {
 #pragma unroll
-    for (int t = 0; t < T; ++t) {
-      a.cand_s[base + t] = ts[g][t];
-      a.cand_i[base + t] = ti[g][t];
+      for (int t = 0; t < T; ++t) {
+        a.cand_s[sbase[g] * T + t] = ts[g][t];
+        a.cand_i[sbase[g] * T + t] = ti[g][t];
+      }
+    } else {
+      a.buf_n[sbase[g]] = cnt[g];
     }
   }
 }
@@ -595,49 +652,90 @@ __device__ __forceinline__ void bitonic_desc_n(float* ss, int* si, int P) {
   }
 }
 
-template <int NC, int T>
-__global__ __launch_bounds__(256) void topk_select_k(const float* __restrict__ cs, const int* __restrict__ ci, int ncand,
-                                                     const float* __restrict__ U, int64_t ldu, const float* __restrict__ I,
-                                                     int64_t ldi, int K, const unsigned* wmax_bits, float* out_s,
-                                                     int64_t* out_i, int* flag) {
+// ||u_q|| * 1.0000001 (fixed-order reduction by the block's first wave; every wave computes it)
+__device__ __forceinline__ float query_norm(const float* U, int64_t ldu, int64_t q) {
+  const float2 uv = reinterpret_cast<const float2*>(U + q * ldu)[threadIdx.x & 63];
+  return sqrtf(rsx::wave_sum_width(uv.x * uv.x + uv.y * uv.y, 64)) * 1.0000001f;
+}
+
+// P2: t_q = c_k - 2 delta_q (c_k: k-th best sampled candidate; -inf if fewer than k)
+template <int NC>
+__global__ __launch_bounds__(256) void topk_bf16_thresh_k(const float* __restrict__ cs, const int* __restrict__ ci,
+                                                          int ncand, const float* __restrict__ U, int64_t ldu, int K,
+                                                          const unsigned* wmax_bits, float* thr) {
   __shared__ float ss[NC];
   __shared__ int si[NC];
-  __shared__ float red[4];
-  __shared__ int nsel_s;
+  const int64_t q = blockIdx.x;
+  for (int t = threadIdx.x; t < NC; t += 256) {
+    const bool ok = t < ncand;
+    ss[t] = ok ? cs[q * ncand + t] : -INFINITY;
+    si[t] = ok ? ci[q * ncand + t] : 0x7fffffff;
+  }
+  const float delta = query_norm(U, ldu, q) * __uint_as_float(*wmax_bits) * kDeltaRel + 1e-30f;
+  __syncthreads();
+  bitonic_desc_n(ss, si, NC);
+  if (threadIdx.x == 0) thr[q] = (si[K - 1] != 0x7fffffff) ? ss[K - 1] - 2.0f * delta : -INFINITY;
+}
+
+// P4: gather the query's appended entries, sort, rescore the margin set exactly, write top-k
+__global__ __launch_bounds__(256) void topk_bf16_select_k(const float* __restrict__ bs, const int* __restrict__ bi,
+                                                          const int* __restrict__ bn, int nstreams,
+                                                          const float* __restrict__ U, int64_t ldu,
+                                                          const float* __restrict__ I, int64_t ldi, int K,
+                                                          const unsigned* wmax_bits, float* out_s, int64_t* out_i,
+                                                          int* qcount, int* qmap) {
+  __shared__ float ss[kSelMax];
+  __shared__ int si[kSelMax];
+  __shared__ int off[513];
+  __shared__ int bad_s, nsel_s;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t q = blockIdx.x;
-  // the query's norm (fixed-order reduction) and its stream minima
-  const float2 uv = reinterpret_cast<const float2*>(U + q * ldu)[lane];
-  const float unorm = sqrtf(rsx::wave_sum_width(uv.x * uv.x + uv.y * uv.y, 64)) * 1.0000001f;
-  float mloc = -INFINITY;
-  for (int t = tid; t < NC; t += 256) {
-    const bool ok = t < ncand;
-    const float sv = ok ? cs[q * ncand + t] : -INFINITY;
-    const int iv = ok ? ci[q * ncand + t] : 0x7fffffff;
-    ss[t] = sv;
-    si[t] = iv;
-    if (ok && (t % T) == T - 1 && iv != 0x7fffffff) mloc = fmaxf(mloc, sv);  // a full stream's T-th
+  const float delta = query_norm(U, ldu, q) * __uint_as_float(*wmax_bits) * kDeltaRel + 1e-30f;
+  if (tid == 0) { bad_s = 0; nsel_s = 0; }
+  // counts (nstreams <= 512) -> exclusive prefix in LDS
+  for (int t = tid; t < 512; t += 256) {
+    const int n = t < nstreams ? bn[q * nstreams + t] : 0;
+    if (n > kStreamCap) bad_s = 1;
+    off[t + 1] = n < kStreamCap ? n : kStreamCap;
   }
-  for (int o = 32; o > 0; o >>= 1) mloc = fmaxf(mloc, __shfl_xor(mloc, o, 64));
-  if (lane == 0) red[wave] = mloc;
-  if (tid == 0) nsel_s = 0;
   __syncthreads();
-  const float mfull = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-  const float delta = unorm * __uint_as_float(*wmax_bits) * kDeltaRel + 1e-30f;
-  bitonic_desc_n(ss, si, NC);
+  if (tid == 0) {
+    off[0] = 0;
+    for (int t = 1; t <= 512; ++t) off[t] += off[t - 1];
+  }
+  __syncthreads();
+  const int total = off[512];
+  if (bad_s || total > kSelMax) {
+    if (tid == 0) qmap[atomicAdd(qcount, 1)] = (int)q;
+    return;
+  }
+  for (int s0 = 0; s0 < nstreams; s0 += 8) {  // 32 threads per stream, 8 streams per pass
+    const int st = s0 + (tid >> 5), e = tid & 31;
+    if (st < nstreams) {
+      const int n = off[st + 1] - off[st];
+      if (e < n) {
+        ss[off[st] + e] = bs[(q * nstreams + st) * kStreamCap + e];
+        si[off[st] + e] = bi[(q * nstreams + st) * kStreamCap + e];
+      }
+    }
+  }
+  int P = 1;
+  while (P < total) P <<= 1;
+  if (P < K) P = 1 << (32 - __builtin_clz(K - 1));
+  for (int t = total + tid; t < P; t += 256) {
+    ss[t] = -INFINITY;
+    si[t] = 0x7fffffff;
+  }
+  __syncthreads();
+  bitonic_desc_n(ss, si, P);
   const bool have_k = si[K - 1] != 0x7fffffff;
   const float thr = have_k ? ss[K - 1] - 2.0f * delta : -INFINITY;
-  // margin set = the sorted prefix with a >= thr (valid entries only)
   int cnt = 0;
-  for (int t = tid; t < NC; t += 256) cnt += (si[t] != 0x7fffffff && ss[t] >= thr) ? 1 : 0;
+  for (int t = tid; t < P; t += 256) cnt += (si[t] != 0x7fffffff && ss[t] >= thr) ? 1 : 0;
   cnt = rsx::wave_sum_width(cnt, 64);
   if (lane == 0) atomicAdd(&nsel_s, cnt);
   __syncthreads();
   const int n = nsel_s;
-  if (n > kSelCap) {
-    if (tid == 0) atomicOr(flag, 1);
-    return;
-  }
   // exact fp32 rescoring: 32 lanes per item, float4 per lane, fixed-order shuffle reduction
   const int sub = lane >> 5, c = lane & 31;
   const float4 u4 = reinterpret_cast<const float4*>(U + q * ldu)[c];
@@ -649,25 +747,21 @@ __global__ __launch_bounds__(256) void topk_select_k(const float* __restrict__ c
       e = u4.x * w4.x + u4.y * w4.y + u4.z * w4.z + u4.w * w4.w;
     }
     for (int o = 16; o > 0; o >>= 1) e += __shfl_xor(e, o, 64);
-    __syncthreads();  // every read of ss[t] (threshold count) is done before the overwrite
+    __syncthreads();  // every read of ss (the margin count) is done before the first overwrite
     if (t < n && c == 0) ss[t] = e;
   }
-  int P = 1;
-  while (P < n) P <<= 1;
-  for (int t = n + tid; t < P; t += 256) {
+  int P2 = 1;
+  while (P2 < n) P2 <<= 1;
+  for (int t = n + tid; t < P2; t += 256) {
     ss[t] = -INFINITY;
     si[t] = 0x7fffffff;
   }
   __syncthreads();
-  bitonic_desc_n(ss, si, P);
+  bitonic_desc_n(ss, si, P2);
   for (int t = tid; t < K; t += 256) {
     const bool ok = t < n;
     out_s[q * K + t] = ok ? ss[t] : -INFINITY;
     out_i[q * K + t] = ok ? (int64_t)si[t] : -1;
-  }
-  if (tid == 0 && mfull > -INFINITY) {
-    // a full stream may have dropped an item whose exact score reaches the k-th
-    if (n < K || !(mfull + delta < ss[K - 1])) atomicOr(flag, 1);
   }
 }
 
@@ -695,18 +789,23 @@ FastPlan fast_plan(int64_t Q, int64_t NI, int64_t k) {
 
 struct BfPlan {
   bool use;
-  int G, T, nsplit, nqb;
+  int G, T, nsplit, nqb, sample;
 };
 
 BfPlan bf_plan(int64_t Q, int64_t NI, int64_t k) {
   BfPlan p;
-  p.T = k <= 128 ? 4 : 8;
+  p.T = 8;
   p.G = Q >= 512 ? 2 : 1;
   p.nqb = (int)((Q + 128 * p.G - 1) / (128 * p.G));
-  // >= 256 items per stream (2 streams per split), at most 256 splits (<= 4096 candidates/query)
+  // at most 256 splits (<= 512 streams per query); >= 512 items per stream where possible
   int ns = 8;
-  while (ns < 256 && NI / (2 * (int64_t)ns * 2) >= 256) ns *= 2;
+  while (ns < 256 && NI / (2 * (int64_t)ns * 2) >= 512) ns *= 2;
   p.nsplit = ns;
+  // sample one tile in S: about k S / (2 nsplit) <= 4 items per stream reach the P3 threshold
+  int S = 1;
+  while (S < 16 && k * (int64_t)S * 2 <= 8 * (int64_t)ns) S *= 2;
+  p.sample = S;
+  // the sample's candidates must hold k items: 2 nsplit T >= 2 k
   p.use = NI > 16384 && k <= 512 && 2 * ns * p.T >= 2 * k;
   static const bool off = getenv("RSX_TOPK_BF16") != nullptr && getenv("RSX_TOPK_BF16")[0] == '0';
   if (off) p.use = false;
@@ -753,26 +852,34 @@ FastLayout fast_layout(int64_t Q, int64_t NI, int64_t k, const FastPlan& p) {
 
 
 struct BfLayout {
-  int64_t img, cand_s, cand_i, fallback, total;
+  int64_t img, thr, cand_s, cand_i, buf_s, buf_i, buf_n, qmap, fallback, total;
 };
 BfLayout bf_layout(int64_t Q, int64_t NI, int64_t k, const BfPlan& p) {
   BfLayout L;
-  L.img = 256;  // [0] overflow flag, [4] max ||w|| bits
-  const int64_t nc = Q * p.nsplit * 2 * (int64_t)p.T;
-  L.cand_s = L.img + align256(NI * kD * 2);
-  L.cand_i = L.cand_s + align256(nc * 4);
-  const int64_t end = L.cand_i + align256(nc * 4);
-  L.fallback = L.img;  // the exact fallback runs after P2: reuses the image / candidate region
+  L.img = 256;  // [0] count of queries sent to the exact kernels, [4] max ||w|| bits
+  const int64_t nstream = Q * p.nsplit * 2;
+  L.thr = L.img + align256(NI * kD * 2);
+  L.cand_s = L.thr + align256(Q * 4);
+  L.cand_i = L.cand_s + align256(nstream * p.T * 4);
+  L.buf_s = L.cand_i + align256(nstream * p.T * 4);
+  L.buf_i = L.buf_s + align256(nstream * kStreamCap * 4);
+  L.buf_n = L.buf_i + align256(nstream * kStreamCap * 4);
+  const int64_t end = L.buf_n + align256(nstream * 4);
+  L.fallback = L.img;  // the exact fallback runs after P4: reuses the image / buffer region
   const int64_t fb_end = L.fallback + old_ws_bytes(Q, NI, k);
-  L.total = (end > fb_end ? end : fb_end) + 256;
+  L.qmap = end > fb_end ? end : fb_end;  // the fallback must not overwrite the query list
+  L.total = L.qmap + align256(Q * 4) + 256;
   return L;
 }
 
 int launch_old(const float* U, int64_t ldu, const float* I, int64_t ldi, int64_t Q, int64_t NI, int64_t k,
-               char* ws, float* out_scores, int64_t* out_idx, const int* gate, hipStream_t st) {
+               char* ws, float* out_scores, int64_t* out_idx, const int* gate, hipStream_t st,
+               const int* qmap = nullptr, const int* qcount = nullptr) {
   const int kmax = k <= 128 ? 128 : 512;
   ScanArgs a;
   a.gate = gate;
+  a.qmap = qmap;
+  a.qcount = qcount;
   a.U = U; a.I = I; a.Q = Q; a.NI = NI; a.ldu = ldu; a.ldi = ldi;
   a.nsplit = choose_nsplit(Q, NI, kmax);
   a.span = ((NI + a.nsplit - 1) / a.nsplit + kTile - 1) / kTile * kTile;
@@ -787,10 +894,10 @@ int launch_old(const float* U, int64_t ldu, const float* I, int64_t ldi, int64_t
   const int ncand = a.nsplit * 2 * kmax;
   if (ncand <= 2048)
     hipLaunchKernelGGL(topk_merge_k<2048>, dim3((unsigned)Q), dim3(256), 0, st, a.cs, a.ci, Q, ncand, (int)k,
-                       out_scores, out_idx, gate);
+                       out_scores, out_idx, gate, qmap, qcount);
   else
     hipLaunchKernelGGL(topk_merge_k<8192>, dim3((unsigned)Q), dim3(256), 0, st, a.cs, a.ci, Q, ncand, (int)k,
-                       out_scores, out_idx, gate);
+                       out_scores, out_idx, gate, qmap, qcount);
   RSX_LAUNCHED();
   return 0;
 }
@@ -823,38 +930,49 @@ RSX_API int rsx_retrieve_topk(const float* U, int64_t ldu, const float* I, int64
   const BfPlan bp = bf_plan(Q, NI, k);
   if (bp.use) {
     const BfLayout L = bf_layout(Q, NI, k, bp);
-    int* flag = reinterpret_cast<int*>(w);
+    int* qcount = reinterpret_cast<int*>(w);
     unsigned* wmax = reinterpret_cast<unsigned*>(w + 4);
+    int* qmap = reinterpret_cast<int*>(w + L.qmap);
     (void)hipMemsetAsync(w, 0, 8, st);
     __bf16* img = reinterpret_cast<__bf16*>(w + L.img);
-    int64_t pb = (NI + 3) / 4;
-    if (pb > 8192) pb = 8192;
+    int64_t pb = (NI + 31) / 32;
+    if (pb > 4096) pb = 4096;
     hipLaunchKernelGGL(topk_bf16_prep_k, dim3((unsigned)pb), dim3(256), 0, st, I, ldi, NI, img, wmax);
     RSX_LAUNCHED();
     BfArgs b;
     b.img = img; b.U = U; b.Q = Q; b.NI = NI; b.ldu = ldu;
-    b.nsplit = bp.nsplit; b.nqb = bp.nqb;
+    b.nsplit = bp.nsplit; b.nqb = bp.nqb; b.sample = bp.sample;
     b.span = ((NI + bp.nsplit - 1) / bp.nsplit + kTile - 1) / kTile * kTile;
     b.cand_s = reinterpret_cast<float*>(w + L.cand_s);
     b.cand_i = reinterpret_cast<int*>(w + L.cand_i);
+    b.thr = reinterpret_cast<const float*>(w + L.thr);
+    b.buf_s = reinterpret_cast<float*>(w + L.buf_s);
+    b.buf_i = reinterpret_cast<int*>(w + L.buf_i);
+    b.buf_n = reinterpret_cast<int*>(w + L.buf_n);
     const dim3 grid((unsigned)(bp.nqb * bp.nsplit));
-    if (bp.G == 2 && bp.T == 4) hipLaunchKernelGGL((topk_bf16_scan_k<2, 4>), grid, dim3(256), 0, st, b);
-    else if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_scan_k<2, 8>), grid, dim3(256), 0, st, b);
-    else if (bp.T == 4) hipLaunchKernelGGL((topk_bf16_scan_k<1, 4>), grid, dim3(256), 0, st, b);
-    else hipLaunchKernelGGL((topk_bf16_scan_k<1, 8>), grid, dim3(256), 0, st, b);
+    if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_scan_k<2, 8, 0>), grid, dim3(256), 0, st, b);
+    else hipLaunchKernelGGL((topk_bf16_scan_k<1, 8, 0>), grid, dim3(256), 0, st, b);
     RSX_LAUNCHED();
     const int ncand = bp.nsplit * 2 * bp.T;
-    if (bp.T == 4 && ncand <= 1024)
-      hipLaunchKernelGGL((topk_select_k<1024, 4>), dim3((unsigned)Q), dim3(256), 0, st, b.cand_s, b.cand_i, ncand, U,
-                         ldu, I, ldi, (int)k, wmax, out_scores, out_idx, flag);
-    else if (bp.T == 4)
-      hipLaunchKernelGGL((topk_select_k<2048, 4>), dim3((unsigned)Q), dim3(256), 0, st, b.cand_s, b.cand_i, ncand, U,
-                         ldu, I, ldi, (int)k, wmax, out_scores, out_idx, flag);
+    float* thr = reinterpret_cast<float*>(w + L.thr);
+    if (ncand <= 1024)
+      hipLaunchKernelGGL(topk_bf16_thresh_k<1024>, dim3((unsigned)Q), dim3(256), 0, st, b.cand_s, b.cand_i, ncand, U,
+                         ldu, (int)k, wmax, thr);
+    else if (ncand <= 2048)
+      hipLaunchKernelGGL(topk_bf16_thresh_k<2048>, dim3((unsigned)Q), dim3(256), 0, st, b.cand_s, b.cand_i, ncand, U,
+                         ldu, (int)k, wmax, thr);
     else
-      hipLaunchKernelGGL((topk_select_k<4096, 8>), dim3((unsigned)Q), dim3(256), 0, st, b.cand_s, b.cand_i, ncand, U,
-                         ldu, I, ldi, (int)k, wmax, out_scores, out_idx, flag);
+      hipLaunchKernelGGL(topk_bf16_thresh_k<4096>, dim3((unsigned)Q), dim3(256), 0, st, b.cand_s, b.cand_i, ncand, U,
+                         ldu, (int)k, wmax, thr);
     RSX_LAUNCHED();
-    return launch_old(U, ldu, I, ldi, Q, NI, k, w + L.fallback, out_scores, out_idx, flag, st);
+    if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_scan_k<2, 8, 1>), grid, dim3(256), 0, st, b);
+    else hipLaunchKernelGGL((topk_bf16_scan_k<1, 8, 1>), grid, dim3(256), 0, st, b);
+    RSX_LAUNCHED();
+    hipLaunchKernelGGL(topk_bf16_select_k, dim3((unsigned)Q), dim3(256), 0, st, b.buf_s, b.buf_i, b.buf_n,
+                       bp.nsplit * 2, U, ldu, I, ldi, (int)k, wmax, out_scores, out_idx, qcount, qmap);
+    RSX_LAUNCHED();
+    // exact list-based kernels for the queries P4 listed (none on spread data)
+    return launch_old(U, ldu, I, ldi, Q, NI, k, w + L.fallback, out_scores, out_idx, nullptr, st, qmap, qcount);
   }
   const FastPlan p = fast_plan(Q, NI, k);
   if (!p.use) return launch_old(U, ldu, I, ldi, Q, NI, k, w, out_scores, out_idx, nullptr, st);

@@ -1199,8 +1199,9 @@ def reranker_batch(uidx, iidx, tables, max_len=50):
 def retrieve_topk(queries, items, k, diag=None):
     """(scores [Q, k] desc, indices [Q, k] int64) of queries @ items.T without materialising
     the score matrix. Ties resolve to the lower item index. D = 128.
-    diag: optional dict; receives "fallback" (bool: the single-scan path's exactness check sent
-    this batch to the exact list-based kernels; one host sync, for tests / diagnostics)."""
+    diag: optional dict; receives "fallback" (bool) and "fallback_queries" (int): how many queries
+    the single-scan path's exactness check sent to the exact list-based kernels (one host sync,
+    for tests / diagnostics)."""
     N.ensure_device(queries)
     q = _c(queries.to(torch.float32))
     it = items if (items.stride(-1) == 1 and items.stride(0) % 4 == 0) else items.contiguous()
@@ -1213,7 +1214,8 @@ def retrieve_topk(queries, items, k, diag=None):
                                        N.ptr(sc), N.ptr(ix), N.stream())
     N.check(rc, "retrieve_topk")
     if diag is not None:
-        diag["fallback"] = bool(ws[:4].view(torch.int32).item())
+        n = int(ws[:4].view(torch.int32).item())
+        diag["fallback"], diag["fallback_queries"] = n > 0, n
     return sc, ix
 
 

@@ -91,11 +91,10 @@ def test_retrieve_topk_realistic(gpu):
     s, i = ops.retrieve_topk(U.to(gpu), I.to(gpu), 100)
     rs, ri = OR.retrieve_topk(U, I, 100)
     torch.testing.assert_close(s.cpu().double(), rs, atol=1e-6, rtol=0)
-    # indices agree except where the oracle's own neighbouring scores are within fp32 noise
-    mism = (i.cpu() != ri)
-    if mism.any():
-        gaps = (rs[:, :-1] - rs[:, 1:]).abs()
-        assert (gaps[mism[:, :-1]] < 1e-6).all()
+    # indices agree except near-ties within fp32 noise: each returned item's float64 score equals
+    # the oracle's score at that rank
+    ours = torch.einsum("qkd,qd->qk", I.double()[i.cpu()], U.double())
+    assert (ours - rs).abs().max().item() < 1e-6
 
 
 def test_reranking_system_deepfm(gpu):
@@ -153,17 +152,19 @@ def test_retrieve_topk_single_scan_no_fallback_on_spread_data(gpu, Q, NI, k):
     assert diag["fallback"] is False
     rs, ri = OR.retrieve_topk(U, I, k)
     torch.testing.assert_close(s.cpu().double(), rs, atol=2e-6, rtol=0)
-    mism = (i.cpu() != ri)
-    if mism.any():
-        gaps = (rs[:, :-1] - rs[:, 1:]).abs()
-        assert (gaps[mism[:, :-1]] < 2e-6).all()
+    # every returned item's float64 score equals the oracle's score at that rank up to fp32
+    # noise: only near-tied neighbours may swap or be exchanged at the k-th position
+    ours = torch.einsum("qkd,qd->qk", I.double()[i.cpu()], U.double())
+    assert (ours - rs).abs().max().item() < 2e-6
+    assert (i.cpu() != ri).float().mean().item() < 0.01
 
 
 def test_retrieve_topk_single_scan_clustered_falls_back_exactly(gpu):
     """Adversarial layout: 400 near-copies of query 0 stored contiguously (they land in a few
     scan streams, each keeping only its best T), dyadic values (exact dot products). The
     exactness check must detect the possibly dropped items and route the batch to the exact
-    kernels: result bit-identical to the oracle, ties included."""
+    kernels for that query (not the whole batch): result bit-identical to the oracle, ties
+    included."""
     g = torch.Generator().manual_seed(77)
     Q, NI = 130, 120_000
     U = torch.randint(-4, 5, (Q, 128), generator=g).float() / 8.0
@@ -173,7 +174,7 @@ def test_retrieve_topk_single_scan_clustered_falls_back_exactly(gpu):
     I[60_400:60_410] = U[0]                  # exact ties among the top items
     diag = {}
     s, i = ops.retrieve_topk(U.to(gpu), I.to(gpu), 100, diag=diag)
-    assert diag["fallback"] is True
+    assert diag["fallback"] is True and 1 <= diag["fallback_queries"] < Q   # per query, not the batch
     rs, ri = OR.retrieve_topk(U, I, 100)
     assert torch.equal(i.cpu(), ri)
     assert torch.equal(s.cpu().double(), rs)

@@ -45,7 +45,7 @@ def main():
         torch.save({"s": s.cpu(), "i": i.cpu()}, args.save)
     print(json.dumps({"path": "legacy-two-pass" if os.environ.get("RSX_TOPK_BF16") == "0" else "bf16-single-scan",
                       "avg_ms": round(ms, 4), "algorithmic_TFLOPs": round(flops / ms / 1e9, 2),
-                      "fallback": diag.get("fallback"), "idx_checksum": int(i.sum().item()),
+                      "fallback_queries": diag.get("fallback_queries"), "idx_checksum": int(i.sum().item()),
                       "score_sum": float(s.double().sum().item())}))
 
 
