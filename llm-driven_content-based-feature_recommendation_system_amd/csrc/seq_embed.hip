@@ -244,7 +244,7 @@ struct BwdCtx {
 // position and table rows (the LN recompute and the gate dot reuse the same table rows) — so a
 // lane has U x (1 + NL) id -> row chains in flight instead of one at a time. NL = kMaxTab is the
 // generic more-than-two-live-tables form (slots guarded by lv.n).
-template <int D, int U, int NL>
+template <int D, int U, int NL, int ABL>
 __device__ __forceinline__ void bwd_groups(const BwdArgs& a, const BwdLive& lv, const BwdCtx& cx, int64_t r00,
                                            float4& acc_w, float4& acc_b, float* acc_l) {
   constexpr int LPR = D / 4;
@@ -286,7 +286,7 @@ __device__ __forceinline__ void bwd_groups(const BwdArgs& a, const BwdLive& lv, 
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       ev[u][k] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (NL > 0 && (NL != kMaxTab || k < lv.n) && need_e)
+      if (NL > 0 && (NL != kMaxTab || k < lv.n) && need_e && !(ABL & 2))
         ev[u][k] = reinterpret_cast<const float4*>(lv.tab[k] + id[u][k] * D)[c];
     }
   if (cx.do_ln) {  // recompute x in the forward's op order: base, + E_j[id] * g_j (j ascending), + pos
@@ -331,7 +331,8 @@ __device__ __forceinline__ void bwd_groups(const BwdArgs& a, const BwdLive& lv, 
       dx.z = (dh.z - c1 - xh.z * c2) * rs;
       dx.w = (dh.w - c1 - xh.w * c2) * rs;
     }
-    if (a.dbase) reinterpret_cast<float4*>(a.dbase + r * D)[c] = dx;
+    if (a.dbase && !(ABL & 4)) reinterpret_cast<float4*>(a.dbase + r * D)[c] = dx;
+    if (ABL & 1) continue;
     // Scatter-adds take the row in lane-strided order (lane c holds elements c + LPR*k): each
     // atomic instruction then covers LPR consecutive floats (one 128-B line per row at D=128)
     // instead of LPR 16-B pieces over four lines — 4x fewer lines per L2 atomic and
@@ -380,7 +381,9 @@ constexpr int kSmallMax = 8192;  // floats (32 KiB)
 // gradients fold in registers; big-table rows are scatter-added with global float atomics.
 // The LDS and global scatter paths are kept apart so no flat (address-space-generic)
 // atomics are emitted.
-template <int D>
+// ABL: timing ablations only (results wrong): 1 no LDS / global scatter, 2 no table-row loads,
+// 4 no dbase store (RSX_SEQ_EMBED_BWD_ABL, tools/seq_embed_step_micro.py)
+template <int D, int ABL>
 __global__ __launch_bounds__(256) void seq_embed_bwd_k(BwdArgs a) {
   constexpr int LPR = D / 4;
   constexpr int RPW = 64 / LPR;
@@ -445,13 +448,13 @@ __global__ __launch_bounds__(256) void seq_embed_bwd_k(BwdArgs a) {
   if (lv.n <= 2) {
     constexpr int U = 2;
     for (int64_t r00 = r_begin; r00 < r_end; r00 += U * NW * RPW) {
-      if (lv.n == 2) bwd_groups<D, U, 2>(a, lv, cx, r00, acc_w, acc_b, acc_l);
-      else if (lv.n == 1) bwd_groups<D, U, 1>(a, lv, cx, r00, acc_w, acc_b, acc_l);
-      else bwd_groups<D, U, 0>(a, lv, cx, r00, acc_w, acc_b, acc_l);
+      if (lv.n == 2) bwd_groups<D, U, 2, ABL>(a, lv, cx, r00, acc_w, acc_b, acc_l);
+      else if (lv.n == 1) bwd_groups<D, U, 1, ABL>(a, lv, cx, r00, acc_w, acc_b, acc_l);
+      else bwd_groups<D, U, 0, ABL>(a, lv, cx, r00, acc_w, acc_b, acc_l);
     }
   } else {
     for (int64_t r00 = r_begin; r00 < r_end; r00 += NW * RPW)
-      bwd_groups<D, 1, kMaxTab>(a, lv, cx, r00, acc_w, acc_b, acc_l);
+      bwd_groups<D, 1, kMaxTab, ABL>(a, lv, cx, r00, acc_w, acc_b, acc_l);
   }
 #pragma unroll
   for (int j = 0; j < kMaxTab; ++j) {
@@ -631,7 +634,17 @@ template <int D>
 int launch_bwd(const BwdArgs& a, hipStream_t st) {
   const int64_t blocks = (a.f.T + a.rows_per_block - 1) / a.rows_per_block;
   const size_t lds = (size_t)(a.f.L * D + a.small_total) * sizeof(float);
-  hipLaunchKernelGGL(seq_embed_bwd_k<D>, dim3((unsigned)blocks), dim3(256), lds, st, a);
+  static const int abl = [] {
+    const char* e = getenv("RSX_SEQ_EMBED_BWD_ABL");
+    return e ? atoi(e) : 0;
+  }();
+  switch (abl) {
+    case 1: hipLaunchKernelGGL((seq_embed_bwd_k<D, 1>), dim3((unsigned)blocks), dim3(256), lds, st, a); break;
+    case 2: hipLaunchKernelGGL((seq_embed_bwd_k<D, 2>), dim3((unsigned)blocks), dim3(256), lds, st, a); break;
+    case 3: hipLaunchKernelGGL((seq_embed_bwd_k<D, 3>), dim3((unsigned)blocks), dim3(256), lds, st, a); break;
+    case 7: hipLaunchKernelGGL((seq_embed_bwd_k<D, 7>), dim3((unsigned)blocks), dim3(256), lds, st, a); break;
+    default: hipLaunchKernelGGL((seq_embed_bwd_k<D, 0>), dim3((unsigned)blocks), dim3(256), lds, st, a); break;
+  }
   return 0;
 }
 
