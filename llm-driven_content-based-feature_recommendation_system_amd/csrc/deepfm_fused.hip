@@ -673,6 +673,258 @@ __global__ __launch_bounds__(256) void deepfm_pack_k(const float* V, const float
   reinterpret_cast<float4*>(out + id * 32)[ch] = v;
 }
 
+// ---- row-owning form (F = 39: the config-3 field count; other F take deepfm_persist_k) -------
+// Every wave owns 64 rows and gathers them itself, straight into MFMA fragment registers: no
+// loader / compute hand-off (the persistent kernel's bound: its compute waves waited a third of
+// their time for the loaders). Per field f and m-tile i (32 rows), lane (c, h) issues three
+// 16-B loads of row 32i + c's packed 128-B line: bytes 16h (V[4h..4h+3]), 32 + 16h
+// (V[8+4h..]) and 64 + 16h (W at byte 64, read by h = 0). A random-line probe reads 53 G lines/s
+// with the first two (one line request per pair, as one 4-lane instruction: 52 G) and 48 G with
+// the third (tools/probe/gather_pieces.hip). The lane's eight values are the B fragment of
+// v_mfma_f32_32x32x16_bf16 for k-slots 8h..8h+7 <-> V[kperm(slot)], kperm = {0-3, 8-11, 4-7,
+// 12-15} (the W1 image uses the same order). W1 (the A operand, [256][16] per field, hi / lo)
+// streams through a two-slot LDS ring: each wave register-loads a quarter of field f + R's
+// image along with its own gathers for f + R, writes it at field f, one barrier per field (no
+// glds: beside it hipcc drains ordinary loads with vmcnt(0)). The field loop is fully unrolled
+// (F is a template parameter) so the R-deep register ring is straight-line code: loop-carried
+// load registers make hipcc drain the loads at the loop header. Layer 2 takes its B fragments
+// from the layer-1 accumulators (the deepfm_fused_k order; W2 image of deepfm_prep_k).
+constexpr int kRowsF = 39;
+constexpr int kRowsR = 8;           // fields of loads in flight ahead of the one computed
+constexpr int kW1Field = 8192;      // bf16 per field image: hi [256][16] then lo [256][16]
+
+struct RArgs {
+  const int64_t* x;          // [R, F]
+  const float* P[kMaxF];     // packed [vocab][32]: V[16], W, pad
+  int64_t R;
+  int64_t nit;               // task rounds (4 tasks of 64 rows per workgroup per round)
+  float bias;
+  const __bf16* w1;          // [F][8192] (swizzled, kperm order; deepfm_prep3_k)
+  const float* b1;
+  const __bf16* w2hi;        // [16 ksteps][128][2][8] (deepfm_prep_k order)
+  const __bf16* w2lo;
+  const float* b2;
+  const float* wo;
+  float* logit;
+  float* prob;
+};
+
+// element index of (n, slot) in a field image's hi half; the 16-B halves of a row are swapped
+// on bit 3 of n, so the 16 lanes of each ds_read_b128 lane group hit all 64 banks
+__device__ __host__ __forceinline__ int w1_idx(int n, int slot) {
+  return n * 16 + 8 * ((slot >> 3) ^ ((n >> 3) & 1)) + (slot & 7);
+}
+
+template <int F>
+__global__ __launch_bounds__(256, 1) void deepfm_rows_k(RArgs a) {
+  constexpr int R = kRowsR, NB = R + 1;
+  __shared__ __attribute__((aligned(16))) __bf16 w1s[2][kW1Field];
+  __shared__ int ids_s[4][32 * F];
+  __shared__ __attribute__((aligned(16))) float b1s[kN1];  // layer-2 epilogue bias via LDS: a
+                                                           // global load there waits out the W2 prefetch
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c = lane & 31, h = lane >> 5;
+  b1s[tid] = a.b1[tid];  // visible after barrier 0
+  int* my_ids = ids_s[wave];
+  const int64_t m0 = ((int64_t)blockIdx.x * 4 + wave) * 32;  // this wave's 32 rows
+  const uint4* w1g = reinterpret_cast<const uint4*>(a.w1);
+  uint4* w1l0 = reinterpret_cast<uint4*>(w1s[0]);
+  uint4* w1l1 = reinterpret_cast<uint4*>(w1s[1]);
+
+  // ---- ids of the 32 rows -> LDS (int32); rows past R re-read the last row, never stored
+  {
+    const int64_t last = a.R - 1;
+    constexpr int NT = (32 * F + 63) / 64;
+    int64_t v[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int e = lane + 64 * t;
+      const int row = e / F, f = e - row * F;
+      const int64_t gr = m0 + row <= last ? m0 + row : last;
+      v[t] = e < 32 * F ? a.x[gr * F + f] : 0;
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      if (lane + 64 * t < 32 * F) my_ids[lane + 64 * t] = (int)v[t];
+  }
+  // ---- layer 1 over the fields: the gathers of fields f+1..f+R and this wave's quarter of
+  // their W1 images in flight (one register ring: both are waited for at the same depth, so the
+  // in-order vmcnt never waits on a younger field)
+  float4 xa[NB], xb[NB], xw[NB];
+  uint4 wq[NB][4];
+  f32x16 acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
+  float fs[8], fq = 0.0f, fw = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) fs[k] = 0.0f;
+  auto issue = [&](int f, int sl) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) wq[sl][k] = w1g[f * (kW1Field / 8) + 256 * wave + lane + 64 * k];
+    const int id = my_ids[c * F + f];
+    const float4* line = reinterpret_cast<const float4*>(a.P[f] + (int64_t)id * 32);
+    xa[sl] = line[h];
+    xb[sl] = line[2 + h];
+    xw[sl] = line[4 + h];
+  };
+#pragma unroll
+  for (int f = 0; f < R; ++f) issue(f, f);
+#pragma unroll
+  for (int f = 0; f < F; ++f) {
+    const int sl = f % NB;
+    if (f + R < F) issue(f + R, (f + R) % NB);
+    __builtin_amdgcn_sched_barrier(0);
+    // field f's registers "redefined" here: left alone, hipcc consumes each field's loads right
+    // after issuing them (fewer live registers) and so waits on them at once
+    asm volatile("" : "+v"(wq[sl][0].x), "+v"(wq[sl][0].y), "+v"(wq[sl][0].z), "+v"(wq[sl][0].w),
+                 "+v"(wq[sl][1].x), "+v"(wq[sl][1].y), "+v"(wq[sl][1].z), "+v"(wq[sl][1].w));
+    asm volatile("" : "+v"(wq[sl][2].x), "+v"(wq[sl][2].y), "+v"(wq[sl][2].z), "+v"(wq[sl][2].w),
+                 "+v"(wq[sl][3].x), "+v"(wq[sl][3].y), "+v"(wq[sl][3].z), "+v"(wq[sl][3].w));
+    uint4* slot = (f & 1) ? w1l1 : w1l0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) slot[256 * wave + lane + 64 * k] = wq[sl][k];
+    __syncthreads();  // barrier f: slot f & 1 holds field f (plain global loads survive it)
+    asm volatile("" : "+v"(xa[sl].x), "+v"(xa[sl].y), "+v"(xa[sl].z), "+v"(xa[sl].w), "+v"(xb[sl].x),
+                 "+v"(xb[sl].y), "+v"(xb[sl].z), "+v"(xb[sl].w), "+v"(xw[sl].x), "+v"(xw[sl].y), "+v"(xw[sl].z),
+                 "+v"(xw[sl].w));
+    const __bf16* ws = (f & 1) ? w1s[1] : w1s[0];
+    // W1 fragments of n-tile pair jp + 1 read while pair jp's MFMAs run; pair 0's reads are
+    // issued before the split, whose VALU then covers their latency
+    bf16x8 ah[2][2], al[2][2];
+    auto wread = [&](int jp, int b) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int n = 32 * (2 * jp + q) + c;
+        ah[b][q] = *reinterpret_cast<const bf16x8*>(ws + w1_idx(n, 8 * h));
+        al[b][q] = *reinterpret_cast<const bf16x8*>(ws + 4096 + w1_idx(n, 8 * h));
+      }
+    };
+    wread(0, 0);
+    bf16x8 bh, bl;
+    {
+      const float4 p = xa[sl], q = xb[sl], w = xw[sl];
+      const float v[8] = {p.x, p.y, p.z, p.w, q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        fs[k] += v[k];
+        fq += v[k] * v[k];
+        const __bf16 hv = (__bf16)v[k];
+        bh[k] = hv;
+        bl[k] = (__bf16)(v[k] - (float)hv);
+      }
+      // bytes 64..95 of the line: W then zeros (deepfm_pack_k), so the whole 16-B piece sums
+      // to W on h = 0 and to 0 on h = 1 (all four components used: a dword load of the same
+      // line runs at 38 G lines/s in the probe, a 16-B piece at 48 G)
+      fw += (w.x + w.y) + (w.z + w.w);
+    }
+#pragma unroll
+    for (int jp = 0; jp < 4; ++jp) {
+      if (jp + 1 < 4) wread(jp + 1, (jp + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
+      const int b = jp & 1;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int j = 2 * jp + q;
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[b][q], bh, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[b][q], bl, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[b][q], bh, acc[j], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // ---- layer 2 in two halves of n2 (64 outputs each, so the accumulators, the next k-step's W2
+  // prefetch and the layer-1 accumulators fit 256 registers): B fragments of k-step t = 2j + g2
+  // from acc[j] (deepfm_fused_k order), rebuilt per half
+  float dot = 0.0f;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    f32x16 acc2[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc2[q][r] = 0.0f;
+    bf16x8 w2h[2][2], w2l[2][2];
+    auto w2load = [&](int t, int b) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int o = ((t * kN2 + 32 * (2 * half + q) + c) * 2 + h) * 8;
+        w2h[b][q] = *reinterpret_cast<const bf16x8*>(a.w2hi + o);
+        w2l[b][q] = *reinterpret_cast<const bf16x8*>(a.w2lo + o);
+      }
+    };
+    w2load(0, 0);
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int j = t >> 1, g2 = t & 1;
+      if (t + 1 < 16) w2load(t + 1, (t + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
+      bf16x8 gh, gl;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const float4 bb = *reinterpret_cast<const float4*>(b1s + 16 * t + 8 * p + 4 * h);
+        const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = acc[j][4 * (2 * g2 + p) + e] + bv[e];
+          v = v > 0.0f ? v : 0.0f;
+          const __bf16 hv = (__bf16)v;
+          gh[4 * p + e] = hv;
+          gl[4 * p + e] = (__bf16)(v - (float)hv);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const bf16x8 ah = w2h[t & 1][q], al = w2l[t & 1][q];
+        acc2[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, gh, acc2[q], 0, 0, 0);
+        acc2[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, gl, acc2[q], 0, 0, 0);
+        acc2[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, gh, acc2[q], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // relu(H2 + b2) . wo over this half's 64 outputs
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int nb = 32 * (2 * half + q) + 8 * g + 4 * h;
+        const float4 bb = *reinterpret_cast<const float4*>(a.b2 + nb);
+        const float4 ww = *reinterpret_cast<const float4*>(a.wo + nb);
+        dot += fmaxf(acc2[q][4 * g + 0] + bb.x, 0.0f) * ww.x;
+        dot += fmaxf(acc2[q][4 * g + 1] + bb.y, 0.0f) * ww.y;
+        dot += fmaxf(acc2[q][4 * g + 2] + bb.z, 0.0f) * ww.z;
+        dot += fmaxf(acc2[q][4 * g + 3] + bb.w, 0.0f) * ww.w;
+      }
+  }
+  float fm = -fq;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) fm += fs[k] * fs[k];
+  dot += __shfl_xor(dot, 32, 64);
+  fm += __shfl_xor(fm, 32, 64);
+  const float first = fw + __shfl_xor(fw, 32, 64);
+  const int64_t row = m0 + c;
+  if (h == 0 && row < a.R) {
+    const float v = a.bias + first + 0.5f * fm + dot;
+    a.logit[row] = v;
+    if (a.prob) a.prob[row] = 1.0f / (1.0f + expf(-v));
+  }
+}
+
+// W1 [256][F*16] -> [F][8192]: hi at w1_idx(n, s), lo at 4096 + w1_idx(n, s), s = k-slot with
+// V index kperm(s) = (s & 3) + 8 * ((s >> 2) & 1) + 4 * (s >> 3)
+__global__ __launch_bounds__(256) void deepfm_prep3_k(const float* w1, int F, __bf16* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)F * 256 * 16) return;
+  const int s = (int)(i & 15), n = (int)((i >> 4) & 255), f = (int)(i >> 12);
+  const int k = (s & 3) + 8 * ((s >> 2) & 1) + 4 * (s >> 3);
+  const float v = w1[(int64_t)n * F * 16 + f * 16 + k];
+  const __bf16 hv = (__bf16)v;
+  __bf16* img = out + (int64_t)f * kW1Field;
+  img[w1_idx(n, s)] = hv;
+  img[4096 + w1_idx(n, s)] = (__bf16)(v - (float)hv);
+}
+
 size_t persist_lds_bytes(int id_stride) {
   return (size_t)4 * kChunk2 * sizeof(__bf16) + 2 * (size_t)kBM * kH1Stride * sizeof(__bf16) +
          4 * kBM * sizeof(float) + 2 * (size_t)kBM * id_stride * sizeof(int);
@@ -681,6 +933,15 @@ size_t persist_lds_bytes(int id_stride) {
 using rsx::cu_count;
 
 bool persist_ok(int F) { return F >= 3 * kFC2 + 1 && F <= kPersistMaxF && getenv("RSX_DEEPFM_PERSIST") == nullptr; }
+
+// row-owning kernel for F = 39 (RSX_DEEPFM_ROWS=0: the persistent kernel, A/B)
+bool rows_ok(int F) {
+  static const bool off = [] {
+    const char* e = getenv("RSX_DEEPFM_ROWS");
+    return e && e[0] == '0';
+  }();
+  return F == kRowsF && !off;
+}
 
 }  // namespace
 
@@ -695,6 +956,13 @@ RSX_API int64_t rsx_deepfm_fused_workspace_bytes(int F) {
 namespace {
 // Builds the weight images of the kernel form rsx_deepfm_fused_run takes for F fields.
 int deepfm_prep_images(int F, const float* w1, const float* w2, __bf16* wsb, hipStream_t st) {
+  if (rows_ok(F)) {  // W1 [F][8192] (deepfm_prep3_k), then W2 in deepfm_prep_k's permuted order
+    const int64_t n1 = (int64_t)F * 256 * 16, m1 = (int64_t)F * kW1Field, n2 = 16 * kN2 * 16;
+    hipLaunchKernelGGL(deepfm_prep3_k, dim3((unsigned)((n1 + 255) / 256)), dim3(256), 0, st, w1, F, wsb);
+    hipLaunchKernelGGL(deepfm_prep_k, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, st, w1, F, 0, w2, wsb, wsb,
+                       wsb + m1, wsb + m1 + n2);
+    return 0;
+  }
   if (persist_ok(F)) {
     const int nchunk = (F + kFC2 - 1) / kFC2;
     const int64_t m1 = (int64_t)nchunk * kFC2 * kN1 * 16, m2 = (int64_t)kN2 * kN1;
@@ -728,7 +996,7 @@ RSX_API int rsx_deepfm_pack(const float* V, const float* W, int64_t vocab, float
   return 0;
 }
 
-RSX_API int rsx_deepfm_fused_uses_packed(int F) { return persist_ok(F) ? 1 : 0; }
+RSX_API int rsx_deepfm_fused_uses_packed(int F) { return (persist_ok(F) || rows_ok(F)) ? 1 : 0; }
 
 RSX_API int rsx_deepfm_fused_run(const int64_t* x, int64_t R, int F, const float* const* V, const float* const* W,
                                  const float* const* packed, float bias, const float* b1, const float* b2,
@@ -739,6 +1007,24 @@ RSX_API int rsx_deepfm_fused_run(const int64_t* x, int64_t R, int F, const float
   for (int f = 0; f < F; ++f) RSX_ARG(V[f] != nullptr, "null field table");
   const __bf16* wsb = reinterpret_cast<const __bf16*>(ws);
   hipStream_t st = (hipStream_t)stream;
+  if (rows_ok(F) && packed) {
+    for (int f = 0; f < F; ++f) RSX_ARG(packed[f] != nullptr, "null packed table");
+    RArgs r;
+    r.x = x;
+    for (int f = 0; f < kMaxF; ++f) r.P[f] = f < F ? packed[f] : nullptr;
+    r.R = R;
+    const int64_t grid = (R + 127) / 128;  // 4 compute waves x 32 rows
+    r.nit = 1;
+    r.bias = bias;
+    const int64_t m1 = (int64_t)F * kW1Field, n2 = 16 * kN2 * 16;
+    r.w1 = wsb;
+    r.w2hi = wsb + m1;
+    r.w2lo = wsb + m1 + n2;
+    r.b1 = b1; r.b2 = b2; r.wo = wo; r.logit = logit; r.prob = prob;
+    hipLaunchKernelGGL(deepfm_rows_k<kRowsF>, dim3((unsigned)grid), dim3(256), 0, st, r);
+    RSX_LAUNCHED();
+    return 0;
+  }
   if (persist_ok(F)) {
     PArgs p;
     p.x = x;

@@ -141,9 +141,33 @@ __global__ __launch_bounds__(256) void segsum_rows_k(const float* __restrict__ s
     if (row == skip) continue;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     const int64_t k1 = seg[u + 1];
-    for (int64_t k = seg[u]; k < k1; ++k) {
-      const float4 x = reinterpret_cast<const float4*>(src + (perm ? perm[k] : k) * ld_src)[c];
-      acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
+    int64_t k = seg[u];
+    // sixteen index loads, then sixteen row loads in flight before the first add (the loop is a
+    // dependent perm -> row chain per row otherwise); the adds keep the segment order
+    for (; k + 16 <= k1; k += 16) {
+      int64_t p[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) p[i] = perm ? perm[k + i] : k + i;
+      float4 x[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) x[i] = reinterpret_cast<const float4*>(src + p[i] * ld_src)[c];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        acc.x += x[i].x; acc.y += x[i].y; acc.z += x[i].z; acc.w += x[i].w;
+      }
+    }
+    if (k < k1) {  // the last < 16 rows, also all in flight at once
+      const int n = (int)(k1 - k);
+      int64_t p[15];
+#pragma unroll
+      for (int i = 0; i < 15; ++i) p[i] = i < n ? (perm ? perm[k + i] : k + i) : 0;
+      float4 x[15];
+#pragma unroll
+      for (int i = 0; i < 15; ++i)
+        x[i] = i < n ? reinterpret_cast<const float4*>(src + p[i] * ld_src)[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int i = 0; i < 15; ++i)
+        if (i < n) { acc.x += x[i].x; acc.y += x[i].y; acc.z += x[i].z; acc.w += x[i].w; }
     }
     float4* d = reinterpret_cast<float4*>(dst + row * ld_dst) + c;
     float4 v = make_float4(sc * acc.x, sc * acc.y, sc * acc.z, sc * acc.w);

@@ -244,7 +244,7 @@ struct BwdCtx {
 // position and table rows (the LN recompute and the gate dot reuse the same table rows) — so a
 // lane has U x (1 + NL) id -> row chains in flight instead of one at a time. NL = kMaxTab is the
 // generic more-than-two-live-tables form (slots guarded by lv.n).
-template <int D, int U, int NL, int ABL>
+template <int D, int U, int NL, int ABL, bool SC>
 __device__ __forceinline__ void bwd_groups(const BwdArgs& a, const BwdLive& lv, const BwdCtx& cx, int64_t r00,
                                            float4& acc_w, float4& acc_b, float* acc_l) {
   constexpr int LPR = D / 4;
@@ -333,6 +333,22 @@ __device__ __forceinline__ void bwd_groups(const BwdArgs& a, const BwdLive& lv, 
     }
     if (a.dbase && !(ABL & 4)) reinterpret_cast<float4*>(a.dbase + r * D)[c] = dx;
     if (ABL & 1) continue;
+    if (!SC) {  // position / small-table sums come from seq_embed_keysum_k over dbase
+      if (a.dgate) {
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+          if (!(NL > 0 && (NL != kMaxTab || k < lv.n))) continue;
+          const float4 e = ev[u][k];
+          acc_l[k] += dx.x * e.x + dx.y * e.y + dx.z * e.z + dx.w * e.w;
+        }
+      }
+      // a live table too large for the LDS image still takes the global scatter below
+      bool big = false;
+#pragma unroll
+      for (int k = 0; k < NS; ++k)
+        if (NL > 0 && (NL != kMaxTab || k < lv.n) && lv.dtab[k] && lv.soff[k] < 0) big = true;
+      if (!big) continue;
+    }
     // Scatter-adds take the row in lane-strided order (lane c holds elements c + LPR*k): each
     // atomic instruction then covers LPR consecutive floats (one 128-B line per row at D=128)
     // instead of LPR 16-B pieces over four lines — 4x fewer lines per L2 atomic and
@@ -344,7 +360,7 @@ __device__ __forceinline__ void bwd_groups(const BwdArgs& a, const BwdLive& lv, 
 #pragma unroll
     for (int k = 0; k < 4; ++k) xs[k] = cx.xr[c + LPR * k];
     __builtin_amdgcn_wave_barrier();
-    if (a.dpos) {
+    if (SC && a.dpos) {
       float* dst = cx.s_pos + lp[u] * D + c;
 #pragma unroll
       for (int k = 0; k < 4; ++k) atomicAdd(dst + LPR * k, xs[k]);
@@ -352,7 +368,7 @@ __device__ __forceinline__ void bwd_groups(const BwdArgs& a, const BwdLive& lv, 
 #pragma unroll
     for (int k = 0; k < NS; ++k) {
       if (!(NL > 0 && (NL != kMaxTab || k < lv.n))) continue;
-      if (a.dgate) {
+      if (SC && a.dgate) {
         const float4 e = ev[u][k];
         acc_l[k] += dx.x * e.x + dx.y * e.y + dx.z * e.z + dx.w * e.w;
       }
@@ -360,6 +376,7 @@ __device__ __forceinline__ void bwd_groups(const BwdArgs& a, const BwdLive& lv, 
       if (lv.dtab[k] && i != lv.pad[k]) {
         const float gk = lv.g[k];
         if (lv.soff[k] >= 0) {
+          if (!SC) continue;
           float* dst = cx.s_small + lv.soff[k] + i * D + c;
 #pragma unroll
           for (int q = 0; q < 4; ++q)
@@ -383,7 +400,10 @@ constexpr int kSmallMax = 8192;  // floats (32 KiB)
 // atomics are emitted.
 // ABL: timing ablations only (results wrong): 1 no LDS / global scatter, 2 no table-row loads,
 // 4 no dbase store (RSX_SEQ_EMBED_BWD_ABL, tools/seq_embed_step_micro.py)
-template <int D, int ABL>
+// SC = false: no scatter at all (every table gradient and the positions come from the sorted
+// segment sums / seq_embed_keysum_k over dbase); only LN weight / bias and gate sums, and only
+// those columns of the partial row are written.
+template <int D, int ABL, bool SC = true, int UB = 2>
 __global__ __launch_bounds__(256) void seq_embed_bwd_k(BwdArgs a) {
   constexpr int LPR = D / 4;
   constexpr int RPW = 64 / LPR;
@@ -399,9 +419,9 @@ __global__ __launch_bounds__(256) void seq_embed_bwd_k(BwdArgs a) {
   const int sub = lane / LPR, c = lane % LPR;
   float* s_pos = s_dyn;
   float* s_small = s_dyn + (int64_t)f.L * D;
-  const int lds_total = f.L * D + a.small_total;
+  const int lds_total = SC ? f.L * D + a.small_total : 0;
   for (int i = tid; i < lds_total; i += blockDim.x) s_dyn[i] = 0.0f;
-  __syncthreads();
+  if (SC) __syncthreads();
 
   float g[kMaxTab];
 #pragma unroll
@@ -446,15 +466,14 @@ __global__ __launch_bounds__(256) void seq_embed_bwd_k(BwdArgs a) {
   for (int k = 0; k < kMaxTab; ++k) acc_l[k] = 0.0f;
   BwdCtx cx{&s_xr[wave][sub][0], s_pos, s_small, r_begin, r_end, wave, sub, c, w, do_ln};
   if (lv.n <= 2) {
-    constexpr int U = 2;
-    for (int64_t r00 = r_begin; r00 < r_end; r00 += U * NW * RPW) {
-      if (lv.n == 2) bwd_groups<D, U, 2, ABL>(a, lv, cx, r00, acc_w, acc_b, acc_l);
-      else if (lv.n == 1) bwd_groups<D, U, 1, ABL>(a, lv, cx, r00, acc_w, acc_b, acc_l);
-      else bwd_groups<D, U, 0, ABL>(a, lv, cx, r00, acc_w, acc_b, acc_l);
+    for (int64_t r00 = r_begin; r00 < r_end; r00 += UB * NW * RPW) {
+      if (lv.n == 2) bwd_groups<D, UB, 2, ABL, SC>(a, lv, cx, r00, acc_w, acc_b, acc_l);
+      else if (lv.n == 1) bwd_groups<D, UB, 1, ABL, SC>(a, lv, cx, r00, acc_w, acc_b, acc_l);
+      else bwd_groups<D, UB, 0, ABL, SC>(a, lv, cx, r00, acc_w, acc_b, acc_l);
     }
   } else {
     for (int64_t r00 = r_begin; r00 < r_end; r00 += NW * RPW)
-      bwd_groups<D, 1, kMaxTab, ABL>(a, lv, cx, r00, acc_w, acc_b, acc_l);
+      bwd_groups<D, 1, kMaxTab, ABL, SC>(a, lv, cx, r00, acc_w, acc_b, acc_l);
   }
 #pragma unroll
   for (int j = 0; j < kMaxTab; ++j) {
@@ -491,7 +510,8 @@ __global__ __launch_bounds__(256) void seq_embed_bwd_k(BwdArgs a) {
     // stores, zeros included), folded over blocks in a fixed order by seq_embed_bwd_reduce_k
     float* prow = a.partials + (int64_t)blockIdx.x * a.part_w;
     const int nlds = f.L * D + a.small_total;
-    for (int i = tid; i < nlds; i += blockDim.x) prow[i] = s_dyn[i];
+    if (SC)
+      for (int i = tid; i < nlds; i += blockDim.x) prow[i] = s_dyn[i];
     for (int i = tid; i < 2 * D; i += blockDim.x) {
       const int which = i / D, col = i % D;
       float v = 0.0f;
@@ -539,6 +559,150 @@ __global__ __launch_bounds__(256) void seq_embed_bwd_k(BwdArgs a) {
   }
 }
 
+// Position and small-table gradients as one-hot products on the MFMA (D = 128), replacing the
+// LDS float atomics (≈ 130 cycles per ds_add_f32 wave-instruction measured: 0.28 ms of the
+// 0.65-ms backward at the bench shape, tools/seq_embed_step_micro.py):
+//   S[key][dim] = sum_t onehot[t][key] * dx[t][dim],  key = position (0..L-1) or
+//                 L + small_off_j / D + id_j(t) for each small table j (id != padding_idx)
+// over dbase (= dx, written by seq_embed_bwd_k<.., SC = false>). Each wave streams 16-token steps:
+// lane (c, h) loads dims 4c..4c+3 of tokens h + 2i (i = 0..7) — exactly the B fragment of
+// v_mfma_f32_32x32x16_bf16 for n = c (dim 4c + j, one MFMA column tile per component j) with
+// k-slot 8h + i <-> token h + 2i; the A fragment (one-hot, keys 32 kt + c) is built in registers
+// from the same tokens' keys. dx = b1 + b2 + b3 split exactly into three bf16 parts (24 mantissa
+// bits), so every product is exact and only the fp32 accumulation rounds. The four waves of a
+// workgroup meet in LDS in wave order; one partial row [nkeys][D] per workgroup, folded by
+// seq_embed_bwd_reduce_k (deterministic).
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+struct KeyArgs {
+  const float* dx;            // [T][128]
+  const int64_t* tok_pos;     // [T] or nullptr => r % L
+  const int64_t* ids[2];      // small tables' ids (nullptr: slot unused)
+  int key_off[2];             // first key of each small table
+  int64_t pad[2];
+  int64_t T;
+  int L;
+  int do_pos;                 // position keys wanted
+  int nkeys;                  // <= 64
+  int64_t rows_per_block;     // multiple of 64
+  float* partials;            // [blocks][nkeys * 128]
+};
+
+__device__ __forceinline__ void split3(float x, __bf16& a, __bf16& b, __bf16& c) {
+  a = (__bf16)x;
+  const float r = x - (float)a;
+  b = (__bf16)r;
+  c = (__bf16)(r - (float)b);
+}
+
+// TP: tok_pos given (else r % L); NS: small tables (0..2). Compile-time so the loop has no
+// branches: a branch join makes the waitcnt pass drain the prefetched step with vmcnt(0).
+template <bool TP, int NS>
+__global__ __launch_bounds__(256, 2) void seq_embed_keysum_k(KeyArgs a) {
+  __shared__ __attribute__((aligned(16))) float s_acc[64 * 128];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c = lane & 31, h = lane >> 5;
+  const int64_t r_begin = (int64_t)blockIdx.x * a.rows_per_block;
+  int64_t r_end = r_begin + a.rows_per_block;
+  if (r_end > a.T) r_end = a.T;
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[kt][j][r] = 0.0f;
+
+  // rows past the block are clamped to its last row (valid memory) and given no key, so their
+  // one-hot column is zero: no per-row branches. load_step only issues loads (keys first); the
+  // keys are formed in compute_step, so no wait lands between the loads of a step.
+  struct Step {
+    float4 x[8];
+    int64_t p, i0, i1;
+  };
+  auto load_step = [&](int64_t s0, Step& st) {
+    const int64_t r0 = s0 + (lane & 15);
+    const int64_t rk = r0 < r_end ? r0 : r_end - 1;
+    st.p = TP ? a.tok_pos[rk] : rk % a.L;
+    st.i0 = NS > 0 ? a.ids[0][rk] : a.pad[0];
+    st.i1 = NS > 1 ? a.ids[1][rk] : a.pad[1];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      int64_t r = s0 + h + 2 * i;
+      r = r < r_end ? r : r_end - 1;
+      st.x[i] = reinterpret_cast<const float4*>(a.dx + r * 128)[c];
+    }
+  };
+  auto compute_step = [&](int64_t s0, const Step& st) {
+    const bool ok = s0 + (lane & 15) < r_end;
+    const int kp = (ok && a.do_pos) ? (int)st.p : -1;
+    const int k0 = (ok && st.i0 != a.pad[0]) ? a.key_off[0] + (int)st.i0 : -1;
+    const int k1 = (ok && st.i1 != a.pad[1]) ? a.key_off[1] + (int)st.i1 : -1;
+    bf16x8 am[2];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int t = h + 2 * i;
+      const int p = __shfl(kp, t, 64), q0 = __shfl(k0, t, 64), q1 = __shfl(k1, t, 64);
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        const int key = 32 * kt + c;
+        am[kt][i] = (p == key || q0 == key || q1 == key) ? (__bf16)1.0f : (__bf16)0.0f;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bf16x8 b1, b2, b3;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float v = j == 0 ? st.x[i].x : (j == 1 ? st.x[i].y : (j == 2 ? st.x[i].z : st.x[i].w));
+        __bf16 p1, p2, p3;
+        split3(v, p1, p2, p3);
+        b1[i] = p1; b2[i] = p2; b3[i] = p3;
+      }
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        acc[kt][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[kt], b3, acc[kt][j], 0, 0, 0);
+        acc[kt][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[kt], b2, acc[kt][j], 0, 0, 0);
+        acc[kt][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[kt], b1, acc[kt][j], 0, 0, 0);
+      }
+    }
+  };
+
+  // 16-token steps, the block's steps dealt to its waves round robin (stride 64 tokens). No
+  // cross-step prefetch (its loop-carried registers made hipcc drain the loads at the loop
+  // header); latency is hidden by two workgroups per CU instead (<= 256 registers per wave).
+  const int64_t first = r_begin + 16 * wave;
+  for (int64_t s0 = first; s0 < r_end; s0 += 64) {
+    Step st;
+    load_step(s0, st);
+    compute_step(s0, st);
+  }
+
+  // waves meet in LDS in wave order: lane (c, h), register r of tile (kt, j) = S[32 kt + row(r, h)][4c + j]
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = 32 * kt + 8 * (r >> 2) + 4 * h + (r & 3);
+          float4* p = reinterpret_cast<float4*>(&s_acc[key * 128 + 4 * c]);
+          float4 v = make_float4(acc[kt][0][r], acc[kt][1][r], acc[kt][2][r], acc[kt][3][r]);
+          if (w > 0) {
+            const float4 o = *p;
+            v.x = o.x + v.x; v.y = o.y + v.y; v.z = o.z + v.z; v.w = o.w + v.w;
+          }
+          *p = v;
+        }
+    }
+    __syncthreads();
+  }
+  float* prow = a.partials + (int64_t)blockIdx.x * a.nkeys * 128;
+  for (int i = tid; i < a.nkeys * 32; i += blockDim.x)
+    reinterpret_cast<float4*>(prow)[i] = reinterpret_cast<const float4*>(s_acc)[i];
+}
+
 // Fold of the per-block partial rows: column j of [blocks][part_w] summed over blocks in block
 // order, then added to its destination (positions, LDS-resident small tables, LN weight / bias,
 // gates). One workgroup per 64 columns; its 4 waves take every 4th block row, 64 lanes read 256
@@ -556,37 +720,51 @@ struct ReduceArgs {
   float* dln_w;
   float* dln_b;
   float* dgate;
+  // seq_embed_keysum_k partial rows [kblocks][kw] (kw = L*D + small_total): when present they,
+  // not the LDS image columns of partials, hold positions and small tables (small-table sums
+  // unscaled: multiplied by their gate here)
+  const float* kpart;
+  int64_t kblocks;
+  const float* gate;
 };
 
 __global__ __launch_bounds__(256) void seq_embed_bwd_reduce_k(ReduceArgs a) {
   __shared__ float s_part[4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int j = blockIdx.x * 64 + lane;
+  const int nlds = a.L * a.D + a.small_total;
+  const bool from_k = a.kpart != nullptr && j < nlds;
+  const float* src = from_k ? a.kpart : a.partials;
+  const int64_t w = from_k ? nlds : a.part_w;
+  const int64_t nb = from_k ? a.kblocks : a.blocks;
   float v = 0.0f;
   if (j < a.part_w) {
-    const float* p = a.partials + j;
+    const float* p = src + j;
     int64_t b = wave;
-    for (; b + 12 < a.blocks; b += 16) {
-      const float x0 = p[b * a.part_w], x1 = p[(b + 4) * a.part_w];
-      const float x2 = p[(b + 8) * a.part_w], x3 = p[(b + 12) * a.part_w];
-      v += x0; v += x1; v += x2; v += x3;
+    for (; b + 28 < nb; b += 32) {
+      float x[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) x[i] = p[(b + 4 * i) * w];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v += x[i];
     }
-    for (; b < a.blocks; b += 4) v += p[b * a.part_w];
+    for (; b < nb; b += 4) v += p[b * w];
   }
   s_part[wave][lane] = v;
   __syncthreads();
   if (wave != 0 || j >= a.part_w) return;
   v = ((s_part[0][lane] + s_part[1][lane]) + s_part[2][lane]) + s_part[3][lane];
   const int npos = a.L * a.D;
-  const int nlds = npos + a.small_total;
   float* dst = nullptr;
   if (j < npos) {
     dst = a.dpos ? a.dpos + j : nullptr;
   } else if (j < nlds) {
     const int o = j - npos;
     for (int t = 0; t < a.ntab; ++t) {
-      if (a.small_off[t] >= 0 && o >= a.small_off[t] && o < a.small_off[t] + a.small_rows[t] * a.D)
+      if (a.small_off[t] >= 0 && o >= a.small_off[t] && o < a.small_off[t] + a.small_rows[t] * a.D) {
         dst = a.dtab[t] ? a.dtab[t] + (o - a.small_off[t]) : nullptr;
+        if (from_k) v *= a.gate ? a.gate[t] : 1.0f;
+      }
     }
   } else if (j < nlds + a.D) {
     dst = a.dln_w ? a.dln_w + (j - nlds) : nullptr;
@@ -631,8 +809,17 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
 }
 
 template <int D>
-int launch_bwd(const BwdArgs& a, hipStream_t st) {
+int launch_bwd(const BwdArgs& a, hipStream_t st, bool keysum) {
   const int64_t blocks = (a.f.T + a.rows_per_block - 1) / a.rows_per_block;
+  if (keysum) {  // no scatter: positions / small tables from seq_embed_keysum_k
+    static const int ub = [] {
+      const char* e = getenv("RSX_SEQ_EMBED_BWD_U");
+      return e ? atoi(e) : 2;
+    }();
+    if (ub == 4) hipLaunchKernelGGL((seq_embed_bwd_k<D, 0, false, 4>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((seq_embed_bwd_k<D, 0, false, 2>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+    return 0;
+  }
   const size_t lds = (size_t)(a.f.L * D + a.small_total) * sizeof(float);
   static const int abl = [] {
     const char* e = getenv("RSX_SEQ_EMBED_BWD_ABL");
@@ -727,12 +914,13 @@ RSX_API int rsx_seq_embed_fwd(const float* base, const int64_t* const* ids, cons
 // flush their LDS sums with global float atomics.
 constexpr int64_t kBwdBlocksWs = 768;  // 3 per CU: the two-group loop runs at 3 waves per SIMD
 constexpr int64_t kBwdBlocksAtomic = 512;
+constexpr int64_t kKeyBlocksMax = 512;  // seq_embed_keysum_k workgroups (2 per CU)
 
 RSX_API int64_t rsx_seq_embed_bwd_workspace_floats(int64_t T, int64_t L, int64_t D) {
   if (T <= 0 || D <= 0) return 0;
   const int64_t rpb = bwd_rows_per_block(T, D, kBwdBlocksWs);
   const int64_t blocks = (T + rpb - 1) / rpb;
-  return blocks * (L * D + kSmallMax + 2 * D + kMaxTab);
+  return blocks * (L * D + kSmallMax + 2 * D + kMaxTab) + kKeyBlocksMax * 64 * D;
 }
 
 RSX_API int rsx_seq_embed_bwd(const float* base, const int64_t* const* ids, const float* const* tables,
@@ -772,10 +960,52 @@ RSX_API int rsx_seq_embed_bwd(const float* base, const int64_t* const* ids, cons
   const int64_t blocks = (T + a.rows_per_block - 1) / a.rows_per_block;
   a.partials = use_ws ? workspace : nullptr;
   a.part_w = (int)(L * D + a.small_total + 2 * D + kMaxTab);
+  // one-hot MFMA key sums instead of LDS atomics: D = 128 with a workspace and dbase, every live
+  // table with a gradient LDS-sized (<= 2 of them), positions + small rows <= 64 keys
+  KeyArgs k{};
+  bool keysum = use_ws && D == 128 && dbase != nullptr && (L * D + a.small_total) <= 64 * D &&
+                getenv("RSX_SEQ_EMBED_KEYSUM") == nullptr;  // =anything: the LDS-atomic kernel (A/B)
+  int nsm = 0;
+  for (int j = 0; j < ntab && keysum; ++j) {
+    // tables too large for the LDS image keep the kernel's global scatter (when live: the gate is
+    // on the device); small ones become keys (a gate of 0 scales their sums to 0 in the reduce)
+    if (!a.dtab[j] || a.small_off[j] < 0) continue;
+    if (nsm == 2) { keysum = false; break; }
+    k.ids[nsm] = ids[j];
+    k.key_off[nsm] = (int)(L + a.small_off[j] / D);
+    k.pad[nsm] = a.pad_idx[j];
+    ++nsm;
+  }
   hipStream_t st = (hipStream_t)stream;
-  if (D == 64) launch_bwd<64>(a, st);
-  else if (D == 128) launch_bwd<128>(a, st);
-  else launch_bwd<256>(a, st);
+  if (D == 64) launch_bwd<64>(a, st, false);
+  else if (D == 128) launch_bwd<128>(a, st, keysum);
+  else launch_bwd<256>(a, st, false);
+  const int64_t ws_a = blocks * a.part_w;
+  int64_t kblocks = 0;
+  if (keysum) {
+    const int64_t nb = 2 * rsx::cu_count() < kKeyBlocksMax ? 2 * rsx::cu_count() : kKeyBlocksMax;  // 2 per CU
+    int64_t rpb = (T + nb - 1) / nb;
+    rpb = (rpb + 63) / 64 * 64;
+    kblocks = (T + rpb - 1) / rpb;
+    k.dx = dbase;
+    k.tok_pos = tok_pos;
+    k.T = T;
+    k.L = (int)L;
+    k.do_pos = dpos != nullptr;
+    k.nkeys = (int)(L + a.small_total / D);
+    k.rows_per_block = rpb;
+    k.partials = workspace + ws_a;
+    const dim3 g((unsigned)kblocks), b(256);
+    if (tok_pos) {
+      if (nsm == 0) hipLaunchKernelGGL((seq_embed_keysum_k<true, 0>), g, b, 0, st, k);
+      else if (nsm == 1) hipLaunchKernelGGL((seq_embed_keysum_k<true, 1>), g, b, 0, st, k);
+      else hipLaunchKernelGGL((seq_embed_keysum_k<true, 2>), g, b, 0, st, k);
+    } else {
+      if (nsm == 0) hipLaunchKernelGGL((seq_embed_keysum_k<false, 0>), g, b, 0, st, k);
+      else if (nsm == 1) hipLaunchKernelGGL((seq_embed_keysum_k<false, 1>), g, b, 0, st, k);
+      else hipLaunchKernelGGL((seq_embed_keysum_k<false, 2>), g, b, 0, st, k);
+    }
+  }
   if (use_ws) {
     ReduceArgs r;
     r.partials = workspace;
@@ -794,6 +1024,9 @@ RSX_API int rsx_seq_embed_bwd(const float* base, const int64_t* const* ids, cons
     r.dln_w = dln_w;
     r.dln_b = dln_b;
     r.dgate = dgate;
+    r.kpart = keysum ? workspace + ws_a : nullptr;
+    r.kblocks = kblocks;
+    r.gate = gate;
     hipLaunchKernelGGL(seq_embed_bwd_reduce_k, dim3((unsigned)((a.part_w + 63) / 64)), dim3(256), 0, st, r);
   }
   RSX_LAUNCHED();

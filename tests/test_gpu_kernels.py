@@ -82,6 +82,56 @@ def test_seq_embed_layernorm_and_backward(gpu, seg):
         torch.testing.assert_close(a.grad.cpu().double(), gr, atol=2e-5, rtol=1e-4, msg=name)
 
 
+@pytest.mark.parametrize("keysum", [True, False])
+def test_seq_embed_backward_packed_step_shape(gpu, keysum, monkeypatch):
+    """Packed layout as the step runs it (tok_pos per token, item table through the sorted
+    segment sums, time table + positions through seq_embed_keysum_k's one-hot MFMA sums, or
+    with keysum=False the LDS-atomic kernel): 24,576 tokens over 40 workgroups' worth of keysum
+    blocks, every gradient vs float64 (atol 5e-5 / rtol 1e-4: sums over ~500-2,000 tokens per
+    position / time row)."""
+    if not keysum:
+        monkeypatch.setenv("RSX_SEQ_EMBED_KEYSUM", "0")
+    g = torch.Generator().manual_seed(11)
+    T, L, D = 24576, 50, 128
+    rows = (997, 12, 51, 51, 51, 51)
+    base = torch.randn(T, D, generator=g)
+    tables = [torch.randn(r, D, generator=g) * 0.02 for r in rows]
+    ids = [torch.randint(0, r, (T,), generator=g) for r in rows]
+    ids[1][torch.rand(T, generator=g) < 0.1] = 0          # time padding rows
+    tok_pos = torch.randint(0, L, (T,), generator=g)
+    gate = torch.sigmoid(torch.randn(6, generator=g)) * torch.tensor([1.0, 1.0, 0.0, 0.0, 0.0, 0.0])
+    pos = torch.randn(L, D, generator=g) * 0.02
+    lw = 1 + 0.1 * torch.randn(D, generator=g)
+    lb = 0.1 * torch.randn(D, generator=g)
+    leaves = [t.clone().double().requires_grad_() for t in [base, *tables, gate, pos, lw, lb]]
+    b64, t64, g64, p64, w64, bb64 = leaves[0], leaves[1:7], leaves[7], leaves[8], leaves[9], leaves[10]
+    x = b64.clone()
+    for t, i, j in zip(t64, ids, range(6)):
+        x = x + t[i] * g64[j]
+    x = x + p64[tok_pos]
+    ref = F.layer_norm(x, (D,), w64, bb64, 1e-5)
+    dout = torch.randn(ref.shape, generator=g, dtype=torch.float64)
+    (ref * dout).sum().backward()
+    dev = [t.clone().to(gpu).requires_grad_() for t in [base, *tables, gate, pos, lw, lb]]
+    ids_d = [i.to(gpu) for i in ids]
+    out = ops.seq_embed(dev[0], ids_d, dev[1:7], dev[7], dev[8], dev[9], dev[10], eps=1e-5,
+                        padding_idx=[0] * 6, tok_pos=tok_pos.to(gpu), tab0_seg=ops.sort_segments(ids_d[0]))
+    (out * dout.float().to(gpu)).sum().backward()
+    names = ["base"] + [f"table{j}" for j in range(6)] + ["gate", "pos", "ln_w", "ln_b"]
+    for name, a, r in zip(names, dev, leaves):
+        gr = r.grad.clone()
+        if name.startswith("table"):
+            gr[0] = 0.0
+            if gate[int(name[-1])] == 0:
+                gr.zero_()
+        if name == "gate":
+            gr = gr * (gate != 0)
+        # sums over up to 24,576 tokens: fp32 rounding of the running partial sums scales with the
+        # gradient's magnitude, not with each element (an ln_b column near 0 still carries it)
+        torch.testing.assert_close(a.grad.cpu().double(), gr, atol=5e-5 + 1e-5 * gr.abs().max().item(),
+                                   rtol=1e-4, msg=lambda m, name=name: f"{name}: {m}")
+
+
 def test_seq_embed_dropout_mask_consistent(gpu):
     base, tables, ids, gate, pos, lw, lb = _embed_inputs(seed=2)
     x = base.to(gpu).requires_grad_()

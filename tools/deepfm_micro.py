@@ -20,11 +20,14 @@ def main():
     ap.add_argument("--vocab", type=int, default=1_000_000)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--uniform", action="store_true")
+    ap.add_argument("--zero", action="store_true", help="every id 0 (L2-resident lines: the non-gather cost)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     model = DeepFM([a.vocab] * 39, device=dev)
     rng = np.random.default_rng(3)
-    if a.uniform:
+    if a.zero:
+        x = torch.zeros(a.rows, 39, dtype=torch.int64, device=dev)
+    elif a.uniform:
         x = torch.from_numpy(rng.integers(0, a.vocab, (a.rows, 39))).to(dev)
     else:
         x = torch.from_numpy(((rng.zipf(1.1, size=(a.rows, 39)) - 1) % a.vocab).astype(np.int64)).to(dev)
