@@ -89,6 +89,15 @@ int rsx_mha_fwd_x3(const float* qkv, const uint8_t* key_pad, const int* seg_off,
 int rsx_mha_bwd_x3(const float* qkv, const uint8_t* key_pad, const int* seg_off, const float* out, const float* lse,
                    const float* dout, int64_t B, int64_t L, int64_t H, int64_t Dh, int causal, float p_drop,
                    uint64_t seed, float* dqkv, void* stream);
+/* Fused in-projection + attention forward (replaces nn.TransformerEncoderLayer's
+ * self_attn in_proj GEMM followed by the attention core, v1_refine_usertower.py:343-352 ->
+ * torch.nn.functional.multi_head_attention_forward): x [T, D] the norm1 output, w [3D, D]
+ * in_proj_weight, bias [3D] in_proj_bias (nullable); D = 128 (4 heads of 32), bf16x3. Writes
+ * out [T, D] and lse [T, H] as rsx_mha_fwd_x3 does, and qkv [T, 3D] (nullable) for
+ * rsx_mha_bwd_x3 and the in_proj weight gradient. */
+int rsx_mha_qkv_fwd_x3(const float* x, const float* w, const float* bias, const uint8_t* key_pad, const int* seg_off,
+                       int64_t B, int64_t L, int64_t H, int causal, float p_drop, uint64_t seed, float* qkv,
+                       float* out, float* lse, void* stream);
 
 /* ---- A6 / A7 / A12: fused in-batch contrastive cross-entropy ------------------------
  * S_ij = <A_i,B_j>/tau - bias_j over an implicit N x M matrix (never materialised),

@@ -39,6 +39,7 @@ _SIGS = {
     "rsx_mha_fwd": (c_i, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i, c_f, c_u64, c_p, c_p, c_p]),
     "rsx_mha_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i, c_f, c_u64, c_p, c_p]),
     "rsx_mha_fwd_x3": (c_i, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i, c_f, c_u64, c_p, c_p, c_p]),
+    "rsx_mha_qkv_fwd_x3": (c_i, [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i, c_f, c_u64, c_p, c_p, c_p, c_p]),
     "rsx_mha_bwd_x3": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i, c_f, c_u64, c_p, c_p]),
     "rsx_nce_workspace_floats": (c_i64, [c_i64, c_i64, c_i, c_i]),
     "rsx_nce_fwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_f, c_i, c_i, c_p,

@@ -715,16 +715,20 @@ __device__ __host__ __forceinline__ int w1_idx(int n, int slot) {
   return n * 16 + 8 * ((slot >> 3) ^ ((n >> 3) & 1)) + (slot & 7);
 }
 
-template <int F>
+// ABL (timing ablations, results wrong; RSX_DEEPFM_ABL): 1 no per-field barrier, 2 no W1 LDS
+// writes, 4 no layer-1 MFMAs, 8 no layer 2
+template <int F, int ABL = 0>
 __global__ __launch_bounds__(256, 1) void deepfm_rows_k(RArgs a) {
   constexpr int R = kRowsR, NB = R + 1;
   __shared__ __attribute__((aligned(16))) __bf16 w1s[2][kW1Field];
   __shared__ int ids_s[4][32 * F];
-  __shared__ __attribute__((aligned(16))) float b1s[kN1];  // layer-2 epilogue bias via LDS: a
-                                                           // global load there waits out the W2 prefetch
+  // b1 / b2 / w_o via LDS: a global load in layer 2 would wait out its W2 prefetch
+  __shared__ __attribute__((aligned(16))) float b1s[kN1], b2s[kN2], wos[kN2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int c = lane & 31, h = lane >> 5;
   b1s[tid] = a.b1[tid];  // visible after barrier 0
+  if (tid < kN2) b2s[tid] = a.b2[tid];
+  else wos[tid - kN2] = a.wo[tid - kN2];
   int* my_ids = ids_s[wave];
   const int64_t m0 = ((int64_t)blockIdx.x * 4 + wave) * 32;  // this wave's 32 rows
   const uint4* w1g = reinterpret_cast<const uint4*>(a.w1);
@@ -783,9 +787,13 @@ __global__ __launch_bounds__(256, 1) void deepfm_rows_k(RArgs a) {
     asm volatile("" : "+v"(wq[sl][2].x), "+v"(wq[sl][2].y), "+v"(wq[sl][2].z), "+v"(wq[sl][2].w),
                  "+v"(wq[sl][3].x), "+v"(wq[sl][3].y), "+v"(wq[sl][3].z), "+v"(wq[sl][3].w));
     uint4* slot = (f & 1) ? w1l1 : w1l0;
+    if (!(ABL & 2)) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) slot[256 * wave + lane + 64 * k] = wq[sl][k];
-    __syncthreads();  // barrier f: slot f & 1 holds field f (plain global loads survive it)
+      for (int k = 0; k < 4; ++k) slot[256 * wave + lane + 64 * k] = wq[sl][k];
+    } else {
+      asm volatile("" :: "v"(wq[sl][0].x), "v"(wq[sl][1].x), "v"(wq[sl][2].x), "v"(wq[sl][3].x));
+    }
+    if (!(ABL & 1)) __syncthreads();  // barrier f: slot f & 1 holds field f (plain global loads survive it)
     asm volatile("" : "+v"(xa[sl].x), "+v"(xa[sl].y), "+v"(xa[sl].z), "+v"(xa[sl].w), "+v"(xb[sl].x),
                  "+v"(xb[sl].y), "+v"(xb[sl].z), "+v"(xb[sl].w), "+v"(xw[sl].x), "+v"(xw[sl].y), "+v"(xw[sl].z),
                  "+v"(xw[sl].w));
@@ -824,6 +832,11 @@ __global__ __launch_bounds__(256, 1) void deepfm_rows_k(RArgs a) {
       if (jp + 1 < 4) wread(jp + 1, (jp + 1) & 1);
       __builtin_amdgcn_sched_barrier(0);
       const int b = jp & 1;
+      if (ABL & 4) {
+        asm volatile("" :: "v"(al[b][0]), "v"(ah[b][0]), "v"(al[b][1]), "v"(ah[b][1]), "v"(bh), "v"(bl));
+        __builtin_amdgcn_sched_barrier(0);
+        continue;
+      }
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int j = 2 * jp + q;
@@ -834,68 +847,313 @@ __global__ __launch_bounds__(256, 1) void deepfm_rows_k(RArgs a) {
       __builtin_amdgcn_sched_barrier(0);
     }
   }
-  // ---- layer 2 in two halves of n2 (64 outputs each, so the accumulators, the next k-step's W2
-  // prefetch and the layer-1 accumulators fit 256 registers): B fragments of k-step t = 2j + g2
-  // from acc[j] (deepfm_fused_k order), rebuilt per half
+  // ---- layer 2 in two halves of n2 (64 outputs each: the half's accumulators, the layer-1
+  // accumulators and a 6-deep W2 prefetch ring fit the registers the layer-1 rings leave free).
+  // The 32 (half, k-step) steps are one flat unrolled sequence, so the ring runs across the
+  // halves; B fragments of k-step t = 2j + g2 from acc[j] (deepfm_fused_k order), rebuilt per
+  // half. b1 / b2 / w_o come from LDS: a global load here would wait out the W2 prefetch.
   float dot = 0.0f;
+  if (ABL & 8) {
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    f32x16 acc2[2];
+    for (int j = 0; j < 8; ++j) asm volatile("" :: "v"(acc[j]));
+  }
+  constexpr int P = 6, NS = 32;
+  bf16x8 w2h[P + 1][2], w2l[P + 1][2];
+  auto w2load = [&](int st) {
+    const int half = st >> 4, t = st & 15, b = st % (P + 1);
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
+    for (int q = 0; q < 2; ++q) {
+      const int o = ((t * kN2 + 32 * (2 * half + q) + c) * 2 + h) * 8;
+      w2h[b][q] = *reinterpret_cast<const bf16x8*>(a.w2hi + o);
+      w2l[b][q] = *reinterpret_cast<const bf16x8*>(a.w2lo + o);
+    }
+  };
+  if (!(ABL & 8)) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc2[q][r] = 0.0f;
-    bf16x8 w2h[2][2], w2l[2][2];
-    auto w2load = [&](int t, int b) {
+    for (int st = 0; st < P; ++st) w2load(st);
+  }
+  f32x16 acc2[2];
+#pragma unroll
+  for (int st = 0; st < (ABL & 8 ? 0 : NS); ++st) {
+    const int half = st >> 4, t = st & 15, j = t >> 1, g2 = t & 1, b = st % (P + 1);
+    if (t == 0) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc2[q][r] = 0.0f;
+    }
+    if (st + P < NS) w2load(st + P);
+    __builtin_amdgcn_sched_barrier(0);
+    bf16x8 gh, gl;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const float4 bb = *reinterpret_cast<const float4*>(b1s + 16 * t + 8 * p + 4 * h);
+      const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = acc[j][4 * (2 * g2 + p) + e] + bv[e];
+        v = v > 0.0f ? v : 0.0f;
+        const __bf16 hv = (__bf16)v;
+        gh[4 * p + e] = hv;
+        gl[4 * p + e] = (__bf16)(v - (float)hv);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const bf16x8 ah = w2h[b][q], al = w2l[b][q];
+      acc2[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, gh, acc2[q], 0, 0, 0);
+      acc2[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, gl, acc2[q], 0, 0, 0);
+      acc2[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, gh, acc2[q], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (t == 15) {  // relu(H2 + b2) . wo over this half's 64 outputs
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int nb = 32 * (2 * half + q) + 8 * g + 4 * h;
+          const float4 bb = *reinterpret_cast<const float4*>(b2s + nb);
+          const float4 ww = *reinterpret_cast<const float4*>(wos + nb);
+          dot += fmaxf(acc2[q][4 * g + 0] + bb.x, 0.0f) * ww.x;
+          dot += fmaxf(acc2[q][4 * g + 1] + bb.y, 0.0f) * ww.y;
+          dot += fmaxf(acc2[q][4 * g + 2] + bb.z, 0.0f) * ww.z;
+          dot += fmaxf(acc2[q][4 * g + 3] + bb.w, 0.0f) * ww.w;
+        }
+    }
+  }
+  float fm = -fq;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) fm += fs[k] * fs[k];
+  dot += __shfl_xor(dot, 32, 64);
+  fm += __shfl_xor(fm, 32, 64);
+  const float first = fw + __shfl_xor(fw, 32, 64);
+  const int64_t row = m0 + c;
+  if (h == 0 && row < a.R) {
+    const float v = a.bias + first + 0.5f * fm + dot;
+    a.logit[row] = v;
+    if (a.prob) a.prob[row] = 1.0f / (1.0f + expf(-v));
+  }
+}
+
+// deepfm_rows_k with W1 staged by a fifth wave through LDS-DMA instead of the compute waves'
+// register ring + ds_write (timing ablations: the per-field W1 writes and barrier were half of the
+// kernel with L2-resident gathers): the compute waves' only global loads are their gathers.
+// 320 threads (the stager shares a SIMD): 256 registers per wave, so R = 5 and a 3-deep W2 ring.
+template <int F>
+__global__ __launch_bounds__(320, 1) void deepfm_rows5_k(RArgs a) {
+  constexpr int R = 4, NB = R + 1, ABL = 0;
+  __shared__ __attribute__((aligned(16))) __bf16 w1s[3][kW1Field];
+  __shared__ int ids_s[4][32 * F];
+  // b1 / b2 / w_o via LDS: a global load in layer 2 would wait out its W2 prefetch
+  __shared__ __attribute__((aligned(16))) float b1s[kN1], b2s[kN2], wos[kN2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c = lane & 31, h = lane >> 5;
+  if (tid < kN1) b1s[tid] = a.b1[tid];  // visible after barrier 0
+  if (tid < kN2) b2s[tid] = a.b2[tid];
+  else if (tid < kN1) wos[tid - kN2] = a.wo[tid - kN2];
+  if (wave == 4) {
+    // ---- W1 stager: field f + 2 into slot (f + 2) % 3 after barrier f (its previous field,
+    // f - 1, was finished by every compute wave before barrier f); a counted vmcnt retires field
+    // f + 1's 16 pieces before barrier f + 1; raw s_barrier (__syncthreads() would drain the DMA)
+    const char* w1b = reinterpret_cast<const char*>(a.w1);
+    auto dma = [&](int f) {
+      char* dst = reinterpret_cast<char*>(w1s[f % 3]);
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(w1b + (int64_t)f * (kW1Field * 2) + 1024 * k + 16 * lane),
+            (__attribute__((address_space(3))) void*)(dst + 1024 * k), 16, 0, 0);
+    };
+    dma(0);
+    dma(1);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // field 0 landed
+    __builtin_amdgcn_s_barrier();                      // barrier 0
+#pragma unroll
+    for (int f = 0; f + 1 < F; ++f) {
+      if (f + 2 < F) {
+        dma(f + 2);
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // field f + 1 landed
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();  // barrier f + 1
+    }
+    return;
+  }
+  int* my_ids = ids_s[wave];
+  const int64_t m0 = ((int64_t)blockIdx.x * 4 + wave) * 32;  // this wave's 32 rows
+
+  // ---- ids of the 32 rows -> LDS (int32); rows past R re-read the last row, never stored
+  {
+    const int64_t last = a.R - 1;
+    constexpr int NT = (32 * F + 63) / 64;
+    int64_t v[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int e = lane + 64 * t;
+      const int row = e / F, f = e - row * F;
+      const int64_t gr = m0 + row <= last ? m0 + row : last;
+      v[t] = e < 32 * F ? a.x[gr * F + f] : 0;
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      if (lane + 64 * t < 32 * F) my_ids[lane + 64 * t] = (int)v[t];
+  }
+  // ---- layer 1 over the fields: the gathers of fields f+1..f+R and this wave's quarter of
+  // their W1 images in flight (one register ring: both are waited for at the same depth, so the
+  // in-order vmcnt never waits on a younger field)
+  float4 xa[NB], xb[NB], xw[NB];
+  f32x16 acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
+  float fs[8], fq = 0.0f, fw = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) fs[k] = 0.0f;
+  auto issue = [&](int f, int sl) {
+    const int id = my_ids[c * F + f];
+    const float4* line = reinterpret_cast<const float4*>(a.P[f] + (int64_t)id * 32);
+    xa[sl] = line[h];
+    xb[sl] = line[2 + h];
+    xw[sl] = line[4 + h];
+  };
+#pragma unroll
+  for (int f = 0; f < R; ++f) issue(f, f);
+#pragma unroll
+  for (int f = 0; f < F; ++f) {
+    const int sl = f % NB;
+    if (f + R < F) issue(f + R, (f + R) % NB);
+    __builtin_amdgcn_sched_barrier(0);
+    // field f's registers "redefined" here: left alone, hipcc consumes each field's loads right
+    // after issuing them (fewer live registers) and so waits on them at once
+    __syncthreads();  // barrier f: slot f % 3 holds field f (plain global loads survive it)
+    asm volatile("" : "+v"(xa[sl].x), "+v"(xa[sl].y), "+v"(xa[sl].z), "+v"(xa[sl].w), "+v"(xb[sl].x),
+                 "+v"(xb[sl].y), "+v"(xb[sl].z), "+v"(xb[sl].w), "+v"(xw[sl].x), "+v"(xw[sl].y), "+v"(xw[sl].z),
+                 "+v"(xw[sl].w));
+    const __bf16* ws = w1s[f % 3];
+    // W1 fragments of n-tile pair jp + 1 read while pair jp's MFMAs run; pair 0's reads are
+    // issued before the split, whose VALU then covers their latency
+    bf16x8 ah[2][2], al[2][2];
+    auto wread = [&](int jp, int b) {
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        const int o = ((t * kN2 + 32 * (2 * half + q) + c) * 2 + h) * 8;
-        w2h[b][q] = *reinterpret_cast<const bf16x8*>(a.w2hi + o);
-        w2l[b][q] = *reinterpret_cast<const bf16x8*>(a.w2lo + o);
+        const int n = 32 * (2 * jp + q) + c;
+        ah[b][q] = *reinterpret_cast<const bf16x8*>(ws + w1_idx(n, 8 * h));
+        al[b][q] = *reinterpret_cast<const bf16x8*>(ws + 4096 + w1_idx(n, 8 * h));
       }
     };
-    w2load(0, 0);
+    wread(0, 0);
+    bf16x8 bh, bl;
+    {
+      const float4 p = xa[sl], q = xb[sl], w = xw[sl];
+      const float v[8] = {p.x, p.y, p.z, p.w, q.x, q.y, q.z, q.w};
 #pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const int j = t >> 1, g2 = t & 1;
-      if (t + 1 < 16) w2load(t + 1, (t + 1) & 1);
+      for (int k = 0; k < 8; ++k) {
+        fs[k] += v[k];
+        fq += v[k] * v[k];
+        const __bf16 hv = (__bf16)v[k];
+        bh[k] = hv;
+        bl[k] = (__bf16)(v[k] - (float)hv);
+      }
+      // bytes 64..95 of the line: W then zeros (deepfm_pack_k), so the whole 16-B piece sums
+      // to W on h = 0 and to 0 on h = 1 (all four components used: a dword load of the same
+      // line runs at 38 G lines/s in the probe, a 16-B piece at 48 G)
+      fw += (w.x + w.y) + (w.z + w.w);
+    }
+#pragma unroll
+    for (int jp = 0; jp < 4; ++jp) {
+      if (jp + 1 < 4) wread(jp + 1, (jp + 1) & 1);
       __builtin_amdgcn_sched_barrier(0);
-      bf16x8 gh, gl;
-#pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        const float4 bb = *reinterpret_cast<const float4*>(b1s + 16 * t + 8 * p + 4 * h);
-        const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float v = acc[j][4 * (2 * g2 + p) + e] + bv[e];
-          v = v > 0.0f ? v : 0.0f;
-          const __bf16 hv = (__bf16)v;
-          gh[4 * p + e] = hv;
-          gl[4 * p + e] = (__bf16)(v - (float)hv);
-        }
+      const int b = jp & 1;
+      if (ABL & 4) {
+        asm volatile("" :: "v"(al[b][0]), "v"(ah[b][0]), "v"(al[b][1]), "v"(ah[b][1]), "v"(bh), "v"(bl));
+        __builtin_amdgcn_sched_barrier(0);
+        continue;
       }
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        const bf16x8 ah = w2h[t & 1][q], al = w2l[t & 1][q];
-        acc2[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, gh, acc2[q], 0, 0, 0);
-        acc2[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, gl, acc2[q], 0, 0, 0);
-        acc2[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, gh, acc2[q], 0, 0, 0);
+        const int j = 2 * jp + q;
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[b][q], bh, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[b][q], bl, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[b][q], bh, acc[j], 0, 0, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    // relu(H2 + b2) . wo over this half's 64 outputs
+  }
+  // ---- layer 2 in two halves of n2 (64 outputs each: the half's accumulators, the layer-1
+  // accumulators and a 6-deep W2 prefetch ring fit the registers the layer-1 rings leave free).
+  // The 32 (half, k-step) steps are one flat unrolled sequence, so the ring runs across the
+  // halves; B fragments of k-step t = 2j + g2 from acc[j] (deepfm_fused_k order), rebuilt per
+  // half. b1 / b2 / w_o come from LDS: a global load here would wait out the W2 prefetch.
+  float dot = 0.0f;
+  if (ABL & 8) {
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
+    for (int j = 0; j < 8; ++j) asm volatile("" :: "v"(acc[j]));
+  }
+  constexpr int P = 3, NS = 32;
+  bf16x8 w2h[P + 1][2], w2l[P + 1][2];
+  auto w2load = [&](int st) {
+    const int half = st >> 4, t = st & 15, b = st % (P + 1);
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int nb = 32 * (2 * half + q) + 8 * g + 4 * h;
-        const float4 bb = *reinterpret_cast<const float4*>(a.b2 + nb);
-        const float4 ww = *reinterpret_cast<const float4*>(a.wo + nb);
-        dot += fmaxf(acc2[q][4 * g + 0] + bb.x, 0.0f) * ww.x;
-        dot += fmaxf(acc2[q][4 * g + 1] + bb.y, 0.0f) * ww.y;
-        dot += fmaxf(acc2[q][4 * g + 2] + bb.z, 0.0f) * ww.z;
-        dot += fmaxf(acc2[q][4 * g + 3] + bb.w, 0.0f) * ww.w;
+    for (int q = 0; q < 2; ++q) {
+      const int o = ((t * kN2 + 32 * (2 * half + q) + c) * 2 + h) * 8;
+      w2h[b][q] = *reinterpret_cast<const bf16x8*>(a.w2hi + o);
+      w2l[b][q] = *reinterpret_cast<const bf16x8*>(a.w2lo + o);
+    }
+  };
+  if (!(ABL & 8)) {
+#pragma unroll
+    for (int st = 0; st < P; ++st) w2load(st);
+  }
+  f32x16 acc2[2];
+#pragma unroll
+  for (int st = 0; st < (ABL & 8 ? 0 : NS); ++st) {
+    const int half = st >> 4, t = st & 15, j = t >> 1, g2 = t & 1, b = st % (P + 1);
+    if (t == 0) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc2[q][r] = 0.0f;
+    }
+    if (st + P < NS) w2load(st + P);
+    __builtin_amdgcn_sched_barrier(0);
+    bf16x8 gh, gl;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const float4 bb = *reinterpret_cast<const float4*>(b1s + 16 * t + 8 * p + 4 * h);
+      const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = acc[j][4 * (2 * g2 + p) + e] + bv[e];
+        v = v > 0.0f ? v : 0.0f;
+        const __bf16 hv = (__bf16)v;
+        gh[4 * p + e] = hv;
+        gl[4 * p + e] = (__bf16)(v - (float)hv);
       }
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const bf16x8 ah = w2h[b][q], al = w2l[b][q];
+      acc2[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, gh, acc2[q], 0, 0, 0);
+      acc2[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, gl, acc2[q], 0, 0, 0);
+      acc2[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, gh, acc2[q], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (t == 15) {  // relu(H2 + b2) . wo over this half's 64 outputs
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int nb = 32 * (2 * half + q) + 8 * g + 4 * h;
+          const float4 bb = *reinterpret_cast<const float4*>(b2s + nb);
+          const float4 ww = *reinterpret_cast<const float4*>(wos + nb);
+          dot += fmaxf(acc2[q][4 * g + 0] + bb.x, 0.0f) * ww.x;
+          dot += fmaxf(acc2[q][4 * g + 1] + bb.y, 0.0f) * ww.y;
+          dot += fmaxf(acc2[q][4 * g + 2] + bb.z, 0.0f) * ww.z;
+          dot += fmaxf(acc2[q][4 * g + 3] + bb.w, 0.0f) * ww.w;
+        }
+    }
   }
   float fm = -fq;
 #pragma unroll
@@ -1021,7 +1279,26 @@ RSX_API int rsx_deepfm_fused_run(const int64_t* x, int64_t R, int F, const float
     r.w2hi = wsb + m1;
     r.w2lo = wsb + m1 + n2;
     r.b1 = b1; r.b2 = b2; r.wo = wo; r.logit = logit; r.prob = prob;
-    hipLaunchKernelGGL(deepfm_rows_k<kRowsF>, dim3((unsigned)grid), dim3(256), 0, st, r);
+    static const bool v4 = [] {
+      const char* e = getenv("RSX_DEEPFM_ROWS");
+      return e && e[0] == '4';
+    }();
+    if (!v4) {
+      hipLaunchKernelGGL(deepfm_rows5_k<kRowsF>, dim3((unsigned)grid), dim3(320), 0, st, r);
+      RSX_LAUNCHED();
+      return 0;
+    }
+    const char* abl_env = getenv("RSX_DEEPFM_ABL");  // timing ablations (diagnostic only)
+    const int abl = abl_env ? atoi(abl_env) : 0;
+    switch (abl) {
+      case 1: hipLaunchKernelGGL((deepfm_rows_k<kRowsF, 1>), dim3((unsigned)grid), dim3(256), 0, st, r); break;
+      case 3: hipLaunchKernelGGL((deepfm_rows_k<kRowsF, 3>), dim3((unsigned)grid), dim3(256), 0, st, r); break;
+      case 4: hipLaunchKernelGGL((deepfm_rows_k<kRowsF, 4>), dim3((unsigned)grid), dim3(256), 0, st, r); break;
+      case 8: hipLaunchKernelGGL((deepfm_rows_k<kRowsF, 8>), dim3((unsigned)grid), dim3(256), 0, st, r); break;
+      case 12: hipLaunchKernelGGL((deepfm_rows_k<kRowsF, 12>), dim3((unsigned)grid), dim3(256), 0, st, r); break;
+      case 15: hipLaunchKernelGGL((deepfm_rows_k<kRowsF, 15>), dim3((unsigned)grid), dim3(256), 0, st, r); break;
+      default: hipLaunchKernelGGL((deepfm_rows_k<kRowsF, 0>), dim3((unsigned)grid), dim3(256), 0, st, r); break;
+    }
     RSX_LAUNCHED();
     return 0;
   }

@@ -1243,6 +1243,245 @@ __global__ __launch_bounds__(256) void mha_bwd_x3p_k(BwdArgs a) {
   }
 }
 
+
+// ---- fused in-projection + attention forward (head dim 32, bf16x3) -------------------------
+// The user tower's `qkv = in_proj(h); mha(qkv)` (v1_refine_usertower.py:343-352 through
+// nn.TransformerEncoderLayer's self_attn) as ONE kernel: each wave (sequence, head) computes its
+// head's Q, K and V for all of the sequence's 16-token blocks from the LayerNorm output h and
+// in_proj_weight / in_proj_bias, then runs mha_fwd_x3b_seq's masked safe-softmax attention on them
+// straight from registers (no qkv round trip through HBM before the attention). The projections
+// are bf16x3 16x16x32 MFMAs (K = D in 32-wide k-steps) whose outputs land in exactly the attention's
+// operand layouts:
+//   Q^T, K^T tiles  A = W rows (dim), B = h rows (token): lane (c, g) register r holds dim
+//                   16 dt + 4g + r of token c — the Row8 operand of the score MFMA with the head
+//                   dims permuted ({4g..4g+3} U {16+4g..16+4g+3} on lane group g, the same
+//                   permutation for Q and K, so S is unchanged);
+//   V tiles         A = h rows, B = W rows: lane (c, g) register r holds token 4g + r, dim c —
+//                   the Col4 operand of P V.
+// qkv is still written (the attention backward, mha_bwd_x3p_k, and the in_proj weight gradient
+// read it), with float4 stores for Q / K; the saving is the attention's qkv read and one launch.
+struct QArgs {
+  const float* x;        // [T, D] in_proj input
+  const float* w;        // [3D, D] in_proj_weight
+  const float* bias;     // [3D] or nullptr
+  const uint8_t* kpad;
+  const int* seg;
+  float* qkv;            // [T, 3D] (for the backward) or nullptr
+  float* out;            // [T, D]
+  float* lse;            // [T, H] or nullptr
+  int B, L, H, causal;
+  float scale;
+  rsx::Dropout drop;
+};
+
+__device__ __forceinline__ f32x4 dot16_x3_acc(const Row8& a, const Row8& b, f32x4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.lo, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.lo, b.hi, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.hi, acc, 0, 0, 0);
+  return acc;
+}
+
+__device__ __forceinline__ Row8 split_f8(const float (&f)[8]) {
+  Row8 r;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const __bf16 h = (__bf16)f[k];
+    r.hi[k] = h;
+    r.lo[k] = (__bf16)(f[k] - (float)h);
+  }
+  return r;
+}
+
+template <int NB, int KS>
+__device__ __forceinline__ void mha_qkv_fwd_x3_seq(const QArgs& a, int hd, int64_t tok0, int L, int lane) {
+  constexpr int DH = 32, D = 32 * KS;
+  const int c = lane & 15, g = lane >> 4;
+  const int H = a.H;
+  // h rows of the sequence through one buffer resource (rows >= L read as zero)
+  const uintptr_t bp = (uintptr_t)(a.x + tok0 * D);
+  const unsigned blo = __builtin_amdgcn_readfirstlane((unsigned)bp), bhi = __builtin_amdgcn_readfirstlane((unsigned)(bp >> 32));
+  const unsigned nbytes = __builtin_amdgcn_readfirstlane((unsigned)(L * D * 4));
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(((uintptr_t)bhi << 32) | blo), 0, (int)nbytes, 0x00020000);
+  u32x4b xr[KS][NB][2];
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb) {
+      const unsigned o = (unsigned)(((16 * bb + c) * D + 32 * s + 8 * g) * 4);
+      xr[s][bb][0] = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0);
+      xr[s][bb][1] = __builtin_amdgcn_raw_buffer_load_b128(rs, o + 16, 0, 0);
+    }
+  // projections: q/k/v accumulators of block bb, 16-dim tile dt
+  f32x4 qa[NB][2], ka[NB][2], va[NB][2];
+#pragma unroll
+  for (int bb = 0; bb < NB; ++bb)
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      qa[bb][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      ka[bb][dt] = qa[bb][dt];
+      va[bb][dt] = qa[bb][dt];
+    }
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    Row8 wf[3][2];  // [q|k|v][dt]: row 16 dt + c of the head's part, k-step s
+#pragma unroll
+    for (int pt = 0; pt < 3; ++pt)
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const float4* p = reinterpret_cast<const float4*>(a.w + (int64_t)(pt * D + hd * DH + 16 * dt + c) * D + 32 * s + 8 * g);
+        const float4 v0 = p[0], v1 = p[1];
+        const float f[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        wf[pt][dt] = split_f8(f);
+      }
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb) {
+      const Row8 xx = split_row8(xr[s][bb][0], xr[s][bb][1]);
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        qa[bb][dt] = dot16_x3_acc(wf[0][dt], xx, qa[bb][dt]);  // [dim 4g+r][token c]
+        ka[bb][dt] = dot16_x3_acc(wf[1][dt], xx, ka[bb][dt]);
+        va[bb][dt] = dot16_x3_acc(xx, wf[2][dt], va[bb][dt]);  // [token 4g+r][dim c]
+      }
+    }
+  }
+  // + bias; Q / K / V values of the attention operands; qkv for the backward
+  float bq[2][4], bk[2][4], bv[2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      bq[dt][r] = a.bias ? a.bias[hd * DH + 16 * dt + 4 * g + r] : 0.0f;
+      bk[dt][r] = a.bias ? a.bias[D + hd * DH + 16 * dt + 4 * g + r] : 0.0f;
+    }
+    bv[dt] = a.bias ? a.bias[2 * D + hd * DH + 16 * dt + c] : 0.0f;
+  }
+  Row8 kx[NB], qxs[NB];
+  Col4 vc[NB][2];
+#pragma unroll
+  for (int bb = 0; bb < NB; ++bb) {
+    float qf[8], kf[8];
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        qf[4 * dt + r] = qa[bb][dt][r] + bq[dt][r];
+        kf[4 * dt + r] = ka[bb][dt][r] + bk[dt][r];
+      }
+    qxs[bb] = split_f8(qf);
+    kx[bb] = split_f8(kf);
+    float vf[2][4];
+#pragma unroll
+    for (int et = 0; et < 2; ++et)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) vf[et][t] = va[bb][et][t] + bv[et];
+    vc[bb][0] = split4(vf[0]);
+    vc[bb][1] = split4(vf[1]);
+    if (a.qkv) {
+      const int64_t D3 = 3 * (int64_t)D;
+      const int tq = 16 * bb + c;
+      if (tq < L) {
+        float* qrow = a.qkv + (tok0 + tq) * D3 + hd * DH + 4 * g;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          *reinterpret_cast<float4*>(qrow + 16 * dt) = make_float4(qf[4 * dt], qf[4 * dt + 1], qf[4 * dt + 2], qf[4 * dt + 3]);
+          *reinterpret_cast<float4*>(qrow + D + 16 * dt) =
+              make_float4(kf[4 * dt], kf[4 * dt + 1], kf[4 * dt + 2], kf[4 * dt + 3]);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int tv = 16 * bb + 4 * g + t;
+        if (tv < L) {
+#pragma unroll
+          for (int et = 0; et < 2; ++et) a.qkv[(tok0 + tv) * D3 + 2 * D + hd * DH + 16 * et + c] = vf[et][t];
+        }
+      }
+    }
+  }
+  // ---- attention (mha_fwd_x3b_seq's masks, safe softmax, dropout hash, lse)
+  const int my_pad = (lane < L) ? (a.kpad ? (int)a.kpad[tok0 + lane] : 0) : 1;
+  float* Ob = a.out + tok0 * D + hd * DH;
+#pragma unroll
+  for (int qb = 0; qb < NB; ++qb) {
+    const int i = 16 * qb + c;
+    const bool iok = i < L;
+    const int kb_end = a.causal ? qb : NB - 1;
+    f32x4 sv[NB];
+    float m = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < NB; ++kb) {
+      if (kb <= kb_end) {
+        sv[kb] = dot16_x3(kx[kb], qxs[qb]);  // S^T: [key 16kb+4g+r][query i]
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int j = 16 * kb + 4 * g + r;
+          const int jpad = __shfl(my_pad, j & 63, 64);
+          const bool allowed = iok && j < L && !jpad && (!a.causal || j <= i);
+          sv[kb][r] = allowed ? sv[kb][r] * a.scale : -INFINITY;
+          m = fmaxf(m, sv[kb][r]);
+        }
+      }
+    }
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float l = 0.0f;
+#pragma unroll
+    for (int kb = 0; kb < NB; ++kb) {
+      if (kb <= kb_end) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = (sv[kb][r] == -INFINITY) ? 0.0f : __expf(sv[kb][r] - m);
+          sv[kb][r] = pv;
+          l += pv;
+        }
+      }
+    }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = (l > 0.0f) ? 1.0f / l : 0.0f;
+    f32x4 o[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    const uint64_t rowidx = ((uint64_t)(tok0 + i) * H + hd) * kLMax;
+#pragma unroll
+    for (int kb = 0; kb < NB; ++kb) {
+      if (kb <= kb_end) {
+        float pr[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pr[r] = a.drop.apply(sv[kb][r] * inv, rowidx + 16 * kb + 4 * g + r);
+        const Col4 pa = split4(pr);
+#pragma unroll
+        for (int et = 0; et < 2; ++et) o[et] = sum16_x3(pa, vc[kb][et], o[et]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * qb + 4 * g + r;
+      if (row < L) {
+        Ob[(int64_t)row * D + c] = o[0][r];
+        Ob[(int64_t)row * D + 16 + c] = o[1][r];
+      }
+    }
+    if (a.lse && g == 0 && iok) a.lse[(tok0 + i) * H + hd] = (l > 0.0f) ? m + logf(l) : -INFINITY;
+  }
+}
+
+template <int KS>
+__global__ __launch_bounds__(256) void mha_qkv_fwd_x3_k(QArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t unit = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (unit >= (int64_t)a.B * a.H) return;  // whole wave exits together
+  const int b = (int)(unit / a.H), hd = (int)(unit % a.H);
+  const int64_t tok0 = a.seg ? (int64_t)a.seg[b] : (int64_t)b * a.L;
+  int L = a.seg ? (a.seg[b + 1] - a.seg[b]) : a.L;
+  if (L > kLMax) L = kLMax;
+  if (L <= 0) return;
+  const int nb = __builtin_amdgcn_readfirstlane((L + 15) >> 4);
+  if (nb == 1) mha_qkv_fwd_x3_seq<1, KS>(a, hd, tok0, L, lane);
+  else if (nb == 2) mha_qkv_fwd_x3_seq<2, KS>(a, hd, tok0, L, lane);
+  else if (nb == 3) mha_qkv_fwd_x3_seq<3, KS>(a, hd, tok0, L, lane);
+  else mha_qkv_fwd_x3_seq<4, KS>(a, hd, tok0, L, lane);
+}
+
 }  // namespace
 
 RSX_API int rsx_mha_fwd(const float* qkv, const uint8_t* key_pad, const int* seg_off, int64_t B, int64_t L,
@@ -1310,6 +1549,27 @@ RSX_API int rsx_mha_fwd_x3(const float* qkv, const uint8_t* key_pad, const int* 
     hipLaunchKernelGGL(mha_fwd_x3_k, dim3((unsigned)((B * H + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a);
   else
     hipLaunchKernelGGL(mha_fwd_x3b_k, dim3((unsigned)((B * H + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a);
+  RSX_LAUNCHED();
+  return 0;
+}
+
+// Fused in_proj + attention forward (head dim 32, model width D = 32 H in {128}): see
+// mha_qkv_fwd_x3_k. x [T, D], w [3D, D] (torch in_proj_weight), bias [3D] or null; qkv [T, 3D]
+// written when non-null (what rsx_mha_bwd_x3 and the in_proj gradient read).
+RSX_API int rsx_mha_qkv_fwd_x3(const float* x, const float* w, const float* bias, const uint8_t* key_pad,
+                               const int* seg_off, int64_t B, int64_t L, int64_t H, int causal, float p_drop,
+                               uint64_t seed, float* qkv, float* out, float* lse, void* stream) {
+  RSX_ARG(x && w && out, "null tensor");
+  RSX_ARG(L >= 1 && L <= kLMax, "L must be in [1,64]");
+  RSX_ARG(H == 4, "fused in_proj + attention: D = 128 (4 heads of 32)");
+  RSX_ARG(p_drop >= 0.0f && p_drop < 1.0f, "p_drop must be in [0,1)");
+  if (B == 0) return 0;
+  QArgs a;
+  a.x = x; a.w = w; a.bias = bias; a.kpad = key_pad; a.seg = seg_off; a.qkv = qkv; a.out = out; a.lse = lse;
+  a.B = (int)B; a.L = (int)L; a.H = (int)H; a.causal = causal;
+  a.scale = 1.0f / sqrtf(32.0f);
+  a.drop = rsx::make_dropout(p_drop, seed);
+  hipLaunchKernelGGL(mha_qkv_fwd_x3_k<4>, dim3((unsigned)((B * H + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a);
   RSX_LAUNCHED();
   return 0;
 }

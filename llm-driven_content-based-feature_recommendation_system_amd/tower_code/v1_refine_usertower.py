@@ -65,8 +65,8 @@ def encoder_stack(layers, x, key_pad, p, training, causal=True, seg_off=None):
         h = ops.layer_norm(x, layers[0].norm1.weight, layers[0].norm1.bias, layers[0].norm1.eps)
     for i, layer in enumerate(layers):
         sa = layer.self_attn
-        qkv = ops.linear_tok(h, sa.in_proj_weight, sa.in_proj_bias)
-        a = ops.mha(qkv, key_pad, sa.num_heads, causal=causal, p_drop=p, seg_off=seg_off)
+        a = ops.qkv_mha(h, sa.in_proj_weight, sa.in_proj_bias, key_pad, sa.num_heads, causal=causal, p_drop=p,
+                        seg_off=seg_off)
         a = ops.linear_tok(a, sa.out_proj.weight, sa.out_proj.bias)
         x, h = ops.add_layer_norm(x, a, layer.norm2.weight, layer.norm2.bias, layer.norm2.eps, p)
         f = ops.ffn(h, layer.linear1.weight, layer.linear1.bias, layer.linear2.weight, layer.linear2.bias, p,

@@ -787,3 +787,52 @@ def test_profile_linear_matches_concat_linear(gpu, users, n):
     for a, r in zip(*outs):
         a = a.double().cpu()
         assert (a - r).abs().max().item() <= 2e-4 + 2e-5 * r.abs().max().item()
+
+
+# ------------------------------------------------------------------ fused in_proj + attention
+@pytest.mark.parametrize("packed,causal,use_pad,p_drop", [(True, True, True, 0.0), (False, True, True, 0.0),
+                                                          (False, False, False, 0.0), (True, True, True, 0.2)])
+def test_qkv_mha_fused_matches_two_op_path(gpu, packed, causal, use_pad, p_drop):
+    """rsx_mha_qkv_fwd_x3 (in_proj fused into the attention forward) against linear_tok + mha on
+    the same inputs and dropout seed: attention output, the qkv it writes for the backward, and
+    dx / dW / db through the shared backward (atol 2e-5: the two paths sum the projection's k
+    products in different orders). Packed segments of 1..64 tokens or dense L = 50 with left
+    padding, as the user tower runs them."""
+    g = torch.Generator().manual_seed(31 + int(packed) + 2 * int(causal) + int(10 * p_drop))
+    D, H = 128, 4
+    if packed:
+        lens = torch.randint(1, 65, (61,), generator=g)
+        seg = torch.cat([torch.zeros(1, dtype=torch.long), torch.cumsum(lens, 0)])
+        T = int(seg[-1])
+        x = torch.randn(T, D, generator=g)
+        pad = torch.zeros(T, dtype=torch.bool)
+        pad[seg[1:] - 1] = torch.rand(len(lens), generator=g) < 0.3
+        seg_d = seg.to(gpu)
+    else:
+        B, L = 23, 50
+        x = torch.randn(B, L, D, generator=g)
+        cnt = torch.randint(1, L + 1, (B,), generator=g)
+        pad = torch.arange(L)[None, :] < (L - cnt)[:, None]  # left padding
+        seg_d = None
+    w = torch.randn(3 * D, D, generator=g) * D ** -0.5
+    b = torch.randn(3 * D, generator=g) * 0.1
+    dout = torch.randn(x.shape, generator=g)
+    kp = pad.to(gpu) if use_pad else None
+    seed = 1234
+    res = []
+    for fused in (True, False):
+        xd = x.to(gpu).requires_grad_()
+        wd = w.to(gpu).requires_grad_()
+        bd = b.to(gpu).requires_grad_()
+        if fused:
+            out = ops._QKVMHA.apply(xd, wd, bd, kp, None if seg_d is None else seg_d.to(torch.int32).contiguous(), H,
+                                    causal, p_drop, seed)
+        else:
+            qkv = ops.linear_tok(xd, wd, bd)
+            out = ops._MHA.apply(qkv, kp, None if seg_d is None else seg_d.to(torch.int32).contiguous(), H, causal,
+                                 p_drop, seed)
+        (out * dout.to(gpu)).sum().backward()
+        res.append((out.detach().cpu(), xd.grad.cpu(), wd.grad.cpu(), bd.grad.cpu()))
+    for name, a, r in zip(["out", "dx", "dw", "db"], res[0], res[1]):
+        tol = 2e-5 * max(1.0, r.abs().max().item())
+        torch.testing.assert_close(a, r, atol=tol, rtol=1e-4, msg=lambda m, name=name: f"{name}: {m}")
