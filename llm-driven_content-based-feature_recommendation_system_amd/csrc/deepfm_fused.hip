@@ -696,6 +696,8 @@ constexpr int kW1Field = 8192;      // bf16 per field image: hi [256][16] then l
 struct RArgs {
   const int64_t* x;          // [R, F]
   const float* P[kMaxF];     // packed [vocab][32]: V[16], W, pad
+  const float* V[kMaxF];     // unpacked form (deepfm_rows5_k<F, false>): V [vocab][16], W [vocab] or null
+  const float* W[kMaxF];
   int64_t R;
   int64_t nit;               // task rounds (4 tasks of 64 rows per workgroup per round)
   float bias;
@@ -939,7 +941,9 @@ __global__ __launch_bounds__(256, 1) void deepfm_rows_k(RArgs a) {
 // register ring + ds_write (timing ablations: the per-field W1 writes and barrier were half of the
 // kernel with L2-resident gathers): the compute waves' only global loads are their gathers.
 // 320 threads (the stager shares a SIMD): 256 registers per wave, so R = 5 and a 3-deep W2 ring.
-template <int F>
+// PK = false: the tables as given (V row: two 16-B pieces of its 64 B; W: one dword), for callers
+// without the packed images (rsx_deepfm_fused, or no table cache).
+template <int F, bool PK = true>
 __global__ __launch_bounds__(320, 1) void deepfm_rows5_k(RArgs a) {
   constexpr int R = 4, NB = R + 1, ABL = 0;
   __shared__ __attribute__((aligned(16))) __bf16 w1s[3][kW1Field];
@@ -1013,10 +1017,18 @@ __global__ __launch_bounds__(320, 1) void deepfm_rows5_k(RArgs a) {
   for (int k = 0; k < 8; ++k) fs[k] = 0.0f;
   auto issue = [&](int f, int sl) {
     const int id = my_ids[c * F + f];
-    const float4* line = reinterpret_cast<const float4*>(a.P[f] + (int64_t)id * 32);
-    xa[sl] = line[h];
-    xb[sl] = line[2 + h];
-    xw[sl] = line[4 + h];
+    if constexpr (PK) {
+      const float4* line = reinterpret_cast<const float4*>(a.P[f] + (int64_t)id * 32);
+      xa[sl] = line[h];
+      xb[sl] = line[2 + h];
+      xw[sl] = line[4 + h];
+    } else {
+      const float4* vr = reinterpret_cast<const float4*>(a.V[f] + (int64_t)id * 16);
+      xa[sl] = vr[h];
+      xb[sl] = vr[2 + h];
+      const float wv = (a.W[f] != nullptr && h == 0) ? a.W[f][id] : 0.0f;
+      xw[sl] = make_float4(wv, 0.0f, 0.0f, 0.0f);
+    }
   };
 #pragma unroll
   for (int f = 0; f < R; ++f) issue(f, f);
@@ -1265,11 +1277,16 @@ RSX_API int rsx_deepfm_fused_run(const int64_t* x, int64_t R, int F, const float
   for (int f = 0; f < F; ++f) RSX_ARG(V[f] != nullptr, "null field table");
   const __bf16* wsb = reinterpret_cast<const __bf16*>(ws);
   hipStream_t st = (hipStream_t)stream;
-  if (rows_ok(F) && packed) {
-    for (int f = 0; f < F; ++f) RSX_ARG(packed[f] != nullptr, "null packed table");
+  if (rows_ok(F)) {  // the weight images are in this kernel's layout (deepfm_prep_images)
+    if (packed)
+      for (int f = 0; f < F; ++f) RSX_ARG(packed[f] != nullptr, "null packed table");
     RArgs r;
     r.x = x;
-    for (int f = 0; f < kMaxF; ++f) r.P[f] = f < F ? packed[f] : nullptr;
+    for (int f = 0; f < kMaxF; ++f) {
+      r.P[f] = (f < F && packed) ? packed[f] : nullptr;
+      r.V[f] = f < F ? V[f] : nullptr;
+      r.W[f] = (f < F && W) ? W[f] : nullptr;
+    }
     r.R = R;
     const int64_t grid = (R + 127) / 128;  // 4 compute waves x 32 rows
     r.nit = 1;
@@ -1283,8 +1300,13 @@ RSX_API int rsx_deepfm_fused_run(const int64_t* x, int64_t R, int F, const float
       const char* e = getenv("RSX_DEEPFM_ROWS");
       return e && e[0] == '4';
     }();
+    if (!packed) {
+      hipLaunchKernelGGL((deepfm_rows5_k<kRowsF, false>), dim3((unsigned)grid), dim3(320), 0, st, r);
+      RSX_LAUNCHED();
+      return 0;
+    }
     if (!v4) {
-      hipLaunchKernelGGL(deepfm_rows5_k<kRowsF>, dim3((unsigned)grid), dim3(320), 0, st, r);
+      hipLaunchKernelGGL((deepfm_rows5_k<kRowsF, true>), dim3((unsigned)grid), dim3(320), 0, st, r);
       RSX_LAUNCHED();
       return 0;
     }

@@ -2212,17 +2212,63 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_fwdg_x3_k(GArgs a) {
   }
 }
 
-__global__ __launch_bounds__(256, 2) void nce_grouped_fwdg_x3p_k(GArgs a) {
+// X3Stage for a workgroup of NW waves: thread tid moves row (tid>>3)&31; NW = 4: chunks tid&7 and
+// 8+(tid&7) of both images; NW = 8: the same two chunks of image tid>>8 only.
+template <int NW>
+struct X3StageT {
+  static constexpr int kN = NW == 4 ? 4 : 2;
+  u32x4 v[kN];
+  __device__ __forceinline__ void load(const __bf16* hi, const __bf16* lo, int64_t row, bool ok, int tid) {
+    if (ok) {
+      const int64_t o = row * kD + (tid & 7) * 8;
+      if constexpr (NW == 4) {
+        v[0] = *reinterpret_cast<const u32x4*>(hi + o);
+        v[1] = *reinterpret_cast<const u32x4*>(hi + o + 64);
+        v[2] = *reinterpret_cast<const u32x4*>(lo + o);
+        v[3] = *reinterpret_cast<const u32x4*>(lo + o + 64);
+      } else {
+        const __bf16* img = (tid >> 8) ? lo : hi;
+        v[0] = *reinterpret_cast<const u32x4*>(img + o);
+        v[1] = *reinterpret_cast<const u32x4*>(img + o + 64);
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < kN; ++t) v[t] = u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+  __device__ __forceinline__ void store(X3Tile& t, int tid) const {
+    const int row = (tid >> 3) & 31, ch = tid & 7;
+    const int o0 = img_off(row, 8 * ch), o1 = img_off(row, 64 + 8 * ch);
+    if constexpr (NW == 4) {
+      *reinterpret_cast<u32x4*>(&t.hi[o0]) = v[0];
+      *reinterpret_cast<u32x4*>(&t.hi[o1]) = v[1];
+      *reinterpret_cast<u32x4*>(&t.lo[o0]) = v[2];
+      *reinterpret_cast<u32x4*>(&t.lo[o1]) = v[3];
+    } else {
+      __bf16* img = (tid >> 8) ? t.lo : t.hi;
+      *reinterpret_cast<u32x4*>(&img[o0]) = v[0];
+      *reinterpret_cast<u32x4*>(&img[o1]) = v[1];
+    }
+  }
+};
+
+// NW = waves per workgroup: 4 (two workgroups per CU) or 8 (one 256-row owner block per CU: each
+// staged tile feeds twice the rows, so the tile loads, LDS stores and L2 requests per MFMA halve).
+// NT: the split-partial rows are written with nontemporal stores (they are read once, by the
+// merge, and should not evict the streamed B images from L2).
+template <int NW, bool NT>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void nce_grouped_fwdg_x3p_k(GArgs a) {
+  constexpr int kRows = 32 * NW;
   __shared__ __attribute__((aligned(16))) X3Tile sT[3];  // ring: t-1 (deferred k-step), t, t+1
   __shared__ __attribute__((aligned(16))) float sB2[3][kTile];   // -bias_d * log2e (-inf past the split)
   __shared__ __attribute__((aligned(16))) float sCnt[3][kTile];  // c_d (0 past the split)
-  __shared__ __attribute__((aligned(16))) float sAlpha[kWaves][32];
+  __shared__ __attribute__((aligned(16))) float sAlpha[NW][32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, c = lane & 31;
   int split;
   int64_t rb, j_begin, j_end;
   fwdg_geometry(a, split, rb, j_begin, j_end);
-  const int64_t i = rb * kOwnRows + wave * 32 + c;
+  const int64_t i = rb * kRows + wave * 32 + c;
   const bool row_ok = i < a.N;
   bf16x8 uh[8], ul[8];
   load_owner_x3(uh, ul, a.A, i, a.lda, row_ok, h);
@@ -2242,10 +2288,10 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_fwdg_x3p_k(GArgs a) {
   for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
     for (int r = 0; r < 16; ++r) gacc[kb][r] = 0.0f;
-  X3Stage stg;
+  X3StageT<NW> stg;
   float stg_b = 0.0f, stg_c = 0.0f;
   auto gload = [&](int64_t j0) {
-    const int64_t j = j0 + (tid >> 3);
+    const int64_t j = j0 + ((tid >> 3) & 31);
     stg.load(a.bhi, a.blo, j, j < j_end, tid);
     if (tid < kTile) {
       const int64_t jj = j0 + tid;
@@ -2392,14 +2438,17 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_fwdg_x3p_k(GArgs a) {
     a.part[2 * stride + o] = 0.0f;
     a.part[3 * stride + o] = 0.0f;
   }
-  const int64_t own_base = rb * kOwnRows + wave * 32;
+  const int64_t own_base = rb * kRows + wave * 32;
   float* dst = a.dout + (int64_t)split * a.N * kD;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int64_t orow = own_base + tile_row(r, h);
     if (orow < a.N) {
 #pragma unroll
-      for (int kb = 0; kb < 4; ++kb) dst[orow * kD + kb * 32 + c] = gacc[kb][r];
+      for (int kb = 0; kb < 4; ++kb) {
+        if (NT) __builtin_nontemporal_store(gacc[kb][r], &dst[orow * kD + kb * 32 + c]);
+        else dst[orow * kD + kb * 32 + c] = gacc[kb][r];
+      }
     }
   }
 }
@@ -2814,6 +2863,23 @@ RSX_API int rsx_nce_grouped_fwd(const float* A, const float* B, const float* bia
   return 0;
 }
 
+// RSX_NCE_FWDG_NW = 4 | 8: waves per workgroup of the pipelined fused forward; RSX_NCE_FWDG_NT=1:
+// nontemporal partial-row stores (A/B measurements)
+static int fwdg_waves() {
+  static const int v = [] {
+    const char* e = getenv("RSX_NCE_FWDG_NW");
+    return (e && e[0] == '4') ? 4 : (e && e[0] == '8') ? 8 : 4;
+  }();
+  return v;
+}
+static bool fwdg_nt() {
+  static const bool v = [] {
+    const char* e = getenv("RSX_NCE_FWDG_NT");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 // RSX_NCE_FWDG=0 selects the unpipelined fused forward (A/B measurements)
 static bool fwdg_pipelined() {
   static const bool v = [] {
@@ -2846,11 +2912,14 @@ RSX_API int rsx_nce_grouped_fwd_grad(const float* A, const float* B, const float
   // as fill whole rounds of the grid at two workgroups per CU; the remaining row blocks run 8
   // half-length splits, dispatched last, so the grid's final round is short and full
   // (batch 8192: 1,152 row blocks x 4 = 9 rounds of 512, then 45 x 8 half-length workgroups)
-  const int64_t rbs = (N + kOwnRows - 1) / kOwnRows;
+  const bool piped = fwdg_pipelined();
+  const int nw = piped ? fwdg_waves() : kWaves;
+  const int64_t rows_wg = 32 * nw;
+  const int64_t rbs = (N + rows_wg - 1) / rows_wg;
   const int ns1 = nsplit == 8 ? 4 : nsplit;
   int64_t rb1 = rbs;
   if (nsplit == 8 && !getenv("RSX_NCE_TAIL8_OFF")) {
-    const int64_t slots = 2 * (int64_t)rsx::cu_count();
+    const int64_t slots = (8 / nw) * (int64_t)rsx::cu_count();
     rb1 = (ns1 * rbs / slots) * slots / ns1;  // whole rounds of the 4-split blocks
   } else if (nsplit == 8) {
     rb1 = 0;
@@ -2876,13 +2945,19 @@ RSX_API int rsx_nce_grouped_fwd_grad(const float* A, const float* B, const float
   launch_split(B, ldb, D, im.bhi, im.blo, st);
   RSX_LAUNCHED();
   const int blocks = (int)(rb1 * ns1 + (rbs - rb1) * (nsplit == 8 ? 8 : 0));
-  if (fwdg_pipelined())
-    hipLaunchKernelGGL(nce_grouped_fwdg_x3p_k, dim3(blocks), dim3(256), 0, st, g);
-  else
+  if (!piped)
     hipLaunchKernelGGL(nce_grouped_fwdg_x3_k, dim3(blocks), dim3(256), 0, st, g);
+  else if (nw == 8 && fwdg_nt())
+    hipLaunchKernelGGL((nce_grouped_fwdg_x3p_k<8, true>), dim3(blocks), dim3(512), 0, st, g);
+  else if (nw == 8)
+    hipLaunchKernelGGL((nce_grouped_fwdg_x3p_k<8, false>), dim3(blocks), dim3(512), 0, st, g);
+  else if (fwdg_nt())
+    hipLaunchKernelGGL((nce_grouped_fwdg_x3p_k<4, true>), dim3(blocks), dim3(256), 0, st, g);
+  else
+    hipLaunchKernelGGL((nce_grouped_fwdg_x3p_k<4, false>), dim3(blocks), dim3(256), 0, st, g);
   RSX_LAUNCHED();
   hipLaunchKernelGGL(nce_grouped_merge_g_k, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, A, B, bias, row_col,
-                     N, lda, ldb, g.inv_tau, ns1, part, opart, lse, row_loss, row_valid, ga, rb1 * kOwnRows, 8,
+                     N, lda, ldb, g.inv_tau, ns1, part, opart, lse, row_loss, row_valid, ga, rb1 * rows_wg, 8,
                      nsplit);
   RSX_LAUNCHED();
   hipLaunchKernelGGL(nce_reduce_k, dim3(1), dim3(1024), 0, st, row_loss, row_valid, N, out2);

@@ -1157,6 +1157,56 @@ _DEEPFM_FUSED = os.environ.get("RSX_DEEPFM_FUSED", "1") != "0"
 _DEEPFM_PACK = os.environ.get("RSX_DEEPFM_PACK", "1") != "0"
 
 
+class _FastKey:
+    """Validity key of derived device state over a list of tensors: identities (the tensors are
+    held, so an id cannot be recycled), storage pointers and in-place version counters, compared
+    as three flat lists (≈ 0.25 µs per tensor; the per-tensor tuple key cost ≈ 0.75 µs)."""
+    __slots__ = ("held", "ids", "ptrs", "vers")
+
+    def __init__(self, ts):
+        self.held = list(ts)
+        self.ids = [id(t) for t in ts]
+        self.ptrs = [t.data_ptr() for t in ts]
+        self.vers = [t._version for t in ts]
+
+    def matches(self, ts) -> bool:
+        return ([id(t) for t in ts] == self.ids and [t._version for t in ts] == self.vers
+                and [t.data_ptr() for t in ts] == self.ptrs)
+
+
+def _deepfm_state(F, dev, emb_tables, lin_tables, dnn_weights, dnn_biases, w_out, cache):
+    """Device state of the fused DeepFM kernel: the bf16 DNN weight images, the packed tables (when
+    the kernel form takes them) and the pointer arrays, rebuilt when any input tensor changes
+    (storage or in-place version). Kept in the caller's cache dict (the DeepFM module) between
+    calls; without one it is built per call."""
+    ts = list(emb_tables) + list(lin_tables) + list(dnn_weights) + list(dnn_biases) + [w_out]
+    if cache is not None:
+        st = cache.get("fused_state")
+        if st is not None and st["dev"] == dev and st["key"].matches(ts):
+            return st
+    emb = [_c(t) for t in emb_tables]
+    lin = [_c(t) for t in lin_tables]
+    w1, w2 = _c(dnn_weights[0]), _c(dnn_weights[1])
+    b1, b2 = _c(dnn_biases[0]), _c(dnn_biases[1])
+    wo = _c(w_out.reshape(-1))
+    ws = torch.empty(N.lib().rsx_deepfm_fused_workspace_bytes(F), device=dev, dtype=torch.uint8)
+    N.check(N.lib().rsx_deepfm_fused_prep(F, N.ptr(w1), N.ptr(w2), N.ptr(ws), N.stream()), "deepfm_prep")
+    packed = None
+    if cache is not None and _DEEPFM_PACK and N.lib().rsx_deepfm_fused_uses_packed(F):
+        # inference images of the tables: [vocab][32] per field (V row, W, pad); one 128-B line
+        # per (row, field) instead of two
+        packed = [torch.empty(v.shape[0], 32, device=dev, dtype=torch.float32) for v in emb]
+        for v, w, p in zip(emb, lin, packed):
+            N.check(N.lib().rsx_deepfm_pack(N.ptr(v), N.ptr(w), v.shape[0], N.ptr(p), N.stream()), "deepfm_pack")
+    st = {"dev": dev, "key": _FastKey(ts), "hold": (emb, lin, w1, w2, b1, b2, wo, packed), "ws": N.ptr(ws),
+          "ws_t": ws, "V": N.ptr_array(emb), "W": N.ptr_array(lin),
+          "P": N.ptr_array(packed) if packed is not None else None,
+          "b1": N.ptr(b1), "b2": N.ptr(b2), "wo": N.ptr(wo)}
+    if cache is not None:
+        cache["fused_state"] = st
+    return st
+
+
 def deepfm_forward(x, emb_tables, lin_tables, out_bias, dnn_weights, dnn_biases, w_out, cache=None):
     """DeepFM logits/probabilities for x [R, F] int64 (see csrc/deepfm.hip).
 
@@ -1173,38 +1223,14 @@ def deepfm_forward(x, emb_tables, lin_tables, out_bias, dnn_weights, dnn_biases,
     dev = x.device
     if (_DEEPFM_FUSED and E == 16 and F <= 64 and len(dnn_weights) == 2 and tuple(dnn_weights[0].shape) == (256, F * 16)
             and tuple(dnn_weights[1].shape) == (128, 256)):
-        logit = torch.empty(R, device=dev, dtype=torch.float32)
-        prob = torch.empty(R, device=dev, dtype=torch.float32)
-        w1, w2 = _c(dnn_weights[0]), _c(dnn_weights[1])
         if len(emb_tables) != F or len(lin_tables) != F:
             raise ValueError(f"deepfm: {len(emb_tables)} embedding / {len(lin_tables)} linear tables for {F} fields")
-        key = (F, dev) + _tensor_key((w1, w2))
-        b1, b2 = dnn_biases
+        logit = torch.empty(R, device=dev, dtype=torch.float32)
+        prob = torch.empty(R, device=dev, dtype=torch.float32)
         with timed("deepfm/fused"):
-            if cache is not None and _key_eq(cache.get("key"), key):
-                ws = cache["ws"]
-            else:
-                ws = torch.empty(N.lib().rsx_deepfm_fused_workspace_bytes(F), device=dev, dtype=torch.uint8)
-                N.check(N.lib().rsx_deepfm_fused_prep(F, N.ptr(w1), N.ptr(w2), N.ptr(ws), N.stream()), "deepfm_prep")
-                if cache is not None:
-                    cache["key"], cache["ws"] = key, ws
-            packed = None
-            if cache is not None and _DEEPFM_PACK and N.lib().rsx_deepfm_fused_uses_packed(F):
-                # inference images of the tables: [vocab][32] per field (V row, W, pad), rebuilt when
-                # any table changes; one 128-B line per (row, field) instead of two
-                tkey = _tensor_key(list(emb_tables) + list(lin_tables))
-                if not _key_eq(cache.get("tkey"), tkey):
-                    cache.pop("packed", None)
-                    packed = [torch.empty(v.shape[0], 32, device=dev, dtype=torch.float32) for v in emb_tables]
-                    for v, w, p in zip(emb_tables, lin_tables, packed):
-                        N.check(N.lib().rsx_deepfm_pack(N.ptr(_c(v)), N.ptr(_c(w)), v.shape[0], N.ptr(p), N.stream()),
-                                "deepfm_pack")
-                    cache["tkey"], cache["packed"] = tkey, packed
-                packed = cache["packed"]
-            rc = N.lib().rsx_deepfm_fused_run(
-                N.ptr(x), R, F, N.ptr_array([_c(t) for t in emb_tables]), N.ptr_array([_c(t) for t in lin_tables]),
-                N.ptr_array(packed) if packed is not None else None, float(out_bias), N.ptr(_c(b1)), N.ptr(_c(b2)),
-                N.ptr(_c(w_out.reshape(-1))), N.ptr(ws), N.ptr(logit), N.ptr(prob), N.stream())
+            st = _deepfm_state(F, dev, emb_tables, lin_tables, dnn_weights, dnn_biases, w_out, cache)
+            rc = N.lib().rsx_deepfm_fused_run(N.ptr(x), R, F, st["V"], st["W"], st["P"], float(out_bias), st["b1"],
+                                              st["b2"], st["wo"], st["ws"], N.ptr(logit), N.ptr(prob), N.stream())
         N.check(rc, "deepfm_fused")
         return logit, prob
     emb = torch.empty(R, F * E, device=dev, dtype=torch.float32)

@@ -67,13 +67,27 @@ class DeepFM(nn.Module):
             c = self.__dict__["_bias_cache"] = (b, b._version, float(b.item()))
         return c[2]
 
+    def _param_lists(self):
+        """(embedding weights, linear weights, DNN weights, DNN biases, output weight), read through
+        the submodules' parameter dicts from a submodule list built once: nn.Module attribute
+        lookups for the 80 tensors cost more host time per call than the fused kernel itself.
+        A parameter replaced on a submodule is still seen; replacing a submodule is not supported."""
+        mods = self.__dict__.get("_mod_lists")
+        if mods is None:
+            mods = self.__dict__["_mod_lists"] = (
+                [self.embedding_dict[n] for n in self.field_names],
+                [self.linear_model.embedding_dict[n] for n in self.field_names],
+                list(self.dnn.linears), self.dnn_linear)
+        emb, lin, dnn, out = mods
+        return ([m._parameters["weight"] for m in emb], [m._parameters["weight"] for m in lin],
+                [m._parameters["weight"] for m in dnn], [m._parameters["bias"] for m in dnn],
+                out._parameters["weight"])
+
     @torch.no_grad()
     def forward_logits(self, X):
-        return ops.deepfm_forward(
-            X, [self.embedding_dict[n].weight for n in self.field_names],
-            [self.linear_model.embedding_dict[n].weight for n in self.field_names], self._bias_value(),
-            [l.weight for l in self.dnn.linears], [l.bias for l in self.dnn.linears], self.dnn_linear.weight,
-            cache=self.__dict__.setdefault("_fused_cache", {}))
+        emb, lin, ws, bs, wo = self._param_lists()
+        return ops.deepfm_forward(X, emb, lin, self._bias_value(), ws, bs, wo,
+                                  cache=self.__dict__.setdefault("_fused_cache", {}))
 
     def predict_proba(self, X) -> np.ndarray:
         """CatBoost-compatible: probability of class 1 (RecommendationRanker.predict_proba :148-149)."""

@@ -206,14 +206,18 @@ def test_golden_gpu_losses(gpu):
 
 
 @pytest.mark.gpu
-def test_golden_gpu_deepfm(gpu):
+@pytest.mark.parametrize("cached", [False, True])  # raw V/W tables, or the packed images of a table cache
+def test_golden_gpu_deepfm(gpu, cached):
     from recsys_amd import ops
     t, meta = load("deepfm_r128")
     emb, lin, ws, bs, wo = deepfm_inputs(t)
-    logit, prob = ops.deepfm_forward(t["in.x"].to(gpu), [e.to(gpu) for e in emb], [w.to(gpu) for w in lin],
-                                     meta["bias"], [w.to(gpu) for w in ws], [b.to(gpu) for b in bs], wo.to(gpu))
-    torch.testing.assert_close(logit.cpu().double(), t["out.logit"], atol=1e-4, rtol=0)  # fp32 logits within 1e-4
-    torch.testing.assert_close(prob.cpu().double(), t["out.prob"], atol=1e-5, rtol=0)
+    cache = {} if cached else None
+    args = (t["in.x"].to(gpu), [e.to(gpu) for e in emb], [w.to(gpu) for w in lin], meta["bias"],
+            [w.to(gpu) for w in ws], [b.to(gpu) for b in bs], wo.to(gpu))
+    for _ in range(2 if cached else 1):  # the second call reuses the cached images
+        logit, prob = ops.deepfm_forward(*args, cache=cache)
+        torch.testing.assert_close(logit.cpu().double(), t["out.logit"], atol=1e-4, rtol=0)  # fp32 logits within 1e-4
+        torch.testing.assert_close(prob.cpu().double(), t["out.prob"], atol=1e-5, rtol=0)
 
 
 @pytest.mark.gpu
