@@ -47,6 +47,26 @@ constexpr int EPI_BIAS = 0, EPI_GELU_DROP = 1, EPI_DGELU_DROP = 2, EPI_ROWADD = 
 
 __device__ __forceinline__ int tile_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
+// gelu(x) = x Phi(x) and gelu'(x) = Phi(x) + x phi(x), branch-free for the weight-stationary
+// epilogue: Phi from erfc(z) ~ t P(t) e^{-z^2}, t = 1 / (1 + p z), z = |x| / sqrt 2 (Abramowitz &
+// Stegun 7.1.26, |erf error| <= 1.5e-7), and e^{-z^2} = e^{-x^2/2} is also phi's exponential: one
+// exp, one rcp and six fma per element instead of erff's two-range polynomial plus an exp.
+// Max |error| over [-12, 12] against float64: 4.2e-7 (gelu), 3.2e-7 (gelu'); torch's fp32 gelu
+// itself is 1.2e-6 off there.
+__device__ __forceinline__ void gelu_pair(float x, float& g, float& d) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float e = __expf(-0.5f * x * x);
+  const float q = 0.5f * (p * t) * e;  // 0.5 erfc(z) = Phi(-|x|)
+  const float cdf = x >= 0.0f ? 1.0f - q : q;
+  g = x * cdf;
+  d = fmaf(x * 0.3989422804014327f, e, cdf);
+}
+
 // rsx::hash_u32(seed, idx) for idx < 2^32 (the high-word terms vanish), in 32-bit ops
 __device__ __forceinline__ bool keep(const rsx::Dropout& d, uint32_t idx) {
   uint32_t x = idx ^ (uint32_t)d.seed;
@@ -252,9 +272,9 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_k(GArgs a) {
 // The summation order over k is a fixed permutation (k-step s of a chunk takes k = 16s + 4h
 // + {0..3} and 16s + 8 + 4h + {0..3}); B's fragments use the same permutation, so each
 // product is the plain sum over k. Same epilogues and dropout hash as gemm_x3_nt_k.
-constexpr int kWsThreads = 256;  // 4 waves: one per SIMD with the whole 512-register file
-constexpr int kWsWaves = kWsThreads / 64;
-constexpr int kWsBufs = 3;       // A chunks per wave: one being computed, two in flight
+// WV = 4: one wave per SIMD with the whole 512-register file, three A chunks per wave (one being
+// computed, two in flight); WV = 8: two waves per SIMD (256 registers each), two chunks per wave
+// (the other wave's loads and stores in flight while one computes).
 
 struct WsArgs {
   GArgs g;
@@ -262,9 +282,9 @@ struct WsArgs {
   int groups;   // workgroups per column block
 };
 
-template <int KC, int NBW, int EPI>
-__global__ __launch_bounds__(kWsThreads, 1) void gemm_ws_k(WsArgs w) {
-  static_assert(kWsBufs == 3, "the main loop below is written for three buffers");
+template <int KC, int NBW, int EPI, int WV>
+__global__ __launch_bounds__(64 * WV, 1) void gemm_ws_k(WsArgs w) {
+  constexpr int kWsThreads = 64 * WV, kWsWaves = WV;
   constexpr int NT = NBW / 32;
   __shared__ __attribute__((aligned(16))) u32x4 sW[KC * 8 * NT * 2 * 64];
   const GArgs& a = w.g;
@@ -370,10 +390,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void gemm_ws_k(WsArgs w) {
           float d[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const float x = v[e];
-            const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-            d[e] = cdf + x * 0.3989422804014327f * __expf(-0.5f * x * x);  // gelu'(x)
-            v[e] = x * cdf;
+            gelu_pair(v[e], v[e], d[e]);
           }
           if (a.aux) *reinterpret_cast<float4*>(xrow + o) = make_float4(d[0], d[1], d[2], d[3]);
         }
@@ -392,12 +409,30 @@ __global__ __launch_bounds__(kWsThreads, 1) void gemm_ws_k(WsArgs w) {
   // sched_barrier fences keep the compiler from hoisting one buffer's conversions into another
   // phase (which raised the register demand past the file and forced early vmcnt waits).
 #define WS_FENCE __builtin_amdgcn_sched_barrier(0)
-  float4 b0[16], b1[16], b2[16];
   if (nitems == 0) return;  // wave-uniform; no barrier follows
   // every load is unconditional (item index clamped to the last item): all paths into the
   // loop then carry the same outstanding-load pattern, so the compiler's vmcnt waits stay
   // per buffer instead of draining the prefetches. The trailing re-loads are never used.
   const int last = nitems - 1;
+  if constexpr (WV == 8) {
+    float4 b0[16], b1[16];
+    load(0, b0);
+    load(last < 1 ? last : 1, b1);
+    for (int t = 0;; t += 2) {
+      WS_FENCE;
+      compute(t, b0);
+      WS_FENCE;
+      load(t + 2 < last ? t + 2 : last, b0);
+      if (t + 1 > last) break;
+      WS_FENCE;
+      compute(t + 1, b1);
+      WS_FENCE;
+      load(t + 3 < last ? t + 3 : last, b1);
+      if (t + 2 > last) break;
+    }
+    return;
+  }
+  float4 b0[16], b1[16], b2[16];
   load(0, b0);
   load(last < 1 ? last : 1, b1);
   load(last < 2 ? last : 2, b2);
@@ -443,8 +478,9 @@ bool ws_enabled() {
   return on == 1;
 }
 
-template <int KC, int NBW>
-void launch_ws(const GArgs& g, hipStream_t st) {
+template <int KC, int NBW, int WV>
+void launch_ws_w(const GArgs& g, hipStream_t st) {
+  constexpr int kWsThreads = 64 * WV, kWsWaves = WV;
   WsArgs w;
   w.g = g;
   w.nblk = g.N / NBW;
@@ -455,12 +491,28 @@ void launch_ws(const GArgs& g, hipStream_t st) {
   if (groups > blocks_rows) groups = (int)blocks_rows;
   w.groups = groups;
   const int grid = (w.nblk * groups + 7) / 8 * 8;
-  if (g.epi == EPI_BIAS) hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_BIAS>), dim3(grid), dim3(kWsThreads), 0, st, w);
+  if (g.epi == EPI_BIAS) hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_BIAS, WV>), dim3(grid), dim3(kWsThreads), 0, st, w);
   else if (g.epi == EPI_ROWADD)
-    hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_ROWADD>), dim3(grid), dim3(kWsThreads), 0, st, w);
+    hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_ROWADD, WV>), dim3(grid), dim3(kWsThreads), 0, st, w);
   else if (g.epi == EPI_GELU_DROP)
-    hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_GELU_DROP>), dim3(grid), dim3(kWsThreads), 0, st, w);
-  else hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_DGELU_DROP>), dim3(grid), dim3(kWsThreads), 0, st, w);
+    hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_GELU_DROP, WV>), dim3(grid), dim3(kWsThreads), 0, st, w);
+  else hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_DGELU_DROP, WV>), dim3(grid), dim3(kWsThreads), 0, st, w);
+}
+
+// RSX_GEMM_WS_WAVES = 4 | 8 (A/B): waves per weight-stationary workgroup
+int ws_waves() {
+  static int v = 0;
+  if (v == 0) {
+    const char* e = getenv("RSX_GEMM_WS_WAVES");
+    v = (e && e[0] == '8') ? 8 : 4;
+  }
+  return v;
+}
+
+template <int KC, int NBW>
+void launch_ws(const GArgs& g, hipStream_t st) {
+  if (ws_waves() == 8) launch_ws_w<KC, NBW, 8>(g, st);
+  else launch_ws_w<KC, NBW, 4>(g, st);
 }
 
 }  // namespace

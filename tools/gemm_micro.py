@@ -60,6 +60,25 @@ def main():
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / args.iters
         res[name] = {"ms": round(ms, 4), "GB/s": round(T * (n + k) * 4 / ms / 1e6, 1)}
+    # copy ceilings of the same byte mixes (torch's copy kernel): [T,128] -> [T,128] (1:1) and
+    # [T,128] -> [T,384] (1:3, three strided copies into one output)
+    x = torch.randn(T, 128, device=dev)
+    y1 = torch.empty_like(x)
+    y3 = torch.empty(T, 384, device=dev)
+    for name, fn, byts in [("copy_1to1", lambda: y1.copy_(x), T * 128 * 8),
+                           ("copy_1to3", lambda: [y3[:, 128 * i:128 * (i + 1)].copy_(x) for i in range(3)],
+                            T * 128 * 4 * 6)]:
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.iters):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / args.iters
+        res[name] = {"ms": round(ms, 4), "GB/s": round(byts / ms / 1e6, 1)}
     print(json.dumps(res), flush=True)
 
 
