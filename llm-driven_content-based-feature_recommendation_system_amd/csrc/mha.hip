@@ -1244,6 +1244,184 @@ __global__ __launch_bounds__(256) void mha_bwd_x3p_k(BwdArgs a) {
 }
 
 
+// ---- bf16x3 backward, causal, one dS evaluation per pair ---------------------------------------
+// mha_bwd_x3p_k's pass 1 (key block on the lanes: S, dP, the softmax gradient dS and the dropped-out
+// P, then dK and dV) also writes each pair's dS tile to LDS (1.25 KB per pair, <= 10 causal pairs
+// per (sequence, head) at L <= 64: 51 KB per 4-wave workgroup, three workgroups per CU as the
+// registers allow). Pass 2 then reads the tiles transposed and forms dQ = dS K with K's columns as
+// its only loads, instead of recomputing S and dP (6 MFMAs), the exp / dropout hash of 16
+// elements and four row splits per pair.
+constexpr int kStashLd = 20;     // tile row stride (floats): conflict-free writes, aligned b128 reads
+constexpr int kStashPairs = 10;  // causal pairs kb <= qb < 4
+__device__ __forceinline__ int stash_slot(int kb, int qb) { return (qb * (qb + 1) >> 1) + kb; }
+
+__global__ __launch_bounds__(256) void mha_bwd_x3s_k(BwdArgs a) {
+  // dS tiles of this wave's (kb, qb <= ... ) pairs, [16 query rows][16 key columns] at row stride 20
+  __shared__ __attribute__((aligned(16))) float sDS[4][kStashPairs][16 * kStashLd];
+  constexpr int DH = 32;
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t unit = (int64_t)blockIdx.x * 4 + wave;
+  if (unit >= (int64_t)a.B * a.H) return;  // whole wave exits together
+  const int b = (int)(unit / a.H), hd = (int)(unit % a.H);
+  const int D = a.H * DH;
+  const int ld = 3 * D;
+  const int64_t tok0 = a.seg ? (int64_t)a.seg[b] : (int64_t)b * a.L;
+  int L = a.seg ? (a.seg[b + 1] - a.seg[b]) : a.L;
+  if (L > kLMax) L = kLMax;
+  if (L <= 0) return;
+  const int nb = __builtin_amdgcn_readfirstlane((L + 15) >> 4);
+  const auto rq = seq_rsrc(a.qkv + tok0 * ld, (unsigned)(L * ld * 4));
+  const auto rd = seq_rsrc(a.dout + tok0 * D, (unsigned)(L * D * 4));
+  const float sc = a.scale;
+  const int cq = hd * DH, ck = D + hd * DH, cv = 2 * D + hd * DH;  // column offsets in a qkv row
+
+  // per-token softmax statistics (token t < L on lane t): lse_t, delta_t = dO_t . O_t, key pad
+  float my_lse = -INFINITY, my_delta = 0.0f;
+  int my_pad = 1;
+  if (lane < L) {
+    my_lse = a.lse[(tok0 + lane) * a.H + hd];
+    const float4* op = reinterpret_cast<const float4*>(a.out + (tok0 + lane) * D + hd * DH);
+    const float4* gp = reinterpret_cast<const float4*>(a.dout + (tok0 + lane) * D + hd * DH);
+    float d = 0.0f;
+#pragma unroll
+    for (int t = 0; t < DH / 4; ++t) {
+      const float4 x = op[t], y = gp[t];
+      d += x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
+    }
+    my_delta = d;
+    my_pad = a.kpad ? (int)a.kpad[tok0 + lane] : 0;
+  }
+  auto grad_elem = [&](int i, int j, float s, float dp, float lse_i, float delta_i, bool allowed, float& pd_out) {
+    pd_out = 0.0f;
+    if (!allowed) return 0.0f;
+    const float p = __expf(s * sc - lse_i);
+    float pd = p, dpd = dp;
+    if (a.drop.active()) {
+      const uint64_t idx = ((uint64_t)(tok0 + i) * a.H + hd) * kLMax + j;
+      const bool keep = rsx::hash_u32(a.drop.seed, idx) >= a.drop.thresh;
+      pd = keep ? p * a.drop.scale : 0.0f;
+      dpd = keep ? dp * a.drop.scale : 0.0f;
+    }
+    pd_out = pd;
+    return p * (dpd - delta_i) * sc;
+  };
+
+  // ---- pass 1: pairs (kb, qb >= kb) in kb-major order; key j = 16kb + c on the score columns ----
+  {
+    auto load1 = [&](Pair1& P, int kb, int qb) {
+      const int j = 16 * kb + c, iq = 16 * qb + c;
+      P.k = load_rawrow(rq, (unsigned)((j * ld + ck + 8 * g) * 4));
+      P.v = load_rawrow(rq, (unsigned)((j * ld + cv + 8 * g) * 4));
+      P.q = load_rawrow(rq, (unsigned)((iq * ld + cq + 8 * g) * 4));
+      P.d = load_rawrow(rd, (unsigned)((iq * D + hd * DH + 8 * g) * 4));
+      load_rawcols(rq, 16 * qb + 4 * g, ld, cq + c, P.qc);
+      load_rawcols(rd, 16 * qb + 4 * g, D, hd * DH + c, P.dc);
+    };
+    f32x4 dk[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    f32x4 dv[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    int kb = 0, qb = 0;
+    // one pair: prefetch the next one into `fill`, compute this one from `use`; false when done
+    auto step = [&](const Pair1& use, Pair1& fill) -> bool {
+      int nkb = kb, nqb = qb + 1;
+      if (nqb >= nb) { nkb = kb + 1; nqb = a.causal ? nkb : 0; }
+      load1(fill, nkb, nqb);
+      const int j = 16 * kb + c;
+      const bool jok = j < L;
+      const int jpad = __shfl(my_pad, j & 63, 64);
+      const f32x4 S = dot16_x3(split_row8(use.q.x0, use.q.x1), split_row8(use.k.x0, use.k.x1));
+      const f32x4 dP = dot16_x3(split_row8(use.d.x0, use.d.x1), split_row8(use.v.x0, use.v.x1));
+      float ds[4], pd[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 16 * qb + 4 * g + r;
+        const float lse_i = __shfl(my_lse, i & 63, 64);
+        const float del_i = __shfl(my_delta, i & 63, 64);
+        const bool allowed = jok && i < L && !jpad && (!a.causal || j <= i) && lse_i != -INFINITY;
+        ds[r] = grad_elem(i, j, S[r], dP[r], lse_i, del_i, allowed, pd[r]);
+      }
+      {  // dS[16qb + 4g + r][16kb + c] -> tile row 4g + r, column c (read transposed in pass 2)
+        float* t = sDS[wave][stash_slot(kb, qb)];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) t[(4 * g + r) * kStashLd + c] = ds[r];
+      }
+      const Col4 pa = split4(pd), sa = split4(ds);
+#pragma unroll
+      for (int et = 0; et < 2; ++et) {
+        dv[et] = sum16_x3(pa, split_col4(use.dc[et]), dv[et]);  // dV[j][e]
+        dk[et] = sum16_x3(sa, split_col4(use.qc[et]), dk[et]);  // dK[j][e]
+      }
+      if (nkb != kb) {
+        float* dKb = a.dqkv + tok0 * ld + ck;
+        float* dVb = a.dqkv + tok0 * ld + cv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * kb + 4 * g + r;
+          if (row < L) {
+#pragma unroll
+            for (int et = 0; et < 2; ++et) {
+              dKb[(int64_t)row * ld + 16 * et + c] = dk[et][r];
+              dVb[(int64_t)row * ld + 16 * et + c] = dv[et][r];
+            }
+          }
+        }
+#pragma unroll
+        for (int et = 0; et < 2; ++et) dk[et] = dv[et] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      kb = nkb;
+      qb = nqb;
+      return kb < nb;
+    };
+    Pair1 p0, p1;
+    load1(p0, 0, 0);
+    for (;;) {
+      if (!step(p0, p1)) break;
+      if (!step(p1, p0)) break;
+    }
+  }
+
+  // ---- pass 2: dQ[i] = sum_j dS[i][j] K[j] from the stashed tiles (qb-major, kb <= qb): the
+  // tile is read transposed (lane (c, g): query 16qb + c, keys 16kb + 4g + 0..3 = the A operand),
+  // K's columns are the only loads; S, dP and the softmax gradient are not recomputed ----
+  {
+    f32x4 dq[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    int qb = 0, kb = 0;
+    auto step = [&](const unsigned (&use)[2][4], unsigned (&fill)[2][4]) -> bool {
+      int nqb = qb, nkb = kb + 1;
+      if (nkb > qb) { nqb = qb + 1; nkb = 0; }
+      load_rawcols(rq, 16 * nkb + 4 * g, ld, ck + c, fill);
+      const float4 t = *reinterpret_cast<const float4*>(&sDS[wave][stash_slot(kb, qb)][c * kStashLd + 4 * g]);
+      const float ds[4] = {t.x, t.y, t.z, t.w};
+      const Col4 sa = split4(ds);
+#pragma unroll
+      for (int et = 0; et < 2; ++et) dq[et] = sum16_x3(sa, split_col4(use[et]), dq[et]);  // dQ[i][e]
+      if (nqb != qb) {
+        float* dQb = a.dqkv + tok0 * ld + cq;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * qb + 4 * g + r;
+          if (row < L) {
+            dQb[(int64_t)row * ld + c] = dq[0][r];
+            dQb[(int64_t)row * ld + 16 + c] = dq[1][r];
+          }
+        }
+        dq[0] = dq[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      qb = nqb;
+      kb = nkb;
+      return qb < nb;
+    };
+    unsigned k0[2][4], k1[2][4];
+    load_rawcols(rq, 4 * g, ld, ck + c, k0);
+    for (;;) {
+      if (!step(k0, k1)) break;
+      if (!step(k1, k0)) break;
+    }
+  }
+}
+
+
+
 // ---- fused in-projection + attention forward (head dim 32, bf16x3) -------------------------
 // The user tower's `qkv = in_proj(h); mha(qkv)` (v1_refine_usertower.py:343-352 through
 // nn.TransformerEncoderLayer's self_attn) as ONE kernel: each wave (sequence, head) computes its
@@ -1588,8 +1766,11 @@ RSX_API int rsx_mha_bwd_x3(const float* qkv, const uint8_t* key_pad, const int* 
   a.scale = 1.0f / sqrtf((float)Dh);
   a.drop = rsx::make_dropout(p_drop, seed);
   static const bool legacy = getenv("RSX_MHA_BWD_LEGACY") != nullptr;  // A/B: one latency per pair
+  static const bool stash = getenv("RSX_MHA_BWD_STASH") == nullptr || getenv("RSX_MHA_BWD_STASH")[0] != '0';
   if (legacy)
     hipLaunchKernelGGL(mha_bwd_x3_k, dim3((unsigned)((B * H + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a);
+  else if (causal && stash)
+    hipLaunchKernelGGL(mha_bwd_x3s_k, dim3((unsigned)((B * H + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a);
   else
     hipLaunchKernelGGL(mha_bwd_x3p_k, dim3((unsigned)((B * H + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a);
   RSX_LAUNCHED();
