@@ -377,7 +377,7 @@ def contrastive_objective_dp(model, item_tower, log_q_tensor, batch, cfg, pretra
     StepIndex of this batch prepared ahead (prepare_step_index[_async]); built here if None.
     Returns (local objective to backward, global total / main / cl for logging; the
     logging values are all-reduced and detached)."""
-    from .tower_code.v1_usertower_train import packed_views
+    from .tower_code.v1_usertower_train import packed_out
 
     rank, ws = world()
     device = batch["item_ids"].device
@@ -386,12 +386,16 @@ def contrastive_objective_dp(model, item_tower, log_q_tensor, batch, cfg, pretra
     else:
         _adopt(index)
     B = index.B
-    pk, out1, out2 = packed_views(model, batch, pretrained_vecs, pretrained_lookup, packed=index.packed)
+    pk, out = packed_out(model, batch, pretrained_vecs, pretrained_lookup, packed=index.packed)
+    # the loss rows of view 1 (valid steps, normalised again: the reference's F.normalize of the
+    # already-normalised output) and the "last" rows of both views, gathered by one autograd node
+    # whose backward writes a single gradient of `out`
+    T = pk.flat.numel()
+    u_loc, z1, z2 = ops.gather_rows_multi(out, [(pk.valid_tok, True), (pk.last_tok, True), (pk.last_tok + T, True)])
 
     # ---- main LogQ loss over all valid steps of the global batch
     n_glob = index.n_glob
     if n_glob > 0:
-        u_loc = ops.gather_rows(out1, pk.valid_tok, normalize=True, unique=True)
         groups = index.groups
         items_d = ops.gather_rows(item_tower.get_all_embeddings(), groups.uniq, normalize=True, unique=True)
         bias = log_q_tensor[groups.uniq] * cfg.lambda_logq if cfg.lambda_logq > 0.0 else None
@@ -401,8 +405,6 @@ def contrastive_objective_dp(model, item_tower, log_q_tensor, batch, cfg, pretra
         main_local = torch.zeros((), device=device)
 
     # ---- DuoRec on the bug-compatible "last" index (count_valid - 1), global B x B
-    z1 = ops.l2_normalize(ops.gather_rows(out1, pk.last_tok, unique=True))
-    z2 = ops.l2_normalize(ops.gather_rows(out2, pk.last_tok, unique=True))
     last_t = index.last_t
     bcounts = [B] * ws
     b_glob = B * ws

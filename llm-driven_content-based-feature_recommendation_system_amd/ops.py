@@ -409,6 +409,57 @@ def gather_rows(src, idx=None, normalize=False, eps=1e-12, unique=False, skip_id
     return _GatherRows.apply(src, idx, bool(normalize), float(eps), bool(unique), int(skip_idx))
 
 
+class _GatherRowsMulti(torch.autograd.Function):
+    """Several row gathers of one source (each index list duplicate-free), with ONE zero-filled
+    source gradient that every gather's backward accumulates into in turn (non-atomic
+    read-add-write, scatter mode 1): the autograd form of k gathers of slices of one tensor
+    costs k zero-filled gradients, the slice gradients and their sums."""
+
+    @staticmethod
+    def forward(ctx, src, norms, eps, *idxs):
+        N.ensure_device(src)
+        src2 = _c(src)
+        D = src2.shape[-1]
+        outs, saved = [], []
+        for idx, nz in zip(idxs, norms):
+            idx = _c(idx)
+            n = idx.numel()
+            out = torch.empty(n, D, device=src.device, dtype=torch.float32)
+            nrm = torch.empty(n, device=src.device, dtype=torch.float32) if nz else None
+            rc = N.lib().rsx_gather_rows(N.ptr(src2), src2.stride(0), N.ptr(idx), n, D, int(nz), eps, N.ptr(out),
+                                         N.ptr(nrm), N.stream())
+            N.check(rc, "gather_rows")
+            outs.append(out)
+            saved += [idx, out if nz else idx, nrm if nz else idx]
+        ctx.cfg = (tuple(norms), eps, src2.shape)
+        ctx.save_for_backward(*saved)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *dys):
+        norms, eps, shape = ctx.cfg
+        saved = ctx.saved_tensors
+        D = shape[-1]
+        dsrc = torch.zeros(shape, device=saved[0].device, dtype=torch.float32)
+        for k, (dy, nz) in enumerate(zip(dys, norms)):
+            if dy is None:
+                continue
+            idx, y, nrm = saved[3 * k], saved[3 * k + 1], saved[3 * k + 2]
+            dy = _c(dy)
+            rc = N.lib().rsx_scatter_rows(N.ptr(dy), N.ptr(y if nz else None), N.ptr(nrm if nz else None), N.ptr(idx),
+                                          idx.numel(), D, int(nz), eps, 1, -1, N.ptr(dsrc), D, N.stream())
+            N.check(rc, "scatter_rows")
+        return (dsrc, None, None) + (None,) * len(dys)
+
+
+def gather_rows_multi(src, specs, eps=1e-12):
+    """[gather_rows(src, idx, normalize=nz, unique=True) for idx, nz in specs] as one autograd
+    node (one source gradient buffer; each idx must be duplicate-free)."""
+    idxs = [i for i, _ in specs]
+    norms = [bool(nz) for _, nz in specs]
+    return list(_GatherRowsMulti.apply(src, norms, float(eps), *idxs))
+
+
 def l2_normalize(x, eps=1e-12):
     """F.normalize(x, p=2, dim=-1) on the last dim."""
     shape = x.shape

@@ -136,12 +136,18 @@ def packed_views(model, batch, pretrained_vecs=None, pretrained_lookup=None, pac
     every kernel launch covers both views (half the launches, no per-parameter gradient adds).
     packed: pack_inputs(batch, ...) computed ahead (else computed here).
     Returns (packed tokens of one view, out_1 [T, D], out_2 [T, D])."""
+    pk, out = packed_out(model, batch, pretrained_vecs, pretrained_lookup, packed)
+    T = pk.flat.numel()
+    return pk, out[:T], out[T:]
+
+
+def packed_out(model, batch, pretrained_vecs=None, pretrained_lookup=None, packed=None):
+    """packed_views without the split: (packed tokens of one view, out [2T, D]); view 2's token t
+    is row T + t (for row gathers of both views in one autograd node, ops.gather_rows_multi)."""
     if packed is None:
         packed = pack_inputs(batch, pretrained_vecs, pretrained_lookup)
     pk, pk2, tok_ids, pv_tok, static = packed
-    T = pk.flat.numel()
-    out = model.forward_packed(pk2, pv_tok, tok_ids, *static)
-    return pk, out[:T], out[T:]
+    return pk, model.forward_packed(pk2, pv_tok, tok_ids, *static)
 
 
 def contrastive_losses(model, item_tower, log_q_tensor, batch, cfg, pretrained_vecs=None, pretrained_lookup=None):

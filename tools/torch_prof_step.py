@@ -35,15 +35,31 @@ def main():
         D.contrastive_step_dp(model, it, it.log_q, batch, opt, cfg, lookup, bucket, index=ix)
     torch.cuda.synchronize()
     from torch.profiler import ProfilerActivity, profile
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True, with_stack=True) as prof:
         for _ in range(3):
             D.contrastive_step_dp(model, it, it.log_q, batch, opt, cfg, lookup, bucket, index=ix)
         torch.cuda.synchronize()
     print(prof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=60,
                                                                max_name_column_width=60, max_shapes_column_width=70))
+    # the framework ops with the largest device time, with their python call sites (one step)
+    evs = [e for e in prof.events() if e.name in ("aten::zeros", "aten::zero_", "aten::add_", "aten::add", "aten::copy_",
+                                                 "aten::clone", "aten::contiguous", "aten::mm", "aten::cat",
+                                                 "aten::addmm", "aten::mul", "aten::fill_")]
+    evs.sort(key=lambda e: -e.device_time_total)
+    seen = set()
+    for e in evs:
+        st = tuple(f for f in e.stack if "recsys_amd" in f or "llm-driven" in f or "tools/" in f)[:4]
+        key = (e.name, st)
+        if key in seen or e.device_time_total < 8:
+            continue
+        seen.add(key)
+        print(f"EV {e.device_time_total:8.1f} us  {e.name}  shapes={e.input_shapes}")
+        for fr in st:
+            print("        ", fr)
     # the small framework ops (fills, copies, cats, index) with their python call sites
     ka = prof.key_averages(group_by_stack_n=6)
-    small = [e for e in ka if any(k in e.key for k in ("fill_", "zero_", "copy_", "cat", "index", "zeros", "empty"))]
+    small = [e for e in ka if any(k in e.key for k in ("fill_", "zero_", "copy_", "cat", "index", "zeros", "empty", "add", "mm",
+                                                       "layer_norm", "gelu", "linear", "clone", "contiguous"))]
     small.sort(key=lambda e: -e.device_time_total)
     for e in small[:40]:
         print(f"{e.device_time_total / 3:9.1f} us/step  n={e.count // 3:4d}  {e.key}")
