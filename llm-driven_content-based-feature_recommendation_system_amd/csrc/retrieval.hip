@@ -543,6 +543,13 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_scan_k(BfArgs a) {
   int64_t sbase[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) sbase[g] = ((q0 + 32 * g) * a.nsplit + split) * 2 + h;
+  float* bsp[G];
+  int* bip[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {  // MODE 1 stream buffers of this lane's queries
+    bsp[g] = MODE == 1 ? a.buf_s + sbase[g] * kStreamCap : nullptr;
+    bip[g] = MODE == 1 ? a.buf_i + sbase[g] * kStreamCap : nullptr;
+  }
 
   // staging: 8 threads per item row, 32 B each
   const int srow = tid >> 3, sb = (tid & 7) * 32;
@@ -583,17 +590,31 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_scan_k(BfArgs a) {
 #pragma unroll
         for (int g = 0; g < G; ++g) acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, ub[g][ks], acc[g], 0, 0, 0);
       }
+      // item ids in 32 bits (NI < 2^31, host-checked) and the split-end check only on the split's
+      // last tile. MODE 0 first compares a lane's tile max (v_max3) with its list minimum: the
+      // sorted insert is then skipped by most lanes once the lists have filled. (In MODE 1 about
+      // 0.25 % of the scores pass t_q, but some lane of a wave passes on ~90 % of the tiles, so a
+      // per-lane gate would not skip work there.)
+      const int jt0 = (int)j0;
+      const bool full_tile = j0 + kTile <= j_end;
+      const int jend = (int)j_end;
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         if (!q_ok[g]) continue;
+        if (MODE == 0) {
+          float mx = fmaxf(acc[g][0], acc[g][1]);
+#pragma unroll
+          for (int r = 2; r < 16; r += 2) mx = fmaxf(mx, fmaxf(acc[g][r], acc[g][r + 1]));
+          if (!(mx > ts[g][T - 1])) continue;  // no score of this lane enters its list
+        }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int64_t j = j0 + tile_row(r, h);
+          const int j = jt0 + tile_row(r, h);
           const float sc = acc[g][r];
           if (MODE == 0) {
-            if (sc > ts[g][T - 1] && j < j_end) {
+            if (sc > ts[g][T - 1] && (full_tile || j < jend)) {
               ts[g][T - 1] = sc;
-              ti[g][T - 1] = (int)j;
+              ti[g][T - 1] = j;
 #pragma unroll
               for (int t = T - 1; t > 0; --t) {
                 if (ts[g][t] > ts[g][t - 1]) {
@@ -602,10 +623,10 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_scan_k(BfArgs a) {
                 }
               }
             }
-          } else if (sc >= thr[g] && j < j_end) {
+          } else if (sc >= thr[g] && (full_tile || j < jend)) {
             if (cnt[g] < kStreamCap) {
-              a.buf_s[sbase[g] * kStreamCap + cnt[g]] = sc;
-              a.buf_i[sbase[g] * kStreamCap + cnt[g]] = (int)j;
+              bsp[g][cnt[g]] = sc;
+              bip[g][cnt[g]] = j;
             }
             ++cnt[g];
           }
@@ -658,50 +679,142 @@ __device__ __forceinline__ float query_norm(const float* U, int64_t ldu, int64_t
   return sqrtf(rsx::wave_sum_width(uv.x * uv.x + uv.y * uv.y, 64)) * 1.0000001f;
 }
 
-// P2: t_q = c_k - 2 delta_q (c_k: k-th best sampled candidate; -inf if fewer than k)
+// Order-preserving uint key of a float (larger float <=> larger key).
+__device__ __forceinline__ unsigned okey(float f) {
+  const unsigned u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float from_okey(unsigned k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+// K-th largest (1 <= K <= n) of v[0, n) in LDS, by a four-pass 8-bit radix select over okey
+// (integer LDS histograms; wave 0 finds each pass's digit with a 64-lane scan over 4 bins per
+// lane). Replaces a full bitonic sort where only the K-th value is needed. Every thread returns it.
+__device__ float block_kth_largest(const float* v, int n, int K, int* hist, int* sel) {
+  unsigned prefix = 0u, mask = 0u;
+  int krem = K;
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    for (int t = threadIdx.x; t < 256; t += blockDim.x) hist[t] = 0;
+    __syncthreads();
+    for (int t = threadIdx.x; t < n; t += blockDim.x) {
+      const unsigned k = okey(v[t]);
+      if ((k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1);
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {  // lane l owns digits 255-4l .. 252-4l (descending)
+      const int l = threadIdx.x;
+      int c[4], sum = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        c[j] = hist[255 - 4 * l - j];
+        sum += c[j];
+      }
+      int incl = sum;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (l >= o) incl += y;
+      }
+      const int excl = incl - sum;
+      if (excl < krem && krem <= incl) {
+        int acc = excl;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (acc + c[j] >= krem) {
+            sel[0] = 255 - 4 * l - j;
+            sel[1] = krem - acc;
+            break;
+          }
+          acc += c[j];
+        }
+      }
+    }
+    __syncthreads();
+    prefix |= (unsigned)sel[0] << shift;
+    mask |= 255u << shift;
+    krem = sel[1];
+    __syncthreads();  // sel / hist are rewritten by the next pass
+  }
+  return from_okey(prefix);
+}
+
+// P2: t_q = c_k - 2 delta_q (c_k: k-th best sampled candidate; -inf if fewer than k valid ones)
 template <int NC>
 __global__ __launch_bounds__(256) void topk_bf16_thresh_k(const float* __restrict__ cs, const int* __restrict__ ci,
                                                           int ncand, const float* __restrict__ U, int64_t ldu, int K,
                                                           const unsigned* wmax_bits, float* thr) {
   __shared__ float ss[NC];
-  __shared__ int si[NC];
+  __shared__ int hist[256], sel[2], nval_s;
   const int64_t q = blockIdx.x;
-  for (int t = threadIdx.x; t < NC; t += 256) {
-    const bool ok = t < ncand;
+  if (threadIdx.x == 0) nval_s = 0;
+  __syncthreads();
+  int nv = 0;
+  for (int t = threadIdx.x; t < ncand; t += 256) {
+    const bool ok = ci[q * ncand + t] != 0x7fffffff;
     ss[t] = ok ? cs[q * ncand + t] : -INFINITY;
-    si[t] = ok ? ci[q * ncand + t] : 0x7fffffff;
+    nv += ok ? 1 : 0;
   }
+  nv = rsx::wave_sum_width(nv, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(&nval_s, nv);
   const float delta = query_norm(U, ldu, q) * __uint_as_float(*wmax_bits) * kDeltaRel + 1e-30f;
   __syncthreads();
-  bitonic_desc_n(ss, si, NC);
-  if (threadIdx.x == 0) thr[q] = (si[K - 1] != 0x7fffffff) ? ss[K - 1] - 2.0f * delta : -INFINITY;
+  if (nval_s < K) {  // block-uniform
+    if (threadIdx.x == 0) thr[q] = -INFINITY;
+    return;
+  }
+  const float ck = block_kth_largest(ss, ncand, K, hist, sel);
+  if (threadIdx.x == 0) thr[q] = ck - 2.0f * delta;
 }
 
-// P4: gather the query's appended entries, sort, rescore the margin set exactly, write top-k
+// P4: gather the query's appended entries; a_k = their k-th best (radix select); compact the
+// margin set {a >= a_k - 2 delta}, rescore it exactly in fp32, sort it by (e desc, idx asc) and
+// write the first k. (The margin set's order before the final sort does not matter: (e, idx)
+// pairs are distinct, so the output is deterministic.)
+constexpr int kMarginMax = 2048;
 __global__ __launch_bounds__(256) void topk_bf16_select_k(const float* __restrict__ bs, const int* __restrict__ bi,
                                                           const int* __restrict__ bn, int nstreams,
                                                           const float* __restrict__ U, int64_t ldu,
                                                           const float* __restrict__ I, int64_t ldi, int K,
                                                           const unsigned* wmax_bits, float* out_s, int64_t* out_i,
                                                           int* qcount, int* qmap) {
+  // LDS: the appended scores only (their item ids are read back from global for the margin set),
+  // so three workgroups fit per CU
   __shared__ float ss[kSelMax];
-  __shared__ int si[kSelMax];
+  __shared__ float ms[kMarginMax];
+  __shared__ int mi[kMarginMax];
   __shared__ int off[513];
+  __shared__ int hist[256], sel[2];
   __shared__ int bad_s, nsel_s;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t q = blockIdx.x;
   const float delta = query_norm(U, ldu, q) * __uint_as_float(*wmax_bits) * kDeltaRel + 1e-30f;
   if (tid == 0) { bad_s = 0; nsel_s = 0; }
-  // counts (nstreams <= 512) -> exclusive prefix in LDS
-  for (int t = tid; t < 512; t += 256) {
-    const int n = t < nstreams ? bn[q * nstreams + t] : 0;
-    if (n > kStreamCap) bad_s = 1;
-    off[t + 1] = n < kStreamCap ? n : kStreamCap;
-  }
   __syncthreads();
-  if (tid == 0) {
-    off[0] = 0;
-    for (int t = 1; t <= 512; ++t) off[t] += off[t - 1];
+  // counts (nstreams <= 512) -> exclusive prefix in LDS: wave 0, eight streams per lane
+  if (wave == 0) {
+    int c8[8], sum = 0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int t = 8 * lane + u;
+      const int n = t < nstreams ? bn[q * nstreams + t] : 0;
+      if (n > kStreamCap) bad_s = 1;
+      c8[u] = n < kStreamCap ? n : kStreamCap;
+      sum += c8[u];
+    }
+    int incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    int run = incl - sum;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      off[8 * lane + u] = run;
+      run += c8[u];
+    }
+    if (lane == 63) off[512] = incl;
   }
   __syncthreads();
   const int total = off[512];
@@ -709,59 +822,76 @@ __global__ __launch_bounds__(256) void topk_bf16_select_k(const float* __restric
     if (tid == 0) qmap[atomicAdd(qcount, 1)] = (int)q;
     return;
   }
-  for (int s0 = 0; s0 < nstreams; s0 += 8) {  // 32 threads per stream, 8 streams per pass
+  // 32 threads per stream, 8 streams per pass; eight passes' loads are issued before their LDS
+  // stores (one memory latency per 64 streams instead of per 8)
+  for (int s0 = 0; s0 < nstreams; s0 += 64) {
+    float v[8];
+    int dst[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int st = s0 + 8 * u + (tid >> 5), e = tid & 31;
+      dst[u] = -1;
+      if (st < nstreams) {
+        const int n = off[st + 1] - off[st];
+        if (e < n) {
+          dst[u] = off[st] + e;
+          v[u] = bs[(q * nstreams + st) * kStreamCap + e];
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (dst[u] >= 0) ss[dst[u]] = v[u];
+  }
+  __syncthreads();
+  const float thr = (total >= K) ? block_kth_largest(ss, total, K, hist, sel) - 2.0f * delta : -INFINITY;
+  // margin set: walk the streams again; the item ids of the selected entries come from global
+  for (int s0 = 0; s0 < nstreams; s0 += 8) {
     const int st = s0 + (tid >> 5), e = tid & 31;
     if (st < nstreams) {
-      const int n = off[st + 1] - off[st];
-      if (e < n) {
-        ss[off[st] + e] = bs[(q * nstreams + st) * kStreamCap + e];
-        si[off[st] + e] = bi[(q * nstreams + st) * kStreamCap + e];
+      const int o = off[st];
+      if (e < off[st + 1] - o && ss[o + e] >= thr) {
+        const int slot = atomicAdd(&nsel_s, 1);
+        if (slot < kMarginMax) mi[slot] = bi[(q * nstreams + st) * kStreamCap + e];
       }
     }
   }
-  int P = 1;
-  while (P < total) P <<= 1;
-  if (P < K) P = 1 << (32 - __builtin_clz(K - 1));
-  for (int t = total + tid; t < P; t += 256) {
-    ss[t] = -INFINITY;
-    si[t] = 0x7fffffff;
-  }
-  __syncthreads();
-  bitonic_desc_n(ss, si, P);
-  const bool have_k = si[K - 1] != 0x7fffffff;
-  const float thr = have_k ? ss[K - 1] - 2.0f * delta : -INFINITY;
-  int cnt = 0;
-  for (int t = tid; t < P; t += 256) cnt += (si[t] != 0x7fffffff && ss[t] >= thr) ? 1 : 0;
-  cnt = rsx::wave_sum_width(cnt, 64);
-  if (lane == 0) atomicAdd(&nsel_s, cnt);
   __syncthreads();
   const int n = nsel_s;
+  if (n > kMarginMax) {  // block-uniform: the exact kernels take this query
+    if (tid == 0) qmap[atomicAdd(qcount, 1)] = (int)q;
+    return;
+  }
   // exact fp32 rescoring: 32 lanes per item, float4 per lane, fixed-order shuffle reduction
   const int sub = lane >> 5, c = lane & 31;
   const float4 u4 = reinterpret_cast<const float4*>(U + q * ldu)[c];
-  for (int t0 = 0; t0 < n; t0 += 8) {
-    const int t = t0 + wave * 2 + sub;
-    float e = 0.0f;
-    if (t < n) {
-      const float4 w4 = reinterpret_cast<const float4*>(I + (int64_t)si[t] * ldi)[c];
-      e = u4.x * w4.x + u4.y * w4.y + u4.z * w4.z + u4.w * w4.w;
+  for (int t0 = 0; t0 < n; t0 += 32) {  // four items per half-wave in flight
+    float4 w4[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int t = t0 + 8 * u + wave * 2 + sub;
+      w4[u] = t < n ? reinterpret_cast<const float4*>(I + (int64_t)mi[t] * ldi)[c] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    for (int o = 16; o > 0; o >>= 1) e += __shfl_xor(e, o, 64);
-    __syncthreads();  // every read of ss (the margin count) is done before the first overwrite
-    if (t < n && c == 0) ss[t] = e;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int t = t0 + 8 * u + wave * 2 + sub;
+      float e = u4.x * w4[u].x + u4.y * w4[u].y + u4.z * w4[u].z + u4.w * w4[u].w;
+      for (int o = 16; o > 0; o >>= 1) e += __shfl_xor(e, o, 64);
+      if (t < n && c == 0) ms[t] = e;
+    }
   }
   int P2 = 1;
   while (P2 < n) P2 <<= 1;
   for (int t = n + tid; t < P2; t += 256) {
-    ss[t] = -INFINITY;
-    si[t] = 0x7fffffff;
+    ms[t] = -INFINITY;
+    mi[t] = 0x7fffffff;
   }
   __syncthreads();
-  bitonic_desc_n(ss, si, P2);
+  bitonic_desc_n(ms, mi, P2);
   for (int t = tid; t < K; t += 256) {
     const bool ok = t < n;
-    out_s[q * K + t] = ok ? ss[t] : -INFINITY;
-    out_i[q * K + t] = ok ? (int64_t)si[t] : -1;
+    out_s[q * K + t] = ok ? ms[t] : -INFINITY;
+    out_i[q * K + t] = ok ? (int64_t)mi[t] : -1;
   }
 }
 
