@@ -37,17 +37,11 @@ def main():
     else:
         x = torch.from_numpy(((rng.zipf(1.1, size=(a.rows, F)) - 1) % a.vocab).astype(np.int64)).to(dev)
     model.forward_logits(x)  # builds the weight images / packed tables in the module's cache
-    cache = model._fused_cache
-    names = model.field_names
-    V = [model.embedding_dict[n].weight for n in names]
-    W = [model.linear_model.embedding_dict[n].weight for n in names]
-    b1, b2 = model.dnn.linears[0].bias, model.dnn.linears[1].bias
-    wo = model.dnn_linear.weight.reshape(-1).contiguous()
+    st = model._fused_cache["fused_state"]  # device state kept by ops.deepfm_forward
     logit = torch.empty(a.rows, device=dev)
     prob = torch.empty(a.rows, device=dev)
-    args = (N.ptr(x), a.rows, F, N.ptr_array(V), N.ptr_array(W), N.ptr_array(cache["packed"]),
-            float(model.out.bias.item()), N.ptr(b1), N.ptr(b2), N.ptr(wo), N.ptr(cache["ws"]), N.ptr(logit),
-            N.ptr(prob), N.stream())
+    args = (N.ptr(x), a.rows, F, st["V"], st["W"], st["P"], float(model.out.bias.item()), st["b1"], st["b2"],
+            st["wo"], st["ws"], N.ptr(logit), N.ptr(prob), N.stream())
     ids = "zero" if a.zero else ("uniform" if a.uniform else "zipf1.1")
     for abl in a.abl.split(","):
         os.environ["RSX_DEEPFM_ABL"] = abl
