@@ -2655,8 +2655,15 @@ namespace {
 // workgroups while every split keeps >= 2 streamed tiles
 int plain_split(int64_t n_own, int64_t n_str) {
   const int64_t ob = (n_own + kOwnRows - 1) / kOwnRows;
+  // workgroup target: one round of two workgroups per CU (512 on MI355X) measured 8 % faster than
+  // 1024 over the DuoRec + SupCon passes at B = 8192 (tools/nce_plain_micro.py: 0.763 vs 0.830 ms;
+  // 256: 1.05, 2048: 0.93). RSX_NCE_PLAIN_WG overrides it (A/B).
+  static const int64_t target = [] {
+    const char* e = getenv("RSX_NCE_PLAIN_WG");
+    return (int64_t)(e ? atoi(e) : 2 * rsx::cu_count());
+  }();
   int ps = 1;
-  while (ps < 64 && ob * ps < 1024 && n_str >= (int64_t)ps * 4 * kTile) ps *= 2;
+  while (ps < 64 && ob * ps < target && n_str >= (int64_t)ps * 4 * kTile) ps *= 2;
   return ps;
 }
 struct X3Plan {
