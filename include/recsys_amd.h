@@ -174,6 +174,13 @@ int rsx_nce_grouped_fwd_grad(const float* A, const float* B, const float* bias, 
                              const int* row_col, const int* row_beg, const int* row_end, const int* exc_cols,
                              int64_t N, int64_t D, int64_t lda, int64_t ldb, float tau, int nsplit, float* ws,
                              float* out2, float* ga, void* stream);
+/* Measurement hooks (no reference counterpart; bench.py's roofline): while enabled,
+ * rsx_nce_grouped_fwd_grad brackets the fused forward kernel's own launch (not the B split or the
+ * merge) with two HIP events on its stream; rsx_kernel_events_read waits for them and writes up to
+ * max_n durations (ms, launch order), returning how many were recorded (-1 on a HIP error).
+ * Enabling clears the list. */
+int rsx_kernel_events(int on);
+int rsx_kernel_events_read(float* ms, int max_n);
 int rsx_nce_grouped_bwd(const float* A, const float* B, const float* bias, const float* colcnt, const int* row_col,
                         const int* row_beg, const int* row_end, const int* exc_cols, const int* col_beg,
                         const int* col_end, const int* exc_s, const int* exc_e, const int* exc_n, int64_t N,

@@ -23,6 +23,9 @@
 // gradient MFMA in the backward (no LDS round trip for dS).
 #include "rsx_common.h"
 #include <math.h>
+#include <mutex>
+#include <utility>
+#include <vector>
 
 namespace {
 
@@ -2896,6 +2899,53 @@ static bool fwdg_pipelined() {
   return v;
 }
 
+// Measurement hooks (include/recsys_amd.h): event pairs around the fused forward kernel's launch.
+namespace {
+struct KernelEvents {
+  std::mutex mu;
+  bool on = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+  void clear() {
+    for (auto& e : ev) {
+      (void)hipEventDestroy(e.first);
+      (void)hipEventDestroy(e.second);
+    }
+    ev.clear();
+  }
+};
+KernelEvents& kernel_events() {
+  static KernelEvents k;
+  return k;
+}
+}  // namespace
+
+RSX_API int rsx_kernel_events(int on) {
+  KernelEvents& k = kernel_events();
+  std::lock_guard<std::mutex> g(k.mu);
+  k.clear();
+  k.on = on != 0;
+  return 0;
+}
+
+RSX_API int rsx_kernel_events_read(float* ms, int max_n) {
+  RSX_ARG(ms != nullptr || max_n == 0, "null output");
+  KernelEvents& k = kernel_events();
+  std::lock_guard<std::mutex> g(k.mu);
+  int n = 0;
+  for (auto& e : k.ev) {
+    if (n >= max_n) break;
+    float t = 0.0f;
+    hipError_t err = hipEventSynchronize(e.second);
+    if (err == hipSuccess) err = hipEventElapsedTime(&t, e.first, e.second);
+    if (err != hipSuccess) {
+      rsx::set_error("%s: %s", __func__, hipGetErrorString(err));
+      return -1;
+    }
+    ms[n++] = t;
+  }
+  return n;
+}
+
 RSX_API int rsx_nce_grouped_fwd_grad(const float* A, const float* B, const float* bias, const float* colcnt,
                                      const int* row_col, const int* row_beg, const int* row_end,
                                      const int* exc_cols, int64_t N, int64_t D, int64_t lda, int64_t ldb, float tau,
@@ -2952,6 +3002,15 @@ RSX_API int rsx_nce_grouped_fwd_grad(const float* A, const float* B, const float
   launch_split(B, ldb, D, im.bhi, im.blo, st);
   RSX_LAUNCHED();
   const int blocks = (int)(rb1 * ns1 + (rbs - rb1) * (nsplit == 8 ? 8 : 0));
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  {
+    KernelEvents& k = kernel_events();
+    std::lock_guard<std::mutex> lk(k.mu);
+    if (k.on && hipEventCreate(&ev0) == hipSuccess && hipEventCreate(&ev1) == hipSuccess) {
+      (void)hipEventRecord(ev0, st);
+      k.ev.emplace_back(ev0, ev1);
+    }
+  }
   if (!piped)
     hipLaunchKernelGGL(nce_grouped_fwdg_x3_k, dim3(blocks), dim3(256), 0, st, g);
   else if (nw == 8 && fwdg_nt())
@@ -2963,6 +3022,7 @@ RSX_API int rsx_nce_grouped_fwd_grad(const float* A, const float* B, const float
   else
     hipLaunchKernelGGL((nce_grouped_fwdg_x3p_k<4, false>), dim3(blocks), dim3(256), 0, st, g);
   RSX_LAUNCHED();
+  if (ev1) (void)hipEventRecord(ev1, st);
   hipLaunchKernelGGL(nce_grouped_merge_g_k, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, A, B, bias, row_col,
                      N, lda, ldb, g.inv_tau, ns1, part, opart, lse, row_loss, row_valid, ga, rb1 * rows_wg, 8,
                      nsplit);
