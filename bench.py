@@ -577,17 +577,25 @@ def train_bench(args, global_batch, steps, warmup, items, cfg, model, item_tower
     # Each step enqueues its work, then builds the NEXT batch's data-dependent index (packed
     # tokens, grouped targets: the host-synchronising size queries) on a side stream while the
     # GPU runs the step (dist.prepare_step_index_async). Every timed step still builds one index.
+    # One rank: the index is built two steps ahead on a background host thread
+    # (dist.IndexPrefetcher), so its host synchronisations never hold up the enqueueing of
+    # the steps (RSX_PREFETCH_THREAD=0: inline, one step ahead, as with several ranks).
     pending = {}
     enqueue = []
+    pf = None
+    if world == 1 and not args.no_prefetch_index and os.environ.get("RSX_PREFETCH_THREAD", "1") != "0":
+        pf = D.IndexPrefetcher()
 
     def step(i):
         h0 = time.perf_counter()
-        ix = pending.pop(i, None)
+        ix = pf.pop(i) if pf is not None else pending.pop(i, None)
         if ix is None:
             ix = D.prepare_step_index(batches[i % 2], pretrained_lookup=lookup)
         out = D.contrastive_step_dp(model, item_tower, log_q, batches[i % 2], opt, cfg, lookup, bucket, index=ix)
         enqueue.append(time.perf_counter() - h0)
-        if not args.no_prefetch_index:
+        if pf is not None:
+            pf.submit(i + 2, batches[i % 2], pretrained_lookup=lookup)
+        elif not args.no_prefetch_index:
             pending[i + 1] = D.prepare_step_index_async(batches[(i + 1) % 2], pretrained_lookup=lookup)
         return out
 
@@ -615,8 +623,10 @@ def train_bench(args, global_batch, steps, warmup, items, cfg, model, item_tower
     fwdg_kernel_ms = [float(kev[i]) for i in range(max(n_kev, 0))]
     N.lib().rsx_kernel_events(0)
     retries = torch.cuda.memory_stats().get("num_alloc_retries", 0) - retries0
-    # drain the prefetched index of the step that never ran
+    # drain the prefetched indexes of the steps that never ran
     pending.clear()
+    if pf is not None:
+        pf.close()
     torch.cuda.synchronize()
     elapsed = torch.tensor([t1 - t0], device=device, dtype=torch.float64)
     if world > 1:

@@ -190,7 +190,8 @@ int rsx_nce_grouped_bwd(const float* A, const float* B, const float* bias, const
 
 /* ---- static-profile embeddings: gated lookups of several tiny tables, concatenated ------
  * out[b, off_j + c] = E_j[ids_j[b]][c] * gate[j]; backward accumulates dE_j (padding_idx rows
- * skipped) and dgate[j] (both added into). Replaces the nine nn.Embedding lookups x u_g of
+ * skipped) and dgate[j] (both added into; one workgroup per table sums in a fixed order, so
+ * the gradients are identical run to run). Replaces the nine nn.Embedding lookups x u_g of
  * tower_code/v1_refine_usertower.py:472-494 (and their sort-based embedding backward).
  * <= 16 tables, <= 256 columns, <= 4096 table floats in total. */
 int rsx_static_embed_fwd(const int64_t* const* ids, const float* const* tables, const int64_t* table_rows,
@@ -255,6 +256,16 @@ int rsx_gemm_x3(const float* A, int64_t lda, const float* B, int64_t ldb, const 
  * each token. K 128 or 256, N % 128 == 0, every pointer 16-byte aligned. */
 int rsx_gemm_x3_rowadd(const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias, int64_t M, int N,
                        int K, const float* R, int64_t ldr, const int64_t* ridx, float* C, int64_t ldc, void* stream);
+/* S = X + dropout_p(A . B^T + bias); Y = LayerNorm(S) * ln_w + ln_b; mean / rstd per row.
+ * Replaces a norm_first encoder layer's `x = x + dropout(out_proj(attn)); norm2(x)`
+ * (v1_refine_usertower.py:343-352, nn.TransformerEncoderLayer._sa_block + norm2) in one
+ * weight-stationary GEMM: the add and the LayerNorm run in its epilogue. N = 128, K 128 or 256,
+ * every pointer 16-byte aligned; dropout mask = rsx_ln_fwd's (hash(seed, m * N + n)), so
+ * rsx_ln_bwd (ds_in, dres) is its backward. ln_w / ln_b nullable (1 / 0). */
+int rsx_gemm_x3_addln(const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias, int64_t M, int N,
+                      int K, const float* X, int64_t ldx, float p_drop, uint64_t seed, const float* ln_w,
+                      const float* ln_b, float eps, float* S, int64_t lds, float* Y, int64_t ldy, float* mean,
+                      float* rstd, void* stream);
 
 /* ---- A14: retrieval top-k ------------------------------------------------------------
  * scores = U I^T (fp32 MFMA, never materialised), per query the k best items sorted by

@@ -18,6 +18,9 @@
 //                  aux = gelu_erf'(z), the backward's multiplier (saved instead of z)
 //   EPI_DGELU_DROP C = acc * keep(m, n) / (1 - p) * aux[m][n]   (backward of the above:
 //                  acc = dAct = dY2 . W2)
+//   EPI_ADDLN      (weight-stationary, N = 128) the residual add + LayerNorm after the
+//                  attention out-projection: C = s = aux + dropout_p(acc + bias),
+//                  y = LayerNorm(s) * ln_w + ln_b, with the row's mean / rstd saved
 //
 // Tiling: 128 x 128 output tile per 256-thread workgroup (four waves of 64 x 64 = 2 x 2
 // MFMA tiles), K staged 16 at a time, double-buffered in LDS with register prefetch and one
@@ -40,7 +43,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kBM = 128, kBN = 128, kBK = RSX_GEMM_BK;
 constexpr int kRow = kBK + 8;  // bf16 per LDS row (80 B at BK 32, 48 B at BK 16: conflict-free b128 reads)
 constexpr int kF4 = kBK / 8;   // float4 loads per thread and operand per stage (two threads per row)
-constexpr int EPI_BIAS = 0, EPI_GELU_DROP = 1, EPI_DGELU_DROP = 2, EPI_ROWADD = 3;
+constexpr int EPI_BIAS = 0, EPI_GELU_DROP = 1, EPI_DGELU_DROP = 2, EPI_ROWADD = 3, EPI_ADDLN = 4;
 #ifndef RSX_GEMM_BLOCKS
 #define RSX_GEMM_BLOCKS (1 << 30)  // workgroup budget of the multi-tile stream: at BK 16 one tile each measured best
 #endif
@@ -92,6 +95,13 @@ struct GArgs {
   float* aux;         // [M, ldaux]: gelu'(pre) (written by EPI_GELU_DROP, read by EPI_DGELU_DROP);
                       // EPI_ROWADD: the row table R [*, ldaux]
   const int64_t* ridx;  // EPI_ROWADD: C[m] += R[ridx[m]]
+  float* y;             // EPI_ADDLN: LayerNorm output [M, ldy]; aux = the residual x [M, ldaux]
+  const float* ln_w;    // EPI_ADDLN: LayerNorm weight / bias [N]
+  const float* ln_b;
+  float* mean;          // EPI_ADDLN: [M] row statistics for the backward
+  float* rstd;
+  float eps;
+  int64_t ldy;
   int64_t lda, ldb, ldc, ldaux, M;
   int N, K, epi, tiles_n, tiles, per;
   rsx::Dropout drop;
@@ -309,6 +319,12 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_ws_k(WsArgs w) {
   }
   __shared__ __attribute__((aligned(16))) float sBias[NBW];
   for (int n = tid; n < NBW; n += kWsThreads) sBias[n] = (EPI != EPI_DGELU_DROP && a.bias) ? a.bias[n0 + n] : 0.0f;
+  __shared__ __attribute__((aligned(16))) float sLn[EPI == EPI_ADDLN ? 2 * NBW : 4];
+  if (EPI == EPI_ADDLN)
+    for (int n = tid; n < NBW; n += kWsThreads) {
+      sLn[n] = a.ln_w ? a.ln_w[n] : 1.0f;
+      sLn[NBW + n] = a.ln_b ? a.ln_b[n] : 0.0f;
+    }
   __syncthreads();
 
   // this wave's strips: (grp + groups * it) * kWsWaves + wave, it = 0, 1, ...
@@ -344,8 +360,9 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_ws_k(WsArgs w) {
     // loaded before its MFMAs (vmcnt retires in order, so a load issued at the epilogue
     // would drain the prefetched strips)
     if (EPI == EPI_ROWADD) xrow = a.aux + a.ridx[m] * a.ldaux + n0 + 4 * h;
+    if (EPI == EPI_ADDLN) xrow = a.aux + m * a.ldaux + 4 * h;
     float4 z[NT][4];
-    if ((EPI == EPI_DGELU_DROP || EPI == EPI_ROWADD) && q == KC - 1) {
+    if ((EPI == EPI_DGELU_DROP || EPI == EPI_ROWADD || EPI == EPI_ADDLN) && q == KC - 1) {
 #pragma unroll
       for (int j = 0; j < NT; ++j)
 #pragma unroll
@@ -371,6 +388,63 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_ws_k(WsArgs w) {
     // written to row M-1 again (same values, dropout hashed on the clamped row), so the stores
     // need no branch.
     const uint32_t e0 = (uint32_t)m * (uint32_t)a.N + (uint32_t)(n0 + 4 * h);
+    if constexpr (EPI == EPI_ADDLN) {
+      // lane (c, h) holds 64 of row m's 128 sums; lane c + 32 the other 64 (one xor-32 swap
+      // per statistic). Two-pass variance over the registers, as ln_fwd_k.
+      float sum = 0.0f;
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int o = 32 * j + 8 * g;
+          const float4 bb = *reinterpret_cast<const float4*>(&sBias[o + 4 * h]);
+          const float zz[4] = {z[j][g].x, z[j][g].y, z[j][g].z, z[j][g].w};
+          const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float v = acc[j][4 * g + e] + bv[e];
+            if (a.drop.active()) v = keep(a.drop, e0 + o + e) ? v * a.drop.scale : 0.0f;
+            v += zz[e];
+            acc[j][4 * g + e] = v;
+            sum += v;
+          }
+        }
+      sum += __shfl_xor(sum, 32, 64);
+      const float mu = sum * (1.0f / NBW);
+      float sq = 0.0f;
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float d = acc[j][r] - mu;
+          sq += d * d;
+        }
+      sq += __shfl_xor(sq, 32, 64);
+      const float rs = 1.0f / sqrtf(sq * (1.0f / NBW) + a.eps);
+      float* yrow = a.y + m * a.ldy + 4 * h;
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int o = 32 * j + 8 * g;
+          const float4 ww = *reinterpret_cast<const float4*>(&sLn[o + 4 * h]);
+          const float4 lb = *reinterpret_cast<const float4*>(&sLn[NBW + o + 4 * h]);
+          const float s0 = acc[j][4 * g], s1 = acc[j][4 * g + 1], s2 = acc[j][4 * g + 2], s3 = acc[j][4 * g + 3];
+          *reinterpret_cast<float4*>(crow + o) = make_float4(s0, s1, s2, s3);
+          *reinterpret_cast<float4*>(yrow + o) =
+              make_float4((s0 - mu) * rs * ww.x + lb.x, (s1 - mu) * rs * ww.y + lb.y, (s2 - mu) * rs * ww.z + lb.z,
+                          (s3 - mu) * rs * ww.w + lb.w);
+        }
+      if (h == 0) {
+        a.mean[m] = mu;
+        a.rstd[m] = rs;
+      }
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < NT; ++j)
 #pragma unroll
@@ -494,6 +568,8 @@ void launch_ws_w(const GArgs& g, hipStream_t st) {
   if (g.epi == EPI_BIAS) hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_BIAS, WV>), dim3(grid), dim3(kWsThreads), 0, st, w);
   else if (g.epi == EPI_ROWADD)
     hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_ROWADD, WV>), dim3(grid), dim3(kWsThreads), 0, st, w);
+  else if (g.epi == EPI_ADDLN)
+    hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_ADDLN, WV>), dim3(grid), dim3(kWsThreads), 0, st, w);
   else if (g.epi == EPI_GELU_DROP)
     hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_GELU_DROP, WV>), dim3(grid), dim3(kWsThreads), 0, st, w);
   else hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_DGELU_DROP, WV>), dim3(grid), dim3(kWsThreads), 0, st, w);
@@ -575,6 +651,38 @@ RSX_API int rsx_gemm_x3_rowadd(const float* A, int64_t lda, const float* B, int6
   g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.ldaux = ldr; g.M = M;
   g.N = N; g.K = K; g.epi = EPI_ROWADD;
   g.drop = rsx::make_dropout(0.0f, 0);
+  hipStream_t st = (hipStream_t)stream;
+  if (K == 128) launch_ws<1, 128>(g, st);
+  else launch_ws<2, 128>(g, st);
+  RSX_LAUNCHED();
+  return 0;
+}
+
+// s = X + dropout_p(A . B^T + bias), y = LayerNorm(s) (ln_w, ln_b, eps), mean / rstd per row:
+// the attention out-projection of a norm_first encoder layer fused with the residual add and the
+// LayerNorm after it (v1_refine_usertower.py:343-352: x = x + drop(out_proj(mha(...)));
+// norm2(x)). N = 128 (one column block holds the whole row), K in {128, 256}. The dropout mask
+// is rsx_ln_fwd's (hash of m * N + n), so rsx_ln_bwd's backward of the add + LayerNorm applies.
+RSX_API int rsx_gemm_x3_addln(const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias,
+                              int64_t M, int N, int K, const float* X, int64_t ldx, float p_drop, uint64_t seed,
+                              const float* ln_w, const float* ln_b, float eps, float* S, int64_t lds, float* Y,
+                              int64_t ldy, float* mean, float* rstd, void* stream) {
+  RSX_ARG(A && B && X && S && Y && mean && rstd, "null tensor");
+  RSX_ARG(M >= 0 && N == 128 && (K == 128 || K == 256), "N must be 128, K 128 or 256");
+  RSX_ARG(lda >= K && ldb >= K && ldx >= N && lds >= N && ldy >= N && lda % 4 == 0 && ldb % 4 == 0 &&
+              ldx % 4 == 0 && lds % 4 == 0 && ldy % 4 == 0, "bad leading dimensions");
+  RSX_ARG(((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0 && ((uintptr_t)X % 16) == 0 &&
+              ((uintptr_t)S % 16) == 0 && ((uintptr_t)Y % 16) == 0, "A/B/X/S/Y must be 16-byte aligned");
+  RSX_ARG(p_drop >= 0.0f && p_drop < 1.0f, "p_drop must be in [0, 1)");
+  RSX_ARG(M * (int64_t)N < (1LL << 32), "M * N must be < 2^32 (dropout element index)");
+  RSX_ARG(eps > 0.0f, "eps must be positive");
+  if (M == 0) return 0;
+  GArgs g = {};
+  g.A = A; g.B = B; g.bias = bias; g.C = S; g.aux = const_cast<float*>(X); g.ridx = nullptr;
+  g.y = Y; g.ln_w = ln_w; g.ln_b = ln_b; g.mean = mean; g.rstd = rstd; g.eps = eps; g.ldy = ldy;
+  g.lda = lda; g.ldb = ldb; g.ldc = lds; g.ldaux = ldx; g.M = M;
+  g.N = N; g.K = K; g.epi = EPI_ADDLN;
+  g.drop = rsx::make_dropout(p_drop, seed);
   hipStream_t st = (hipStream_t)stream;
   if (K == 128) launch_ws<1, 128>(g, st);
   else launch_ws<2, 128>(g, st);

@@ -7,10 +7,9 @@
 // u_g[j] = sigmoid(static_gate)[j], concatenated before cont_proj's part). PyTorch runs one
 // gather per table forward and one sort-based embedding backward (~8 kernels) per table.
 // Here: one forward kernel and one backward kernel for all tables. The tables are tiny (a
-// few hundred floats), so each backward workgroup accumulates the table gradients of its
-// row chunk in LDS and flushes the non-zero entries with one global atomic each; the gate
-// gradients sum_b <dout_j, E_j[id_j[b]]> take the same route. padding_idx rows (nn.Embedding
-// semantics) receive no gradient.
+// few hundred floats): the backward gives each table one workgroup that sums its gradient and
+// its gate gradient sum_b <dout_j, E_j[id_j[b]]> over the users in a fixed order
+// (deterministic, no atomics). padding_idx rows (nn.Embedding semantics) receive no gradient.
 #include "rsx_common.h"
 
 namespace {
@@ -55,51 +54,66 @@ __global__ __launch_bounds__(256) void static_embed_fwd_k(SArgs a) {
   }
 }
 
-__global__ __launch_bounds__(256) void static_embed_bwd_k(SArgs a) {
-  __shared__ float s_grad[kMaxFloats];
-  __shared__ float s_gate[kMaxTab];
-  int total = 0;
-  for (int j = 0; j < a.ntab; ++j) total = a.lds_off[j] + a.rows[j] * a.dim[j];
-  for (int i = threadIdx.x; i < total; i += blockDim.x) s_grad[i] = 0.0f;
-  if (threadIdx.x < kMaxTab) s_gate[threadIdx.x] = 0.0f;
-  __syncthreads();
-  const int64_t b0 = (int64_t)blockIdx.x * a.rows_per_block;
-  int64_t b1 = b0 + a.rows_per_block;
-  if (b1 > a.B) b1 = a.B;
-  const int64_t n = (b1 - b0) * a.ncols;
+// Backward, deterministic: one 1024-thread workgroup per table owns every entry of dE_j and
+// dgate[j]. Thread (slice, c) walks the users b = slice, slice + nslice, ... in order, keeping
+// the column-c gradient of 16 table rows in registers (a select per row: the tables have <= 11
+// rows, larger ones take further 16-row passes); the slices' partials meet in LDS and are
+// summed in slice order, the gate partials by a fixed shuffle tree. Same result on every run
+// (no float atomics), added into dE_j / dgate like the atomics it replaces.
+constexpr int kBwdThreads = 1024, kRowChunk = 16;
+
+__global__ __launch_bounds__(1024) void static_embed_bwd_k(SArgs a) {
+  __shared__ float part[kBwdThreads * kRowChunk];  // [slice][row][col]: nslice * dim <= 1024
+  __shared__ float wsum[kBwdThreads / 64];
+  const int j = blockIdx.x, t = threadIdx.x;
+  const int dim = a.dim[j], R = a.rows[j], off = a.col_off[j];
+  const int nslice = kBwdThreads / dim;
+  const int cc = t % dim, sl = t / dim;
+  const bool active = sl < nslice;
+  const int64_t* ids = a.ids[j];
+  const float* tab = a.tab[j];
+  float* dtab = a.dtab[j];
+  const float g = a.gate ? a.gate[j] : 1.0f;
   float gsum = 0.0f;
-  int gj = -1;
-  for (int64_t e = threadIdx.x; e < n; e += blockDim.x) {
-    const int64_t b = b0 + e / a.ncols;
-    const int c = (int)(e % a.ncols);
-    const int j = table_of(a, c);
-    const int cc = c - a.col_off[j];
-    const int64_t id = a.ids[j][b];
-    const float d = a.dout[b * a.ld_out + c];
-    const float g = a.gate ? a.gate[j] : 1.0f;
-    if (a.dtab[j] && id != a.pad_idx[j])
-      __hip_atomic_fetch_add(&s_grad[a.lds_off[j] + id * a.dim[j] + cc], d * g, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (a.dgate) {
-      if (j != gj) {  // flush the running gate partial when the table changes
-        if (gj >= 0) __hip_atomic_fetch_add(&s_gate[gj], gsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        gsum = 0.0f;
-        gj = j;
+  for (int r0 = 0; r0 < R; r0 += kRowChunk) {
+    float acc[kRowChunk];
+#pragma unroll
+    for (int r = 0; r < kRowChunk; ++r) acc[r] = 0.0f;
+    if (active) {
+      for (int64_t b = sl; b < a.B; b += nslice) {
+        const int64_t id = ids[b];
+        const float d = a.dout[b * a.ld_out + off + cc];
+        if (r0 == 0 && a.dgate) gsum += d * tab[id * dim + cc];
+        const int64_t rel = id - r0;
+#pragma unroll
+        for (int r = 0; r < kRowChunk; ++r) acc[r] += rel == r ? d : 0.0f;
       }
-      gsum += d * a.tab[j][id * a.dim[j] + cc];
+#pragma unroll
+      for (int r = 0; r < kRowChunk; ++r) part[(sl * kRowChunk + r) * dim + cc] = acc[r];
+    }
+    __syncthreads();
+    if (dtab) {
+      for (int o = t; o < kRowChunk * dim; o += kBwdThreads) {
+        const int r = o / dim, c2 = o % dim;
+        if (r0 + r < R && r0 + r != a.pad_idx[j]) {
+          float sum = 0.0f;
+          for (int q = 0; q < nslice; ++q) sum += part[(q * kRowChunk + r) * dim + c2];
+          dtab[(int64_t)(r0 + r) * dim + c2] += sum * g;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (a.dgate) {
+    const float w = rsx::wave_sum_width(gsum, 64);
+    if ((t & 63) == 0) wsum[t >> 6] = w;
+    __syncthreads();
+    if (t == 0) {
+      float total = 0.0f;
+      for (int i = 0; i < kBwdThreads / 64; ++i) total += wsum[i];
+      a.dgate[j] += total;
     }
   }
-  if (a.dgate && gj >= 0) __hip_atomic_fetch_add(&s_gate[gj], gsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  __syncthreads();
-  for (int j = 0; j < a.ntab; ++j) {
-    if (!a.dtab[j]) continue;
-    const int m = a.rows[j] * a.dim[j];
-    for (int i = threadIdx.x; i < m; i += blockDim.x) {
-      const float v = s_grad[a.lds_off[j] + i];
-      if (v != 0.0f) atomicAdd(a.dtab[j] + i, v);
-    }
-  }
-  if (a.dgate && threadIdx.x < a.ntab) atomicAdd(a.dgate + threadIdx.x, s_gate[threadIdx.x]);
 }
 
 bool fill(SArgs& a, const int64_t* const* ids, const float* const* tables, const int64_t* rows, const int64_t* dims,
@@ -160,9 +174,8 @@ RSX_API int rsx_static_embed_bwd(const int64_t* const* ids, const float* const* 
   }
   if (B == 0) return 0;
   a.gate = gate; a.dgate = dgate; a.dout = dout; a.out = nullptr; a.B = B; a.ld_out = ld_dout;
-  a.rows_per_block = 128;
-  const int64_t blocks = (B + a.rows_per_block - 1) / a.rows_per_block;
-  hipLaunchKernelGGL(static_embed_bwd_k, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
+  a.rows_per_block = 0;
+  hipLaunchKernelGGL(static_embed_bwd_k, dim3((unsigned)ntab), dim3(kBwdThreads), 0, (hipStream_t)stream, a);
   RSX_LAUNCHED();
   return 0;
 }

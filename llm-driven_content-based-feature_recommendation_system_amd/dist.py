@@ -356,6 +356,41 @@ def prepare_step_index_async(batch, pretrained_vecs=None, pretrained_lookup=None
     return ix
 
 
+class IndexPrefetcher:
+    """prepare_step_index_async on one background host thread: the index's host
+    synchronisations (size queries behind the side stream's kernels, which wait for CU slots
+    while the step's loss kernels hold the whole chip) then block that thread instead of the
+    thread enqueueing the steps, so the main stream's queue never runs dry waiting for them.
+    One worker: indexes are built in submission order. Single-rank only — with several ranks
+    the index all-gathers (index_group) must stay in program order with the step's collectives."""
+
+    def __init__(self):
+        import concurrent.futures
+        if world()[1] > 1:
+            raise RuntimeError("IndexPrefetcher is single-rank only (use prepare_step_index_async with several ranks)")
+        self._ex = concurrent.futures.ThreadPoolExecutor(max_workers=1, thread_name_prefix="rsx-index")
+        self._pending = {}
+
+    def submit(self, key, batch, pretrained_vecs=None, pretrained_lookup=None):
+        dev = torch.cuda.current_device()
+
+        def work():
+            torch.cuda.set_device(dev)
+            return prepare_step_index_async(batch, pretrained_vecs, pretrained_lookup)
+
+        self._pending[key] = self._ex.submit(work)
+
+    def pop(self, key):
+        fut = self._pending.pop(key, None)
+        return None if fut is None else fut.result()
+
+    def close(self):
+        for fut in self._pending.values():
+            fut.result()
+        self._pending.clear()
+        self._ex.shutdown(wait=True)
+
+
 def _adopt(ix):
     """Order the current stream after an async-prepared index and keep its memory alive for it."""
     ev = getattr(ix, "ready", None)

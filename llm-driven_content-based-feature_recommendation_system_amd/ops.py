@@ -980,6 +980,60 @@ class _TokLinear(torch.autograd.Function):
         return dx, dw, db
 
 
+class _LinearAddLayerNorm(torch.autograd.Function):
+    """(s, LayerNorm(s)), s = x + dropout(a W^T + b): rsx_gemm_x3_addln (the add and the
+    LayerNorm in the GEMM's epilogue; the projection itself is never written). Backward: the
+    add + LayerNorm backward (rsx_ln_bwd, whose dres is the projection's gradient), then dA on
+    rsx_gemm_x3 and dW / db on the split-K weight-gradient kernel, as _TokLinear."""
+
+    @staticmethod
+    def forward(ctx, x, a, weight, bias, w, b, eps, p_drop, seed):
+        T, D = x.shape
+        s = torch.empty_like(x)
+        y = torch.empty_like(x)
+        mean = torch.empty(T, device=x.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        with timed("tok_linear_addln"):
+            rc = N.lib().rsx_gemm_x3_addln(N.ptr(a), a.stride(0), N.ptr(weight), weight.stride(0), N.ptr(bias), T, D,
+                                           a.shape[1], N.ptr(x), x.stride(0), p_drop, seed, N.ptr(w), N.ptr(b), eps,
+                                           N.ptr(s), s.stride(0), N.ptr(y), y.stride(0), N.ptr(mean), N.ptr(rstd),
+                                           N.stream())
+        N.check(rc, "gemm_x3_addln")
+        ctx.save_for_backward(a, weight, s, mean, rstd, w, b)
+        ctx.cfg = (p_drop, seed, bias is not None)
+        return s, y
+
+    @staticmethod
+    def backward(ctx, ds, dy):
+        a, weight, s, mean, rstd, w, b = ctx.saved_tensors
+        p_drop, seed, has_bias = ctx.cfg
+        need = ctx.needs_input_grad
+        if dy is None:
+            dy = torch.zeros_like(s)
+        dx, dres, dw, db = _ln_bwd(s, mean, rstd, w, b, 0, dy, ds, p_drop, seed, need[0], True, need[4], need[5])
+        da = gemm_x3(dres, weight.t(), tag="tok_linear_dx") if need[1] else None
+        dwt = dbt = None
+        if need[2] or (has_bias and need[3]):
+            dwt, dbt = linear_wgrad(dres, a, weight.shape, has_bias and need[3])
+        return dx, da, dwt, dbt, dw, db, None, None, None
+
+
+def linear_add_layer_norm(x, a, weight, bias, ln_weight, ln_bias, eps=1e-5, p_drop=0.0):
+    """(s, LayerNorm(s)) with s = x + dropout(linear(a, weight, bias)): a norm_first encoder
+    layer's attention out-projection, residual add and the LayerNorm after it in one kernel
+    (bf16x3 mode, D = 128, K 128 or 256); otherwise linear_tok + add_layer_norm."""
+    shp = x.shape
+    D = shp[-1]
+    if not (_x3_ok(weight.shape[0], weight.shape[1]) and D == 128 and weight.shape[0] == 128
+            and weight.shape[1] in (128, 256) and x.numel() > 0):
+        return add_layer_norm(x, linear_tok(a, weight, bias), ln_weight, ln_bias, eps, p_drop)
+    N.ensure_device(x)
+    seed = next_seed() if p_drop > 0 else 0
+    s, y = _LinearAddLayerNorm.apply(_c(x.reshape(-1, D)), _c(a.reshape(-1, a.shape[-1])), _c(weight), bias,
+                                     ln_weight, ln_bias, float(eps), float(p_drop), seed)
+    return s.reshape(shp), y.reshape(shp)
+
+
 def linear_tok(x, weight, bias=None):
     """F.linear over a token axis (x [..., K]) whose weight/bias gradients come from the
     split-K rsx_linear_wgrad kernel instead of the library GEMM (T >> N, K); forward and

@@ -12,6 +12,8 @@ issued through torch (hipBLASLt).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -47,11 +49,16 @@ class FeatureProcessor:
         return get_logq_probs(self.items["raw_probability"].reindex(self.item_ids).values, device)
 
 
+_ADDLN = os.environ.get("RSX_LINEAR_ADDLN", "1") != "0"
+
+
 def encoder_stack(layers, x, key_pad, p, training, causal=True, seg_off=None):
     """norm_first nn.TransformerEncoderLayer stack (gelu), reference semantics
     (v1_refine_usertower.py:343-352, item_tower.py:169-182):
       x = x + drop(out_proj(mha(norm1(x)))) ; x = x + drop(linear2(drop(gelu(linear1(norm2(x))))))
-    Each residual add is fused with the LayerNorm that follows it (ops.add_layer_norm), the
+    Each residual add is fused with the LayerNorm that follows it (ops.add_layer_norm; after the
+    attention that add and LayerNorm run in the out-projection GEMM's epilogue,
+    ops.linear_add_layer_norm, unless RSX_LINEAR_ADDLN=0), the
     first norm1 folds the residual path's gradient into its backward (ops.layer_norm_pass), the
     last residual add + dropout is one pass (ops.add_dropout); the token linears run on the
     bf16x3 GEMMs (ops.linear_tok), the feed-forward's GELU and dropout in their epilogues
@@ -67,8 +74,12 @@ def encoder_stack(layers, x, key_pad, p, training, causal=True, seg_off=None):
         sa = layer.self_attn
         a = ops.qkv_mha(h, sa.in_proj_weight, sa.in_proj_bias, key_pad, sa.num_heads, causal=causal, p_drop=p,
                         seg_off=seg_off)
-        a = ops.linear_tok(a, sa.out_proj.weight, sa.out_proj.bias)
-        x, h = ops.add_layer_norm(x, a, layer.norm2.weight, layer.norm2.bias, layer.norm2.eps, p)
+        if fused and _ADDLN:
+            x, h = ops.linear_add_layer_norm(x, a, sa.out_proj.weight, sa.out_proj.bias, layer.norm2.weight,
+                                             layer.norm2.bias, layer.norm2.eps, p)
+        else:
+            a = ops.linear_tok(a, sa.out_proj.weight, sa.out_proj.bias)
+            x, h = ops.add_layer_norm(x, a, layer.norm2.weight, layer.norm2.bias, layer.norm2.eps, p)
         f = ops.ffn(h, layer.linear1.weight, layer.linear1.bias, layer.linear2.weight, layer.linear2.bias, p,
                     training)
         if i + 1 < len(layers):

@@ -729,6 +729,43 @@ def test_add_layer_norm_residual_and_dropout(gpu):
     torch.testing.assert_close(rr.grad, torch.where(kept, gs / (1 - p), torch.zeros_like(gs)), atol=1e-5, rtol=1e-5)
 
 
+@pytest.mark.parametrize("K,M", [(128, 999), (256, 4101)])
+def test_linear_add_layer_norm_fused(gpu, K, M):
+    """rsx_gemm_x3_addln (out-projection + residual add + LayerNorm in one epilogue): p = 0 against
+    torch fp32 (forward and every gradient); p > 0 against the unfused linear_tok + add_layer_norm
+    with the same dropout seed (same mask, same gradients)."""
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(M, 128, generator=g).to(gpu)
+    a = torch.randn(M, K, generator=g).to(gpu)
+    W = (torch.randn(128, K, generator=g) / K ** 0.5).to(gpu)
+    bW = torch.randn(128, generator=g).to(gpu) * 0.1
+    w = (torch.rand(128, generator=g) + 0.5).to(gpu)
+    b = torch.randn(128, generator=g).to(gpu)
+    gs = torch.randn(M, 128, generator=g).to(gpu)
+    gy = torch.randn(M, 128, generator=g).to(gpu)
+
+    def run(impl, p=0.0, seed=0):
+        xx, aa, WW, bb, ww, lb = (t.clone().requires_grad_() for t in (x, a, W, bW, w, b))
+        if impl == "fused":
+            s, y = ops._LinearAddLayerNorm.apply(xx, aa, WW, bb, ww, lb, 1e-5, p, seed)
+        elif impl == "unfused":
+            s, y = ops._AddLayerNorm.apply(xx, ops.linear_tok(aa, WW, bb), ww, lb, 1e-5, p, seed)
+        else:
+            s = xx + F.linear(aa, WW, bb)
+            y = F.layer_norm(s, (128,), ww, lb, 1e-5)
+        ((s * gs).sum() + (y * gy).sum()).backward()
+        return [s.detach(), y.detach(), xx.grad, aa.grad, WW.grad, bb.grad, ww.grad, lb.grad]
+
+    for u, r in zip(run("fused"), run("torch")):  # bf16x3 products: ~1e-5 of the largest entry
+        torch.testing.assert_close(u, r, atol=2e-4 + 2e-5 * r.abs().max().item(), rtol=1e-4)
+    fu, un = run("fused", 0.2, 1234567), run("unfused", 0.2, 1234567)
+    torch.testing.assert_close(fu[0], un[0], atol=0, rtol=0)  # same products, same mask, same add
+    for u, r in zip(fu[1:], un[1:]):  # row statistics summed in another order: ulp-level y, dres
+        torch.testing.assert_close(u, r, atol=2e-5 + 1e-5 * r.abs().max().item(), rtol=1e-5)
+    kept = (fu[0] - x).abs() > 0
+    assert abs(kept.float().mean().item() - 0.8) < 0.02
+
+
 def test_static_embed_against_torch(gpu):
     """Nine gated tiny-table lookups (static profile): forward bit-exact vs torch, table and
     gate gradients (padding_idx 0 rows excluded) vs torch autograd (1e-5)."""

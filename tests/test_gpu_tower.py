@@ -162,3 +162,43 @@ def test_gated_off_tables_still_decay(gpu):
         assert g is not None and torch.count_nonzero(g) == 0, n
         torch.testing.assert_close(params[n].detach(), before[n] * (1 - cfg.lr * cfg.weight_decay),
                                    atol=0, rtol=1e-6)
+
+
+def test_index_prefetcher_steps_equal_inline(gpu):
+    """dist.IndexPrefetcher (indexes built two steps ahead on a background thread, the bench's
+    single-rank loop) gives exactly the inline-index training trajectory: same losses, same
+    parameters after four AdamW steps over two alternating batches with dropout."""
+    from recsys_amd import dist as Dd
+    cfg = small_cfg(num_items=500, dropout=0.2)
+    items = small_universe(500)
+    batches = [to_dev(synth.make_batch(items, 64, seed=s), gpu) for s in (31, 32)]
+    lookup = items.pretrained.to(gpu)
+
+    def run(prefetch):
+        torch.manual_seed(0)
+        model = T.SASRecUserTower(cfg).to(gpu).train()
+        it = TT.SASRecItemTower(500, 128, items.log_q.clone()).to(gpu)
+        it.init_from_pretrained(lookup)
+        it.set_freeze_state(False)
+        opt = torch.optim.AdamW(list(model.parameters()) + list(it.parameters()), lr=cfg.lr)
+        bucket = Dd.GradBucket(list(model.parameters()) + list(it.parameters()))
+        pf = Dd.IndexPrefetcher() if prefetch else None
+        losses = []
+        for i in range(4):
+            ix = pf.pop(i) if pf else None
+            if ix is None:
+                ix = Dd.prepare_step_index(batches[i % 2], pretrained_lookup=lookup)
+            out = Dd.contrastive_step_dp(model, it, it.log_q, batches[i % 2], opt, cfg, lookup, bucket, index=ix)
+            losses.append([float(v) for v in out])
+            if pf:
+                pf.submit(i + 2, batches[i % 2], pretrained_lookup=lookup)
+        if pf:
+            pf.close()
+        torch.cuda.synchronize()
+        return losses, [p.detach().clone() for p in model.parameters()]
+
+    l0, p0 = run(False)
+    l1, p1 = run(True)
+    assert l0 == l1
+    for a, b in zip(p0, p1):
+        assert torch.equal(a, b)
