@@ -17,6 +17,7 @@
 // The A operand of token pair (2s, 2s+1) is dY[2s+h][n] on lane (n, h): a plain row read of
 // the token-major LDS tile, so no transpose is needed anywhere.
 #include "rsx_common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -205,8 +206,10 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_k(WArgs a) {
   for (int q = 0; q < kFpt; ++q) dbp[q] = 0.0f;
 
   const int srow = tid / (kTile / kFpt), scol = (tid % (kTile / kFpt)) * kFpt;
-  float4 py[kFpt / 4], px[kFpt / 4];
-  auto gload = [&](int64_t t0) {
+  // two register sets: stage s + 2 is in flight while stage s is multiplied and stage s + 1
+  // is converted into LDS (one stage in flight left each workgroup waiting on HBM latency)
+  float4 py0[kFpt / 4], px0[kFpt / 4], py1[kFpt / 4], px1[kFpt / 4];
+  auto gload = [&](int64_t t0, float4 (&py)[kFpt / 4], float4 (&px)[kFpt / 4]) {
     const int64_t t = t0 + srow;
     const bool ok = t < t_end;
     const bool oky = ok && n0 + scol < a.N;
@@ -223,7 +226,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_k(WArgs a) {
       px[q] = okx ? vx : z;
     }
   };
-  auto lstore = [&](int buf) {
+  auto lstore = [&](int buf, const float4 (&py)[kFpt / 4], const float4 (&px)[kFpt / 4]) {
 #pragma unroll
     for (int q = 0; q < kFpt / 8; ++q) {
       const int o = img_off(srow, scol + 8 * q);
@@ -254,39 +257,48 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_k(WArgs a) {
     const bf16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(&img[o1]));
     return __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
   };
+  auto compute = [&](int cur) {
+    if (!live) return;
+#pragma unroll
+    for (int ks = 0; ks < kStageX3 / 16; ++ks) {
+      bf16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        ah[i] = rd(sY[cur].hi, ks, 2 * wn + i);
+        al[i] = rd(sY[cur].lo, ks, 2 * wn + i);
+        bh[i] = rd(sX[cur].hi, ks, 2 * wk + i);
+        bl[i] = rd(sX[cur].lo, ks, 2 * wk + i);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+    }
+  };
 
   if (t_begin < t_end) {
-    gload(t_begin);
-    lstore(0);
+    // stage s lives in LDS buffer s & 1; even stages load into set 0, odd into set 1. Loads past
+    // t_end read row 0 and are zeroed (never stored: the loop ends first).
+    const int nst = (int)((t_end - t_begin + kStageX3 - 1) / kStageX3);
+    gload(t_begin, py0, px0);
+    gload(t_begin + kStageX3, py1, px1);
+    lstore(0, py0, px0);
     __syncthreads();
-    int cur = 0;
-    for (int64_t t0 = t_begin; t0 < t_end; t0 += kStageX3) {
-      const bool has_next = t0 + kStageX3 < t_end;
-      if (has_next) gload(t0 + kStageX3);
-      if (live) {
-#pragma unroll
-        for (int ks = 0; ks < kStageX3 / 16; ++ks) {
-          bf16x8 ah[2], al[2], bh[2], bl[2];
-#pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            ah[i] = rd(sY[cur].hi, ks, 2 * wn + i);
-            al[i] = rd(sY[cur].lo, ks, 2 * wn + i);
-            bh[i] = rd(sX[cur].hi, ks, 2 * wk + i);
-            bl[i] = rd(sX[cur].lo, ks, 2 * wk + i);
-          }
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-            }
-        }
-      }
-      if (has_next) lstore(cur ^ 1);  // cur^1 was read in the previous stage, fenced by its barrier
+    for (int st = 0;; st += 2) {
+      gload(t_begin + (int64_t)(st + 2) * kStageX3, py0, px0);
+      compute(0);
+      if (st + 1 >= nst) break;
+      lstore(1, py1, px1);
       __syncthreads();
-      cur ^= 1;
+      gload(t_begin + (int64_t)(st + 3) * kStageX3, py1, px1);
+      compute(1);
+      if (st + 2 >= nst) break;
+      lstore(0, py0, px0);
+      __syncthreads();
     }
   }
   if (live) {
@@ -403,7 +415,11 @@ int wgrad_launch(bool x3, const float* dY, int64_t ldy, const float* X, int64_t 
   const int blocks = a.tiles_n * a.tiles_k * a.nsplit;
   // 16-token stages measured faster for three or more output row tiles (tools/gemm_micro.py wgrad_384x128:
   // 0.119 vs 0.146 ms) and slower for fewer (wgrad_128x256: 0.075 vs 0.068 ms).
-  if (x3 && a.tiles_n >= 3) hipLaunchKernelGGL(wgrad_x3_k<16>, dim3(blocks), dim3(256), 0, st, a);
+  static const int stage16_min_tiles = [] {  // RSX_WGRAD_STAGE16_TILES: A/B of the stage choice
+    const char* e = getenv("RSX_WGRAD_STAGE16_TILES");
+    return e ? atoi(e) : 3;
+  }();
+  if (x3 && a.tiles_n >= stage16_min_tiles) hipLaunchKernelGGL(wgrad_x3_k<16>, dim3(blocks), dim3(256), 0, st, a);
   else if (x3) hipLaunchKernelGGL(wgrad_x3_k<32>, dim3(blocks), dim3(256), 0, st, a);
   else hipLaunchKernelGGL(wgrad_k, dim3(blocks), dim3(256), 0, st, a);
   RSX_LAUNCHED();

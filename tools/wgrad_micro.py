@@ -11,7 +11,7 @@ import recsys_amd  # noqa: E402,F401
 from recsys_amd import ops  # noqa: E402
 
 dev = torch.device("cuda", 0)
-T = 80946
+T = int(os.environ.get("T", "317506"))  # packed tokens of the headline step (both views)
 res = {}
 for (n, k) in [(384, 128), (128, 128), (256, 128), (128, 256)]:
     dy = torch.randn(T, n, device=dev)
