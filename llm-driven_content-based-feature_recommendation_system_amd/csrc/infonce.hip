@@ -564,6 +564,7 @@ __global__ __launch_bounds__(256) void nce_sum_splits_k(const float* part, int n
   const int64_t total4 = n * kD / 4;
   if (idx >= total4) return;
   float4 s = reinterpret_cast<const float4*>(part)[idx];
+#pragma unroll 8
   for (int k = 1; k < nsplit; ++k) {
     const float4 v = reinterpret_cast<const float4*>(part + (int64_t)k * n * kD)[idx];
     s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
@@ -2487,13 +2488,20 @@ __global__ __launch_bounds__(256) void nce_grouped_merge_g_k(const float* A, con
   for (int o = 32; o > 0; o >>= 1) dd += __shfl_xor(dd, o, 64);
   const float sii = dd * inv_tau - (bias ? bias[d] : 0.0f);
   const float inv_t = (t > 0.0f) ? 1.0f / t : 0.0f;
+  // every split's partial row is loaded unconditionally (all in flight at once) and a split
+  // with no columns (f = 0: its slot was never written) is dropped by a select, not a branch
   float2 acc = make_float2(0.0f, 0.0f);
-  for (int s = 0; s < nsplit; ++s) {
-    const float fs = __shfl(f, s, 64) * inv_t;
-    if (fs != 0.0f) {
-      const float2 v = reinterpret_cast<const float2*>(opart + ((int64_t)s * N + i) * kD)[lane];
-      acc.x = fmaf(fs, v.x, acc.x);
-      acc.y = fmaf(fs, v.y, acc.y);
+  for (int s0 = 0; s0 < nsplit; s0 += 8) {
+    float2 v[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+      if (s0 + s < nsplit) v[s] = reinterpret_cast<const float2*>(opart + ((int64_t)(s0 + s) * N + i) * kD)[lane];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      if (s0 + s >= nsplit) break;
+      const float fs = __shfl(f, s0 + s, 64) * inv_t;
+      acc.x = fs != 0.0f ? fmaf(fs, v[s].x, acc.x) : acc.x;
+      acc.y = fs != 0.0f ? fmaf(fs, v[s].y, acc.y) : acc.y;
     }
   }
   reinterpret_cast<float2*>(ga + i * kD)[lane] = make_float2((acc.x - y.x) * inv_tau, (acc.y - y.y) * inv_tau);
