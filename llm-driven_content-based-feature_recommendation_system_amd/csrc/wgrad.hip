@@ -301,6 +301,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_k(WArgs a) {
       __syncthreads();
     }
   }
+  // the loop leaves after a compute without a barrier: the db reduction below reuses sY[0]
+  __syncthreads();
   if (live) {
     float* dst = a.part + split * pstride;
 #pragma unroll

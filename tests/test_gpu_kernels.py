@@ -550,7 +550,8 @@ def gemm_precision(request):
 
 
 @pytest.mark.parametrize("T,N,K", [(80001, 384, 128), (4133, 128, 256), (37, 64, 48), (5, 16, 16), (0, 32, 32),
-                                   (70000, 256, 128), (1000, 400, 144), (9, 512, 32)])
+                                   (70000, 256, 128), (1000, 400, 144), (9, 512, 32), (256, 64, 64),
+                                   (33, 64, 768), (256, 64, 768)])
 def test_linear_wgrad_against_float64(gpu, gemm_precision, T, N, K):
     """dW = dY^T X and db = sum_t dY (split-K; fp32 MFMA or bf16x3) vs a float64 product: max
     error <= 2e-5 * sqrt(T) — fp32 accumulation over T terms (bf16x3 adds <= 2^-17 |dy x| per
