@@ -42,6 +42,12 @@ def _worker(rank, world, port, q):
         exp = torch.cat([torch.arange(3 + r * 2) + 100 * r for r in range(world)])
         assert counts == [3 + 2 * r for r in range(world)]
         assert torch.equal(got, exp)
+        # the background index builder is single-rank only (its all-gathers would leave program order)
+        try:
+            D.IndexPrefetcher()
+            raise AssertionError("IndexPrefetcher must refuse world > 1")
+        except RuntimeError:
+            pass
 
         # decomposition of a two-view InfoNCE over a global batch of 8 users
         g = torch.Generator().manual_seed(0)
