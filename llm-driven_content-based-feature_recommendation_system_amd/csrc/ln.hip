@@ -328,8 +328,12 @@ __global__ __launch_bounds__(256) void colsum_k(const float* part, int nblk, int
   const int o = threadIdx.x & 15, g = threadIdx.x >> 4;
   const int i = blockIdx.x * 16 + o;
   float s = 0.0f;
-  if (i < n)
+  // unrolled: eight partial loads in flight per thread (the sum order, and so the result, is
+  // unchanged); one load at a time left these 16-workgroup launches waiting out the latency
+  if (i < n) {
+#pragma unroll 8
     for (int k = g; k < nblk; k += 16) s += part[(int64_t)k * n + i];
+  }
   red[g][o] = s;
   __syncthreads();
   if (g != 0 || i >= n) return;
