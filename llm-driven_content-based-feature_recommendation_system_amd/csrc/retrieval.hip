@@ -443,18 +443,17 @@ constexpr int kStreamCap = 32;    // P3 entries per lane stream
 constexpr int kSelMax = 8192;     // P4 entries per query (LDS sort)
 constexpr float kDeltaRel = 0.0078125f + 0.000244140625f;  // 2^-7 + 2^-12
 
-// 16 threads per row, 8 floats each; 4 rows per wave per step, kPrepU steps of loads in flight
-constexpr int kPrepU = 4;
+// 16 threads per row, 8 floats each; 4 rows per wave per step
 __global__ __launch_bounds__(256) void topk_bf16_prep_k(const float* __restrict__ I, int64_t ldi, int64_t NI,
                                                         __bf16* __restrict__ img, unsigned* wmax_bits) {
   const int lane = threadIdx.x & 63, sub = lane >> 4, c = lane & 15;
   const int64_t wave_g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t nw = (int64_t)gridDim.x * 4;
   float mx = 0.0f;
-  for (int64_t j0 = wave_g * (4 * kPrepU); j0 < NI; j0 += nw * (4 * kPrepU)) {
-    float4 v[kPrepU][2];
+  for (int64_t j0 = wave_g * 8; j0 < NI; j0 += nw * 8) {
+    float4 v[2][2];
 #pragma unroll
-    for (int u = 0; u < kPrepU; ++u) {
+    for (int u = 0; u < 2; ++u) {
       const int64_t j = j0 + 4 * u + sub;
       if (j < NI) {
         const float4* src = reinterpret_cast<const float4*>(I + j * ldi) + 2 * c;
@@ -466,7 +465,7 @@ __global__ __launch_bounds__(256) void topk_bf16_prep_k(const float* __restrict_
       }
     }
 #pragma unroll
-    for (int u = 0; u < kPrepU; ++u) {
+    for (int u = 0; u < 2; ++u) {
       const int64_t j = j0 + 4 * u + sub;
       const float4 a = v[u][0], b = v[u][1];
       const float ss = rsx::wave_sum_width(a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w +
@@ -497,15 +496,8 @@ struct BfArgs {
   int* buf_n;          // MODE 1: [Q][nsplit][2] appended count (may exceed the cap: overflow)
 };
 
-// MODE 0: sample scan (sorted per-lane lists); MODE 1: the full scan, appends through a per-lane
-// pass mask (16 compares, then a loop over the set bits: one iteration for a lane with one pass,
-// zero trips for a wave with none; the sample scan's sorted inserts the same way); MODES 2 / 3:
-// the collect / sample scans with one predicated branch per score (round-3 form,
-// RSX_TOPK_SCAN_BRANCHY=1). Both collect modes append in ascending r per lane, so
-// the stream buffers are identical.
 template <int G, int T, int MODE>
 __global__ __launch_bounds__(256, 2) void topk_bf16_scan_k(BfArgs a) {
-  constexpr bool SAMPLE = MODE == 0 || MODE == 3, COLLECT = !SAMPLE, MASKED = MODE <= 1;
   __shared__ __attribute__((aligned(16))) unsigned char sI[2][kTile * kImgStride];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, c = lane & 31;
@@ -521,7 +513,7 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_scan_k(BfArgs a) {
   for (int g = 0; g < G; ++g) {
     const int64_t q = q0 + 32 * g;
     q_ok[g] = q < a.Q;
-    thr[g] = (COLLECT && q_ok[g]) ? a.thr[q] : INFINITY;
+    thr[g] = (MODE == 1 && q_ok[g]) ? a.thr[q] : INFINITY;
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
       float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
@@ -537,7 +529,7 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_scan_k(BfArgs a) {
   const int64_t j_begin = (int64_t)split * a.span;
   int64_t j_end = j_begin + a.span;
   if (j_end > a.NI) j_end = a.NI;
-  const int64_t step = SAMPLE ? (int64_t)kTile * a.sample : kTile;
+  const int64_t step = MODE == 0 ? (int64_t)kTile * a.sample : kTile;
 
   float ts[G][T];
   int ti[G][T];
@@ -555,8 +547,8 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_scan_k(BfArgs a) {
   int* bip[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) {  // MODE 1 stream buffers of this lane's queries
-    bsp[g] = COLLECT ? a.buf_s + sbase[g] * kStreamCap : nullptr;
-    bip[g] = COLLECT ? a.buf_i + sbase[g] * kStreamCap : nullptr;
+    bsp[g] = MODE == 1 ? a.buf_s + sbase[g] * kStreamCap : nullptr;
+    bip[g] = MODE == 1 ? a.buf_i + sbase[g] * kStreamCap : nullptr;
   }
 
   // staging: 8 threads per item row, 32 B each
@@ -609,64 +601,17 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_scan_k(BfArgs a) {
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         if (!q_ok[g]) continue;
-        if (SAMPLE) {
+        if (MODE == 0) {
           float mx = fmaxf(acc[g][0], acc[g][1]);
 #pragma unroll
           for (int r = 2; r < 16; r += 2) mx = fmaxf(mx, fmaxf(acc[g][r], acc[g][r + 1]));
           if (!(mx > ts[g][T - 1])) continue;  // no score of this lane enters its list
         }
-        if (MASKED) {
-          // MODE 0: scores above the list minimum at the tile's start (a superset of the inserts;
-          // each is re-checked against the current minimum, in the same ascending-r order)
-          const float t0 = SAMPLE ? ts[g][T - 1] : thr[g];
-          unsigned m = 0u;
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            m |= (SAMPLE ? acc[g][r] > t0 : acc[g][r] >= t0) ? (1u << r) : 0u;
-          if (!full_tile) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-              if (jt0 + tile_row(r, h) >= jend) m &= ~(1u << r);
-          }
-          while (m != 0u) {
-            const int r = __builtin_ctz(m);
-            m &= m - 1u;
-            // acc[g][r] for a lane-varying r: a 4-level select tree (no register indexing)
-            float s8[8], s4[4], s2[2];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) s8[i] = (r & 8) ? acc[g][i + 8] : acc[g][i];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) s4[i] = (r & 4) ? s8[i + 4] : s8[i];
-#pragma unroll
-            for (int i = 0; i < 2; ++i) s2[i] = (r & 2) ? s4[i + 2] : s4[i];
-            const float sc = (r & 1) ? s2[1] : s2[0];
-            if (SAMPLE) {
-              if (sc > ts[g][T - 1]) {
-                ts[g][T - 1] = sc;
-                ti[g][T - 1] = jt0 + tile_row(r, h);
-#pragma unroll
-                for (int t = T - 1; t > 0; --t) {
-                  if (ts[g][t] > ts[g][t - 1]) {
-                    const float fs = ts[g][t]; ts[g][t] = ts[g][t - 1]; ts[g][t - 1] = fs;
-                    const int fi = ti[g][t]; ti[g][t] = ti[g][t - 1]; ti[g][t - 1] = fi;
-                  }
-                }
-              }
-            } else {
-              if (cnt[g] < kStreamCap) {
-                bsp[g][cnt[g]] = sc;
-                bip[g][cnt[g]] = jt0 + tile_row(r, h);
-              }
-              ++cnt[g];
-            }
-          }
-          continue;
-        }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int j = jt0 + tile_row(r, h);
           const float sc = acc[g][r];
-          if (SAMPLE) {
+          if (MODE == 0) {
             if (sc > ts[g][T - 1] && (full_tile || j < jend)) {
               ts[g][T - 1] = sc;
               ti[g][T - 1] = j;
@@ -695,7 +640,7 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_scan_k(BfArgs a) {
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     if (!q_ok[g]) continue;
-    if (SAMPLE) {
+    if (MODE == 0) {
 #pragma unroll
       for (int t = 0; t < T; ++t) {
         a.cand_s[sbase[g] * T + t] = ts[g][t];
@@ -1120,7 +1065,7 @@ RSX_API int rsx_retrieve_topk(const float* U, int64_t ldu, const float* I, int64
     int* qmap = reinterpret_cast<int*>(w + L.qmap);
     (void)hipMemsetAsync(w, 0, 8, st);
     __bf16* img = reinterpret_cast<__bf16*>(w + L.img);
-    int64_t pb = (NI + 16 * kPrepU - 1) / (16 * kPrepU);
+    int64_t pb = (NI + 31) / 32;
     if (pb > 4096) pb = 4096;
     hipLaunchKernelGGL(topk_bf16_prep_k, dim3((unsigned)pb), dim3(256), 0, st, I, ldi, NI, img, wmax);
     RSX_LAUNCHED();
@@ -1135,17 +1080,8 @@ RSX_API int rsx_retrieve_topk(const float* U, int64_t ldu, const float* I, int64
     b.buf_i = reinterpret_cast<int*>(w + L.buf_i);
     b.buf_n = reinterpret_cast<int*>(w + L.buf_n);
     const dim3 grid((unsigned)(bp.nqb * bp.nsplit));
-    static const bool branchy = [] {
-      const char* e = getenv("RSX_TOPK_SCAN_BRANCHY");
-      return e && e[0] == '1';
-    }();
-    if (branchy) {
-      if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_scan_k<2, 8, 3>), grid, dim3(256), 0, st, b);
-      else hipLaunchKernelGGL((topk_bf16_scan_k<1, 8, 3>), grid, dim3(256), 0, st, b);
-    } else {
-      if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_scan_k<2, 8, 0>), grid, dim3(256), 0, st, b);
-      else hipLaunchKernelGGL((topk_bf16_scan_k<1, 8, 0>), grid, dim3(256), 0, st, b);
-    }
+    if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_scan_k<2, 8, 0>), grid, dim3(256), 0, st, b);
+    else hipLaunchKernelGGL((topk_bf16_scan_k<1, 8, 0>), grid, dim3(256), 0, st, b);
     RSX_LAUNCHED();
     const int ncand = bp.nsplit * 2 * bp.T;
     float* thr = reinterpret_cast<float*>(w + L.thr);
@@ -1159,13 +1095,8 @@ RSX_API int rsx_retrieve_topk(const float* U, int64_t ldu, const float* I, int64
       hipLaunchKernelGGL(topk_bf16_thresh_k<4096>, dim3((unsigned)Q), dim3(256), 0, st, b.cand_s, b.cand_i, ncand, U,
                          ldu, (int)k, wmax, thr);
     RSX_LAUNCHED();
-    if (branchy) {
-      if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_scan_k<2, 8, 2>), grid, dim3(256), 0, st, b);
-      else hipLaunchKernelGGL((topk_bf16_scan_k<1, 8, 2>), grid, dim3(256), 0, st, b);
-    } else {
-      if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_scan_k<2, 8, 1>), grid, dim3(256), 0, st, b);
-      else hipLaunchKernelGGL((topk_bf16_scan_k<1, 8, 1>), grid, dim3(256), 0, st, b);
-    }
+    if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_scan_k<2, 8, 1>), grid, dim3(256), 0, st, b);
+    else hipLaunchKernelGGL((topk_bf16_scan_k<1, 8, 1>), grid, dim3(256), 0, st, b);
     RSX_LAUNCHED();
     hipLaunchKernelGGL(topk_bf16_select_k, dim3((unsigned)Q), dim3(256), 0, st, b.buf_s, b.buf_i, b.buf_n,
                        bp.nsplit * 2, U, ldu, I, ldi, (int)k, wmax, out_scores, out_idx, qcount, qmap);
