@@ -424,8 +424,9 @@ __global__ __launch_bounds__(256) void topk_final_k(const float* bs, const int* 
 //     (bf16 RNE operands: 2^-7 + 2^-16 relative per product, fp32 accumulation) and the fp32
 //     score e of the rescoring (fp32 accumulation; both accumulations < 2^-16 relative).
 // P1 (topk_bf16_scan_k<MODE 0>): a strided sample of the corpus (every S-th 32-item tile of each
-//     split, S ~ 8 nsplit / k so that ~4 collected entries per stream are expected in P3); each
-//     lane keeps its best T sample scores in registers.
+//     split, S ~ 8 nsplit / k so that ~4 collected entries per stream are expected in P3) over
+//     ns0 <= nsplit splits (sample_nsplit); each lane keeps its best T0 sample scores in registers
+//     (T0 = 1 where 2 ns0 >= 2k: a compare and two selects per score, no sorted insert).
 // P2 (topk_bf16_thresh_k): per query, c_k = k-th best of the sampled candidates. The k sampled
 //     items with a >= c_k have e >= c_k - delta, so the true k-th best exact score e_k >= c_k -
 //     delta, and every true top-k item has a >= e_k - delta >= c_k - 2 delta =: t_q.
@@ -942,6 +943,31 @@ BfPlan bf_plan(int64_t Q, int64_t NI, int64_t k) {
   return p;
 }
 
+// splits of the P1 sample scan: nsplit / 4 (>= 8, a multiple of 8 like nsplit) unless
+// RSX_TOPK_SAMPLE_DIV names another divisor (1 = the full split count, the round-3 form); at
+// least k / T splits, so the 2 ns0 T candidates hold 2k (bf_plan's condition for nsplit)
+int sample_nsplit(int nsplit, int64_t k, int T) {
+  static const int div = [] {
+    const char* e = getenv("RSX_TOPK_SAMPLE_DIV");
+    const int v = e ? atoi(e) : 4;
+    return (v == 1 || v == 2 || v == 4 || v == 8) ? v : 4;
+  }();
+  int ns0 = nsplit / div;
+  if (ns0 < 8) ns0 = 8;
+  while (ns0 < nsplit && 2 * (int64_t)ns0 * T < 2 * k) ns0 *= 2;
+  if (ns0 > nsplit) ns0 = nsplit;
+  return ns0;
+}
+
+// RSX_TOPK_SAMPLE_T1=0: the sample scan keeps T best per lane stream (A/B)
+bool sample_t1() {
+  static const bool on = [] {
+    const char* e = getenv("RSX_TOPK_SAMPLE_T1");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int choose_nsplit(int64_t Q, int64_t NI, int kmax) {
   // >= ~1024 workgroups when there are enough items; each split keeps >= 2048 items; the
   // merge sorts at most 8192 candidates per query in LDS (2 * nsplit * kmax <= 8192)
@@ -1080,10 +1106,26 @@ RSX_API int rsx_retrieve_topk(const float* U, int64_t ldu, const float* I, int64
     b.buf_i = reinterpret_cast<int*>(w + L.buf_i);
     b.buf_n = reinterpret_cast<int*>(w + L.buf_n);
     const dim3 grid((unsigned)(bp.nqb * bp.nsplit));
-    if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_scan_k<2, 8, 0>), grid, dim3(256), 0, st, b);
-    else hipLaunchKernelGGL((topk_bf16_scan_k<1, 8, 0>), grid, dim3(256), 0, st, b);
+    // P1 over ns0 <= nsplit splits: each workgroup samples nsplit / ns0 times the items (same
+    // sampled fraction), so the query-fragment prologue is amortised over more tiles; any subset's
+    // k-th best gives a valid t_q (P2), so the split count only moves the threshold's tightness
+    // T0 = 1 (each lane stream keeps only its best sample: a compare and two selects per score
+    // instead of a sorted insert) where 2 nsplit streams can hold 2k candidates, else T0 = T
+    BfArgs b0 = b;
+    const int T0 = sample_t1() && bp.nsplit >= k ? 1 : bp.T;
+    const int ns0 = sample_nsplit(bp.nsplit, k, T0);
+    b0.nsplit = ns0;
+    b0.span = ((NI + ns0 - 1) / ns0 + kTile - 1) / kTile * kTile;
+    const dim3 grid0((unsigned)(bp.nqb * ns0));
+    if (T0 == 1) {
+      if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_scan_k<2, 1, 0>), grid0, dim3(256), 0, st, b0);
+      else hipLaunchKernelGGL((topk_bf16_scan_k<1, 1, 0>), grid0, dim3(256), 0, st, b0);
+    } else {
+      if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_scan_k<2, 8, 0>), grid0, dim3(256), 0, st, b0);
+      else hipLaunchKernelGGL((topk_bf16_scan_k<1, 8, 0>), grid0, dim3(256), 0, st, b0);
+    }
     RSX_LAUNCHED();
-    const int ncand = bp.nsplit * 2 * bp.T;
+    const int ncand = ns0 * 2 * T0;
     float* thr = reinterpret_cast<float*>(w + L.thr);
     if (ncand <= 1024)
       hipLaunchKernelGGL(topk_bf16_thresh_k<1024>, dim3((unsigned)Q), dim3(256), 0, st, b.cand_s, b.cand_i, ncand, U,
