@@ -823,13 +823,13 @@ __global__ __launch_bounds__(256) void topk_bf16_select_k(const float* __restric
     if (tid == 0) qmap[atomicAdd(qcount, 1)] = (int)q;
     return;
   }
-  // 32 threads per stream, 8 streams per pass; eight passes' loads are issued before their LDS
-  // stores (one memory latency per 64 streams instead of per 8)
-  for (int s0 = 0; s0 < nstreams; s0 += 64) {
-    float v[8];
-    int dst[8];
+  // 32 threads per stream, 8 streams per pass; sixteen passes' loads are issued before their LDS
+  // stores (one memory latency per 128 streams instead of per 8)
+  for (int s0 = 0; s0 < nstreams; s0 += 128) {
+    float v[16];
+    int dst[16];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 16; ++u) {
       const int st = s0 + 8 * u + (tid >> 5), e = tid & 31;
       dst[u] = -1;
       if (st < nstreams) {
@@ -841,19 +841,21 @@ __global__ __launch_bounds__(256) void topk_bf16_select_k(const float* __restric
       }
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
+    for (int u = 0; u < 16; ++u)
       if (dst[u] >= 0) ss[dst[u]] = v[u];
   }
   __syncthreads();
   const float thr = (total >= K) ? block_kth_largest(ss, total, K, hist, sel) - 2.0f * delta : -INFINITY;
-  // margin set: walk the streams again; the item ids of the selected entries come from global
+  // margin set: walk the streams again (LDS only: the selected entries' buffer slots are noted),
+  // then every selected item id is loaded from global at once (one memory latency, not one per
+  // walk step that holds a selected entry)
   for (int s0 = 0; s0 < nstreams; s0 += 8) {
     const int st = s0 + (tid >> 5), e = tid & 31;
     if (st < nstreams) {
       const int o = off[st];
       if (e < off[st + 1] - o && ss[o + e] >= thr) {
         const int slot = atomicAdd(&nsel_s, 1);
-        if (slot < kMarginMax) mi[slot] = bi[(q * nstreams + st) * kStreamCap + e];
+        if (slot < kMarginMax) mi[slot] = st * kStreamCap + e;
       }
     }
   }
@@ -862,6 +864,21 @@ __global__ __launch_bounds__(256) void topk_bf16_select_k(const float* __restric
   if (n > kMarginMax) {  // block-uniform: the exact kernels take this query
     if (tid == 0) qmap[atomicAdd(qcount, 1)] = (int)q;
     return;
+  }
+  {
+    int ids[kMarginMax / 256];
+#pragma unroll
+    for (int u = 0; u < kMarginMax / 256; ++u) {
+      const int t = tid + 256 * u;
+      ids[u] = t < n ? bi[q * nstreams * kStreamCap + mi[t]] : 0;
+    }
+    __syncthreads();  // every slot read before any is overwritten
+#pragma unroll
+    for (int u = 0; u < kMarginMax / 256; ++u) {
+      const int t = tid + 256 * u;
+      if (t < n) mi[t] = ids[u];
+    }
+    __syncthreads();
   }
   // exact fp32 rescoring: 32 lanes per item, float4 per lane, fixed-order shuffle reduction
   const int sub = lane >> 5, c = lane & 31;
