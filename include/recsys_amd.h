@@ -267,6 +267,12 @@ int rsx_gemm_x3_addln(const float* A, int64_t lda, const float* B, int64_t ldb, 
                       const float* ln_b, float eps, float* S, int64_t lds, float* Y, int64_t ldy, float* mean,
                       float* rstd, void* stream);
 
+/* Device-side id range check (no host sync): out[i] = ids[i] if lo <= ids[i] < hi else 0, and
+ * *flag = 1 if any id was outside [lo, hi) (untouched otherwise). Replaces the out-of-range
+ * failure of nn.Embedding on the item tower's STD ids (item_tower.py:240, vocab ids 0..383,
+ * utils/vocab.py:436-441): the caller raises when the flag reaches the host. */
+int rsx_ids_check(const int64_t* ids, int64_t n, int64_t lo, int64_t hi, int64_t* out, int* flag, void* stream);
+
 /* ---- A14: retrieval top-k ------------------------------------------------------------
  * scores = U I^T (fp32 MFMA, never materialised), per query the k best items sorted by
  * (score desc, index asc). Replaces `scores = matmul(user, items.T); topk(k)` at
@@ -276,6 +282,22 @@ int rsx_gemm_x3_addln(const float* A, int64_t lda, const float* B, int64_t ldb, 
 int64_t rsx_topk_workspace_bytes(int64_t Q, int64_t NI, int64_t k);
 int rsx_retrieve_topk(const float* U, int64_t ldu, const float* I, int64_t ldi, int64_t Q, int64_t NI, int64_t k,
                       void* ws, float* out_scores, int64_t* out_idx, void* stream);
+/* Which exact path a (Q, NI, k) call takes: 0 list kernels, 1 fp32 candidate/threshold path,
+ * 2 bf16 single scan + exact fp32 rescoring (large corpora). Every call writes a workspace
+ * header: int32 ws[0] = queries path 2 sent to the exact kernels, ws[1] = path id, ws[2] = path
+ * 1's whole-batch fallback flag. Path 2 runs the queries in chunks of at most 4096 (workspace
+ * bounded in Q). */
+int rsx_topk_path(int64_t Q, int64_t NI, int64_t k);
+/* Path 2 with a caller-cached corpus image (a static corpus, e.g. the serving item matrix of
+ * controller.py:62-124 or evaluate_model's normalised item table, :672): rsx_topk_prepare_corpus
+ * writes max ||w|| and the bf16 image of I into `corpus` (rsx_topk_corpus_bytes(NI) bytes) once;
+ * rsx_retrieve_topk_corpus then skips that pass (ws: rsx_topk_workspace_bytes_corpus). I must
+ * be the corpus the image was made from (the exact rescoring reads it). */
+int64_t rsx_topk_corpus_bytes(int64_t NI);
+int rsx_topk_prepare_corpus(const float* I, int64_t ldi, int64_t NI, void* corpus, void* stream);
+int64_t rsx_topk_workspace_bytes_corpus(int64_t Q, int64_t NI, int64_t k);
+int rsx_retrieve_topk_corpus(const float* U, int64_t ldu, const float* I, int64_t ldi, const void* corpus, int64_t Q,
+                             int64_t NI, int64_t k, void* ws, float* out_scores, int64_t* out_idx, void* stream);
 
 /* ---- A16: DeepFM rerank forward ------------------------------------------------------
  * deepctr-torch 0.2.9 DeepFM semantics (absent from the reference tree).

@@ -24,7 +24,7 @@ c_i = ctypes.c_int
 c_f = ctypes.c_float
 c_u64 = ctypes.c_uint64
 
-ABI_VERSION = 2  # rsx_abi_version() of the library these signatures describe
+ABI_VERSION = 3  # rsx_abi_version() of the library these signatures describe
 
 # name -> (restype, argtypes)
 _SIGS = {
@@ -88,6 +88,12 @@ _SIGS = {
                                 c_p, c_i64, c_p, c_i64, c_p, c_p, c_p]),
     "rsx_topk_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64]),
     "rsx_retrieve_topk": (c_i, [c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p]),
+    "rsx_topk_path": (c_i, [c_i64, c_i64, c_i64]),
+    "rsx_ids_check": (c_i, [c_p, c_i64, c_i64, c_i64, c_p, c_p, c_p]),
+    "rsx_topk_corpus_bytes": (c_i64, [c_i64]),
+    "rsx_topk_prepare_corpus": (c_i, [c_p, c_i64, c_i64, c_p, c_p]),
+    "rsx_topk_workspace_bytes_corpus": (c_i64, [c_i64, c_i64, c_i64]),
+    "rsx_retrieve_topk_corpus": (c_i, [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p]),
     "rsx_gather_rows": (c_i, [c_p, c_i64, c_p, c_i64, c_i64, c_i, c_f, c_p, c_p, c_p]),
     "rsx_embed3_ln": (c_i, [c_p, c_i64, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_i64, c_i64, c_p, c_p]),
     "rsx_crossnet": (c_i, [c_p, c_i64, c_i64, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p]),

@@ -778,7 +778,7 @@ __global__ __launch_bounds__(256) void topk_bf16_select_k(const float* __restric
                                                           const float* __restrict__ U, int64_t ldu,
                                                           const float* __restrict__ I, int64_t ldi, int K,
                                                           const unsigned* wmax_bits, float* out_s, int64_t* out_i,
-                                                          int* qcount, int* qmap) {
+                                                          int* qcount, int* qmap, int* qtotal) {
   // LDS: the appended scores only (their item ids are read back from global for the margin set),
   // so three workgroups fit per CU
   __shared__ float ss[kSelMax];
@@ -820,7 +820,10 @@ __global__ __launch_bounds__(256) void topk_bf16_select_k(const float* __restric
   __syncthreads();
   const int total = off[512];
   if (bad_s || total > kSelMax) {
-    if (tid == 0) qmap[atomicAdd(qcount, 1)] = (int)q;
+    if (tid == 0) {
+      qmap[atomicAdd(qcount, 1)] = (int)q;
+      atomicAdd(qtotal, 1);
+    }
     return;
   }
   // 32 threads per stream, 8 streams per pass; sixteen passes' loads are issued before their LDS
@@ -862,7 +865,10 @@ __global__ __launch_bounds__(256) void topk_bf16_select_k(const float* __restric
   __syncthreads();
   const int n = nsel_s;
   if (n > kMarginMax) {  // block-uniform: the exact kernels take this query
-    if (tid == 0) qmap[atomicAdd(qcount, 1)] = (int)q;
+    if (tid == 0) {
+      qmap[atomicAdd(qcount, 1)] = (int)q;
+      atomicAdd(qtotal, 1);
+    }
     return;
   }
   {
@@ -1024,24 +1030,37 @@ FastLayout fast_layout(int64_t Q, int64_t NI, int64_t k, const FastPlan& p) {
 }
 
 
+// Every workspace starts with a 256-byte header (zeroed by each call):
+//   int32 [0] queries the bf16 path sent to the exact kernels (all chunks), [1] path id
+//   (rsx_topk_path), [2] the fast path's whole-batch fallback flag, [3] the current chunk's
+//   fallback-query count (indexes qmap).
+// The bf16 path's corpus image (rsx_topk_prepare_corpus: a 256-byte header holding max ||w|| bits,
+// then the [NI][128] bf16 image) either lives in the caller's cached buffer or is built into the
+// workspace per call. Queries run in chunks of at most kQChunk (workspace bounded in Q).
+constexpr int64_t kHeader = 256;
+constexpr int64_t kQChunk = 4096;
+int64_t corpus_bytes(int64_t NI) { return kHeader + align256(NI * kD * 2); }
+
 struct BfLayout {
-  int64_t img, thr, cand_s, cand_i, buf_s, buf_i, buf_n, qmap, fallback, total;
+  int64_t corpus, thr, qmap, cand_s, cand_i, buf_s, buf_i, buf_n, fallback, total;
 };
-BfLayout bf_layout(int64_t Q, int64_t NI, int64_t k, const BfPlan& p) {
+BfLayout bf_layout(int64_t Qc, int64_t NI, int64_t k, const BfPlan& p, bool own_corpus) {
   BfLayout L;
-  L.img = 256;  // [0] count of queries sent to the exact kernels, [4] max ||w|| bits
-  const int64_t nstream = Q * p.nsplit * 2;
-  L.thr = L.img + align256(NI * kD * 2);
-  L.cand_s = L.thr + align256(Q * 4);
+  L.corpus = kHeader;
+  const int64_t nstream = Qc * p.nsplit * 2;
+  L.thr = L.corpus + (own_corpus ? corpus_bytes(NI) : 0);
+  L.qmap = L.thr + align256(Qc * 4);
+  L.cand_s = L.qmap + align256(Qc * 4);
   L.cand_i = L.cand_s + align256(nstream * p.T * 4);
   L.buf_s = L.cand_i + align256(nstream * p.T * 4);
   L.buf_i = L.buf_s + align256(nstream * kStreamCap * 4);
   L.buf_n = L.buf_i + align256(nstream * kStreamCap * 4);
   const int64_t end = L.buf_n + align256(nstream * 4);
-  L.fallback = L.img;  // the exact fallback runs after P4: reuses the image / buffer region
-  const int64_t fb_end = L.fallback + old_ws_bytes(Q, NI, k);
-  L.qmap = end > fb_end ? end : fb_end;  // the fallback must not overwrite the query list
-  L.total = L.qmap + align256(Q * 4) + 256;
+  // the exact kernels for the chunk's listed queries run after its P4: they reuse the
+  // candidate / stream-buffer region (never the corpus image, which later chunks still read)
+  L.fallback = L.cand_s;
+  const int64_t fb_end = L.fallback + old_ws_bytes(Qc, NI, k);
+  L.total = (end > fb_end ? end : fb_end) + 256;
   return L;
 }
 
@@ -1082,92 +1101,127 @@ void launch_fast_scans(FastArgs f, int blocks, int mode, hipStream_t st) {
 }
 }  // namespace
 
-RSX_API int64_t rsx_topk_workspace_bytes(int64_t Q, int64_t NI, int64_t k) {
-  const BfPlan bp = bf_plan(Q, NI, k);
-  if (bp.use) return bf_layout(Q, NI, k, bp).total;
-  const FastPlan p = fast_plan(Q, NI, k);
-  if (!p.use) return old_ws_bytes(Q, NI, k) + 256;
-  return fast_layout(Q, NI, k, p).total;
+namespace {
+int topk_path(int64_t Q, int64_t NI, int64_t k) {
+  if (bf_plan(Q < kQChunk ? Q : kQChunk, NI, k).use) return 2;
+  return fast_plan(Q, NI, k).use ? 1 : 0;
 }
 
-// scores [Q, k] (desc), idx [Q, k] int64 (-1 where fewer than k items exist).
-RSX_API int rsx_retrieve_topk(const float* U, int64_t ldu, const float* I, int64_t ldi, int64_t Q, int64_t NI,
-                              int64_t k, void* ws, float* out_scores, int64_t* out_idx, void* stream) {
+void launch_prep(const float* I, int64_t ldi, int64_t NI, char* corpus, hipStream_t st) {
+  (void)hipMemsetAsync(corpus, 0, 4, st);
+  int64_t pb = (NI + 31) / 32;
+  if (pb > 4096) pb = 4096;
+  hipLaunchKernelGGL(topk_bf16_prep_k, dim3((unsigned)pb), dim3(256), 0, st, I, ldi, NI,
+                     reinterpret_cast<__bf16*>(corpus + kHeader), reinterpret_cast<unsigned*>(corpus));
+}
+
+// P1-P4 (+ the exact kernels for listed queries) over queries [0, Q) of U / out (one chunk)
+int run_bf16_chunk(const BfPlan& bp, const BfLayout& L, const float* U, int64_t ldu, const float* I, int64_t ldi,
+                   int64_t Q, int64_t NI, int64_t k, const char* corpus, char* w, float* out_scores,
+                   int64_t* out_idx, hipStream_t st) {
+  int* qtotal = reinterpret_cast<int*>(w);
+  int* qcount = reinterpret_cast<int*>(w + 12);
+  int* qmap = reinterpret_cast<int*>(w + L.qmap);
+  const unsigned* wmax = reinterpret_cast<const unsigned*>(corpus);
+  (void)hipMemsetAsync(qcount, 0, 4, st);
+  BfArgs b;
+  b.img = reinterpret_cast<const __bf16*>(corpus + kHeader);
+  b.U = U; b.Q = Q; b.NI = NI; b.ldu = ldu;
+  b.nsplit = bp.nsplit; b.nqb = bp.nqb; b.sample = bp.sample;
+  b.span = ((NI + bp.nsplit - 1) / bp.nsplit + kTile - 1) / kTile * kTile;
+  b.cand_s = reinterpret_cast<float*>(w + L.cand_s);
+  b.cand_i = reinterpret_cast<int*>(w + L.cand_i);
+  b.thr = reinterpret_cast<const float*>(w + L.thr);
+  b.buf_s = reinterpret_cast<float*>(w + L.buf_s);
+  b.buf_i = reinterpret_cast<int*>(w + L.buf_i);
+  b.buf_n = reinterpret_cast<int*>(w + L.buf_n);
+  const dim3 grid((unsigned)(bp.nqb * bp.nsplit));
+  // P1 over ns0 <= nsplit splits: each workgroup samples nsplit / ns0 times the items (same
+  // sampled fraction), so the query-fragment prologue is amortised over more tiles; any subset's
+  // k-th best gives a valid t_q (P2), so the split count only moves the threshold's tightness
+  // T0 = 1 (each lane stream keeps only its best sample: a compare and two selects per score
+  // instead of a sorted insert) where 2 nsplit streams can hold 2k candidates, else T0 = T
+  BfArgs b0 = b;
+  const int T0 = sample_t1() && bp.nsplit >= k ? 1 : bp.T;
+  const int ns0 = sample_nsplit(bp.nsplit, k, T0);
+  b0.nsplit = ns0;
+  b0.span = ((NI + ns0 - 1) / ns0 + kTile - 1) / kTile * kTile;
+  const dim3 grid0((unsigned)(bp.nqb * ns0));
+  if (T0 == 1) {
+    if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_scan_k<2, 1, 0>), grid0, dim3(256), 0, st, b0);
+    else hipLaunchKernelGGL((topk_bf16_scan_k<1, 1, 0>), grid0, dim3(256), 0, st, b0);
+  } else {
+    if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_scan_k<2, 8, 0>), grid0, dim3(256), 0, st, b0);
+    else hipLaunchKernelGGL((topk_bf16_scan_k<1, 8, 0>), grid0, dim3(256), 0, st, b0);
+  }
+  RSX_LAUNCHED();
+  const int ncand = ns0 * 2 * T0;
+  float* thr = reinterpret_cast<float*>(w + L.thr);
+  if (ncand <= 1024)
+    hipLaunchKernelGGL(topk_bf16_thresh_k<1024>, dim3((unsigned)Q), dim3(256), 0, st, b.cand_s, b.cand_i, ncand, U,
+                       ldu, (int)k, wmax, thr);
+  else if (ncand <= 2048)
+    hipLaunchKernelGGL(topk_bf16_thresh_k<2048>, dim3((unsigned)Q), dim3(256), 0, st, b.cand_s, b.cand_i, ncand, U,
+                       ldu, (int)k, wmax, thr);
+  else
+    hipLaunchKernelGGL(topk_bf16_thresh_k<4096>, dim3((unsigned)Q), dim3(256), 0, st, b.cand_s, b.cand_i, ncand, U,
+                       ldu, (int)k, wmax, thr);
+  RSX_LAUNCHED();
+  if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_scan_k<2, 8, 1>), grid, dim3(256), 0, st, b);
+  else hipLaunchKernelGGL((topk_bf16_scan_k<1, 8, 1>), grid, dim3(256), 0, st, b);
+  RSX_LAUNCHED();
+  hipLaunchKernelGGL(topk_bf16_select_k, dim3((unsigned)Q), dim3(256), 0, st, b.buf_s, b.buf_i, b.buf_n,
+                     bp.nsplit * 2, U, ldu, I, ldi, (int)k, wmax, out_scores, out_idx, qcount, qmap, qtotal);
+  RSX_LAUNCHED();
+  // exact list-based kernels for the queries P4 listed (none on spread data)
+  return launch_old(U, ldu, I, ldi, Q, NI, k, w + L.fallback, out_scores, out_idx, nullptr, st, qmap, qcount);
+}
+
+int64_t ws_bytes(int64_t Q, int64_t NI, int64_t k, bool own_corpus) {
+  const int path = topk_path(Q, NI, k);
+  if (path == 2) {
+    const int64_t Qc = Q < kQChunk ? Q : kQChunk;
+    return bf_layout(Qc, NI, k, bf_plan(Qc, NI, k), own_corpus).total;
+  }
+  if (path == 1) return fast_layout(Q, NI, k, fast_plan(Q, NI, k)).total;
+  return kHeader + old_ws_bytes(Q, NI, k) + 256;
+}
+
+int retrieve(const float* U, int64_t ldu, const float* I, int64_t ldi, const void* corpus_in, int64_t Q, int64_t NI,
+             int64_t k, void* ws, float* out_scores, int64_t* out_idx, void* stream) {
   RSX_ARG(U && I && ws && out_scores && out_idx, "null tensor");
   RSX_ARG(k >= 1 && k <= 512, "k must be in [1,512]");
   RSX_ARG(ldu >= kD && ldi >= kD && ldu % 4 == 0 && ldi % 4 == 0, "D must be 128 (row strides >= 128)");
   RSX_ARG(NI < 0x7fffffff, "item count must fit int32");
-  if (Q == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   char* w = reinterpret_cast<char*>(ws);
-  const BfPlan bp = bf_plan(Q, NI, k);
-  if (bp.use) {
-    const BfLayout L = bf_layout(Q, NI, k, bp);
-    int* qcount = reinterpret_cast<int*>(w);
-    unsigned* wmax = reinterpret_cast<unsigned*>(w + 4);
-    int* qmap = reinterpret_cast<int*>(w + L.qmap);
-    (void)hipMemsetAsync(w, 0, 8, st);
-    __bf16* img = reinterpret_cast<__bf16*>(w + L.img);
-    int64_t pb = (NI + 31) / 32;
-    if (pb > 4096) pb = 4096;
-    hipLaunchKernelGGL(topk_bf16_prep_k, dim3((unsigned)pb), dim3(256), 0, st, I, ldi, NI, img, wmax);
-    RSX_LAUNCHED();
-    BfArgs b;
-    b.img = img; b.U = U; b.Q = Q; b.NI = NI; b.ldu = ldu;
-    b.nsplit = bp.nsplit; b.nqb = bp.nqb; b.sample = bp.sample;
-    b.span = ((NI + bp.nsplit - 1) / bp.nsplit + kTile - 1) / kTile * kTile;
-    b.cand_s = reinterpret_cast<float*>(w + L.cand_s);
-    b.cand_i = reinterpret_cast<int*>(w + L.cand_i);
-    b.thr = reinterpret_cast<const float*>(w + L.thr);
-    b.buf_s = reinterpret_cast<float*>(w + L.buf_s);
-    b.buf_i = reinterpret_cast<int*>(w + L.buf_i);
-    b.buf_n = reinterpret_cast<int*>(w + L.buf_n);
-    const dim3 grid((unsigned)(bp.nqb * bp.nsplit));
-    // P1 over ns0 <= nsplit splits: each workgroup samples nsplit / ns0 times the items (same
-    // sampled fraction), so the query-fragment prologue is amortised over more tiles; any subset's
-    // k-th best gives a valid t_q (P2), so the split count only moves the threshold's tightness
-    // T0 = 1 (each lane stream keeps only its best sample: a compare and two selects per score
-    // instead of a sorted insert) where 2 nsplit streams can hold 2k candidates, else T0 = T
-    BfArgs b0 = b;
-    const int T0 = sample_t1() && bp.nsplit >= k ? 1 : bp.T;
-    const int ns0 = sample_nsplit(bp.nsplit, k, T0);
-    b0.nsplit = ns0;
-    b0.span = ((NI + ns0 - 1) / ns0 + kTile - 1) / kTile * kTile;
-    const dim3 grid0((unsigned)(bp.nqb * ns0));
-    if (T0 == 1) {
-      if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_scan_k<2, 1, 0>), grid0, dim3(256), 0, st, b0);
-      else hipLaunchKernelGGL((topk_bf16_scan_k<1, 1, 0>), grid0, dim3(256), 0, st, b0);
-    } else {
-      if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_scan_k<2, 8, 0>), grid0, dim3(256), 0, st, b0);
-      else hipLaunchKernelGGL((topk_bf16_scan_k<1, 8, 0>), grid0, dim3(256), 0, st, b0);
+  const int path = topk_path(Q, NI, k);
+  (void)hipMemsetAsync(w, 0, 16, st);
+  (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(w + 4), path, 1, st);
+  if (Q == 0) return 0;
+  if (path == 2) {
+    const int64_t Qc = Q < kQChunk ? Q : kQChunk;
+    const BfPlan bp = bf_plan(Qc, NI, k);
+    const BfLayout L = bf_layout(Qc, NI, k, bp, corpus_in == nullptr);
+    const char* corpus = reinterpret_cast<const char*>(corpus_in);
+    if (!corpus) {
+      launch_prep(I, ldi, NI, w + L.corpus, st);
+      RSX_LAUNCHED();
+      corpus = w + L.corpus;
     }
-    RSX_LAUNCHED();
-    const int ncand = ns0 * 2 * T0;
-    float* thr = reinterpret_cast<float*>(w + L.thr);
-    if (ncand <= 1024)
-      hipLaunchKernelGGL(topk_bf16_thresh_k<1024>, dim3((unsigned)Q), dim3(256), 0, st, b.cand_s, b.cand_i, ncand, U,
-                         ldu, (int)k, wmax, thr);
-    else if (ncand <= 2048)
-      hipLaunchKernelGGL(topk_bf16_thresh_k<2048>, dim3((unsigned)Q), dim3(256), 0, st, b.cand_s, b.cand_i, ncand, U,
-                         ldu, (int)k, wmax, thr);
-    else
-      hipLaunchKernelGGL(topk_bf16_thresh_k<4096>, dim3((unsigned)Q), dim3(256), 0, st, b.cand_s, b.cand_i, ncand, U,
-                         ldu, (int)k, wmax, thr);
-    RSX_LAUNCHED();
-    if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_scan_k<2, 8, 1>), grid, dim3(256), 0, st, b);
-    else hipLaunchKernelGGL((topk_bf16_scan_k<1, 8, 1>), grid, dim3(256), 0, st, b);
-    RSX_LAUNCHED();
-    hipLaunchKernelGGL(topk_bf16_select_k, dim3((unsigned)Q), dim3(256), 0, st, b.buf_s, b.buf_i, b.buf_n,
-                       bp.nsplit * 2, U, ldu, I, ldi, (int)k, wmax, out_scores, out_idx, qcount, qmap);
-    RSX_LAUNCHED();
-    // exact list-based kernels for the queries P4 listed (none on spread data)
-    return launch_old(U, ldu, I, ldi, Q, NI, k, w + L.fallback, out_scores, out_idx, nullptr, st, qmap, qcount);
+    for (int64_t q0 = 0; q0 < Q; q0 += Qc) {
+      const int64_t qn = Q - q0 < Qc ? Q - q0 : Qc;
+      const BfPlan bc = qn == Qc ? bp : bf_plan(qn, NI, k);
+      const int rc = run_bf16_chunk(bc, L, U + q0 * ldu, ldu, I, ldi, qn, NI, k, corpus, w, out_scores + q0 * k,
+                                    out_idx + q0 * k, st);
+      if (rc) return rc;
+    }
+    return 0;
   }
+  if (path == 0) return launch_old(U, ldu, I, ldi, Q, NI, k, w + kHeader, out_scores, out_idx, nullptr, st);
   const FastPlan p = fast_plan(Q, NI, k);
-  if (!p.use) return launch_old(U, ldu, I, ldi, Q, NI, k, w, out_scores, out_idx, nullptr, st);
   const FastLayout L = fast_layout(Q, NI, k, p);
-  int* flag = reinterpret_cast<int*>(w);
-  (void)hipMemsetAsync(flag, 0, sizeof(int), st);
+  int* flag = reinterpret_cast<int*>(w + 8);
   FastArgs f;
   f.U = U; f.I = I; f.Q = Q; f.NI = NI; f.ldu = ldu; f.ldi = ldi;
   f.nsplit = p.nsplit;
@@ -1202,4 +1256,37 @@ RSX_API int rsx_retrieve_topk(const float* U, int64_t ldu, const float* I, int64
   RSX_LAUNCHED();
   // exact fallback for the whole batch, a no-op unless some query overflowed its buffer
   return launch_old(U, ldu, I, ldi, Q, NI, k, w + L.fallback, out_scores, out_idx, flag, st);
+}
+}  // namespace
+
+RSX_API int rsx_topk_path(int64_t Q, int64_t NI, int64_t k) { return topk_path(Q, NI, k); }
+
+RSX_API int64_t rsx_topk_workspace_bytes(int64_t Q, int64_t NI, int64_t k) { return ws_bytes(Q, NI, k, true); }
+
+RSX_API int64_t rsx_topk_workspace_bytes_corpus(int64_t Q, int64_t NI, int64_t k) {
+  return ws_bytes(Q, NI, k, false);
+}
+
+RSX_API int64_t rsx_topk_corpus_bytes(int64_t NI) { return corpus_bytes(NI); }
+
+RSX_API int rsx_topk_prepare_corpus(const float* I, int64_t ldi, int64_t NI, void* corpus, void* stream) {
+  RSX_ARG(I && corpus, "null tensor");
+  RSX_ARG(ldi >= kD && ldi % 4 == 0, "D must be 128 (row stride >= 128)");
+  RSX_ARG(NI >= 1 && NI < 0x7fffffff, "item count must be in [1, 2^31)");
+  launch_prep(I, ldi, NI, reinterpret_cast<char*>(corpus), (hipStream_t)stream);
+  RSX_LAUNCHED();
+  return 0;
+}
+
+// scores [Q, k] (desc), idx [Q, k] int64 (-1 where fewer than k items exist).
+RSX_API int rsx_retrieve_topk(const float* U, int64_t ldu, const float* I, int64_t ldi, int64_t Q, int64_t NI,
+                              int64_t k, void* ws, float* out_scores, int64_t* out_idx, void* stream) {
+  return retrieve(U, ldu, I, ldi, nullptr, Q, NI, k, ws, out_scores, out_idx, stream);
+}
+
+RSX_API int rsx_retrieve_topk_corpus(const float* U, int64_t ldu, const float* I, int64_t ldi, const void* corpus,
+                                     int64_t Q, int64_t NI, int64_t k, void* ws, float* out_scores,
+                                     int64_t* out_idx, void* stream) {
+  RSX_ARG(corpus, "null corpus image");
+  return retrieve(U, ldu, I, ldi, corpus, Q, NI, k, ws, out_scores, out_idx, stream);
 }

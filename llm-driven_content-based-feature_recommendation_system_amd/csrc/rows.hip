@@ -179,6 +179,19 @@ __global__ __launch_bounds__(256) void segsum_rows_k(const float* __restrict__ s
   }
 }
 
+// out[i] = ids[i] if lo <= ids[i] < hi else 0; *flag |= 1 for any id outside [lo, hi)
+__global__ __launch_bounds__(256) void ids_check_k(const int64_t* __restrict__ ids, int64_t n, int64_t lo, int64_t hi,
+                                                   int64_t* __restrict__ out, int* flag) {
+  bool bad = false;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t v = ids[i];
+    const bool ok = v >= lo && v < hi;
+    out[i] = ok ? v : 0;
+    bad |= !ok;
+  }
+  if (__builtin_amdgcn_ballot_w64(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
 }  // namespace
 
 RSX_API int rsx_gather_rows(const float* src, int64_t ld_src, const int64_t* idx, int64_t n, int64_t D, int normalize,
@@ -244,6 +257,21 @@ RSX_API int rsx_segment_sum_rows(const float* src, int64_t ld_src, const int64_t
                        scale, skip_row, dst, ld_dst, accumulate);
   RSX_SS(64) RSX_SS(128) RSX_SS(256)
 #undef RSX_SS
+  RSX_LAUNCHED();
+  return 0;
+}
+
+// Range check of an id tensor on the device, with no host synchronisation: out = ids with every
+// id outside [lo, hi) replaced by 0 (so a following gather never reads out of bounds), *flag set
+// to 1 if any id was out of range, else left as the caller initialised it.
+RSX_API int rsx_ids_check(const int64_t* ids, int64_t n, int64_t lo, int64_t hi, int64_t* out, int* flag,
+                          void* stream) {
+  RSX_ARG(ids && out && flag, "null tensor");
+  RSX_ARG(lo <= 0 && 0 < hi, "the replacement id 0 must lie in [lo, hi)");
+  if (n == 0) return 0;
+  int64_t g = (n + 255) / 256;
+  if (g > 1024) g = 1024;
+  hipLaunchKernelGGL(ids_check_k, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, ids, n, lo, hi, out, flag);
   RSX_LAUNCHED();
   return 0;
 }

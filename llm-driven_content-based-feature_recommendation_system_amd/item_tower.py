@@ -214,6 +214,13 @@ class HybridItemTower(nn.Module):
         self.transformer = nn.TransformerEncoder(encoder_layer, num_layers=2, enable_nested_tensor=False)
         self.head = DeepResidualHead(input_dim=embed_dim, output_dim=output_dim)
         self.embed_dim = embed_dim
+        self._std_guard = ops.IdRangeGuard("std_embedding (STD ids, utils/vocab.py:436-441)")
+
+    def check_inputs(self):
+        """Raise IndexError if any forward so far received an STD id outside the embedding
+        (checked on the device; waits for those checks). The serving / training loops call it
+        where they synchronise anyway."""
+        self._std_guard.check()
 
     def re_vectors(self, re_input_ids, re_attn_mask):
         """RE fields: BERT word embeddings (no grad) -> re_proj -> masked mean over the field's
@@ -253,9 +260,9 @@ class HybridItemTower(nn.Module):
         return _ln(vec, self.re_ln)
 
     def forward(self, std_input, re_input_ids, re_attn_mask, text_input_ids, text_attn_mask):
-        n_std = self.std_embedding.num_embeddings
-        if std_input.numel() and (int(std_input.max()) >= n_std or int(std_input.min()) < 0):
-            raise IndexError(f"STD id out of range [0, {n_std}) for std_embedding (utils/vocab.py ids 0..383)")
+        # the ids' range is checked on the device (no host sync); an out-of-range id raises
+        # IndexError from the next forward or check_inputs() (the callers' sync points)
+        std_input = self._std_guard(std_input, self.std_embedding.num_embeddings)
         std_emb = _ln(self.std_embedding(std_input) + self.std_field_emb, self.std_ln)        # :240-243
         re_vec = self.re_vectors(re_input_ids, re_attn_mask)                                   # :247-262
         if (not torch.is_grad_enabled() and not self.bert_model.training
@@ -395,6 +402,8 @@ def train_simcse_from_db(encoder: nn.Module, projector: nn.Module, db_session, b
                 align, uni = calculate_metrics(e1, e2)
                 print(f"epoch {epoch + 1} step {step} loss {loss.item():.4f} align {align:.4f} uni {uni:.4f}")
             total += float(loss.item())
+            if hasattr(encoder, "check_inputs"):
+                encoder.check_inputs()          # after the step's own sync: STD id range errors
             step += 1
         avg = total / step if step else float("nan")
         history.append(avg)

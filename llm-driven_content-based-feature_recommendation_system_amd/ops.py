@@ -1396,25 +1396,108 @@ def reranker_batch(uidx, iidx, tables, max_len=50):
 
 # ----------------------------------------------------------------------------------------
 # A14: retrieval top-k
+class IdRangeGuard:
+    """Range check of embedding ids on the device without a host sync (rsx_ids_check): the call
+    returns the ids with every out-of-range id replaced by 0 (the following gather stays in
+    bounds) and copies a device flag into pinned host memory behind an event. The error is
+    raised as IndexError by the next call whose flag is visible (a non-blocking event query) or
+    by check(), which the callers run at their own synchronisation points -- like the
+    asynchronous device-side assert an out-of-range nn.Embedding index raises on the
+    reference's CUDA path."""
+
+    def __init__(self, what):
+        self.what = what
+        self.pending = []
+
+    def __call__(self, ids, n):
+        self.poll()
+        N.ensure_device(ids)
+        ids = _c(ids.to(torch.int64))
+        out = torch.empty_like(ids)
+        flag = torch.zeros(1, device=ids.device, dtype=torch.int32)
+        N.check(N.lib().rsx_ids_check(N.ptr(ids), ids.numel(), 0, int(n), N.ptr(out), N.ptr(flag), N.stream()),
+                "ids_check")
+        host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+        host.copy_(flag, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.pending.append((ev, host, flag, int(n)))
+        return out
+
+    def poll(self, wait=False):
+        while self.pending and (wait or self.pending[0][0].query()):
+            ev, host, _, n = self.pending.pop(0)
+            ev.synchronize()
+            if int(host[0]):
+                self.pending.clear()
+                raise IndexError(f"{self.what}: id out of range [0, {n})")
+
+    def check(self):
+        """Raise for any call so far whose ids were out of range (waits for their checks)."""
+        self.poll(wait=True)
+
+
+_TOPK_PATHS = {0: "list", 1: "fast", 2: "bf16"}
+_TOPK_CORPUS = {}
+
+
+def _topk_corpus(it):
+    """The bf16 corpus image of `it` for the single-scan path (rsx_topk_prepare_corpus), cached
+    for the most recent corpus and rebuilt when it changes (identity, storage or in-place
+    version, as DeepFM's images): retrieval corpora are static between calls (the serving
+    index, evaluate_model's normalised item table), so the conversion pass runs once, not per
+    call. A call on another stream waits for the image's build."""
+    dev = it.device
+    st = _TOPK_CORPUS.get(dev)
+    if st is not None and st["key"].matches([it]):
+        cur = torch.cuda.current_stream(dev)
+        if cur != st["stream"]:
+            cur.wait_event(st["event"])
+        return st["buf"]
+    NI = it.shape[0]
+    buf = torch.empty(N.lib().rsx_topk_corpus_bytes(NI), device=dev, dtype=torch.uint8)
+    with timed("retrieve_topk/prepare"):
+        rc = N.lib().rsx_topk_prepare_corpus(N.ptr(it), it.stride(0), NI, N.ptr(buf), N.stream())
+    N.check(rc, "topk_prepare_corpus")
+    ev = torch.cuda.Event()
+    ev.record()
+    _TOPK_CORPUS[dev] = {"key": _FastKey([it]), "buf": buf, "event": ev,
+                         "stream": torch.cuda.current_stream(dev)}
+    return buf
+
+
 def retrieve_topk(queries, items, k, diag=None):
     """(scores [Q, k] desc, indices [Q, k] int64) of queries @ items.T without materialising
     the score matrix. Ties resolve to the lower item index. D = 128.
-    diag: optional dict; receives "fallback" (bool) and "fallback_queries" (int): how many queries
-    the single-scan path's exactness check sent to the exact list-based kernels (one host sync,
-    for tests / diagnostics)."""
+    Large corpora take the bf16 single scan + exact fp32 rescoring (path "bf16"), whose corpus
+    image is cached across calls (_topk_corpus). diag: optional dict; receives "path" ("list" /
+    "fast" / "bf16"), "fallback" (bool) and "fallback_queries" (int): how many queries the
+    path's exactness check sent to the exact list-based kernels (the "fast" path re-runs the
+    whole batch; one host sync, for tests / diagnostics)."""
     N.ensure_device(queries)
     q = _c(queries.to(torch.float32))
     it = items if (items.stride(-1) == 1 and items.stride(0) % 4 == 0) else items.contiguous()
     Q, NI = q.shape[0], it.shape[0]
-    ws = torch.empty(N.lib().rsx_topk_workspace_bytes(Q, NI, k), device=q.device, dtype=torch.uint8)
+    path = N.lib().rsx_topk_path(Q, NI, k)
+    corpus = _topk_corpus(it) if path == 2 and Q > 0 else None
+    nws = (N.lib().rsx_topk_workspace_bytes_corpus(Q, NI, k) if corpus is not None
+           else N.lib().rsx_topk_workspace_bytes(Q, NI, k))
+    ws = torch.empty(nws, device=q.device, dtype=torch.uint8)
     sc = torch.empty(Q, k, device=q.device, dtype=torch.float32)
     ix = torch.empty(Q, k, device=q.device, dtype=torch.int64)
     with timed("retrieve_topk"):
-        rc = N.lib().rsx_retrieve_topk(N.ptr(q), q.stride(0), N.ptr(it), it.stride(0), Q, NI, k, N.ptr(ws),
-                                       N.ptr(sc), N.ptr(ix), N.stream())
+        if corpus is not None:
+            rc = N.lib().rsx_retrieve_topk_corpus(N.ptr(q), q.stride(0), N.ptr(it), it.stride(0), N.ptr(corpus), Q,
+                                                  NI, k, N.ptr(ws), N.ptr(sc), N.ptr(ix), N.stream())
+        else:
+            rc = N.lib().rsx_retrieve_topk(N.ptr(q), q.stride(0), N.ptr(it), it.stride(0), Q, NI, k, N.ptr(ws),
+                                           N.ptr(sc), N.ptr(ix), N.stream())
     N.check(rc, "retrieve_topk")
     if diag is not None:
-        n = int(ws[:4].view(torch.int32).item())
+        h = ws[:16].view(torch.int32).cpu().tolist()
+        assert h[1] == path, (h, path)
+        n = h[0] if path == 2 else (Q if (path == 1 and h[2]) else 0)
+        diag["path"] = _TOPK_PATHS[path]
         diag["fallback"], diag["fallback_queries"] = n > 0, n
     return sc, ix
 

@@ -55,6 +55,8 @@ def generate_and_save_item_vectors(db_session, save_dir: str = "models", safe_mo
                     v = model(*inputs)
                     vecs.append(v.cpu() if safe_mode else v)
             final = torch.cat(vecs, dim=0).cpu()
+            if hasattr(model, "check_inputs"):
+                model.check_inputs()            # STD ids range-checked on the device
         except RuntimeError as e:
             if "out of memory" in str(e).lower():
                 torch.cuda.empty_cache()

@@ -131,6 +131,12 @@ def test_golden_oracle_deepfm_and_retrieval():
     t, meta = load("retrieval_q24")
     sc, idx = OR.retrieve_topk(t["in.queries_x8"].float() / 8, t["in.items_x16"].float() / 16, meta["k"])
     assert torch.equal(idx, t["out.index"]) and torch.equal(sc, t["out.scores"])
+    # the chunked form (the 1M-item tests' oracle) on the same fixture, with chunks that cut
+    # through the planted tie groups, in both score dtypes (dyadic inputs: fp32 scores are exact)
+    for dtype in (torch.float64, torch.float32):
+        sc2, idx2 = OR.retrieve_topk_chunked(t["in.queries_x8"].float() / 8, t["in.items_x16"].float() / 16,
+                                             meta["k"], dtype=dtype, chunk=333)
+        assert torch.equal(idx2, t["out.index"]) and torch.equal(sc2.double(), t["out.scores"])
 
 
 # ------------------------------------------------------------------ GPU: HIP path vs fixtures

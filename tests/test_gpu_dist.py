@@ -124,8 +124,8 @@ def test_dp_objective_grads_and_sharded_topk_world2(gpu):
             assert launched >= 1, (precision, launched)
 
 
-def _dp_fullsize_worker(rank, world, port, q):
-    """Global batch 8192 split 2 x 4096 (H&M-shaped lengths, 47,062 items: ~153k valid steps,
+def _dp_fullsize_worker(rank, world, port, q, G=8192, precisions=("bf16x3", "fp32")):
+    """Global batch G (8192: 2 x 4096; configs[3]'s 32,768: 2 x 16,384) split over the ranks (H&M-shaped lengths, 47,062 items: ~153k valid steps,
     ~24.4k distinct targets), so the grouped loss's column split, XCD remap and tail split run
     with FOREIGN columns (the other rank's targets, t_cols = the gathered ids) and user ids
     offset by rank * 4096 (dist.py prepare_step_index)."""
@@ -147,14 +147,13 @@ def _dp_fullsize_worker(rank, world, port, q):
         cfg = TT.PipelineConfig(num_items=I, num_prod_types=hs, num_colors=hs, num_graphics=hs, num_sections=hs,
                                 dropout=0.0)
         items = synth.make_items(num_items=I, d=128, seed=0)
-        G = 8192
         b = G // world
         full = to_dev(synth.make_batch(items, G, seed=100), dev)
         mine = {k: (v[rank * b:(rank + 1) * b] if torch.is_tensor(v) else v) for k, v in full.items()}
         lookup = items.pretrained.to(dev)
         n_dist = int(torch.unique(full["target_ids"][~full["padding_mask"]]).numel())
         res = {"distinct_targets": n_dist}
-        for precision in ("bf16x3", "fp32"):
+        for precision in precisions:
             ops.set_nce_precision(precision)
 
             def build():
@@ -214,3 +213,77 @@ def test_dp_fullsize_world2_equals_single_gpu(gpu):
     assert status == {0: "ok", 1: "ok"}, status
     print({r: res for r, _, res in out})
     assert out[0][2]["distinct_targets"] >= 10_000
+
+
+def test_dp_global_batch_32768_world2_equals_single_gpu(gpu):
+    """configs[3]'s global batch: 2 ranks x 16,384 users (~600k valid steps, ~41k distinct
+    targets, all-gathered ids so every rank's loss runs against the global pool) ==
+    TT.contrastive_losses / its gradients on the concatenated 32,768-user batch on one device:
+    loss 1e-4, every gradient 2e-3 of its scale (bf16x3, the step's precision)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_fullsize_worker, args=(r, 2, port, q, 32_768, ("bf16x3",))) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=115) for _ in procs]
+    for p in procs:
+        p.join(timeout=30)
+    status = {r: s for r, s, _ in out}
+    assert status == {0: "ok", 1: "ok"}, status
+    print({r: res for r, _, res in out})
+    assert out[0][2]["distinct_targets"] >= 35_000
+
+
+def _sharded_1m_worker(rank, world, port, q):
+    """configs[4]'s corpus sharded by item range over 2 ranks (500,001 + 499,999 items): dyadic
+    values (exact scores, heavy exact ties, some of them planted across the shard boundary),
+    k = 100 and 500; the merged result is bit-identical to the unsharded call and the oracle."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import recsys_amd  # noqa: F401
+        from recsys_amd import dist as D
+        from recsys_amd import ops
+        from oracle import retrieval as OR
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        g = torch.Generator().manual_seed(51)
+        NI = 1_000_000
+        corpus = torch.randint(-4, 5, (NI, 128), generator=g).float() / 8.0
+        queries = torch.randint(-4, 5, (64, 128), generator=g).float() / 8.0
+        corpus[500_001] = corpus[17]
+        corpus[499_999] = corpus[900_000]
+        bounds = [0, 500_001, NI]
+        lo, hi = bounds[rank], bounds[rank + 1]
+        cd, qd = corpus.to(dev), queries.to(dev)
+        for k in (100, 500):
+            s, i = D.retrieve_topk_sharded(qd, cd[lo:hi], lo, k)
+            s_ref, i_ref = ops.retrieve_topk(qd, cd, k)
+            assert torch.equal(i.cpu(), i_ref.cpu()), k
+            assert torch.equal(s.cpu(), s_ref.float().cpu()), k
+            if rank == 0:
+                rs, ri = OR.retrieve_topk_chunked(queries, corpus, k)
+                assert torch.equal(i.cpu(), ri) and torch.equal(s.cpu().double(), rs), k
+        q.put((rank, "ok", None))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc()[-1500:], None))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_topk_1m_world2_bit_exact(gpu):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sharded_1m_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=115) for _ in procs]
+    for p in procs:
+        p.join(timeout=30)
+    status = {r: s for r, s, _ in out}
+    assert status == {0: "ok", 1: "ok"}, status

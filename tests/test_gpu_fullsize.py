@@ -103,6 +103,61 @@ def test_grouped_logq_loss_full_size(gpu, B, precision):
     assert err <= 1e-3 * g_cpu.abs().max().item(), err
 
 
+def test_grouped_logq_loss_global_batch_32768(gpu):
+    """configs[3]'s global batch (32,768 users: N ~ 600k valid rows, D ~ 41.3k distinct targets)
+    on one device, both precisions, against the oracle's chunked reference formula in float64 (one
+    evaluation shared by both precisions; 1,024-row chunks of the N x N logits): loss 1e-4, both
+    gradients 1e-3 of their scale; plus 512 sampled rows in plain CPU float64."""
+    items = _universe()
+    B = 32_768
+    batch = synth.make_batch(items, B, seed=300)
+    valid = ~batch["padding_mask"]
+    t = batch["target_ids"][valid]
+    uid = torch.arange(B).unsqueeze(1).expand(-1, valid.shape[1])[valid]
+    N = t.numel()
+    assert N > 500_000
+    g = torch.Generator().manual_seed(B)
+    U = F.normalize(torch.randn(N, 128, generator=g), dim=1)
+    Wn = F.normalize(items.pretrained, dim=1)
+    lq = items.log_q
+
+    U64 = U.double().to(gpu).requires_grad_()
+    W64 = Wn.double().to(gpu).requires_grad_()
+    ref = O.inbatch_corrected_logq_loss_chunked(U64, W64, t.to(gpu), uid.to(gpu), lq.double().to(gpu), chunk=1024)
+    ref.backward()
+    ref_loss = ref.item()
+    gu_ref = U64.grad.detach()
+    del U64, ref
+    torch.cuda.empty_cache()
+
+    rows = torch.cat([torch.tensor([0, 1, N - 2, N - 1]), torch.randperm(N, generator=g)[:508]]).unique()
+    l_cpu, g_cpu = _cpu_rows_f64(U.double(), Wn.double(), t, uid, lq.double(), rows)
+    assert torch.isfinite(l_cpu).all()
+
+    groups = ops.TargetGroups(t.to(gpu), uid.to(gpu))
+    assert groups.n_cols > 35_000
+    gw_ref = W64.grad[groups.uniq]
+    for precision in ("bf16x3", "fp32"):
+        Ud = U.to(gpu).requires_grad_()
+        items_d = Wn.to(gpu)[groups.uniq].clone().requires_grad_()
+        s, cnt = ops.nce_grouped_sum(Ud, items_d, lq.to(gpu)[groups.uniq], groups, tau=0.1, tag="fullsize",
+                                     precision=precision)
+        loss = s / cnt
+        loss.backward()
+        assert int(cnt.item()) == N
+        assert abs(loss.item() - ref_loss) < 1e-4, (precision, loss.item(), ref_loss)
+        err_u = (Ud.grad.double() - gu_ref).abs().max().item()
+        assert err_u <= 1e-3 * gu_ref.abs().max().item(), (precision, err_u)
+        err_w = (items_d.grad.double() - gw_ref).abs().max().item()
+        assert err_w <= 1e-3 * gw_ref.abs().max().item(), (precision, err_w)
+        g_dut = Ud.grad.detach().cpu().double()[rows] * N
+        err = (g_dut - g_cpu).abs().max().item()
+        assert err <= 1e-3 * g_cpu.abs().max().item(), (precision, err)
+        print(f"[32768 {precision}] N={N} D={groups.n_cols} |dloss|={abs(loss.item() - ref_loss):.2e} "
+              f"grad_u {err_u / gu_ref.abs().max().item():.2e} grad_w {err_w / gw_ref.abs().max().item():.2e}")
+        del Ud, items_d, s, cnt, loss
+
+
 def test_deepfm_full_size_vocab_1e6(gpu):
     from recsys_amd.temp_model.ranker_skelet import DeepFM
     R, Fn, V = 65_536, 39, 1_000_000

@@ -268,3 +268,29 @@ def test_item_tower_inference_uses_packed_bert_and_falls_back(gpu):
         got2 = tower(*x)
     want2 = tower(*x).detach()
     torch.testing.assert_close(got2, want2, atol=1e-5, rtol=1e-5)
+
+
+def test_std_id_range_checked_on_device(gpu):
+    """An STD id outside the embedding (here 384 for std_vocab_size 384) is caught by the device
+    check (rsx_ids_check, no host sync in forward): check_inputs() -- and, once the flag has
+    reached the host, the next forward -- raises IndexError; the gather itself never reads out
+    of bounds, and in-range batches after the error run normally."""
+    _, dut = _pair(64)
+    dut = dut.to(gpu).eval()
+    x = [t.to(gpu) for t in _inputs(8, seed=5)]
+    with torch.no_grad():
+        good = dut(*x)
+        dut.check_inputs()
+        bad = [t.clone() for t in x]
+        bad[0][3, 2] = 384
+        dut(*bad)
+        with pytest.raises(IndexError, match=r"out of range \[0, 384\)"):
+            dut.check_inputs()
+        again = dut(*x)                       # the error was reported once; in-range runs on
+        dut.check_inputs()
+        torch.testing.assert_close(again, good, atol=0, rtol=0)
+        bad[0][0, 0] = -1
+        dut(*bad)
+        torch.cuda.synchronize()
+        with pytest.raises(IndexError):
+            dut(*x)                           # the flag is visible: raised by the next forward

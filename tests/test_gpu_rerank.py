@@ -113,16 +113,21 @@ def test_reranking_system_deepfm(gpu):
     assert scores == sorted(scores, reverse=True)
 
 
-@pytest.mark.parametrize("Q,NI,k", [(130, 100003, 100), (70, 60000, 500), (257, 40000, 7)])
-def test_retrieve_topk_fast_path_bit_exact(gpu, Q, NI, k):
-    """Large corpora take the bf16 single scan + exact rescoring path: on dyadic inputs (exact
-    dot products and exact bf16 images, many exact ties) the result must equal the oracle's
-    (score desc, index asc), whether or not the exactness check falls back."""
+@pytest.mark.parametrize("Q,NI,k,path", [(130, 100003, 100, "bf16"), (70, 60000, 500, "fast"), (257, 40000, 7, "bf16"),
+                                         (5000, 70000, 64, "bf16")])
+def test_retrieve_topk_fast_path_bit_exact(gpu, Q, NI, k, path):
+    """Large corpora take the bf16 single scan + exact rescoring path (or, where its sample
+    cannot hold 2k candidates, the fp32 candidate/threshold path): on dyadic inputs (exact dot
+    products and exact bf16 images, many exact ties) the result must equal the oracle's (score
+    desc, index asc), whether or not the exactness check falls back. Q = 5000 runs the bf16 path
+    in two query chunks (4096 + 904)."""
     g = torch.Generator().manual_seed(Q * 7 + k)
     U = torch.randint(-4, 5, (Q, 128), generator=g).float() / 8.0
     I = torch.randint(-4, 5, (NI, 128), generator=g).float() / 8.0
-    s, i = ops.retrieve_topk(U.to(gpu), I.to(gpu), k)
-    rs, ri = OR.retrieve_topk(U, I, k)
+    diag = {}
+    s, i = ops.retrieve_topk(U.to(gpu), I.to(gpu), k, diag=diag)
+    assert diag["path"] == path
+    rs, ri = OR.retrieve_topk_chunked(U, I, k)
     assert torch.equal(i.cpu(), ri)
     assert torch.equal(s.cpu().double(), rs)
 
@@ -140,15 +145,17 @@ def test_retrieve_topk_fast_path_overflow_fallback(gpu):
     assert torch.equal(s.cpu().double(), rs)
 
 
-@pytest.mark.parametrize("Q,NI,k", [(600, 200_000, 100), (40, 50_000, 300)])
+@pytest.mark.parametrize("Q,NI,k", [(600, 200_000, 100), (40, 200_000, 300)])
 def test_retrieve_topk_single_scan_no_fallback_on_spread_data(gpu, Q, NI, k):
-    """Realistic normalised data: the bf16 single scan + exact rescoring is exact by its own
-    check (no fallback), and the result equals the float64 oracle up to fp32-noise near-ties."""
+    """Realistic normalised data: the bf16 single scan + exact rescoring (both cases take that
+    path: asserted from the workspace header) is exact by its own check (no fallback), and the
+    result equals the float64 oracle up to fp32-noise near-ties."""
     g = torch.Generator().manual_seed(NI + k)
     U = torch.nn.functional.normalize(torch.randn(Q, 128, generator=g), dim=1)
     I = torch.nn.functional.normalize(torch.randn(NI, 128, generator=g), dim=1)
     diag = {}
     s, i = ops.retrieve_topk(U.to(gpu), I.to(gpu), k, diag=diag)
+    assert diag["path"] == "bf16"
     assert diag["fallback"] is False
     rs, ri = OR.retrieve_topk(U, I, k)
     torch.testing.assert_close(s.cpu().double(), rs, atol=2e-6, rtol=0)
@@ -174,6 +181,7 @@ def test_retrieve_topk_single_scan_clustered_falls_back_exactly(gpu):
     I[60_400:60_410] = U[0]                  # exact ties among the top items
     diag = {}
     s, i = ops.retrieve_topk(U.to(gpu), I.to(gpu), 100, diag=diag)
+    assert diag["path"] == "bf16"
     assert diag["fallback"] is True and 1 <= diag["fallback_queries"] < Q   # per query, not the batch
     rs, ri = OR.retrieve_topk(U, I, 100)
     assert torch.equal(i.cpu(), ri)

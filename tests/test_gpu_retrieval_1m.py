@@ -1,0 +1,123 @@
+"""configs[4] at its size: exact top-k over a 1,000,000-item corpus (evaluate_model's scores = U
+normalize(W)^T; topk(max_k), tower_code/v1_usertower_train.py:672-675; ReRankingSystem.recommend,
+temp_model/ranker_skelet.py:193-196) on the HIP path (rsx_retrieve_topk, bf16 single scan + exact
+fp32 rescoring, with the per-query exact fallback), 256 queries per case.
+
+* Dyadic corpus (every score exact in fp32 and in the bf16 image, heavy exact ties): indices and
+  scores bit-identical to the float64 oracle, k = 100 and 500.
+* Spread normalised data, k = 100 and 500 (recommend's top-100, evaluate_model's max_k = 500):
+  against the float64 oracle and the fp32 oracle (the reference's own fp32 matmul). With
+  eps = the fp32 dot-product rounding bound (oracle.retrieval.fp32_dot_bound), each rank's exact
+  score is within 2 eps of the exact r-th best, and every index that differs from the fp32
+  oracle's is a near-tie: the two items' exact scores within 4 eps.
+* A clustered corpus (near-copies of four queries stored contiguously, i.e. inside one split's
+  lane streams): the buffers of exactly those queries overflow and they alone go to the exact
+  kernels; results pass the same checks.
+The fallback counts are printed (pytest -s) and summarised in DESIGN.md.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+import recsys_amd  # noqa: F401
+from recsys_amd import ops
+from oracle import retrieval as OR
+
+pytestmark = pytest.mark.gpu
+
+NI = 1_000_000
+Q = 256
+
+
+def _dyadic(seed):
+    g = torch.Generator().manual_seed(seed)
+    U = torch.randint(-4, 5, (Q, 128), generator=g).float() / 8.0
+    I = torch.randint(-4, 5, (NI, 128), generator=g).float() / 8.0
+    return U, I
+
+
+def _spread(seed):
+    g = torch.Generator().manual_seed(seed)
+    U = F.normalize(torch.randn(Q, 128, generator=g), dim=1)
+    I = F.normalize(torch.randn(NI, 128, generator=g), dim=1)
+    return U, I
+
+
+def _exact_scores(U, I, idx):
+    """float64 scores of the items idx [Q, k] for each query."""
+    return torch.einsum("qkd,qd->qk", I[idx].double(), U.double())
+
+
+def _check_near_ties(U, I, k, s, i):
+    """s, i: the HIP result (CPU). Near-tie criterion against the float64 and fp32 oracles."""
+    eps = OR.fp32_dot_bound(128, U.norm(dim=1).max().item(), I.norm(dim=1).max().item())
+    assert (i >= 0).all() and (i < NI).all()
+    assert all(row.unique().numel() == k for row in i)                 # k distinct items per query
+    assert (s[:, :-1] >= s[:, 1:]).all()                               # sorted by score desc
+    ours = _exact_scores(U, I, i)
+    assert (s.double() - ours).abs().max().item() <= eps               # fp32 rescoring of these items
+    rs64, _ = OR.retrieve_topk_chunked(U, I, k, dtype=torch.float64)
+    assert (ours - rs64).abs().max().item() <= 2 * eps                 # rank-wise vs the exact ranking
+    rs32, ri32 = OR.retrieve_topk_chunked(U, I, k, dtype=torch.float32)
+    mism = i != ri32
+    ref = _exact_scores(U, I, ri32)
+    if mism.any():
+        assert (ours - ref).abs()[mism].max().item() <= 4 * eps        # every mismatch is a near-tie
+    frac = mism.float().mean().item()
+    assert frac < 0.01, frac
+    return frac, eps
+
+
+@pytest.mark.parametrize("k", [100, 500])
+def test_retrieval_1m_dyadic_bit_exact(gpu, k):
+    U, I = _dyadic(1000 + k)
+    diag = {}
+    s, i = ops.retrieve_topk(U.to(gpu), I.to(gpu), k, diag=diag)
+    assert diag["path"] == "bf16"
+    rs, ri = OR.retrieve_topk_chunked(U, I, k, dtype=torch.float64)
+    print(f"[1M dyadic k={k}] exact-kernel queries {diag['fallback_queries']}/{Q}")
+    assert torch.equal(i.cpu(), ri)
+    assert torch.equal(s.cpu().double(), rs)
+
+
+@pytest.mark.parametrize("k", [100, 500])
+def test_retrieval_1m_spread_near_ties(gpu, k):
+    U, I = _spread(2000 + k)
+    diag = {}
+    s, i = ops.retrieve_topk(U.to(gpu), I.to(gpu), k, diag=diag)
+    assert diag["path"] == "bf16"
+    frac, eps = _check_near_ties(U, I, k, s.cpu(), i.cpu())
+    print(f"[1M spread k={k}] exact-kernel queries {diag['fallback_queries']}/{Q}, "
+          f"index mismatches vs the fp32 oracle {frac:.5f} (all within 4 eps = {4 * eps:.2e})")
+    assert diag["fallback_queries"] <= Q // 64                         # spread data: the fallback is rare
+
+
+def test_retrieval_1m_clustered_per_query_fallback(gpu):
+    U, I = _spread(3000)
+    g = torch.Generator().manual_seed(3001)
+    for c in range(4):                          # 2,000 near-copies of query c, contiguous
+        lo = 400_000 + 2_000 * c
+        I[lo:lo + 2_000] = F.normalize(U[c] + 0.05 * torch.randn(2_000, 128, generator=g), dim=1)
+    diag = {}
+    s, i = ops.retrieve_topk(U.to(gpu), I.to(gpu), 100, diag=diag)
+    print(f"[1M clustered] exact-kernel queries {diag['fallback_queries']}/{Q}")
+    assert diag["path"] == "bf16" and 4 <= diag["fallback_queries"] < Q // 8
+    _check_near_ties(U, I, 100, s.cpu(), i.cpu())
+    assert (i[:4].cpu() >= 400_000).all() and (i[:4].cpu() < 408_000).all()   # each cluster wins
+
+
+def test_retrieval_cached_corpus_follows_updates(gpu):
+    """The bf16 corpus image is cached across calls (ops._topk_corpus) and rebuilt when the
+    corpus changes in place; a new corpus tensor replaces it."""
+    g = torch.Generator().manual_seed(9)
+    U = (torch.randint(-4, 5, (64, 128), generator=g).float() / 8.0).to(gpu)
+    I = (torch.randint(-4, 5, (200_000, 128), generator=g).float() / 8.0).to(gpu)
+    for step in range(3):
+        s, i = ops.retrieve_topk(U, I, 50)
+        rs, ri = OR.retrieve_topk_chunked(U.cpu(), I.cpu(), 50)
+        assert torch.equal(i.cpu(), ri) and torch.equal(s.cpu().double(), rs), step
+        if step == 0:
+            I[123] = U[0]                        # in place: a new winner for query 0
+        else:
+            I = I.flip(0).contiguous()           # a new tensor
+    assert ops._TOPK_CORPUS[gpu]["key"].matches([I])
