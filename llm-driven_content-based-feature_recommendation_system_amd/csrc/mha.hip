@@ -1380,6 +1380,12 @@ __global__ __launch_bounds__(256) void mha_bwd_x3s_k(BwdArgs a) {
     }
   }
 
+  // pass 2 reads dS entries other lanes of this wave wrote in pass 1: order the wave's LDS
+  // writes before those reads explicitly (the per-wave stash is never touched by other waves)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
   // ---- pass 2: dQ[i] = sum_j dS[i][j] K[j] from the stashed tiles (qb-major, kb <= qb): the
   // tile is read transposed (lane (c, g): query 16qb + c, keys 16kb + 4g + 0..3 = the A operand),
   // K's columns are the only loads; S, dP and the softmax gradient are not recomputed ----

@@ -4,7 +4,11 @@ Layout contract follows the reference's producers:
   * SASRecDataset.__getitem__   tower_code/v1_refine_usertower.py:204-306
       left padding with 0 to max_len, input = seq[:-1], target = seq[1:] of the last
       max_len+1 purchases, padding_mask True = pad, time buckets 1..9 (0 = pad)
-  * item side ids (md5 % 1000 + 1)  tower_code/v1_usertower_train.py:211-262
+  * item side ids: the reference hashes four metadata strings per item with get_hash_id
+      (md5 of the stripped lower-cased text % 1000 + 1, 0 for empty / unknown / nan / none;
+      tower_code/v1_usertower_train.py:211-262, restated below as get_hash_id /
+      hashed_side_ids). Synthetic items have no metadata text, so make_items draws the ids
+      uniformly from that function's range 1..HASH_SIZE (row 0 = pad).
   * aligned pretrained matrix row 0 = 0  tower_code/v1_usertower_train.py:137-139
   * FeatureProcessor.get_logq_probs   tower_code/v1_refine_usertower.py:124-137
 Sequence lengths are drawn from the purchase counts of the 100 customers in the
@@ -57,6 +61,31 @@ def logq_from_probs(raw_probs: np.ndarray) -> torch.Tensor:
     full[1:] = lq
     full[0] = -20.0
     return torch.from_numpy(full)
+
+
+def get_hash_id(text, hash_size: int = 1000) -> int:
+    """v1_usertower_train.py:211-218: a session-stable id in 1..hash_size for a metadata string
+    (0 = padding for empty / 'unknown' / 'nan' / 'none')."""
+    import hashlib
+    if not text or str(text).lower() in ("unknown", "nan", "none"):
+        return 0
+    return int(hashlib.md5(str(text).strip().lower().encode("utf-8")).hexdigest(), 16) % hash_size + 1
+
+
+SIDE_FIELDS = ("product_type_name", "colour_group_name", "graphical_appearance_name", "section_name")
+
+
+def hashed_side_ids(item_meta, hash_size: int = 1000) -> torch.Tensor:
+    """load_item_metadata_hashed (v1_usertower_train.py:220-262) without the file IO: item_meta
+    is a list (index i = item id i + 1) of metadata dicts or None (unmatched -> zeros); returns
+    the [len + 1, 4] int64 side-id table (type, colour, graphic, section), row 0 = pad."""
+    arr = np.zeros((len(item_meta) + 1, 4), dtype=np.int64)
+    for i, meta in enumerate(item_meta):
+        if meta is None:
+            continue
+        for f, key in enumerate(SIDE_FIELDS):
+            arr[i + 1, f] = get_hash_id(meta.get(key, ""), hash_size)
+    return torch.tensor(arr, dtype=torch.long)
 
 
 @dataclass

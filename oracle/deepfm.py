@@ -11,16 +11,18 @@ import torch
 import torch.nn.functional as F
 
 
-def deepfm_forward(x, emb_tables, lin_tables, out_bias, dnn_weights, dnn_biases, w_out):
-    """x [R, F] int64 -> (logit [R], prob [R]) in float64 on the CPU."""
-    emb = torch.stack([t.double()[x[:, f]] for f, t in enumerate(emb_tables)], dim=1)      # [R, F, E]
-    linear = sum(t.double().reshape(-1)[x[:, f]] for f, t in enumerate(lin_tables))        # [R]
+def deepfm_forward(x, emb_tables, lin_tables, out_bias, dnn_weights, dnn_biases, w_out, dtype=torch.float64):
+    """x [R, F] int64 -> (logit [R], prob [R]) in `dtype` (float64 for the parity tests; float32,
+    the reference arithmetic, for bench.py's CPU baseline) on the CPU. Rows are gathered before
+    the conversion (the same values as converting the tables)."""
+    emb = torch.stack([t[x[:, f]].to(dtype) for f, t in enumerate(emb_tables)], dim=1)      # [R, F, E]
+    linear = sum(t.reshape(-1)[x[:, f]].to(dtype) for f, t in enumerate(lin_tables))        # [R]
     square_of_sum = emb.sum(dim=1) ** 2
     sum_of_square = (emb * emb).sum(dim=1)
     fm = 0.5 * (square_of_sum - sum_of_square).sum(dim=1)
     h = emb.reshape(emb.shape[0], -1)
     for w, b in zip(dnn_weights, dnn_biases):
-        h = F.relu(h @ w.double().T + b.double())
-    dnn = h @ w_out.double().reshape(-1)
+        h = F.relu(h @ w.to(dtype).T + b.to(dtype))
+    dnn = h @ w_out.to(dtype).reshape(-1)
     logit = out_bias + linear + fm + dnn
     return logit, torch.sigmoid(logit)

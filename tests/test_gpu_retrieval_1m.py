@@ -118,6 +118,6 @@ def test_retrieval_cached_corpus_follows_updates(gpu):
         assert torch.equal(i.cpu(), ri) and torch.equal(s.cpu().double(), rs), step
         if step == 0:
             I[123] = U[0]                        # in place: a new winner for query 0
-        else:
+        elif step == 1:
             I = I.flip(0).contiguous()           # a new tensor
     assert ops._TOPK_CORPUS[gpu]["key"].matches([I])

@@ -128,3 +128,23 @@ def test_packed_tokens_layout():
     # the extra (padded) token of a user is its first packed token and has no valid key before it
     extra = pk.tok_pad.bool()
     assert torch.equal(extra.nonzero().squeeze(1), seg[:-1][pad[torch.arange(B), last]])
+
+
+def test_get_hash_id_and_side_table():
+    """synth.get_hash_id / hashed_side_ids restate v1_usertower_train.py:211-262: md5 of the
+    stripped lower-cased text, % hash_size + 1; 0 for empty / unknown / nan / none; unmatched
+    items keep zeros; row 0 is the pad row."""
+    import hashlib
+    from recsys_amd import synth
+    h = lambda t: int(hashlib.md5(t.encode("utf-8")).hexdigest(), 16) % 1000 + 1  # noqa: E731
+    assert synth.get_hash_id("Vest top") == h("vest top") == synth.get_hash_id("  VEST TOP ")
+    for t in ("", None, "Unknown", "NaN", "none"):
+        assert synth.get_hash_id(t) == 0
+    assert 1 <= synth.get_hash_id("Solid", 7) <= 7
+    meta = [{"product_type_name": "Vest top", "colour_group_name": "Black", "graphical_appearance_name": "Solid",
+             "section_name": "Womens Everyday Basics"}, None, {"product_type_name": "Sweater"}]
+    tab = synth.hashed_side_ids(meta)
+    assert tab.shape == (4, 4) and tab.dtype == torch.int64
+    assert tab[0].tolist() == [0, 0, 0, 0] and tab[2].tolist() == [0, 0, 0, 0]
+    assert tab[1].tolist() == [h("vest top"), h("black"), h("solid"), h("womens everyday basics")]
+    assert tab[3].tolist() == [h("sweater"), 0, 0, 0]
