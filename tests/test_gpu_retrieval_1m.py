@@ -10,9 +10,10 @@ fp32 rescoring, with the per-query exact fallback), 256 queries per case.
   eps = the fp32 dot-product rounding bound (oracle.retrieval.fp32_dot_bound), each rank's exact
   score is within 2 eps of the exact r-th best, and every index that differs from the fp32
   oracle's is a near-tie: the two items' exact scores within 4 eps.
-* A clustered corpus (near-copies of four queries stored contiguously, i.e. inside one split's
-  lane streams): the buffers of exactly those queries overflow and they alone go to the exact
-  kernels; results pass the same checks.
+* A clustered corpus (2,000 near-copies of each of four queries stored contiguously, i.e. inside
+  one or two splits' lane streams): the stream buffers of those queries -- and of the few other
+  queries correlated with them, whose high scores also concentrate there (20 of 256 on the
+  round-4 run) -- overflow and only they go to the exact kernels; results pass the same checks.
 The fallback counts are printed (pytest -s) and summarised in DESIGN.md.
 """
 import pytest
