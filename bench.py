@@ -183,19 +183,50 @@ class _Heartbeat:
         return False
 
 
-def cpu_baseline(args, items, cfg, batch_size, batch_seed):
-    """The oracle (CPU PyTorch fp32 restatement of tower_code/v1_usertower_train.py:717-893) on
-    the SAME global batch the GPU headline runs (same generator, same seed): one timed step
-    after a small warm-up step; the main loss row-chunked (same arithmetic, bounded RAM)."""
-    from oracle import user_tower as O
-    from recsys_amd import synth
+def cpu_threads(args):
+    """(threads, host info, rule): BASELINE.md's P = physical host cores, capped by this
+    process's affinity mask and cgroup CPU quota (the GPU box grants a share of the host)."""
     info = host_cpu_info()
     phys = info.get("physical_cores") or os.cpu_count() or 1
     avail = min(info.get("affinity_cpus") or phys, int(info.get("cgroup_cpu_quota") or phys))
     threads = max(1, min(args.cpu_threads or phys, phys, avail))
+    rule = ("physical cores (BASELINE.md), capped by this process's affinity mask / cgroup CPU quota: "
+            f"physical {phys}, usable {avail}")
+    return threads, info, rule
+
+
+def cpu_timed(fn, warm=2, reps=5, single_over_s=60.0):
+    """BASELINE.md's CPU timing rule: `warm` untimed calls, then the median of `reps` timed calls
+    (one timed call when a call takes longer than single_over_s). -> (median s, timed calls)."""
+    t0 = time.perf_counter()
+    fn()
+    first = time.perf_counter() - t0
+    if first > single_over_s:
+        return first, 1
+    for _ in range(warm - 1):
+        fn()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    return ts[len(ts) // 2], reps
+
+
+def cpu_baseline(args, items, cfg, batch_size, batch_seed):
+    """The oracle (CPU PyTorch fp32 restatement of tower_code/v1_usertower_train.py:717-893) on
+    the SAME global batch the GPU headline runs (same generator, same seed), dropout p = 0
+    (BASELINE.md): one timed step after a small warm-up step; the main loss row-chunked (same
+    arithmetic, bounded RAM)."""
+    import dataclasses
+    from oracle import user_tower as O
+    from recsys_amd import synth
+    threads, info, rule = cpu_threads(args)
     prev_threads = torch.get_num_threads()
     torch.set_num_threads(threads)
     torch.manual_seed(args.seed)
+    cfg = dataclasses.replace(cfg, dropout=0.0)
     model = O.OracleUserTower(cfg)
     model.train()
     W = torch.nn.Parameter(items.pretrained.clone())
@@ -212,15 +243,116 @@ def cpu_baseline(args, items, cfg, batch_size, batch_seed):
     torch.set_num_threads(prev_threads)
     return {"value": round(batch_size / dt, 3), "unit": "pairs/s", "cores": threads,
             "kind": "port",
-            "threads_rule": ("physical cores (BASELINE.md), capped by this process's affinity mask / cgroup CPU "
-                             f"quota: physical {phys}, usable {avail}"),
+            "threads_rule": rule,
             "host": info,
-            "sample": (f"oracle/user_tower.py contrastive_step (fp32 PyTorch CPU, dropout 0.2, AdamW) on the GPU "
+            "sample": (f"oracle/user_tower.py contrastive_step (fp32 PyTorch CPU, dropout 0, AdamW) on the GPU "
                        f"headline's first global batch ({batch_size} users, {n_valid} valid steps, same seed); "
                        f"ONE timed step ({dt:.1f} s) after a 64-user warm-up step; main loss evaluated over "
                        f"{args.cpu_loss_chunk}-row chunks of the N x N logits under activation checkpointing "
                        f"(same per-element arithmetic; the one-shot N x N tensors would need ~{4 * n_valid ** 2 / 1e9:.0f} GB)"),
             "seconds_per_step": round(dt, 2)}
+
+
+def deepfm_cpu_state(model):
+    """Host copies of a DeepFM module's tables and DNN weights (the CPU baselines' inputs)."""
+    names = model.field_names
+    with torch.no_grad():
+        return {"emb": [model.embedding_dict[n].weight.detach().cpu() for n in names],
+                "lin": [model.linear_model.embedding_dict[n].weight.detach().cpu() for n in names],
+                "ws": [m.weight.detach().cpu() for m in model.dnn.linears],
+                "bs": [m.bias.detach().cpu() for m in model.dnn.linears],
+                "wo": model.dnn_linear.weight.detach().cpu(), "bias": float(model.out.bias.item())}
+
+
+def _deepfm_cpu(st, x):
+    from oracle import deepfm as OD
+    return OD.deepfm_forward(x, st["emb"], st["lin"], st["bias"], st["ws"], st["bs"], st["wo"], dtype=torch.float32)
+
+
+def cpu_baseline_deepfm(args, st, x):
+    """configs[2] on the host: oracle/deepfm.py (gather + FM + DNN, fp32) on the GPU line's own
+    65,536 Zipf(1.1) rows over the same 39 x 1e6-row tables."""
+    threads, info, rule = cpu_threads(args)
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    xc = x.cpu()
+    with torch.no_grad(), _Heartbeat("cpu_baseline deepfm"):
+        dt, n = cpu_timed(lambda: _deepfm_cpu(st, xc))
+    torch.set_num_threads(prev)
+    R = xc.shape[0]
+    return {"value": round(R / dt, 1), "unit": "rows/s", "cores": threads, "kind": "port", "threads_rule": rule,
+            "sample": (f"oracle/deepfm.py deepfm_forward (fp32 PyTorch CPU: 39 table gathers, FM, DNN 624-256-128-1) "
+                       f"on the GPU line's {R} rows (the whole batch, same ids and tables); median of {n} calls "
+                       f"after 2 warm-up calls"),
+            "seconds_per_call": round(dt, 4)}
+
+
+def cpu_baseline_retrieve_rerank(args, st, Qs=512, K=100, F=39, chunk=250_000):
+    """configs[4] on the host, one rank's worth (the whole 1M corpus): the reference arithmetic
+    scores = user @ items.T in fp32 + torch.topk(100) (v1_usertower_train.py:672-675,
+    ranker_skelet.py:193-196; items in 250k-row chunks, per-chunk top-100 merged) + the same
+    hashed rerank ids + oracle DeepFM + top-10, for the first Qs of the GPU line's 4,096 queries
+    (same seed-5 corpus and users). queries/s."""
+    threads, info, rule = cpu_threads(args)
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    I, V = args.corpus, args.deepfm_vocab
+    g = torch.Generator(device="cpu").manual_seed(5)
+    corpus = torch.nn.functional.normalize(torch.randn(I, 128, generator=g), dim=1)
+    users = torch.nn.functional.normalize(torch.randn(4096, 128, generator=g), dim=1)[:Qs].contiguous()
+    fld = torch.arange(F, dtype=torch.int64).view(1, 1, F)
+    ubucket = (torch.arange(Qs, dtype=torch.int64) % 1000).view(Qs, 1, 1)
+
+    def step():
+        bs = bi = None
+        for c0 in range(0, I, chunk):
+            sc = users @ corpus[c0:c0 + chunk].T
+            s, i = torch.topk(sc, K, dim=1)
+            i = i + c0
+            if bs is not None:
+                s, j = torch.topk(torch.cat([bs, s], 1), K, dim=1)
+                i = torch.gather(torch.cat([bi, i], 1), 1, j)
+            bs, bi = s, i
+        h = bi.unsqueeze(-1) * 0x9E3779B1 + ubucket * 0x85EBCA77 + fld * 0xC2B2AE35
+        feats = ((h ^ (h >> 29)) & 0x7FFFFFFF) % V
+        _, prob = _deepfm_cpu(st, feats.view(Qs * K, F))
+        top_p, top_j = torch.topk(prob.view(Qs, K), 10, dim=1)
+        return torch.gather(bi, 1, top_j), top_p
+
+    with torch.no_grad(), _Heartbeat("cpu_baseline retrieve->rerank"):
+        dt, n = cpu_timed(step)
+    torch.set_num_threads(prev)
+    return {"value": round(Qs / dt, 1), "unit": "queries/s", "cores": threads, "kind": "port", "threads_rule": rule,
+            "sample": (f"fp32 matmul + torch.topk({K}) over the {I}-item corpus ({chunk}-item chunks, merged) + hashed "
+                       f"rerank ids + oracle/deepfm.py on {Qs}x{K} rows + top-10, for the first {Qs} of the GPU "
+                       f"line's 4,096 queries (same corpus and users); median of {n} calls after 2 warm-up calls"),
+            "seconds_per_call": round(dt, 4)}
+
+
+def cpu_baseline_item_tower(args, gpu_model, inputs):
+    """configs[0] as BASELINE.md specifies it (its own CPU-runnable case): oracle/item_tower.py
+    OracleHybridItemTower forward (eval) on 256 items, d = 64, with the GPU line's weights (the
+    bert-base-shaped local BERT included) and inputs. items/s."""
+    import copy
+    from oracle import item_tower as OIT
+    threads, info, rule = cpu_threads(args)
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    bert = copy.deepcopy(gpu_model.bert_model).cpu()
+    ref = OIT.OracleHybridItemTower(gpu_model.std_embedding.num_embeddings, gpu_model.std_field_emb.shape[1],
+                                    gpu_model.embed_dim, gpu_model.head.final_proj.out_features, bert_model=bert)
+    ref.load_state_dict({k: v.detach().cpu() for k, v in gpu_model.state_dict().items()})
+    ref.eval()
+    xs = [t.cpu() for t in inputs]
+    with torch.no_grad(), _Heartbeat("cpu_baseline item tower"):
+        dt, n = cpu_timed(lambda: ref(*xs), warm=1, reps=3)
+    torch.set_num_threads(prev)
+    B = xs[0].shape[0]
+    return {"value": round(B / dt, 1), "unit": "items/s", "cores": threads, "kind": "port", "threads_rule": rule,
+            "sample": (f"oracle/item_tower.py OracleHybridItemTower forward (fp32 PyTorch CPU, eval) on the GPU "
+                       f"line's {B} items and weights (bert-base-shaped local BERT); median of {n} calls after 1 "
+                       f"warm-up call"),
+            "seconds_per_call": round(dt, 4)}
 
 
 def bench_deepfm(args, device):
@@ -285,7 +417,7 @@ def bench_deepfm(args, device):
         model.forward_logits(xu)
     torch.cuda.synchronize()
     out["uniform_ids_rows_per_s"] = round(R / ((time.perf_counter() - t0) / iters), 1)
-    return model, out
+    return model, out, x
 
 
 def bench_gather_1m(device, T=316_372, rows=1_000_000, iters=10, flush_mb=1024):
@@ -546,7 +678,8 @@ def bench_item_tower(args, device):
     dt = (time.perf_counter() - t0) / iters
     return {"metric": "HybridItemTower forward items/sec (256 items, d=64, bert-base-shaped local BERT)",
             "value": round(B / dt, 1), "unit": "items/s", "ms_per_batch": round(dt * 1e3, 3),
-            "data": "synthetic std/RE/text ids (SURVEY.md 8d config 1), random BERT weights"}
+            "data": "synthetic std/RE/text ids (SURVEY.md 8d config 1), random BERT weights"}, \
+        (model, [std, re_ids, re_mask, txt, txt_mask])
 
 
 def train_bench(args, global_batch, steps, warmup, items, cfg, model, item_tower, opt, bucket, rank, world,
@@ -851,13 +984,24 @@ def main():
     if rank == 0 and world == 1:
         result["secondary_gather_1m"] = bench_gather_1m(device)
         torch.cuda.empty_cache()
+    cpu_lines = rank == 0 and world == 1 and not args.no_cpu_baseline
     if rank == 0 and world == 1 and not args.no_deepfm:
         torch.cuda.empty_cache()
-        deepfm, result["secondary"] = bench_deepfm(args, device)
+        deepfm, result["secondary"], dfm_x = bench_deepfm(args, device)
         if not args.no_rerank:
             result["secondary_retrieve_rerank"] = bench_retrieve_rerank(args, device, deepfm)
             result["secondary_dcn_rerank"] = bench_dcn(args, device)
-        del deepfm
+        if cpu_lines:
+            dst = deepfm_cpu_state(deepfm)
+            line = result["secondary"]
+            line["cpu_baseline"] = cpu_baseline_deepfm(args, dst, dfm_x)
+            line["gpu_over_cpu"] = round(line["value"] / line["cpu_baseline"]["value"], 1)
+            if not args.no_rerank:
+                line = result["secondary_retrieve_rerank"]
+                line["cpu_baseline"] = cpu_baseline_retrieve_rerank(args, dst)
+                line["gpu_over_cpu"] = round(line["value"] / line["cpu_baseline"]["value"], 1)
+            del dst
+        del deepfm, dfm_x
         torch.cuda.empty_cache()
     if world > 1 and not args.no_deepfm and not args.no_rerank:
         # configs[4] on N GPUs: corpus sharded by item range, DeepFM rerank sharded by query
@@ -869,12 +1013,27 @@ def main():
         del deepfm
         torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_item_tower:
-        result["secondary_item_tower"] = bench_item_tower(args, device)
+        result["secondary_item_tower"], (it_model, it_inputs) = bench_item_tower(args, device)
+        if cpu_lines:
+            line = result["secondary_item_tower"]
+            line["cpu_baseline"] = cpu_baseline_item_tower(args, it_model, it_inputs)
+            line["gpu_over_cpu"] = round(line["value"] / line["cpu_baseline"]["value"], 1)
+        del it_model, it_inputs
         result["secondary_item_refresh"] = bench_item_refresh(args, device)
         result["secondary_hnm"] = bench_hnm(args, device)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, items, cfg, args.batch, args.seed + 100)
         result["gpu_over_cpu"] = round(result["value"] / result["cpu_baseline"]["value"], 1)
+        if "secondary_batch4096" in result:       # configs[1]: the same step at 4,096 users
+            line = result["secondary_batch4096"]
+            line["cpu_baseline"] = cpu_baseline(args, items, cfg, 4096, args.seed + 100)
+            line["gpu_over_cpu"] = round(line["value"] / line["cpu_baseline"]["value"], 1)
+        if "strong_32768" in result:
+            result["strong_32768"]["cpu_baseline"] = None
+            result["strong_32768"]["cpu_baseline_note"] = (
+                "not timed: the oracle step at 32,768 users (N ~ 600k valid steps) is ~16x the headline's "
+                "N x N loss work, i.e. ~40 min on these cores, past BASELINE.md's bounded-sample rule; the "
+                "headline and configs[1] lines carry the measured per-pair CPU rate")
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
