@@ -653,6 +653,153 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_scan_k(BfArgs a) {
   }
 }
 
+// P3 as its own kernel (the default; RSX_TOPK_COLLECT=0 selects topk_bf16_scan_k<G, 8, 1>): the
+// per-score compare-and-append of that form (a branch per score: ~3 VALU + 5 SALU for each of a
+// lane's 32 scores per tile, about twice the wave's MFMA issue time) is replaced by
+//   * a max gate: each lane takes the max of its 16 scores of a query (v_max3) and only lanes
+//     whose max reaches t_q walk their scores (one divergent branch per query group and tile);
+//   * software pipelining: the MFMAs of tile t are issued before the compares of tile t-1 (a
+//     second accumulator set), so the compares run under the matrix pipe in the wave's own
+//     instruction stream;
+//   * a clamped slot instead of a capacity branch: a stream that overflows keeps counting and its
+//     query goes to the exact kernels (P4), so what lands in its last slot is never read;
+//   * staging stores without bank conflicts: the 8 threads of an item row write its two 128-B
+//     halves as 8 contiguous 16-B pieces each (the previous 32-B-per-thread order was 2-way).
+// Same collected sets (same entries, same order within each stream) as topk_bf16_scan_k<.., 1>.
+template <int G>
+__global__ __launch_bounds__(256, 2) void topk_bf16_collect_k(BfArgs a) {
+  __shared__ __attribute__((aligned(16))) unsigned char sI[2][kTile * kImgStride];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, c = lane & 31;
+  const int b = blockIdx.x, x = b & 7, y = b >> 3;
+  const int qb = y % a.nqb;
+  const int split = (y / a.nqb) * 8 + x;
+  const int64_t q0 = (int64_t)qb * (128 * G) + wave * (32 * G) + c;
+  bf16x8 ub[G][8];
+  float thr[G];
+  int cnt[G];
+  float* bsp[G];
+  int* bip[G];
+  int64_t sbase[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int64_t q = q0 + 32 * g;
+    const bool ok = q < a.Q;
+    thr[g] = ok ? a.thr[q] : INFINITY;  // no finite score reaches +inf: rows past Q collect nothing
+    cnt[g] = 0;
+    sbase[g] = ((ok ? q : 0) * a.nsplit + split) * 2 + h;
+    bsp[g] = a.buf_s + sbase[g] * kStreamCap;
+    bip[g] = a.buf_i + sbase[g] * kStreamCap;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
+      if (ok) {
+        const float4* src = reinterpret_cast<const float4*>(a.U + q * a.ldu + 16 * ks + 8 * h);
+        v0 = src[0];
+        v1 = src[1];
+      }
+      ub[g][ks][0] = (__bf16)v0.x; ub[g][ks][1] = (__bf16)v0.y; ub[g][ks][2] = (__bf16)v0.z; ub[g][ks][3] = (__bf16)v0.w;
+      ub[g][ks][4] = (__bf16)v1.x; ub[g][ks][5] = (__bf16)v1.y; ub[g][ks][6] = (__bf16)v1.z; ub[g][ks][7] = (__bf16)v1.w;
+    }
+  }
+  const int64_t j_begin = (int64_t)split * a.span;
+  int64_t j_end = j_begin + a.span;
+  if (j_end > a.NI) j_end = a.NI;
+  const int jend = (int)j_end;
+
+  const int srow = tid >> 3, sb = (tid & 7) * 16;
+  u32x4 stg[2];
+  auto gload = [&](int64_t j0) {
+    const int64_t j = j0 + srow;
+    if (j < j_end) {
+      const unsigned char* src = reinterpret_cast<const unsigned char*>(a.img + j * kD);
+      stg[0] = *reinterpret_cast<const u32x4*>(src + sb);
+      stg[1] = *reinterpret_cast<const u32x4*>(src + 128 + sb);
+    } else {
+      stg[0] = u32x4{0u, 0u, 0u, 0u};
+      stg[1] = stg[0];
+    }
+  };
+  auto lstore = [&](int buf) {
+    unsigned char* dst = &sI[buf][srow * kImgStride];
+    *reinterpret_cast<u32x4*>(dst + sb) = stg[0];
+    *reinterpret_cast<u32x4*>(dst + 128 + sb) = stg[1];
+  };
+  auto scores = [&](int buf, f32x16 (&acc)[G]) {
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[g][r] = 0.0f;
+    const unsigned char* xrow = &sI[buf][c * kImgStride + 16 * h];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const bf16x8 av = *reinterpret_cast<const bf16x8*>(xrow + 32 * ks);
+#pragma unroll
+      for (int g = 0; g < G; ++g) acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, ub[g][ks], acc[g], 0, 0, 0);
+    }
+  };
+  auto collect = [&](const f32x16 (&acc)[G], int jt0) {
+    const bool full = jt0 + kTile <= jend;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      float m0 = fmaxf(fmaxf(acc[g][0], acc[g][1]), acc[g][2]);
+      float m1 = fmaxf(fmaxf(acc[g][3], acc[g][4]), acc[g][5]);
+      float m2 = fmaxf(fmaxf(acc[g][6], acc[g][7]), acc[g][8]);
+      float m3 = fmaxf(fmaxf(acc[g][9], acc[g][10]), acc[g][11]);
+      float m4 = fmaxf(fmaxf(acc[g][12], acc[g][13]), acc[g][14]);
+      const float mx = fmaxf(fmaxf(fmaxf(m0, m1), fmaxf(m2, m3)), fmaxf(m4, acc[g][15]));
+      if (mx >= thr[g]) {  // rare per lane: this lane's query has a collected item in the tile
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int j = jt0 + tile_row(r, h);
+          const float sc = acc[g][r];
+          if (sc >= thr[g] && (full || j < jend)) {
+            const int slot = cnt[g] < kStreamCap ? cnt[g] : kStreamCap - 1;
+            bsp[g][slot] = sc;
+            bip[g][slot] = j;
+            ++cnt[g];
+          }
+        }
+      }
+    }
+  };
+  if (j_begin < j_end) {
+    gload(j_begin);
+    lstore(0);
+    __syncthreads();
+    f32x16 accA[G], accB[G];
+    int cur = 0;
+    int64_t j0 = j_begin;
+    // one tile per step: MFMAs of tile j0 into `fresh`, then the compares of the previous tile
+    // (`old`, if any) under them; the two accumulator sets swap roles every step
+    auto step = [&](f32x16 (&fresh)[G], const f32x16 (&old)[G], bool has_old) -> bool {
+      const bool has_next = j0 + kTile < j_end;
+      if (has_next) gload(j0 + kTile);
+      scores(cur, fresh);
+      if (has_old) collect(old, (int)(j0 - kTile));
+      if (has_next) lstore(cur ^ 1);  // cur^1 was read in the previous step, fenced by its barrier
+      __syncthreads();
+      cur ^= 1;
+      j0 += kTile;
+      return has_next;
+    };
+    bool more = step(accA, accB, false);
+    bool last_in_a = true;
+    while (more) {
+      more = step(accB, accA, true);
+      last_in_a = false;
+      if (!more) break;
+      more = step(accA, accB, true);
+      last_in_a = true;
+    }
+    if (last_in_a) collect(accA, (int)(j0 - kTile));
+    else collect(accB, (int)(j0 - kTile));
+  }
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+    if (q0 + 32 * g < a.Q) a.buf_n[sbase[g]] = cnt[g];
+}
+
 // bitonic sort of the first P (power of two) entries, (score desc, idx asc)
 __device__ __forceinline__ void bitonic_desc_n(float* ss, int* si, int P) {
   for (int size = 2; size <= P; size <<= 1) {
@@ -1167,8 +1314,17 @@ int run_bf16_chunk(const BfPlan& bp, const BfLayout& L, const float* U, int64_t 
     hipLaunchKernelGGL(topk_bf16_thresh_k<4096>, dim3((unsigned)Q), dim3(256), 0, st, b.cand_s, b.cand_i, ncand, U,
                        ldu, (int)k, wmax, thr);
   RSX_LAUNCHED();
-  if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_scan_k<2, 8, 1>), grid, dim3(256), 0, st, b);
-  else hipLaunchKernelGGL((topk_bf16_scan_k<1, 8, 1>), grid, dim3(256), 0, st, b);
+  static const bool collect_k = [] {
+    const char* e = getenv("RSX_TOPK_COLLECT");
+    return !(e && e[0] == '0');
+  }();
+  if (collect_k) {
+    if (bp.G == 2) hipLaunchKernelGGL(topk_bf16_collect_k<2>, grid, dim3(256), 0, st, b);
+    else hipLaunchKernelGGL(topk_bf16_collect_k<1>, grid, dim3(256), 0, st, b);
+  } else {
+    if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_scan_k<2, 8, 1>), grid, dim3(256), 0, st, b);
+    else hipLaunchKernelGGL((topk_bf16_scan_k<1, 8, 1>), grid, dim3(256), 0, st, b);
+  }
   RSX_LAUNCHED();
   hipLaunchKernelGGL(topk_bf16_select_k, dim3((unsigned)Q), dim3(256), 0, st, b.buf_s, b.buf_i, b.buf_n,
                      bp.nsplit * 2, U, ldu, I, ldi, (int)k, wmax, out_scores, out_idx, qcount, qmap, qtotal);
