@@ -273,6 +273,38 @@ int rsx_gemm_x3_addln(const float* A, int64_t lda, const float* B, int64_t ldb, 
  * utils/vocab.py:436-441): the caller raises when the flag reaches the host. */
 int rsx_ids_check(const int64_t* ids, int64_t n, int64_t lo, int64_t hi, int64_t* out, int* flag, void* stream);
 
+/* ---- A8: the step index on the device ----------------------------------------------------
+ * Every data-dependent structure of one contrastive step (train_user_tower_all_time's per-batch
+ * flattening, v1_usertower_train.py:794-835, plus the grouped loss's target index) from the
+ * batch's [B, L] tensors, with ONE host read (the totals). pm: padding_mask as bytes (1 = pad),
+ * tgt / item: target_ids / item_ids int64 [B, L], ids in [0, n_items); L <= 64.
+ *   1. rsx_step_index_count   -> tloc [B*L + 1] int32: this rank's loss-row targets (flat
+ *      order, -1 padded) and its row count in the last slot
+ *   2. (world > 1) the caller all-gathers tloc blocks rank-major into tglob [world][B*L + 1]
+ *   3. rsx_step_index_totals  -> totals [8 + world] int64 on the device: T (packed tokens per
+ *      view), N (loss rows), D (distinct target columns over tglob), E (distinct (user, target)
+ *      pairs), U (distinct item ids among the tokens), C (segment-sum chunks), error flag (ids
+ *      out of range), 0, then every rank's row count
+ *   4. rsx_step_index_fill(sizes = totals[0..5] read on the host) writes out[0..32]:
+ *      0 flat [T] i64, 1 tok_user [T] i64, 2 tok_pos [T] i64, 3 tok_pad [T] u8, 4 seg_off [B+1] i32,
+ *      5 seg_off [B+1] i64, 6 valid_tok [N] i64, 7 last_tok [B] i64; the doubled two-view batch:
+ *      8 flat [2T], 9 tok_user [2T], 10 tok_pos [2T] i64, 11 tok_pad [2T] u8, 12 seg_off [2B+1]
+ *      i32, 13 seg_off [2B+1] i64, 14 tok_ids [6][2T] i64 (seq_ids per token, both views),
+ *      15 pretrained rows [2T][128] f32 (nullable; from lookup [n_items][ld_lookup]); the
+ *      item-id segment-sum plan: 16 perm [2T], 17 cb [C+1], 18 chunk ids [C], 19 ch_off [U+1],
+ *      20 ids [U] (all i64); the grouped-loss index: 21 uniq [D] i64, 22 colcnt [D] f32,
+ *      23 row_col, 24 row_beg, 25 row_end, 26 exc_cols [N] i32, 27 exc_s, 28 exc_e, 29 exc_n [E]
+ *      i32, 30 col_beg, 31 col_end [D] i32; 32 last_t [B] i64 (DuoRec targets).
+ * ws: rsx_step_index_workspace_bytes(B, L, n_items), the same buffer for all three calls. */
+int64_t rsx_step_index_workspace_bytes(int64_t B, int64_t L, int64_t n_items);
+int rsx_step_index_count(const uint8_t* pm, const int64_t* tgt, const int64_t* item, int64_t B, int64_t L,
+                         int64_t n_items, void* ws, int64_t ws_bytes, int* tloc, void* stream);
+int rsx_step_index_totals(const int* tglob, int world, int64_t B, int64_t L, int64_t n_items, void* ws,
+                          int64_t ws_bytes, int64_t* totals, void* stream);
+int rsx_step_index_fill(const uint8_t* pm, const int64_t* tgt, const int64_t* const* seq_ids, const float* lookup,
+                        int64_t ld_lookup, int64_t B, int64_t L, int64_t n_items, const int64_t* sizes, void* ws,
+                        int64_t ws_bytes, void* const* out, void* stream);
+
 /* ---- A14: retrieval top-k ------------------------------------------------------------
  * scores = U I^T (fp32 MFMA, never materialised), per query the k best items sorted by
  * (score desc, index asc). Replaces `scores = matmul(user, items.T); topk(k)` at

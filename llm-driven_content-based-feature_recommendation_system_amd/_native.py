@@ -90,6 +90,10 @@ _SIGS = {
     "rsx_retrieve_topk": (c_i, [c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p]),
     "rsx_topk_path": (c_i, [c_i64, c_i64, c_i64]),
     "rsx_ids_check": (c_i, [c_p, c_i64, c_i64, c_i64, c_p, c_p, c_p]),
+    "rsx_step_index_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64]),
+    "rsx_step_index_count": (c_i, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_p]),
+    "rsx_step_index_totals": (c_i, [c_p, c_i, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_p]),
+    "rsx_step_index_fill": (c_i, [c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_i64, c_p, c_p]),
     "rsx_topk_corpus_bytes": (c_i64, [c_i64]),
     "rsx_topk_prepare_corpus": (c_i, [c_p, c_i64, c_i64, c_p, c_p]),
     "rsx_topk_workspace_bytes_corpus": (c_i64, [c_i64, c_i64, c_i64]),

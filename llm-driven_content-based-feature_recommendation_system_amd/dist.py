@@ -23,10 +23,12 @@ the HIP kernels through ops.
 from __future__ import annotations
 
 import contextlib
+import os
 
 import torch
 import torch.distributed as dist
 
+from . import _native as N
 from . import ops
 
 
@@ -295,11 +297,107 @@ class StepIndex:
     counts, the main loss's grouped-target index and the DuoRec keys."""
 
 
-def prepare_step_index(batch, pretrained_vecs=None, pretrained_lookup=None) -> StepIndex:
-    """Builds the StepIndex of `batch` on the current stream. Its size queries (nonzero /
-    unique / the count all-gather) synchronise the host with that stream."""
+class _Packed:
+    """PackedTokens' attributes for the device-built index (tower_code.v1_refine_usertower)."""
+
+    def take(self, t: torch.Tensor) -> torch.Tensor:
+        return t.reshape((-1,) + tuple(t.shape[2:]))[self.flat]
+
+
+# RSX_DEVICE_INDEX=0: the torch builders (PackedTokens / pack_inputs / sort_segments /
+# TargetGroups, ~12 host size queries per batch) instead of rsx_step_index_* (one host read)
+_DEVICE_INDEX = os.environ.get("RSX_DEVICE_INDEX", "1") != "0"
+
+
+def _prepare_step_index_device(batch, pretrained_vecs, pretrained_lookup, n_items) -> StepIndex:
+    """prepare_step_index on rsx_step_index_* (csrc/step_index.hip): the same arrays in the same
+    orders as the torch builders, with ONE host read (the totals) per batch; at world > 1 the
+    ranks exchange fixed-size [B*L + 1] target blocks, so no size is needed before the exchange."""
+    from .tower_code.v1_usertower_train import _SEQ_ID_KEYS, _STATIC_KEYS
+
+    lib = N.lib()
+    rank, ws = world()
+    pm = batch["padding_mask"]
+    B, L = pm.shape
+    dev = pm.device
+    pm8 = ops._c(pm).view(torch.uint8) if pm.dtype == torch.bool else ops._c(pm.to(torch.uint8))
+    tgt = ops._c(batch["target_ids"].to(torch.int64))
+    seq = [ops._c(batch[k].to(torch.int64)) for k in _SEQ_ID_KEYS]
+    nb = lib.rsx_step_index_workspace_bytes(B, L, n_items)
+    wsb = torch.empty(nb, device=dev, dtype=torch.uint8)
+    tloc = torch.empty(B * L + 1, device=dev, dtype=torch.int32)
+    N.check(lib.rsx_step_index_count(N.ptr(pm8), N.ptr(tgt), N.ptr(seq[0]), B, L, n_items, N.ptr(wsb), nb,
+                                     N.ptr(tloc), N.stream()), "step_index_count")
+    if ws > 1:
+        tglob = torch.empty(ws, B * L + 1, device=dev, dtype=torch.int32)
+        all_gather_into(list(tglob.unbind(0)), tloc, group=index_group())
+    else:
+        tglob = tloc
+    totals = torch.empty(8 + ws, device=dev, dtype=torch.int64)
+    N.check(lib.rsx_step_index_totals(N.ptr(tglob), ws, B, L, n_items, N.ptr(wsb), nb, N.ptr(totals), N.stream()),
+            "step_index_totals")
+    tot = totals.tolist()  # the one host read
+    T, Nr, D, E, U, C, err = tot[:7]
+    if err:
+        raise IndexError(f"step index: a target / item id outside [0, {n_items})")
+    i64 = dict(device=dev, dtype=torch.int64)
+    i32 = dict(device=dev, dtype=torch.int32)
+    u8 = dict(device=dev, dtype=torch.uint8)
+    out = [torch.empty(T, **i64), torch.empty(T, **i64), torch.empty(T, **i64), torch.empty(T, **u8),
+           torch.empty(B + 1, **i32), torch.empty(B + 1, **i64), torch.empty(Nr, **i64), torch.empty(B, **i64),
+           torch.empty(2 * T, **i64), torch.empty(2 * T, **i64), torch.empty(2 * T, **i64), torch.empty(2 * T, **u8),
+           torch.empty(2 * B + 1, **i32), torch.empty(2 * B + 1, **i64), torch.empty(6, 2 * T, **i64),
+           (torch.empty(2 * T, 128, device=dev, dtype=torch.float32) if pretrained_vecs is None else None),
+           torch.empty(2 * T, **i64), torch.empty(C + 1, **i64), torch.empty(C, **i64), torch.empty(U + 1, **i64),
+           torch.empty(U, **i64),
+           torch.empty(D, **i64), torch.empty(D, device=dev, dtype=torch.float32), torch.empty(Nr, **i32),
+           torch.empty(Nr, **i32), torch.empty(Nr, **i32), torch.empty(Nr, **i32), torch.empty(E, **i32),
+           torch.empty(E, **i32), torch.empty(E, **i32), torch.empty(D, **i32), torch.empty(D, **i32),
+           torch.empty(B, **i64)]
+    lk = ops._c(pretrained_lookup) if pretrained_vecs is None else None
+    N.check(lib.rsx_step_index_fill(N.ptr(pm8), N.ptr(tgt), N.ptr_array(seq), N.ptr(lk),
+                                    lk.stride(0) if lk is not None else 0, B, L, n_items,
+                                    N.i64_array([T, Nr, D, E, U, C]), N.ptr(wsb), nb, N.ptr_array(out), N.stream()),
+            "step_index_fill")
+    pk, pk2 = _Packed(), _Packed()
+    pk.flat, pk.tok_user, pk.tok_pos, pk.tok_pad, pk.seg_off, pk.seg_off64, pk.valid_tok, pk.last_tok = out[:8]
+    pk.B, pk.L = B, L
+    (pk2.flat, pk2.tok_user, pk2.tok_pos, pk2.tok_pad, pk2.seg_off, pk2.seg_off64) = out[8:14]
+    pk2.B, pk2.L = 2 * B, L
+    pk2.item_seg = tuple(out[16:21])
+    tok_ids = list(out[14].unbind(0))
+    if pretrained_vecs is None:
+        pv_tok = out[15]
+    else:
+        pv_tok = pk.take(pretrained_vecs)
+        pv_tok = torch.cat([pv_tok, pv_tok])
+    static = [torch.cat([batch[k], batch[k]]) for k in _STATIC_KEYS]
+    ix = StepIndex()
+    ix.packed = (pk, pk2, tok_ids, pv_tok, static)
+    ix.B = B
+    ix.counts = [int(c) for c in tot[8:8 + ws]]
+    ix.n_glob = sum(ix.counts)
+    ix.groups = None
+    if ix.n_glob > 0:
+        ix.groups = ops.TargetGroups.from_arrays(*out[21:32], n_rows=Nr)
+    ix.last_t = out[32]
+    ix.t_glob_last = all_gather_var(ix.last_t, [B] * ws, group=index_group() if ws > 1 else None)
+    ix.wsb = wsb  # keeps the workspace alive with the index (stream-ordered reuse)
+    return ix
+
+
+def prepare_step_index(batch, pretrained_vecs=None, pretrained_lookup=None, n_items=None) -> StepIndex:
+    """Builds the StepIndex of `batch` on the current stream. Device batches (L <= 64) use
+    rsx_step_index_* (one host read: the totals); otherwise, or with RSX_DEVICE_INDEX=0, the torch
+    builders, whose size queries (nonzero / unique / the count all-gather) each synchronise the
+    host with that stream. n_items: the id domain (default: the pretrained lookup's rows)."""
     from .tower_code.v1_usertower_train import pack_inputs
 
+    if n_items is None and pretrained_lookup is not None:
+        n_items = pretrained_lookup.shape[0]
+    if (_DEVICE_INDEX and n_items is not None and batch["item_ids"].is_cuda
+            and batch["padding_mask"].shape[1] <= 64):
+        return _prepare_step_index_device(batch, pretrained_vecs, pretrained_lookup, int(n_items))
     rank, ws = world()
     device = batch["item_ids"].device
     B = batch["item_ids"].shape[0]

@@ -588,6 +588,16 @@ class TargetGroups:
         self.n_rows = n
         self.n_cols = D
 
+    @classmethod
+    def from_arrays(cls, uniq, colcnt, row_col, row_beg, row_end, exc_cols, exc_s, exc_e, exc_n, col_beg, col_end,
+                    n_rows):
+        """The same structure from prepared arrays (rsx_step_index_fill, dist.py)."""
+        g = cls.__new__(cls)
+        g.uniq, g.colcnt, g.row_col, g.row_beg, g.row_end, g.exc_cols = uniq, colcnt, row_col, row_beg, row_end, exc_cols
+        g.exc_s, g.exc_e, g.exc_n, g.col_beg, g.col_end = exc_s, exc_e, exc_n, col_beg, col_end
+        g.n_rows, g.n_cols = int(n_rows), uniq.numel()
+        return g
+
 
 # bf16x3 + the rows need a gradient: the forward also produces the row gradient (one sweep of
 # S instead of two; rsx_nce_grouped_fwd_grad). RSX_NCE_FUSED_ROWGRAD=0 restores the separate
