@@ -653,7 +653,8 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_scan_k(BfArgs a) {
   }
 }
 
-// P3 as its own kernel (the default; RSX_TOPK_COLLECT=0 selects topk_bf16_scan_k<G, 8, 1>): the
+// P3 as its own kernel (opt-in, RSX_TOPK_COLLECT=1 / 2; measured slower than topk_bf16_scan_k<G,
+// 8, 1> in round 4: 2.51 vs 2.22 ms per 4096 x 1M call): the
 // per-score compare-and-append of that form (a branch per score: ~3 VALU + 5 SALU for each of a
 // lane's 32 scores per tile, about twice the wave's MFMA issue time) is replaced by
 //   * a max gate: each lane takes the max of its 16 scores of a query (v_max3) and only lanes
@@ -666,7 +667,7 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_scan_k(BfArgs a) {
 //   * staging stores without bank conflicts: the 8 threads of an item row write its two 128-B
 //     halves as 8 contiguous 16-B pieces each (the previous 32-B-per-thread order was 2-way).
 // Same collected sets (same entries, same order within each stream) as topk_bf16_scan_k<.., 1>.
-template <int G>
+template <int G, bool PIPE>
 __global__ __launch_bounds__(256, 2) void topk_bf16_collect_k(BfArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned char sI[2][kTile * kImgStride];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -763,7 +764,22 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_collect_k(BfArgs a) {
       }
     }
   };
-  if (j_begin < j_end) {
+  if (j_begin < j_end && !PIPE) {  // gate only: compares right after each tile's MFMAs
+    gload(j_begin);
+    lstore(0);
+    __syncthreads();
+    int cur = 0;
+    for (int64_t j0 = j_begin; j0 < j_end; j0 += kTile) {
+      const bool has_next = j0 + kTile < j_end;
+      if (has_next) gload(j0 + kTile);
+      f32x16 acc[G];
+      scores(cur, acc);
+      collect(acc, (int)j0);
+      if (has_next) lstore(cur ^ 1);
+      __syncthreads();
+      cur ^= 1;
+    }
+  } else if (j_begin < j_end) {
     gload(j_begin);
     lstore(0);
     __syncthreads();
@@ -1314,13 +1330,18 @@ int run_bf16_chunk(const BfPlan& bp, const BfLayout& L, const float* U, int64_t 
     hipLaunchKernelGGL(topk_bf16_thresh_k<4096>, dim3((unsigned)Q), dim3(256), 0, st, b.cand_s, b.cand_i, ncand, U,
                        ldu, (int)k, wmax, thr);
   RSX_LAUNCHED();
-  static const bool collect_k = [] {
+  // RSX_TOPK_COLLECT: 0 (default) topk_bf16_scan_k<G, 8, 1>; 1 topk_bf16_collect_k pipelined;
+  // 2 topk_bf16_collect_k gate only (A/B measurements)
+  static const int collect_k = [] {
     const char* e = getenv("RSX_TOPK_COLLECT");
-    return !(e && e[0] == '0');
+    return e ? atoi(e) : 0;
   }();
-  if (collect_k) {
-    if (bp.G == 2) hipLaunchKernelGGL(topk_bf16_collect_k<2>, grid, dim3(256), 0, st, b);
-    else hipLaunchKernelGGL(topk_bf16_collect_k<1>, grid, dim3(256), 0, st, b);
+  if (collect_k == 1) {
+    if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_collect_k<2, true>), grid, dim3(256), 0, st, b);
+    else hipLaunchKernelGGL((topk_bf16_collect_k<1, true>), grid, dim3(256), 0, st, b);
+  } else if (collect_k == 2) {
+    if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_collect_k<2, false>), grid, dim3(256), 0, st, b);
+    else hipLaunchKernelGGL((topk_bf16_collect_k<1, false>), grid, dim3(256), 0, st, b);
   } else {
     if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_scan_k<2, 8, 1>), grid, dim3(256), 0, st, b);
     else hipLaunchKernelGGL((topk_bf16_scan_k<1, 8, 1>), grid, dim3(256), 0, st, b);

@@ -52,14 +52,28 @@ def main():
         s, c = ops.nce_grouped_sum(U, B, bias, grp, tau=0.1, tag="micro", precision=args.precision)
         s.backward()
     torch.cuda.synchronize()
+    import ctypes
+    from recsys_amd import _native as N
+    U.grad = None
+    B.grad = None
     ops.timing_start()
+    N.lib().rsx_kernel_events(1)
     for i in range(args.iters):
         s, c = ops.nce_grouped_sum(U, B, bias, grp, tau=0.1, tag="micro", precision=args.precision)
         s.backward()
     torch.cuda.synchronize()
     kt = ops.timing_stop()
+    kev = (ctypes.c_float * 256)()
+    nk = N.lib().rsx_kernel_events_read(kev, 256)
+    N.lib().rsx_kernel_events(0)
+    kms = [float(kev[i]) for i in range(max(nk, 0))]
+    flops = 4.0 * n * int(grp.uniq.numel()) * 128
     out = {"rows": n, "distinct_targets": int(grp.uniq.numel()), "precision": args.precision,
-           "loss_sum": float(s.item()),
+           "env_fwdg": os.environ.get("RSX_NCE_FWDG", ""), "loss_sum": float(s.item()),
+           "grad_u_abs_sum": float(U.grad.abs().sum().item()) / args.iters,
+           "grad_b_abs_sum": float(B.grad.abs().sum().item()) / args.iters,
+           "fwd_kernel_ms": round(sum(kms) / len(kms), 4) if kms else None,
+           "fwd_kernel_frac_bf16x3": (round(flops / (sum(kms) / len(kms) / 1e3) / 838.9e12, 4) if kms else None),
            "avg_ms": {k: round(ms / max(cnt, 1), 4) for k, (cnt, ms) in sorted(kt.items())}}
     print(json.dumps(out), flush=True)
 
