@@ -2457,378 +2457,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void nce_grouped_fwdg_x3p_k(GArgs 
   }
 }
 
-// Ping-pong form of the fused forward (RSX_NCE_FWDG=pp). 8 waves, one 256-row owner block per
-// CU: group A (waves 0-3, rows 0-127) and group B (waves 4-7, rows 128-255), one wave of each
-// per SIMD. Every tile step has two phases separated by workgroup barriers; in each phase one
-// group runs its matrix block and the other its VALU block, so each SIMD's matrix pipe always
-// has a wave feeding it (the lockstep 8-wave form ran both waves of a SIMD in the same phase;
-// the two-workgroup form pairs waves of unrelated phases):
-//   matrix block (tile k): gacc += G(k-1)^T X(k-1) (24 MFMA), S(k) = U X(k)^T (24 MFMA)
-//   VALU block  (tile k): logits, exceptions, tile max / lazy rescale, G(k) = 2^(x - m) split to
-//                         hi/lo, the running sum; the group's half of the staging (A: hi image +
-//                         column metadata, B: lo image) of tile k+1 stored, tile k+2 loaded
-//   phase 1: A matrix(k),  B VALU(k-1)      phase 2: A VALU(k),  B matrix(k)
-// Ring of 3 tiles (k-1 read by the gradients, k by S, k+1 being stored). Same arithmetic per
-// element as nce_grouped_fwdg_x3_k (same exp / split / lazy max), so the same partials up to the
-// fixed summation order; the merge is unchanged.
-__global__ __launch_bounds__(512, 1) void nce_grouped_fwdg_pp_k(GArgs a) {
-  constexpr int kRows = 256;
-  __shared__ __attribute__((aligned(16))) X3Tile sT[3];
-  __shared__ __attribute__((aligned(16))) float sB2[3][kTile];
-  __shared__ __attribute__((aligned(16))) float sCnt[3][kTile];
-  __shared__ __attribute__((aligned(16))) float sAlpha[8][32];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int h = lane >> 5, c = lane & 31;
-  const int grp = wave >> 2;  // 0 = A, 1 = B (wave-uniform)
-  int split;
-  int64_t rb, j_begin, j_end;
-  fwdg_geometry(a, split, rb, j_begin, j_end);
-  const int64_t i = rb * kRows + wave * 32 + c;
-  const bool row_ok = i < a.N;
-  bf16x8 uh[8], ul[8];
-  load_owner_x3(uh, ul, a.A, i, a.lda, row_ok, h);
-  constexpr int kNone = 0x7fffffff;
-  int di = -1, p = 0, e = 0, next = kNone;
-  if (row_ok) {
-    di = a.row_col[i];
-    p = a.row_beg[i];
-    e = a.row_end[i];
-    p = lower_bound_i(a.exc_cols, p, e, j_begin);
-    next = (p < e) ? a.exc_cols[p] : kNone;
-  }
-  const float it2 = a.inv_tau * kLog2e;
-  float m = -INFINITY, l = 0.0f;
-  f32x16 gacc[4];
-#pragma unroll
-  for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) gacc[kb][r] = 0.0f;
-  X3StageT<8> stg;  // thread tid: image tid >> 8 (= its group), row (tid >> 3) & 31
-  float stg_b = 0.0f, stg_c = 0.0f;
-  auto gload = [&](int64_t j0) {
-    const int64_t j = j0 + ((tid >> 3) & 31);
-    stg.load(a.bhi, a.blo, j, j < j_end, tid);
-    if (tid < kTile) {
-      const int64_t jj = j0 + tid;
-      const bool ok = jj < j_end;
-      stg_b = ok ? (a.bias ? a.bias[jj] : 0.0f) : INFINITY;
-      stg_c = ok ? a.colcnt[jj] : 0.0f;
-    }
-  };
-  auto lstore = [&](int buf) {
-    stg.store(sT[buf], tid);
-    if (tid < kTile) {
-      sB2[buf][tid] = -(stg_b * kLog2e) + __log2f(stg_c);
-      sCnt[buf][tid] = stg_c;
-    }
-  };
-  const int64_t ntile = (j_end - j_begin + kTile - 1) / kTile;
-  if (ntile > 0) {
-    gload(j_begin);
-    lstore(0);  // both images of tile 0
-    if (ntile > 1) {
-      gload(j_begin + kTile);
-      if (grp == 1) lstore(1);  // B's lo of tile 1 (A keeps hi of tile 1 for its first VALU block)
-    }
-    if (grp == 1 && ntile > 2) gload(j_begin + 2 * kTile);
-    __syncthreads();
-    f32x16 acc;
-    bf16x8 gh[2], gl[2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        gh[s][k] = (__bf16)0.0f;
-        gl[s][k] = (__bf16)0.0f;
-      }
-    // matrix block of tile k: the gradient of tile k-1 (zero fragments at k = 0 add exactly 0),
-    // then S of tile k (none past the last tile)
-    auto matrix = [&](int64_t k) {
-      if (k > 0) grad_x3s(gacc, gh, gl, sT[(k - 1) % 3], lane);
-      if (k < ntile) acc = dots_x3(sT[k % 3], c, h, uh, ul);
-    };
-    // VALU block of tile k (k < ntile): G(k) and the staging of tiles k+1 (store) / k+2 (load)
-    auto valu = [&](int64_t k) {
-      const int cur = (int)(k % 3);
-      const int64_t j0 = j_begin + k * kTile;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 nb = *reinterpret_cast<const float4*>(&sB2[cur][8 * g + 4 * h]);
-        acc[4 * g + 0] = fmaf(acc[4 * g + 0], it2, nb.x);
-        acc[4 * g + 1] = fmaf(acc[4 * g + 1], it2, nb.y);
-        acc[4 * g + 2] = fmaf(acc[4 * g + 2], it2, nb.z);
-        acc[4 * g + 3] = fmaf(acc[4 * g + 3], it2, nb.w);
-      }
-      if ((int64_t)next < j0 + kTile) {  // the row's own targets (loads before this phase's prefetch)
-        int q = p;
-        while (q < e && (int64_t)a.exc_cols[q] < j0 + kTile) ++q;
-        float n[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) n[r] = 0.0f;
-        for (int kk = p; kk < q; ++kk) {
-          const int tk = (int)(a.exc_cols[kk] - j0);
-#pragma unroll
-          for (int r = 0; r < 16; ++r) n[r] += (tk == tile_row(r, h)) ? 1.0f : 0.0f;
-        }
-        const int tl = ((int64_t)di < j_end) ? (int)(di - j0) : -1;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const float4 cw = *reinterpret_cast<const float4*>(&sCnt[cur][8 * g + 4 * h]);
-          const float cv[4] = {cw.x, cw.y, cw.z, cw.w};
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const int r = 4 * g + t;
-            const float wn = (tile_row(r, h) == tl) ? 1.0f : cv[t] - n[r];
-            if (wn != cv[t]) acc[r] = (wn > 0.0f) ? acc[r] + __log2f(wn / cv[t]) : -INFINITY;
-          }
-        }
-        p = q;
-        next = (p < e) ? a.exc_cols[p] : kNone;
-      }
-      float tmax = -INFINITY;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, acc[r]);
-      {
-        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(tmax), __float_as_uint(tmax), false, false);
-        tmax = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
-      }
-      if (!row_ok) tmax = -INFINITY;
-      const bool raise = tmax > m + kLazyLog2;
-      if (__any(raise)) {  // gacc holds the tiles before k: rescale the raised owners' rows
-        const float alpha = raise ? ((m == -INFINITY) ? 0.0f : __builtin_amdgcn_exp2f(m - tmax)) : 1.0f;
-        if (raise) {
-          l *= alpha;
-          m = tmax;
-        }
-        if (h == 0) sAlpha[wave][c] = alpha;
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float al = sAlpha[wave][tile_row(r, h)];
-#pragma unroll
-          for (int kb = 0; kb < 4; ++kb) gacc[kb][r] *= al;
-        }
-        __builtin_amdgcn_wave_barrier();
-      }
-      const float ms = (m == -INFINITY) ? 0.0f : m;
-      float ls;
-      exp_split_tile(acc, ms, gh, gl, ls);
-      l += ls;
-      // staging of this group's image (loaded one tile step ago): A stores hi (+ metadata) of
-      // tile k+1 in phase 2 of step k, B stores lo of tile k+2 in phase 1 of step k+1 -- each into
-      // the slot of tile k-2, which no wave reads after step k-1 (and never into a tile the other
-      // group's matrix block reads in the same phase)
-      const int64_t ahead = grp == 0 ? 1 : 2;
-      if (k + ahead < ntile) lstore((int)((k + ahead) % 3));
-      if (k + ahead + 1 < ntile) gload(j_begin + (k + ahead + 1) * kTile);
-    };
-    // half-steps: phase 1 of step k = A matrix(k) | B valu(k-1); phase 2 = A valu(k) | B matrix(k)
-    // (one call site per block, so each is compiled once)
-    for (int64_t hs = 0; hs < 2 * (ntile + 1); ++hs) {
-      const int64_t k = hs >> 1;
-      const bool ph2 = (hs & 1) != 0;
-      if ((grp == 0) != ph2) {
-        __builtin_amdgcn_s_setprio(1);
-        matrix(k);
-        __builtin_amdgcn_s_setprio(0);
-      } else {
-        const int64_t kv = grp == 0 ? k : k - 1;
-        if (kv >= 0 && kv < ntile) valu(kv);
-      }
-      __syncthreads();
-    }
-  }
-  const float lt = l + __shfl_xor(l, 32, 64);
-  if (h == 0 && row_ok) {
-    const int64_t stride = (int64_t)a.nslots * a.N;
-    const int64_t o = (int64_t)split * a.N + i;
-    a.part[o] = (m == -INFINITY) ? -INFINITY : m * kLn2;
-    a.part[stride + o] = lt;
-    a.part[2 * stride + o] = 0.0f;
-    a.part[3 * stride + o] = 0.0f;
-  }
-  const int64_t own_base = rb * kRows + wave * 32;
-  float* dst = a.dout + (int64_t)split * a.N * kD;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int64_t orow = own_base + tile_row(r, h);
-    if (orow < a.N) {
-#pragma unroll
-      for (int kb = 0; kb < 4; ++kb) dst[orow * kD + kb * 32 + c] = gacc[kb][r];
-    }
-  }
-}
-
-// Ping-pong form of the column pass (RSX_NCE_BWD=pp; see nce_grouped_fwdg_pp_k): 8 waves, 256
-// owner columns per workgroup in two groups (A: waves 0-3, B: waves 4-7, one of each per SIMD);
-// matrix block of tile k = gacc += G(k-1)^T X(k-1) then S(k); VALU block = G(k) (exceptions
-// included) and the staging; phase 1: A matrix(k), B VALU(k-1); phase 2: A VALU(k), B matrix(k).
-// Split-major XCD order over 256-column owner blocks, as the 128-column kernel.
-__global__ __launch_bounds__(512, 1) void nce_grouped_colpp_k(GArgs a) {
-  constexpr int kOwn = 256;
-  __shared__ __attribute__((aligned(16))) X3Tile sT[3];
-  __shared__ __attribute__((aligned(16))) float sM0[3][kTile];  // lse_i*log2e (+inf past the split)
-  __shared__ __attribute__((aligned(16))) int sM2[3][kTile];    // d(i)
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int h = lane >> 5, c = lane & 31;
-  const int grp = wave >> 2;
-  const int64_t n_own = a.M, n_str = a.N;
-  const int b = blockIdx.x, xcd = b & 7, qq = b >> 3;
-  const int nob = (int)((n_own + kOwn - 1) / kOwn);
-  const int split = xcd + 8 * (qq / nob);
-  const int ob = qq % nob;
-  const float gs = a.gout[0] * a.inv_tau;
-  const float it2 = a.inv_tau * kLog2e;
-  const int64_t o = (int64_t)ob * kOwn + wave * 32 + c;
-  const bool own_ok = o < n_own;
-  bf16x8 uh[8], ul[8];
-  load_owner_x3(uh, ul, a.B, o, a.ldb, own_ok, h);
-  const int64_t s_begin = (int64_t)split * a.span;
-  int64_t s_end = s_begin + a.span;
-  if (s_end > n_str) s_end = n_str;
-  constexpr int kNone = 0x7fffffff;
-  float o_m2 = 0.0f, o_cnt = 0.0f;
-  int p = 0, e = 0;
-  if (own_ok) {
-    o_m2 = a.bias ? a.bias[o] * kLog2e : 0.0f;
-    o_cnt = a.colcnt[o];
-    p = a.col_beg[o];
-    e = a.col_end[o];
-    p = lower_bound_i(a.exc_e, p, e, s_begin + 1);
-  }
-  const float gso = own_ok ? gs : 0.0f;
-  const float fo = gso * o_cnt;
-  int q = p, e_first = 0, s_next = kNone;
-  if (own_ok && q < e) s_next = a.exc_s[q];
-  f32x16 gacc[4];
-#pragma unroll
-  for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) gacc[kb][r] = 0.0f;
-  X3StageT<8> stg;
-  float stg0 = 0.0f;
-  int stg2 = 0;
-  auto gload = [&](int64_t s0) {
-    const int64_t sidx = s0 + ((tid >> 3) & 31);
-    stg.load(a.ahi, a.alo, sidx, sidx < s_end, tid);
-    if (tid < kTile) {
-      const int64_t ss = s0 + tid;
-      const bool ok = ss < s_end;
-      stg0 = ok ? a.lse[ss] : INFINITY;
-      stg2 = ok ? a.row_col[ss] : -2;
-    }
-  };
-  auto lstore = [&](int buf) {
-    stg.store(sT[buf], tid);
-    if (tid < kTile) {
-      sM0[buf][tid] = stg0 * kLog2e;
-      sM2[buf][tid] = stg2;
-    }
-  };
-  auto exc_flag = [&](int64_t s0) -> bool {
-    while (p < q && (int64_t)e_first <= s0) {
-      ++p;
-      if (p < q) e_first = a.exc_e[p];
-    }
-    while ((int64_t)s_next < s0 + kTile) {
-      if (p == q) e_first = a.exc_e[q];
-      ++q;
-      s_next = (q < e) ? a.exc_s[q] : kNone;
-    }
-    return q != p;
-  };
-  const int64_t ntile = (s_end - s_begin + kTile - 1) / kTile;
-  if (ntile > 0) {
-    gload(s_begin);
-    lstore(0);
-    if (ntile > 1) {
-      gload(s_begin + kTile);
-      if (grp == 1) lstore(1);
-    }
-    if (grp == 1 && ntile > 2) gload(s_begin + 2 * kTile);
-    __syncthreads();
-    f32x16 acc;
-    bf16x8 gh[2], gl[2];
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        gh[s2][k] = (__bf16)0.0f;
-        gl[s2][k] = (__bf16)0.0f;
-      }
-    auto matrix = [&](int64_t k) {
-      if (k > 0) grad_x3s(gacc, gh, gl, sT[(k - 1) % 3], lane);
-      if (k < ntile) acc = dots_x3(sT[k % 3], c, h, uh, ul);
-    };
-    auto valu = [&](int64_t k) {
-      const int cur = (int)(k % 3);
-      const int64_t s0 = s_begin + k * kTile;
-      const bool exc = exc_flag(s0);
-      if (__any(exc)) {
-        float n[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) n[r] = 0.0f;
-        if (exc) {
-          for (int kk = p; kk < q; ++kk) {
-            const int ks = (int)(a.exc_s[kk] - s0), ke = (int)(a.exc_e[kk] - s0);
-            const float nk = (float)a.exc_n[kk];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) n[r] += (tile_row(r, h) >= ks && tile_row(r, h) < ke) ? nk : 0.0f;
-          }
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int tr = tile_row(r, h);
-          const float x = fmaf(acc[r], it2, -(sM0[cur][tr] + o_m2));
-          const bool lab = exc && sM2[cur][tr] == (int)o;
-          const float wr = lab ? 1.0f : o_cnt - n[r];
-          const float g = (wr > 0.0f ? wr * __builtin_amdgcn_exp2f(x) : 0.0f) - (lab ? 1.0f : 0.0f);
-          acc[r] = gso * g;
-        }
-        split_tile(acc, gh, gl);
-      } else {  // g = c_o * gout/tau * 2^(S log2e/tau - bias_o log2e - lse_i log2e): dots_g_x3's per-element form
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const float4 mv = *reinterpret_cast<const float4*>(&sM0[cur][8 * g4 + 4 * h]);
-          const float m4[4] = {mv.x, mv.y, mv.z, mv.w};
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const int r = 4 * g4 + t;
-            acc[r] = fo * __builtin_amdgcn_exp2f(fmaf(acc[r], it2, -(m4[t] + o_m2)));
-          }
-        }
-        split_tile(acc, gh, gl);
-      }
-      const int64_t ahead = grp == 0 ? 1 : 2;
-      if (k + ahead < ntile) lstore((int)((k + ahead) % 3));
-      if (k + ahead + 1 < ntile) gload(s_begin + (k + ahead + 1) * kTile);
-    };
-    for (int64_t hs = 0; hs < 2 * (ntile + 1); ++hs) {  // as nce_grouped_fwdg_pp_k
-      const int64_t k = hs >> 1;
-      const bool ph2 = (hs & 1) != 0;
-      if ((grp == 0) != ph2) {
-        __builtin_amdgcn_s_setprio(1);
-        matrix(k);
-        __builtin_amdgcn_s_setprio(0);
-      } else {
-        const int64_t kv = grp == 0 ? k : k - 1;
-        if (kv >= 0 && kv < ntile) valu(kv);
-      }
-      __syncthreads();
-    }
-  }
-  const int64_t own_base = (int64_t)ob * kOwn + wave * 32;
-  float* dst = a.dout + (int64_t)split * n_own * kD;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int64_t orow = own_base + tile_row(r, h);
-    if (orow < n_own) {
-#pragma unroll
-      for (int kb = 0; kb < 4; ++kb) dst[orow * kD + kb * 32 + c] = gacc[kb][r];
-    }
-  }
-}
-
 // merge of the fused forward: lse / row loss as nce_grouped_merge_k, plus the row gradient
 // per unit upstream gradient  ga_i = (sum_s O_s e^(m_s - M) / sum_s l_s e^(m_s - M) - B_d(i)) / tau
 __global__ __launch_bounds__(256) void nce_grouped_merge_g_k(const float* A, const float* B, const float* bias,
@@ -3270,7 +2898,7 @@ static bool fwdg_nt() {
   return v;
 }
 
-// RSX_NCE_FWDG=0 selects the unpipelined fused forward, =pp the ping-pong form (A/B measurements)
+// RSX_NCE_FWDG=0 selects the unpipelined fused forward (A/B measurements)
 static bool fwdg_pipelined() {
   static const bool v = [] {
     const char* e = getenv("RSX_NCE_FWDG");
@@ -3278,13 +2906,7 @@ static bool fwdg_pipelined() {
   }();
   return v;
 }
-static bool fwdg_pingpong() {
-  static const bool v = [] {
-    const char* e = getenv("RSX_NCE_FWDG");
-    return e && e[0] == 'p';
-  }();
-  return v;
-}
+
 
 // Measurement hooks (include/recsys_amd.h): event pairs around the fused forward kernel's launch.
 namespace {
@@ -3356,9 +2978,8 @@ RSX_API int rsx_nce_grouped_fwd_grad(const float* A, const float* B, const float
   // as fill whole rounds of the grid at two workgroups per CU; the remaining row blocks run 8
   // half-length splits, dispatched last, so the grid's final round is short and full
   // (batch 8192: 1,152 row blocks x 4 = 9 rounds of 512, then 45 x 8 half-length workgroups)
-  const bool pp = fwdg_pingpong();
   const bool piped = fwdg_pipelined();
-  const int nw = pp ? 8 : piped ? fwdg_waves() : kWaves;
+  const int nw = piped ? fwdg_waves() : kWaves;
   const int64_t rows_wg = 32 * nw;
   const int64_t rbs = (N + rows_wg - 1) / rows_wg;
   const int ns1 = nsplit == 8 ? 4 : nsplit;
@@ -3399,9 +3020,7 @@ RSX_API int rsx_nce_grouped_fwd_grad(const float* A, const float* B, const float
       k.ev.emplace_back(ev0, ev1);
     }
   }
-  if (pp)
-    hipLaunchKernelGGL(nce_grouped_fwdg_pp_k, dim3(blocks), dim3(512), 0, st, g);
-  else if (!piped)
+  if (!piped)
     hipLaunchKernelGGL(nce_grouped_fwdg_x3_k, dim3(blocks), dim3(256), 0, st, g);
   else if (nw == 8 && fwdg_nt())
     hipLaunchKernelGGL((nce_grouped_fwdg_x3p_k<8, true>), dim3(blocks), dim3(512), 0, st, g);
@@ -3491,15 +3110,8 @@ RSX_API int rsx_nce_grouped_bwd(const float* A, const float* B, const float* bia
         RSX_LAUNCHED();
       }
     }
-    static const bool col_pp = [] {
-      const char* e = getenv("RSX_NCE_BWD");
-      return e && e[0] == 'p';
-    }();
     if (row_owned && x3) hipLaunchKernelGGL(nce_grouped_bwd_x3_k<true>, dim3(blocks), dim3(256), 0, st, g);
-    else if (x3 && col_pp && g.split_major) {
-      const int64_t ob256 = (n_own + 255) / 256;
-      hipLaunchKernelGGL(nce_grouped_colpp_k, dim3((unsigned)(ob256 * ps)), dim3(512), 0, st, g);
-    } else if (x3) hipLaunchKernelGGL(nce_grouped_bwd_x3_k<false>, dim3(blocks), dim3(256), 0, st, g);
+    else if (x3) hipLaunchKernelGGL(nce_grouped_bwd_x3_k<false>, dim3(blocks), dim3(256), 0, st, g);
     else if (row_owned) hipLaunchKernelGGL(nce_grouped_bwd_k<true>, dim3(blocks), dim3(256), 0, st, g);
     else hipLaunchKernelGGL(nce_grouped_bwd_k<false>, dim3(blocks), dim3(256), 0, st, g);
     RSX_LAUNCHED();
