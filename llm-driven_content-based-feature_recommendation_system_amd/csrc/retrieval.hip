@@ -653,8 +653,8 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_scan_k(BfArgs a) {
   }
 }
 
-// P3 as its own kernel (opt-in, RSX_TOPK_COLLECT=1 / 2; measured slower than topk_bf16_scan_k<G,
-// 8, 1> in round 4: 2.51 vs 2.22 ms per 4096 x 1M call): the
+// P3 as its own kernel (round 4; PIPE = false is the default, RSX_TOPK_COLLECT=2: 2.16 vs 2.21 ms per
+// 4096 x 1M call for round 3's topk_bf16_scan_k<G, 8, 1>; PIPE = true measured 2.49 ms): the
 // per-score compare-and-append of that form (a branch per score: ~3 VALU + 5 SALU for each of a
 // lane's 32 scores per tile, about twice the wave's MFMA issue time) is replaced by
 //   * a max gate: each lane takes the max of its 16 scores of a query (v_max3) and only lanes
@@ -1330,11 +1330,11 @@ int run_bf16_chunk(const BfPlan& bp, const BfLayout& L, const float* U, int64_t 
     hipLaunchKernelGGL(topk_bf16_thresh_k<4096>, dim3((unsigned)Q), dim3(256), 0, st, b.cand_s, b.cand_i, ncand, U,
                        ldu, (int)k, wmax, thr);
   RSX_LAUNCHED();
-  // RSX_TOPK_COLLECT: 0 (default) topk_bf16_scan_k<G, 8, 1>; 1 topk_bf16_collect_k pipelined;
-  // 2 topk_bf16_collect_k gate only (A/B measurements)
+  // RSX_TOPK_COLLECT: 2 (default) topk_bf16_collect_k gate only; 1 topk_bf16_collect_k pipelined;
+  // 0 topk_bf16_scan_k<G, 8, 1> (round 3's full scan) -- A/B measurements
   static const int collect_k = [] {
     const char* e = getenv("RSX_TOPK_COLLECT");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 2;
   }();
   if (collect_k == 1) {
     if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_collect_k<2, true>), grid, dim3(256), 0, st, b);

@@ -19,7 +19,7 @@ NCE_SUPCON = 9
 _NSPLIT_FWD = 8
 # partial slots of the grouped forward; the fused forward (rsx_nce_grouped_fwd_grad) accepts 1/2/4/8 and
 # runs 4 splits on the leading row blocks, 8 on the tail
-_NSPLIT_FWD_GROUPED = int(os.environ.get("RSX_NCE_NSPLIT_FWD", "8"))
+_NSPLIT_FWD_GROUPED = int(os.environ.get("RSX_NCE_NSPLIT_FWD", "2"))
 if _NSPLIT_FWD_GROUPED not in (1, 2, 4, 8):
     raise ValueError("RSX_NCE_NSPLIT_FWD must be 1, 2, 4 or 8 (the fused forward's supported partial-slot counts)")
 _NSPLIT_BWD = 8

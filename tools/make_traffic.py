@@ -3,7 +3,7 @@ tools/nce_micro.py (rocprofv3 --pmc, separate passes; see tools/steps_final_r01.
 
 FETCH_SIZE is doubled (gfx950 reports half the bytes of 16-B/lane streaming reads,
 MI355X_MICROARCH.md HBM section); WRITE_SIZE is taken as reported.
-  python tools/make_traffic.py gpurun_out/pmcf gpurun_out/pmcw out.json [global_batch N D]"""
+  python tools/make_traffic.py gpurun_out/pmcf gpurun_out/pmcw out.json [global_batch N D [nslots]]"""
 import csv
 import glob
 import json
@@ -26,16 +26,17 @@ def main():
     write = vals(sys.argv[2], "WRITE_SIZE")
     # tools/nce_micro.py --batch B shapes (bench batch 0): 4096 -> N 76850, D 16363
     batch, N, D = (int(sys.argv[4]), int(sys.argv[5]), int(sys.argv[6])) if len(sys.argv) > 6 else (4096, 76850, 16363)
+    ns = int(sys.argv[7]) if len(sys.argv) > 7 else 4  # partial slots per row (RSX_NCE_NSPLIT_FWD; 4 in rounds 1-3)
     f = sum(fetch) / len(fetch)
     w = sum(write) / len(write)
     hbm = int((2 * f + w) * 1024)
-    # algorithmic: A and B rows (fp32) read once, the row-gradient partials [4][N][128] written
-    # once, the per-row (m, l) partials; images of B (hi/lo bf16) are written by the split
+    # algorithmic: A and B rows (fp32) read once, the row-gradient partials [ns][N][128] written
+    # once, the per-row (m, l, 0, 0) partials; images of B (hi/lo bf16) are written by the split
     # kernel outside this launch
-    alg = 4 * (N + D) * 128 + 4 * 4 * N * 128 + 4 * 4 * 4 * N
+    alg = 4 * (N + D) * 128 + ns * 4 * N * 128 + ns * 4 * 4 * N
     out = {
         "kernel": "nce_grouped_fwdg_x3p_k (grouped LogQ forward fused with the row gradient, pipelined)",
-        "precision": "bf16x3", "global_batch": batch, "rows_N": N, "distinct_targets_D": D,
+        "precision": "bf16x3", "global_batch": batch, "rows_N": N, "distinct_targets_D": D, "partial_slots": ns,
         "fetch_size_kb_raw": round(f, 1), "write_size_kb": round(w, 1),
         "hbm_bytes_per_launch": hbm,
         "correction": "FETCH_SIZE doubled (gfx950 reports half the bytes of 16-B/lane streaming reads, "
