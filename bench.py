@@ -40,7 +40,7 @@ FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32-input MFMA (= f
 BF16_MFMA_PEAK_TFLOPS = 16 * FP32_MFMA_PEAK_TFLOPS  # 2516.8: dense bf16 MFMA (16x the f32 rate, same guide)
 # bf16x3: every fp32-equivalent FLOP is three bf16 MFMA products (hi*hi + hi*lo + lo*hi)
 BF16X3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 3
-TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r03_nce_fwdg_traffic_b8192.json")
+TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r04_nce_fwdg_traffic_b8192.json")
 HBM_PEAK_GBS = 8000.0
 
 
@@ -794,12 +794,14 @@ def nce_roofline(args, tb, global_batch, rank, world, precision):
         avg_s = sum(kms) / len(kms) / 1e3
     achieved = (flops / max(launches, 1)) / avg_s / 1e12 if launches else None
     peak = BF16X3_PEAK_TFLOPS if x3 else FP32_MFMA_PEAK_TFLOPS
-    traffic, traffic_src = None, None
+    traffic, traffic_src, alg_bytes = None, None, None
     if os.path.exists(TRAFFIC_FILE):
         with open(TRAFFIC_FILE) as f:
             tr = json.load(f)
-        if tr.get("precision") == precision and tr.get("global_batch") == global_batch and world == 1 and fused:
+        if (tr.get("precision") == precision and tr.get("global_batch") == global_batch and world == 1 and fused
+                and tr.get("partial_slots", 4) == ops._NSPLIT_FWD_GROUPED):
             traffic, traffic_src = tr.get("hbm_bytes_per_launch"), os.path.basename(TRAFFIC_FILE)
+            alg_bytes = tr.get("algorithmic_bytes_per_launch")
     fwdg = "nce_grouped_fwdg_x3_k" if os.environ.get("RSX_NCE_FWDG", "1") == "0" else "nce_grouped_fwdg_x3p_k"
     return {"kernel": (f"{fwdg} (main LogQ loss forward fused with the row gradient)"
                        if fused else ("nce_grouped_bwd_x3_k<true>" if x3 else "nce_grouped_bwd_k<true>")
@@ -809,7 +811,8 @@ def nce_roofline(args, tb, global_batch, rank, world, precision):
             "op_window_ms": round(op_window_s * 1e3, 4), "bound": "mfma",
             "achieved": round(achieved, 2) if achieved else None, "peak": round(peak, 1),
             "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
-            "traffic": traffic, "traffic_source": traffic_src,
+            "traffic": traffic, "traffic_source": traffic_src, "algorithmic_bytes": alg_bytes,
+            "traffic_over_algorithmic": round(traffic / alg_bytes, 3) if traffic and alg_bytes else None,
             "flops_per_launch": round(flops / max(launches, 1)), "avg_launch_ms": round(avg_s * 1e3, 4),
             "peak_note": ("bf16 dense MFMA 2516.8 TF / 3 split products" if x3 else "fp32-input MFMA dense")}
 
