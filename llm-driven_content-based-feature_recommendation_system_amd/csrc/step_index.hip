@@ -13,11 +13,11 @@
 //   si_user_k      one wave per user: token / valid-step / distinct-target counts, the user's
 //                  valid targets sorted (wave bitonic sort), item-id and (user, target) pair
 //                  histograms
-//   scans          exclusive sums over users (token, row and pair offsets)
+//   si_scan_k      exclusive sums over users (token, row and pair offsets)
 //   si_tloc_k      this rank's loss-row targets in flat order into a [B*L + 1] buffer (-1 pad,
 //                  the row count in the last slot): the fixed-size block the ranks all-gather
 //   si_colhist_k   target histogram over the gathered blocks (the global columns)
-//   scans          over the item-id domain: column index, item segment offsets and chunk counts
+//   si_scan_k      over the item-id domain: column index, item segment offsets and chunk counts
 //   si_totals_k    T, N, D, E, U, C (+ every rank's row count) -> the one host read
 // Phase B (rsx_step_index_fill, sizes known): si_tokens_k (packed tokens of both views, per-token
 //   ids, loss rows and their column / user ranges, per-user sorted columns, pair keys), a stable
@@ -123,12 +123,66 @@ __global__ __launch_bounds__(256) void si_colhist_k(const int* tglob, int64_t n,
   }
 }
 
-struct Positive {
-  __host__ __device__ int operator()(int x) const { return x > 0 ? 1 : 0; }
+__device__ __forceinline__ int scan_xform(int x, int mode) {
+  return mode == 0 ? x : mode == 1 ? (x > 0 ? 1 : 0) : (2 * x + kSegChunk - 1) / kSegChunk;
+}
+
+// Exclusive sums of up to five int arrays, one workgroup per array (the arrays are short: B + 1
+// users or n_items + 1 ids), each thread holding 4 consecutive elements of a 4096-element tile,
+// with an optional transform of the input (mode 0 identity, 1 "> 0", 2 DuoRec-segment chunk
+// count of an item id with x view-1 tokens). One launch instead of one multi-kernel library scan
+// per array: the step index runs beside the step on a side stream, where every extra launch
+// waits for CU slots.
+struct ScanJob {
+  const int* in;
+  int* out;
+  int n, mode;
 };
-struct Chunks {  // chunks of the two-view segment of an item id with x view-1 tokens
-  __host__ __device__ int operator()(int x) const { return (2 * x + kSegChunk - 1) / kSegChunk; }
+struct ScanJobs {
+  ScanJob j[5];
 };
+
+__global__ __launch_bounds__(1024) void si_scan_k(ScanJobs js) {
+  const ScanJob J = js.j[blockIdx.x];
+  __shared__ int wsum[16];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int carry = 0;
+  for (int base = 0; base < J.n; base += 4096) {
+    const int i0 = base + tid * 4;
+    int v[4], s = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[k] = i0 + k < J.n ? scan_xform(J.in[i0 + k], J.mode) : 0;
+      s += v[k];
+    }
+    int x = s;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y = __shfl_up(x, d, 64);
+      if (lane >= d) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    if (w == 0) {
+      int t = lane < 16 ? wsum[lane] : 0;
+#pragma unroll
+      for (int d = 1; d < 16; d <<= 1) {
+        const int y = __shfl_up(t, d, 64);
+        if (lane >= d) t += y;
+      }
+      if (lane < 16) wsum[lane] = t;
+    }
+    __syncthreads();
+    int e = carry + (w > 0 ? wsum[w - 1] : 0) + x - s;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (i0 + k < J.n) J.out[i0 + k] = e;
+      e += v[k];
+    }
+    carry += wsum[15];
+    __syncthreads();  // wsum is rewritten by the next tile
+  }
+}
 
 __global__ void si_totals_k(const int* offT, const int* offN, const int* offE, const int* colidx, const int* itemidx,
                             const int* chunkoff, const int* err, const int* tglob, int world, int64_t B, int64_t L,
@@ -326,22 +380,11 @@ int bits_for(int64_t n) {  // bits of the largest key value n - 1
 }
 
 size_t temp_bytes(int64_t B, int64_t L, int64_t n_items) {
-  size_t mx = 0, s = 0;
+  size_t s = 0;
   int* ip = nullptr;
   unsigned* up = nullptr;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, s, ip, ip, (int)(B + 1));
-  mx = s > mx ? s : mx;
-  hipcub::TransformInputIterator<int, Positive, const int*> pos_it(ip, Positive());
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, s, pos_it, ip, (int)(n_items + 1));
-  mx = s > mx ? s : mx;
-  hipcub::TransformInputIterator<int, Chunks, const int*> ch_it(ip, Chunks());
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, s, ch_it, ip, (int)(n_items + 1));
-  mx = s > mx ? s : mx;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, s, ip, ip, (int)(n_items + 1));
-  mx = s > mx ? s : mx;
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, s, up, up, ip, ip, (int)(B * L), 0, 32);
-  mx = s > mx ? s : mx;
-  return mx;
+  return s;
 }
 
 SiLayout si_layout(int64_t B, int64_t L, int64_t n_items) {
@@ -420,12 +463,15 @@ RSX_API int rsx_step_index_count(const uint8_t* pm, const int64_t* tgt, const in
                      at<int>(ws, l.Nb), at<int>(ws, l.Eb), at<int>(ws, l.srt), at<int>(ws, l.hist_i),
                      at<int>(ws, l.hist_u), at<int>(ws, l.err));
   RSX_LAUNCHED();
-  size_t tb = (size_t)l.temp_bytes;
-  void* tmp = at<void>(ws, l.temp);
-  (void)hipcub::DeviceScan::ExclusiveSum(tmp, tb, at<int>(ws, l.Tb), at<int>(ws, l.offT), (int)(B + 1), st);
-  (void)hipcub::DeviceScan::ExclusiveSum(tmp, tb, at<int>(ws, l.Nb), at<int>(ws, l.offN), (int)(B + 1), st);
-  (void)hipcub::DeviceScan::ExclusiveSum(tmp, tb, at<int>(ws, l.Eb), at<int>(ws, l.offE), (int)(B + 1), st);
-  RSX_LAUNCHED();
+  {
+    ScanJobs js{};
+    const int nb = (int)(B + 1);
+    js.j[0] = {at<int>(ws, l.Tb), at<int>(ws, l.offT), nb, 0};
+    js.j[1] = {at<int>(ws, l.Nb), at<int>(ws, l.offN), nb, 0};
+    js.j[2] = {at<int>(ws, l.Eb), at<int>(ws, l.offE), nb, 0};
+    hipLaunchKernelGGL(si_scan_k, dim3(3), dim3(1024), 0, st, js);
+    RSX_LAUNCHED();
+  }
   hipLaunchKernelGGL(si_tloc_k, dim3(gu), dim3(256), 0, st, pm, tgt, B, (int)L, n_items, at<int>(ws, l.offN), tloc,
                      at<int>(ws, l.err));
   RSX_LAUNCHED();
@@ -443,18 +489,17 @@ RSX_API int rsx_step_index_totals(const int* tglob, int world, int64_t B, int64_
   hipLaunchKernelGGL(si_colhist_k, dim3(grid_for(n)), dim3(256), 0, st, tglob, n, blk, n_items,
                      at<int>(ws, l.hist_t));
   RSX_LAUNCHED();
-  size_t tb = (size_t)l.temp_bytes;
-  void* tmp = at<void>(ws, l.temp);
-  const int ni = (int)(n_items + 1);  // the extra (zero) element makes entry n_items the total
-  hipcub::TransformInputIterator<int, Positive, const int*> pos_t(at<int>(ws, l.hist_t), Positive());
-  hipcub::TransformInputIterator<int, Positive, const int*> pos_i(at<int>(ws, l.hist_i), Positive());
-  hipcub::TransformInputIterator<int, Chunks, const int*> ch_i(at<int>(ws, l.hist_i), Chunks());
-  (void)hipcub::DeviceScan::ExclusiveSum(tmp, tb, pos_t, at<int>(ws, l.colidx), ni, st);
-  (void)hipcub::DeviceScan::ExclusiveSum(tmp, tb, pos_i, at<int>(ws, l.itemidx), ni, st);
-  (void)hipcub::DeviceScan::ExclusiveSum(tmp, tb, at<int>(ws, l.hist_i), at<int>(ws, l.itemoff), ni, st);
-  (void)hipcub::DeviceScan::ExclusiveSum(tmp, tb, ch_i, at<int>(ws, l.chunkoff), ni, st);
-  (void)hipcub::DeviceScan::ExclusiveSum(tmp, tb, at<int>(ws, l.hist_u), at<int>(ws, l.pairoff), ni, st);
-  RSX_LAUNCHED();
+  {
+    const int ni = (int)(n_items + 1);  // the extra (zero) element makes entry n_items the total
+    ScanJobs js{};
+    js.j[0] = {at<int>(ws, l.hist_t), at<int>(ws, l.colidx), ni, 1};
+    js.j[1] = {at<int>(ws, l.hist_i), at<int>(ws, l.itemidx), ni, 1};
+    js.j[2] = {at<int>(ws, l.hist_i), at<int>(ws, l.itemoff), ni, 0};
+    js.j[3] = {at<int>(ws, l.hist_i), at<int>(ws, l.chunkoff), ni, 2};
+    js.j[4] = {at<int>(ws, l.hist_u), at<int>(ws, l.pairoff), ni, 0};
+    hipLaunchKernelGGL(si_scan_k, dim3(5), dim3(1024), 0, st, js);
+    RSX_LAUNCHED();
+  }
   hipLaunchKernelGGL(si_totals_k, dim3(1), dim3(64), 0, st, at<int>(ws, l.offT), at<int>(ws, l.offN),
                      at<int>(ws, l.offE), at<int>(ws, l.colidx), at<int>(ws, l.itemidx), at<int>(ws, l.chunkoff),
                      at<int>(ws, l.err), tglob, world, B, L, n_items, totals);
