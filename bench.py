@@ -761,12 +761,32 @@ def train_bench(args, global_batch, steps, warmup, items, cfg, model, item_tower
     if pf is not None:
         pf.close()
     torch.cuda.synchronize()
+    # Host cost of one step with the GPU idle when it starts: inside the timed loop the host runs
+    # ahead until the launch queue is full, after which every launch waits for the GPU, so the
+    # timed loop's enqueue time approaches the GPU step time. Here each step starts from an
+    # empty queue; the index is built inline (no prefetch thread), as at world > 1. Untimed.
+    unloaded = []
+    for j in range(3):
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        h0 = time.perf_counter()
+        ix = D.prepare_step_index(batches[j % 2], pretrained_lookup=lookup)
+        h1 = time.perf_counter()
+        D.contrastive_step_dp(model, item_tower, log_q, batches[j % 2], opt, cfg, lookup, bucket, index=ix)
+        h2 = time.perf_counter()
+        unloaded.append((h1 - h0, h2 - h1))
+    torch.cuda.synchronize()
+    unloaded = unloaded[1:]
+    host_unloaded = {"index_inline_ms": round(1e3 * sum(u[0] for u in unloaded) / len(unloaded), 3),
+                     "step_enqueue_ms": round(1e3 * sum(u[1] for u in unloaded) / len(unloaded), 3)}
+    host_unloaded["total_ms"] = round(host_unloaded["index_inline_ms"] + host_unloaded["step_enqueue_ms"], 3)
     elapsed = torch.tensor([t1 - t0], device=device, dtype=torch.float64)
     if world > 1:
         D.all_reduce_(elapsed, op=torch.distributed.ReduceOp.MAX)
     return {"elapsed": float(elapsed.item()), "kernel_times": kernel_times, "losses": losses, "n_glob": n_glob,
             "n_dist": n_dist, "n_tok": n_tok, "host_enqueue_ms": round(1e3 * sum(enqueue) / max(len(enqueue), 1), 3),
-            "alloc_retries": int(retries), "fwdg_kernel_ms": fwdg_kernel_ms}
+            "host_unloaded": host_unloaded, "alloc_retries": int(retries), "fwdg_kernel_ms": fwdg_kernel_ms}
 
 
 def nce_roofline(args, tb, global_batch, rank, world, precision):
@@ -845,7 +865,7 @@ def train_line(args, tb, global_batch, steps, warmup):
             "warmup": warmup, "ms_per_step": round(1e3 * tb["elapsed"] / steps, 3),
             "valid_positions_per_batch": [sum(c) for c in tb["n_glob"]], "distinct_targets_per_batch": tb["n_dist"],
             "main_loss_fwd_ms": round(nf[1] / max(nf[0], 1), 4), "host_enqueue_ms_per_step": tb["host_enqueue_ms"],
-            "alloc_retries": tb["alloc_retries"]}
+            "host_ms_per_step_unloaded": tb["host_unloaded"], "alloc_retries": tb["alloc_retries"]}
 
 
 def main():
@@ -923,6 +943,7 @@ def main():
         "roofline": nce_roofline(args, tb, args.batch, rank, world, args.nce_precision),
         "gather_roofline": gather_roofline(args, tb),
         "host_enqueue_ms_per_step": tb["host_enqueue_ms"],
+        "host_ms_per_step_unloaded": tb["host_unloaded"],
         "alloc_retries": tb["alloc_retries"],
         "kernels": kt,
         "final_loss": round(total_loss, 5),

@@ -653,21 +653,31 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_scan_k(BfArgs a) {
   }
 }
 
-// P3 as its own kernel (round 4; PIPE = false is the default, RSX_TOPK_COLLECT=2: 2.16 vs 2.21 ms per
-// 4096 x 1M call for round 3's topk_bf16_scan_k<G, 8, 1>; PIPE = true measured 2.49 ms): the
-// per-score compare-and-append of that form (a branch per score: ~3 VALU + 5 SALU for each of a
-// lane's 32 scores per tile, about twice the wave's MFMA issue time) is replaced by
-//   * a max gate: each lane takes the max of its 16 scores of a query (v_max3) and only lanes
-//     whose max reaches t_q walk their scores (one divergent branch per query group and tile);
-//   * software pipelining: the MFMAs of tile t are issued before the compares of tile t-1 (a
-//     second accumulator set), so the compares run under the matrix pipe in the wave's own
-//     instruction stream;
+// P3 as its own kernel (round 4): the one full scan, with every (a, j), a >= t_q, appended to its
+// lane's stream buffer. Against round 3's topk_bf16_scan_k<G, 8, 1> (a compare-and-append branch
+// per score: ~3 VALU + 5 SALU for each of a lane's 32 scores per tile):
+//   * a max gate: each lane takes the max of its 16 scores of a query group (v_max3) and only
+//     lanes whose max reaches t_q go on (one divergent branch per query group and tile);
+//   * max-first extraction (EXTRACT, the default): a passing lane appends its current max, knocks
+//     it out and repeats while the new max passes -- one or two rounds on almost every passing
+//     lane, instead of the 16 per-score compare-and-append branches that the whole wave walks
+//     whenever any one of its lanes passes (t_q lets ~0.25 % of the scores through, so some lane
+//     of a wave passes on ~90 % of the (tile, group) pairs: the extraction, not the MFMAs, sets
+//     the kernel's time -- the same kernel with the gate but no appends runs 0.83 ms, the MFMA
+//     floor is ~0.5 ms);
 //   * a clamped slot instead of a capacity branch: a stream that overflows keeps counting and its
 //     query goes to the exact kernels (P4), so what lands in its last slot is never read;
 //   * staging stores without bank conflicts: the 8 threads of an item row write its two 128-B
-//     halves as 8 contiguous 16-B pieces each (the previous 32-B-per-thread order was 2-way).
-// Same collected sets (same entries, same order within each stream) as topk_bf16_scan_k<.., 1>.
-template <int G, bool PIPE>
+//     halves as 8 contiguous 16-B pieces each.
+// 4096 x 1M, k = 100 (rocprof, same box): 1.70 ms per-score gate (EXTRACT = false), 1.56 ms
+// max-first; round 3's form 1.66-1.76. Measured and not kept (profiles/r04_retrieval_collect_ab.json):
+// a loader wave filling a 4-slot LDS ring by LDS-DMA (3.24 ms: 2 compute waves per SIMD instead of
+// 3), a per-wave LDS event queue drained one event per lane (1.60 / 1.91 ms), the appends placed
+// after the next tile's staging store (1.67 ms), a second accumulator set pipelining the compares
+// under the next tile's MFMAs (2.49 ms). The entries of a stream are the same set in every form;
+// their order within the stream differs with EXTRACT, which P4 never sees (its margin set and
+// final sort use the total order (score desc, index asc)).
+template <int G, bool EXTRACT>
 __global__ __launch_bounds__(256, 2) void topk_bf16_collect_k(BfArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned char sI[2][kTile * kImgStride];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -726,18 +736,11 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_collect_k(BfArgs a) {
     *reinterpret_cast<u32x4*>(dst + sb) = stg[0];
     *reinterpret_cast<u32x4*>(dst + 128 + sb) = stg[1];
   };
-  auto scores = [&](int buf, f32x16 (&acc)[G]) {
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[g][r] = 0.0f;
-    const unsigned char* xrow = &sI[buf][c * kImgStride + 16 * h];
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      const bf16x8 av = *reinterpret_cast<const bf16x8*>(xrow + 32 * ks);
-#pragma unroll
-      for (int g = 0; g < G; ++g) acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, ub[g][ks], acc[g], 0, 0, 0);
-    }
+  auto append = [&](int g, float sc, int j) {
+    const int slot = cnt[g] < kStreamCap ? cnt[g] : kStreamCap - 1;
+    bsp[g][slot] = sc;
+    bip[g][slot] = j;
+    ++cnt[g];
   };
   auto collect = [&](const f32x16 (&acc)[G], int jt0) {
     const bool full = jt0 + kTile <= jend;
@@ -749,22 +752,38 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_collect_k(BfArgs a) {
       float m3 = fmaxf(fmaxf(acc[g][9], acc[g][10]), acc[g][11]);
       float m4 = fmaxf(fmaxf(acc[g][12], acc[g][13]), acc[g][14]);
       const float mx = fmaxf(fmaxf(fmaxf(m0, m1), fmaxf(m2, m3)), fmaxf(m4, acc[g][15]));
-      if (mx >= thr[g]) {  // rare per lane: this lane's query has a collected item in the tile
+      if (!(mx >= thr[g])) continue;  // most lanes: no collected item of this query in the tile
+      if (EXTRACT) {
+        float v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = acc[g][r];
+        float m = mx;
+        // at most 16 rounds (t_q = -inf lets every score through)
+        for (int it = 0; it < 16 && m >= thr[g]; ++it) {
+          int rs = 15;
+#pragma unroll
+          for (int r = 14; r >= 0; --r) rs = v[r] == m ? r : rs;  // lowest position holding the max
+          const int j = jt0 + tile_row(rs, h);
+          if (full || j < jend) append(g, m, j);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = r == rs ? -INFINITY : v[r];
+          const float n0 = fmaxf(fmaxf(v[0], v[1]), v[2]);
+          const float n1 = fmaxf(fmaxf(v[3], v[4]), v[5]);
+          const float n2 = fmaxf(fmaxf(v[6], v[7]), v[8]);
+          const float n3 = fmaxf(fmaxf(v[9], v[10]), v[11]);
+          const float n4 = fmaxf(fmaxf(v[12], v[13]), v[14]);
+          m = fmaxf(fmaxf(fmaxf(n0, n1), fmaxf(n2, n3)), fmaxf(n4, v[15]));
+        }
+      } else {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int j = jt0 + tile_row(r, h);
-          const float sc = acc[g][r];
-          if (sc >= thr[g] && (full || j < jend)) {
-            const int slot = cnt[g] < kStreamCap ? cnt[g] : kStreamCap - 1;
-            bsp[g][slot] = sc;
-            bip[g][slot] = j;
-            ++cnt[g];
-          }
+          if (acc[g][r] >= thr[g] && (full || j < jend)) append(g, acc[g][r], j);
         }
       }
     }
   };
-  if (j_begin < j_end && !PIPE) {  // gate only: compares right after each tile's MFMAs
+  if (j_begin < j_end) {
     gload(j_begin);
     lstore(0);
     __syncthreads();
@@ -773,43 +792,22 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_collect_k(BfArgs a) {
       const bool has_next = j0 + kTile < j_end;
       if (has_next) gload(j0 + kTile);
       f32x16 acc[G];
-      scores(cur, acc);
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[g][r] = 0.0f;
+      const unsigned char* xrow = &sI[cur][c * kImgStride + 16 * h];
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        const bf16x8 av = *reinterpret_cast<const bf16x8*>(xrow + 32 * ks);
+#pragma unroll
+        for (int g = 0; g < G; ++g) acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, ub[g][ks], acc[g], 0, 0, 0);
+      }
       collect(acc, (int)j0);
-      if (has_next) lstore(cur ^ 1);
+      if (has_next) lstore(cur ^ 1);  // cur^1 was read in the previous tile, fenced by its barrier
       __syncthreads();
       cur ^= 1;
     }
-  } else if (j_begin < j_end) {
-    gload(j_begin);
-    lstore(0);
-    __syncthreads();
-    f32x16 accA[G], accB[G];
-    int cur = 0;
-    int64_t j0 = j_begin;
-    // one tile per step: MFMAs of tile j0 into `fresh`, then the compares of the previous tile
-    // (`old`, if any) under them; the two accumulator sets swap roles every step
-    auto step = [&](f32x16 (&fresh)[G], const f32x16 (&old)[G], bool has_old) -> bool {
-      const bool has_next = j0 + kTile < j_end;
-      if (has_next) gload(j0 + kTile);
-      scores(cur, fresh);
-      if (has_old) collect(old, (int)(j0 - kTile));
-      if (has_next) lstore(cur ^ 1);  // cur^1 was read in the previous step, fenced by its barrier
-      __syncthreads();
-      cur ^= 1;
-      j0 += kTile;
-      return has_next;
-    };
-    bool more = step(accA, accB, false);
-    bool last_in_a = true;
-    while (more) {
-      more = step(accB, accA, true);
-      last_in_a = false;
-      if (!more) break;
-      more = step(accA, accB, true);
-      last_in_a = true;
-    }
-    if (last_in_a) collect(accA, (int)(j0 - kTile));
-    else collect(accB, (int)(j0 - kTile));
   }
 #pragma unroll
   for (int g = 0; g < G; ++g)
@@ -1330,21 +1328,21 @@ int run_bf16_chunk(const BfPlan& bp, const BfLayout& L, const float* U, int64_t 
     hipLaunchKernelGGL(topk_bf16_thresh_k<4096>, dim3((unsigned)Q), dim3(256), 0, st, b.cand_s, b.cand_i, ncand, U,
                        ldu, (int)k, wmax, thr);
   RSX_LAUNCHED();
-  // RSX_TOPK_COLLECT: 2 (default) topk_bf16_collect_k gate only; 1 topk_bf16_collect_k pipelined;
-  // 0 topk_bf16_scan_k<G, 8, 1> (round 3's full scan) -- A/B measurements
+  // RSX_TOPK_COLLECT (A/B): 1 (default) topk_bf16_collect_k max-first extraction; 2 its per-score
+  // form; 0 topk_bf16_scan_k<G, 8, 1> (round 3's full scan)
   static const int collect_k = [] {
     const char* e = getenv("RSX_TOPK_COLLECT");
-    return e ? atoi(e) : 2;
+    return e ? atoi(e) : 1;
   }();
-  if (collect_k == 1) {
-    if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_collect_k<2, true>), grid, dim3(256), 0, st, b);
-    else hipLaunchKernelGGL((topk_bf16_collect_k<1, true>), grid, dim3(256), 0, st, b);
-  } else if (collect_k == 2) {
+  if (collect_k == 2) {
     if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_collect_k<2, false>), grid, dim3(256), 0, st, b);
     else hipLaunchKernelGGL((topk_bf16_collect_k<1, false>), grid, dim3(256), 0, st, b);
-  } else {
+  } else if (collect_k == 0) {
     if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_scan_k<2, 8, 1>), grid, dim3(256), 0, st, b);
     else hipLaunchKernelGGL((topk_bf16_scan_k<1, 8, 1>), grid, dim3(256), 0, st, b);
+  } else {
+    if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_collect_k<2, true>), grid, dim3(256), 0, st, b);
+    else hipLaunchKernelGGL((topk_bf16_collect_k<1, true>), grid, dim3(256), 0, st, b);
   }
   RSX_LAUNCHED();
   hipLaunchKernelGGL(topk_bf16_select_k, dim3((unsigned)Q), dim3(256), 0, st, b.buf_s, b.buf_i, b.buf_n,
