@@ -766,7 +766,13 @@ def train_bench(args, global_batch, steps, warmup, items, cfg, model, item_tower
     # timed loop's enqueue time approaches the GPU step time. Here each step starts from an
     # empty queue; the index is built inline (no prefetch thread), as at world > 1. Untimed.
     unloaded = []
-    for j in range(3):
+    prof_path = os.environ.get("RSX_HOST_PROFILE")  # cProfile of the unloaded steps (tools only)
+    prof = None
+    if prof_path:
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
+    for j in range(12 if prof else 3):
         torch.cuda.synchronize()
         if world > 1:
             torch.distributed.barrier()
@@ -777,6 +783,9 @@ def train_bench(args, global_batch, steps, warmup, items, cfg, model, item_tower
         h2 = time.perf_counter()
         unloaded.append((h1 - h0, h2 - h1))
     torch.cuda.synchronize()
+    if prof is not None:
+        prof.disable()
+        prof.dump_stats(prof_path)
     unloaded = unloaded[1:]
     host_unloaded = {"index_inline_ms": round(1e3 * sum(u[0] for u in unloaded) / len(unloaded), 3),
                      "step_enqueue_ms": round(1e3 * sum(u[1] for u in unloaded) / len(unloaded), 3)}
