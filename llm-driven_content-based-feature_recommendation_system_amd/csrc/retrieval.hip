@@ -492,8 +492,9 @@ struct BfArgs {
   float* cand_s;       // MODE 0: [Q][nsplit][2][T], each stream's list sorted desc
   int* cand_i;
   const float* thr;    // MODE 1: [Q] collection threshold t_q
-  float* buf_s;        // MODE 1: [Q][nsplit][2][kStreamCap]
-  int* buf_i;
+  // MODE 1: [Q][nsplit][2][kStreamCap] entries (score, item id as float bits): one 8-B store per
+  // append (two separate 4-B arrays made two write requests of a partial line each)
+  float2* buf_e;
   int* buf_n;          // MODE 1: [Q][nsplit][2] appended count (may exceed the cap: overflow)
 };
 
@@ -544,32 +545,31 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_scan_k(BfArgs a) {
   int64_t sbase[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) sbase[g] = ((q0 + 32 * g) * a.nsplit + split) * 2 + h;
-  float* bsp[G];
-  int* bip[G];
+  float2* bep[G];
 #pragma unroll
-  for (int g = 0; g < G; ++g) {  // MODE 1 stream buffers of this lane's queries
-    bsp[g] = MODE == 1 ? a.buf_s + sbase[g] * kStreamCap : nullptr;
-    bip[g] = MODE == 1 ? a.buf_i + sbase[g] * kStreamCap : nullptr;
-  }
+  for (int g = 0; g < G; ++g)  // MODE 1 stream buffers of this lane's queries
+    bep[g] = MODE == 1 ? a.buf_e + sbase[g] * kStreamCap : nullptr;
 
-  // staging: 8 threads per item row, 32 B each
-  const int srow = tid >> 3, sb = (tid & 7) * 32;
+  // staging: 8 threads per item row, each moving 16-B piece (tid & 7) of both 128-B halves (the
+  // 8 threads of a row write 128 contiguous bytes per store: no bank conflicts, as in
+  // topk_bf16_collect_k; the previous 32 B per thread was 2-way)
+  const int srow = tid >> 3, sb = (tid & 7) * 16;
   u32x4 stg[2];
   auto gload = [&](int64_t j0) {
     const int64_t j = j0 + srow;
     if (j < j_end) {
-      const u32x4* src = reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(a.img + j * kD) + sb);
-      stg[0] = src[0];
-      stg[1] = src[1];
+      const unsigned char* src = reinterpret_cast<const unsigned char*>(a.img + j * kD);
+      stg[0] = *reinterpret_cast<const u32x4*>(src + sb);
+      stg[1] = *reinterpret_cast<const u32x4*>(src + 128 + sb);
     } else {
       stg[0] = u32x4{0u, 0u, 0u, 0u};
       stg[1] = stg[0];
     }
   };
   auto lstore = [&](int buf) {
-    u32x4* dst = reinterpret_cast<u32x4*>(&sI[buf][srow * kImgStride + sb]);
-    dst[0] = stg[0];
-    dst[1] = stg[1];
+    unsigned char* dst = &sI[buf][srow * kImgStride];
+    *reinterpret_cast<u32x4*>(dst + sb) = stg[0];
+    *reinterpret_cast<u32x4*>(dst + 128 + sb) = stg[1];
   };
   if (j_begin < j_end) {
     gload(j_begin);
@@ -625,10 +625,7 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_scan_k(BfArgs a) {
               }
             }
           } else if (sc >= thr[g] && (full_tile || j < jend)) {
-            if (cnt[g] < kStreamCap) {
-              bsp[g][cnt[g]] = sc;
-              bip[g][cnt[g]] = j;
-            }
+            if (cnt[g] < kStreamCap) bep[g][cnt[g]] = make_float2(sc, __int_as_float(j));
             ++cnt[g];
           }
         }
@@ -689,8 +686,7 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_collect_k(BfArgs a) {
   bf16x8 ub[G][8];
   float thr[G];
   int cnt[G];
-  float* bsp[G];
-  int* bip[G];
+  float2* bep[G];
   int64_t sbase[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
@@ -699,8 +695,7 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_collect_k(BfArgs a) {
     thr[g] = ok ? a.thr[q] : INFINITY;  // no finite score reaches +inf: rows past Q collect nothing
     cnt[g] = 0;
     sbase[g] = ((ok ? q : 0) * a.nsplit + split) * 2 + h;
-    bsp[g] = a.buf_s + sbase[g] * kStreamCap;
-    bip[g] = a.buf_i + sbase[g] * kStreamCap;
+    bep[g] = a.buf_e + sbase[g] * kStreamCap;
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
       float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
@@ -738,8 +733,7 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_collect_k(BfArgs a) {
   };
   auto append = [&](int g, float sc, int j) {
     const int slot = cnt[g] < kStreamCap ? cnt[g] : kStreamCap - 1;
-    bsp[g][slot] = sc;
-    bip[g][slot] = j;
+    bep[g][slot] = make_float2(sc, __int_as_float(j));
     ++cnt[g];
   };
   auto collect = [&](const f32x16 (&acc)[G], int jt0) {
@@ -934,7 +928,7 @@ __global__ __launch_bounds__(256) void topk_bf16_thresh_k(const float* __restric
 // write the first k. (The margin set's order before the final sort does not matter: (e, idx)
 // pairs are distinct, so the output is deterministic.)
 constexpr int kMarginMax = 2048;
-__global__ __launch_bounds__(256) void topk_bf16_select_k(const float* __restrict__ bs, const int* __restrict__ bi,
+__global__ __launch_bounds__(256) void topk_bf16_select_k(const float2* __restrict__ be,
                                                           const int* __restrict__ bn, int nstreams,
                                                           const float* __restrict__ U, int64_t ldu,
                                                           const float* __restrict__ I, int64_t ldi, int K,
@@ -1000,7 +994,7 @@ __global__ __launch_bounds__(256) void topk_bf16_select_k(const float* __restric
         const int n = off[st + 1] - off[st];
         if (e < n) {
           dst[u] = off[st] + e;
-          v[u] = bs[(q * nstreams + st) * kStreamCap + e];
+          v[u] = be[(q * nstreams + st) * kStreamCap + e].x;
         }
       }
     }
@@ -1037,7 +1031,7 @@ __global__ __launch_bounds__(256) void topk_bf16_select_k(const float* __restric
 #pragma unroll
     for (int u = 0; u < kMarginMax / 256; ++u) {
       const int t = tid + 256 * u;
-      ids[u] = t < n ? bi[q * nstreams * kStreamCap + mi[t]] : 0;
+      ids[u] = t < n ? __float_as_int(be[q * nstreams * kStreamCap + mi[t]].y) : 0;
     }
     __syncthreads();  // every slot read before any is overwritten
 #pragma unroll
@@ -1203,7 +1197,7 @@ constexpr int64_t kQChunk = 4096;
 int64_t corpus_bytes(int64_t NI) { return kHeader + align256(NI * kD * 2); }
 
 struct BfLayout {
-  int64_t corpus, thr, qmap, cand_s, cand_i, buf_s, buf_i, buf_n, fallback, total;
+  int64_t corpus, thr, qmap, cand_s, cand_i, buf_e, buf_n, fallback, total;
 };
 BfLayout bf_layout(int64_t Qc, int64_t NI, int64_t k, const BfPlan& p, bool own_corpus) {
   BfLayout L;
@@ -1213,9 +1207,8 @@ BfLayout bf_layout(int64_t Qc, int64_t NI, int64_t k, const BfPlan& p, bool own_
   L.qmap = L.thr + align256(Qc * 4);
   L.cand_s = L.qmap + align256(Qc * 4);
   L.cand_i = L.cand_s + align256(nstream * p.T * 4);
-  L.buf_s = L.cand_i + align256(nstream * p.T * 4);
-  L.buf_i = L.buf_s + align256(nstream * kStreamCap * 4);
-  L.buf_n = L.buf_i + align256(nstream * kStreamCap * 4);
+  L.buf_e = L.cand_i + align256(nstream * p.T * 4);
+  L.buf_n = L.buf_e + align256(nstream * kStreamCap * 8);
   const int64_t end = L.buf_n + align256(nstream * 4);
   // the exact kernels for the chunk's listed queries run after its P4: they reuse the
   // candidate / stream-buffer region (never the corpus image, which later chunks still read)
@@ -1293,8 +1286,7 @@ int run_bf16_chunk(const BfPlan& bp, const BfLayout& L, const float* U, int64_t 
   b.cand_s = reinterpret_cast<float*>(w + L.cand_s);
   b.cand_i = reinterpret_cast<int*>(w + L.cand_i);
   b.thr = reinterpret_cast<const float*>(w + L.thr);
-  b.buf_s = reinterpret_cast<float*>(w + L.buf_s);
-  b.buf_i = reinterpret_cast<int*>(w + L.buf_i);
+  b.buf_e = reinterpret_cast<float2*>(w + L.buf_e);
   b.buf_n = reinterpret_cast<int*>(w + L.buf_n);
   const dim3 grid((unsigned)(bp.nqb * bp.nsplit));
   // P1 over ns0 <= nsplit splits: each workgroup samples nsplit / ns0 times the items (same
@@ -1345,7 +1337,7 @@ int run_bf16_chunk(const BfPlan& bp, const BfLayout& L, const float* U, int64_t 
     else hipLaunchKernelGGL((topk_bf16_collect_k<1, true>), grid, dim3(256), 0, st, b);
   }
   RSX_LAUNCHED();
-  hipLaunchKernelGGL(topk_bf16_select_k, dim3((unsigned)Q), dim3(256), 0, st, b.buf_s, b.buf_i, b.buf_n,
+  hipLaunchKernelGGL(topk_bf16_select_k, dim3((unsigned)Q), dim3(256), 0, st, b.buf_e, b.buf_n,
                      bp.nsplit * 2, U, ldu, I, ldi, (int)k, wmax, out_scores, out_idx, qcount, qmap, qtotal);
   RSX_LAUNCHED();
   // exact list-based kernels for the queries P4 listed (none on spread data)
