@@ -530,9 +530,11 @@ def bench_retrieve_rerank(args, device, deepfm, rank=0, world=1):
            "value": round(Q / dt, 1), "unit": "queries/s", "queries": Q, "corpus": I, "n_gpus": world,
            "ms_per_batch": round(dt * 1e3, 3), "rerank_rows_per_s": round(Q * K / dt, 1),
            "data": "synthetic normalised N(0,1) corpus / users, hashed rerank ids",
-           "retrieval": {"kernel": "rsx_retrieve_topk: topk_bf16_prep_k (corpus bf16 image) + topk_bf16_scan_k "
-                                   "(the one pass: bf16 MFMA scores, per-lane best-T lists) + topk_select_k "
-                                   "(margin set rescored exactly in fp32, exactness check)",
+           "retrieval": {"kernel": "rsx_retrieve_topk: topk_bf16_prep_k (corpus bf16 image, cached across calls) + "
+                                   "topk_bf16_scan_k (strided sample, best per lane stream) + topk_bf16_thresh_k "
+                                   "(per-query threshold) + topk_bf16_collect_k (the one full scan: bf16 MFMA "
+                                   "scores, max-gated appends) + topk_bf16_select_k (margin set rescored exactly "
+                                   "in fp32, exactness check)",
                          "avg_ms": round(rs * 1e3, 4), "items_per_rank": hi - lo,
                          "achieved_TFLOPs": round(flops / rs / 1e12, 2),
                          "peak_TFLOPs": round(BF16_MFMA_PEAK_TFLOPS, 1),
