@@ -844,18 +844,49 @@ __device__ __forceinline__ float from_okey(unsigned k) {
   return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
 }
 
-// K-th largest (1 <= K <= n) of v[0, n) in LDS, by a four-pass 8-bit radix select over okey
-// (integer LDS histograms; wave 0 finds each pass's digit with a 64-lane scan over 4 bins per
-// lane). Replaces a full bitonic sort where only the K-th value is needed. Every thread returns it.
-__device__ float block_kth_largest(const float* v, int n, int K, int* hist, int* sel) {
-  unsigned prefix = 0u, mask = 0u;
+// K-th largest (1 <= K <= n) of v[0, n) in LDS, by an 8-bit radix select over okey (integer LDS
+// histograms; wave 0 finds each pass's digit with a 64-lane scan over 4 bins per lane). Replaces a
+// full bitonic sort where only the K-th value is needed. The passes start at the highest bit in
+// which the keys differ (block min / max first): scores of one query share their sign and top
+// exponent bits, and a pass over a constant digit put every key's LDS atomic on one address (the
+// round-3 form's first pass). Every thread returns the value. red: >= 8 ints of LDS scratch.
+__device__ float block_kth_largest(const float* v, int n, int K, int* hist, int* sel, unsigned* red) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  unsigned kmin = 0xffffffffu, kmax = 0u;
+  for (int t = threadIdx.x; t < n; t += blockDim.x) {
+    const unsigned k = okey(v[t]);
+    kmin = min(kmin, k);
+    kmax = max(kmax, k);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    kmin = min(kmin, (unsigned)__shfl_xor((int)kmin, o, 64));
+    kmax = max(kmax, (unsigned)__shfl_xor((int)kmax, o, 64));
+  }
+  if (lane == 0) {
+    red[wave] = kmin;
+    red[4 + wave] = kmax;
+  }
+  __syncthreads();
+  kmin = red[0];
+  kmax = red[4];
+  for (int w = 1; w < nw; ++w) {
+    kmin = min(kmin, red[w]);
+    kmax = max(kmax, red[4 + w]);
+  }
+  const unsigned diff = kmin ^ kmax;
+  if (diff == 0u) return from_okey(kmin);  // block-uniform: every key equal
+  const int hb = 31 - __clz((int)diff);
+  unsigned mask = ~((2u << hb) - 1u);       // hb = 31: 2u << 31 wraps to 0, mask 0
+  unsigned prefix = kmin & mask;
   int krem = K;
-  for (int shift = 24; shift >= 0; shift -= 8) {
+  for (int top = hb; top >= 0; top -= 8) {
+    const int lo = top >= 7 ? top - 7 : 0;
+    const unsigned dm = (2u << (top - lo)) - 1u;  // digit mask, top - lo + 1 bits
     for (int t = threadIdx.x; t < 256; t += blockDim.x) hist[t] = 0;
     __syncthreads();
     for (int t = threadIdx.x; t < n; t += blockDim.x) {
       const unsigned k = okey(v[t]);
-      if ((k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1);
+      if ((k & mask) == prefix) atomicAdd(&hist[(k >> lo) & dm], 1);
     }
     __syncthreads();
     if (threadIdx.x < 64) {  // lane l owns digits 255-4l .. 252-4l (descending)
@@ -887,8 +918,8 @@ __device__ float block_kth_largest(const float* v, int n, int K, int* hist, int*
       }
     }
     __syncthreads();
-    prefix |= (unsigned)sel[0] << shift;
-    mask |= 255u << shift;
+    prefix |= (unsigned)sel[0] << lo;
+    mask |= dm << lo;
     krem = sel[1];
     __syncthreads();  // sel / hist are rewritten by the next pass
   }
@@ -902,6 +933,7 @@ __global__ __launch_bounds__(256) void topk_bf16_thresh_k(const float* __restric
                                                           const unsigned* wmax_bits, float* thr) {
   __shared__ float ss[NC];
   __shared__ int hist[256], sel[2], nval_s;
+  __shared__ unsigned red[8];
   const int64_t q = blockIdx.x;
   if (threadIdx.x == 0) nval_s = 0;
   __syncthreads();
@@ -919,7 +951,7 @@ __global__ __launch_bounds__(256) void topk_bf16_thresh_k(const float* __restric
     if (threadIdx.x == 0) thr[q] = -INFINITY;
     return;
   }
-  const float ck = block_kth_largest(ss, ncand, K, hist, sel);
+  const float ck = block_kth_largest(ss, ncand, K, hist, sel, red);
   if (threadIdx.x == 0) thr[q] = ck - 2.0f * delta;
 }
 
@@ -936,11 +968,12 @@ __global__ __launch_bounds__(256) void topk_bf16_select_k(const float2* __restri
                                                           int* qcount, int* qmap, int* qtotal) {
   // LDS: the appended scores only (their item ids are read back from global for the margin set),
   // so three workgroups fit per CU
-  __shared__ float ss[kSelMax];
-  __shared__ float ms[kMarginMax];
-  __shared__ int mi[kMarginMax];
+  __shared__ __attribute__((aligned(16))) float ss[kSelMax];
+  __shared__ __attribute__((aligned(16))) float ms[kMarginMax];
+  __shared__ __attribute__((aligned(16))) int mi[kMarginMax];
   __shared__ int off[513];
   __shared__ int hist[256], sel[2];
+  __shared__ unsigned red[8];
   __shared__ int bad_s, nsel_s;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t q = blockIdx.x;
@@ -981,13 +1014,13 @@ __global__ __launch_bounds__(256) void topk_bf16_select_k(const float2* __restri
     }
     return;
   }
-  // 32 threads per stream, 8 streams per pass; sixteen passes' loads are issued before their LDS
-  // stores (one memory latency per 128 streams instead of per 8)
-  for (int s0 = 0; s0 < nstreams; s0 += 128) {
-    float v[16];
-    int dst[16];
+  // 32 threads per stream, 8 streams per pass; 32 passes' loads are issued before their LDS
+  // stores (one memory latency per 256 streams instead of per 8)
+  for (int s0 = 0; s0 < nstreams; s0 += 256) {
+    float v[32];
+    int dst[32];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
+    for (int u = 0; u < 32; ++u) {
       const int st = s0 + 8 * u + (tid >> 5), e = tid & 31;
       dst[u] = -1;
       if (st < nstreams) {
@@ -999,19 +1032,19 @@ __global__ __launch_bounds__(256) void topk_bf16_select_k(const float2* __restri
       }
     }
 #pragma unroll
-    for (int u = 0; u < 16; ++u)
+    for (int u = 0; u < 32; ++u)
       if (dst[u] >= 0) ss[dst[u]] = v[u];
   }
   __syncthreads();
-  const float thr = (total >= K) ? block_kth_largest(ss, total, K, hist, sel) - 2.0f * delta : -INFINITY;
-  // margin set: walk the streams again (LDS only: the selected entries' buffer slots are noted),
-  // then every selected item id is loaded from global at once (one memory latency, not one per
-  // walk step that holds a selected entry)
-  for (int s0 = 0; s0 < nstreams; s0 += 8) {
-    const int st = s0 + (tid >> 5), e = tid & 31;
-    if (st < nstreams) {
-      const int o = off[st];
-      if (e < off[st + 1] - o && ss[o + e] >= thr) {
+  const float thr = (total >= K) ? block_kth_largest(ss, total, K, hist, sel, red) - 2.0f * delta : -INFINITY;
+  // margin set: one thread per stream walks that stream's entries (~5 on spread data) and notes
+  // the buffer slot of each selected one; every selected item id is then loaded from global at
+  // once (one memory latency). (Round 3 walked 8 streams per step with 32 threads each: 64
+  // dependent LDS steps per query.)
+  for (int st = tid; st < nstreams; st += 256) {
+    const int o = off[st], cn = off[st + 1] - o;
+    for (int e = 0; e < cn; ++e) {
+      if (ss[o + e] >= thr) {
         const int slot = atomicAdd(&nsel_s, 1);
         if (slot < kMarginMax) mi[slot] = st * kStreamCap + e;
       }
@@ -1044,33 +1077,71 @@ __global__ __launch_bounds__(256) void topk_bf16_select_k(const float2* __restri
   // exact fp32 rescoring: 32 lanes per item, float4 per lane, fixed-order shuffle reduction
   const int sub = lane >> 5, c = lane & 31;
   const float4 u4 = reinterpret_cast<const float4*>(U + q * ldu)[c];
-  for (int t0 = 0; t0 < n; t0 += 32) {  // four items per half-wave in flight
-    float4 w4[4];
+  for (int t0 = 0; t0 < n; t0 += 64) {  // eight items per half-wave in flight
+    float4 w4[8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < 8; ++u) {
       const int t = t0 + 8 * u + wave * 2 + sub;
       w4[u] = t < n ? reinterpret_cast<const float4*>(I + (int64_t)mi[t] * ldi)[c] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < 8; ++u) {
       const int t = t0 + 8 * u + wave * 2 + sub;
       float e = u4.x * w4[u].x + u4.y * w4[u].y + u4.z * w4[u].z + u4.w * w4[u].w;
       for (int o = 16; o > 0; o >>= 1) e += __shfl_xor(e, o, 64);
       if (t < n && c == 0) ms[t] = e;
     }
   }
-  int P2 = 1;
-  while (P2 < n) P2 <<= 1;
-  for (int t = n + tid; t < P2; t += 256) {
-    ms[t] = -INFINITY;
-    mi[t] = 0x7fffffff;
-  }
+  // rank-sort keys (n <= 512): okey(e) << 32 | ~id, so "beats" is one unsigned 64-bit compare
+  // (e desc, then id asc); padded to a multiple of two with 0 (beats nothing). ss is free now.
+  unsigned long long* rk = reinterpret_cast<unsigned long long*>(ss);
+  __syncthreads();  // every rescored ms[t] written
+  if (n <= 512)
+    for (int t = tid; t < ((n + 1) & ~1); t += 256)
+      rk[t] = t < n ? ((unsigned long long)okey(ms[t]) << 32) | (unsigned)(~mi[t]) : 0ull;
   __syncthreads();
-  bitonic_desc_n(ms, mi, P2);
-  for (int t = tid; t < K; t += 256) {
-    const bool ok = t < n;
-    out_s[q * K + t] = ok ? ms[t] : -INFINITY;
-    out_i[q * K + t] = ok ? (int64_t)mi[t] : -1;
+  if (n <= 512) {
+    // rank sort: an entry's output position is the number of entries that beat it under (e desc,
+    // index asc) -- distinct item ids make the ranks a permutation; all threads read entry j at
+    // once (LDS broadcast), no barrier per step as in the bitonic network below
+    for (int t = tid; t < K; t += 256) {
+      if (t >= n) {
+        out_s[q * K + t] = -INFINITY;
+        out_i[q * K + t] = -1;
+      }
+    }
+    const int n2 = (n + 1) >> 1;
+    const ulonglong2* rk2 = reinterpret_cast<const ulonglong2*>(rk);
+    for (int t = tid; t < n; t += 256) {
+      const float e = ms[t];
+      const int id = mi[t];
+      const unsigned long long kt = rk[t];
+      int r = 0;
+#pragma unroll 4
+      for (int j = 0; j < n2; ++j) {
+        const ulonglong2 kj = rk2[j];
+        r += (kj.x > kt) ? 1 : 0;
+        r += (kj.y > kt) ? 1 : 0;
+      }
+      if (r < K) {
+        out_s[q * K + r] = e;
+        out_i[q * K + r] = (int64_t)id;
+      }
+    }
+  } else {
+    int P2 = 1;
+    while (P2 < n) P2 <<= 1;
+    for (int t = n + tid; t < P2; t += 256) {
+      ms[t] = -INFINITY;
+      mi[t] = 0x7fffffff;
+    }
+    __syncthreads();
+    bitonic_desc_n(ms, mi, P2);
+    for (int t = tid; t < K; t += 256) {
+      const bool ok = t < n;
+      out_s[q * K + t] = ok ? ms[t] : -INFINITY;
+      out_i[q * K + t] = ok ? (int64_t)mi[t] : -1;
+    }
   }
 }
 
