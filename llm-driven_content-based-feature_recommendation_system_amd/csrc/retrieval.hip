@@ -655,19 +655,20 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_scan_k(BfArgs a) {
 // per score: ~3 VALU + 5 SALU for each of a lane's 32 scores per tile):
 //   * a max gate: each lane takes the max of its 16 scores of a query group (v_max3) and only
 //     lanes whose max reaches t_q go on (one divergent branch per query group and tile);
-//   * max-first extraction (EXTRACT, the default): a passing lane appends its current max, knocks
-//     it out and repeats while the new max passes -- one or two rounds on almost every passing
-//     lane, instead of the 16 per-score compare-and-append branches that the whole wave walks
-//     whenever any one of its lanes passes (t_q lets ~0.25 % of the scores through, so some lane
-//     of a wave passes on ~90 % of the (tile, group) pairs: the extraction, not the MFMAs, sets
-//     the kernel's time -- the same kernel with the gate but no appends runs 0.83 ms, the MFMA
-//     floor is ~0.5 ms);
+//   * behind the gate, one compare per score on tiles wholly inside the split (the split-end
+//     check only on its last tile) and the append as one 8-B (score, id) store -- t_q lets ~0.25 %
+//     of the scores through, so some lane of a wave passes on ~90 % of the (tile, group) pairs and
+//     the appends, not the MFMAs, set the kernel's time (the same kernel with the gate but no
+//     appends runs 0.83 ms, the MFMA floor is ~0.5 ms). EXTRACT (RSX_TOPK_COLLECT=1) appends
+//     max-first instead (the lane's max, knocked out, repeated while the new max passes);
 //   * a clamped slot instead of a capacity branch: a stream that overflows keeps counting and its
 //     query goes to the exact kernels (P4), so what lands in its last slot is never read;
 //   * staging stores without bank conflicts: the 8 threads of an item row write its two 128-B
 //     halves as 8 contiguous 16-B pieces each.
-// 4096 x 1M, k = 100 (rocprof, same box): 1.70 ms per-score gate (EXTRACT = false), 1.56 ms
-// max-first; round 3's form 1.66-1.76. Measured and not kept (profiles/r04_retrieval_collect_ab.json):
+// 4096 x 1M, k = 100 (rocprof): with 4-B score and id stores, 1.70 ms per-score, 1.56 ms max-first;
+// with 8-B entries 1.49 max-first, 1.47 per-score with the whole-tile compare (the default);
+// round 3's form 1.66-1.76. Measured and not kept (profiles/r04_retrieval_collect_ab.json): a
+// two-level gate (groups of four scores, 1.54 ms),
 // a loader wave filling a 4-slot LDS ring by LDS-DMA (3.24 ms: 2 compute waves per SIMD instead of
 // 3), a per-wave LDS event queue drained one event per lane (1.60 / 1.91 ms), the appends placed
 // after the next tile's staging store (1.67 ms), a second accumulator set pipelining the compares
@@ -768,6 +769,10 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_collect_k(BfArgs a) {
           const float n4 = fmaxf(fmaxf(v[12], v[13]), v[14]);
           m = fmaxf(fmaxf(fmaxf(n0, n1), fmaxf(n2, n3)), fmaxf(n4, v[15]));
         }
+      } else if (full) {  // whole tile inside the split: one compare per score
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (acc[g][r] >= thr[g]) append(g, acc[g][r], jt0 + tile_row(r, h));
       } else {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -1391,21 +1396,21 @@ int run_bf16_chunk(const BfPlan& bp, const BfLayout& L, const float* U, int64_t 
     hipLaunchKernelGGL(topk_bf16_thresh_k<4096>, dim3((unsigned)Q), dim3(256), 0, st, b.cand_s, b.cand_i, ncand, U,
                        ldu, (int)k, wmax, thr);
   RSX_LAUNCHED();
-  // RSX_TOPK_COLLECT (A/B): 1 (default) topk_bf16_collect_k max-first extraction; 2 its per-score
-  // form; 0 topk_bf16_scan_k<G, 8, 1> (round 3's full scan)
+  // RSX_TOPK_COLLECT (A/B): 2 (default) topk_bf16_collect_k, per-score appends behind the max gate;
+  // 1 its max-first extraction; 0 topk_bf16_scan_k<G, 8, 1> (round 3's full scan)
   static const int collect_k = [] {
     const char* e = getenv("RSX_TOPK_COLLECT");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 2;
   }();
-  if (collect_k == 2) {
-    if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_collect_k<2, false>), grid, dim3(256), 0, st, b);
-    else hipLaunchKernelGGL((topk_bf16_collect_k<1, false>), grid, dim3(256), 0, st, b);
+  if (collect_k == 1) {
+    if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_collect_k<2, true>), grid, dim3(256), 0, st, b);
+    else hipLaunchKernelGGL((topk_bf16_collect_k<1, true>), grid, dim3(256), 0, st, b);
   } else if (collect_k == 0) {
     if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_scan_k<2, 8, 1>), grid, dim3(256), 0, st, b);
     else hipLaunchKernelGGL((topk_bf16_scan_k<1, 8, 1>), grid, dim3(256), 0, st, b);
   } else {
-    if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_collect_k<2, true>), grid, dim3(256), 0, st, b);
-    else hipLaunchKernelGGL((topk_bf16_collect_k<1, true>), grid, dim3(256), 0, st, b);
+    if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_collect_k<2, false>), grid, dim3(256), 0, st, b);
+    else hipLaunchKernelGGL((topk_bf16_collect_k<1, false>), grid, dim3(256), 0, st, b);
   }
   RSX_LAUNCHED();
   hipLaunchKernelGGL(topk_bf16_select_k, dim3((unsigned)Q), dim3(256), 0, st, b.buf_e, b.buf_n,
