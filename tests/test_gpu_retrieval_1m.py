@@ -122,3 +122,26 @@ def test_retrieval_cached_corpus_follows_updates(gpu):
         elif step == 1:
             I = I.flip(0).contiguous()           # a new tensor
     assert ops._TOPK_CORPUS[gpu]["key"].matches([I])
+
+
+def test_retrieval_all_tied_margin_set(gpu):
+    """Every collected entry of a query ties exactly (300 scattered exact copies of the query in a
+    100k-item dyadic corpus whose other rows score far lower, k = 20): the select kernel's radix
+    select sees one key value (its early exit) and its rank sort orders the whole margin set by
+    index alone. Top-k = the 20 lowest copy positions, score u.u, as the float64 oracle gives."""
+    n_items, q, k = 100_000, 64, 20
+    g = torch.Generator().manual_seed(77)
+    U = torch.randint(-4, 5, (q, 128), generator=g).float() / 8.0
+    I = torch.randint(-4, 5, (n_items, 128), generator=g).float() / 512.0
+    pos = torch.stack([torch.randperm(n_items, generator=g)[:300] for _ in range(q)])
+    for r in range(q):
+        I[pos[r]] = U[r]
+    diag = {}
+    s, i = ops.retrieve_topk(U.to(gpu), I.to(gpu), k, diag=diag)
+    assert diag["path"] == "bf16" and diag["fallback_queries"] == 0
+    rs, ri = OR.retrieve_topk_chunked(U, I, k, dtype=torch.float64)
+    assert torch.equal(i.cpu(), ri) and torch.equal(s.cpu().double(), rs)
+    # the copies of query r that no later query overwrote, lowest positions first
+    want = torch.stack([(I == U[r]).all(dim=1).nonzero().flatten()[:k] for r in range(q)])
+    assert torch.equal(i.cpu(), want)
+    assert (s.cpu() == (U * U).sum(dim=1, keepdim=True)).all()
