@@ -158,7 +158,10 @@ def ensure_device(t: torch.Tensor) -> None:
 
 
 def stream() -> int:
-    return torch.cuda.current_stream().cuda_stream
+    """The current HIP stream of the current device, as a raw pointer. The raw query skips the
+    torch.cuda.Stream object that current_stream() builds per call (~33 native calls per train
+    step: 0.3 ms of host time per step in the unloaded-step profile)."""
+    return torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice())
 
 
 def ptr(t) -> int | None:
