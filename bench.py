@@ -287,12 +287,15 @@ def cpu_baseline_deepfm(args, st, x):
             "seconds_per_call": round(dt, 4)}
 
 
-def cpu_baseline_retrieve_rerank(args, st, Qs=512, K=100, F=39, chunk=250_000):
-    """configs[4] on the host, one rank's worth (the whole 1M corpus): the reference arithmetic
-    scores = user @ items.T in fp32 + torch.topk(100) (v1_usertower_train.py:672-675,
-    ranker_skelet.py:193-196; items in 250k-row chunks, per-chunk top-100 merged) + the same
-    hashed rerank ids + oracle DeepFM + top-10, for the first Qs of the GPU line's 4,096 queries
-    (same seed-5 corpus and users). queries/s."""
+def cpu_baseline_retrieve_rerank(args, st, gpu_out, Qs=512, K=100, F=39, chunk=250_000):
+    """configs[4] on the host, one rank's worth (the whole 1M corpus): oracle/ranker.py
+    retrieve_rerank -- the reference arithmetic scores = user @ items.T in fp32 + torch.topk(100)
+    (v1_usertower_train.py:672-675, ranker_skelet.py:193-196; items in 250k-row chunks, per-chunk
+    top-100 merged) + the same hashed rerank ids + oracle DeepFM + top-10 -- for the first Qs of the
+    GPU line's 4,096 queries (same seed-5 corpus and users). queries/s. The timed call's output is
+    then checked against the GPU line's own output for those queries (oracle.ranker.compare_rerank:
+    candidate sets, final ids up to ranker near-ties, final scores within 1e-5)."""
+    from oracle import ranker as ORK
     threads, info, rule = cpu_threads(args)
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
@@ -300,33 +303,27 @@ def cpu_baseline_retrieve_rerank(args, st, Qs=512, K=100, F=39, chunk=250_000):
     g = torch.Generator(device="cpu").manual_seed(5)
     corpus = torch.nn.functional.normalize(torch.randn(I, 128, generator=g), dim=1)
     users = torch.nn.functional.normalize(torch.randn(4096, 128, generator=g), dim=1)[:Qs].contiguous()
-    fld = torch.arange(F, dtype=torch.int64).view(1, 1, F)
-    ubucket = (torch.arange(Qs, dtype=torch.int64) % 1000).view(Qs, 1, 1)
+    bucket = torch.arange(Qs, dtype=torch.int64) % 1000
+    res = {}
 
     def step():
-        bs = bi = None
-        for c0 in range(0, I, chunk):
-            sc = users @ corpus[c0:c0 + chunk].T
-            s, i = torch.topk(sc, K, dim=1)
-            i = i + c0
-            if bs is not None:
-                s, j = torch.topk(torch.cat([bs, s], 1), K, dim=1)
-                i = torch.gather(torch.cat([bi, i], 1), 1, j)
-            bs, bi = s, i
-        h = bi.unsqueeze(-1) * 0x9E3779B1 + ubucket * 0x85EBCA77 + fld * 0xC2B2AE35
-        feats = ((h ^ (h >> 29)) & 0x7FFFFFFF) % V
-        _, prob = _deepfm_cpu(st, feats.view(Qs * K, F))
-        top_p, top_j = torch.topk(prob.view(Qs, K), 10, dim=1)
-        return torch.gather(bi, 1, top_j), top_p
+        res["out"] = ORK.retrieve_rerank(users, corpus, st, [V] * F, k=K, final_k=10, user_bucket=bucket,
+                                         chunk=chunk)
 
     with torch.no_grad(), _Heartbeat("cpu_baseline retrieve->rerank"):
         dt, n = cpu_timed(step)
     torch.set_num_threads(prev)
+    _, ci, p_all, top_ref, _ = res["out"]
+    ids, p, cand = (t[:Qs].cpu() for t in gpu_out)
+    check = ORK.compare_rerank(ids, p, cand, ci, top_ref, p_all, p_tol=1e-5)
+    assert check["same_candidate_set"] >= int(0.95 * Qs), check
     return {"value": round(Qs / dt, 1), "unit": "queries/s", "cores": threads, "kind": "port", "threads_rule": rule,
-            "sample": (f"fp32 matmul + torch.topk({K}) over the {I}-item corpus ({chunk}-item chunks, merged) + hashed "
-                       f"rerank ids + oracle/deepfm.py on {Qs}x{K} rows + top-10, for the first {Qs} of the GPU "
-                       f"line's 4,096 queries (same corpus and users); median of {n} calls after 2 warm-up calls"),
-            "seconds_per_call": round(dt, 4)}
+            "sample": (f"oracle/ranker.py retrieve_rerank: fp32 matmul + torch.topk({K}) over the {I}-item corpus "
+                       f"({chunk}-item chunks, merged) + hashed rerank ids + oracle/deepfm.py on {Qs}x{K} rows + "
+                       f"top-10, for the first {Qs} of the GPU line's 4,096 queries (same corpus and users); median "
+                       f"of {n} calls after 2 warm-up calls"),
+            "seconds_per_call": round(dt, 4),
+            "agreement_with_gpu": check}
 
 
 def cpu_baseline_item_tower(args, gpu_model, inputs):
@@ -470,18 +467,21 @@ def bench_gather_1m(device, T=316_372, rows=1_000_000, iters=10, flush_mb=1024):
 
 def bench_retrieve_rerank(args, device, deepfm, rank=0, world=1):
     """BASELINE configs[4]: Q=4096 normalised user vectors against a 1M-item normalised corpus
-    (seed 5), top-100 by rsx_retrieve_topk, 39 hashed (user bucket, item) sparse ids per
-    candidate, DeepFM on the Q x 100 rows, final top-10 per query by probability. queries/s; the
-    retrieval kernel priced at the fp32 MFMA peak.
+    (seed 5), ReRankingSystem.recommend_batch: top-100 by rsx_retrieve_topk, 39 hashed (user
+    bucket, item) sparse ids per candidate (hashed_cross_features), DeepFM on the Q x 100 rows,
+    final top-10 per query by probability. queries/s; the retrieval op priced at the dense bf16
+    MFMA peak.
 
     world > 1: the corpus is sharded by item range (I/N rows per rank); every rank
     scores all Q queries against its shard, the [Q, 100] (score, global index) lists are
     all-gathered over RCCL and merged by (score desc, index asc) (dist.retrieve_topk_sharded);
-    the DeepFM rerank is sharded by query (rank r reranks queries [r Q/N, (r+1) Q/N)). The step
-    time is the max over ranks; value = Q / that time."""
+    the DeepFM rerank is sharded by query (rank r reranks queries [r Q/N, (r+1) Q/N),
+    ReRankingSystem.rerank_batch). The step time is the max over ranks; value = Q / that time.
+    Returns (line, (final ids, final scores, candidates) of this rank's queries)."""
     from recsys_amd import dist as D
     from recsys_amd import ops
-    Q, I, K, F = 4096, args.corpus, 100, 39
+    from recsys_amd.temp_model.ranker_skelet import ReRankingSystem
+    Q, I, K = 4096, args.corpus, 100
     g = torch.Generator(device="cpu").manual_seed(5)
     corpus_full = torch.nn.functional.normalize(torch.randn(I, 128, generator=g), dim=1)
     users = torch.nn.functional.normalize(torch.randn(Q, 128, generator=g), dim=1).to(device)
@@ -489,21 +489,17 @@ def bench_retrieve_rerank(args, device, deepfm, rank=0, world=1):
     corpus = corpus_full[lo:hi].to(device)
     del corpus_full
     q0, q1 = rank * Q // world, (rank + 1) * Q // world
-    V = args.deepfm_vocab
-    fld = torch.arange(F, device=device, dtype=torch.int64).view(1, 1, F)
-    ubucket = (torch.arange(q0, q1, device=device, dtype=torch.int64) % 1000).view(q1 - q0, 1, 1)
+    system = ReRankingSystem(None, None, deepfm, {}, corpus)
+    buckets = torch.arange(q0, q1, device=device, dtype=torch.int64) % 1000
+    last = {}
 
     def step():
         if world > 1:
             sc, idx = D.retrieve_topk_sharded(users, corpus, lo, K)
-        else:
-            sc, idx = ops.retrieve_topk(users, corpus, K)
-        idx = idx[q0:q1]
-        h = idx.unsqueeze(-1) * 0x9E3779B1 + ubucket * 0x85EBCA77 + fld * 0xC2B2AE35
-        feats = ((h ^ (h >> 29)) & 0x7FFFFFFF) % V
-        _, prob = deepfm.forward_logits(feats.view((q1 - q0) * K, F))
-        top_p, top_j = torch.topk(prob.view(q1 - q0, K), 10, dim=1)
-        return torch.gather(idx, 1, top_j), top_p
+            last["cand"] = idx[q0:q1]
+            return system.rerank_batch(idx[q0:q1], sc[q0:q1], buckets, final_k=10)
+        out = system.recommend_batch(users, buckets, top_k_retrieval=K, final_k=10)
+        return out
 
     for _ in range(2):
         step()
@@ -514,7 +510,7 @@ def bench_retrieve_rerank(args, device, deepfm, rank=0, world=1):
     ops.timing_start()
     t0 = time.perf_counter()
     for _ in range(iters):
-        step()
+        out = step()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -523,30 +519,34 @@ def bench_retrieve_rerank(args, device, deepfm, rank=0, world=1):
         D.all_reduce_(el, op=torch.distributed.ReduceOp.MAX)
     dt = float(el.item()) / iters
     kt = ops.timing_stop()
+    cand = last.get("cand")
+    if cand is None:   # one rank: the candidates recommend_batch reranked (same deterministic call)
+        cand = ops.retrieve_topk(users, corpus, K)[1]
     n, ms = kt.get("retrieve_topk", (1, 0.0))
     rs = ms / 1e3 / max(n, 1)
     flops = 2.0 * Q * (hi - lo) * 128  # algorithmic (one score per (query, item) of this rank's shard)
-    out = {"metric": "retrieve->rerank queries/sec (1M-item corpus, top-100, DeepFM rerank, top-10)",
-           "value": round(Q / dt, 1), "unit": "queries/s", "queries": Q, "corpus": I, "n_gpus": world,
-           "ms_per_batch": round(dt * 1e3, 3), "rerank_rows_per_s": round(Q * K / dt, 1),
-           "data": "synthetic normalised N(0,1) corpus / users, hashed rerank ids",
-           "retrieval": {"kernel": "rsx_retrieve_topk: topk_bf16_prep_k (corpus bf16 image, cached across calls) + "
-                                   "topk_bf16_scan_k (strided sample, best per lane stream) + topk_bf16_thresh_k "
-                                   "(per-query threshold) + topk_bf16_collect_k (the one full scan: bf16 MFMA "
-                                   "scores, max-gated appends) + topk_bf16_select_k (margin set rescored exactly "
-                                   "in fp32, exactness check)",
-                         "avg_ms": round(rs * 1e3, 4), "items_per_rank": hi - lo,
-                         "achieved_TFLOPs": round(flops / rs / 1e12, 2),
-                         "peak_TFLOPs": round(BF16_MFMA_PEAK_TFLOPS, 1),
-                         "frac": round(flops / rs / 1e12 / BF16_MFMA_PEAK_TFLOPS, 4),
-                         "peak_note": "2 Q I 128 algorithmic FLOPs over the whole op, priced at the dense bf16 "
-                                      "MFMA peak (the scan's arithmetic); fp32-MFMA peak 157.3 TF for reference",
-                         "corpus_hbm_bytes": int((hi - lo) * 128 * (4 + 2 + 2))}}
+    line = {"metric": "retrieve->rerank queries/sec (1M-item corpus, top-100, DeepFM rerank, top-10)",
+            "value": round(Q / dt, 1), "unit": "queries/s", "queries": Q, "corpus": I, "n_gpus": world,
+            "ms_per_batch": round(dt * 1e3, 3), "rerank_rows_per_s": round(Q * K / dt, 1),
+            "data": "synthetic normalised N(0,1) corpus / users, hashed rerank ids",
+            "pipeline": "ReRankingSystem.recommend_batch (temp_model/ranker_skelet.py)",
+            "retrieval": {"kernel": "rsx_retrieve_topk: topk_bf16_prep_k (corpus bf16 image, cached across calls) + "
+                                    "topk_bf16_scan_k (strided sample, best per lane stream) + topk_bf16_thresh_k "
+                                    "(per-query threshold) + topk_bf16_collect_k (the one full scan: bf16 MFMA "
+                                    "scores, max-gated appends) + topk_bf16_select_k (margin set rescored exactly "
+                                    "in fp32, exactness check)",
+                          "avg_ms": round(rs * 1e3, 4), "items_per_rank": hi - lo,
+                          "achieved_TFLOPs": round(flops / rs / 1e12, 2),
+                          "peak_TFLOPs": round(BF16_MFMA_PEAK_TFLOPS, 1),
+                          "frac": round(flops / rs / 1e12 / BF16_MFMA_PEAK_TFLOPS, 4),
+                          "peak_note": "2 Q I 128 algorithmic FLOPs over the whole op, priced at the dense bf16 "
+                                       "MFMA peak (the scan's arithmetic); fp32-MFMA peak 157.3 TF for reference",
+                          "corpus_hbm_bytes": int((hi - lo) * 128 * (4 + 2 + 2))}}
     if world > 1:
-        out["sharding"] = (f"corpus by item range ({hi - lo} rows on rank {rank}), per-rank top-{K} with global "
-                           f"indices all-gathered over RCCL and merged (score desc, index asc); DeepFM by query "
-                           f"({q1 - q0} queries x {K} rows per rank)")
-    return out
+        line["sharding"] = (f"corpus by item range ({hi - lo} rows on rank {rank}), per-rank top-{K} with global "
+                            f"indices all-gathered over RCCL and merged (score desc, index asc); DeepFM by query "
+                            f"({q1 - q0} queries x {K} rows per rank)")
+    return line, (out[0], out[2], cand)
 
 
 def bench_dcn(args, device):
@@ -682,6 +682,41 @@ def bench_item_tower(args, device):
             "value": round(B / dt, 1), "unit": "items/s", "ms_per_batch": round(dt * 1e3, 3),
             "data": "synthetic std/RE/text ids (SURVEY.md 8d config 1), random BERT weights"}, \
         (model, [std, re_ids, re_mask, txt, txt_mask])
+
+
+def bench_eval_forward(args, device, model, items, users=4096, iters=10):
+    """evaluate_model's tower pass (tower_code/v1_usertower_train.py:548-711 on the GPU:
+    SASRecUserTower forward in eval mode, training_mode=False -> the last position's [B, D]
+    vector, F.normalize), at 4,096 users of the synthetic H&M-shaped batch, pretrained rows
+    gathered on the device. users/s; the model's weights are the headline run's."""
+    from recsys_amd import ops, synth
+    from recsys_amd.tower_code import v1_usertower_train as TT
+    batch = {k: (v.to(device) if torch.is_tensor(v) else v)
+             for k, v in synth.make_batch(items, users, seed=args.seed + 300).items()}
+    lookup = items.pretrained.to(device)
+    kw = {k: batch[k] for k in TT._SEQ_ID_KEYS + TT._STATIC_KEYS}
+    was = model.training
+    model.eval()
+
+    def step():
+        pv = TT.lookup_pretrained(lookup, batch["item_ids"])
+        out = model(pretrained_vecs=pv, padding_mask=batch["padding_mask"], training_mode=False, **kw)
+        return ops.l2_normalize(out)
+
+    with torch.no_grad():
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            step()
+        torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / iters
+    model.train(was)
+    return {"metric": "evaluate_model tower pass users/sec (SASRecUserTower eval forward, last position, "
+                      "4096 users x 50 steps)",
+            "value": round(users / dt, 1), "unit": "users/s", "ms_per_batch": round(dt * 1e3, 4),
+            "data": "synthetic H&M-shaped batch (dense [B, 50] layout, left-padded), headline weights"}
 
 
 def train_bench(args, global_batch, steps, warmup, items, cfg, model, item_tower, opt, bucket, rank, world,
@@ -928,7 +963,11 @@ def main():
         "value": round(args.batch * args.steps / tb["elapsed"], 2),
         "unit": "pairs/s",
         "n_gpus": world,
-        "rccl_world_size": (torch.distributed.get_world_size() if world > 1 else 1),
+        "world_size": (torch.distributed.get_world_size() if world > 1 else 1),
+        "collective_backend": (torch.distributed.get_backend() if world > 1 else None),
+        "transport": (None if world == 1 else
+                      ("RCCL over xGMI" if torch.distributed.get_backend() == "nccl"
+                       else f"{torch.distributed.get_backend()} (host-staged; a rehearsal, not an RCCL run)")),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(1e3 * tb["elapsed"] / args.steps, 3),
@@ -1017,6 +1056,7 @@ def main():
         if world == 1:
             result["secondary_batch32768"] = line
     if rank == 0 and world == 1:
+        result["secondary_eval_forward"] = bench_eval_forward(args, device, model, items)
         result["secondary_gather_1m"] = bench_gather_1m(device)
         torch.cuda.empty_cache()
     cpu_lines = rank == 0 and world == 1 and not args.no_cpu_baseline
@@ -1024,7 +1064,7 @@ def main():
         torch.cuda.empty_cache()
         deepfm, result["secondary"], dfm_x = bench_deepfm(args, device)
         if not args.no_rerank:
-            result["secondary_retrieve_rerank"] = bench_retrieve_rerank(args, device, deepfm)
+            result["secondary_retrieve_rerank"], rr_out = bench_retrieve_rerank(args, device, deepfm)
             result["secondary_dcn_rerank"] = bench_dcn(args, device)
         if cpu_lines:
             dst = deepfm_cpu_state(deepfm)
@@ -1033,7 +1073,7 @@ def main():
             line["gpu_over_cpu"] = round(line["value"] / line["cpu_baseline"]["value"], 1)
             if not args.no_rerank:
                 line = result["secondary_retrieve_rerank"]
-                line["cpu_baseline"] = cpu_baseline_retrieve_rerank(args, dst)
+                line["cpu_baseline"] = cpu_baseline_retrieve_rerank(args, dst, rr_out)
                 line["gpu_over_cpu"] = round(line["value"] / line["cpu_baseline"]["value"], 1)
             del dst
         del deepfm, dfm_x
@@ -1044,7 +1084,7 @@ def main():
         torch.cuda.empty_cache()
         torch.manual_seed(args.seed + 3)       # the replicated reranker: identical on every rank
         deepfm = DeepFM([args.deepfm_vocab] * 39, device=device)
-        result["retrieve_rerank_sharded"] = bench_retrieve_rerank(args, device, deepfm, rank, world)
+        result["retrieve_rerank_sharded"], _ = bench_retrieve_rerank(args, device, deepfm, rank, world)
         del deepfm
         torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_item_tower:

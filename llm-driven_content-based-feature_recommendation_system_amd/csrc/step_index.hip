@@ -111,7 +111,15 @@ __global__ __launch_bounds__(256) void si_tloc_k(const uint8_t* pm, const int64_
   if (b >= B) return;
   const User u = user_sel(pm, b, L, lane);
   if (u.valid) tloc[offN[b] + below(u.vm, lane)] = checked(tgt[b * L + lane], n_items, err);
-  if (b == B - 1 && lane == 0) tloc[B * L] = offN[B];
+}
+
+// The block's row-count slot, with this rank's id-range error in bit 30 (written after every
+// range check of the count phase): at world > 1 the slots are all-gathered with the targets, so
+// every rank's totals see every rank's error and all of them raise together (no rank carries on
+// into the step's collectives alone).
+constexpr int kSlotErr = 1 << 30;
+__global__ void si_slot_k(const int* offN, const int* err, int64_t B, int64_t L, int* tloc) {
+  if (threadIdx.x == 0) tloc[B * L] = offN[B] | (*err ? kSlotErr : 0);
 }
 
 __global__ __launch_bounds__(256) void si_colhist_k(const int* tglob, int64_t n, int64_t blk, int64_t n_items,
@@ -194,9 +202,14 @@ __global__ void si_totals_k(const int* offT, const int* offN, const int* offE, c
   tot[3] = offE[B];
   tot[4] = itemidx[n_items];
   tot[5] = chunkoff[n_items];
-  tot[6] = *err;
+  int e = *err ? 1 : 0;
   tot[7] = 0;
-  for (int r = 0; r < world; ++r) tot[8 + r] = tglob[(int64_t)r * (B * L + 1) + B * L];
+  for (int r = 0; r < world; ++r) {
+    const int v = tglob[(int64_t)r * (B * L + 1) + B * L];
+    e |= (v & kSlotErr) ? 1 : 0;
+    tot[8 + r] = v & ~kSlotErr;
+  }
+  tot[6] = e;
 }
 
 struct FillOut {
@@ -450,7 +463,7 @@ RSX_API int rsx_step_index_count(const uint8_t* pm, const int64_t* tgt, const in
                                  int64_t n_items, void* ws, int64_t ws_bytes, int* tloc, void* stream) {
   RSX_ARG(pm && tgt && item && ws && tloc, "null tensor");
   RSX_ARG(B >= 1 && L >= 1 && L <= 64, "need B >= 1 and 1 <= L <= 64 (one wave per user)");
-  RSX_ARG(n_items >= 1 && n_items < INT_MAX && B * L < INT_MAX, "sizes must fit int32");
+  RSX_ARG(n_items >= 1 && n_items < INT_MAX && B * L < (1 << 30), "sizes must fit int32 (B * L < 2^30)");
   const SiLayout l = si_layout(B, L, n_items);
   RSX_ARG(ws_bytes >= l.total, "workspace too small (rsx_step_index_workspace_bytes)");
   hipStream_t st = (hipStream_t)stream;
@@ -474,6 +487,8 @@ RSX_API int rsx_step_index_count(const uint8_t* pm, const int64_t* tgt, const in
   }
   hipLaunchKernelGGL(si_tloc_k, dim3(gu), dim3(256), 0, st, pm, tgt, B, (int)L, n_items, at<int>(ws, l.offN), tloc,
                      at<int>(ws, l.err));
+  RSX_LAUNCHED();
+  hipLaunchKernelGGL(si_slot_k, dim3(1), dim3(64), 0, st, at<int>(ws, l.offN), at<int>(ws, l.err), B, L, tloc);
   RSX_LAUNCHED();
   return 0;
 }

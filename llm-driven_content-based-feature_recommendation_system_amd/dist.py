@@ -386,6 +386,17 @@ def _prepare_step_index_device(batch, pretrained_vecs, pretrained_lookup, n_item
     return ix
 
 
+def _device_lookup_ok(pretrained_vecs, lookup, device) -> bool:
+    """The device builder gathers the pretrained rows itself (si_pv_k: fp32 rows of exactly 128
+    columns, read through a device pointer, no autograd). Any other lookup -- on the host, of
+    another dtype or width, or one that requires grad -- takes the torch builders, whose
+    ops.gather_rows handles those (and carries the gradient)."""
+    if pretrained_vecs is not None:
+        return True
+    return (lookup is not None and lookup.device == device and lookup.dtype == torch.float32 and lookup.dim() == 2
+            and lookup.shape[1] == 128 and lookup.stride(1) == 1 and not lookup.requires_grad)
+
+
 def prepare_step_index(batch, pretrained_vecs=None, pretrained_lookup=None, n_items=None) -> StepIndex:
     """Builds the StepIndex of `batch` on the current stream. Device batches (L <= 64) use
     rsx_step_index_* (one host read: the totals); otherwise, or with RSX_DEVICE_INDEX=0, the torch
@@ -396,7 +407,8 @@ def prepare_step_index(batch, pretrained_vecs=None, pretrained_lookup=None, n_it
     if n_items is None and pretrained_lookup is not None:
         n_items = pretrained_lookup.shape[0]
     if (_DEVICE_INDEX and n_items is not None and batch["item_ids"].is_cuda
-            and batch["padding_mask"].shape[1] <= 64):
+            and batch["padding_mask"].shape[1] <= 64 and _device_lookup_ok(pretrained_vecs, pretrained_lookup,
+                                                                          batch["item_ids"].device)):
         return _prepare_step_index_device(batch, pretrained_vecs, pretrained_lookup, int(n_items))
     rank, ws = world()
     device = batch["item_ids"].device

@@ -332,6 +332,9 @@ def simcse_train_step(model, inputs_v1, inputs_v2, optimizer, temperature: float
     emb2 = model(*inputs_v2)
     loss = simcse_loss(emb1, emb2, temperature)
     loss.backward()
+    enc = getattr(model, "encoder", model)
+    if hasattr(enc, "check_inputs"):
+        enc.check_inputs()   # out-of-range STD ids raise before the update, not after it
     optimizer.step()
     if scheduler is not None:
         scheduler.step()
@@ -402,8 +405,6 @@ def train_simcse_from_db(encoder: nn.Module, projector: nn.Module, db_session, b
                 align, uni = calculate_metrics(e1, e2)
                 print(f"epoch {epoch + 1} step {step} loss {loss.item():.4f} align {align:.4f} uni {uni:.4f}")
             total += float(loss.item())
-            if hasattr(encoder, "check_inputs"):
-                encoder.check_inputs()          # after the step's own sync: STD id range errors
             step += 1
         avg = total / step if step else float("nan")
         history.append(avg)

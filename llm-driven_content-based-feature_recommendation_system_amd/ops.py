@@ -405,7 +405,12 @@ class _GatherRows(torch.autograd.Function):
 
 
 def gather_rows(src, idx=None, normalize=False, eps=1e-12, unique=False, skip_idx=-1):
-    """out[r] = src.view(-1, D)[idx[r]] (idx None => all rows), optionally L2-normalised."""
+    """out[r] = src.view(-1, D)[idx[r]] (idx None => all rows), optionally L2-normalised. The kernel
+    reads fp32 rows: another floating dtype is cast first (autograd-aware), anything else refused."""
+    if src.dtype != torch.float32:
+        if not src.is_floating_point():
+            raise TypeError(f"gather_rows: floating-point rows expected, got {src.dtype}")
+        src = src.float()
     return _GatherRows.apply(src, idx, bool(normalize), float(eps), bool(unique), int(skip_idx))
 
 
@@ -1463,6 +1468,9 @@ def _topk_corpus(it):
         cur = torch.cuda.current_stream(dev)
         if cur != st["stream"]:
             cur.wait_event(st["event"])
+            # the image is read on this stream too: its block must not return to the building
+            # stream's pool (when the cache entry is replaced) before this stream's reads finish
+            st["buf"].record_stream(cur)
         return st["buf"]
     NI = it.shape[0]
     buf = torch.empty(N.lib().rsx_topk_corpus_bytes(NI), device=dev, dtype=torch.uint8)
@@ -1474,6 +1482,15 @@ def _topk_corpus(it):
     _TOPK_CORPUS[dev] = {"key": _FastKey([it]), "buf": buf, "event": ev,
                          "stream": torch.cuda.current_stream(dev)}
     return buf
+
+
+def clear_retrieval_cache(device=None) -> None:
+    """Drop the cached bf16 corpus image(s) (and the references to their corpora): about
+    0.75 GB at 1M items. The next retrieval over a corpus rebuilds its image."""
+    if device is None:
+        _TOPK_CORPUS.clear()
+    else:
+        _TOPK_CORPUS.pop(torch.device(device), None)
 
 
 def retrieve_topk(queries, items, k, diag=None):

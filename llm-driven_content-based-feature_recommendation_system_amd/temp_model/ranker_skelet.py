@@ -147,6 +147,22 @@ class RecommendationRanker:
         return self.model.predict_proba(X)[:, 1]
 
 
+_HASH_ITEM, _HASH_USER, _HASH_FIELD = 0x9E3779B1, 0x85EBCA77, 0xC2B2AE35
+
+
+def hashed_cross_features(user_bucket: torch.Tensor, cand_ids: torch.Tensor, vocab_sizes) -> torch.Tensor:
+    """Sparse DeepFM rerank ids for (user, candidate) pairs ("39 sparse ids
+    per (user, item) derived by hashing (user_bucket, item_id) pairs"): field f of pair (q, j) is
+    mix(item * A + bucket[q] * B + f * C) % vocab_f with mix(h) = (h ^ (h >> 29)) & 0x7FFFFFFF.
+    user_bucket [Q] int64, cand_ids [Q, K] int64 -> [Q, K, F] int64."""
+    F = len(vocab_sizes)
+    dev = cand_ids.device
+    fld = torch.arange(F, device=dev, dtype=torch.int64).view(1, 1, F)
+    h = cand_ids.unsqueeze(-1) * _HASH_ITEM + user_bucket.view(-1, 1, 1) * _HASH_USER + fld * _HASH_FIELD
+    voc = torch.as_tensor(list(vocab_sizes), dtype=torch.int64, device=dev).view(1, 1, F)
+    return ((h ^ (h >> 29)) & 0x7FFFFFFF) % voc
+
+
 class ReRankingSystem:
     """Reference :155-237: retrieval (user_vec @ item_vectors.T, top-k) then rerank.
 
@@ -183,6 +199,41 @@ class ReRankingSystem:
         sc_cpu = top_scores[0].cpu().numpy()
         return [{"product_id": int(idx_cpu[o]), "two_tower_score": float(sc_cpu[o]), "final_score": float(probs[o])}
                 for o in order]
+
+    def rerank_batch(self, cand_ids: torch.Tensor, cand_scores: torch.Tensor, user_buckets: torch.Tensor,
+                     final_k: int = 10, features=None):
+        """The DeepFM half of recommend for a batch of queries, on the device: candidates [Q, K]
+        (global item ids) -> rerank ids (features(cand_ids, user_buckets) -> [Q, K, F]; default the
+        hashed (user bucket, item) crosses of hashed_cross_features) -> DeepFM probabilities -> the
+        final_k most probable per query (torch.topk: probability desc). Returns (product ids,
+        two-tower scores, final scores), each [Q, final_k]."""
+        if not isinstance(self.ranker, DeepFM):
+            raise TypeError("rerank_batch needs a DeepFM ranker (the CatBoost path is per-user, recommend)")
+        Q, K = cand_ids.shape
+        if features is not None:
+            feats = features(cand_ids, user_buckets)
+        else:
+            voc = self.__dict__.get("_vocab")
+            if voc is None:
+                voc = self.__dict__["_vocab"] = [self.ranker.embedding_dict[n].num_embeddings
+                                                 for n in self.ranker.field_names]
+            feats = hashed_cross_features(user_buckets, cand_ids, voc)
+        _, prob = self.ranker.forward_logits(feats.reshape(Q * K, -1))
+        top_p, top_j = torch.topk(prob.view(Q, K), final_k, dim=1)
+        return torch.gather(cand_ids, 1, top_j), torch.gather(cand_scores, 1, top_j), top_p
+
+    def recommend_batch(self, user_vectors: torch.Tensor, user_buckets: torch.Tensor = None,
+                        top_k_retrieval: int = 100, final_k: int = 10):
+        """recommend (reference :170-237) for a batch of users with a DeepFM ranker, entirely on the
+        device: exact top-k retrieval of user_vectors [Q, D] against the item vectors
+        (rsx_retrieve_topk), then rerank_batch. user_buckets [Q] int64 (default: q % 1000).
+        Returns (product ids, two-tower scores, final scores), each [Q, final_k]."""
+        uv = user_vectors.to(self.device, torch.float32)
+        Q = uv.shape[0]
+        if user_buckets is None:
+            user_buckets = torch.arange(Q, device=self.device, dtype=torch.int64) % 1000
+        sc, idx = ops.retrieve_topk(uv, self.item_vectors, top_k_retrieval)
+        return self.rerank_batch(idx, sc, user_buckets, final_k)
 
 
 class CrossNet(nn.Module):

@@ -1,14 +1,20 @@
-"""Drop-in for tower_code/v1_refine_usertower.py: SASRecUserTower and its losses.
+"""Drop-in for tower_code/v1_refine_usertower.py: SASRecUserTower, its input producer
+(FeatureProcessor, SASRecDataset) and its losses.
 
 Same constructor arguments, parameter names/shapes/init (so state_dicts load both ways)
 and forward signature as the reference; the forward runs on the MI355X kernels of
 librecsys_amd.so:
   * embedding stage (gathers + gated sum + pos + LayerNorm + dropout): rsx_seq_embed_*
+  * token linears (item_proj, in/out_proj, FFN with GELU + dropout epilogues, static MLP,
+    output_proj): rsx_gemm_x3 (bf16x3 products, fp32 accumulation; out_proj fused with the
+    residual add + LayerNorm, output_proj[0]'s per-user profile half added in the epilogue),
+    weight gradients on the split-K rsx_linear_wgrad_x3
   * masked self-attention core of each encoder layer:                  rsx_mha_*
+  * LayerNorm (+ GELU):                                                 rsx_ln_*
   * final F.normalize:                                                  rsx_gather_rows
-  * losses (no N x N materialisation, fp32 MFMA):                       rsx_nce_*
-Dense projections (item_proj, in/out_proj, FFN, static MLP, output_proj) are plain GEMMs
-issued through torch (hipBLASLt).
+  * losses (no N x N materialisation; bf16x3 or fp32 MFMA products):   rsx_nce_*
+RSX_GEMM_PRECISION=fp32 / ops.set_gemm_precision("fp32") puts the token linears on exact fp32
+products (the library GEMM) instead.
 """
 from __future__ import annotations
 
@@ -33,20 +39,134 @@ def get_logq_probs(raw_probs, device="cpu"):
     return torch.tensor(full, dtype=torch.float32).to(device)
 
 
-class FeatureProcessor:
-    """The part of the reference FeatureProcessor (:40-140) the GPU path consumes: item
-    vocabulary (item2id, 1-based; 0 = padding) and get_logq_probs. The per-user/-item
-    feature tables it builds from pandas frames are host-side data preparation (out of
-    scope)."""
+def _frame(src):
+    """A parquet path (the reference's pd.read_parquet) or an in-memory DataFrame (copied)."""
+    import pandas as pd
+    return src.copy() if isinstance(src, pd.DataFrame) else pd.read_parquet(src)
 
-    def __init__(self, items_df, item_id_col="article_id"):
-        self.items = items_df.set_index(item_id_col) if item_id_col in items_df.columns else items_df
-        self.item_ids = list(self.items.index)
-        self.item2id = {iid: i + 1 for i, iid in enumerate(self.item_ids)}
+
+_U_BUCKET_COLS = ("age_bucket", "user_avg_price_bucket", "total_cnt_bucket", "recency_bucket")
+_U_CAT_COLS = ("preferred_channel", "club_member_status_idx", "fashion_news_frequency_idx", "FN", "Active")
+_U_CONT_COLS = ("price_std_scaled", "last_price_diff_scaled", "repurchase_ratio_scaled", "weekend_ratio_scaled")
+_I_SIDE_COLS = ("type_id", "color_id", "graphic_id", "section_id")
+
+
+class FeatureProcessor:
+    """Reference FeatureProcessor (:40-137): the user / item / sequence frames (parquet paths as
+    in the reference, or DataFrames), 1-based id maps (0 = padding; a validation processor
+    inherits the train item map through base_processor) and the dense lookup arrays
+    SASRecDataset indexes. The arrays are filled column-wise instead of by iterrows (same values:
+    every user of the frame is in user2id; item rows outside item2id are skipped, missing item
+    side columns give 0 as row.get(col, 0) does)."""
+
+    def __init__(self, user_path, item_path, seq_path, base_processor=None):
+        import numpy as np
+        users = _frame(user_path).drop_duplicates(subset=["customer_id"]).set_index("customer_id")
+        items = _frame(item_path).drop_duplicates(subset=["article_id"]).set_index("article_id")
+        seqs = _frame(seq_path).set_index("customer_id")
+        users.index = users.index.astype(str)
+        items.index = items.index.astype(str)
+        seqs.index = seqs.index.astype(str)
+        self.users, self.items, self.seqs = users, items, seqs
+        self.user_ids = seqs.index.tolist()
+        self.user2id = {uid: i + 1 for i, uid in enumerate(users.index)}
+        if base_processor is None:
+            self.item_ids = items.index.tolist()
+            self.item2id = {iid: i + 1 for i, iid in enumerate(self.item_ids)}
+        else:
+            self.item_ids = base_processor.item_ids
+            self.item2id = base_processor.item2id
         self.num_items = len(self.item_ids)
+
+        n_users = len(users) + 1
+        self.u_bucket_arr = np.zeros((n_users, 4), dtype=np.int64)
+        self.u_cat_arr = np.zeros((n_users, 5), dtype=np.int64)
+        self.u_cont_arr = np.zeros((n_users, 4), dtype=np.float32)
+        if len(users):
+            rows = np.fromiter((self.user2id[u] for u in users.index), dtype=np.int64, count=len(users))
+            self.u_bucket_arr[rows] = users[list(_U_BUCKET_COLS)].to_numpy(dtype=np.float64)
+            self.u_cat_arr[rows] = users[list(_U_CAT_COLS)].to_numpy(dtype=np.float64)
+            self.u_cont_arr[rows] = users[list(_U_CONT_COLS)].to_numpy(dtype=np.float64)
+        self.i_side_arr = np.zeros((self.num_items + 1, 4), dtype=np.int64)
+        known = [iid for iid in items.index if iid in self.item2id]
+        if known:
+            rows = np.array([self.item2id[iid] for iid in known], dtype=np.int64)
+            sub = items.loc[known]
+            for j, col in enumerate(_I_SIDE_COLS):
+                if col in sub.columns:
+                    self.i_side_arr[rows, j] = sub[col].to_numpy(dtype=np.float64)
 
     def get_logq_probs(self, device):
         return get_logq_probs(self.items["raw_probability"].reindex(self.item_ids).values, device)
+
+
+TIME_BUCKET_BINS = (0, 3, 7, 14, 30, 60, 180, 330, 395)
+
+
+class SASRecDataset(torch.utils.data.Dataset):
+    """Reference SASRecDataset (:194-306), the user-side input producer of the training step
+    (create_dataloaders, v1_usertower_train.py:162-184). processor: anything with user_ids,
+    user2id, item2id, seqs (customer_id-indexed, columns sequence_ids / sequence_deltas),
+    i_side_arr, u_bucket_arr, u_cat_arr, u_cont_arr (FeatureProcessor above).
+
+    One sample: the customer's item ids mapped through item2id (unknown -> 0), days-ago deltas
+    bucketed by np.digitize(delta, TIME_BUCKET_BINS) (1..9); train: the last max_len + 1
+    purchases, input = seq[:-1], target = seq[1:], input_time = buckets[:-1] (a single purchase
+    is its own target); eval: the last max_len inputs, target all 0. Left padding with 0,
+    padding_mask True on pads, side ids i_side_arr[input] (pad -> row 0), the user's static
+    rows through user2id (unknown user -> row 0)."""
+
+    def __init__(self, processor, max_len=30, is_train=True):
+        self.processor = processor
+        self.max_len = max_len
+        self.is_train = is_train
+        self.user_ids = processor.user_ids
+
+    def __len__(self):
+        return len(self.user_ids)
+
+    def __getitem__(self, idx):
+        import numpy as np
+        pr = self.processor
+        L = self.max_len
+        user_id = self.user_ids[idx]
+        u = pr.user2id.get(user_id, 0)
+        seq = [pr.item2id.get(item, 0) for item in pr.seqs.loc[user_id, "sequence_ids"]]
+        tb = np.digitize(pr.seqs.loc[user_id, "sequence_deltas"], np.array(TIME_BUCKET_BINS), right=False).tolist()
+        if self.is_train:
+            seq, tb = seq[-(L + 1):], tb[-(L + 1):]
+            if len(seq) > 1:
+                inp, tgt, tin = seq[:-1], seq[1:], tb[:-1]
+            else:
+                inp, tgt, tin = seq, seq, tb
+        else:
+            inp, tgt, tin = seq[-L:], [], tb[-L:]
+        pad = L - len(inp)
+        item = np.zeros(L, dtype=np.int64)
+        time_ = np.zeros(L, dtype=np.int64)
+        target = np.zeros(L, dtype=np.int64)
+        item[pad:] = inp
+        time_[pad:] = tin
+        if self.is_train:
+            target[pad:] = tgt
+        side = pr.i_side_arr[item]
+        mask = np.zeros(L, dtype=bool)
+        mask[:pad] = True
+        ub, uc, ucont = pr.u_bucket_arr[u], pr.u_cat_arr[u], pr.u_cont_arr[u]
+        long = torch.long
+        return {
+            "user_ids": user_id,
+            "item_ids": torch.from_numpy(item), "target_ids": torch.from_numpy(target),
+            "padding_mask": torch.from_numpy(mask), "time_bucket_ids": torch.from_numpy(time_),
+            "type_ids": torch.from_numpy(side[:, 0].copy()), "color_ids": torch.from_numpy(side[:, 1].copy()),
+            "graphic_ids": torch.from_numpy(side[:, 2].copy()), "section_ids": torch.from_numpy(side[:, 3].copy()),
+            "age_bucket": torch.tensor(ub[0], dtype=long), "price_bucket": torch.tensor(ub[1], dtype=long),
+            "cnt_bucket": torch.tensor(ub[2], dtype=long), "recency_bucket": torch.tensor(ub[3], dtype=long),
+            "channel_ids": torch.tensor(uc[0], dtype=long), "club_status_ids": torch.tensor(uc[1], dtype=long),
+            "news_freq_ids": torch.tensor(uc[2], dtype=long), "fn_ids": torch.tensor(uc[3], dtype=long),
+            "active_ids": torch.tensor(uc[4], dtype=long),
+            "cont_feats": torch.tensor(ucont, dtype=torch.float32),
+        }
 
 
 _ADDLN = os.environ.get("RSX_LINEAR_ADDLN", "1") != "0"
@@ -175,7 +295,7 @@ class SASRecUserTower(nn.Module):
         u_g = torch.sigmoid(self.static_gate)
 
         # Phase 1: sequence encoding (reference :447-466)
-        base = F.linear(pretrained_vecs, self.item_proj.weight, self.item_proj.bias)
+        base = ops.linear_tok(pretrained_vecs, self.item_proj.weight, self.item_proj.bias)
         x = ops.seq_embed(
             base,
             [item_ids, time_bucket_ids, type_ids, color_ids, graphic_ids, section_ids],
@@ -188,18 +308,22 @@ class SASRecUserTower(nn.Module):
         user_profile_vec = self._static_profile(age_bucket, price_bucket, cnt_bucket, recency_bucket, channel_ids,
                                                 club_status_ids, news_freq_ids, fn_ids, active_ids, cont_feats, u_g)
 
-        # Phase 3: late fusion (reference :499-510). Linear(cat[a, b]) = a W_a^T + (b W_b^T + bias):
-        # the per-user profile half is computed once per user and broadcast over L.
+        # Phase 3: late fusion (reference :499-510). Training mode: Linear(cat[token, profile[user]])
+        # over all B*L tokens as ops.profile_linear (the per-user profile half computed once per
+        # user and added in the token GEMM's epilogue, no broadcast tensor); eval mode: the last
+        # position only, one GEMM over cat(last, profile) [B, 2D].
         lin0, ln, lin3 = self.output_proj[0], self.output_proj[1], self.output_proj[3]
         D = self.d_model
-        w_seq, w_prof = lin0.weight[:, :D], lin0.weight[:, D:]
-        prof = F.linear(user_profile_vec, w_prof, lin0.bias)
         if training_mode:
-            h = F.linear(output, w_seq) + prof.unsqueeze(1)
+            dev = output.device
+            tok_user = torch.arange(B, device=dev).repeat_interleave(seq_len)
+            seg = torch.arange(0, B * seq_len + 1, seq_len, device=dev)
+            h = ops.profile_linear(output.reshape(B * seq_len, D), user_profile_vec, lin0.weight, lin0.bias,
+                                   tok_user, seg).view(B, seq_len, -1)
         else:
-            h = F.linear(output[:, -1, :], w_seq) + prof
+            h = ops.linear_tok(torch.cat([output[:, -1, :], user_profile_vec], dim=1), lin0.weight, lin0.bias)
         h = ops.layer_norm(h, ln.weight, ln.bias, ln.eps, act=ops.ACT_GELU_ERF)
-        final_vec = F.linear(h, lin3.weight, lin3.bias)
+        final_vec = ops.linear_tok(h, lin3.weight, lin3.bias)
         return ops.l2_normalize(final_vec)
 
     def _static_profile(self, age_bucket, price_bucket, cnt_bucket, recency_bucket, channel_ids, club_status_ids,

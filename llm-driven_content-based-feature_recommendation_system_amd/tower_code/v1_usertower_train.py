@@ -14,9 +14,9 @@ import torch
 import torch.nn as nn
 
 from .. import ops
-from .v1_refine_usertower import (PackedTokens, SASRecUserTower, duorec_loss_refined, full_batch_hard_emphasis_loss,  # noqa: F401
-                                  inbatch_corrected_logq_loss, inbatch_hnm_corrected_loss_with_stats,
-                                  inbatch_mixed_hnm_loss_with_stats)
+from .v1_refine_usertower import (FeatureProcessor, PackedTokens, SASRecDataset, SASRecUserTower,  # noqa: F401
+                                  duorec_loss_refined, full_batch_hard_emphasis_loss, inbatch_corrected_logq_loss,
+                                  inbatch_hnm_corrected_loss_with_stats, inbatch_mixed_hnm_loss_with_stats)
 
 try:  # the reference hard-imports wandb (v1_usertower_train.py:14); here it is optional
     import wandb  # type: ignore
@@ -348,6 +348,16 @@ def evaluate_model(model, item_tower, dataloader, target_df_path, device, proces
             res[f"Recall@{k}"] = hits[k] / n_users * 100
     print(f"[Validation Results] Valid Users: {n_users}")
     return res
+
+
+def create_dataloaders(processor, cfg: PipelineConfig, aligned_pretrained_vecs=None, is_train=True):
+    """Reference :162-184: SASRecDataset(processor, cfg.max_len, is_train) with the aligned
+    pretrained lookup attached (the step gathers its rows on the device), shuffled with
+    drop_last for training, in order with every user for validation."""
+    dataset = SASRecDataset(processor, max_len=cfg.max_len, is_train=is_train)
+    dataset.pretrained_lookup = aligned_pretrained_vecs
+    return torch.utils.data.DataLoader(dataset, batch_size=cfg.batch_size, shuffle=is_train, num_workers=0,
+                                       pin_memory=torch.cuda.is_available(), drop_last=is_train)
 
 
 def load_aligned_pretrained_embeddings(processor, model_dir, pretrained_dim):

@@ -79,6 +79,57 @@ def test_hybrid_item_tower_forward_and_grads(gpu, embed_dim):
     assert n > 30
 
 
+def _config0_inputs(B=256, n_std=6, vocab=384, R=32, S=32, seed=0):
+    """SURVEY.md 8d config 1 (BASELINE configs[0]): std [B, 6] ~ U{0..383} with ~10 % PAD;
+    RE ids [B, 9, 32] and text [B, 32]: [CLS]=101, length ~ U{2..32} ([CLS][SEP] for an empty
+    field), word pieces ~ U{1000..30521}, [SEP]=102 last, 0-padded, masks 1 / 0."""
+    g = torch.Generator().manual_seed(seed)
+    std = torch.randint(0, vocab, (B, n_std), generator=g)
+    std[torch.rand(B, n_std, generator=g) < 0.1] = 0
+
+    def seqs(shape, width):
+        lens = torch.randint(2, width + 1, shape, generator=g)
+        ar = torch.arange(width).view(*([1] * len(shape)), width)
+        ids = torch.randint(1000, 30522, shape + (width,), generator=g)
+        ids = torch.where(ar == 0, torch.full_like(ids, 101), ids)
+        ids = torch.where(ar == (lens - 1).unsqueeze(-1), torch.full_like(ids, 102), ids)
+        mask = (ar < lens.unsqueeze(-1)).long()
+        return ids * mask, mask
+
+    re_ids, re_mask = seqs((B, 9), R)
+    txt, txt_mask = seqs((B,), S)
+    return [std, re_ids, re_mask, txt, txt_mask]
+
+
+@pytest.mark.parametrize("grad", [False, True])
+def test_hybrid_item_tower_config0_full_size(gpu, grad):
+    """BASELINE configs[0] at its size: HybridItemTower(384, 6, embed_dim=64, output_dim=128) on 256
+    items with a bert-base-shaped BERT (hidden 768, 12 heads, intermediate 3072, vocab 30522;
+    2 of its 12 layers, to bound the CPU oracle's time), eval mode, against
+    oracle/item_tower.py (item_tower.py:228-286): rtol 1e-4. no_grad is the serving /
+    refresh path (the text BERT over packed valid tokens, bf16x3 GEMMs); with grad the text BERT
+    is HF's module and the rest runs on this package's kernels."""
+    bert = IT.build_local_bert(hidden_size=768, num_layers=2, num_heads=12, intermediate=3072, vocab_size=30522,
+                               max_position=512, seed=5)
+    torch.manual_seed(8)
+    ref = OIT.OracleHybridItemTower(384, 6, 64, 128, bert_model=bert).eval()
+    dut = IT.HybridItemTower(384, 6, 64, 128, bert_model=copy.deepcopy(bert))
+    dut.load_state_dict(ref.state_dict())
+    dut = dut.to(gpu).eval()
+    x = _config0_inputs()
+    with torch.no_grad():
+        y_ref = ref(*x)
+    xd = [t.to(gpu) for t in x]
+    if grad:
+        y = dut(*xd)
+        y.sum().backward()
+    else:
+        with torch.no_grad():
+            y = dut(*xd)
+    assert y.shape == (256, 128)
+    torch.testing.assert_close(y.detach().cpu(), y_ref, atol=1e-5, rtol=1e-4)
+
+
 def test_projector_wrapper_and_simcse_loss(gpu):
     """OptimizedItemTower + SimCSEModelWrapper forward and the symmetric SimCSE loss (fused
     InfoNCE, both directions) vs the oracle: loss within 1e-5 relative, grads 1e-4."""

@@ -115,3 +115,34 @@ def test_step_index_rejects_out_of_range_ids(gpu):
     batch["target_ids"][2, -1] = 101              # the id domain is the lookup's 101 rows
     with pytest.raises(IndexError, match="outside"):
         D.prepare_step_index(batch, pretrained_lookup=items.pretrained.to(gpu))
+
+
+@pytest.mark.parametrize("kind", ["width64", "fp16", "cpu", "requires_grad"])
+def test_step_index_lookup_not_taken_by_device_builder(gpu, kind):
+    """The device builder gathers 128-wide fp32 device rows itself (si_pv_k); any other pretrained
+    lookup takes the torch builders: a 64-wide or fp16 one is gathered by ops.gather_rows as is, a
+    lookup that requires grad keeps its autograd edge, a host lookup raises RuntimeError (no host
+    pointer reaches a kernel)."""
+    items = small_universe(100)
+    batch = to_dev(synth.make_batch(items, 16, seed=3), gpu)
+    lk = items.pretrained.to(gpu)
+    if kind == "width64":
+        lk = lk[:, :64].contiguous()
+    elif kind == "fp16":
+        lk = lk.half()
+    elif kind == "cpu":
+        lk = items.pretrained.clone()
+    else:
+        lk = lk.clone().requires_grad_()
+    if kind == "cpu":
+        with pytest.raises(RuntimeError):
+            D.prepare_step_index(batch, pretrained_lookup=lk)
+        return
+    ix = D.prepare_step_index(batch, pretrained_lookup=lk)
+    assert not hasattr(ix, "wsb")                      # the torch builders ran
+    pk, _, ids, pv, _ = ix.packed
+    exp = lk.float()[ids[0]] if kind != "requires_grad" else lk[ids[0]]
+    torch.testing.assert_close(pv.float(), exp.float(), rtol=0, atol=0)
+    if kind == "requires_grad":
+        pv.sum().backward()
+        assert lk.grad is not None and float(lk.grad.abs().sum()) > 0

@@ -202,3 +202,42 @@ def test_index_prefetcher_steps_equal_inline(gpu):
     assert l0 == l1
     for a, b in zip(p0, p1):
         assert torch.equal(a, b)
+
+
+def test_step_parity_on_reference_sample_batch(gpu):
+    """A real SASRecDataset batch (the 13 customers of the reference's own sample file, through
+    FeatureProcessor + the DataLoader's default collation, tests/test_user_dataset_cpu.py) through
+    the GPU step's losses and gradients vs the oracle: the drop-in producer feeds the drop-in step."""
+    from torch.utils.data import default_collate
+    from tests.test_user_dataset_cpu import _frames
+    users, items_df, sq, _ = _frames(cap=10_000)
+    fp = T.FeatureProcessor(users, items_df, sq)
+    ds = T.SASRecDataset(fp, max_len=50, is_train=True)
+    batch = default_collate([ds[i] for i in range(len(ds))])
+    I = fp.num_items
+    cfg = small_cfg(num_items=I, hash_size=100)
+    g = torch.Generator().manual_seed(31)
+    pre = F.normalize(torch.randn(I + 1, 128, generator=g), dim=1)
+    pre[0] = 0.0
+    log_q = fp.get_logq_probs("cpu")
+    ref, dut = paired_towers(cfg, gpu)
+    ref.train(); dut.train()
+    W_ref = pre.clone().requires_grad_()
+    tot_r, main_r, cl_r = O.contrastive_losses(ref, W_ref, log_q, batch, pre)
+    tot_r.backward()
+    item_tower = TT.SASRecItemTower(I, 128, log_q.clone()).to(gpu)
+    item_tower.init_from_pretrained(pre.to(gpu))
+    item_tower.set_freeze_state(False)
+    bd = to_dev(batch, gpu)
+    tot, main, cl = TT.contrastive_losses(dut, item_tower, item_tower.log_q, bd, cfg,
+                                          pretrained_lookup=pre.to(gpu))
+    for a, b in [(tot, tot_r), (main, main_r), (cl, cl_r)]:
+        assert abs(a.item() - b.item()) < 1e-4, (a.item(), b.item())
+    tot.backward()
+    for (name, pr), (_, pd) in zip(ref.named_parameters(), dut.named_parameters()):
+        gr = pr.grad if pr.grad is not None else torch.zeros_like(pr)
+        gd = pd.grad.cpu() if pd.grad is not None else torch.zeros_like(pr)
+        err = (gd - gr).abs().max().item()
+        assert err <= 2e-3 * (gr.abs().max().item() + 1e-12) + 1e-6, f"{name}: max err {err}"
+    gw = item_tower.item_matrix.weight.grad.cpu()
+    assert (gw - W_ref.grad).abs().max().item() <= 2e-3 * W_ref.grad.abs().max().item() + 1e-6

@@ -53,11 +53,13 @@ def test_feature_processor_logq():
     import pandas as pd
     probs = np.array([0.5, np.nan, 0.2, 0.0, 0.3])
     df = pd.DataFrame({"article_id": [11, 12, 13, 14, 15], "raw_probability": probs})
-    fp = T.FeatureProcessor(df)
+    users = pd.DataFrame({"customer_id": []})
+    seqs = pd.DataFrame({"customer_id": [], "sequence_ids": [], "sequence_deltas": []})
+    fp = T.FeatureProcessor(users, df, seqs)
     lq = fp.get_logq_probs("cpu")
     exp = synth.logq_from_probs(probs)
     assert torch.equal(lq, exp)
-    assert fp.item2id[13] == 3 and lq[0].item() == -20.0
+    assert fp.item2id["13"] == 3 and lq[0].item() == -20.0
 
 
 def test_oracle_hnm_losses_num_k_and_mining():
