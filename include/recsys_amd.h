@@ -249,6 +249,14 @@ int rsx_linear_wgrad_x3(const float* dY, int64_t ldy, const float* X, int64_t ld
  * N % 128 == 0, K % 32 == 0, A/B 16-byte aligned, leading dimensions multiples of 4. */
 int rsx_gemm_x3(const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias, int64_t M, int N, int K,
                 int epi, float* aux, int64_t ldaux, float p_drop, uint64_t seed, float* C, int64_t ldc, void* stream);
+/* C = epi(A . Bt + bias) with Bt [K, N] as stored (row stride ldbt >= N): the input gradient
+ * dX = dY . W of the same token linears straight from W [out, in] (K = out, N = in; autograd's
+ * dX GEMM of nn.Linear, v1_refine_usertower.py:447-510), no transposed copy of W; epi / aux /
+ * p_drop / seed as rsx_gemm_x3 (EPI_DGELU_DROP: the feed-forward's backward through GELU and
+ * dropout). K in {128, 256, 384}, N % 128 == 0, A/C 16-byte aligned. */
+int rsx_gemm_x3_tn(const float* A, int64_t lda, const float* Bt, int64_t ldbt, const float* bias, int64_t M, int N,
+                   int K, int epi, float* aux, int64_t ldaux, float p_drop, uint64_t seed, float* C, int64_t ldc,
+                   void* stream);
 /* C[m] = A[m] . B^T + bias + R[ridx[m]]: a per-row table added in the epilogue. Replaces
  * output_proj[0](cat(enc_out, profile.expand)) of SASRecUserTower.forward
  * (v1_refine_usertower.py:498-505) over the packed tokens: A = encoder output, B = the token

@@ -104,6 +104,7 @@ struct GArgs {
   int64_t ldy;
   int64_t lda, ldb, ldc, ldaux, M;
   int N, K, epi, tiles_n, tiles, per;
+  int transb;  // weight-stationary path only: B given as Bt [K, ldb] (B[n][k] = Bt[k * ldb + n])
   rsx::Dropout drop;
 };
 
@@ -310,10 +311,20 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_ws_k(WsArgs w) {
   for (int slot = tid; slot < KC * 8 * NT * 64; slot += kWsThreads) {
     const int l = slot & 63, rest = slot >> 6;
     const int j = rest % NT, st = rest / NT;
-    const float* src = a.B + (int64_t)(n0 + 32 * j + (l & 31)) * a.ldb + (st >> 3) * 128 + 16 * (st & 7) +
-                       4 * (l >> 5);
+    const int n = n0 + 32 * j + (l & 31), k0 = (st >> 3) * 128 + 16 * (st & 7) + 4 * (l >> 5);
+    float4 x0, x1;
+    if (a.transb) {  // dX = dY W with W [K, N] as stored: column n of W (lanes read consecutive n)
+      const float* src = a.B + (int64_t)k0 * a.ldb + n;
+      x0 = make_float4(src[0], src[a.ldb], src[2 * a.ldb], src[3 * a.ldb]);
+      src += 8 * a.ldb;
+      x1 = make_float4(src[0], src[a.ldb], src[2 * a.ldb], src[3 * a.ldb]);
+    } else {
+      const float* src = a.B + (int64_t)n * a.ldb + k0;
+      x0 = *reinterpret_cast<const float4*>(src);
+      x1 = *reinterpret_cast<const float4*>(src + 8);
+    }
     u32x4 hi, lo;
-    split8(*reinterpret_cast<const float4*>(src), *reinterpret_cast<const float4*>(src + 8), hi, lo);
+    split8(x0, x1, hi, lo);
     sW[(rest * 2 + 0) * 64 + l] = hi;
     sW[(rest * 2 + 1) * 64 + l] = lo;
   }
@@ -607,7 +618,7 @@ RSX_API int rsx_gemm_x3(const float* A, int64_t lda, const float* B, int64_t ldb
   RSX_ARG(p_drop >= 0.0f && p_drop < 1.0f, "p_drop must be in [0, 1)");
   RSX_ARG(M * (int64_t)N < (1LL << 32), "M * N must be < 2^32 (dropout element index)");
   if (M == 0) return 0;
-  GArgs g;
+  GArgs g = {};
   g.A = A; g.B = B; g.bias = bias; g.C = C; g.aux = aux; g.ridx = nullptr;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.ldaux = ldaux; g.M = M;
   g.N = N; g.K = K; g.epi = epi;
@@ -629,6 +640,38 @@ RSX_API int rsx_gemm_x3(const float* A, int64_t lda, const float* B, int64_t ldb
   if (epi == EPI_BIAS) hipLaunchKernelGGL(gemm_x3_nt_k<EPI_BIAS>, dim3(grid), dim3(256), 0, st, g);
   else if (epi == EPI_GELU_DROP) hipLaunchKernelGGL(gemm_x3_nt_k<EPI_GELU_DROP>, dim3(grid), dim3(256), 0, st, g);
   else hipLaunchKernelGGL(gemm_x3_nt_k<EPI_DGELU_DROP>, dim3(grid), dim3(256), 0, st, g);
+  RSX_LAUNCHED();
+  return 0;
+}
+
+// C = epi(A . Bt + bias) with the right operand as stored, Bt [K, N] (row stride ldbt >= N): the
+// input gradient dX = dY . W of a token linear straight from its weight W [out, in] (K = out,
+// N = in), without a transposed copy of W per call; epi as rsx_gemm_x3 (EPI_DGELU_DROP: the
+// feed-forward's dPre = (dF . W2) * keep / (1 - p) * gelu'). Weight-stationary path: K in
+// {128, 256, 384}, N % 128 == 0 (the staging reads W's columns; it runs once per workgroup).
+RSX_API int rsx_gemm_x3_tn(const float* A, int64_t lda, const float* Bt, int64_t ldbt, const float* bias, int64_t M,
+                           int N, int K, int epi, float* aux, int64_t ldaux, float p_drop, uint64_t seed, float* C,
+                           int64_t ldc, void* stream) {
+  RSX_ARG(A && Bt && C, "null tensor");
+  RSX_ARG(M >= 0 && N > 0 && N % 128 == 0 && (K == 128 || K == 256 || K == 384),
+          "N must be a multiple of 128, K 128, 256 or 384");
+  RSX_ARG(lda >= K && ldbt >= N && ldc >= N && lda % 4 == 0 && ldc % 4 == 0, "bad leading dimensions");
+  RSX_ARG(((uintptr_t)A % 16) == 0 && ((uintptr_t)C % 16) == 0, "A/C must be 16-byte aligned");
+  RSX_ARG(epi == EPI_BIAS || epi == EPI_GELU_DROP || epi == EPI_DGELU_DROP, "epi must be 0, 1 or 2");
+  RSX_ARG(epi == EPI_BIAS || (epi == EPI_GELU_DROP && !aux) || (aux && ldaux >= N),
+          "the GELU epilogues need aux [M, >=N] (EPI_GELU_DROP: aux may be null for inference)");
+  RSX_ARG(p_drop >= 0.0f && p_drop < 1.0f, "p_drop must be in [0, 1)");
+  RSX_ARG(M * (int64_t)N < (1LL << 32), "M * N must be < 2^32 (dropout element index)");
+  if (M == 0) return 0;
+  GArgs g = {};
+  g.A = A; g.B = Bt; g.bias = bias; g.C = C; g.aux = aux; g.ridx = nullptr;
+  g.lda = lda; g.ldb = ldbt; g.ldc = ldc; g.ldaux = ldaux; g.M = M;
+  g.N = N; g.K = K; g.epi = epi; g.transb = 1;
+  g.drop = rsx::make_dropout(epi == EPI_BIAS ? 0.0f : p_drop, seed);
+  hipStream_t st = (hipStream_t)stream;
+  if (K == 128) launch_ws<1, 128>(g, st);
+  else if (K == 256) launch_ws<2, 128>(g, st);
+  else launch_ws<3, 64>(g, st);
   RSX_LAUNCHED();
   return 0;
 }

@@ -322,7 +322,7 @@ class _QKVMHA(torch.autograd.Function):
         N.check(rc, "mha_bwd")
         D = x.shape[-1]
         dq2 = dqkv.reshape(-1, 3 * D)
-        dx = gemm_x3(dq2, w.t(), tag="tok_linear_dx").reshape(x.shape) if ctx.needs_input_grad[0] else None
+        dx = _dx(dq2, w).reshape(x.shape) if ctx.needs_input_grad[0] else None
         dw = db = None
         if ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2]):
             dw, db = linear_wgrad(dq2, x.reshape(-1, D), w.shape, has_bias and ctx.needs_input_grad[2])
@@ -950,6 +950,37 @@ def gemm_x3(a, b, bias=None, epi=EPI_BIAS, aux=None, p_drop=0.0, seed=0, tag=Non
     return out
 
 
+def _tn_ok(w) -> bool:
+    """rsx_gemm_x3_tn takes W [out, in] as stored for dX = dY W (weight-stationary path)."""
+    return (_gemm_precision == "bf16x3" and w.shape[0] in (128, 256, 384) and w.shape[1] % 128 == 0
+            and w.stride(1) == 1 and w.stride(0) % 4 == 0)
+
+
+def gemm_x3_tn(a, w, epi=EPI_BIAS, aux=None, p_drop=0.0, seed=0, tag=None):
+    """epi(a [M, K] @ w [K, N]) on rsx_gemm_x3_tn: the input gradient dY W of a token linear with W
+    as stored ([out, in], K = out in {128, 256, 384}, N = in % 128 == 0), no transposed copy;
+    EPI_DGELU_DROP as gemm_x3."""
+    a = _c(a)
+    M, K = a.shape
+    n = w.shape[1]
+    out = torch.empty(M, n, device=a.device, dtype=torch.float32)
+    if M == 0:
+        return out
+    with timed(tag or "gemm_x3"):
+        rc = N.lib().rsx_gemm_x3_tn(N.ptr(a), a.stride(0), N.ptr(w), w.stride(0), None, M, n, K, epi, N.ptr(aux),
+                                    0 if aux is None else aux.stride(0), float(p_drop), int(seed), N.ptr(out),
+                                    out.stride(0), N.stream())
+    N.check(rc, "gemm_x3_tn")
+    return out
+
+
+def _dx(dy, w, tag="tok_linear_dx"):
+    """dX = dY W of a token linear (rsx_gemm_x3_tn when the shape allows, else a transposed copy)."""
+    if _tn_ok(w):
+        return gemm_x3_tn(dy, w, tag=tag)
+    return gemm_x3(dy, w.t(), tag=tag)
+
+
 def linear_wgrad(dy, x, weight_shape, need_bias, tag="linear_wgrad"):
     """(dW, db) of y = x W^T + b over the token axis: split-K over tokens, deterministic."""
     N.ensure_device(dy)
@@ -986,7 +1017,7 @@ class _TokLinear(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             if _x3_ok(weight.shape[1], weight.shape[0]):
-                dx = gemm_x3(dy, weight.t(), tag="tok_linear_dx")
+                dx = _dx(dy, weight)
             else:
                 dx = dy @ weight
         dw = db = None
@@ -1026,7 +1057,7 @@ class _LinearAddLayerNorm(torch.autograd.Function):
         if dy is None:
             dy = torch.zeros_like(s)
         dx, dres, dw, db = _ln_bwd(s, mean, rstd, w, b, 0, dy, ds, p_drop, seed, need[0], True, need[4], need[5])
-        da = gemm_x3(dres, weight.t(), tag="tok_linear_dx") if need[1] else None
+        da = _dx(dres, weight) if need[1] else None
         dwt = dbt = None
         if need[2] or (has_bias and need[3]):
             dwt, dbt = linear_wgrad(dres, a, weight.shape, has_bias and need[3])
@@ -1101,9 +1132,9 @@ class _ProfileLinear(torch.autograd.Function):
         N.check(rc, "segment_sum_rows(profile)")
         dx = dprofile = None
         if ctx.needs_input_grad[0]:
-            dx = gemm_x3(dh, weight[:, :D].t(), tag="tok_linear_dx")
+            dx = _dx(dh, weight[:, :D])
         if ctx.needs_input_grad[1]:
-            dprofile = gemm_x3(dprof, weight[:, D:].t(), tag="tok_linear_dx") if _x3_ok(D, n) else \
+            dprofile = _dx(dprof, weight[:, D:]) if _x3_ok(D, n) else \
                 dprof @ weight[:, D:]
         dw = torch.empty_like(weight)
         db = torch.empty(n, device=dh.device, dtype=torch.float32)
@@ -1158,13 +1189,16 @@ class _FFN(torch.autograd.Function):
         p_drop, seed, has_b1, has_b2 = ctx.cfg
         df = _c(df)
         need = ctx.needs_input_grad
-        dpre = gemm_x3(df, w2.t(), None, EPI_DGELU_DROP, ggrad, p_drop, seed, tag="ffn_dpre")
+        if _tn_ok(w2):
+            dpre = gemm_x3_tn(df, w2, EPI_DGELU_DROP, ggrad, p_drop, seed, tag="ffn_dpre")
+        else:
+            dpre = gemm_x3(df, w2.t(), None, EPI_DGELU_DROP, ggrad, p_drop, seed, tag="ffn_dpre")
         dw2 = db2 = dw1 = db1 = None
         if need[3] or need[4]:
             dw2, db2 = linear_wgrad(df, act, w2.shape, has_b2 and need[4])
         if need[1] or need[2]:
             dw1, db1 = linear_wgrad(dpre, h, w1.shape, has_b1 and need[2])
-        dh = gemm_x3(dpre, w1.t(), tag="ffn_dh") if need[0] else None
+        dh = _dx(dpre, w1, tag="ffn_dh") if need[0] else None
         return dh, dw1, db1, dw2, db2, None, None
 
 
