@@ -437,6 +437,17 @@ int rsx_segment_sum_rows(const float* src, int64_t ld_src, const int64_t* perm, 
                          const int64_t* rows, int64_t nseg, int64_t D, const float* scale, int64_t skip_row,
                          float* dst, int64_t ld_dst, int accumulate, void* stream);
 
+/* The contrastive step's objective from its device loss sums, one launch instead of the
+ * scalar tensor ops of train_user_tower_all_time (tower_code/v1_usertower_train.py:814-845):
+ * main = s_main * inv_n (s_main nullable: 0), cl = s_un * inv_b + lambda_sup * s_sup / max(cnt, 1)
+ * (s_sup nullable), total = main + lambda_cl * cl; out[6] = {total, main, cl} twice (the second
+ * copy for logging / all-reduce). Backward: g3[3] = gradients of g * total w.r.t. s_main, s_un,
+ * s_sup (cnt nullable when s_sup was). All device scalars. */
+int rsx_loss_combine(const float* s_main, const float* s_un, const float* s_sup, const float* cnt, float inv_n,
+                     float inv_b, float lambda_sup, float lambda_cl, float* out, void* stream);
+int rsx_loss_combine_bwd(const float* g, const float* cnt, float inv_n, float inv_b, float lambda_sup,
+                         float lambda_cl, float* g3, void* stream);
+
 /* Hard-negative mining: for each row i of u_norm [N,D] against the columns
  * i_norm [N,D] (both already L2-normalised), ignore column j when target_ids[j] ==
  * target_ids[i] or (i_norm[i].i_norm[j] > hnm_threshold and j != i); mining value =
@@ -454,6 +465,51 @@ int rsx_hnm_mine(const float* u_norm, const float* i_norm, const int64_t* target
                  float* top_cos, int32_t* avail, void* stream);
 int64_t rsx_hnm_workspace_bytes(int64_t N);
 int64_t rsx_hnm_max_rows(void);
+
+/* ---- A2 + A3 + A4: the user tower's packed-token training program ---------------------
+ * SASRecUserTower.forward in training mode over the contrastive step's packed tokens
+ * (tower_code/v1_refine_usertower.py:434-510: item_proj, the gated embedding sum + position +
+ * emb_ln + dropout, the norm_first TransformerEncoder stack, output_proj[0] over
+ * cat(token, profile[user]), LayerNorm + GELU, output_proj[3], F.normalize) and its backward,
+ * each as ONE call that launches the same kernels as the per-op entry points above, in the
+ * same order with the same arguments (bit-identical results), from the library instead of
+ * one host-language call per op. Shapes: d_model 128, 4 heads of 32, feed-forward 256,
+ * bf16x3 token linears and attention, L <= 64, 1..8 layers. The static profile rows
+ * (:472-494) are an input (computed by the caller, whose autograd takes their gradient).
+ *
+ * p[] (device pointers, RSX_TW_* order; layer l's 12 parameters at RSX_TW_LAYER0 + 12 l, the
+ * output head's 6 after the last layer):
+ *   inputs  pretrained rows [T,128], six id arrays int64 [T] (item, time, type, colour,
+ *           graphic, section), token positions int64 [T], key-pad flags uint8 [T], user token
+ *           offsets int32 / int64 [U+1], token user int64 [T], seq gate [6] (sigmoid(seq_gate)
+ *           * s_mask), profile rows [U,128], the item-id gradient plan (perm [T], chunk bounds
+ *           [C+1], chunk ids [C], chunk offsets per id [Uq+1], ids [Uq]; ops.sort_segments)
+ *   params  item_proj w/b, the six tables, pos_emb, emb_ln w/b; per layer norm1 w/b,
+ *           in_proj w/b, out_proj w/b, norm2 w/b, linear1 w/b, linear2 w/b; output_proj[0] w/b,
+ *           output_proj[1] w/b, output_proj[3] w/b
+ * dims[]  T, U, pos rows (max_len), layers, C, Uq, rows of the six tables
+ * fargs[] p_drop, emb_ln eps, per layer norm1 eps, norm2 eps, output LayerNorm eps
+ * seeds[] 1 + 4 x layers dropout seeds: embedding, then per layer attention, out-projection
+ *         add, feed-forward, closing add (the per-op entry points' seed order)
+ * arena   saved activations (rsx_tower_arena_bytes), read by the backward; out [T,128] (the
+ *         backward reads it too: the F.normalize backward).
+ * grads[] parallel to p[]: params' gradients written, except the embedding stage's (six
+ *         tables, pos_emb, emb_ln w/b) and the seq gate's, which are ACCUMULATED (caller
+ *         zeroes); the profile's [U,128] written; the pretrained rows' nullable (written).
+ * ws      backward scratch (rsx_tower_bwd_workspace_bytes). */
+enum {
+  RSX_TW_PV = 0, RSX_TW_IDS = 1, RSX_TW_TOK_POS = 7, RSX_TW_TOK_PAD = 8, RSX_TW_SEG32 = 9, RSX_TW_SEG64 = 10,
+  RSX_TW_TOK_USER = 11, RSX_TW_GATE = 12, RSX_TW_PROFILE = 13, RSX_TW_ITEMSEG = 14, RSX_TW_ITEM_PROJ = 19,
+  RSX_TW_TABLES = 21, RSX_TW_POS = 27, RSX_TW_EMB_LN = 28, RSX_TW_LAYER0 = 30
+};
+int64_t rsx_tower_n_ptrs(int layers);
+int64_t rsx_tower_arena_bytes(int64_t T, int64_t U, int layers);
+int64_t rsx_tower_bwd_workspace_bytes(int64_t T, int64_t U, int64_t L, int layers, int64_t C);
+int rsx_tower_fwd(const void* const* p, const int64_t* dims, const float* fargs, const uint64_t* seeds, void* arena,
+                  int64_t arena_bytes, float* out, void* stream);
+int rsx_tower_bwd(const void* const* p, const int64_t* dims, const float* fargs, const uint64_t* seeds,
+                  const void* arena, const float* out, const float* dout, void* const* grads, void* ws,
+                  int64_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

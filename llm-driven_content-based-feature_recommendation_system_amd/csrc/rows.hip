@@ -192,7 +192,50 @@ __global__ __launch_bounds__(256) void ids_check_k(const int64_t* __restrict__ i
   if (__builtin_amdgcn_ballot_w64(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
 }
 
+// The contrastive step's objective from its device loss sums (train_user_tower_all_time,
+// tower_code/v1_usertower_train.py:814-845, per rank of the global batch: dist.py): main = s_main /
+// n, cl = s_un / b + lambda_sup * s_sup / max(cnt, 1), total = main + lambda_cl * cl.
+// out = {total, main, cl, total, main, cl} (the second three: detached copies for logging).
+__global__ void loss_combine_k(const float* s_main, const float* s_un, const float* s_sup, const float* cnt,
+                               float inv_n, float inv_b, float lsup, float lcl, float* out) {
+  if (threadIdx.x != 0) return;
+  const float m = s_main ? s_main[0] * inv_n : 0.0f;
+  float cl = s_un[0] * inv_b;
+  if (s_sup) cl += lsup * (s_sup[0] / fmaxf(cnt[0], 1.0f));
+  const float t = m + lcl * cl;
+  out[0] = t; out[1] = m; out[2] = cl;
+  out[3] = t; out[4] = m; out[5] = cl;
+}
+
+// its backward: g3 = {d/d s_main, d/d s_un, d/d s_sup} of g * total
+__global__ void loss_combine_bwd_k(const float* g, const float* cnt, float inv_n, float inv_b, float lsup, float lcl,
+                                   float* g3) {
+  if (threadIdx.x != 0) return;
+  const float gv = g[0];
+  g3[0] = gv * inv_n;
+  g3[1] = gv * lcl * inv_b;
+  g3[2] = cnt ? gv * lcl * lsup / fmaxf(cnt[0], 1.0f) : 0.0f;
+}
+
 }  // namespace
+
+RSX_API int rsx_loss_combine(const float* s_main, const float* s_un, const float* s_sup, const float* cnt,
+                             float inv_n, float inv_b, float lambda_sup, float lambda_cl, float* out, void* stream) {
+  RSX_ARG(s_un && out && (!s_sup || cnt), "null tensor");
+  hipLaunchKernelGGL(loss_combine_k, dim3(1), dim3(64), 0, (hipStream_t)stream, s_main, s_un, s_sup, cnt, inv_n,
+                     inv_b, lambda_sup, lambda_cl, out);
+  RSX_LAUNCHED();
+  return 0;
+}
+
+RSX_API int rsx_loss_combine_bwd(const float* g, const float* cnt, float inv_n, float inv_b, float lambda_sup,
+                                 float lambda_cl, float* g3, void* stream) {
+  RSX_ARG(g && g3, "null tensor");
+  hipLaunchKernelGGL(loss_combine_bwd_k, dim3(1), dim3(64), 0, (hipStream_t)stream, g, cnt, inv_n, inv_b,
+                     lambda_sup, lambda_cl, g3);
+  RSX_LAUNCHED();
+  return 0;
+}
 
 RSX_API int rsx_gather_rows(const float* src, int64_t ld_src, const int64_t* idx, int64_t n, int64_t D, int normalize,
                             float eps, float* out, float* nrm_out, void* stream) {

@@ -309,6 +309,16 @@ class _Packed:
 _DEVICE_INDEX = os.environ.get("RSX_DEVICE_INDEX", "1") != "0"
 
 
+def doubled_static(batch):
+    """The per-user static inputs of both dropout views (users b and B + b share them): the nine id
+    columns stacked and doubled in two launches, cont_feats in one, instead of ten concatenations."""
+    from .tower_code.v1_usertower_train import _STATIC_KEYS
+    ids = torch.stack([batch[k].reshape(-1).to(torch.int64) for k in _STATIC_KEYS[:9]])
+    ids = torch.cat([ids, ids], dim=1)
+    cont = batch[_STATIC_KEYS[9]]
+    return list(ids.unbind(0)) + [torch.cat([cont, cont])]
+
+
 def _prepare_step_index_device(batch, pretrained_vecs, pretrained_lookup, n_items) -> StepIndex:
     """prepare_step_index on rsx_step_index_* (csrc/step_index.hip): the same arrays in the same
     orders as the torch builders, with ONE host read (the totals) per batch; at world > 1 the
@@ -371,7 +381,7 @@ def _prepare_step_index_device(batch, pretrained_vecs, pretrained_lookup, n_item
     else:
         pv_tok = pk.take(pretrained_vecs)
         pv_tok = torch.cat([pv_tok, pv_tok])
-    static = [torch.cat([batch[k], batch[k]]) for k in _STATIC_KEYS]
+    static = doubled_static(batch)
     ix = StepIndex()
     ix.packed = (pk, pk2, tok_ids, pv_tok, static)
     ix.B = B
@@ -540,14 +550,16 @@ def contrastive_objective_dp(model, item_tower, log_q_tensor, batch, cfg, pretra
 
     # ---- main LogQ loss over all valid steps of the global batch
     n_glob = index.n_glob
+    main_sum = None
     if n_glob > 0:
         groups = index.groups
         items_d = ops.gather_rows(item_tower.get_all_embeddings(), groups.uniq, normalize=True, unique=True)
-        bias = log_q_tensor[groups.uniq] * cfg.lambda_logq if cfg.lambda_logq > 0.0 else None
+        bias = None
+        if cfg.lambda_logq > 0.0:
+            bias = log_q_tensor[groups.uniq]
+            if cfg.lambda_logq != 1.0:
+                bias = bias * cfg.lambda_logq
         main_sum, _ = ops.nce_grouped_sum(u_loc, items_d, bias, groups, tau=temperature, tag="main")
-        main_local = main_sum / float(n_glob)
-    else:
-        main_local = torch.zeros((), device=device)
 
     # ---- DuoRec on the bug-compatible "last" index (count_valid - 1), global B x B
     last_t = index.last_t
@@ -558,18 +570,17 @@ def contrastive_objective_dp(model, item_tower, log_q_tensor, batch, cfg, pretra
     t_glob_last = index.t_glob_last
     un_sum, _ = ops.nce_sum(z1, z2_glob, tau=temperature, flags=ops.NCE_PLAIN, diag_offset=rank * B,
                             tag="duorec")
-    unsup_local = un_sum / float(b_glob)
+    sup_sum = cnt_glob = None
     if cfg.lambda_sup > 0:
         sup_sum, sup_cnt = ops.nce_sum(z1, z1_glob, None, last_t, t_glob_last, tau=temperature,
                                        flags=ops.NCE_SUPCON, diag_offset=rank * B, tag="supcon")
-        cnt_glob = all_reduce_sum_(sup_cnt.detach().clone())
-        sup_local = sup_sum / cnt_glob.clamp(min=1.0)
-    else:
-        sup_local = torch.zeros((), device=device)
-    cl_local = unsup_local + cfg.lambda_sup * sup_local
-    objective = main_local + cfg.lambda_cl * cl_local
-
-    logs = torch.stack([objective.detach(), main_local.detach(), cl_local.detach()])
+        cnt_glob = sup_cnt.detach()
+        if ws > 1:
+            cnt_glob = all_reduce_sum_(cnt_glob.clone())
+    # objective = main / n_glob + lambda_cl * (unsup / b_glob + lambda_sup * sup / max(cnt_glob, 1)),
+    # one device launch (ops.loss_combine) instead of ~10 scalar tensor ops and their backward
+    objective, logs = ops.loss_combine(main_sum, un_sum, sup_sum, cnt_glob, n_glob, b_glob, cfg.lambda_sup,
+                                       cfg.lambda_cl)
     all_reduce_sum_(logs)
     return objective, logs[0], logs[1], logs[2]
 

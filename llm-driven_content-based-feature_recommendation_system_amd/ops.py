@@ -5,6 +5,7 @@ There is no CPU path: a non-ROCm tensor raises.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 
 import torch
@@ -680,6 +681,45 @@ def nce_grouped_sum(A, B_distinct, bias, groups: TargetGroups, tau=0.1, tag="nce
     return _NCEGrouped.apply(A, B_distinct, bias, groups, float(tau), str(tag), prec)
 
 
+class _LossCombine(torch.autograd.Function):
+    """total = s_main / n + lambda_cl * (s_un / b + lambda_sup * s_sup / max(cnt, 1)) on the device
+    (rsx_loss_combine), with (total, main, cl) also returned detached for logging."""
+
+    @staticmethod
+    def forward(ctx, s_main, s_un, s_sup, cnt, consts):
+        inv_n, inv_b, lsup, lcl = consts
+        out = torch.empty(6, device=s_un.device, dtype=torch.float32)
+        rc = N.lib().rsx_loss_combine(N.ptr(s_main), N.ptr(s_un), N.ptr(s_sup), N.ptr(cnt), inv_n, inv_b, lsup, lcl,
+                                      N.ptr(out), N.stream())
+        N.check(rc, "loss_combine")
+        ctx.consts = consts
+        ctx.has = (s_main is not None, s_sup is not None)
+        ctx.save_for_backward(cnt)
+        logs = out[3:6]
+        ctx.mark_non_differentiable(logs)
+        return out[0], logs
+
+    @staticmethod
+    def backward(ctx, g, _glogs):
+        (cnt,) = ctx.saved_tensors
+        inv_n, inv_b, lsup, lcl = ctx.consts
+        g3 = torch.empty(3, device=g.device, dtype=torch.float32)
+        rc = N.lib().rsx_loss_combine_bwd(N.ptr(_c(g.reshape(1))), N.ptr(cnt), inv_n, inv_b, lsup, lcl, N.ptr(g3),
+                                          N.stream())
+        N.check(rc, "loss_combine_bwd")
+        has_main, has_sup = ctx.has
+        return (g3[0] if has_main else None), g3[1], (g3[2] if has_sup else None), None, None
+
+
+def loss_combine(s_main, s_un, s_sup, cnt, n, b, lambda_sup, lambda_cl):
+    """(objective, detached [total, main, cl]) of the contrastive step from device scalars:
+    s_main / n + lambda_cl * (s_un / b + lambda_sup * s_sup / max(cnt, 1)); s_main / s_sup may be
+    None (no valid step / lambda_sup = 0), cnt is not differentiated."""
+    consts = (1.0 / float(n) if n else 0.0, 1.0 / float(b), float(lambda_sup), float(lambda_cl))
+    cnt = None if cnt is None else _c(cnt.detach().reshape(1))
+    return _LossCombine.apply(s_main, s_un, s_sup, cnt, consts)
+
+
 # ----------------------------------------------------------------------------------------
 # Static-profile embeddings (several tiny gated tables, concatenated): rsx_static_embed_*
 class _StaticEmbed(torch.autograd.Function):
@@ -1216,6 +1256,132 @@ def ffn(h, w1, b1, w2, b2, p_drop=0.0, training=True):
         return f.reshape(*shp[:-1], w2.shape[0])
     return linear_tok(torch.nn.functional.dropout(torch.nn.functional.gelu(linear_tok(h, w1, b1)), p, training),
                       w2, b2)
+
+
+# ----------------------------------------------------------------------------------------
+# A2 + A3 + A4: the user tower's packed-token training program as one native call per direction
+# (rsx_tower_fwd / rsx_tower_bwd, csrc/tower.hip). RSX_TOWER_NATIVE=0 keeps the per-op path.
+_TOWER_NATIVE = os.environ.get("RSX_TOWER_NATIVE", "1") != "0"
+
+
+def tower_params(model):
+    """SASRecUserTower parameters in rsx_tower_* order (include/recsys_amd.h RSX_TW_ITEM_PROJ ..)."""
+    ps = [model.item_proj.weight, model.item_proj.bias, model.item_id_emb.weight, model.time_emb.weight,
+          model.type_emb.weight, model.color_emb.weight, model.graphic_emb.weight, model.section_emb.weight,
+          model.pos_emb.weight, model.emb_ln.weight, model.emb_ln.bias]
+    for layer in model.transformer_encoder.layers:
+        sa = layer.self_attn
+        ps += [layer.norm1.weight, layer.norm1.bias, sa.in_proj_weight, sa.in_proj_bias, sa.out_proj.weight,
+               sa.out_proj.bias, layer.norm2.weight, layer.norm2.bias, layer.linear1.weight, layer.linear1.bias,
+               layer.linear2.weight, layer.linear2.bias]
+    op = model.output_proj
+    ps += [op[0].weight, op[0].bias, op[1].weight, op[1].bias, op[3].weight, op[3].bias]
+    return ps
+
+
+def tower_native_ok(model, packed, pv) -> bool:
+    """Whether rsx_tower_* runs exactly what forward_packed's per-op path runs: bf16x3 token linears
+    and attention, d_model 128 with 4 heads and a 256-wide feed-forward, every parameter trained,
+    fp32 contiguous rows, the item-id gradient plan present."""
+    if not (_TOWER_NATIVE and _gemm_precision == "bf16x3" and _mha_precision == "bf16x3" and _ADDLN_ON):
+        return False
+    if getattr(packed, "item_seg", None) is None or not pv.is_cuda:
+        return False
+    layers = model.transformer_encoder.layers
+    if model.d_model != 128 or not (1 <= len(layers) <= 8) or model.pos_emb.weight.shape[0] > 64:
+        return False
+    for layer in layers:
+        if (layer.self_attn.num_heads != 4 or layer.linear1.out_features != 256 or not layer.norm_first
+                or layer.activation_relu_or_gelu != 2):
+            return False
+    ps = tower_params(model)
+    return all(p.requires_grad and p.dtype == torch.float32 and p.is_contiguous() for p in ps)
+
+
+_ADDLN_ON = os.environ.get("RSX_LINEAR_ADDLN", "1") != "0"
+
+
+class _TowerPacked(torch.autograd.Function):
+    """out = normalize(output_proj(...encoder(seq_embed(item_proj(pv)))...)) over packed tokens; see
+    rsx_tower_fwd. Inputs with gradients: pv (optional), gate, profile and the tower parameters."""
+
+    @staticmethod
+    def forward(ctx, pv, gate, profile, cfg, *params):
+        packed, tok_ids, p_drop, eps, nl = cfg
+        T, D = pv.shape
+        U = packed.seg_off.numel() - 1
+        dev = pv.device
+        pv = _c(pv)
+        gate = _c(gate)
+        profile = _c(profile)
+        perm, cb, chunk_ids, ch_off, uniq = packed.item_seg
+        inputs = ([pv] + list(tok_ids) + [packed.tok_pos, packed.tok_pad, packed.seg_off, packed.seg_off64,
+                                            packed.tok_user, gate, profile, perm, cb, chunk_ids, ch_off, uniq])
+        ptrs = N.ptr_array(inputs + list(params))
+        tabs = params[2:8]
+        dims = N.i64_array([T, U, params[8].shape[0], nl, chunk_ids.numel(), uniq.numel()]
+                           + [t.shape[0] for t in tabs])
+        fargs = (ctypes.c_float * (len(eps) + 1))(p_drop, *eps)
+        seeds = [next_seed() if p_drop > 0 else 0 for _ in range(1 + 4 * nl)]
+        seeds_arr = (ctypes.c_uint64 * len(seeds))(*seeds)
+        nbytes = N.lib().rsx_tower_arena_bytes(T, U, nl)
+        arena = torch.empty(nbytes, device=dev, dtype=torch.uint8)
+        out = torch.empty(T, D, device=dev, dtype=torch.float32)
+        with timed("tower_fwd"):
+            rc = N.lib().rsx_tower_fwd(ptrs, dims, fargs, seeds_arr, N.ptr(arena), nbytes, N.ptr(out), N.stream())
+        N.check(rc, "tower_fwd")
+        ctx.save_for_backward(pv, gate, profile, out, *params)
+        ctx.keep = (inputs, arena, ptrs, dims, fargs, seeds_arr)
+        ctx.shape = (T, U, params[8].shape[0], nl, chunk_ids.numel())
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        pv, gate, profile, out, *params = ctx.saved_tensors
+        inputs, arena, ptrs, dims, fargs, seeds_arr = ctx.keep
+        T, U, L, nl, C = ctx.shape
+        dev = dout.device
+        dout = _c(dout)
+        # accumulated: the six tables, pos_emb, emb_ln w / b, the gate (one zero-filled allocation);
+        # written: every other parameter's gradient and the profile's
+        acc_like = [gate] + [params[i] for i in range(2, 11)]
+        dgate, *acc = _zeros_group(acc_like)
+        written = _empty_group([params[0], params[1]] + list(params[11:]) + [profile])
+        dprofile = written[-1]
+        dparams = [written[0], written[1]] + acc + written[2:-1]
+        dpv = torch.empty_like(pv) if ctx.needs_input_grad[0] else None
+        grads = [dpv] + [None] * 11 + [dgate, dprofile] + [None] * 5 + dparams
+        nws = N.lib().rsx_tower_bwd_workspace_bytes(T, U, L, nl, C)
+        ws = torch.empty(nws, device=dev, dtype=torch.uint8)
+        with timed("tower_bwd"):
+            rc = N.lib().rsx_tower_bwd(ptrs, dims, fargs, seeds_arr, N.ptr(arena), N.ptr(out), N.ptr(dout),
+                                       N.ptr_array(grads), N.ptr(ws), nws, N.stream())
+        N.check(rc, "tower_bwd")
+        ctx.keep = None
+        return (dpv, dgate, dprofile, None) + tuple(dparams)
+
+
+def _empty_group(likes):
+    """Uninitialised fp32 buffers shaped like each tensor, carved out of ONE allocation (16-B
+    aligned slices)."""
+    sizes = [(t.numel() + 3) // 4 * 4 for t in likes]
+    flat = torch.empty(sum(sizes), device=likes[0].device, dtype=torch.float32)
+    out, o = [], 0
+    for t, n in zip(likes, sizes):
+        out.append(flat[o:o + t.numel()].view(t.shape))
+        o += n
+    return out
+
+
+def tower_packed(model, packed, pv_tok, tok_ids, s_g, profile, p_drop):
+    """The native form of SASRecUserTower.forward_packed after the static profile: [T, 128]."""
+    layers = model.transformer_encoder.layers
+    eps = [model.emb_ln.eps]
+    for layer in layers:
+        eps += [layer.norm1.eps, layer.norm2.eps]
+    eps.append(model.output_proj[1].eps)
+    cfg = (packed, [_c(t) for t in tok_ids], float(p_drop), [float(e) for e in eps], len(layers))
+    return _TowerPacked.apply(pv_tok, s_g, profile, cfg, *tower_params(model))
 
 
 # ----------------------------------------------------------------------------------------

@@ -366,6 +366,12 @@ class SASRecUserTower(nn.Module):
         p = self.dropout_rate if self.training else 0.0
         s_g = torch.sigmoid(self.seq_gate) * self._seq_gate_mask
         u_g = torch.sigmoid(self.static_gate)
+        if torch.is_grad_enabled() and ops.tower_native_ok(self, packed, pretrained_tok):
+            # the same kernels in the same order as below, issued by the library in one call per
+            # direction (rsx_tower_fwd / rsx_tower_bwd); the static profile stays here (autograd)
+            profile = self._static_profile(age_bucket, price_bucket, cnt_bucket, recency_bucket, channel_ids,
+                                           club_status_ids, news_freq_ids, fn_ids, active_ids, cont_feats, u_g)
+            return ops.tower_packed(self, packed, pretrained_tok, tok_ids, s_g, profile, p)
         base = ops.linear_tok(pretrained_tok, self.item_proj.weight, self.item_proj.bias)
         x = ops.seq_embed(
             base, tok_ids,

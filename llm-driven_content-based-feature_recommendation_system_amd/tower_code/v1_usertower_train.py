@@ -124,8 +124,8 @@ def pack_inputs(batch, pretrained_vecs=None, pretrained_lookup=None):
     else:
         pv_tok = ops.gather_rows(pretrained_lookup, tok_ids[0][:T])
     pv_tok = torch.cat([pv_tok, pv_tok])
-    static = [torch.cat([batch[k], batch[k]]) for k in _STATIC_KEYS]
-    return pk, pk2, tok_ids, pv_tok, static
+    from ..dist import doubled_static
+    return pk, pk2, tok_ids, pv_tok, doubled_static(batch)
 
 
 def packed_views(model, batch, pretrained_vecs=None, pretrained_lookup=None, packed=None):

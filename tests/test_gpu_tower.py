@@ -241,3 +241,42 @@ def test_step_parity_on_reference_sample_batch(gpu):
         assert err <= 2e-3 * (gr.abs().max().item() + 1e-12) + 1e-6, f"{name}: max err {err}"
     gw = item_tower.item_matrix.weight.grad.cpu()
     assert (gw - W_ref.grad).abs().max().item() <= 2e-3 * W_ref.grad.abs().max().item() + 1e-6
+
+
+@pytest.mark.parametrize("p_drop", [0.0, 0.2])
+def test_native_tower_program_equals_per_op_path(gpu, p_drop):
+    """rsx_tower_fwd / rsx_tower_bwd (csrc/tower.hip: the packed forward and its backward as one
+    native call each) against forward_packed's per-op path (RSX_TOWER_NATIVE=0): the same kernels
+    with the same arguments and dropout seeds, so the output and every gradient are bit-identical,
+    with dropout too (same torch seed -> same per-op seeds)."""
+    cfg = small_cfg(num_items=500, dropout=p_drop)
+    items = small_universe(500)
+    batch = to_dev(synth.make_batch(items, 96, seed=21), gpu)
+    lookup = items.pretrained.to(gpu)
+    from recsys_amd import dist as D
+    ix = D.prepare_step_index(batch, pretrained_lookup=lookup)
+    res = []
+    for native in (True, False):
+        torch.manual_seed(5)
+        model = T.SASRecUserTower(cfg).to(gpu).train()
+        prev = ops._TOWER_NATIVE
+        ops._TOWER_NATIVE = native
+        try:
+            pk, pk2, tok_ids, pv, static = ix.packed
+            assert ops.tower_native_ok(model, pk2, pv) == native
+            torch.manual_seed(9)
+            torch.cuda.manual_seed(9)
+            out = model.forward_packed(pk2, pv, tok_ids, *static)
+            g = torch.Generator(device="cpu").manual_seed(3)
+            w = torch.randn(out.shape, generator=g).to(gpu)
+            (out * w).sum().backward()
+        finally:
+            ops._TOWER_NATIVE = prev
+        torch.cuda.synchronize()
+        res.append((out.detach(), {n: p.grad.detach().clone() for n, p in model.named_parameters()
+                                   if p.grad is not None}))
+    (o1, g1), (o2, g2) = res
+    assert torch.equal(o1, o2)
+    assert g1.keys() == g2.keys() and len(g1) > 40
+    for n in g1:
+        assert torch.equal(g1[n], g2[n]), n
