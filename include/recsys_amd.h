@@ -440,11 +440,11 @@ int rsx_segment_sum_rows(const float* src, int64_t ld_src, const int64_t* perm, 
 /* The contrastive step's objective from its device loss sums, one launch instead of the
  * scalar tensor ops of train_user_tower_all_time (tower_code/v1_usertower_train.py:814-845):
  * main = s_main * inv_n (s_main nullable: 0), cl = s_un * inv_b + lambda_sup * s_sup / max(cnt, 1)
- * (s_sup nullable), total = main + lambda_cl * cl; out[6] = {total, main, cl} twice (the second
- * copy for logging / all-reduce). Backward: g3[3] = gradients of g * total w.r.t. s_main, s_un,
+ * (s_sup nullable), total = main + lambda_cl * cl; total[1] and logs[3] = {total, main, cl} (separate
+ * storage: a detached copy for logging / all-reduce). Backward: g3[3] = gradients of g * total w.r.t. s_main, s_un,
  * s_sup (cnt nullable when s_sup was). All device scalars. */
 int rsx_loss_combine(const float* s_main, const float* s_un, const float* s_sup, const float* cnt, float inv_n,
-                     float inv_b, float lambda_sup, float lambda_cl, float* out, void* stream);
+                     float inv_b, float lambda_sup, float lambda_cl, float* total, float* logs, void* stream);
 int rsx_loss_combine_bwd(const float* g, const float* cnt, float inv_n, float inv_b, float lambda_sup,
                          float lambda_cl, float* g3, void* stream);
 

@@ -85,7 +85,7 @@ _SIGS = {
     "rsx_gemm_x3": (c_i, [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_i, c_i, c_i, c_p, c_i64, c_f, c_u64, c_p, c_i64, c_p]),
     "rsx_gemm_x3_tn": (c_i, [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_i, c_i, c_i, c_p, c_i64, c_f, c_u64, c_p, c_i64,
                              c_p]),
-    "rsx_loss_combine": (c_i, [c_p, c_p, c_p, c_p, c_f, c_f, c_f, c_f, c_p, c_p]),
+    "rsx_loss_combine": (c_i, [c_p, c_p, c_p, c_p, c_f, c_f, c_f, c_f, c_p, c_p, c_p]),
     "rsx_loss_combine_bwd": (c_i, [c_p, c_p, c_f, c_f, c_f, c_f, c_p, c_p]),
     "rsx_tower_n_ptrs": (c_i64, [c_i]),
     "rsx_tower_arena_bytes": (c_i64, [c_i64, c_i64, c_i]),

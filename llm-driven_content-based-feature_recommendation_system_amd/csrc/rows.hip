@@ -195,16 +195,16 @@ __global__ __launch_bounds__(256) void ids_check_k(const int64_t* __restrict__ i
 // The contrastive step's objective from its device loss sums (train_user_tower_all_time,
 // tower_code/v1_usertower_train.py:814-845, per rank of the global batch: dist.py): main = s_main /
 // n, cl = s_un / b + lambda_sup * s_sup / max(cnt, 1), total = main + lambda_cl * cl.
-// out = {total, main, cl, total, main, cl} (the second three: detached copies for logging).
+// total[0] = total; logs = {total, main, cl} (separate storage: detached copies for logging).
 __global__ void loss_combine_k(const float* s_main, const float* s_un, const float* s_sup, const float* cnt,
-                               float inv_n, float inv_b, float lsup, float lcl, float* out) {
+                               float inv_n, float inv_b, float lsup, float lcl, float* total, float* logs) {
   if (threadIdx.x != 0) return;
   const float m = s_main ? s_main[0] * inv_n : 0.0f;
   float cl = s_un[0] * inv_b;
   if (s_sup) cl += lsup * (s_sup[0] / fmaxf(cnt[0], 1.0f));
   const float t = m + lcl * cl;
-  out[0] = t; out[1] = m; out[2] = cl;
-  out[3] = t; out[4] = m; out[5] = cl;
+  total[0] = t;
+  logs[0] = t; logs[1] = m; logs[2] = cl;
 }
 
 // its backward: g3 = {d/d s_main, d/d s_un, d/d s_sup} of g * total
@@ -220,10 +220,11 @@ __global__ void loss_combine_bwd_k(const float* g, const float* cnt, float inv_n
 }  // namespace
 
 RSX_API int rsx_loss_combine(const float* s_main, const float* s_un, const float* s_sup, const float* cnt,
-                             float inv_n, float inv_b, float lambda_sup, float lambda_cl, float* out, void* stream) {
-  RSX_ARG(s_un && out && (!s_sup || cnt), "null tensor");
+                             float inv_n, float inv_b, float lambda_sup, float lambda_cl, float* total, float* logs,
+                             void* stream) {
+  RSX_ARG(s_un && total && logs && (!s_sup || cnt), "null tensor");
   hipLaunchKernelGGL(loss_combine_k, dim3(1), dim3(64), 0, (hipStream_t)stream, s_main, s_un, s_sup, cnt, inv_n,
-                     inv_b, lambda_sup, lambda_cl, out);
+                     inv_b, lambda_sup, lambda_cl, total, logs);
   RSX_LAUNCHED();
   return 0;
 }

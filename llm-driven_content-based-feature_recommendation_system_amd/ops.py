@@ -688,16 +688,16 @@ class _LossCombine(torch.autograd.Function):
     @staticmethod
     def forward(ctx, s_main, s_un, s_sup, cnt, consts):
         inv_n, inv_b, lsup, lcl = consts
-        out = torch.empty(6, device=s_un.device, dtype=torch.float32)
+        total = torch.empty((), device=s_un.device, dtype=torch.float32)
+        logs = torch.empty(3, device=s_un.device, dtype=torch.float32)
         rc = N.lib().rsx_loss_combine(N.ptr(s_main), N.ptr(s_un), N.ptr(s_sup), N.ptr(cnt), inv_n, inv_b, lsup, lcl,
-                                      N.ptr(out), N.stream())
+                                      N.ptr(total), N.ptr(logs), N.stream())
         N.check(rc, "loss_combine")
         ctx.consts = consts
         ctx.has = (s_main is not None, s_sup is not None)
         ctx.save_for_backward(cnt)
-        logs = out[3:6]
         ctx.mark_non_differentiable(logs)
-        return out[0], logs
+        return total, logs
 
     @staticmethod
     def backward(ctx, g, _glogs):

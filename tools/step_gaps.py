@@ -11,11 +11,9 @@ MARK = "nce_grouped_fwdg_x3"
 
 
 def main():
-    rows = []
-    for f in glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True):
-        for r in csv.DictReader(open(f)):
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"][:70]))
-    rows.sort()
+    sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.abspath(__file__)))
+    from loss_overlap import load
+    rows = [(s, e, n[:70]) for s, e, n, _ in load(sys.argv[1])]
     marks = [i for i, r in enumerate(rows) if MARK in r[2]]
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 5
     gaps = collections.Counter()
