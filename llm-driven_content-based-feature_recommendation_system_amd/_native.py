@@ -24,7 +24,7 @@ c_i = ctypes.c_int
 c_f = ctypes.c_float
 c_u64 = ctypes.c_uint64
 
-ABI_VERSION = 3  # rsx_abi_version() of the library these signatures describe
+ABI_VERSION = 4  # rsx_abi_version() of the library these signatures describe
 
 # name -> (restype, argtypes)
 _SIGS = {

@@ -16,7 +16,7 @@ void set_error(const char* fmt, ...) {
 
 RSX_API const char* rsx_last_error(void) { return rsx::g_err; }
 
-RSX_API int rsx_abi_version(void) { return 3; }
+RSX_API int rsx_abi_version(void) { return 4; }
 
 // Device the library's kernels were compiled for; callers compare against the
 // running device's gcnArchName before the first launch.

@@ -442,21 +442,6 @@ def prepare_step_index(batch, pretrained_vecs=None, pretrained_lookup=None, n_it
     return ix
 
 
-def _tensors_of(obj, seen=None):
-    seen = set() if seen is None else seen
-    if id(obj) in seen:
-        return
-    seen.add(id(obj))
-    if torch.is_tensor(obj):
-        yield obj
-    elif isinstance(obj, (list, tuple)):
-        for x in obj:
-            yield from _tensors_of(x, seen)
-    elif hasattr(obj, "__dict__"):
-        for x in vars(obj).values():
-            yield from _tensors_of(x, seen)
-
-
 _PREP_STREAM = None
 
 
@@ -511,17 +496,41 @@ class IndexPrefetcher:
         self._ex.shutdown(wait=True)
 
 
+_HELD = []          # (index, event): adopted indexes kept alive until the consuming stream passed them
+_LAST_ADOPTED = None
+
+
 def _adopt(ix):
-    """Order the current stream after an async-prepared index and keep its memory alive for it."""
+    """Order the current stream after an async-prepared index and keep its memory alive for it.
+
+    The index's tensors were allocated on the prefetch stream, so once freed the caching allocator
+    may hand their blocks to that stream's next index while this stream's kernels of the step still
+    read them. Instead of a record_stream per tensor (~40 per index), the adopted index itself is held
+    until an event recorded on this stream at the NEXT adoption -- after all of its step's work --
+    has completed; then it is released."""
+    global _LAST_ADOPTED
     ev = getattr(ix, "ready", None)
     if ev is None:
         return
     cur = torch.cuda.current_stream()
     cur.wait_event(ev)
-    for t in _tensors_of(ix):
-        if t.is_cuda:
-            t.record_stream(cur)
     ix.ready = None
+    if _LAST_ADOPTED is not None:
+        done = torch.cuda.Event()
+        done.record(cur)
+        _HELD.append((_LAST_ADOPTED, done))
+    _LAST_ADOPTED = ix
+    while _HELD and _HELD[0][1].query():
+        _HELD.pop(0)
+
+
+def release_held_indexes(sync=True):
+    """Drop the indexes _adopt keeps alive (end of training); sync: wait for the device first."""
+    global _LAST_ADOPTED
+    if sync and torch.cuda.is_available():
+        torch.cuda.synchronize()
+    _HELD.clear()
+    _LAST_ADOPTED = None
 
 
 def contrastive_objective_dp(model, item_tower, log_q_tensor, batch, cfg, pretrained_lookup=None,
