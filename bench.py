@@ -809,7 +809,12 @@ def train_bench(args, global_batch, steps, warmup, items, cfg, model, item_tower
         import cProfile
         prof = cProfile.Profile()
         prof.enable()
-    for j in range(12 if prof else 3):
+    trace_path = os.environ.get("RSX_HOST_TRACE")  # torch.profiler CPU table of the same steps (tools only)
+    tprof = None
+    if trace_path:
+        tprof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU])
+        tprof.__enter__()
+    for j in range(12 if (prof or tprof) else 3):
         torch.cuda.synchronize()
         if world > 1:
             torch.distributed.barrier()
@@ -823,6 +828,10 @@ def train_bench(args, global_batch, steps, warmup, items, cfg, model, item_tower
     if prof is not None:
         prof.disable()
         prof.dump_stats(prof_path)
+    if tprof is not None:
+        tprof.__exit__(None, None, None)
+        with open(trace_path, "w") as f:
+            f.write(tprof.key_averages().table(sort_by="cpu_time_total", row_limit=120, max_name_column_width=90))
     unloaded = unloaded[1:]
     host_unloaded = {"index_inline_ms": round(1e3 * sum(u[0] for u in unloaded) / len(unloaded), 3),
                      "step_enqueue_ms": round(1e3 * sum(u[1] for u in unloaded) / len(unloaded), 3)}

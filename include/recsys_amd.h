@@ -200,7 +200,7 @@ int rsx_static_embed_fwd(const int64_t* const* ids, const float* const* tables, 
 int rsx_static_embed_bwd(const int64_t* const* ids, const float* const* tables, const int64_t* table_rows,
                          const int64_t* dims, const int64_t* padding_idx, int ntab, const float* gate,
                          const float* dout, int64_t ld_dout, int64_t B, float* const* dtables, float* dgate,
-                         void* stream);
+                         int accumulate, void* stream);
 
 /* ---- LayerNorm fused with the preceding residual add + dropout and a following GELU ----
  * s = x + dropout(res) (res nullable), y = act(LN(s) * w + b), act 0 none / 2 GELU(erf).
@@ -447,6 +447,44 @@ int rsx_loss_combine(const float* s_main, const float* s_un, const float* s_sup,
                      float inv_b, float lambda_sup, float lambda_cl, float* total, float* logs, void* stream);
 int rsx_loss_combine_bwd(const float* g, const float* cnt, float inv_n, float inv_b, float lambda_sup,
                          float lambda_cl, float* g3, void* stream);
+
+/* The user tower's static profile (v1_refine_usertower.py:472-494) as one call per direction:
+ *   u_g = sigmoid(static_gate); x = cat(E_j[id_j] * u_g[j] (j < ntab), relu(cont @ Wc^T + bc) * u_g[ntab]);
+ *   out = dropout_p(gelu_erf(LayerNorm(x @ Wm^T + bm)))     [U, 128]
+ * p[] pointer table (RSX_SP_*; table slots beyond ntab unused): ids int64 [U] and tables
+ * [rows_j, dim_j] per table, static_gate [ntab + 1] (raw parameter), cont [U, C], Wc [P, C],
+ * bc [P], Wm [128, K], bm [128], ln_w / ln_b [128]. dims[] = {U, ntab, C, P, K, rows[ntab],
+ * dim[ntab], padding_idx[ntab]} with sum(dim) + P == K <= 128, C <= 8, P <= 32. arena:
+ * rsx_static_profile_arena_bytes(U), written by the forward and read by the backward.
+ * Backward: grads[] parallel to p[] (the ids' and cont's slots unused), every gradient WRITTEN
+ * (padding rows 0); U > 0; ws: rsx_static_profile_bwd_workspace_bytes(U). Dropout mask
+ * hash(seed, row * 128 + col). */
+enum {
+  RSX_SP_IDS = 0, RSX_SP_TABLES = 16, RSX_SP_GATE = 32, RSX_SP_CONT = 33, RSX_SP_WC = 34, RSX_SP_BC = 35,
+  RSX_SP_WM = 36, RSX_SP_BM = 37, RSX_SP_LNW = 38, RSX_SP_LNB = 39, RSX_SP_N = 40
+};
+int64_t rsx_static_profile_arena_bytes(int64_t U);
+int64_t rsx_static_profile_bwd_workspace_bytes(int64_t U);
+int rsx_static_profile_fwd(const void* const* p, const int64_t* dims, float eps, float p_drop, uint64_t seed,
+                           void* arena, int64_t arena_bytes, float* out, void* stream);
+int rsx_static_profile_bwd(const void* const* p, const int64_t* dims, float p_drop, uint64_t seed, const void* arena,
+                           const float* dout, float* const* grads, void* ws, int64_t ws_bytes, void* stream);
+
+/* The step's tail: torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm) followed by
+ * torch.optim.AdamW.step() (tower_code/v1_usertower_train.py:852-853, :495-496) in two launches.
+ * n tensors, each fp32 contiguous with its gradient and both moments (exp_avg, exp_avg_sq);
+ * clip[i] != 0 marks the tensors whose gradients form the clipped norm (and are scaled in
+ * place by min(max_norm / (norm + 1e-6), 1), as clip_grad_norm_ does); the others (e.g. the item
+ * matrix's parameter group) get the unclipped update. Per-tensor hyper-parameters lr,
+ * weight_decay, beta1, beta2, eps; the step count AFTER this step's increment is step_dev[i][0]
+ * (a device scalar, torch's fused/capturable state) when step_dev and step_dev[i] are non-null,
+ * else step[i]. norm_out (device, nullable) receives the total norm. Deterministic: fixed-slot
+ * partials reduced in a fixed order. ws: rsx_clip_adamw_workspace_bytes(n, numel, clip). */
+int64_t rsx_clip_adamw_workspace_bytes(int n, const int64_t* numel, const int* clip);
+int rsx_clip_adamw(int n, float* const* params, float* const* grads, float* const* exp_avg, float* const* exp_avg_sq,
+                   const int64_t* numel, const int* clip, const float* step, const float* const* step_dev,
+                   const float* lr, const float* weight_decay, const float* beta1, const float* beta2,
+                   const float* eps, float max_norm, void* ws, int64_t ws_bytes, float* norm_out, void* stream);
 
 /* Hard-negative mining: for each row i of u_norm [N,D] against the columns
  * i_norm [N,D] (both already L2-normalised), ignore column j when target_ids[j] ==

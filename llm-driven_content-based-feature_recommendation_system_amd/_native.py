@@ -73,7 +73,7 @@ _SIGS = {
     "rsx_linear_fwd": (c_i, [c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i64, c_i, c_p, c_p]),
     "rsx_linear_dot_fwd": (c_i, [c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i64, c_i, c_p, c_p, c_p, c_p, c_p]),
     "rsx_static_embed_fwd": (c_i, [c_p, c_p, c_p, c_p, c_i, c_p, c_i64, c_p, c_i64, c_p]),
-    "rsx_static_embed_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_i, c_p, c_p, c_i64, c_i64, c_p, c_p, c_p]),
+    "rsx_static_embed_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_i, c_p, c_p, c_i64, c_i64, c_p, c_p, c_i, c_p]),
     "rsx_dropout_bwd": (c_i, [c_p, c_i64, c_i64, c_f, c_u64, c_p, c_p]),
     "rsx_ln_fwd": (c_i, [c_p, c_p, c_f, c_u64, c_p, c_p, c_f, c_i, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p]),
     "rsx_ln_bwd_workspace_floats": (c_i64, [c_i64, c_i64]),
@@ -87,6 +87,13 @@ _SIGS = {
                              c_p]),
     "rsx_loss_combine": (c_i, [c_p, c_p, c_p, c_p, c_f, c_f, c_f, c_f, c_p, c_p, c_p]),
     "rsx_loss_combine_bwd": (c_i, [c_p, c_p, c_f, c_f, c_f, c_f, c_p, c_p]),
+    "rsx_static_profile_arena_bytes": (c_i64, [c_i64]),
+    "rsx_static_profile_bwd_workspace_bytes": (c_i64, [c_i64]),
+    "rsx_static_profile_fwd": (c_i, [c_p, c_p, c_f, c_f, c_u64, c_p, c_i64, c_p, c_p]),
+    "rsx_static_profile_bwd": (c_i, [c_p, c_p, c_f, c_u64, c_p, c_p, c_p, c_p, c_i64, c_p]),
+    "rsx_clip_adamw_workspace_bytes": (c_i64, [c_i, c_p, c_p]),
+    "rsx_clip_adamw": (c_i, [c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_i64,
+                             c_p, c_p]),
     "rsx_tower_n_ptrs": (c_i64, [c_i]),
     "rsx_tower_arena_bytes": (c_i64, [c_i64, c_i64, c_i]),
     "rsx_tower_bwd_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64, c_i, c_i64]),

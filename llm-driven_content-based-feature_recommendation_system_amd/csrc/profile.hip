@@ -1,0 +1,321 @@
+// The user tower's static profile as one native call per direction (include/recsys_amd.h
+// rsx_static_profile_fwd / rsx_static_profile_bwd).
+//
+// Reference: SASRecUserTower phase 2 (tower_code/v1_refine_usertower.py:472-494):
+//   u_g  = sigmoid(static_gate)                                   [10]
+//   x    = cat(E_j(id_j) * u_g[j] for the nine tables,            [U, 84]
+//              relu(cont_proj(cont_feats)) * u_g[9])              [U, 16]
+//   prof = Dropout(GELU(LayerNorm(static_mlp[0](x))))             [U, 128]
+// PyTorch runs this as ~25 forward and ~35 backward launches (nine gathers, a library GEMM for
+// the 4 -> 16 projection, ReLU / gate products, cat, the MLP GEMM, LayerNorm, GELU, dropout, and
+// every op's backward node). Here: forward = one kernel that builds the whole [U, 128] input row
+// (the nine gated gathers, the 4 -> 16 projection + ReLU + gate, zero padding to 128 columns) and
+// the zero-padded [128, 128] MLP weight, then the library's bf16x3 GEMM, fused LayerNorm + GELU
+// and dropout kernels. Backward = dropout, LayerNorm + GELU backward (dW / db of the norm), the
+// MLP's weight gradient and input gradient, the nine tables' gradients (rsx_static_embed_bwd in
+// write mode) and one tail kernel for the projection's gradients, the gates' sigmoid backward and
+// the [128, 100] weight slice. All reductions have a fixed order (bit-reproducible).
+#include "rsx_common.h"
+#include "recsys_amd.h"
+
+namespace {
+
+constexpr int kD = 128, kKp = 128, kMaxTab = 16, kMaxC = 8, kMaxP = 32;
+
+int64_t al(int64_t floats) { return (floats + 63) / 64 * 64; }  // 256-B granules
+
+struct Cfg {
+  int64_t U;
+  int ntab, C, P, K, ncols;  // ncols = table columns (the projection's start column)
+  int64_t rows[kMaxTab], dims[kMaxTab], pad[kMaxTab];
+  int col_off[kMaxTab + 1];
+};
+
+struct ArenaLayout {
+  int64_t X, Wp, H, mean, rstd, ug, total;
+};
+ArenaLayout arena_layout(int64_t U) {
+  ArenaLayout s{};
+  int64_t o = 0;
+  auto take = [&](int64_t n) { const int64_t r = o; o += al(n); return r; };
+  s.X = take(U * kKp); s.Wp = take(kD * kKp); s.H = take(U * kD); s.mean = take(U); s.rstd = take(U);
+  s.ug = take(kMaxTab + 1);
+  s.total = o;
+  return s;
+}
+
+struct WsLayout {
+  int64_t dY, dH, dX, dWp, dgu, wsw, wsl, total, n_wsw, n_wsl;
+};
+WsLayout ws_layout(int64_t U) {
+  WsLayout s{};
+  int64_t o = 0;
+  auto take = [&](int64_t n) { const int64_t r = o; o += al(n); return r; };
+  s.dY = take(U * kD); s.dH = take(U * kD); s.dX = take(U * kKp); s.dWp = take(kD * kKp); s.dgu = take(kMaxTab + 1);
+  s.n_wsw = rsx_linear_wgrad_workspace_floats(U, kD, kKp);
+  s.n_wsl = rsx_ln_bwd_workspace_floats(U, kD);
+  s.wsw = take(s.n_wsw); s.wsl = take(s.n_wsl);
+  s.total = o;
+  return s;
+}
+
+int parse(Cfg& c, const int64_t* dims) {
+  c.U = dims[0];
+  c.ntab = (int)dims[1];
+  c.C = (int)dims[2];
+  c.P = (int)dims[3];
+  c.K = (int)dims[4];
+  RSX_ARG(c.U >= 0 && c.ntab >= 1 && c.ntab <= kMaxTab, "1..16 tables");
+  RSX_ARG(c.C >= 1 && c.C <= kMaxC && c.P >= 1 && c.P <= kMaxP, "continuous features 1..8, projection 1..32");
+  int off = 0;
+  for (int j = 0; j < c.ntab; ++j) {
+    c.rows[j] = dims[5 + j];
+    c.dims[j] = dims[5 + c.ntab + j];
+    c.pad[j] = dims[5 + 2 * c.ntab + j];
+    RSX_ARG(c.rows[j] >= 1 && c.dims[j] >= 1, "empty table");
+    c.col_off[j] = off;
+    off += (int)c.dims[j];
+  }
+  c.col_off[c.ntab] = off;
+  c.ncols = off;
+  RSX_ARG(c.ncols + c.P == c.K && c.K <= kKp, "table columns + projection width must equal K <= 128");
+  return 0;
+}
+
+struct InArgs {
+  const int64_t* ids[kMaxTab];
+  const float* tab[kMaxTab];
+  int dim[kMaxTab];
+  int col_off[kMaxTab + 1];
+  int ntab, C, P, K, ncols;
+  const float* gate;  // static_gate [ntab + 1] (raw parameter)
+  const float* cont;  // [U, C]
+  const float* wc;    // [P, C]
+  const float* bc;    // [P]
+  const float* wm;    // [128, K]
+  float* X;           // [U, 128]
+  float* Wp;          // [128, 128]
+  float* ug;          // [ntab + 1] sigmoid(static_gate), for the backward
+  int64_t U, x_blocks;
+};
+
+__device__ __forceinline__ float sigm(float g) { return 1.0f / (1.0f + __expf(-g)); }
+
+__global__ __launch_bounds__(256) void prof_in_k(InArgs a) {
+  if (blockIdx.x >= a.x_blocks) {  // the zero-padded MLP weight [128, 128]
+    const int64_t e = (blockIdx.x - a.x_blocks) * 256 + threadIdx.x;
+    if (e < kD * kKp) {
+      const int n = (int)(e / kKp), k = (int)(e % kKp);
+      a.Wp[e] = k < a.K ? a.wm[(int64_t)n * a.K + k] : 0.0f;
+    }
+    return;
+  }
+  if (blockIdx.x == 0 && threadIdx.x <= a.ntab) a.ug[threadIdx.x] = sigm(a.gate[threadIdx.x]);
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= a.U * kKp) return;
+  const int64_t r = e / kKp;
+  const int c = (int)(e % kKp);
+  float v = 0.0f;
+  if (c < a.ncols) {
+    int j = 0;
+    while (j + 1 < a.ntab && c >= a.col_off[j + 1]) ++j;
+    const int64_t id = a.ids[j][r];
+    v = a.tab[j][id * a.dim[j] + (c - a.col_off[j])] * sigm(a.gate[j]);
+  } else if (c < a.K) {
+    const int q = c - a.ncols;
+    float pre = a.bc[q];
+    for (int k = 0; k < a.C; ++k) pre += a.cont[r * a.C + k] * a.wc[q * a.C + k];
+    v = fmaxf(pre, 0.0f) * sigm(a.gate[a.ntab]);
+  }
+  a.X[e] = v;
+}
+
+struct TailArgs {
+  const float* dX;    // [U, 128]
+  const float* cont;  // [U, C]
+  const float* wc;
+  const float* bc;
+  const float* ug;    // [ntab + 1]
+  const float* dgu;   // [ntab] table-gate gradients (rsx_static_embed_bwd)
+  const float* dWp;   // [128, 128]
+  float* dwc;         // [P, C]
+  float* dbc;         // [P]
+  float* dgate;       // [ntab + 1] gradient of the raw static_gate
+  float* dwm;         // [128, K]
+  int64_t U;
+  int ntab, C, P, K, ncols;
+};
+
+constexpr int kTail = 1024;
+
+// block 0: the projection's gradients and the gates'; blocks >= 1: the [128, K] weight slice.
+// Block 0's thread (slice s, output o) sums output o over the rows s, s + nslice, ...; outputs
+// are dWc[q][k] (P*C), dbc[q] (P) and the per-column part of the cont gate's gradient (P); the
+// slices meet in LDS and are summed in slice order.
+__global__ __launch_bounds__(kTail) void prof_tail_k(TailArgs a) {
+  if (blockIdx.x > 0) {
+    for (int64_t e = (int64_t)(blockIdx.x - 1) * kTail + threadIdx.x; e < (int64_t)kD * a.K;
+         e += (int64_t)(gridDim.x - 1) * kTail) {
+      const int64_t n = e / a.K, k = e % a.K;
+      a.dwm[e] = a.dWp[n * kKp + k];
+    }
+    return;
+  }
+  __shared__ float part[kTail];
+  __shared__ float outs[kMaxP * kMaxC + 2 * kMaxP];
+  const int nout = a.P * a.C + 2 * a.P;
+  const int nslice = kTail / nout;
+  const int t = threadIdx.x, o = t % nout, s = t / nout;
+  const float g9 = a.ug[a.ntab];
+  float acc = 0.0f;
+  if (s < nslice) {
+    const int q = o < a.P * a.C ? o / a.C : (o < a.P * a.C + a.P ? o - a.P * a.C : o - a.P * a.C - a.P);
+    const int kk = o < a.P * a.C ? o % a.C : -1;
+    const int kind = o < a.P * a.C ? 0 : (o < a.P * a.C + a.P ? 1 : 2);
+    for (int64_t r = s; r < a.U; r += nslice) {
+      float pre = a.bc[q];
+      for (int k = 0; k < a.C; ++k) pre += a.cont[r * a.C + k] * a.wc[q * a.C + k];
+      const float dc = a.dX[r * kKp + a.ncols + q];
+      if (kind == 2) {
+        acc += dc * fmaxf(pre, 0.0f);
+      } else {
+        const float dpre = pre > 0.0f ? dc * g9 : 0.0f;
+        acc += kind == 0 ? dpre * a.cont[r * a.C + kk] : dpre;
+      }
+    }
+  }
+  part[t] = acc;
+  __syncthreads();
+  if (t < nout) {
+    float v = 0.0f;
+    for (int q2 = 0; q2 < nslice; ++q2) v += part[q2 * nout + t];
+    outs[t] = v;
+  }
+  __syncthreads();
+  if (t < a.P * a.C) a.dwc[t] = outs[t];
+  else if (t < a.P * a.C + a.P) a.dbc[t - a.P * a.C] = outs[t];
+  if (t <= a.ntab) {
+    float dg;
+    if (t < a.ntab) {
+      dg = a.dgu[t];
+    } else {
+      dg = 0.0f;
+      for (int q = 0; q < a.P; ++q) dg += outs[a.P * a.C + a.P + q];
+    }
+    const float sg = a.ug[t];
+    a.dgate[t] = dg * (1.0f - sg) * sg;  // torch's sigmoid backward
+  }
+}
+
+#define SP_CALL(x)            \
+  do {                        \
+    const int rc_ = (x);      \
+    if (rc_ != 0) return rc_; \
+  } while (0)
+
+}  // namespace
+
+RSX_API int64_t rsx_static_profile_arena_bytes(int64_t U) { return U < 0 ? -1 : arena_layout(U).total * 4; }
+RSX_API int64_t rsx_static_profile_bwd_workspace_bytes(int64_t U) { return U < 0 ? -1 : ws_layout(U).total * 4; }
+
+RSX_API int rsx_static_profile_fwd(const void* const* p, const int64_t* dims, float eps, float p_drop, uint64_t seed,
+                                   void* arena, int64_t arena_bytes, float* out, void* stream) {
+  RSX_ARG(p && dims && arena && out, "null argument");
+  Cfg c;
+  SP_CALL(parse(c, dims));
+  const ArenaLayout s = arena_layout(c.U);
+  RSX_ARG(arena_bytes >= s.total * 4, "arena too small (rsx_static_profile_arena_bytes)");
+  RSX_ARG(p_drop >= 0.0f && p_drop < 1.0f, "p_drop must be in [0, 1)");
+  for (int i = 0; i < RSX_SP_N; ++i)
+    if ((i < RSX_SP_IDS + c.ntab || i >= RSX_SP_IDS + kMaxTab) && (i < RSX_SP_TABLES + c.ntab || i >= RSX_SP_TABLES + kMaxTab))
+      RSX_ARG(p[i] != nullptr, "null input / parameter pointer");
+  if (c.U == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  float* A = static_cast<float*>(arena);
+  InArgs a{};
+  for (int j = 0; j < c.ntab; ++j) {
+    a.ids[j] = static_cast<const int64_t*>(p[RSX_SP_IDS + j]);
+    a.tab[j] = static_cast<const float*>(p[RSX_SP_TABLES + j]);
+    a.dim[j] = (int)c.dims[j];
+  }
+  for (int j = 0; j <= c.ntab; ++j) a.col_off[j] = c.col_off[j];
+  a.ntab = c.ntab; a.C = c.C; a.P = c.P; a.K = c.K; a.ncols = c.ncols;
+  a.gate = static_cast<const float*>(p[RSX_SP_GATE]);
+  a.cont = static_cast<const float*>(p[RSX_SP_CONT]);
+  a.wc = static_cast<const float*>(p[RSX_SP_WC]);
+  a.bc = static_cast<const float*>(p[RSX_SP_BC]);
+  a.wm = static_cast<const float*>(p[RSX_SP_WM]);
+  a.X = A + s.X; a.Wp = A + s.Wp; a.ug = A + s.ug;
+  a.U = c.U;
+  a.x_blocks = (c.U * kKp + 255) / 256;
+  const int64_t blocks = a.x_blocks + (kD * kKp + 255) / 256;
+  hipLaunchKernelGGL(prof_in_k, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  RSX_LAUNCHED();
+  SP_CALL(rsx_gemm_x3(A + s.X, kKp, A + s.Wp, kKp, static_cast<const float*>(p[RSX_SP_BM]), c.U, kD, kKp, 0, nullptr,
+                      0, 0.0f, 0, A + s.H, kD, stream));
+  SP_CALL(rsx_ln_fwd(A + s.H, nullptr, 0.0f, 0, static_cast<const float*>(p[RSX_SP_LNW]),
+                     static_cast<const float*>(p[RSX_SP_LNB]), eps, 2, c.U, kD, nullptr, out, A + s.mean, A + s.rstd,
+                     stream));
+  // Dropout(p) after the GELU: the keep-mask hash(seed, row * 128 + col) applied in place (the
+  // dropout "backward" kernel is the same elementwise mask-and-scale)
+  if (p_drop > 0.0f) SP_CALL(rsx_dropout_bwd(out, c.U, kD, p_drop, seed, out, stream));
+  return 0;
+}
+
+RSX_API int rsx_static_profile_bwd(const void* const* p, const int64_t* dims, float p_drop, uint64_t seed,
+                                   const void* arena, const float* dout, float* const* grads, void* ws,
+                                   int64_t ws_bytes, void* stream) {
+  RSX_ARG(p && dims && arena && dout && grads && ws, "null argument");
+  Cfg c;
+  SP_CALL(parse(c, dims));
+  const WsLayout w = ws_layout(c.U);
+  const ArenaLayout s = arena_layout(c.U);
+  RSX_ARG(c.U > 0, "U must be > 0");
+  RSX_ARG(ws_bytes >= w.total * 4, "workspace too small (rsx_static_profile_bwd_workspace_bytes)");
+  for (int i = RSX_SP_GATE; i < RSX_SP_N; ++i)
+    if (i != RSX_SP_CONT) RSX_ARG(grads[i] != nullptr, "null parameter gradient");
+  for (int j = 0; j < c.ntab; ++j) RSX_ARG(grads[RSX_SP_TABLES + j] != nullptr, "null table gradient");
+  hipStream_t st = (hipStream_t)stream;
+  const float* A = static_cast<const float*>(arena);
+  float* W = static_cast<float*>(ws);
+  const float* dY = dout;
+  if (c.U > 0 && p_drop > 0.0f) {
+    SP_CALL(rsx_dropout_bwd(dout, c.U, kD, p_drop, seed, W + w.dY, stream));
+    dY = W + w.dY;
+  }
+  SP_CALL(rsx_ln_bwd(A + s.H, A + s.mean, A + s.rstd, static_cast<const float*>(p[RSX_SP_LNW]),
+                     static_cast<const float*>(p[RSX_SP_LNB]), 2, dY, nullptr, 0.0f, 0, c.U, kD, W + w.dH, nullptr,
+                     grads[RSX_SP_LNW], grads[RSX_SP_LNB], W + w.wsl, w.n_wsl, stream));
+  SP_CALL(rsx_linear_wgrad_x3(W + w.dH, kD, A + s.X, kKp, c.U, kD, kKp, W + w.dWp, kKp, grads[RSX_SP_BM], 0,
+                              W + w.wsw, w.n_wsw, stream));
+  if (c.U > 0)
+    SP_CALL(rsx_gemm_x3_tn(W + w.dH, kD, A + s.Wp, kKp, nullptr, c.U, kKp, kD, 0, nullptr, 0, 0.0f, 0, W + w.dX, kKp,
+                           stream));
+  const int64_t* ids[kMaxTab];
+  const float* tabs[kMaxTab];
+  float* dtabs[kMaxTab];
+  for (int j = 0; j < c.ntab; ++j) {
+    ids[j] = static_cast<const int64_t*>(p[RSX_SP_IDS + j]);
+    tabs[j] = static_cast<const float*>(p[RSX_SP_TABLES + j]);
+    dtabs[j] = grads[RSX_SP_TABLES + j];
+  }
+  SP_CALL(rsx_static_embed_bwd(ids, tabs, c.rows, c.dims, c.pad, c.ntab, A + s.ug, W + w.dX, kKp, c.U, dtabs,
+                               W + w.dgu, 0, stream));
+  TailArgs t{};
+  t.dX = W + w.dX;
+  t.cont = static_cast<const float*>(p[RSX_SP_CONT]);
+  t.wc = static_cast<const float*>(p[RSX_SP_WC]);
+  t.bc = static_cast<const float*>(p[RSX_SP_BC]);
+  t.ug = A + s.ug;
+  t.dgu = W + w.dgu;
+  t.dWp = W + w.dWp;
+  t.dwc = grads[RSX_SP_WC];
+  t.dbc = grads[RSX_SP_BC];
+  t.dgate = grads[RSX_SP_GATE];
+  t.dwm = grads[RSX_SP_WM];
+  t.U = c.U;
+  t.ntab = c.ntab; t.C = c.C; t.P = c.P; t.K = c.K; t.ncols = c.ncols;
+  hipLaunchKernelGGL(prof_tail_k, dim3(1 + 16), dim3(kTail), 0, st, t);
+  RSX_LAUNCHED();
+  return 0;
+}

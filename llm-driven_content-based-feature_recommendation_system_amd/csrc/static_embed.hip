@@ -10,6 +10,7 @@
 // few hundred floats): the backward gives each table one workgroup that sums its gradient and
 // its gate gradient sum_b <dout_j, E_j[id_j[b]]> over the users in a fixed order
 // (deterministic, no atomics). padding_idx rows (nn.Embedding semantics) receive no gradient.
+// The backward adds into dE / dgate (autograd accumulation) or, with accumulate = 0, writes them.
 #include "rsx_common.h"
 
 namespace {
@@ -28,6 +29,7 @@ struct SArgs {
   int lds_off[kMaxTab];   // offset of table j's gradient in LDS
   int rows[kMaxTab];
   int ntab, ncols;
+  int accumulate;         // backward: 1 adds into dE / dgate, 0 writes them (padding rows get 0)
   const float* gate;      // [ntab] (nullable: 1)
   float* dgate;           // [ntab] (nullable)
   const float* dout;      // [B, ld_out]
@@ -98,7 +100,12 @@ __global__ __launch_bounds__(1024) void static_embed_bwd_k(SArgs a) {
         if (r0 + r < R && r0 + r != a.pad_idx[j]) {
           float sum = 0.0f;
           for (int q = 0; q < nslice; ++q) sum += part[(q * kRowChunk + r) * dim + c2];
-          dtab[(int64_t)(r0 + r) * dim + c2] += sum * g;
+          if (a.accumulate)
+            dtab[(int64_t)(r0 + r) * dim + c2] += sum * g;
+          else
+            dtab[(int64_t)(r0 + r) * dim + c2] = sum * g;
+        } else if (r0 + r < R && !a.accumulate) {
+          dtab[(int64_t)(r0 + r) * dim + c2] = 0.0f;
         }
       }
     }
@@ -111,7 +118,10 @@ __global__ __launch_bounds__(1024) void static_embed_bwd_k(SArgs a) {
     if (t == 0) {
       float total = 0.0f;
       for (int i = 0; i < kBwdThreads / 64; ++i) total += wsum[i];
-      a.dgate[j] += total;
+      if (a.accumulate)
+        a.dgate[j] += total;
+      else
+        a.dgate[j] = total;
     }
   }
 }
@@ -139,6 +149,7 @@ bool fill(SArgs& a, const int64_t* const* ids, const float* const* tables, const
   }
   a.ntab = ntab;
   a.ncols = c;
+  a.accumulate = 1;
   return c <= kMaxCols && l <= kMaxFloats;
 }
 
@@ -163,7 +174,7 @@ RSX_API int rsx_static_embed_fwd(const int64_t* const* ids, const float* const* 
 RSX_API int rsx_static_embed_bwd(const int64_t* const* ids, const float* const* tables, const int64_t* table_rows,
                                  const int64_t* dims, const int64_t* padding_idx, int ntab, const float* gate,
                                  const float* dout, int64_t ld_dout, int64_t B, float* const* dtables, float* dgate,
-                                 void* stream) {
+                                 int accumulate, void* stream) {
   RSX_ARG(ids && tables && table_rows && dims && dout, "null argument");
   SArgs a;
   RSX_ARG(fill(a, ids, tables, table_rows, dims, ntab), "tables: 1..16, <= 256 columns, <= 4096 floats in total");
@@ -172,9 +183,10 @@ RSX_API int rsx_static_embed_bwd(const int64_t* const* ids, const float* const* 
     a.dtab[j] = dtables ? dtables[j] : nullptr;
     a.pad_idx[j] = padding_idx ? padding_idx[j] : -1;
   }
-  if (B == 0) return 0;
+  if (B == 0 && accumulate) return 0;  // write mode still writes (zero) gradients
   a.gate = gate; a.dgate = dgate; a.dout = dout; a.out = nullptr; a.B = B; a.ld_out = ld_dout;
   a.rows_per_block = 0;
+  a.accumulate = accumulate ? 1 : 0;
   hipLaunchKernelGGL(static_embed_bwd_k, dim3((unsigned)ntab), dim3(kBwdThreads), 0, (hipStream_t)stream, a);
   RSX_LAUNCHED();
   return 0;

@@ -600,13 +600,15 @@ def contrastive_step_dp(model, item_tower, log_q_tensor, batch, optimizer, cfg, 
     clip_grad_norm_(5.0) on the summed gradients, AdamW (replicated, identical on all ranks).
     index: the batch's StepIndex prepared ahead (e.g. prepare_step_index_async while the
     previous step runs); built inline if None."""
-    optimizer.zero_grad(set_to_none=True)
+    ops.zero_grad_(optimizer)
     objective, total, main, cl = contrastive_objective_dp(model, item_tower, log_q_tensor, batch, cfg,
                                                           pretrained_lookup=pretrained_lookup, index=index)
     objective.backward()
     bucket()
-    torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=max_norm)
-    optimizer.step()
+    # clip + AdamW in two launches (rsx_clip_adamw); torch's pair for optimizers it does not cover
+    if ops.clip_adamw_step(optimizer, model.parameters(), max_norm) is None:
+        torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=max_norm)
+        optimizer.step()
     return total, main, cl
 
 

@@ -721,6 +721,113 @@ def loss_combine(s_main, s_un, s_sup, cnt, n, b, lambda_sup, lambda_cl):
 
 
 # ----------------------------------------------------------------------------------------
+# The step's tail: clip_grad_norm_ + AdamW.step (v1_usertower_train.py:852-853), rsx_clip_adamw
+_CLIP_ADAMW = os.environ.get("RSX_CLIP_ADAMW", "1") != "0"
+
+
+def _adamw_native_ok(opt) -> bool:
+    """torch.optim.AdamW configurations rsx_clip_adamw reproduces: no amsgrad / maximize /
+    capturable / differentiable, float hyper-parameters, no step hooks."""
+    if type(opt) is not torch.optim.AdamW or opt._optimizer_step_pre_hooks or opt._optimizer_step_post_hooks:
+        return False
+    from torch.optim import optimizer as _om
+    if _om._global_optimizer_pre_hooks or _om._global_optimizer_post_hooks:
+        return False
+    if torch.get_default_dtype() != torch.float32:
+        return False
+    for g in opt.param_groups:
+        if g.get("amsgrad") or g.get("maximize") or g.get("capturable") or g.get("differentiable"):
+            return False
+        if not g.get("decoupled_weight_decay", True):
+            return False
+        if any(isinstance(v, torch.Tensor) for v in (g["lr"], g["eps"], g["weight_decay"], *g["betas"])):
+            return False
+    return True
+
+
+def clip_adamw_step(optimizer, clip_params, max_norm: float):
+    """torch.nn.utils.clip_grad_norm_(clip_params, max_norm) followed by optimizer.step() for a
+    torch.optim.AdamW, as two launches (rsx_clip_adamw) instead of torch's ~10 (per-tensor norms,
+    stack, norm, clamp, foreach multiply, the AdamW kernels) and their ~1 ms of host time.
+    Same state (optimizer.state[p]: step / exp_avg / exp_avg_sq, created as torch does), same
+    in-place gradient scaling; the update follows torch's fused AdamW arithmetic. Returns the
+    total norm (device scalar), or None when the optimizer or a tensor is one this does not
+    handle (sparse / non-fp32 / non-contiguous / CPU, a clipped parameter the optimizer does not
+    own): then nothing was changed and the caller runs torch's pair."""
+    if not _CLIP_ADAMW or not _adamw_native_ok(optimizer):
+        return None
+    clip_ids = {id(p) for p in clip_params if p.grad is not None}
+    items = []
+    for g in optimizer.param_groups:
+        for p in g["params"]:
+            gr = p.grad
+            if gr is None:
+                continue
+            if (gr.is_sparse or p.dtype != torch.float32 or gr.dtype != torch.float32 or p.device.type != "cuda"
+                    or not p.is_contiguous() or not gr.is_contiguous() or gr.shape != p.shape):
+                return None
+            items.append((p, gr, g))
+    if not items:
+        return None
+    if sum(1 for p, _, _ in items if id(p) in clip_ids) != len(clip_ids):
+        return None
+    N.ensure_device(items[0][0])
+    state = optimizer.state
+    dev_steps, cpu_steps = [], []
+    m_l, v_l = [], []
+    for p, gr, g in items:
+        st = state[p]
+        if len(st) == 0:   # torch.optim.Adam._init_group
+            st["step"] = (torch.zeros((), dtype=torch.float32, device=p.device) if g["fused"]
+                          else torch.tensor(0.0, dtype=torch.float32))
+            st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        m, v, s = st["exp_avg"], st["exp_avg_sq"], st["step"]
+        if not (m.is_contiguous() and v.is_contiguous() and m.dtype == torch.float32 and v.dtype == torch.float32):
+            return None
+        m_l.append(m)
+        v_l.append(v)
+        (dev_steps if s.device.type == "cuda" else cpu_steps).append(s)
+    # the step counts first, as torch's AdamW does (one multi-tensor launch for device counts)
+    if dev_steps:
+        torch._foreach_add_(dev_steps, 1.0)
+    if cpu_steps:
+        torch._foreach_add_(cpu_steps, 1.0)
+    n = len(items)
+    ps = N.ptr_array([p for p, _, _ in items])
+    gs = N.ptr_array([gr for _, gr, _ in items])
+    ms = N.ptr_array(m_l)
+    vs = N.ptr_array(v_l)
+    numel = N.i64_array([p.numel() for p, _, _ in items])
+    clip = (ctypes.c_int * n)(*[1 if id(p) in clip_ids else 0 for p, _, _ in items])
+    steps_t = [state[p]["step"] for p, _, _ in items]
+    step_h = (ctypes.c_float * n)(*[0.0 if s.device.type == "cuda" else float(s) for s in steps_t])
+    step_d = N.ptr_array([s if s.device.type == "cuda" else None for s in steps_t]) if dev_steps else None
+    lr = (ctypes.c_float * n)(*[g["lr"] for _, _, g in items])
+    wd = (ctypes.c_float * n)(*[g["weight_decay"] for _, _, g in items])
+    b1 = (ctypes.c_float * n)(*[g["betas"][0] for _, _, g in items])
+    b2 = (ctypes.c_float * n)(*[g["betas"][1] for _, _, g in items])
+    eps = (ctypes.c_float * n)(*[g["eps"] for _, _, g in items])
+    lib = N.lib()
+    nbytes = lib.rsx_clip_adamw_workspace_bytes(n, numel, clip)
+    dev = items[0][0].device
+    ws = torch.empty(nbytes, device=dev, dtype=torch.uint8)
+    norm = torch.empty((), device=dev, dtype=torch.float32)
+    rc = lib.rsx_clip_adamw(n, ps, gs, ms, vs, numel, clip, step_h, step_d, lr, wd, b1, b2, eps, float(max_norm),
+                            N.ptr(ws), nbytes, N.ptr(norm), N.stream())
+    N.check(rc, "clip_adamw")
+    optimizer._opt_called = True   # what torch's step wrapper records (LR schedulers check it)
+    return norm
+
+
+def zero_grad_(optimizer) -> None:
+    """optimizer.zero_grad(set_to_none=True) without the profiler record_function around it."""
+    for g in optimizer.param_groups:
+        for p in g["params"]:
+            p.grad = None
+
+
+# ----------------------------------------------------------------------------------------
 # Static-profile embeddings (several tiny gated tables, concatenated): rsx_static_embed_*
 class _StaticEmbed(torch.autograd.Function):
     @staticmethod
@@ -746,14 +853,14 @@ class _StaticEmbed(torch.autograd.Function):
         saved = ctx.saved_tensors
         gate, ids, tables = saved[0], list(saved[1:1 + nt]), list(saved[1 + nt:1 + 2 * nt])
         need = ctx.needs_input_grad
-        dgate, *dtabs = _zeros_group([gate if need[0] else None] +
+        dgate, *dtabs = _empty_group([gate if need[0] else None] +
                                      [t if need[3 + j] else None for j, t in enumerate(tables)])
         dout = _c(dout)
         rc = N.lib().rsx_static_embed_bwd(N.ptr_array(ids), N.ptr_array(tables),
                                           N.i64_array([t.shape[0] for t in tables]),
                                           N.i64_array([t.shape[1] for t in tables]), N.i64_array(pad), nt,
                                           N.ptr(gate), N.ptr(dout), dout.stride(0), ids[0].shape[0],
-                                          N.ptr_array(dtabs), N.ptr(dgate), N.stream())
+                                          N.ptr_array(dtabs), N.ptr(dgate), 0, N.stream())  # written
         N.check(rc, "static_embed_bwd")
         return (dgate, None, None, *dtabs)
 
@@ -765,6 +872,72 @@ def static_embed(ids, tables, gate, padding_idx=None):
         padding_idx = [-1] * len(tables)
     padding_idx = [(-1 if p is None else int(p)) for p in padding_idx]
     return _StaticEmbed.apply(gate, list(ids), padding_idx, *tables)
+
+
+# ----------------------------------------------------------------------------------------
+# A4: the static profile as one native call per direction (rsx_static_profile_*)
+_SP_IDS, _SP_TABLES, _SP_GATE, _SP_N = 0, 16, 32, 40
+
+
+class _StaticProfile(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, cfg, static_gate, cont, wc, bc, wm, bm, ln_w, ln_b, *tables):
+        ids, pads, eps, p_drop, seed = cfg
+        N.ensure_device(static_gate)
+        ids = [_c(t) for t in ids]
+        tables = [_c(t) for t in tables]
+        params = [_c(t) for t in (static_gate, cont, wc, bc, wm, bm, ln_w, ln_b)]
+        U = ids[0].shape[0]
+        nt = len(tables)
+        ptrs = [None] * _SP_N
+        ptrs[_SP_IDS:_SP_IDS + nt] = ids
+        ptrs[_SP_TABLES:_SP_TABLES + nt] = tables
+        ptrs[_SP_GATE:_SP_N] = params
+        p_arr = N.ptr_array(ptrs)
+        dims = N.i64_array([U, nt, cont.shape[1], wc.shape[0], wm.shape[1]] + [t.shape[0] for t in tables]
+                           + [t.shape[1] for t in tables] + list(pads))
+        lib = N.lib()
+        arena = torch.empty(lib.rsx_static_profile_arena_bytes(U), device=static_gate.device, dtype=torch.uint8)
+        out = torch.empty(U, wm.shape[0], device=static_gate.device, dtype=torch.float32)
+        rc = lib.rsx_static_profile_fwd(p_arr, dims, eps, p_drop, seed, N.ptr(arena), arena.numel(), N.ptr(out),
+                                        N.stream())
+        N.check(rc, "static_profile_fwd")
+        ctx.keep = (p_arr, dims, ptrs, arena, p_drop, seed, U)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        p_arr, dims, ptrs, arena, p_drop, seed, U = ctx.keep
+        nt = len(ctx.needs_input_grad) - 9
+        likes = [ptrs[_SP_GATE]] + [None] + ptrs[_SP_GATE + 2:_SP_N] + ptrs[_SP_TABLES:_SP_TABLES + nt]
+        if U == 0:
+            grads = [None if t is None else torch.zeros_like(t) for t in likes]
+        else:
+            grads = _empty_group(likes)
+            g_ptrs = [None] * _SP_N
+            g_ptrs[_SP_GATE:_SP_N] = grads[:8]
+            g_ptrs[_SP_TABLES:_SP_TABLES + nt] = grads[8:]
+            lib = N.lib()
+            nws = lib.rsx_static_profile_bwd_workspace_bytes(U)
+            ws = torch.empty(nws, device=dout.device, dtype=torch.uint8)
+            rc = lib.rsx_static_profile_bwd(p_arr, dims, p_drop, seed, N.ptr(arena), N.ptr(_c(dout)),
+                                            N.ptr_array(g_ptrs), N.ptr(ws), nws, N.stream())
+            N.check(rc, "static_profile_bwd")
+        return (None, *grads)
+
+
+def static_profile(model, ids, cont_feats, p_drop):
+    """SASRecUserTower phase 2 (v1_refine_usertower.py:472-494): sigmoid(static_gate), the nine
+    gated lookups, relu(cont_proj(cont)) * u_g[9], static_mlp (Linear + LayerNorm + GELU +
+    Dropout) -> [U, 128], as rsx_static_profile_fwd / _bwd (dropout: counter-hash mask)."""
+    embs = [model.age_emb, model.price_emb, model.cnt_emb, model.recency_emb, model.channel_emb,
+            model.club_status_emb, model.news_freq_emb, model.fn_emb, model.active_emb]
+    lin, ln = model.static_mlp[0], model.static_mlp[1]
+    seed = next_seed() if p_drop > 0 else 0
+    pads = [(-1 if e.padding_idx is None else int(e.padding_idx)) for e in embs]
+    cfg = (list(ids), pads, float(ln.eps), float(p_drop), seed)
+    return _StaticProfile.apply(cfg, model.static_gate, cont_feats, model.cont_proj.weight, model.cont_proj.bias,
+                                lin.weight, lin.bias, ln.weight, ln.bias, *[e.weight for e in embs])
 
 
 # ----------------------------------------------------------------------------------------
@@ -1362,13 +1535,16 @@ class _TowerPacked(torch.autograd.Function):
 
 
 def _empty_group(likes):
-    """Uninitialised fp32 buffers shaped like each tensor, carved out of ONE allocation (16-B
-    aligned slices)."""
-    sizes = [(t.numel() + 3) // 4 * 4 for t in likes]
-    flat = torch.empty(sum(sizes), device=likes[0].device, dtype=torch.float32)
+    """Uninitialised fp32 buffers shaped like each tensor (None -> None), carved out of ONE
+    allocation (16-B aligned slices)."""
+    sizes = [0 if t is None else (t.numel() + 3) // 4 * 4 for t in likes]
+    if sum(sizes) == 0:
+        return [None] * len(likes)
+    ref = next(t for t in likes if t is not None)
+    flat = torch.empty(sum(sizes), device=ref.device, dtype=torch.float32)
     out, o = [], 0
     for t, n in zip(likes, sizes):
-        out.append(flat[o:o + t.numel()].view(t.shape))
+        out.append(None if t is None else flat[o:o + t.numel()].view(t.shape))
         o += n
     return out
 

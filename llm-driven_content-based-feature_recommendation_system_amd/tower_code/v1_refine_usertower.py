@@ -292,7 +292,6 @@ class SASRecUserTower(nn.Module):
         p = self.dropout_rate if self.training else 0.0
 
         s_g = torch.sigmoid(self.seq_gate) * self._seq_gate_mask
-        u_g = torch.sigmoid(self.static_gate)
 
         # Phase 1: sequence encoding (reference :447-466)
         base = ops.linear_tok(pretrained_vecs, self.item_proj.weight, self.item_proj.bias)
@@ -306,7 +305,7 @@ class SASRecUserTower(nn.Module):
         output = self._encoder_stack(x, padding_mask, p)
 
         user_profile_vec = self._static_profile(age_bucket, price_bucket, cnt_bucket, recency_bucket, channel_ids,
-                                                club_status_ids, news_freq_ids, fn_ids, active_ids, cont_feats, u_g)
+                                                club_status_ids, news_freq_ids, fn_ids, active_ids, cont_feats, p)
 
         # Phase 3: late fusion (reference :499-510). Training mode: Linear(cat[token, profile[user]])
         # over all B*L tokens as ops.profile_linear (the per-user profile half computed once per
@@ -327,31 +326,14 @@ class SASRecUserTower(nn.Module):
         return ops.l2_normalize(final_vec)
 
     def _static_profile(self, age_bucket, price_bucket, cnt_bucket, recency_bucket, channel_ids, club_status_ids,
-                        news_freq_ids, fn_ids, active_ids, cont_feats, u_g):
-        # Phase 2: static encoding (reference :472-494): the nine gated lookups in one kernel
-        # (rsx_static_embed), then relu(cont_proj(cont)) * u_g[9], static_mlp.
-        embs = [self.age_emb, self.price_emb, self.cnt_emb, self.recency_emb, self.channel_emb,
-                self.club_status_emb, self.news_freq_emb, self.fn_emb, self.active_emb]
+                        news_freq_ids, fn_ids, active_ids, cont_feats, p):
+        # Phase 2: static encoding (reference :472-494) as one native call per direction
+        # (ops.static_profile -> rsx_static_profile_fwd / _bwd): sigmoid(static_gate), the nine
+        # gated lookups, relu(cont_proj(cont)) * u_g[9] and static_mlp (Linear 100 -> d on the
+        # bf16x3 GEMM with the input zero-padded to 128 columns, LayerNorm + GELU, Dropout).
         ids = [age_bucket, price_bucket, cnt_bucket, recency_bucket, channel_ids, club_status_ids, news_freq_ids,
                fn_ids, active_ids]
-        looked = ops.static_embed(ids, [e.weight for e in embs], u_g[:9], [e.padding_idx for e in embs])
-        cont = F.relu(self.cont_proj(cont_feats)) * u_g[9]
-        # static_mlp = Linear(100 -> d) + LayerNorm + GELU + Dropout on the token-GEMM / fused LN+GELU
-        # kernels: the input and weight are zero-padded to 128 columns (the padding adds exact zeros
-        # to every product), so the forward, dX and dW run on rsx_gemm_x3 / rsx_linear_wgrad_x3
-        # instead of library GEMMs (the library's [128 x 16384] x [16384 x 100] weight gradient
-        # alone took 0.13 ms per step) and torch's LayerNorm / GELU pair becomes one kernel.
-        lin, ln, drop = self.static_mlp[0], self.static_mlp[1], self.static_mlp[3]
-        kin = lin.in_features
-        kp = (kin + 31) // 32 * 32
-        parts = [looked, cont]
-        w = lin.weight
-        if kp != kin:
-            parts.append(looked.new_zeros(looked.shape[0], kp - kin))
-            w = torch.cat([w, w.new_zeros(w.shape[0], kp - kin)], dim=1)
-        h = ops.linear_tok(torch.cat(parts, dim=1), w, lin.bias)
-        h = ops.layer_norm(h, ln.weight, ln.bias, ln.eps, act=ops.ACT_GELU_ERF)
-        return drop(h)
+        return ops.static_profile(self, ids, cont_feats, p)
 
     def forward_packed(self, packed, pretrained_tok, tok_ids, age_bucket, price_bucket, cnt_bucket, recency_bucket,
                        channel_ids, club_status_ids, news_freq_ids, fn_ids, active_ids, cont_feats):
@@ -365,12 +347,12 @@ class SASRecUserTower(nn.Module):
         the losses see. tok_ids: [item, time, type, color, graphic, section] ids per token."""
         p = self.dropout_rate if self.training else 0.0
         s_g = torch.sigmoid(self.seq_gate) * self._seq_gate_mask
-        u_g = torch.sigmoid(self.static_gate)
+        # the static profile first (its dropout seed is drawn before the tower's, on both paths)
+        profile = self._static_profile(age_bucket, price_bucket, cnt_bucket, recency_bucket, channel_ids,
+                                       club_status_ids, news_freq_ids, fn_ids, active_ids, cont_feats, p)
         if torch.is_grad_enabled() and ops.tower_native_ok(self, packed, pretrained_tok):
             # the same kernels in the same order as below, issued by the library in one call per
-            # direction (rsx_tower_fwd / rsx_tower_bwd); the static profile stays here (autograd)
-            profile = self._static_profile(age_bucket, price_bucket, cnt_bucket, recency_bucket, channel_ids,
-                                           club_status_ids, news_freq_ids, fn_ids, active_ids, cont_feats, u_g)
+            # direction (rsx_tower_fwd / rsx_tower_bwd)
             return ops.tower_packed(self, packed, pretrained_tok, tok_ids, s_g, profile, p)
         base = ops.linear_tok(pretrained_tok, self.item_proj.weight, self.item_proj.bias)
         x = ops.seq_embed(
@@ -380,8 +362,6 @@ class SASRecUserTower(nn.Module):
             s_g, self.pos_emb.weight, self.emb_ln.weight, self.emb_ln.bias, eps=self.emb_ln.eps, p_drop=p,
             padding_idx=[0, 0, 0, 0, 0, 0], tok_pos=packed.tok_pos, tab0_seg=getattr(packed, "item_seg", None))
         x = self._encoder_stack(x, packed.tok_pad, p, seg_off=packed.seg_off)
-        profile = self._static_profile(age_bucket, price_bucket, cnt_bucket, recency_bucket, channel_ids,
-                                       club_status_ids, news_freq_ids, fn_ids, active_ids, cont_feats, u_g)
         lin0, ln, lin3 = self.output_proj[0], self.output_proj[1], self.output_proj[3]
         D = self.d_model
         h = ops.profile_linear(x, profile, lin0.weight, lin0.bias, packed.tok_user, packed.seg_off64)
