@@ -189,18 +189,22 @@ int rsx_nce_grouped_bwd(const float* A, const float* B, const float* bias, const
                         void* stream);
 
 /* ---- static-profile embeddings: gated lookups of several tiny tables, concatenated ------
- * out[b, off_j + c] = E_j[ids_j[b]][c] * gate[j]; backward accumulates dE_j (padding_idx rows
- * skipped) and dgate[j] (both added into; one workgroup per table sums in a fixed order, so
- * the gradients are identical run to run). Replaces the nine nn.Embedding lookups x u_g of
+ * out[b, off_j + c] = E_j[ids_j[b]][c] * gate[j]. The backward's dout has B rows, row b from
+ * user b % ids_rows (ids hold ids_rows entries: the contrastive step's two dropout views share
+ * their users), and gives dE_j (padding_idx rows: 0 when written, untouched when added) and
+ * dgate[j], added into (accumulate = 1) or written (0); per-64-row workgroup partials in ws
+ * (rsx_static_embed_bwd_workspace_floats) reduced in a fixed order, so the gradients are
+ * identical run to run. Replaces the nine nn.Embedding lookups x u_g of
  * tower_code/v1_refine_usertower.py:472-494 (and their sort-based embedding backward).
  * <= 16 tables, <= 256 columns, <= 4096 table floats in total. */
 int rsx_static_embed_fwd(const int64_t* const* ids, const float* const* tables, const int64_t* table_rows,
                          const int64_t* dims, int ntab, const float* gate, int64_t B, float* out, int64_t ld_out,
                          void* stream);
+int64_t rsx_static_embed_bwd_workspace_floats(int64_t B, int ntab, const int64_t* table_rows, const int64_t* dims);
 int rsx_static_embed_bwd(const int64_t* const* ids, const float* const* tables, const int64_t* table_rows,
                          const int64_t* dims, const int64_t* padding_idx, int ntab, const float* gate,
-                         const float* dout, int64_t ld_dout, int64_t B, float* const* dtables, float* dgate,
-                         int accumulate, void* stream);
+                         const float* dout, int64_t ld_dout, int64_t B, int64_t ids_rows, float* const* dtables,
+                         float* dgate, int accumulate, float* ws, int64_t ws_floats, void* stream);
 
 /* ---- LayerNorm fused with the preceding residual add + dropout and a following GELU ----
  * s = x + dropout(res) (res nullable), y = act(LN(s) * w + b), act 0 none / 2 GELU(erf).
@@ -453,8 +457,10 @@ int rsx_loss_combine_bwd(const float* g, const float* cnt, float inv_n, float in
  *   out = dropout_p(gelu_erf(LayerNorm(x @ Wm^T + bm)))     [U, 128]
  * p[] pointer table (RSX_SP_*; table slots beyond ntab unused): ids int64 [U] and tables
  * [rows_j, dim_j] per table, static_gate [ntab + 1] (raw parameter), cont [U, C], Wc [P, C],
- * bc [P], Wm [128, K], bm [128], ln_w / ln_b [128]. dims[] = {U, ntab, C, P, K, rows[ntab],
- * dim[ntab], padding_idx[ntab]} with sum(dim) + P == K <= 128, C <= 8, P <= 32. arena:
+ * bc [P], Wm [128, K], bm [128], ln_w / ln_b [128]. dims[] = {U, ntab, C, P, K, src, rows[ntab],
+ * dim[ntab], padding_idx[ntab]} with sum(dim) + P == K <= 128, C == 4, P == 16; the ids and cont
+ * hold src rows and output row r reads input row r % src (U % src == 0: the contrastive step's two
+ * dropout views share their users' inputs, so they are not duplicated). arena:
  * rsx_static_profile_arena_bytes(U), written by the forward and read by the backward.
  * Backward: grads[] parallel to p[] (the ids' and cont's slots unused), every gradient WRITTEN
  * (padding rows 0); U > 0; ws: rsx_static_profile_bwd_workspace_bytes(U). Dropout mask
@@ -483,8 +489,8 @@ int rsx_static_profile_bwd(const void* const* p, const int64_t* dims, float p_dr
 int64_t rsx_clip_adamw_workspace_bytes(int n, const int64_t* numel, const int* clip);
 int rsx_clip_adamw(int n, float* const* params, float* const* grads, float* const* exp_avg, float* const* exp_avg_sq,
                    const int64_t* numel, const int* clip, const float* step, const float* const* step_dev,
-                   const float* lr, const float* weight_decay, const float* beta1, const float* beta2,
-                   const float* eps, float max_norm, void* ws, int64_t ws_bytes, float* norm_out, void* stream);
+                   const double* lr, const double* weight_decay, const double* beta1, const double* beta2,
+                   const double* eps, float max_norm, void* ws, int64_t ws_bytes, float* norm_out, void* stream);
 
 /* Hard-negative mining: for each row i of u_norm [N,D] against the columns
  * i_norm [N,D] (both already L2-normalised), ignore column j when target_ids[j] ==

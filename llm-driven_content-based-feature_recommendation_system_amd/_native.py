@@ -73,7 +73,9 @@ _SIGS = {
     "rsx_linear_fwd": (c_i, [c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i64, c_i, c_p, c_p]),
     "rsx_linear_dot_fwd": (c_i, [c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i64, c_i, c_p, c_p, c_p, c_p, c_p]),
     "rsx_static_embed_fwd": (c_i, [c_p, c_p, c_p, c_p, c_i, c_p, c_i64, c_p, c_i64, c_p]),
-    "rsx_static_embed_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_i, c_p, c_p, c_i64, c_i64, c_p, c_p, c_i, c_p]),
+    "rsx_static_embed_bwd_workspace_floats": (c_i64, [c_i64, c_i, c_p, c_p]),
+    "rsx_static_embed_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_i, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_i, c_p,
+                                   c_i64, c_p]),
     "rsx_dropout_bwd": (c_i, [c_p, c_i64, c_i64, c_f, c_u64, c_p, c_p]),
     "rsx_ln_fwd": (c_i, [c_p, c_p, c_f, c_u64, c_p, c_p, c_f, c_i, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p]),
     "rsx_ln_bwd_workspace_floats": (c_i64, [c_i64, c_i64]),

@@ -22,7 +22,7 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kTile = 8192;   // elements per workgroup: 256 threads x 8 float4
-constexpr int kChunk = 24;    // tensors per launch (kernel argument block ~2.3 KB)
+constexpr int kChunk = 24;    // tensors per launch (kernel argument block ~2.5 KB)
 
 struct OptTensor {
   float* p;
@@ -31,7 +31,8 @@ struct OptTensor {
   float* v;
   const float* step_dev;  // device step count (already incremented), or null: use step
   int64_t n;
-  float step, lr, wd, b1, b2, eps;
+  double lr, wd, b1, b2, eps;  // torch keeps these as Python floats (double)
+  float step;
   int clip;               // 1: the gradient is part of the clipped norm and gets scaled
   int vec;                // 1: every pointer 16-B aligned and n % 4 == 0
 };
@@ -159,8 +160,8 @@ RSX_API int64_t rsx_clip_adamw_workspace_bytes(int n, const int64_t* numel, cons
 
 RSX_API int rsx_clip_adamw(int n, float* const* params, float* const* grads, float* const* exp_avg,
                            float* const* exp_avg_sq, const int64_t* numel, const int* clip, const float* step,
-                           const float* const* step_dev, const float* lr, const float* weight_decay,
-                           const float* beta1, const float* beta2, const float* eps, float max_norm, void* ws,
+                           const float* const* step_dev, const double* lr, const double* weight_decay,
+                           const double* beta1, const double* beta2, const double* eps, float max_norm, void* ws,
                            int64_t ws_bytes, float* norm_out, void* stream) {
   RSX_ARG(n >= 0, "n < 0");
   if (n == 0) return 0;

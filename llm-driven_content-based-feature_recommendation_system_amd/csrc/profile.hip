@@ -13,19 +13,20 @@
 // the zero-padded [128, 128] MLP weight, then the library's bf16x3 GEMM, fused LayerNorm + GELU
 // and dropout kernels. Backward = dropout, LayerNorm + GELU backward (dW / db of the norm), the
 // MLP's weight gradient and input gradient, the nine tables' gradients (rsx_static_embed_bwd in
-// write mode) and one tail kernel for the projection's gradients, the gates' sigmoid backward and
-// the [128, 100] weight slice. All reductions have a fixed order (bit-reproducible).
+// write mode), the projection's gradients as per-workgroup partials and one tail kernel for their
+// sum, the gates' sigmoid backward and the [128, 100] weight slice. All reductions have a fixed
+// order (bit-reproducible).
 #include "rsx_common.h"
 #include "recsys_amd.h"
 
 namespace {
 
-constexpr int kD = 128, kKp = 128, kMaxTab = 16, kMaxC = 8, kMaxP = 32;
+constexpr int kD = 128, kKp = 128, kMaxTab = 16;
 
 int64_t al(int64_t floats) { return (floats + 63) / 64 * 64; }  // 256-B granules
 
 struct Cfg {
-  int64_t U;
+  int64_t U, src;  // output rows; input rows (row r reads input row r % src: both dropout views)
   int ntab, C, P, K, ncols;  // ncols = table columns (the projection's start column)
   int64_t rows[kMaxTab], dims[kMaxTab], pad[kMaxTab];
   int col_off[kMaxTab + 1];
@@ -44,8 +45,12 @@ ArenaLayout arena_layout(int64_t U) {
   return s;
 }
 
+constexpr int kCP = 16, kCC = 4;            // cont_proj: 4 -> 16 (the reference's fixed shape)
+constexpr int kNout = kCP * kCC + kCP + 1;  // dWc, dbc, the cont gate's gradient
+constexpr int kRowsPerBlk = 256;
+
 struct WsLayout {
-  int64_t dY, dH, dX, dWp, dgu, wsw, wsl, total, n_wsw, n_wsl;
+  int64_t dY, dH, dX, dWp, dgu, wsw, wsl, wse, cpart, total, n_wsw, n_wsl, n_wse;
 };
 WsLayout ws_layout(int64_t U) {
   WsLayout s{};
@@ -54,7 +59,9 @@ WsLayout ws_layout(int64_t U) {
   s.dY = take(U * kD); s.dH = take(U * kD); s.dX = take(U * kKp); s.dWp = take(kD * kKp); s.dgu = take(kMaxTab + 1);
   s.n_wsw = rsx_linear_wgrad_workspace_floats(U, kD, kKp);
   s.n_wsl = rsx_ln_bwd_workspace_floats(U, kD);
-  s.wsw = take(s.n_wsw); s.wsl = take(s.n_wsl);
+  s.n_wse = ((U + 63) / 64) * (4096 + kMaxTab) + 1;  // >= rsx_static_embed_bwd_workspace_floats for any tables
+  s.wsw = take(s.n_wsw); s.wsl = take(s.n_wsl); s.wse = take(s.n_wse);
+  s.cpart = take(((U + kRowsPerBlk - 1) / kRowsPerBlk) * kNout);
   s.total = o;
   return s;
 }
@@ -65,13 +72,15 @@ int parse(Cfg& c, const int64_t* dims) {
   c.C = (int)dims[2];
   c.P = (int)dims[3];
   c.K = (int)dims[4];
+  c.src = dims[5];
   RSX_ARG(c.U >= 0 && c.ntab >= 1 && c.ntab <= kMaxTab, "1..16 tables");
-  RSX_ARG(c.C >= 1 && c.C <= kMaxC && c.P >= 1 && c.P <= kMaxP, "continuous features 1..8, projection 1..32");
+  RSX_ARG(c.src >= 1 && c.U % c.src == 0, "U must be a multiple of the input rows");
+  RSX_ARG(c.C == 4 && c.P == 16, "cont_proj must be Linear(4, 16) (the reference's shape)");
   int off = 0;
   for (int j = 0; j < c.ntab; ++j) {
-    c.rows[j] = dims[5 + j];
-    c.dims[j] = dims[5 + c.ntab + j];
-    c.pad[j] = dims[5 + 2 * c.ntab + j];
+    c.rows[j] = dims[6 + j];
+    c.dims[j] = dims[6 + c.ntab + j];
+    c.pad[j] = dims[6 + 2 * c.ntab + j];
     RSX_ARG(c.rows[j] >= 1 && c.dims[j] >= 1, "empty table");
     c.col_off[j] = off;
     off += (int)c.dims[j];
@@ -96,7 +105,7 @@ struct InArgs {
   float* X;           // [U, 128]
   float* Wp;          // [128, 128]
   float* ug;          // [ntab + 1] sigmoid(static_gate), for the backward
-  int64_t U, x_blocks;
+  int64_t U, src, x_blocks;
 };
 
 __device__ __forceinline__ float sigm(float g) { return 1.0f / (1.0f + __expf(-g)); }
@@ -113,7 +122,7 @@ __global__ __launch_bounds__(256) void prof_in_k(InArgs a) {
   if (blockIdx.x == 0 && threadIdx.x <= a.ntab) a.ug[threadIdx.x] = sigm(a.gate[threadIdx.x]);
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= a.U * kKp) return;
-  const int64_t r = e / kKp;
+  const int64_t r = e / kKp % a.src;
   const int c = (int)(e % kKp);
   float v = 0.0f;
   if (c < a.ncols) {
@@ -132,76 +141,90 @@ __global__ __launch_bounds__(256) void prof_in_k(InArgs a) {
 
 struct TailArgs {
   const float* dX;    // [U, 128]
-  const float* cont;  // [U, C]
+  const float* cont;  // [src, C]
   const float* wc;
   const float* bc;
   const float* ug;    // [ntab + 1]
   const float* dgu;   // [ntab] table-gate gradients (rsx_static_embed_bwd)
   const float* dWp;   // [128, 128]
+  float* cpart;       // [nblk][kNout] per-workgroup partials
   float* dwc;         // [P, C]
   float* dbc;         // [P]
   float* dgate;       // [ntab + 1] gradient of the raw static_gate
   float* dwm;         // [128, K]
-  int64_t U;
-  int ntab, C, P, K, ncols;
+  int64_t U, src;
+  int ntab, K, ncols, nblk;
 };
 
-constexpr int kTail = 1024;
+// The projection's backward, per-workgroup partials: thread = one output row r (input row
+// r % src); its contributions to dWc [16, 4], dbc [16] and the cont gate's gradient
+// sum_q dX[r, q] * relu(pre_q) are summed over the wave by a fixed shuffle tree and over the
+// workgroup's four waves in order.
+__global__ __launch_bounds__(kRowsPerBlk) void prof_cont_part_k(TailArgs a) {
+  __shared__ float red[kRowsPerBlk / 64][kNout];
+  const int64_t r = (int64_t)blockIdx.x * kRowsPerBlk + threadIdx.x;
+  float acc[kNout];
+#pragma unroll
+  for (int o = 0; o < kNout; ++o) acc[o] = 0.0f;
+  if (r < a.U) {
+    const float* xr = a.cont + (r % a.src) * kCC;
+    float x[kCC];
+#pragma unroll
+    for (int k = 0; k < kCC; ++k) x[k] = xr[k];
+    const float g9 = a.ug[a.ntab];
+    const float* dx = a.dX + r * kKp + a.ncols;
+#pragma unroll
+    for (int q = 0; q < kCP; ++q) {
+      float pre = a.bc[q];
+#pragma unroll
+      for (int k = 0; k < kCC; ++k) pre += x[k] * a.wc[q * kCC + k];
+      const float dc = dx[q];
+      acc[kNout - 1] += dc * fmaxf(pre, 0.0f);
+      const float dpre = pre > 0.0f ? dc * g9 : 0.0f;
+#pragma unroll
+      for (int k = 0; k < kCC; ++k) acc[q * kCC + k] = dpre * x[k];
+      acc[kCP * kCC + q] = dpre;
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < kNout; ++o) {
+    float v = acc[o];
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) v += __shfl_xor(v, m, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][o] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < kNout) {
+    float v = 0.0f;
+#pragma unroll
+    for (int w = 0; w < kRowsPerBlk / 64; ++w) v += red[w][threadIdx.x];
+    a.cpart[(int64_t)blockIdx.x * kNout + threadIdx.x] = v;
+  }
+}
 
-// block 0: the projection's gradients and the gates'; blocks >= 1: the [128, K] weight slice.
-// Block 0's thread (slice s, output o) sums output o over the rows s, s + nslice, ...; outputs
-// are dWc[q][k] (P*C), dbc[q] (P) and the per-column part of the cont gate's gradient (P); the
-// slices meet in LDS and are summed in slice order.
-__global__ __launch_bounds__(kTail) void prof_tail_k(TailArgs a) {
+// block 0: the partials summed in workgroup order -> dWc, dbc, the gates' sigmoid backward;
+// blocks >= 1: the [128, K] slice of the padded weight gradient.
+__global__ __launch_bounds__(256) void prof_tail_k(TailArgs a) {
   if (blockIdx.x > 0) {
-    for (int64_t e = (int64_t)(blockIdx.x - 1) * kTail + threadIdx.x; e < (int64_t)kD * a.K;
-         e += (int64_t)(gridDim.x - 1) * kTail) {
+    for (int64_t e = (int64_t)(blockIdx.x - 1) * 256 + threadIdx.x; e < (int64_t)kD * a.K;
+         e += (int64_t)(gridDim.x - 1) * 256) {
       const int64_t n = e / a.K, k = e % a.K;
       a.dwm[e] = a.dWp[n * kKp + k];
     }
     return;
   }
-  __shared__ float part[kTail];
-  __shared__ float outs[kMaxP * kMaxC + 2 * kMaxP];
-  const int nout = a.P * a.C + 2 * a.P;
-  const int nslice = kTail / nout;
-  const int t = threadIdx.x, o = t % nout, s = t / nout;
-  const float g9 = a.ug[a.ntab];
-  float acc = 0.0f;
-  if (s < nslice) {
-    const int q = o < a.P * a.C ? o / a.C : (o < a.P * a.C + a.P ? o - a.P * a.C : o - a.P * a.C - a.P);
-    const int kk = o < a.P * a.C ? o % a.C : -1;
-    const int kind = o < a.P * a.C ? 0 : (o < a.P * a.C + a.P ? 1 : 2);
-    for (int64_t r = s; r < a.U; r += nslice) {
-      float pre = a.bc[q];
-      for (int k = 0; k < a.C; ++k) pre += a.cont[r * a.C + k] * a.wc[q * a.C + k];
-      const float dc = a.dX[r * kKp + a.ncols + q];
-      if (kind == 2) {
-        acc += dc * fmaxf(pre, 0.0f);
-      } else {
-        const float dpre = pre > 0.0f ? dc * g9 : 0.0f;
-        acc += kind == 0 ? dpre * a.cont[r * a.C + kk] : dpre;
-      }
-    }
-  }
-  part[t] = acc;
-  __syncthreads();
-  if (t < nout) {
+  __shared__ float outs[kNout];
+  const int t = threadIdx.x;
+  if (t < kNout) {
     float v = 0.0f;
-    for (int q2 = 0; q2 < nslice; ++q2) v += part[q2 * nout + t];
+    for (int b = 0; b < a.nblk; ++b) v += a.cpart[(int64_t)b * kNout + t];
     outs[t] = v;
+    if (t < kCP * kCC) a.dwc[t] = v;
+    else if (t < kCP * kCC + kCP) a.dbc[t - kCP * kCC] = v;
   }
   __syncthreads();
-  if (t < a.P * a.C) a.dwc[t] = outs[t];
-  else if (t < a.P * a.C + a.P) a.dbc[t - a.P * a.C] = outs[t];
   if (t <= a.ntab) {
-    float dg;
-    if (t < a.ntab) {
-      dg = a.dgu[t];
-    } else {
-      dg = 0.0f;
-      for (int q = 0; q < a.P; ++q) dg += outs[a.P * a.C + a.P + q];
-    }
+    const float dg = t < a.ntab ? a.dgu[t] : outs[kNout - 1];
     const float sg = a.ug[t];
     a.dgate[t] = dg * (1.0f - sg) * sg;  // torch's sigmoid backward
   }
@@ -247,6 +270,7 @@ RSX_API int rsx_static_profile_fwd(const void* const* p, const int64_t* dims, fl
   a.wm = static_cast<const float*>(p[RSX_SP_WM]);
   a.X = A + s.X; a.Wp = A + s.Wp; a.ug = A + s.ug;
   a.U = c.U;
+  a.src = c.src;
   a.x_blocks = (c.U * kKp + 255) / 256;
   const int64_t blocks = a.x_blocks + (kD * kKp + 255) / 256;
   hipLaunchKernelGGL(prof_in_k, dim3((unsigned)blocks), dim3(256), 0, st, a);
@@ -299,8 +323,9 @@ RSX_API int rsx_static_profile_bwd(const void* const* p, const int64_t* dims, fl
     tabs[j] = static_cast<const float*>(p[RSX_SP_TABLES + j]);
     dtabs[j] = grads[RSX_SP_TABLES + j];
   }
-  SP_CALL(rsx_static_embed_bwd(ids, tabs, c.rows, c.dims, c.pad, c.ntab, A + s.ug, W + w.dX, kKp, c.U, dtabs,
-                               W + w.dgu, 0, stream));
+  // the tables' and their gates' gradients (written; row r reads user r % src)
+  SP_CALL(rsx_static_embed_bwd(ids, tabs, c.rows, c.dims, c.pad, c.ntab, A + s.ug, W + w.dX, kKp, c.U, c.src, dtabs,
+                               W + w.dgu, 0, W + w.wse, w.n_wse, stream));
   TailArgs t{};
   t.dX = W + w.dX;
   t.cont = static_cast<const float*>(p[RSX_SP_CONT]);
@@ -313,9 +338,14 @@ RSX_API int rsx_static_profile_bwd(const void* const* p, const int64_t* dims, fl
   t.dbc = grads[RSX_SP_BC];
   t.dgate = grads[RSX_SP_GATE];
   t.dwm = grads[RSX_SP_WM];
+  t.cpart = W + w.cpart;
   t.U = c.U;
-  t.ntab = c.ntab; t.C = c.C; t.P = c.P; t.K = c.K; t.ncols = c.ncols;
-  hipLaunchKernelGGL(prof_tail_k, dim3(1 + 16), dim3(kTail), 0, st, t);
+  t.src = c.src;
+  t.ntab = c.ntab; t.K = c.K; t.ncols = c.ncols;
+  t.nblk = (int)((c.U + kRowsPerBlk - 1) / kRowsPerBlk);
+  hipLaunchKernelGGL(prof_cont_part_k, dim3((unsigned)t.nblk), dim3(kRowsPerBlk), 0, st, t);
+  RSX_LAUNCHED();
+  hipLaunchKernelGGL(prof_tail_k, dim3(1 + 16), dim3(256), 0, st, t);
   RSX_LAUNCHED();
   return 0;
 }

@@ -309,14 +309,12 @@ class _Packed:
 _DEVICE_INDEX = os.environ.get("RSX_DEVICE_INDEX", "1") != "0"
 
 
-def doubled_static(batch):
-    """The per-user static inputs of both dropout views (users b and B + b share them): the nine id
-    columns stacked and doubled in two launches, cont_feats in one, instead of ten concatenations."""
+def static_inputs(batch):
+    """The per-user static inputs of the step: the nine id columns (int64) and cont_feats, NOT
+    doubled for the two dropout views -- the static-profile program reads user r % B for output
+    row r (ops.static_profile rows = 2B)."""
     from .tower_code.v1_usertower_train import _STATIC_KEYS
-    ids = torch.stack([batch[k].reshape(-1).to(torch.int64) for k in _STATIC_KEYS[:9]])
-    ids = torch.cat([ids, ids], dim=1)
-    cont = batch[_STATIC_KEYS[9]]
-    return list(ids.unbind(0)) + [torch.cat([cont, cont])]
+    return [batch[k].reshape(-1).to(torch.int64) for k in _STATIC_KEYS[:9]] + [batch[_STATIC_KEYS[9]]]
 
 
 def _prepare_step_index_device(batch, pretrained_vecs, pretrained_lookup, n_items) -> StepIndex:
@@ -381,7 +379,7 @@ def _prepare_step_index_device(batch, pretrained_vecs, pretrained_lookup, n_item
     else:
         pv_tok = pk.take(pretrained_vecs)
         pv_tok = torch.cat([pv_tok, pv_tok])
-    static = doubled_static(batch)
+    static = static_inputs(batch)
     ix = StepIndex()
     ix.packed = (pk, pk2, tok_ids, pv_tok, static)
     ix.B = B

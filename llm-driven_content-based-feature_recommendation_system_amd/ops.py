@@ -803,11 +803,11 @@ def clip_adamw_step(optimizer, clip_params, max_norm: float):
     steps_t = [state[p]["step"] for p, _, _ in items]
     step_h = (ctypes.c_float * n)(*[0.0 if s.device.type == "cuda" else float(s) for s in steps_t])
     step_d = N.ptr_array([s if s.device.type == "cuda" else None for s in steps_t]) if dev_steps else None
-    lr = (ctypes.c_float * n)(*[g["lr"] for _, _, g in items])
-    wd = (ctypes.c_float * n)(*[g["weight_decay"] for _, _, g in items])
-    b1 = (ctypes.c_float * n)(*[g["betas"][0] for _, _, g in items])
-    b2 = (ctypes.c_float * n)(*[g["betas"][1] for _, _, g in items])
-    eps = (ctypes.c_float * n)(*[g["eps"] for _, _, g in items])
+    lr = (ctypes.c_double * n)(*[g["lr"] for _, _, g in items])   # doubles, as torch's kernels take them
+    wd = (ctypes.c_double * n)(*[g["weight_decay"] for _, _, g in items])
+    b1 = (ctypes.c_double * n)(*[g["betas"][0] for _, _, g in items])
+    b2 = (ctypes.c_double * n)(*[g["betas"][1] for _, _, g in items])
+    eps = (ctypes.c_double * n)(*[g["eps"] for _, _, g in items])
     lib = N.lib()
     nbytes = lib.rsx_clip_adamw_workspace_bytes(n, numel, clip)
     dev = items[0][0].device
@@ -856,11 +856,14 @@ class _StaticEmbed(torch.autograd.Function):
         dgate, *dtabs = _empty_group([gate if need[0] else None] +
                                      [t if need[3 + j] else None for j, t in enumerate(tables)])
         dout = _c(dout)
-        rc = N.lib().rsx_static_embed_bwd(N.ptr_array(ids), N.ptr_array(tables),
-                                          N.i64_array([t.shape[0] for t in tables]),
-                                          N.i64_array([t.shape[1] for t in tables]), N.i64_array(pad), nt,
-                                          N.ptr(gate), N.ptr(dout), dout.stride(0), ids[0].shape[0],
-                                          N.ptr_array(dtabs), N.ptr(dgate), 0, N.stream())  # written
+        B = ids[0].shape[0]
+        rows = N.i64_array([t.shape[0] for t in tables])
+        dims = N.i64_array([t.shape[1] for t in tables])
+        nws = N.lib().rsx_static_embed_bwd_workspace_floats(B, nt, rows, dims)
+        ws = torch.empty(nws, device=dout.device, dtype=torch.float32)
+        rc = N.lib().rsx_static_embed_bwd(N.ptr_array(ids), N.ptr_array(tables), rows, dims, N.i64_array(pad), nt,
+                                          N.ptr(gate), N.ptr(dout), dout.stride(0), B, B, N.ptr_array(dtabs),
+                                          N.ptr(dgate), 0, N.ptr(ws), nws, N.stream())  # written
         N.check(rc, "static_embed_bwd")
         return (dgate, None, None, *dtabs)
 
@@ -882,19 +885,19 @@ _SP_IDS, _SP_TABLES, _SP_GATE, _SP_N = 0, 16, 32, 40
 class _StaticProfile(torch.autograd.Function):
     @staticmethod
     def forward(ctx, cfg, static_gate, cont, wc, bc, wm, bm, ln_w, ln_b, *tables):
-        ids, pads, eps, p_drop, seed = cfg
+        ids, pads, eps, p_drop, seed, U = cfg
         N.ensure_device(static_gate)
         ids = [_c(t) for t in ids]
         tables = [_c(t) for t in tables]
         params = [_c(t) for t in (static_gate, cont, wc, bc, wm, bm, ln_w, ln_b)]
-        U = ids[0].shape[0]
+        src = ids[0].shape[0]
         nt = len(tables)
         ptrs = [None] * _SP_N
         ptrs[_SP_IDS:_SP_IDS + nt] = ids
         ptrs[_SP_TABLES:_SP_TABLES + nt] = tables
         ptrs[_SP_GATE:_SP_N] = params
         p_arr = N.ptr_array(ptrs)
-        dims = N.i64_array([U, nt, cont.shape[1], wc.shape[0], wm.shape[1]] + [t.shape[0] for t in tables]
+        dims = N.i64_array([U, nt, cont.shape[1], wc.shape[0], wm.shape[1], src] + [t.shape[0] for t in tables]
                            + [t.shape[1] for t in tables] + list(pads))
         lib = N.lib()
         arena = torch.empty(lib.rsx_static_profile_arena_bytes(U), device=static_gate.device, dtype=torch.uint8)
@@ -926,17 +929,24 @@ class _StaticProfile(torch.autograd.Function):
         return (None, *grads)
 
 
-def static_profile(model, ids, cont_feats, p_drop):
+def static_profile(model, ids, cont_feats, p_drop, rows=None):
     """SASRecUserTower phase 2 (v1_refine_usertower.py:472-494): sigmoid(static_gate), the nine
     gated lookups, relu(cont_proj(cont)) * u_g[9], static_mlp (Linear + LayerNorm + GELU +
-    Dropout) -> [U, 128], as rsx_static_profile_fwd / _bwd (dropout: counter-hash mask)."""
+    Dropout) -> [rows, 128], as rsx_static_profile_fwd / _bwd (dropout: counter-hash mask).
+    ids (nine int64 [B]) / cont_feats [B, 4] hold B users; rows (default B, a multiple of B):
+    output row r is user r % B (the two dropout views of the contrastive step: rows = 2B)."""
+    B = ids[0].shape[0]
+    rows = B if rows is None else int(rows)
+    if B == 0 or rows % B:
+        raise ValueError(f"static_profile: rows ({rows}) must be a positive multiple of the users ({B})")
     embs = [model.age_emb, model.price_emb, model.cnt_emb, model.recency_emb, model.channel_emb,
             model.club_status_emb, model.news_freq_emb, model.fn_emb, model.active_emb]
     lin, ln = model.static_mlp[0], model.static_mlp[1]
     seed = next_seed() if p_drop > 0 else 0
     pads = [(-1 if e.padding_idx is None else int(e.padding_idx)) for e in embs]
-    cfg = (list(ids), pads, float(ln.eps), float(p_drop), seed)
-    return _StaticProfile.apply(cfg, model.static_gate, cont_feats, model.cont_proj.weight, model.cont_proj.bias,
+    cfg = ([t.to(torch.int64) for t in ids], pads, float(ln.eps), float(p_drop), seed, rows)
+    return _StaticProfile.apply(cfg, model.static_gate, cont_feats.to(torch.float32), model.cont_proj.weight,
+                                model.cont_proj.bias,
                                 lin.weight, lin.bias, ln.weight, ln.bias, *[e.weight for e in embs])
 
 

@@ -326,14 +326,14 @@ class SASRecUserTower(nn.Module):
         return ops.l2_normalize(final_vec)
 
     def _static_profile(self, age_bucket, price_bucket, cnt_bucket, recency_bucket, channel_ids, club_status_ids,
-                        news_freq_ids, fn_ids, active_ids, cont_feats, p):
+                        news_freq_ids, fn_ids, active_ids, cont_feats, p, rows=None):
         # Phase 2: static encoding (reference :472-494) as one native call per direction
         # (ops.static_profile -> rsx_static_profile_fwd / _bwd): sigmoid(static_gate), the nine
         # gated lookups, relu(cont_proj(cont)) * u_g[9] and static_mlp (Linear 100 -> d on the
         # bf16x3 GEMM with the input zero-padded to 128 columns, LayerNorm + GELU, Dropout).
         ids = [age_bucket, price_bucket, cnt_bucket, recency_bucket, channel_ids, club_status_ids, news_freq_ids,
                fn_ids, active_ids]
-        return ops.static_profile(self, ids, cont_feats, p)
+        return ops.static_profile(self, ids, cont_feats, p, rows)
 
     def forward_packed(self, packed, pretrained_tok, tok_ids, age_bucket, price_bucket, cnt_bucket, recency_bucket,
                        channel_ids, club_status_ids, news_freq_ids, fn_ids, active_ids, cont_feats):
@@ -349,7 +349,7 @@ class SASRecUserTower(nn.Module):
         s_g = torch.sigmoid(self.seq_gate) * self._seq_gate_mask
         # the static profile first (its dropout seed is drawn before the tower's, on both paths)
         profile = self._static_profile(age_bucket, price_bucket, cnt_bucket, recency_bucket, channel_ids,
-                                       club_status_ids, news_freq_ids, fn_ids, active_ids, cont_feats, p)
+                                       club_status_ids, news_freq_ids, fn_ids, active_ids, cont_feats, p, packed.B)
         if torch.is_grad_enabled() and ops.tower_native_ok(self, packed, pretrained_tok):
             # the same kernels in the same order as below, issued by the library in one call per
             # direction (rsx_tower_fwd / rsx_tower_bwd)

@@ -124,8 +124,8 @@ def pack_inputs(batch, pretrained_vecs=None, pretrained_lookup=None):
     else:
         pv_tok = ops.gather_rows(pretrained_lookup, tok_ids[0][:T])
     pv_tok = torch.cat([pv_tok, pv_tok])
-    from ..dist import doubled_static
-    return pk, pk2, tok_ids, pv_tok, doubled_static(batch)
+    from ..dist import static_inputs
+    return pk, pk2, tok_ids, pv_tok, static_inputs(batch)
 
 
 def packed_views(model, batch, pretrained_vecs=None, pretrained_lookup=None, packed=None):

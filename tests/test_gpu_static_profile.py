@@ -105,3 +105,23 @@ def test_static_profile_deterministic_and_eval():
         assert torch.equal(grads[0][n], grads[1][n]), n
     with torch.no_grad():
         assert torch.equal(ops.static_profile(m, ids, cont, 0.0), outs[0])
+
+
+def test_static_profile_shared_rows_equal_doubled_inputs():
+    """rows = 2B (the contrastive step's two dropout views read the same B users): identical to
+    the program run on the explicitly doubled inputs, output and every gradient (dropout 0)."""
+    m = _model(4)
+    ids, cont = _inputs(300, seed=7)
+    dy = torch.randn(600, 128, device="cuda")
+    res = []
+    for shared in (True, False):
+        m.zero_grad(set_to_none=True)
+        if shared:
+            o = ops.static_profile(m, ids, cont, 0.0, rows=600)
+        else:
+            o = ops.static_profile(m, [torch.cat([i, i]) for i in ids], torch.cat([cont, cont]), 0.0)
+        o.backward(dy)
+        res.append((o.detach(), _grads(m)))
+    assert torch.equal(res[0][0], res[1][0])
+    for n in res[0][1]:
+        assert torch.equal(res[0][1][n], res[1][1][n]), n
