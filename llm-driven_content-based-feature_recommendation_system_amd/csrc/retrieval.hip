@@ -675,7 +675,7 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_scan_k(BfArgs a) {
 // under the next tile's MFMAs (2.49 ms). The entries of a stream are the same set in every form;
 // their order within the stream differs with EXTRACT, which P4 never sees (its margin set and
 // final sort use the total order (score desc, index asc)).
-template <int G, bool EXTRACT>
+template <int G, bool EXTRACT, bool BALLOT = true>
 __global__ __launch_bounds__(256, 2) void topk_bf16_collect_k(BfArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned char sI[2][kTile * kImgStride];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -747,6 +747,8 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_collect_k(BfArgs a) {
       float m3 = fmaxf(fmaxf(acc[g][9], acc[g][10]), acc[g][11]);
       float m4 = fmaxf(fmaxf(acc[g][12], acc[g][13]), acc[g][14]);
       const float mx = fmaxf(fmaxf(fmaxf(m0, m1), fmaxf(m2, m3)), fmaxf(m4, acc[g][15]));
+      // wave-uniform gate: skip the group unless some lane's max reaches its threshold
+      if (BALLOT && !__builtin_amdgcn_ballot_w64(mx >= thr[g])) continue;
       if (!(mx >= thr[g])) continue;  // most lanes: no collected item of this query in the tile
       if (EXTRACT) {
         float v[16];
@@ -770,14 +772,24 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_collect_k(BfArgs a) {
           m = fmaxf(fmaxf(fmaxf(n0, n1), fmaxf(n2, n3)), fmaxf(n4, v[15]));
         }
       } else if (full) {  // whole tile inside the split: one compare per score
+        // each append behind a wave-uniform branch on the ballot of its compare: with ~1 passing
+        // score per wave and group, the other 15 append bodies are skipped, not executed under an
+        // empty exec mask (the compiler's choice for short divergent blocks: ~8 VALU each)
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (acc[g][r] >= thr[g]) append(g, acc[g][r], jt0 + tile_row(r, h));
+        for (int r = 0; r < 16; ++r) {
+          const bool pass = acc[g][r] >= thr[g];
+          if (!BALLOT || __builtin_amdgcn_ballot_w64(pass)) {
+            if (pass) append(g, acc[g][r], jt0 + tile_row(r, h));
+          }
+        }
       } else {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int j = jt0 + tile_row(r, h);
-          if (acc[g][r] >= thr[g] && (full || j < jend)) append(g, acc[g][r], j);
+          const bool pass = acc[g][r] >= thr[g] && (full || j < jend);
+          if (!BALLOT || __builtin_amdgcn_ballot_w64(pass)) {
+            if (pass) append(g, acc[g][r], j);
+          }
         }
       }
     }
@@ -931,7 +943,10 @@ __device__ float block_kth_largest(const float* v, int n, int K, int* hist, int*
   return from_okey(prefix);
 }
 
-// P2: t_q = c_k - 2 delta_q (c_k: k-th best sampled candidate; -inf if fewer than k valid ones)
+// P2: t_q = c_r - 2 delta_q (c_r: r-th best sampled candidate, r <= k (thr_rank); -inf if fewer
+// than r valid ones). r = k guarantees >= k collected items at or above c_k; r < k admits fewer
+// items and P4 checks, per query, that its k-th best collected score still clears c_r (else the
+// query goes to the exact kernels).
 template <int NC>
 __global__ __launch_bounds__(256) void topk_bf16_thresh_k(const float* __restrict__ cs, const int* __restrict__ ci,
                                                           int ncand, const float* __restrict__ U, int64_t ldu, int K,
@@ -969,8 +984,9 @@ __global__ __launch_bounds__(256) void topk_bf16_select_k(const float2* __restri
                                                           const int* __restrict__ bn, int nstreams,
                                                           const float* __restrict__ U, int64_t ldu,
                                                           const float* __restrict__ I, int64_t ldi, int K,
-                                                          const unsigned* wmax_bits, float* out_s, int64_t* out_i,
-                                                          int* qcount, int* qmap, int* qtotal) {
+                                                          const unsigned* wmax_bits, const float* __restrict__ thr_q,
+                                                          int check, float* out_s, int64_t* out_i, int* qcount,
+                                                          int* qmap, int* qtotal) {
   // LDS: the appended scores only (their item ids are read back from global for the margin set),
   // so three workgroups fit per CU
   __shared__ __attribute__((aligned(16))) float ss[kSelMax];
@@ -1041,7 +1057,19 @@ __global__ __launch_bounds__(256) void topk_bf16_select_k(const float2* __restri
       if (dst[u] >= 0) ss[dst[u]] = v[u];
   }
   __syncthreads();
-  const float thr = (total >= K) ? block_kth_largest(ss, total, K, hist, sel, red) - 2.0f * delta : -INFINITY;
+  const float ak = (total >= K) ? block_kth_largest(ss, total, K, hist, sel, red) : -INFINITY;
+  // threshold rank r < k (check): the collected set holds every true top-k item iff its k-th best
+  // bf16 score a_k satisfies a_k - 2 delta >= t_q (k items with a >= a_k have exact scores >= a_k -
+  // delta, so every top-k item has a >= a_k - 2 delta); delta inflated by 1e-5 against the
+  // subtraction's rounding. Otherwise (or with fewer than k collected) the exact kernels run it.
+  if (check && thr_q[q] > -INFINITY && (total < K || ak - 2.0f * (delta * 1.00001f) < thr_q[q])) {
+    if (tid == 0) {
+      qmap[atomicAdd(qcount, 1)] = (int)q;
+      atomicAdd(qtotal, 1);
+    }
+    return;
+  }
+  const float thr = (total >= K) ? ak - 2.0f * delta : -INFINITY;
   // margin set: one thread per stream walks that stream's entries (~5 on spread data) and notes
   // the buffer slot of each selected one; every selected item id is then loaded from global at
   // once (one memory latency). (Round 3 walked 8 streams per step with 32 threads each: 64
@@ -1211,6 +1239,26 @@ int sample_nsplit(int nsplit, int64_t k, int T) {
   while (ns0 < nsplit && 2 * (int64_t)ns0 * T < 2 * k) ns0 *= 2;
   if (ns0 > nsplit) ns0 = nsplit;
   return ns0;
+}
+
+// Rank r of the sampled candidate that sets t_q. The candidates are stream maxima of 1/S of the
+// corpus, so about S r corpus items score above c_r and the collect pass appends a multiple of
+// that: at 4096 x 1M, k = 100 (S = 8), r = k admits ~0.25 % of the scores and the appends set the
+// collect kernel's time. r < k is exact only while the k-th best collected score clears c_r (P4
+// checks it per query; a query that fails runs on the exact kernels, whose latency is that of a
+// whole batch). r = clamp(ceil(3 k / S), 32, k) keeps S r >= 3k with r >= 32 candidates behind the
+// estimate (tools/retrieval_micro.py, 4096 spread queries: no fallback down to r = 25 at k = 100,
+// 2 at r = 17; k = 10 at r = 3: 88); RSX_TOPK_RANK_DIV=d forces r = ceil(k / d) (A/B).
+int thr_rank(int k, int S) {
+  static const int div = [] {
+    const char* e = getenv("RSX_TOPK_RANK_DIV");
+    const int v = e ? atoi(e) : 0;
+    return v >= 1 && v <= 16 ? v : 0;
+  }();
+  int r = div ? (k + div - 1) / div : (3 * k + S - 1) / S;
+  if (!div && r < 32) r = 32;
+  if (r > k) r = k;
+  return r < 1 ? 1 : r;
 }
 
 // RSX_TOPK_SAMPLE_T1=0: the sample scan keeps T best per lane stream (A/B)
@@ -1391,15 +1439,16 @@ int run_bf16_chunk(const BfPlan& bp, const BfLayout& L, const float* U, int64_t 
   RSX_LAUNCHED();
   const int ncand = ns0 * 2 * T0;
   float* thr = reinterpret_cast<float*>(w + L.thr);
+  const int r = thr_rank((int)k, bp.sample);
   if (ncand <= 1024)
     hipLaunchKernelGGL(topk_bf16_thresh_k<1024>, dim3((unsigned)Q), dim3(256), 0, st, b.cand_s, b.cand_i, ncand, U,
-                       ldu, (int)k, wmax, thr);
+                       ldu, r, wmax, thr);
   else if (ncand <= 2048)
     hipLaunchKernelGGL(topk_bf16_thresh_k<2048>, dim3((unsigned)Q), dim3(256), 0, st, b.cand_s, b.cand_i, ncand, U,
-                       ldu, (int)k, wmax, thr);
+                       ldu, r, wmax, thr);
   else
     hipLaunchKernelGGL(topk_bf16_thresh_k<4096>, dim3((unsigned)Q), dim3(256), 0, st, b.cand_s, b.cand_i, ncand, U,
-                       ldu, (int)k, wmax, thr);
+                       ldu, r, wmax, thr);
   RSX_LAUNCHED();
   // RSX_TOPK_COLLECT (A/B): 2 (default) topk_bf16_collect_k, per-score appends behind the max gate;
   // 1 its max-first extraction; 0 topk_bf16_scan_k<G, 8, 1> (round 3's full scan)
@@ -1413,13 +1462,17 @@ int run_bf16_chunk(const BfPlan& bp, const BfLayout& L, const float* U, int64_t 
   } else if (collect_k == 0) {
     if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_scan_k<2, 8, 1>), grid, dim3(256), 0, st, b);
     else hipLaunchKernelGGL((topk_bf16_scan_k<1, 8, 1>), grid, dim3(256), 0, st, b);
+  } else if (collect_k == 3) {  // A/B: the appends without the wave-uniform ballot branches
+    if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_collect_k<2, false, false>), grid, dim3(256), 0, st, b);
+    else hipLaunchKernelGGL((topk_bf16_collect_k<1, false, false>), grid, dim3(256), 0, st, b);
   } else {
     if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_collect_k<2, false>), grid, dim3(256), 0, st, b);
     else hipLaunchKernelGGL((topk_bf16_collect_k<1, false>), grid, dim3(256), 0, st, b);
   }
   RSX_LAUNCHED();
   hipLaunchKernelGGL(topk_bf16_select_k, dim3((unsigned)Q), dim3(256), 0, st, b.buf_e, b.buf_n,
-                     bp.nsplit * 2, U, ldu, I, ldi, (int)k, wmax, out_scores, out_idx, qcount, qmap, qtotal);
+                     bp.nsplit * 2, U, ldu, I, ldi, (int)k, wmax, thr, r < k ? 1 : 0, out_scores, out_idx, qcount,
+                     qmap, qtotal);
   RSX_LAUNCHED();
   // exact list-based kernels for the queries P4 listed (none on spread data)
   return launch_old(U, ldu, I, ldi, Q, NI, k, w + L.fallback, out_scores, out_idx, nullptr, st, qmap, qcount);
