@@ -1391,6 +1391,55 @@ __device__ __forceinline__ f32x16 dots_g_x3(const X3Tile& t, int c, int h, const
   return acc;
 }
 
+// One G pair (rows 2p, 2p+1 of the tile, the dots_g_x3 formula) as hi/lo bf16 words.
+template <bool ROW>
+__device__ __forceinline__ void g_pair(const f32x16& S, int p, int h, const float* m0, const float* m1, float o_m2,
+                                       float it2, float fo, uint32_t& hp, uint32_t& lp) {
+  const f32x4 q0 = *reinterpret_cast<const f32x4*>(m0 + 8 * (p >> 1) + 4 * h);
+  f32x4 q1 = q0;
+  if (ROW) q1 = *reinterpret_cast<const f32x4*>(m1 + 8 * (p >> 1) + 4 * h);
+  float gp[2];
+#pragma unroll
+  for (int rr = 0; rr < 2; ++rr) {
+    const int r = 2 * p + rr, e = r & 3;
+    const float f = ROW ? fo * q1[e] : fo;
+    gp[rr] = f * __builtin_amdgcn_exp2f(fmaf(S[r], it2, -(q0[e] + o_m2)));
+  }
+  split_pair(gp[0], gp[1], hp, lp);
+}
+
+// k-step ks of the backward's gradient product, gacc[nb] += G_ks^T X; WORK: G pair 4 + nb (the
+// next k-step's rows) computed under step nb's three MFMAs, so half of the tile's G work runs
+// in the MFMA issue gaps of the same wave (grad_half_x3's pattern for the fused forward). Same
+// MFMA order as grad_x3s, same G arithmetic as dots_g_x3: bit-identical results.
+template <bool ROW, bool WORK>
+__device__ __forceinline__ void grad_half_g_x3(f32x16 (&gacc)[4], const bf16x8& gh, const bf16x8& gl, const X3Tile& t,
+                                               int base, int ks, const f32x16& S, int h, const float* m0,
+                                               const float* m1, float o_m2, float it2, float fo, uint32_t (&oh)[4],
+                                               uint32_t (&ol)[4]) {
+  bf16x8 bh, bl;
+  grad_rd(t.hi, base, ks, 0, bh);
+  grad_rd(t.lo, base, ks, 0, bl);
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) {
+    bf16x8 nh = bh, nl = bl;
+    if (nb < 3) {
+      grad_rd(t.hi, base, ks, nb + 1, nh);
+      grad_rd(t.lo, base, ks, nb + 1, nl);
+    }
+    gacc[nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gl, bh, gacc[nb], 0, 0, 0);
+    gacc[nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gh, bl, gacc[nb], 0, 0, 0);
+    gacc[nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gh, bh, gacc[nb], 0, 0, 0);
+    if (WORK) {
+      g_pair<ROW>(S, 4 + nb, h, m0, m1, o_m2, it2, fo, oh[nb], ol[nb]);
+      asm volatile("" : "+v"(oh[nb]), "+v"(ol[nb]));  // pins the work to this step (no sinking)
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    bh = nh;
+    bl = nl;
+  }
+}
+
 __global__ __launch_bounds__(256, 2) void nce_grouped_fwd_x3_k(GArgs a) {
   __shared__ __attribute__((aligned(16))) X3Tile sT[2];
   __shared__ __attribute__((aligned(16))) float sB2[2][kTile];   // bias_d * log2e (0 past the split)
@@ -1533,7 +1582,7 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_fwd_x3_k(GArgs a) {
 // common path never waits on memory before its LDS store. Only the rare exception tiles
 // load after the prefetch. PIPE: the S tile of tile t+1 runs
 // interleaved with G of tile t (dots_g_x3) over a three-deep LDS ring.
-template <bool ROW_OWNED>
+template <bool ROW_OWNED, bool HALFG = true>
 __global__ __launch_bounds__(256, RSX_BWD_X3_OCC) void nce_grouped_bwd_x3_k(GArgs a) {
   constexpr int kRing = RSX_BWD_X3_PIPE ? 3 : 2;
   __shared__ __attribute__((aligned(16))) X3Tile sT[kRing];
@@ -1741,16 +1790,37 @@ __global__ __launch_bounds__(256, RSX_BWD_X3_OCC) void nce_grouped_bwd_x3_k(GArg
       if (has_next) gload(s0 + kTile);
       f32x16 acc = dots_x3(sT[cur], c, h, uh, ul);
       bf16x8 gh[2], gl[2];
-      if (__any(exc)) {
+      const bool any_exc = __any(exc);
+      if (any_exc) {
         float n[16];
         int tl;
         exc_counts(s0, exc, n, tl);
         g_exc(acc, cur, exc, n, tl);
         split_tile(acc, gh, gl);
+      } else if (HALFG) {
+        // G rows of k-step 0, then k-step 0's product with k-step 1's G rows under its MFMAs
+        u32x4 h0, l0;
+#pragma unroll
+        for (int pp = 0; pp < 4; ++pp) {
+          uint32_t hp, lp;
+          g_pair<ROW_OWNED>(acc, pp, h, sM0[cur], sM1[cur], o_m2, it2, fo, hp, lp);
+          h0[pp] = hp;
+          l0[pp] = lp;
+        }
+        gh[0] = __builtin_bit_cast(bf16x8, h0);
+        gl[0] = __builtin_bit_cast(bf16x8, l0);
+        uint32_t oh[4], ol[4];
+        const int gbase = grad_lane_base(lane);
+        grad_half_g_x3<ROW_OWNED, true>(gacc, gh[0], gl[0], sT[cur], gbase, 0, acc, h, sM0[cur], sM1[cur], o_m2, it2,
+                                        fo, oh, ol);
+        gh[1] = __builtin_bit_cast(bf16x8, u32x4{oh[0], oh[1], oh[2], oh[3]});
+        gl[1] = __builtin_bit_cast(bf16x8, u32x4{ol[0], ol[1], ol[2], ol[3]});
+        grad_half_g_x3<ROW_OWNED, false>(gacc, gh[1], gl[1], sT[cur], gbase, 1, acc, h, sM0[cur], sM1[cur], o_m2,
+                                         it2, fo, oh, ol);
       } else {
         dots_g_x3<ROW_OWNED, false>(sT[cur], c, h, uh, ul, acc, sM0[cur], sM1[cur], o_m2, it2, fo, gh, gl);
       }
-      grad_x3s(gacc, gh, gl, sT[cur], lane);
+      if (!HALFG || any_exc) grad_x3s(gacc, gh, gl, sT[cur], lane);
       if (has_next) lstore(cur ^ 1);  // cur^1: read in the previous tile, fenced by its barrier
 #if RSX_BWD_VMCNT0
       __builtin_amdgcn_s_waitcnt(kVmcnt0);  // nothing pending at the loop head on any path
@@ -3041,6 +3111,17 @@ RSX_API int rsx_nce_grouped_fwd_grad(const float* A, const float* B, const float
   return 0;
 }
 
+namespace {
+// RSX_NCE_BWD_HALFG=0: the column backward without the half-G overlap (A/B)
+bool bwd_halfg() {
+  static const bool on = [] {
+    const char* e = getenv("RSX_NCE_BWD_HALFG");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+}  // namespace
+
 RSX_API int rsx_nce_grouped_bwd(const float* A, const float* B, const float* bias, const float* colcnt,
                                 const int* row_col, const int* row_beg, const int* row_end, const int* exc_cols,
                                 const int* col_beg, const int* col_end, const int* exc_s, const int* exc_e,
@@ -3110,8 +3191,9 @@ RSX_API int rsx_nce_grouped_bwd(const float* A, const float* B, const float* bia
         RSX_LAUNCHED();
       }
     }
-    if (row_owned && x3) hipLaunchKernelGGL(nce_grouped_bwd_x3_k<true>, dim3(blocks), dim3(256), 0, st, g);
-    else if (x3) hipLaunchKernelGGL(nce_grouped_bwd_x3_k<false>, dim3(blocks), dim3(256), 0, st, g);
+    if (row_owned && x3) hipLaunchKernelGGL((nce_grouped_bwd_x3_k<true, false>), dim3(blocks), dim3(256), 0, st, g);
+    else if (x3 && bwd_halfg()) hipLaunchKernelGGL((nce_grouped_bwd_x3_k<false, true>), dim3(blocks), dim3(256), 0, st, g);
+    else if (x3) hipLaunchKernelGGL((nce_grouped_bwd_x3_k<false, false>), dim3(blocks), dim3(256), 0, st, g);
     else if (row_owned) hipLaunchKernelGGL(nce_grouped_bwd_k<true>, dim3(blocks), dim3(256), 0, st, g);
     else hipLaunchKernelGGL(nce_grouped_bwd_k<false>, dim3(blocks), dim3(256), 0, st, g);
     RSX_LAUNCHED();

@@ -675,7 +675,7 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_scan_k(BfArgs a) {
 // under the next tile's MFMAs (2.49 ms). The entries of a stream are the same set in every form;
 // their order within the stream differs with EXTRACT, which P4 never sees (its margin set and
 // final sort use the total order (score desc, index asc)).
-template <int G, bool EXTRACT, bool BALLOT = true>
+template <int G, bool EXTRACT, bool BALLOT = false>
 __global__ __launch_bounds__(256, 2) void topk_bf16_collect_k(BfArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned char sI[2][kTile * kImgStride];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -772,9 +772,9 @@ __global__ __launch_bounds__(256, 2) void topk_bf16_collect_k(BfArgs a) {
           m = fmaxf(fmaxf(fmaxf(n0, n1), fmaxf(n2, n3)), fmaxf(n4, v[15]));
         }
       } else if (full) {  // whole tile inside the split: one compare per score
-        // each append behind a wave-uniform branch on the ballot of its compare: with ~1 passing
-        // score per wave and group, the other 15 append bodies are skipped, not executed under an
-        // empty exec mask (the compiler's choice for short divergent blocks: ~8 VALU each)
+        // BALLOT (A/B, RSX_TOPK_COLLECT=3): each append behind a wave-uniform branch on the ballot of
+        // its compare. The compiler already skips empty append bodies (s_cbranch_execnz to
+        // out-of-line blocks); the ballots only add SALU (4096 x 1M: 1.69 vs 1.50 ms)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const bool pass = acc[g][r] >= thr[g];
@@ -1462,9 +1462,9 @@ int run_bf16_chunk(const BfPlan& bp, const BfLayout& L, const float* U, int64_t 
   } else if (collect_k == 0) {
     if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_scan_k<2, 8, 1>), grid, dim3(256), 0, st, b);
     else hipLaunchKernelGGL((topk_bf16_scan_k<1, 8, 1>), grid, dim3(256), 0, st, b);
-  } else if (collect_k == 3) {  // A/B: the appends without the wave-uniform ballot branches
-    if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_collect_k<2, false, false>), grid, dim3(256), 0, st, b);
-    else hipLaunchKernelGGL((topk_bf16_collect_k<1, false, false>), grid, dim3(256), 0, st, b);
+  } else if (collect_k == 3) {  // A/B: each append behind a wave-uniform ballot branch (slower: 1.69 vs 1.50 ms)
+    if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_collect_k<2, false, true>), grid, dim3(256), 0, st, b);
+    else hipLaunchKernelGGL((topk_bf16_collect_k<1, false, true>), grid, dim3(256), 0, st, b);
   } else {
     if (bp.G == 2) hipLaunchKernelGGL((topk_bf16_collect_k<2, false>), grid, dim3(256), 0, st, b);
     else hipLaunchKernelGGL((topk_bf16_collect_k<1, false>), grid, dim3(256), 0, st, b);
