@@ -1145,6 +1145,9 @@ __global__ __launch_bounds__(256) void nce_split_k(const float* src, int64_t ld,
 // S tile: acc[r] = <streamed row tile_row(r,h), owner row c> (owner on the lane).
 // The next k-step's fragments are read before this step's MFMAs (LDS latency under MFMA);
 // the scheduling barrier keeps the compiler from hoisting more reads (VGPR budget).
+#ifndef RSX_ABL_LDS
+#define RSX_ABL_LDS 0  // timing probe only (wrong results): reuse every other LDS fragment read
+#endif
 __device__ __forceinline__ f32x16 dots_x3(const X3Tile& t, int c, int h, const bf16x8 (&uh)[8],
                                           const bf16x8 (&ul)[8]) {
   f32x16 acc;
@@ -1156,7 +1159,7 @@ __device__ __forceinline__ f32x16 dots_x3(const X3Tile& t, int c, int h, const b
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
     bf16x8 nh = ah, nl = al;
-    if (s < 7) {
+    if (s < 7 && !(RSX_ABL_LDS && (s & 1) == 0)) {
       nh = *reinterpret_cast<const bf16x8*>(&t.hi[base + 8 * (s + 1)]);
       nl = *reinterpret_cast<const bf16x8*>(&t.lo[base + 8 * (s + 1)]);
     }
@@ -1191,7 +1194,7 @@ __device__ __forceinline__ void grad_x3s(f32x16 (&gacc)[4], const bf16x8 (&gh)[2
 #pragma unroll
   for (int step = 0; step < 8; ++step) {
     bf16x8 nh = bh, nl = bl;
-    if (step < 7) {
+    if (step < 7 && !(RSX_ABL_LDS && (step & 1) == 0)) {
       rd(t.hi, step + 1, nh);
       rd(t.lo, step + 1, nl);
     }
