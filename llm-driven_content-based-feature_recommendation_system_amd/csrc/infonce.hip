@@ -1148,11 +1148,23 @@ __global__ __launch_bounds__(256) void nce_split_k(const float* src, int64_t ld,
 #ifndef RSX_ABL_LDS
 #define RSX_ABL_LDS 0  // timing probe only (wrong results): reuse every other LDS fragment read
 #endif
+#ifndef RSX_ABL_2ACC
+#define RSX_ABL_2ACC 0  // timing probe: S product on two alternating accumulators
+#endif
+#ifndef RSX_ABL_NOBAR
+#define RSX_ABL_NOBAR 0  // timing probe (races, wrong results): the column pass without its tile barrier
+#endif
+#ifndef RSX_ABL_NOLOAD
+#define RSX_ABL_NOLOAD 0  // timing probe (wrong results): the column pass re-stages stale registers
+#endif
 __device__ __forceinline__ f32x16 dots_x3(const X3Tile& t, int c, int h, const bf16x8 (&uh)[8],
                                           const bf16x8 (&ul)[8]) {
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+#if RSX_ABL_2ACC
+  f32x16 acc2 = acc;
+#endif
   const int base = img_off(c, 64 * h);
   bf16x8 ah = *reinterpret_cast<const bf16x8*>(&t.hi[base]);
   bf16x8 al = *reinterpret_cast<const bf16x8*>(&t.lo[base]);
@@ -1163,13 +1175,26 @@ __device__ __forceinline__ f32x16 dots_x3(const X3Tile& t, int c, int h, const b
       nh = *reinterpret_cast<const bf16x8*>(&t.hi[base + 8 * (s + 1)]);
       nl = *reinterpret_cast<const bf16x8*>(&t.lo[base + 8 * (s + 1)]);
     }
+#if RSX_ABL_2ACC
+    // timing probe: two accumulators alternating MFMA by MFMA (no back-to-back srcC chain)
+    f32x16& x0 = (s & 1) ? acc2 : acc;
+    f32x16& x1 = (s & 1) ? acc : acc2;
+    x0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, uh[s], x0, 0, 0, 0);
+    x1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, ul[s], x1, 0, 0, 0);
+    x0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, uh[s], x0, 0, 0, 0);
+#else
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, uh[s], acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, ul[s], acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, uh[s], acc, 0, 0, 0);
+#endif
     __builtin_amdgcn_sched_barrier(0);
     ah = nh;
     al = nl;
   }
+#if RSX_ABL_2ACC
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] += acc2[r];
+#endif
   return acc;
 }
 
@@ -1790,7 +1815,7 @@ __global__ __launch_bounds__(256, RSX_BWD_X3_OCC) void nce_grouped_bwd_x3_k(GArg
       const int64_t s0 = s_begin + (int64_t)t * kTile;
       const bool has_next = t + 1 < ntile;
       const bool exc = exc_flag(s0);
-      if (has_next) gload(s0 + kTile);
+      if (has_next && !RSX_ABL_NOLOAD) gload(s0 + kTile);  // RSX_ABL_NOLOAD: timing probe (stale tiles)
       f32x16 acc = dots_x3(sT[cur], c, h, uh, ul);
       bf16x8 gh[2], gl[2];
       const bool any_exc = __any(exc);
@@ -1828,7 +1853,7 @@ __global__ __launch_bounds__(256, RSX_BWD_X3_OCC) void nce_grouped_bwd_x3_k(GArg
 #if RSX_BWD_VMCNT0
       __builtin_amdgcn_s_waitcnt(kVmcnt0);  // nothing pending at the loop head on any path
 #endif
-      __syncthreads();
+      if (!RSX_ABL_NOBAR) __syncthreads();  // RSX_ABL_NOBAR: timing probe only (races)
       cur ^= 1;
     }
 #endif

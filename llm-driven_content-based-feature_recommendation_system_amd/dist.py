@@ -317,6 +317,35 @@ def static_inputs(batch):
     return [batch[k].reshape(-1).to(torch.int64) for k in _STATIC_KEYS[:9]] + [batch[_STATIC_KEYS[9]]]
 
 
+_ELEM = {torch.int64: 8, torch.int32: 4, torch.float32: 4, torch.uint8: 1}
+
+
+def _carve(specs, dev):
+    """Uninitialised tensors ((shape, dtype) per entry, None -> None) carved from one uint8
+    allocation at 256-B aligned offsets (one allocator call instead of one per array)."""
+    sizes, total = [], 0
+    for sp in specs:
+        if sp is None:
+            sizes.append(None)
+            continue
+        shape, dt = sp
+        n = 1
+        for d in shape:
+            n *= d
+        nb = n * _ELEM[dt]
+        sizes.append((total, nb))
+        total += (nb + 255) // 256 * 256
+    buf = torch.empty(max(total, 256), device=dev, dtype=torch.uint8)
+    out = []
+    for sp, sz in zip(specs, sizes):
+        if sp is None:
+            out.append(None)
+            continue
+        o, nb = sz
+        out.append(buf[o:o + nb].view(sp[1]).view(sp[0]))
+    return out
+
+
 def _prepare_step_index_device(batch, pretrained_vecs, pretrained_lookup, n_items) -> StepIndex:
     """prepare_step_index on rsx_step_index_* (csrc/step_index.hip): the same arrays in the same
     orders as the torch builders, with ONE host read (the totals) per batch; at world > 1 the
@@ -348,20 +377,14 @@ def _prepare_step_index_device(batch, pretrained_vecs, pretrained_lookup, n_item
     T, Nr, D, E, U, C, err = tot[:7]
     if err:
         raise IndexError(f"step index: a target / item id outside [0, {n_items})")
-    i64 = dict(device=dev, dtype=torch.int64)
-    i32 = dict(device=dev, dtype=torch.int32)
-    u8 = dict(device=dev, dtype=torch.uint8)
-    out = [torch.empty(T, **i64), torch.empty(T, **i64), torch.empty(T, **i64), torch.empty(T, **u8),
-           torch.empty(B + 1, **i32), torch.empty(B + 1, **i64), torch.empty(Nr, **i64), torch.empty(B, **i64),
-           torch.empty(2 * T, **i64), torch.empty(2 * T, **i64), torch.empty(2 * T, **i64), torch.empty(2 * T, **u8),
-           torch.empty(2 * B + 1, **i32), torch.empty(2 * B + 1, **i64), torch.empty(6, 2 * T, **i64),
-           (torch.empty(2 * T, 128, device=dev, dtype=torch.float32) if pretrained_vecs is None else None),
-           torch.empty(2 * T, **i64), torch.empty(C + 1, **i64), torch.empty(C, **i64), torch.empty(U + 1, **i64),
-           torch.empty(U, **i64),
-           torch.empty(D, **i64), torch.empty(D, device=dev, dtype=torch.float32), torch.empty(Nr, **i32),
-           torch.empty(Nr, **i32), torch.empty(Nr, **i32), torch.empty(Nr, **i32), torch.empty(E, **i32),
-           torch.empty(E, **i32), torch.empty(E, **i32), torch.empty(D, **i32), torch.empty(D, **i32),
-           torch.empty(B, **i64)]
+    i64, i32, u8, f32 = torch.int64, torch.int32, torch.uint8, torch.float32
+    specs = [((T,), i64), ((T,), i64), ((T,), i64), ((T,), u8), ((B + 1,), i32), ((B + 1,), i64), ((Nr,), i64),
+             ((B,), i64), ((2 * T,), i64), ((2 * T,), i64), ((2 * T,), i64), ((2 * T,), u8), ((2 * B + 1,), i32),
+             ((2 * B + 1,), i64), ((6, 2 * T), i64), (((2 * T, 128), f32) if pretrained_vecs is None else None),
+             ((2 * T,), i64), ((C + 1,), i64), ((C,), i64), ((U + 1,), i64), ((U,), i64), ((D,), i64), ((D,), f32),
+             ((Nr,), i32), ((Nr,), i32), ((Nr,), i32), ((Nr,), i32), ((E,), i32), ((E,), i32), ((E,), i32),
+             ((D,), i32), ((D,), i32), ((B,), i64)]
+    out = _carve(specs, dev)  # the 33 index arrays out of ONE allocation
     lk = ops._c(pretrained_lookup) if pretrained_vecs is None else None
     N.check(lib.rsx_step_index_fill(N.ptr(pm8), N.ptr(tgt), N.ptr_array(seq), N.ptr(lk),
                                     lk.stride(0) if lk is not None else 0, B, L, n_items,

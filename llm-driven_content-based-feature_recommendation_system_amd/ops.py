@@ -1462,23 +1462,25 @@ def tower_params(model):
     return ps
 
 
-def tower_native_ok(model, packed, pv) -> bool:
+def tower_native_ok(model, packed, pv):
     """Whether rsx_tower_* runs exactly what forward_packed's per-op path runs: bf16x3 token linears
     and attention, d_model 128 with 4 heads and a 256-wide feed-forward, every parameter trained,
-    fp32 contiguous rows, the item-id gradient plan present."""
+    fp32 contiguous rows, the item-id gradient plan present. Returns the parameter list in
+    rsx_tower_* order (truthy; tower_packed takes it) or None."""
     if not (_TOWER_NATIVE and _gemm_precision == "bf16x3" and _mha_precision == "bf16x3" and _ADDLN_ON):
-        return False
+        return None
     if getattr(packed, "item_seg", None) is None or not pv.is_cuda:
-        return False
+        return None
     layers = model.transformer_encoder.layers
     if model.d_model != 128 or not (1 <= len(layers) <= 8) or model.pos_emb.weight.shape[0] > 64:
-        return False
+        return None
     for layer in layers:
         if (layer.self_attn.num_heads != 4 or layer.linear1.out_features != 256 or not layer.norm_first
                 or layer.activation_relu_or_gelu != 2):
-            return False
+            return None
     ps = tower_params(model)
-    return all(p.requires_grad and p.dtype == torch.float32 and p.is_contiguous() for p in ps)
+    ok = all(p.requires_grad and p.dtype == torch.float32 and p.is_contiguous() for p in ps)
+    return ps if ok else None
 
 
 _ADDLN_ON = os.environ.get("RSX_LINEAR_ADDLN", "1") != "0"
@@ -1559,15 +1561,16 @@ def _empty_group(likes):
     return out
 
 
-def tower_packed(model, packed, pv_tok, tok_ids, s_g, profile, p_drop):
-    """The native form of SASRecUserTower.forward_packed after the static profile: [T, 128]."""
+def tower_packed(model, packed, pv_tok, tok_ids, s_g, profile, p_drop, params=None):
+    """The native form of SASRecUserTower.forward_packed after the static profile: [T, 128].
+    params: tower_native_ok's list (else rebuilt)."""
     layers = model.transformer_encoder.layers
     eps = [model.emb_ln.eps]
     for layer in layers:
         eps += [layer.norm1.eps, layer.norm2.eps]
     eps.append(model.output_proj[1].eps)
     cfg = (packed, [_c(t) for t in tok_ids], float(p_drop), [float(e) for e in eps], len(layers))
-    return _TowerPacked.apply(pv_tok, s_g, profile, cfg, *tower_params(model))
+    return _TowerPacked.apply(pv_tok, s_g, profile, cfg, *(params if params is not None else tower_params(model)))
 
 
 # ----------------------------------------------------------------------------------------

@@ -350,10 +350,11 @@ class SASRecUserTower(nn.Module):
         # the static profile first (its dropout seed is drawn before the tower's, on both paths)
         profile = self._static_profile(age_bucket, price_bucket, cnt_bucket, recency_bucket, channel_ids,
                                        club_status_ids, news_freq_ids, fn_ids, active_ids, cont_feats, p, packed.B)
-        if torch.is_grad_enabled() and ops.tower_native_ok(self, packed, pretrained_tok):
+        params = ops.tower_native_ok(self, packed, pretrained_tok) if torch.is_grad_enabled() else None
+        if params is not None:
             # the same kernels in the same order as below, issued by the library in one call per
             # direction (rsx_tower_fwd / rsx_tower_bwd)
-            return ops.tower_packed(self, packed, pretrained_tok, tok_ids, s_g, profile, p)
+            return ops.tower_packed(self, packed, pretrained_tok, tok_ids, s_g, profile, p, params)
         base = ops.linear_tok(pretrained_tok, self.item_proj.weight, self.item_proj.bias)
         x = ops.seq_embed(
             base, tok_ids,

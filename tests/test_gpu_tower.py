@@ -263,7 +263,7 @@ def test_native_tower_program_equals_per_op_path(gpu, p_drop):
         ops._TOWER_NATIVE = native
         try:
             pk, pk2, tok_ids, pv, static = ix.packed
-            assert ops.tower_native_ok(model, pk2, pv) == native
+            assert (ops.tower_native_ok(model, pk2, pv) is not None) == native
             torch.manual_seed(9)
             torch.cuda.manual_seed(9)
             out = model.forward_packed(pk2, pv, tok_ids, *static)
