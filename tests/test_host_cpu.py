@@ -1,0 +1,42 @@
+"""Host-side logic of the round-5 step (no GPU): the step index's single-allocation carving
+(dist._carve) and the native clip+AdamW's applicability rules (ops.clip_adamw_step declines what
+it does not reproduce, leaving torch's clip_grad_norm_ + optimizer.step to run)."""
+import torch
+
+from recsys_amd import dist, ops
+
+
+def test_carve_shapes_alignment_and_disjointness():
+    specs = [((5,), torch.int64), None, ((3, 4), torch.float32), ((0,), torch.int32), ((7,), torch.uint8),
+             ((2, 0), torch.int64), ((9,), torch.int32)]
+    out = dist._carve(specs, "cpu")
+    assert out[1] is None
+    spans = []
+    base = out[0].data_ptr()  # the allocation's start (the device allocator aligns it to >= 256 B)
+    for sp, t in zip(specs, out):
+        if sp is None:
+            continue
+        assert tuple(t.shape) == sp[0] and t.dtype == sp[1] and t.is_contiguous()
+        if t.numel():
+            assert (t.data_ptr() - base) % 256 == 0
+            spans.append((t.data_ptr(), t.data_ptr() + t.numel() * t.element_size()))
+    spans.sort()
+    for (a0, a1), (b0, b1) in zip(spans, spans[1:]):
+        assert a1 <= b0                                  # no two arrays overlap
+    out[0].fill_(-1)
+    out[2].fill_(2.5)
+    out[6].fill_(7)
+    assert out[0].tolist() == [-1] * 5 and float(out[2].sum()) == 30.0 and out[6].tolist() == [7] * 9
+
+
+def test_clip_adamw_declines_what_it_does_not_reproduce():
+    p = torch.nn.Parameter(torch.randn(8))
+    p.grad = torch.randn(8)
+    # CPU parameters, another optimizer, amsgrad, a tensor learning rate: nothing done, None returned
+    assert ops.clip_adamw_step(torch.optim.AdamW([p]), [p], 5.0) is None
+    assert ops.clip_adamw_step(torch.optim.SGD([p], lr=0.1), [p], 5.0) is None
+    assert not ops._adamw_native_ok(torch.optim.AdamW([p], amsgrad=True))
+    assert not ops._adamw_native_ok(torch.optim.AdamW([p], lr=torch.tensor(1e-3)))
+    assert not ops._adamw_native_ok(torch.optim.Adam([p]))
+    assert ops._adamw_native_ok(torch.optim.AdamW([p], lr=5e-4, weight_decay=0.01))
+    assert len(torch.optim.AdamW([p]).state) == 0
