@@ -531,11 +531,17 @@ int64_t rsx_hnm_max_rows(void);
  *   params  item_proj w/b, the six tables, pos_emb, emb_ln w/b; per layer norm1 w/b,
  *           in_proj w/b, out_proj w/b, norm2 w/b, linear1 w/b, linear2 w/b; output_proj[0] w/b,
  *           output_proj[1] w/b, output_proj[3] w/b
- * dims[]  T, U, pos rows (max_len), layers, C, Uq, rows of the six tables
+ * dims[]  T, U, pos rows (max_len), layers, C, Uq, rows of the six tables, tail B, tail T1
+ * tail    (dims[12] = B > 0, round 5) the packed rows are two views of B users each (U = 2B,
+ *         T = 2 T1, view 2's token t at row T1 + t) and p[rsx_tower_n_ptrs - 1] holds view 1's
+ *         "last" token of each user [B] int64: the last layer past its attention and the output
+ *         head run on the R = T1 + B rows the contrastive step reads (all of view 1, then view
+ *         2's last row of user b at row T1 + b), `out` is [R,128] and the backward expands their
+ *         gradients to every row (the dropped rows' are zero). dims[12] = 0: every row.
  * fargs[] p_drop, emb_ln eps, per layer norm1 eps, norm2 eps, output LayerNorm eps
  * seeds[] 1 + 4 x layers dropout seeds: embedding, then per layer attention, out-projection
  *         add, feed-forward, closing add (the per-op entry points' seed order)
- * arena   saved activations (rsx_tower_arena_bytes), read by the backward; out [T,128] (the
+ * arena   saved activations (rsx_tower_arena_bytes), read by the backward; out [T or R,128] (the
  *         backward reads it too: the F.normalize backward).
  * grads[] parallel to p[]: params' gradients written, except the embedding stage's (six
  *         tables, pos_emb, emb_ln w/b) and the seq gate's, which are ACCUMULATED (caller

@@ -32,7 +32,7 @@ struct LayerAct {
 struct Layout {  // float offsets into the arena
   int64_t base, x0, m0, r0, h0, mh0, rh0;
   LayerAct l[kMaxLayers];
-  int64_t prof, hp, g, mo, ro, o, nrm, total;
+  int64_t prof, hp, g, mo, ro, o, nrm, aR, xR, tidx, tinv, tuser, tseg, total;
 };
 
 Layout layout(int64_t T, int64_t U, int nl) {
@@ -50,12 +50,16 @@ Layout layout(int64_t T, int64_t U, int nl) {
   }
   s.prof = take(U * kD); s.hp = take(T * kD); s.g = take(T * kD); s.mo = take(T); s.ro = take(T);
   s.o = take(T * kD); s.nrm = take(T);
+  // the tail (rows the losses read, see rsx_tower_fwd): gathered attention output and layer input,
+  // and the row maps (int64, two floats each)
+  s.aR = take(T * kD); s.xR = take(T * kD); s.tidx = take(2 * T); s.tinv = take(2 * T); s.tuser = take(2 * T);
+  s.tseg = take(2 * (U + 1));
   s.total = o;
   return s;
 }
 
 struct BwdLayout {  // float offsets into the workspace
-  int64_t dO, dG, dHp, dX, dXs, dH, dHs, dF, dPre, dRes, dA, dQKV, dProf, dBase, part, wsw, wsl, wse, total;
+  int64_t dO, dG, dHp, dX, dXs, dH, dHs, dF, dPre, dRes, dA, dQKV, dProf, dBase, part, dAR, dXR, wsw, wsl, wse, total;
   int64_t n_wsw, n_wsl, n_wse;
 };
 
@@ -67,6 +71,7 @@ BwdLayout bwd_layout(int64_t T, int64_t U, int64_t L, int64_t C) {
   s.dH = take(T * kD); s.dHs = take(T * kD); s.dF = take(T * kD); s.dPre = take(T * kF); s.dRes = take(T * kD);
   s.dA = take(T * kD); s.dQKV = take(T * kQKV); s.dProf = take(U * kD); s.dBase = take(T * kD);
   s.part = take((C > 0 ? C : 1) * kD);
+  s.dAR = take((T + 1) * kD); s.dXR = take((T + 1) * kD);  // tail rows + one zero row (the expand's source)
   int64_t w = 0;
   const int64_t nk[5][3] = {{T, kD, kD}, {T, kQKV, kD}, {T, kD, kF}, {T, kF, kD}, {U, kD, kD}};
   for (auto& q : nk) {
@@ -81,7 +86,33 @@ BwdLayout bwd_layout(int64_t T, int64_t U, int64_t L, int64_t C) {
   return s;
 }
 
-int64_t n_ptrs(int nl) { return RSX_TW_LAYER0 + 12 * (int64_t)nl + 6; }
+int64_t n_ptrs(int nl) { return RSX_TW_LAYER0 + 12 * (int64_t)nl + 6 + 1; }  // + the tail's last rows
+
+// The tail's row maps. Packed rows [0, T1) are view 1's tokens, [T1, 2 T1) view 2's in the same
+// order; the kept rows are all of view 1 and view 2's "last" row of each user (T1 + last[j]):
+// tidx[r] = the packed row of kept row r; tinv[t] = the kept row of packed row t, or R (a zero
+// row) for the dropped ones; tuser[r] = its user (view 2's user j is B + j); tseg = the kept
+// rows' user offsets (view 1's as they are, then one row per view-2 user).
+__global__ __launch_bounds__(256) void tw_tail_k(const int64_t* __restrict__ last, int64_t T1, int64_t B,
+                                                 const int64_t* __restrict__ tok_user, const int64_t* __restrict__ seg64,
+                                                 int64_t* __restrict__ tidx, int64_t* __restrict__ tinv,
+                                                 int64_t* __restrict__ tuser, int64_t* __restrict__ tseg) {
+  const int64_t T = 2 * T1, R = T1 + B, n = T > 2 * B + 1 ? T : 2 * B + 1;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    if (i <= 2 * B) tseg[i] = i <= B ? seg64[i] : T1 + (i - B);
+    if (i >= T) continue;
+    if (i < R) {
+      tidx[i] = i < T1 ? i : T1 + last[i - T1];
+      tuser[i] = i < T1 ? tok_user[i] : B + (i - T1);
+    }
+    if (i < T1) {
+      tinv[i] = i;
+    } else {
+      const int64_t j = tok_user[i] - B;
+      tinv[i] = (i - T1 == last[j]) ? T1 + j : R;
+    }
+  }
+}
 
 #define TW_CALL(x)            \
   do {                        \
@@ -118,8 +149,14 @@ RSX_API int rsx_tower_fwd(const void* const* p, const int64_t* dims, const float
   RSX_ARG(T > 0 && U > 0 && L > 0 && L <= 64, "need T, U > 0 and 0 < L <= 64");
   const Layout s = layout(T, U, nl);
   RSX_ARG(arena_bytes >= s.total * 4, "arena too small (rsx_tower_arena_bytes)");
-  for (int64_t i = 0; i < n_ptrs(nl); ++i)
+  for (int64_t i = 0; i < n_ptrs(nl) - 1; ++i)
     if (i < RSX_TW_ITEMSEG || i >= RSX_TW_ITEM_PROJ) RSX_ARG(p[i] != nullptr, "null input / parameter pointer");
+  // tail: dims[12] = B users per view (U = 2B), dims[13] = T1 view-1 tokens (T = 2 T1), p[last] =
+  // view 1's "last" token of each user; 0 = every row
+  const int64_t tB = dims[12], T1 = dims[13];
+  const bool tail = tB > 0;
+  RSX_ARG(!tail || (U == 2 * tB && T == 2 * T1 && p[n_ptrs(nl) - 1]), "tail needs U = 2B, T = 2 T1 and the last rows");
+  const int64_t R = tail ? T1 + tB : T;
   const View v{p};
   float* A = static_cast<float*>(arena);
   const float pd = fargs[0];
@@ -144,6 +181,18 @@ RSX_API int rsx_tower_fwd(const void* const* p, const int64_t* dims, const float
   const float* h = A + s.h0;
   const uint8_t* kp = static_cast<const uint8_t*>(p[RSX_TW_TOK_PAD]);
   const int* seg = static_cast<const int*>(p[RSX_TW_SEG32]);
+  int64_t* tidx = reinterpret_cast<int64_t*>(A + s.tidx);
+  int64_t* tuser = reinterpret_cast<int64_t*>(A + s.tuser);
+  int64_t* tseg = reinterpret_cast<int64_t*>(A + s.tseg);
+  if (tail) {
+    const int64_t n = T > 2 * tB + 1 ? T : 2 * tB + 1;
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(tw_tail_k, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                       static_cast<const int64_t*>(p[n_ptrs(nl) - 1]), T1, tB, v.i64(RSX_TW_TOK_USER),
+                       v.i64(RSX_TW_SEG64), tidx, reinterpret_cast<int64_t*>(A + s.tinv), tuser, tseg);
+    RSX_LAUNCHED();
+  }
   for (int i = 0; i < nl; ++i) {
     const int q = RSX_TW_LAYER0 + 12 * i;
     const LayerAct& a = s.l[i];
@@ -152,21 +201,33 @@ RSX_API int rsx_tower_fwd(const void* const* p, const int64_t* dims, const float
     TW_CALL(rsx_gemm_x3(h, kD, v.f(q + 2), kD, v.f(q + 3), T, (int)kQKV, (int)kD, kEpiBias, nullptr, 0, 0.0f, 0,
                         A + a.qkv, kQKV, stream));
     TW_CALL(rsx_mha_fwd_x3(A + a.qkv, kp, seg, U, 64, kHeads, kDh, 1, pd, sd[0], A + a.a, A + a.lse, stream));
+    // the last layer past its attention runs on the tail rows only (the losses read no other row
+    // of view 2; every op from here on is per row)
+    const float* ain = A + a.a;
+    const float* xin = x;
+    int64_t rows = T;
+    if (tail && i == nl - 1) {
+      TW_CALL(rsx_gather_rows(A + a.a, kD, tidx, R, kD, 0, 0.0f, A + s.aR, nullptr, stream));
+      TW_CALL(rsx_gather_rows(x, kD, tidx, R, kD, 0, 0.0f, A + s.xR, nullptr, stream));
+      ain = A + s.aR;
+      xin = A + s.xR;
+      rows = R;
+    }
     // out_proj + residual + norm2 (ops.linear_add_layer_norm)
-    TW_CALL(rsx_gemm_x3_addln(A + a.a, kD, v.f(q + 4), kD, v.f(q + 5), T, kD, kD, x, kD, pd, sd[1], v.f(q + 6),
+    TW_CALL(rsx_gemm_x3_addln(ain, kD, v.f(q + 4), kD, v.f(q + 5), rows, kD, kD, xin, kD, pd, sd[1], v.f(q + 6),
                               v.f(q + 7), fargs[3 + 2 * i], A + a.xs, kD, A + a.hs, kD, A + a.m2, A + a.r2, stream));
     // feed-forward (ops.ffn)
-    TW_CALL(rsx_gemm_x3(A + a.hs, kD, v.f(q + 8), kD, v.f(q + 9), T, (int)kF, (int)kD, kEpiGeluDrop, A + a.gg, kF,
+    TW_CALL(rsx_gemm_x3(A + a.hs, kD, v.f(q + 8), kD, v.f(q + 9), rows, (int)kF, (int)kD, kEpiGeluDrop, A + a.gg, kF,
                         pd, sd[2], A + a.act, kF, stream));
-    TW_CALL(rsx_gemm_x3(A + a.act, kF, v.f(q + 10), kF, v.f(q + 11), T, (int)kD, (int)kF, kEpiBias, nullptr, 0, 0.0f,
-                        0, A + a.f, kD, stream));
+    TW_CALL(rsx_gemm_x3(A + a.act, kF, v.f(q + 10), kF, v.f(q + 11), rows, (int)kD, (int)kF, kEpiBias, nullptr, 0,
+                        0.0f, 0, A + a.f, kD, stream));
     if (i + 1 < nl) {  // residual + the next layer's norm1 (ops.add_layer_norm)
       TW_CALL(rsx_ln_fwd(A + a.xs, A + a.f, pd, sd[3], v.f(q + 12), v.f(q + 13), fargs[2 + 2 * (i + 1)], 0, T, kD,
                          A + a.xn, A + a.hn, A + a.mn, A + a.rn, stream));
       h = A + a.hn;
     } else {  // the closing residual add (ops.add_dropout)
-      TW_CALL(rsx_ln_fwd(A + a.xs, A + a.f, pd, sd[3], nullptr, nullptr, 0.0f, 0, T, kD, A + a.xn, nullptr, nullptr,
-                         nullptr, stream));
+      TW_CALL(rsx_ln_fwd(A + a.xs, A + a.f, pd, sd[3], nullptr, nullptr, 0.0f, 0, rows, kD, A + a.xn, nullptr,
+                         nullptr, nullptr, stream));
     }
     x = A + a.xn;
   }
@@ -175,14 +236,14 @@ RSX_API int rsx_tower_fwd(const void* const* p, const int64_t* dims, const float
   const float* w0 = v.f(pl);
   TW_CALL(rsx_gemm_x3(v.f(RSX_TW_PROFILE), kD, w0 + kD, 2 * kD, v.f(pl + 1), U, kD, kD, kEpiBias, nullptr, 0, 0.0f, 0,
                       A + s.prof, kD, stream));
-  TW_CALL(rsx_gemm_x3_rowadd(x, kD, w0, 2 * kD, nullptr, T, kD, kD, A + s.prof, kD, v.i64(RSX_TW_TOK_USER), A + s.hp,
-                             kD, stream));
+  TW_CALL(rsx_gemm_x3_rowadd(x, kD, w0, 2 * kD, nullptr, R, kD, kD, A + s.prof, kD,
+                             tail ? tuser : v.i64(RSX_TW_TOK_USER), A + s.hp, kD, stream));
   // output_proj[1] + GELU (ops.layer_norm act), output_proj[3], F.normalize (ops.l2_normalize)
-  TW_CALL(rsx_ln_fwd(A + s.hp, nullptr, 0.0f, 0, v.f(pl + 2), v.f(pl + 3), fargs[2 + 2 * nl], kActGelu, T, kD, nullptr,
+  TW_CALL(rsx_ln_fwd(A + s.hp, nullptr, 0.0f, 0, v.f(pl + 2), v.f(pl + 3), fargs[2 + 2 * nl], kActGelu, R, kD, nullptr,
                      A + s.g, A + s.mo, A + s.ro, stream));
-  TW_CALL(rsx_gemm_x3(A + s.g, kD, v.f(pl + 4), kD, v.f(pl + 5), T, kD, kD, kEpiBias, nullptr, 0, 0.0f, 0, A + s.o, kD,
+  TW_CALL(rsx_gemm_x3(A + s.g, kD, v.f(pl + 4), kD, v.f(pl + 5), R, kD, kD, kEpiBias, nullptr, 0, 0.0f, 0, A + s.o, kD,
                       stream));
-  TW_CALL(rsx_gather_rows(A + s.o, kD, nullptr, T, kD, 1, 1e-12f, out, A + s.nrm, stream));
+  TW_CALL(rsx_gather_rows(A + s.o, kD, nullptr, R, kD, 1, 1e-12f, out, A + s.nrm, stream));
   return 0;
 }
 
@@ -198,7 +259,11 @@ RSX_API int rsx_tower_bwd(const void* const* p, const int64_t* dims, const float
   const BwdLayout b = bwd_layout(T, U, L, C);
   RSX_ARG(ws_bytes >= b.total * 4, "workspace too small (rsx_tower_bwd_workspace_bytes)");
   const int pl = RSX_TW_LAYER0 + 12 * nl;
-  for (int64_t i = RSX_TW_ITEM_PROJ; i < n_ptrs(nl); ++i) RSX_ARG(grads[i] != nullptr, "null parameter gradient");
+  for (int64_t i = RSX_TW_ITEM_PROJ; i < n_ptrs(nl) - 1; ++i) RSX_ARG(grads[i] != nullptr, "null parameter gradient");
+  const int64_t tB = dims[12], T1 = dims[13];
+  const bool tail = tB > 0;
+  RSX_ARG(!tail || (U == 2 * tB && T == 2 * T1), "tail needs U = 2B and T = 2 T1");
+  const int64_t R = tail ? T1 + tB : T;
   RSX_ARG(grads[RSX_TW_GATE] && grads[RSX_TW_PROFILE], "null gate / profile gradient");
   RSX_ARG(C == 0 || (p[RSX_TW_ITEMSEG] && p[RSX_TW_ITEMSEG + 1] && p[RSX_TW_ITEMSEG + 2] && p[RSX_TW_ITEMSEG + 3] &&
                      p[RSX_TW_ITEMSEG + 4]), "item-id gradient plan required");
@@ -221,22 +286,22 @@ RSX_API int rsx_tower_bwd(const void* const* p, const int64_t* dims, const float
                 int64_t ldc) {
     return rsx_gemm_x3_tn(dy, ldy, w, ldw, nullptr, m, n, k, kEpiBias, nullptr, 0, 0.0f, 0, c, ldc, stream);
   };
-  // F.normalize (ops.l2_normalize: gather_rows backward, store)
-  TW_CALL(rsx_scatter_rows(dout, out, A + s.nrm, nullptr, T, kD, 1, 1e-12f, 0, -1, W + b.dO, kD, stream));
+  // F.normalize (ops.l2_normalize: gather_rows backward, store); the head runs on the R output rows
+  TW_CALL(rsx_scatter_rows(dout, out, A + s.nrm, nullptr, R, kD, 1, 1e-12f, 0, -1, W + b.dO, kD, stream));
   // output_proj[3] (_TokLinear: dX, then dW / db)
-  TW_CALL(tn(W + b.dO, kD, v.f(pl + 4), kD, T, kD, kD, W + b.dG, kD));
-  TW_CALL(wgrad(W + b.dO, kD, A + s.g, kD, T, kD, kD, G(pl + 4), kD, G(pl + 5)));
+  TW_CALL(tn(W + b.dO, kD, v.f(pl + 4), kD, R, kD, kD, W + b.dG, kD));
+  TW_CALL(wgrad(W + b.dO, kD, A + s.g, kD, R, kD, kD, G(pl + 4), kD, G(pl + 5)));
   // output_proj[1] + GELU (_LayerNorm)
-  TW_CALL(rsx_ln_bwd(A + s.hp, A + s.mo, A + s.ro, v.f(pl + 2), v.f(pl + 3), kActGelu, W + b.dG, nullptr, 0.0f, 0, T,
+  TW_CALL(rsx_ln_bwd(A + s.hp, A + s.mo, A + s.ro, v.f(pl + 2), v.f(pl + 3), kActGelu, W + b.dG, nullptr, 0.0f, 0, R,
                      kD, W + b.dHp, nullptr, G(pl + 2), G(pl + 3), wsl, b.n_wsl, stream));
   // output_proj[0] (_ProfileLinear): per-user sums, dX, d(profile), both weight halves and the bias
   const float* w0 = v.f(pl);
   const float* xl = A + s.l[nl - 1].xn;
-  TW_CALL(rsx_segment_sum_rows(W + b.dHp, kD, nullptr, v.i64(RSX_TW_SEG64), nullptr, U, kD, nullptr, -1, W + b.dProf,
-                               kD, 0, stream));
-  TW_CALL(tn(W + b.dHp, kD, w0, 2 * kD, T, kD, kD, W + b.dX, kD));
+  const int64_t* useg = tail ? reinterpret_cast<const int64_t*>(A + s.tseg) : v.i64(RSX_TW_SEG64);
+  TW_CALL(rsx_segment_sum_rows(W + b.dHp, kD, nullptr, useg, nullptr, U, kD, nullptr, -1, W + b.dProf, kD, 0, stream));
+  TW_CALL(tn(W + b.dHp, kD, w0, 2 * kD, R, kD, kD, W + b.dX, kD));
   TW_CALL(tn(W + b.dProf, kD, w0 + kD, 2 * kD, U, kD, kD, G(RSX_TW_PROFILE), kD));
-  TW_CALL(wgrad(W + b.dHp, kD, xl, kD, T, kD, kD, G(pl), 2 * kD, nullptr));
+  TW_CALL(wgrad(W + b.dHp, kD, xl, kD, R, kD, kD, G(pl), 2 * kD, nullptr));
   TW_CALL(wgrad(W + b.dProf, kD, v.f(RSX_TW_PROFILE), kD, U, kD, kD, G(pl) + kD, 2 * kD, G(pl + 1)));
   // encoder stack, last layer first. dX: gradient of the layer's output x; dH: of its output h
   // (the next layer's norm1 output, none for the last layer)
@@ -247,9 +312,11 @@ RSX_API int rsx_tower_bwd(const void* const* p, const int64_t* dims, const float
     const int q = RSX_TW_LAYER0 + 12 * i;
     const LayerAct& a = s.l[i];
     const uint64_t* sd = seeds + 1 + 4 * i;
+    const bool tl = tail && i == nl - 1;  // this layer's post-attention ops ran on the R tail rows
+    const int64_t rows = tl ? R : T;
     float* dF = W + b.dF;
     if (i == nl - 1) {  // _AddDropout: d(xs) = dX itself, d(f) = the dropout mask applied to it
-      TW_CALL(rsx_dropout_bwd(dX, T, kD, pd, sd[3], dF, stream));
+      TW_CALL(rsx_dropout_bwd(dX, rows, kD, pd, sd[3], dF, stream));
       std::swap(dX, dXs);  // dXs now names the gradient of xs
     } else {  // _AddLayerNorm of the next layer's norm1: (ds = dX, dy = dH) -> d(xs), d(f)
       const int qn = RSX_TW_LAYER0 + 12 * (i + 1);
@@ -259,18 +326,34 @@ RSX_API int rsx_tower_bwd(const void* const* p, const int64_t* dims, const float
     // _FFN: dPre (dGELU + dropout epilogue), dW2 / db2, dW1 / db1, d(hs)
     float* dPre = W + b.dPre;
     float* dHs = W + b.dHs;
-    TW_CALL(rsx_gemm_x3_tn(dF, kD, v.f(q + 10), kF, nullptr, T, (int)kF, (int)kD, kEpiDgeluDrop,
+    TW_CALL(rsx_gemm_x3_tn(dF, kD, v.f(q + 10), kF, nullptr, rows, (int)kF, (int)kD, kEpiDgeluDrop,
                            const_cast<float*>(A + a.gg), kF, pd, sd[2], dPre, kF, stream));
-    TW_CALL(wgrad(dF, kD, A + a.act, kF, T, kD, kF, G(q + 10), kF, G(q + 11)));
-    TW_CALL(wgrad(dPre, kF, A + a.hs, kD, T, kF, kD, G(q + 8), kD, G(q + 9)));
-    TW_CALL(tn(dPre, kF, v.f(q + 8), kD, T, (int)kD, (int)kF, dHs, kD));
+    TW_CALL(wgrad(dF, kD, A + a.act, kF, rows, kD, kF, G(q + 10), kF, G(q + 11)));
+    TW_CALL(wgrad(dPre, kF, A + a.hs, kD, rows, kF, kD, G(q + 8), kD, G(q + 9)));
+    TW_CALL(tn(dPre, kF, v.f(q + 8), kD, rows, (int)kD, (int)kF, dHs, kD));
     // _LinearAddLayerNorm: (ds = d(xs), dy = d(hs)) -> d(x_in), d(out_proj output); then d(a), dWo, dbo
     float* dRes = W + b.dRes;
-    TW_CALL(rsx_ln_bwd(A + a.xs, A + a.m2, A + a.r2, v.f(q + 6), v.f(q + 7), 0, dHs, dXs, pd, sd[1], T, kD, dX, dRes,
-                       G(q + 6), G(q + 7), wsl, b.n_wsl, stream));
     float* dA = W + b.dA;
-    TW_CALL(tn(dRes, kD, v.f(q + 4), kD, T, kD, kD, dA, kD));
-    TW_CALL(wgrad(dRes, kD, A + a.a, kD, T, kD, kD, G(q + 4), kD, G(q + 5)));
+    if (tl) {
+      // tail rows: d(x_in) and d(a) land in R-row buffers with a zero row R, then expand to every
+      // packed row through the inverse map (dropped rows read the zero row)
+      float* dXR = W + b.dXR;
+      float* dAR = W + b.dAR;
+      (void)hipMemsetAsync(dXR + R * kD, 0, kD * sizeof(float), (hipStream_t)stream);
+      (void)hipMemsetAsync(dAR + R * kD, 0, kD * sizeof(float), (hipStream_t)stream);
+      TW_CALL(rsx_ln_bwd(A + a.xs, A + a.m2, A + a.r2, v.f(q + 6), v.f(q + 7), 0, dHs, dXs, pd, sd[1], R, kD, dXR, dRes,
+                         G(q + 6), G(q + 7), wsl, b.n_wsl, stream));
+      TW_CALL(tn(dRes, kD, v.f(q + 4), kD, R, kD, kD, dAR, kD));
+      TW_CALL(wgrad(dRes, kD, A + s.aR, kD, R, kD, kD, G(q + 4), kD, G(q + 5)));
+      const int64_t* tinv = reinterpret_cast<const int64_t*>(A + s.tinv);
+      TW_CALL(rsx_gather_rows(dXR, kD, tinv, T, kD, 0, 0.0f, dX, nullptr, stream));
+      TW_CALL(rsx_gather_rows(dAR, kD, tinv, T, kD, 0, 0.0f, dA, nullptr, stream));
+    } else {
+      TW_CALL(rsx_ln_bwd(A + a.xs, A + a.m2, A + a.r2, v.f(q + 6), v.f(q + 7), 0, dHs, dXs, pd, sd[1], T, kD, dX, dRes,
+                         G(q + 6), G(q + 7), wsl, b.n_wsl, stream));
+      TW_CALL(tn(dRes, kD, v.f(q + 4), kD, T, kD, kD, dA, kD));
+      TW_CALL(wgrad(dRes, kD, A + a.a, kD, T, kD, kD, G(q + 4), kD, G(q + 5)));
+    }
     // _MHA, then in_proj (_TokLinear)
     float* dQKV = W + b.dQKV;
     TW_CALL(rsx_mha_bwd_x3(A + a.qkv, kp, seg, A + a.a, A + a.lse, dA, U, 64, kHeads, kDh, 1, pd, sd[0], dQKV,

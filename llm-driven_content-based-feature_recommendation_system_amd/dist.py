@@ -571,12 +571,15 @@ def contrastive_objective_dp(model, item_tower, log_q_tensor, batch, cfg, pretra
     else:
         _adopt(index)
     B = index.B
-    pk, out = packed_out(model, batch, pretrained_vecs, pretrained_lookup, packed=index.packed)
+    # tail: the tower's last layer past attention and its output head run only on the rows read
+    # here (all of view 1; view 2's "last" row per user, rows T..T+B-1 of `out`)
+    pk, out = packed_out(model, batch, pretrained_vecs, pretrained_lookup, packed=index.packed, tail=True)
     # the loss rows of view 1 (valid steps, normalised again: the reference's F.normalize of the
     # already-normalised output) and the "last" rows of both views, gathered by one autograd node
     # whose backward writes a single gradient of `out`
     T = pk.flat.numel()
-    u_loc, z1, z2 = ops.gather_rows_multi(out, [(pk.valid_tok, True), (pk.last_tok, True), (pk.last_tok + T, True)])
+    last2 = torch.arange(T, T + pk.last_tok.numel(), device=out.device)
+    u_loc, z1, z2 = ops.gather_rows_multi(out, [(pk.valid_tok, True), (pk.last_tok, True), (last2, True)])
 
     # ---- main LogQ loss over all valid steps of the global batch
     n_glob = index.n_glob

@@ -1492,7 +1492,7 @@ class _TowerPacked(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, pv, gate, profile, cfg, *params):
-        packed, tok_ids, p_drop, eps, nl = cfg
+        packed, tok_ids, p_drop, eps, nl, tail_last = cfg
         T, D = pv.shape
         U = packed.seg_off.numel() - 1
         dev = pv.device
@@ -1502,21 +1502,24 @@ class _TowerPacked(torch.autograd.Function):
         perm, cb, chunk_ids, ch_off, uniq = packed.item_seg
         inputs = ([pv] + list(tok_ids) + [packed.tok_pos, packed.tok_pad, packed.seg_off, packed.seg_off64,
                                             packed.tok_user, gate, profile, perm, cb, chunk_ids, ch_off, uniq])
-        ptrs = N.ptr_array(inputs + list(params))
+        tail_last = None if tail_last is None else _c(tail_last)
+        ptrs = N.ptr_array(inputs + list(params) + [tail_last])
         tabs = params[2:8]
+        tB = 0 if tail_last is None else tail_last.numel()
+        R = T // 2 + tB if tB else T
         dims = N.i64_array([T, U, params[8].shape[0], nl, chunk_ids.numel(), uniq.numel()]
-                           + [t.shape[0] for t in tabs])
+                           + [t.shape[0] for t in tabs] + [tB, T // 2])
         fargs = (ctypes.c_float * (len(eps) + 1))(p_drop, *eps)
         seeds = [next_seed() if p_drop > 0 else 0 for _ in range(1 + 4 * nl)]
         seeds_arr = (ctypes.c_uint64 * len(seeds))(*seeds)
         nbytes = N.lib().rsx_tower_arena_bytes(T, U, nl)
         arena = torch.empty(nbytes, device=dev, dtype=torch.uint8)
-        out = torch.empty(T, D, device=dev, dtype=torch.float32)
+        out = torch.empty(R, D, device=dev, dtype=torch.float32)
         with timed("tower_fwd"):
             rc = N.lib().rsx_tower_fwd(ptrs, dims, fargs, seeds_arr, N.ptr(arena), nbytes, N.ptr(out), N.stream())
         N.check(rc, "tower_fwd")
         ctx.save_for_backward(pv, gate, profile, out, *params)
-        ctx.keep = (inputs, arena, ptrs, dims, fargs, seeds_arr)
+        ctx.keep = (inputs + [tail_last], arena, ptrs, dims, fargs, seeds_arr)
         ctx.shape = (T, U, params[8].shape[0], nl, chunk_ids.numel())
         return out
 
@@ -1535,7 +1538,7 @@ class _TowerPacked(torch.autograd.Function):
         dprofile = written[-1]
         dparams = [written[0], written[1]] + acc + written[2:-1]
         dpv = torch.empty_like(pv) if ctx.needs_input_grad[0] else None
-        grads = [dpv] + [None] * 11 + [dgate, dprofile] + [None] * 5 + dparams
+        grads = [dpv] + [None] * 11 + [dgate, dprofile] + [None] * 5 + dparams + [None]
         nws = N.lib().rsx_tower_bwd_workspace_bytes(T, U, L, nl, C)
         ws = torch.empty(nws, device=dev, dtype=torch.uint8)
         with timed("tower_bwd"):
@@ -1561,15 +1564,16 @@ def _empty_group(likes):
     return out
 
 
-def tower_packed(model, packed, pv_tok, tok_ids, s_g, profile, p_drop, params=None):
-    """The native form of SASRecUserTower.forward_packed after the static profile: [T, 128].
-    params: tower_native_ok's list (else rebuilt)."""
+def tower_packed(model, packed, pv_tok, tok_ids, s_g, profile, p_drop, params=None, tail_last=None):
+    """The native form of SASRecUserTower.forward_packed after the static profile: [T, 128], or with
+    tail_last (view 1's "last" token per user, [B]) the [T/2 + B, 128] tail rows (see
+    rsx_tower_fwd). params: tower_native_ok's list (else rebuilt)."""
     layers = model.transformer_encoder.layers
     eps = [model.emb_ln.eps]
     for layer in layers:
         eps += [layer.norm1.eps, layer.norm2.eps]
     eps.append(model.output_proj[1].eps)
-    cfg = (packed, [_c(t) for t in tok_ids], float(p_drop), [float(e) for e in eps], len(layers))
+    cfg = (packed, [_c(t) for t in tok_ids], float(p_drop), [float(e) for e in eps], len(layers), tail_last)
     return _TowerPacked.apply(pv_tok, s_g, profile, cfg, *(params if params is not None else tower_params(model)))
 
 

@@ -336,7 +336,7 @@ class SASRecUserTower(nn.Module):
         return ops.static_profile(self, ids, cont_feats, p, rows)
 
     def forward_packed(self, packed, pretrained_tok, tok_ids, age_bucket, price_bucket, cnt_bucket, recency_bucket,
-                       channel_ids, club_status_ids, news_freq_ids, fn_ids, active_ids, cont_feats):
+                       channel_ids, club_status_ids, news_freq_ids, fn_ids, active_ids, cont_feats, tail_last=None):
         """Training-mode forward restricted to the tokens whose outputs the contrastive step
         reads (every valid step + the bug-compatible DuoRec "last" position of each user).
 
@@ -344,7 +344,12 @@ class SASRecUserTower(nn.Module):
         equals the corresponding row of forward(..., training_mode=True): with left padding a
         valid query never attends to padded keys, a padded query attends to nothing, and
         every other op is per token, so dropping the other padded tokens changes no value
-        the losses see. tok_ids: [item, time, type, color, graphic, section] ids per token."""
+        the losses see. tok_ids: [item, time, type, color, graphic, section] ids per token.
+
+        tail_last (view 1's DuoRec "last" token of each user, [B]; packed = both views, view 2's
+        tokens at rows T/2 + t): return only the rows the contrastive step reads, all of view 1
+        and view 2's last row per user ([T/2 + B, D], view 2's in user order). The native program
+        then runs the last layer past its attention and the output head on those rows only."""
         p = self.dropout_rate if self.training else 0.0
         s_g = torch.sigmoid(self.seq_gate) * self._seq_gate_mask
         # the static profile first (its dropout seed is drawn before the tower's, on both paths)
@@ -354,7 +359,7 @@ class SASRecUserTower(nn.Module):
         if params is not None:
             # the same kernels in the same order as below, issued by the library in one call per
             # direction (rsx_tower_fwd / rsx_tower_bwd)
-            return ops.tower_packed(self, packed, pretrained_tok, tok_ids, s_g, profile, p, params)
+            return ops.tower_packed(self, packed, pretrained_tok, tok_ids, s_g, profile, p, params, tail_last)
         base = ops.linear_tok(pretrained_tok, self.item_proj.weight, self.item_proj.bias)
         x = ops.seq_embed(
             base, tok_ids,
@@ -367,7 +372,12 @@ class SASRecUserTower(nn.Module):
         D = self.d_model
         h = ops.profile_linear(x, profile, lin0.weight, lin0.bias, packed.tok_user, packed.seg_off64)
         h = ops.layer_norm(h, ln.weight, ln.bias, ln.eps, act=ops.ACT_GELU_ERF)
-        return ops.l2_normalize(ops.linear_tok(h, lin3.weight, lin3.bias))
+        out = ops.l2_normalize(ops.linear_tok(h, lin3.weight, lin3.bias))
+        if tail_last is not None:  # the per-op path computes every row and keeps the tail ones
+            T1 = out.shape[0] // 2
+            keep = torch.cat([torch.arange(T1, device=out.device), tail_last + T1])
+            out = ops.gather_rows(out, keep, unique=True)
+        return out
 
 
 class PackedTokens:

@@ -128,33 +128,35 @@ def pack_inputs(batch, pretrained_vecs=None, pretrained_lookup=None):
     return pk, pk2, tok_ids, pv_tok, static_inputs(batch)
 
 
-def packed_views(model, batch, pretrained_vecs=None, pretrained_lookup=None, packed=None):
+def packed_views(model, batch, pretrained_vecs=None, pretrained_lookup=None, packed=None, tail=False):
     """Both dropout views (reference :788-789) on the packed token set of the step, run as ONE
     packed pass over the doubled batch: users b and B + b carry the same inputs, so view 1 is
     tokens [0, T) and view 2 tokens [T, 2T) of the output. The views still draw independent
     dropout masks (the kernels key their masks by token row; torch dropout is per element), and
     every kernel launch covers both views (half the launches, no per-parameter gradient adds).
     packed: pack_inputs(batch, ...) computed ahead (else computed here).
-    Returns (packed tokens of one view, out_1 [T, D], out_2 [T, D])."""
-    pk, out = packed_out(model, batch, pretrained_vecs, pretrained_lookup, packed)
+    Returns (packed tokens of one view, out_1 [T, D], out_2 [T, D]); tail: out_2 holds only each
+    user's "last" row [B, D] (the only view-2 rows the losses read; forward_packed tail_last)."""
+    pk, out = packed_out(model, batch, pretrained_vecs, pretrained_lookup, packed, tail=tail)
     T = pk.flat.numel()
     return pk, out[:T], out[T:]
 
 
-def packed_out(model, batch, pretrained_vecs=None, pretrained_lookup=None, packed=None):
+def packed_out(model, batch, pretrained_vecs=None, pretrained_lookup=None, packed=None, tail=False):
     """packed_views without the split: (packed tokens of one view, out [2T, D]); view 2's token t
-    is row T + t (for row gathers of both views in one autograd node, ops.gather_rows_multi)."""
+    is row T + t (for row gathers of both views in one autograd node, ops.gather_rows_multi).
+    tail: out [T + B, D], view 2's "last" row of user b at row T + b."""
     if packed is None:
         packed = pack_inputs(batch, pretrained_vecs, pretrained_lookup)
     pk, pk2, tok_ids, pv_tok, static = packed
-    return pk, model.forward_packed(pk2, pv_tok, tok_ids, *static)
+    return pk, model.forward_packed(pk2, pv_tok, tok_ids, *static, tail_last=pk.last_tok if tail else None)
 
 
 def contrastive_losses(model, item_tower, log_q_tensor, batch, cfg, pretrained_vecs=None, pretrained_lookup=None):
     """Forward of one step (reference :787-845) on the packed token set. Returns (total, main, cl)."""
     device = batch["item_ids"].device
     target_ids = batch["target_ids"]
-    pk, out1, out2 = packed_views(model, batch, pretrained_vecs, pretrained_lookup)
+    pk, out1, out2 = packed_views(model, batch, pretrained_vecs, pretrained_lookup, tail=True)
     n_valid = pk.valid_tok.numel()
     if n_valid > 0:
         # flat_output = output_1[valid_mask] (row-major b, t); F.normalize(flat_output)
@@ -175,7 +177,7 @@ def contrastive_losses(model, item_tower, log_q_tensor, batch, cfg, pretrained_v
 
     # DuoRec on the "last" step: count_valid - 1 (bug-compatible on left-padded rows, :830-835)
     last_output_1 = ops.gather_rows(out1, pk.last_tok, unique=True)
-    last_output_2 = ops.gather_rows(out2, pk.last_tok, unique=True)
+    last_output_2 = out2  # the tail rows: view 2's "last" row of every user, in user order
     last_targets = target_ids.reshape(-1)[pk.flat[pk.last_tok]]
     cl_loss = duorec_loss_refined(last_output_1, last_output_2, last_targets, lambda_sup=cfg.lambda_sup)
     total_loss = main_loss + cfg.lambda_cl * cl_loss

@@ -280,3 +280,41 @@ def test_native_tower_program_equals_per_op_path(gpu, p_drop):
     assert g1.keys() == g2.keys() and len(g1) > 40
     for n in g1:
         assert torch.equal(g1[n], g2[n]), n
+
+
+def test_native_tower_tail_rows(gpu):
+    """The tail form (forward_packed tail_last: the last layer past attention and the head on the
+    rows the losses read: all of view 1 and view 2's "last" row per user) against the per-op path
+    computing every row and keeping those (dropout 0): the kept rows are per-row identical, so
+    the output is bit-identical; the gradients differ only in which zero rows the weight-gradient
+    sums skip (2e-6 of each gradient's scale)."""
+    cfg = small_cfg(num_items=500, dropout=0.0)
+    items = small_universe(500)
+    batch = to_dev(synth.make_batch(items, 96, seed=23), gpu)
+    lookup = items.pretrained.to(gpu)
+    from recsys_amd import dist as D
+    ix = D.prepare_step_index(batch, pretrained_lookup=lookup)
+    pk, pk2, tok_ids, pv, static = ix.packed
+    res = []
+    for native in (True, False):
+        torch.manual_seed(5)
+        model = T.SASRecUserTower(cfg).to(gpu).train()
+        prev = ops._TOWER_NATIVE
+        ops._TOWER_NATIVE = native
+        try:
+            out = model.forward_packed(pk2, pv, tok_ids, *static, tail_last=pk.last_tok)
+            assert out.shape == (pk.flat.numel() + pk.last_tok.numel(), 128)
+            g = torch.Generator(device="cpu").manual_seed(3)
+            w = torch.randn(out.shape, generator=g).to(gpu)
+            (out * w).sum().backward()
+        finally:
+            ops._TOWER_NATIVE = prev
+        torch.cuda.synchronize()
+        res.append((out.detach(), {n: p.grad.detach().clone() for n, p in model.named_parameters()
+                                   if p.grad is not None}))
+    (o1, g1), (o2, g2) = res
+    assert torch.equal(o1, o2)
+    assert g1.keys() == g2.keys()
+    for n in g1:
+        scale = float(g2[n].abs().max()) + 1e-30
+        assert (g1[n] - g2[n]).abs().max().item() <= 2e-6 * scale, n
