@@ -32,7 +32,7 @@ struct LayerAct {
 struct Layout {  // float offsets into the arena
   int64_t base, x0, m0, r0, h0, mh0, rh0;
   LayerAct l[kMaxLayers];
-  int64_t prof, hp, g, mo, ro, o, nrm, aR, xR, tidx, tinv, tuser, tseg, total;
+  int64_t prof, hp, g, mo, ro, o, nrm, aR, xR, tidx, tinv, tuser, tseg, lseq, total;
 };
 
 Layout layout(int64_t T, int64_t U, int nl) {
@@ -53,7 +53,7 @@ Layout layout(int64_t T, int64_t U, int nl) {
   // the tail (rows the losses read, see rsx_tower_fwd): gathered attention output and layer input,
   // and the row maps (int64, two floats each)
   s.aR = take(T * kD); s.xR = take(T * kD); s.tidx = take(2 * T); s.tinv = take(2 * T); s.tuser = take(2 * T);
-  s.tseg = take(2 * (U + 1));
+  s.tseg = take(2 * (U + 1)); s.lseq = take(kHeads * U);
   s.total = o;
   return s;
 }
@@ -125,6 +125,131 @@ struct View {  // typed views of the pointer table
   const float* f(int i) const { return static_cast<const float*>(p[i]); }
   const int64_t* i64(int i) const { return static_cast<const int64_t*>(p[i]); }
 };
+
+// View 2's attention in the tail layer: only each user's "last" query row is read downstream, so
+// instead of the whole causal attention of view 2's sequences, one wave per (user, head) forms
+// that single row: lane k holds key k of the user's segment (L <= 64), fp32 scores over the
+// head's 32 dims (scaled by 1/sqrt(32)), causal (key index <= query index) + key-padding mask,
+// softmax, dropout on the probabilities (keep-mask hash(seed, ((b * 4 + h) * 64 + k)), scaled by
+// 1 / (1 - p)), out = P V. A query with no valid key gets zero output (the training path's
+// fully-masked-row semantics). lse (natural log, -inf when masked) is kept for the backward.
+struct LastQ {
+  const float* qkv;        // [T, 384]
+  const uint8_t* kpad;     // [T]
+  const int64_t* seg64;    // [U + 1] packed user offsets (view 2's users are B + j)
+  const int64_t* last;     // [B] view-1 token index of user j's last row (view 2: + T1)
+  float* out;              // [B, 128] rows of the tail's attention output (view 2 part)
+  float* lse;              // [B, 4]
+  const float* dout;       // [B, 128] (backward)
+  float* dqkv;             // [T, 384] (backward: view 2's rows written whole)
+  int64_t T1, B;
+  rsx::Dropout drop;
+};
+
+__global__ __launch_bounds__(256) void tw_lastq_fwd_k(LastQ a) {
+  const int lane = threadIdx.x & 63, hd = threadIdx.x >> 6;
+  const int64_t j = blockIdx.x;
+  const int64_t s0 = a.seg64[a.B + j], len = a.seg64[a.B + j + 1] - s0;
+  const int64_t q = a.T1 + a.last[j], qi = q - s0;
+  const float* qr = a.qkv + q * kQKV + kDh * hd;
+  const bool in = lane < len;
+  const int64_t kr = s0 + lane;
+  bool valid = in && lane <= qi && a.kpad[kr] == 0;
+  float sc = -INFINITY;
+  if (valid) {
+    const float* kk = a.qkv + kr * kQKV + kD + kDh * hd;
+    float d = 0.0f;
+#pragma unroll
+    for (int e = 0; e < kDh; e += 4) {
+      const float4 x = *reinterpret_cast<const float4*>(qr + e), y = *reinterpret_cast<const float4*>(kk + e);
+      d += x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
+    }
+    sc = d * 0.17677669529663687f;
+  }
+  float m = sc;
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  const float pe = valid ? expf(sc - m) : 0.0f;
+  float l = pe;
+  for (int o = 32; o > 0; o >>= 1) l += __shfl_xor(l, o, 64);
+  float* orow = a.out + j * kD + kDh * hd;
+  if (m == -INFINITY) {  // fully masked query: zero row
+    if (lane < kDh) orow[lane] = 0.0f;
+    if (lane == 0) a.lse[j * kHeads + hd] = -INFINITY;
+    return;
+  }
+  float pr = pe / l;
+  pr = a.drop.apply(pr, (uint64_t)(j * kHeads + hd) * 64 + lane);
+  const float* vr = a.qkv + kr * kQKV + 2 * kD + kDh * hd;
+  float acc = 0.0f;  // lane d < 32 ends with output dim d
+  for (int d = 0; d < kDh; ++d) {
+    float t = (in && pr != 0.0f) ? pr * vr[d] : 0.0f;
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+    if (lane == d) acc = t;
+  }
+  if (lane < kDh) orow[lane] = acc;
+  if (lane == 0) a.lse[j * kHeads + hd] = m + logf(l);
+}
+
+// Its backward, writing every dqkv row of view 2's user j for head hd (32-column slices of q, k
+// and v): dQ on the query row, dK / dV on the valid keys, zero elsewhere.
+__global__ __launch_bounds__(256) void tw_lastq_bwd_k(LastQ a) {
+  const int lane = threadIdx.x & 63, hd = threadIdx.x >> 6;
+  const int64_t j = blockIdx.x;
+  const int64_t s0 = a.seg64[a.B + j], len = a.seg64[a.B + j + 1] - s0;
+  const int64_t q = a.T1 + a.last[j], qi = q - s0;
+  const float* qr = a.qkv + q * kQKV + kDh * hd;
+  const bool in = lane < len;
+  const int64_t kr = s0 + lane;
+  const float lse = a.lse[j * kHeads + hd];
+  const bool valid = in && lane <= qi && a.kpad[kr] == 0 && lse != -INFINITY;
+  const float* kk = a.qkv + kr * kQKV + kD + kDh * hd;
+  const float* vr = a.qkv + kr * kQKV + 2 * kD + kDh * hd;
+  const float* dor = a.dout + j * kD + kDh * hd;
+  float p = 0.0f, dp = 0.0f;
+  if (valid) {
+    float d = 0.0f, dv = 0.0f;
+#pragma unroll
+    for (int e = 0; e < kDh; e += 4) {
+      const float4 x = *reinterpret_cast<const float4*>(qr + e), y = *reinterpret_cast<const float4*>(kk + e);
+      const float4 g = *reinterpret_cast<const float4*>(dor + e), w = *reinterpret_cast<const float4*>(vr + e);
+      d += x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
+      dv += g.x * w.x + g.y * w.y + g.z * w.z + g.w * w.w;
+    }
+    p = expf(d * 0.17677669529663687f - lse);
+    const uint64_t idx = (uint64_t)(j * kHeads + hd) * 64 + lane;
+    dp = a.drop.apply(dv, idx);       // d/dP of out = sum_k D_k P_k v_k
+  }
+  float sdp = p * dp;
+  for (int o = 32; o > 0; o >>= 1) sdp += __shfl_xor(sdp, o, 64);
+  const float ds = valid ? p * (dp - sdp) * 0.17677669529663687f : 0.0f;  // dL/dscore, scale folded in
+  // dQ = sum_k ds_k K_k (lane d < 32 ends with dim d)
+  float dq = 0.0f;
+  for (int d = 0; d < kDh; ++d) {
+    float t = valid ? ds * kk[d] : 0.0f;
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+    if (lane == d) dq = t;
+  }
+  const float dq_d = dq;  // lanes 0..31 hold dQ
+  if (in) {
+    float* drow = a.dqkv + kr * kQKV;
+    const float pd = valid ? a.drop.apply(p, (uint64_t)(j * kHeads + hd) * 64 + lane) : 0.0f;  // D_k P_k
+#pragma unroll
+    for (int e = 0; e < kDh; e += 4) {
+      const float4 x = *reinterpret_cast<const float4*>(qr + e), g = *reinterpret_cast<const float4*>(dor + e);
+      *reinterpret_cast<float4*>(drow + kD + kDh * hd + e) =
+          make_float4(ds * x.x, ds * x.y, ds * x.z, ds * x.w);                     // dK
+      *reinterpret_cast<float4*>(drow + 2 * kD + kDh * hd + e) =
+          make_float4(pd * g.x, pd * g.y, pd * g.z, pd * g.w);                     // dV
+    }
+    if (lane != qi) {
+#pragma unroll
+      for (int e = 0; e < kDh; e += 4)
+        *reinterpret_cast<float4*>(drow + kDh * hd + e) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  // the query row's dQ slice: lane d writes dim d
+  if (lane < kDh) a.dqkv[q * kQKV + kDh * hd + lane] = dq_d;
+}
 
 }  // namespace
 
@@ -200,18 +325,26 @@ RSX_API int rsx_tower_fwd(const void* const* p, const int64_t* dims, const float
     // in_proj + attention (ops.qkv_mha -> linear_tok + mha)
     TW_CALL(rsx_gemm_x3(h, kD, v.f(q + 2), kD, v.f(q + 3), T, (int)kQKV, (int)kD, kEpiBias, nullptr, 0, 0.0f, 0,
                         A + a.qkv, kQKV, stream));
-    TW_CALL(rsx_mha_fwd_x3(A + a.qkv, kp, seg, U, 64, kHeads, kDh, 1, pd, sd[0], A + a.a, A + a.lse, stream));
-    // the last layer past its attention runs on the tail rows only (the losses read no other row
-    // of view 2; every op from here on is per row)
+    // the last layer from its attention on runs on the tail rows only (the losses read no other
+    // row of view 2; every op past the attention is per row)
     const float* ain = A + a.a;
     const float* xin = x;
     int64_t rows = T;
     if (tail && i == nl - 1) {
-      TW_CALL(rsx_gather_rows(A + a.a, kD, tidx, R, kD, 0, 0.0f, A + s.aR, nullptr, stream));
+      // view 1: the whole causal attention of its B sequences, written straight into tail rows
+      // [0, T1); view 2: only each user's last query row (tw_lastq_fwd_k) into rows [T1, R)
+      TW_CALL(rsx_mha_fwd_x3(A + a.qkv, kp, seg, tB, 64, kHeads, kDh, 1, pd, sd[0], A + s.aR, A + a.lse, stream));
+      LastQ lq{};
+      lq.qkv = A + a.qkv; lq.kpad = kp; lq.seg64 = v.i64(RSX_TW_SEG64); lq.last = v.i64(n_ptrs(nl) - 1);
+      lq.out = A + s.aR + T1 * kD; lq.lse = A + s.lseq; lq.T1 = T1; lq.B = tB; lq.drop = rsx::make_dropout(pd, sd[0]);
+      hipLaunchKernelGGL(tw_lastq_fwd_k, dim3((unsigned)tB), dim3(256), 0, (hipStream_t)stream, lq);
+      RSX_LAUNCHED();
       TW_CALL(rsx_gather_rows(x, kD, tidx, R, kD, 0, 0.0f, A + s.xR, nullptr, stream));
       ain = A + s.aR;
       xin = A + s.xR;
       rows = R;
+    } else {
+      TW_CALL(rsx_mha_fwd_x3(A + a.qkv, kp, seg, U, 64, kHeads, kDh, 1, pd, sd[0], A + a.a, A + a.lse, stream));
     }
     // out_proj + residual + norm2 (ops.linear_add_layer_norm)
     TW_CALL(rsx_gemm_x3_addln(ain, kD, v.f(q + 4), kD, v.f(q + 5), rows, kD, kD, xin, kD, pd, sd[1], v.f(q + 6),
@@ -334,30 +467,39 @@ RSX_API int rsx_tower_bwd(const void* const* p, const int64_t* dims, const float
     // _LinearAddLayerNorm: (ds = d(xs), dy = d(hs)) -> d(x_in), d(out_proj output); then d(a), dWo, dbo
     float* dRes = W + b.dRes;
     float* dA = W + b.dA;
+    float* dQKV = W + b.dQKV;
     if (tl) {
-      // tail rows: d(x_in) and d(a) land in R-row buffers with a zero row R, then expand to every
-      // packed row through the inverse map (dropped rows read the zero row)
+      // tail rows: d(x_in) lands in an R-row buffer with a zero row R and expands to every packed
+      // row through the inverse map (dropped rows read the zero row); d(a) of view 1 feeds its
+      // attention backward, view 2's last rows the last-query backward, which writes view 2's
+      // whole dqkv rows
       float* dXR = W + b.dXR;
       float* dAR = W + b.dAR;
       (void)hipMemsetAsync(dXR + R * kD, 0, kD * sizeof(float), (hipStream_t)stream);
-      (void)hipMemsetAsync(dAR + R * kD, 0, kD * sizeof(float), (hipStream_t)stream);
       TW_CALL(rsx_ln_bwd(A + a.xs, A + a.m2, A + a.r2, v.f(q + 6), v.f(q + 7), 0, dHs, dXs, pd, sd[1], R, kD, dXR, dRes,
                          G(q + 6), G(q + 7), wsl, b.n_wsl, stream));
       TW_CALL(tn(dRes, kD, v.f(q + 4), kD, R, kD, kD, dAR, kD));
       TW_CALL(wgrad(dRes, kD, A + s.aR, kD, R, kD, kD, G(q + 4), kD, G(q + 5)));
       const int64_t* tinv = reinterpret_cast<const int64_t*>(A + s.tinv);
       TW_CALL(rsx_gather_rows(dXR, kD, tinv, T, kD, 0, 0.0f, dX, nullptr, stream));
-      TW_CALL(rsx_gather_rows(dAR, kD, tinv, T, kD, 0, 0.0f, dA, nullptr, stream));
+      TW_CALL(rsx_mha_bwd_x3(A + a.qkv, kp, seg, A + s.aR, A + a.lse, dAR, tB, 64, kHeads, kDh, 1, pd, sd[0], dQKV,
+                             stream));
+      LastQ lq{};
+      lq.qkv = A + a.qkv; lq.kpad = kp; lq.seg64 = v.i64(RSX_TW_SEG64); lq.last = v.i64(n_ptrs(nl) - 1);
+      lq.lse = const_cast<float*>(A + s.lseq); lq.dout = dAR + T1 * kD; lq.dqkv = dQKV; lq.T1 = T1; lq.B = tB;
+      lq.drop = rsx::make_dropout(pd, sd[0]);
+      hipLaunchKernelGGL(tw_lastq_bwd_k, dim3((unsigned)tB), dim3(256), 0, (hipStream_t)stream, lq);
+      RSX_LAUNCHED();
     } else {
       TW_CALL(rsx_ln_bwd(A + a.xs, A + a.m2, A + a.r2, v.f(q + 6), v.f(q + 7), 0, dHs, dXs, pd, sd[1], T, kD, dX, dRes,
                          G(q + 6), G(q + 7), wsl, b.n_wsl, stream));
       TW_CALL(tn(dRes, kD, v.f(q + 4), kD, T, kD, kD, dA, kD));
       TW_CALL(wgrad(dRes, kD, A + a.a, kD, T, kD, kD, G(q + 4), kD, G(q + 5)));
+      // _MHA
+      TW_CALL(rsx_mha_bwd_x3(A + a.qkv, kp, seg, A + a.a, A + a.lse, dA, U, 64, kHeads, kDh, 1, pd, sd[0], dQKV,
+                             stream));
     }
-    // _MHA, then in_proj (_TokLinear)
-    float* dQKV = W + b.dQKV;
-    TW_CALL(rsx_mha_bwd_x3(A + a.qkv, kp, seg, A + a.a, A + a.lse, dA, U, 64, kHeads, kDh, 1, pd, sd[0], dQKV,
-                           stream));
+    // in_proj (_TokLinear)
     const float* h_in = (i == 0) ? A + s.h0 : A + s.l[i - 1].hn;
     TW_CALL(tn(dQKV, kQKV, v.f(q + 2), kD, T, (int)kD, (int)kQKV, dH, kD));
     TW_CALL(wgrad(dQKV, kQKV, h_in, kD, T, kQKV, kD, G(q + 2), kD, G(q + 3)));

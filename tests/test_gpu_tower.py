@@ -283,11 +283,12 @@ def test_native_tower_program_equals_per_op_path(gpu, p_drop):
 
 
 def test_native_tower_tail_rows(gpu):
-    """The tail form (forward_packed tail_last: the last layer past attention and the head on the
-    rows the losses read: all of view 1 and view 2's "last" row per user) against the per-op path
-    computing every row and keeping those (dropout 0): the kept rows are per-row identical, so
-    the output is bit-identical; the gradients differ only in which zero rows the weight-gradient
-    sums skip (2e-6 of each gradient's scale)."""
+    """The tail form (forward_packed tail_last: the last layer from its attention on and the head
+    on the rows the losses read: all of view 1 and view 2's "last" row per user) against the
+    per-op path computing every row and keeping those (dropout 0). View 1's rows are per-row
+    identical; view 2's last rows come from the fp32 single-query attention (tw_lastq_fwd_k)
+    instead of the bf16x3 sequence kernel: outputs within 2e-5, gradients within 2e-5 of each
+    gradient's scale (the weight-gradient sums also skip the zero rows)."""
     cfg = small_cfg(num_items=500, dropout=0.0)
     items = small_universe(500)
     batch = to_dev(synth.make_batch(items, 96, seed=23), gpu)
@@ -313,8 +314,10 @@ def test_native_tower_tail_rows(gpu):
         res.append((out.detach(), {n: p.grad.detach().clone() for n, p in model.named_parameters()
                                    if p.grad is not None}))
     (o1, g1), (o2, g2) = res
-    assert torch.equal(o1, o2)
+    T1 = pk.flat.numel()
+    assert torch.equal(o1[:T1], o2[:T1])           # view 1: the same kernels row for row
+    torch.testing.assert_close(o1, o2, atol=2e-5, rtol=1e-4)
     assert g1.keys() == g2.keys()
     for n in g1:
         scale = float(g2[n].abs().max()) + 1e-30
-        assert (g1[n] - g2[n]).abs().max().item() <= 2e-6 * scale, n
+        assert (g1[n] - g2[n]).abs().max().item() <= 2e-5 * scale, n
