@@ -812,7 +812,8 @@ def train_bench(args, global_batch, steps, warmup, items, cfg, model, item_tower
     trace_path = os.environ.get("RSX_HOST_TRACE")  # torch.profiler CPU table of the same steps (tools only)
     tprof = None
     if trace_path:
-        tprof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU])
+        tprof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU],
+                                       with_stack=bool(os.environ.get("RSX_HOST_TRACE_STACK")))
         tprof.__enter__()
     for j in range(12 if (prof or tprof) else 3):
         torch.cuda.synchronize()
@@ -832,6 +833,11 @@ def train_bench(args, global_batch, steps, warmup, items, cfg, model, item_tower
         tprof.__exit__(None, None, None)
         with open(trace_path, "w") as f:
             f.write(tprof.key_averages().table(sort_by="cpu_time_total", row_limit=120, max_name_column_width=90))
+            if os.environ.get("RSX_HOST_TRACE_STACK"):  # where the host copies come from
+                for ev in tprof.key_averages(group_by_stack_n=12):
+                    if ev.key in ("aten::_to_copy", "aten::copy_", "aten::item", "aten::_local_scalar_dense"):
+                        f.write(f"\n{ev.key} calls {ev.count} cpu_total_us {ev.cpu_time_total:.1f}\n  " +
+                                "\n  ".join(ev.stack or []) + "\n")
     unloaded = unloaded[1:]
     host_unloaded = {"index_inline_ms": round(1e3 * sum(u[0] for u in unloaded) / len(unloaded), 3),
                      "step_enqueue_ms": round(1e3 * sum(u[1] for u in unloaded) / len(unloaded), 3)}
