@@ -384,7 +384,7 @@ def bench_deepfm(args, device):
            "data": "synthetic Zipf(1.1) ids, deepctr-style N(0,1e-4) init"}
     if f_n:
         fs = f_ms / 1e3 / f_n
-        out["fused"] = {"kernel": "deepfm_rows5_k (F = 39; deepfm_persist_k for other F in [25, 48], deepfm_fused_k otherwise) on cached packed tables and weight images", "avg_ms": round(fs * 1e3, 4),
+        out["fused"] = {"kernel": "deepfm_rows2m_k<39, 1> (F = 39: eight 32-row waves per 256-row workgroup; deepfm_rows5_k on unpacked tables, deepfm_persist_k for other F in [25, 48], deepfm_fused_k otherwise) on cached packed tables and weight images", "avg_ms": round(fs * 1e3, 4),
                         "bytes_per_row": bytes_row,
                         "gather_achieved_GBs": round(bytes_row * R / fs / 1e9, 1), "hbm_peak_GBs": HBM_PEAK_GBS,
                         "gather_frac": round(bytes_row * R / fs / 1e9 / HBM_PEAK_GBS, 4),

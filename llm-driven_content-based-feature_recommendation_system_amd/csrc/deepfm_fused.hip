@@ -1181,6 +1181,414 @@ __global__ __launch_bounds__(320, 1) void deepfm_rows5_k(RArgs a) {
   }
 }
 
+template <int I, int N, typename Fn>
+__device__ __forceinline__ void static_for_(Fn&& fn) {
+  if constexpr (I < N) {
+    fn(std::integral_constant<int, I>{});
+    static_for_<I + 1, N>(fn);
+  }
+}
+
+// s_waitcnt vmcnt(n) for a count known after unrolling (the switch folds to one instruction)
+#define RSX_VMW(N) \
+  case N:          \
+    asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); \
+    break;
+__device__ __forceinline__ void vm_wait_n(int n) {
+  switch (n) {
+    RSX_VMW(0) RSX_VMW(1) RSX_VMW(2) RSX_VMW(3) RSX_VMW(4) RSX_VMW(5) RSX_VMW(6) RSX_VMW(7)
+    RSX_VMW(8) RSX_VMW(9) RSX_VMW(10) RSX_VMW(11) RSX_VMW(12) RSX_VMW(13) RSX_VMW(14) RSX_VMW(15)
+    RSX_VMW(16) RSX_VMW(17) RSX_VMW(18) RSX_VMW(19) RSX_VMW(20) RSX_VMW(21) RSX_VMW(22) RSX_VMW(23)
+    RSX_VMW(24) RSX_VMW(25) RSX_VMW(26) RSX_VMW(27) RSX_VMW(28) RSX_VMW(29) RSX_VMW(30) RSX_VMW(31)
+    RSX_VMW(32) RSX_VMW(33) RSX_VMW(34) RSX_VMW(35) RSX_VMW(36) RSX_VMW(37) RSX_VMW(38) RSX_VMW(39)
+    RSX_VMW(40) RSX_VMW(41) RSX_VMW(42) RSX_VMW(43) RSX_VMW(44) RSX_VMW(45) RSX_VMW(46) RSX_VMW(47)
+    RSX_VMW(48) RSX_VMW(49) RSX_VMW(50) RSX_VMW(51) RSX_VMW(52) RSX_VMW(53) RSX_VMW(54) RSX_VMW(55)
+    RSX_VMW(56) RSX_VMW(57) RSX_VMW(58) RSX_VMW(59) RSX_VMW(60) RSX_VMW(61) RSX_VMW(62) RSX_VMW(63)
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;  // > 63: the counter's limit
+  }
+}
+#undef RSX_VMW
+
+// deepfm_rows5_k reorganised around 256-row workgroups (65,536 rows: one round of the grid
+// instead of two) with the layer-1 accumulators in the AGPR file, in two shapes:
+//   MT = 2: four waves of 64 rows (two 32-row m-tiles sharing every W1 fragment read, half the LDS
+//           read traffic per MFMA; 256 accumulator floats, one wave per SIMD);
+//   MT = 1: eight waves of 32 rows (128 accumulator floats, two waves per SIMD).
+// There is no stager wave (no room beside AGPR-holding compute waves): each wave stages its share
+// of a field's W1 image by LDS-DMA (inline asm: hipcc would drain vmcnt in front of every LDS read
+// if it saw a pending DMA) and waits for it with a counted vmcnt. Field f's work is software-
+// pipelined around barrier B_{f+1}, which sits after its first two n-tile pairs: behind B_{f+1}
+// (slot (f+1) % 4 complete everywhere) the wave issues the DMA of field f + 3 into slot (f + 3) % 4
+// (field f - 1's, finished before B_{f+1}), splits field f + 1's gathered rows and reads its first
+// W1 fragments under field f's last two pairs of MFMAs. Layer 2 reads W2 from LDS: the 128-KiB
+// image (1-KiB pieces, piece p at byte 1024 p of the union) is staged as space frees up -- pieces
+// 104..127 (unused by layer 1) in the prologue, each wave's id region after its last gather, the
+// slots of fields F-4 / F-3 after B_{F-1}, the last two slots after layer 1 -- and each step's B
+// fragments are built under the previous step's MFMAs.
+template <int F>
+__host__ __device__ constexpr int rows2m_after_dma(int g, int R, int iss, int idp, int dp) {
+  // loads a wave issues between its DMA of field g and its wait for it (before B_g): gathers,
+  // the next field's DMA and the W2 pieces staged into the wave's id region at field F - 1 - R
+  // (idp of them). An exact count: a smaller one would also wait for younger loads.
+  const int fi = F - 1 - R;
+  return g == 0 ? dp + iss * R
+       : g == 1 ? iss * R + dp + (R < F ? iss : 0) + (fi == 0 ? idp : 0)
+                : (g - 2 + R < F ? iss : 0) + (g + 1 < F ? dp : 0) + (g - 1 + R < F ? iss : 0) +
+                      ((fi == g - 2 || fi == g - 1) ? idp : 0);
+}
+
+constexpr int kRows2mLds = 2 * 16 * kN2 * 16 * 2;  // bytes: the W2 hi + lo images (128 KiB)
+
+#ifndef RSX_DFM_R
+#define RSX_DFM_R 3
+#endif
+#ifndef RSX_DFM_L2PIPE
+#define RSX_DFM_L2PIPE 1  // layer 2: the next step's B fragments built under this step's MFMAs
+#endif
+#ifndef RSX_DFM_ABL
+#define RSX_DFM_ABL 0  // timing probes (wrong results): 1 no field barriers, 2 no W1 DMA in the loop
+#endif
+
+template <int F, int MT, bool L2 = true>
+__global__ __launch_bounds__(512 / MT, 1) void deepfm_rows2m_k(RArgs a) {
+  constexpr int NW = 8 / MT;        // waves per workgroup (256 rows)
+  constexpr int R = RSX_DFM_R, NB = R + 1;  // gather ring: fields in flight ahead of the one computed
+  constexpr int kIss = 3 * MT;      // global loads per issue() (m-tiles x three 16-B pieces)
+  constexpr int kDp = 16 / NW;      // 1-KiB W1 pieces a wave stages per field
+  constexpr int kSlots = 4;         // W1 ring
+  constexpr int kIdBlk = 5 * MT;    // 1-KiB blocks per wave's id region (32 MT F ints)
+  constexpr int kIdp = kIdBlk;      // W2 pieces a wave stages into its id region
+  static_assert(32 * MT * F * 4 <= kIdBlk * 1024 && 64 + NW * kIdBlk <= 104, "id regions must fit blocks 64..103");
+  static_assert(F - 1 - R >= 2, "the staging schedule assumes F >= R + 3");
+  // union (1-KiB blocks): layer 1 = W1 ring blocks 0..63 + ids blocks 64..103 (104..127 free);
+  // layer 2 = W2 hi | lo, piece p in block p
+  __shared__ __attribute__((aligned(16))) unsigned char lds[kRows2mLds];
+  __shared__ __attribute__((aligned(16))) float b1s[kN1], b2s[kN2], wos[kN2];
+  __bf16* w1s = reinterpret_cast<__bf16*>(lds);
+  int* ids_all = reinterpret_cast<int*>(lds + kSlots * kW1Field * 2);
+  // MT = 2: an AGPR operand anywhere in the kernel keeps hipcc from inferring "no AGPRs", which
+  // selects the VGPR form of every MFMA (the 256 accumulators would then spill). MT = 1: the VGPR
+  // form, 256 architectural registers per wave at two waves per SIMD (with AGPR-form MFMAs the
+  // layer-2 accumulators would not fit beside the layer-1 ones in a 128 / 128 split)
+  if (MT == 2) asm volatile("" ::"a"(0.0f));
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c = lane & 31, h = lane >> 5;
+  if (tid < kN1) b1s[tid] = a.b1[tid];
+  if (tid < kN2) b2s[tid] = a.b2[tid];
+  else if (tid < kN1) wos[tid - kN2] = a.wo[tid - kN2];
+  int* my_ids = ids_all + wave * (kIdBlk * 256);
+  const int64_t m0 = ((int64_t)blockIdx.x * NW + wave) * (32 * MT);  // this wave's 32 MT rows
+  const char* w1g = reinterpret_cast<const char*>(a.w1);
+  // LDS-DMA from inline asm (M0 = the LDS base; M0 has no other user in this kernel; one wait state
+  // between the M0 write and the DMA that reads it)
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const unsigned lds_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)lds;
+  auto dma1k = [&](const char* src_block, unsigned dst_block) {
+    const char* src = src_block + 16 * lane;
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(dst_block) : "memory");
+  };
+  auto dma = [&](int f) {  // pieces kDp wave .. kDp wave + kDp - 1 (1 KiB each) of field f's image
+#pragma unroll
+    for (int k = 0; k < kDp; ++k) {
+      const int piece = kDp * wave_u + k;
+      dma1k(w1g + (int64_t)f * (kW1Field * 2) + 1024 * piece, lds_base + (f % kSlots) * (kW1Field * 2) + 1024 * piece);
+    }
+  };
+
+  const char* w2g = reinterpret_cast<const char*>(a.w2hi);  // w2lo follows w2hi (deepfm_prep_images)
+  auto w2dma = [&](int piece) { dma1k(w2g + 1024 * piece, lds_base + 1024 * piece); };
+  if (L2) {
+#pragma unroll
+    for (int k = 0; k < 24 / NW; ++k) w2dma(104 + (24 / NW) * wave_u + k);  // blocks no layer-1 data uses
+  }
+  // ---- ids of the 32 MT rows -> LDS (int32); rows past R re-read the last row, never stored
+  {
+    const int64_t last = a.R - 1;
+    constexpr int NE = 32 * MT * F, NT = (NE + 63) / 64;
+#pragma unroll
+    for (int t0 = 0; t0 < NT; t0 += 13) {
+      int64_t v[13];
+#pragma unroll
+      for (int t = 0; t < 13; ++t) {
+        const int e = lane + 64 * (t0 + t);
+        const int row = e / F, f = e - row * F;
+        const int64_t gr = m0 + row <= last ? m0 + row : last;
+        v[t] = (t0 + t < NT && e < NE) ? a.x[gr * F + f] : 0;
+      }
+#pragma unroll
+      for (int t = 0; t < 13; ++t)
+        if (t0 + t < NT && lane + 64 * (t0 + t) < NE) my_ids[lane + 64 * (t0 + t)] = (int)v[t];
+    }
+  }
+  float4 xa[MT][NB], xb[MT][NB], xw[MT][NB];
+  f32x16 acc[MT][8];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[m][j][r] = 0.0f;
+  float fs[MT][8], fq[MT], fw[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    fq[m] = 0.0f;
+    fw[m] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) fs[m][k] = 0.0f;
+  }
+  auto issue = [&](int f, int sl) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int id = my_ids[(32 * m + c) * F + f];
+      const float4* line = reinterpret_cast<const float4*>(a.P[f] + (int64_t)id * 32);
+      xa[m][sl] = line[h];
+      xb[m][sl] = line[2 + h];
+      xw[m][sl] = line[4 + h];
+    }
+  };
+  // field f's gathered rows (ring slot sl) -> split fragments (set st) + the FM sums
+  bf16x8 bh[2][MT], bl[2][MT];  // [set][m-tile]
+  auto split = [&](int sl, int st) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+      asm volatile("" : "+v"(xa[m][sl].x), "+v"(xa[m][sl].y), "+v"(xa[m][sl].z), "+v"(xa[m][sl].w), "+v"(xb[m][sl].x),
+                   "+v"(xb[m][sl].y), "+v"(xb[m][sl].z), "+v"(xb[m][sl].w), "+v"(xw[m][sl].x), "+v"(xw[m][sl].y),
+                   "+v"(xw[m][sl].z), "+v"(xw[m][sl].w));
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const float4 p = xa[m][sl], q = xb[m][sl], w = xw[m][sl];
+      const float v[8] = {p.x, p.y, p.z, p.w, q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        fs[m][k] += v[k];
+        fq[m] += v[k] * v[k];
+        const __bf16 hv = (__bf16)v[k];
+        bh[st][m][k] = hv;
+        bl[st][m][k] = (__bf16)(v[k] - (float)hv);
+      }
+      fw[m] += (w.x + w.y) + (w.z + w.w);  // W then zeros (deepfm_pack_k): see deepfm_rows5_k
+      // the FM sums are formed here, field by field: left alone, hipcc sinks the 39-term chains to
+      // their use after the field loop and keeps every gathered piece alive until then (spills)
+      asm volatile("" : "+v"(fs[m][0]), "+v"(fs[m][1]), "+v"(fs[m][2]), "+v"(fs[m][3]), "+v"(fs[m][4]),
+                   "+v"(fs[m][5]), "+v"(fs[m][6]), "+v"(fs[m][7]), "+v"(fq[m]), "+v"(fw[m]));
+    }
+  };
+  bf16x8 ah[2][2], al[2][2];  // W1 fragments [buffer][n-tile of the pair]
+  auto wread = [&](int f, int jp, int b) {
+    const __bf16* ws = w1s + (f % kSlots) * kW1Field;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int n = 32 * (2 * jp + q) + c;
+      ah[b][q] = *reinterpret_cast<const bf16x8*>(ws + w1_idx(n, 8 * h));
+      al[b][q] = *reinterpret_cast<const bf16x8*>(ws + 4096 + w1_idx(n, 8 * h));
+    }
+  };
+  auto pair_mfma = [&](int jp, int b, int st) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int j = 2 * jp + q;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        acc[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[b][q], bh[st][m], acc[m][j], 0, 0, 0);
+        acc[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[b][q], bl[st][m], acc[m][j], 0, 0, 0);
+        acc[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[b][q], bh[st][m], acc[m][j], 0, 0, 0);
+      }
+    }
+  };
+  dma(0);
+  dma(1);
+#pragma unroll
+  for (int f = 0; f < R; ++f) issue(f, f);
+  __builtin_amdgcn_sched_barrier(0);
+  vm_wait_n(rows2m_after_dma<F>(0, R, kIss, L2 ? kIdp : 0, kDp));  // this wave's quarter of field 0 landed
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ids, b1 / b2 / w_o stores
+  __builtin_amdgcn_s_barrier();  // B_0
+  __builtin_amdgcn_sched_barrier(0);
+  dma(2);
+  split(0, 0);
+  wread(0, 0, 0);
+  __builtin_amdgcn_sched_barrier(0);
+  static_for_<0, F>([&](auto fc) __attribute__((always_inline)) {
+    constexpr int f = decltype(fc)::value;
+    constexpr int cs = f & 1;
+    if (f + R < F) issue(f + R, (f + R) % NB);
+    if (L2 && f == F - 1 - R) {  // last gather issued: this wave's id region takes W2 pieces
+#pragma unroll
+      for (int k = 0; k < kIdp; ++k) w2dma(64 + kIdBlk * wave_u + k);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // pairs 0 and 1 of field f (the next pair's fragments read under each pair's MFMAs)
+    wread(f, 1, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    pair_mfma(0, 0, cs);
+    __builtin_amdgcn_sched_barrier(0);
+    wread(f, 2, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    pair_mfma(1, 1, cs);
+    __builtin_amdgcn_sched_barrier(0);
+    if (f + 1 < F) {
+      if (!(RSX_DFM_ABL & 1)) {
+        vm_wait_n(rows2m_after_dma<F>(f + 1, R, kIss, L2 ? kIdp : 0, kDp));  // this wave's quarter of field f + 1
+        __builtin_amdgcn_s_barrier();                                    // B_{f+1}
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (f + 3 < F && !(RSX_DFM_ABL & 2)) dma(f + 3);
+      if (L2 && f + 1 == F - 1) {  // slots of fields F-4 and F-3 are free: W2 pieces into them
+        constexpr int s0 = (F - 4) % kSlots, s1 = (F - 3) % kSlots;
+#pragma unroll
+        for (int k = 0; k < kDp; ++k) {
+          w2dma(16 * s0 + kDp * wave_u + k);
+          w2dma(16 * s1 + kDp * wave_u + k);
+        }
+      }
+    }
+    // pair 2 with field f + 1's split in its MFMA issue gaps, then pair 3 with field f + 1's
+    // first fragments read under it
+    wread(f, 3, 1);
+    if (f + 1 < F) split((f + 1) % NB, cs ^ 1);
+    pair_mfma(2, 0, cs);
+    if (f + 1 < F) {
+#pragma unroll
+      for (int i = 0; i < 6 * MT; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);  // six VALU
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (f + 1 < F) wread(f + 1, 0, 0);
+    pair_mfma(3, 1, cs);
+    __builtin_amdgcn_sched_barrier(0);
+  });
+  // ---- W2 (hi | lo, 128 KiB) into the layer-1 space: every wave is past its last W1 / id read
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  if (L2) {  // the last two slots (fields F-2, F-1)
+    constexpr int s0 = (F - 2) % kSlots, s1 = (F - 1) % kSlots;
+#pragma unroll
+    for (int k = 0; k < kDp; ++k) {
+      w2dma(16 * s0 + kDp * wave_u + k);
+      w2dma(16 * s1 + kDp * wave_u + k);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // ---- layer 2 (deepfm_rows5_k's flat 32-step sequence, each W2 fragment used by both m-tiles)
+  float dot[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) dot[m] = 0.0f;
+  constexpr int NS = 32;
+  bf16x8 w2h[2][2], w2l[2][2];
+  auto w2read = [&](int st) {
+    const int half = st >> 4, t = st & 15, b = st & 1;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {  // piece 4 t + 2 half + q of each image; 16 B at lane (c, h)
+      const int p = 4 * t + 2 * half + q, o = (2 * c + h) * 16;
+      w2h[b][q] = *reinterpret_cast<const bf16x8*>(lds + 1024 * p + o);
+      w2l[b][q] = *reinterpret_cast<const bf16x8*>(lds + 1024 * (64 + p) + o);
+    }
+  };
+  f32x16 acc2[MT][2];
+  if (!L2) {  // timing ablation (wrong results): layer 1 only (one element per tile kept live)
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dot[m] += acc[m][j][0] * 1e-30f;
+  }
+  // B fragments of step st (relu(H1 + b1) of k-step t = st & 15, split), both m-tiles
+  bf16x8 gh[2][MT], gl[2][MT];  // [set][m-tile]
+  auto build = [&](int st, int set) {
+    const int t = st & 15, j = t >> 1, g2 = t & 1;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const float4 bb = *reinterpret_cast<const float4*>(b1s + 16 * t + 8 * p + 4 * h);
+        const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = acc[m][j][4 * (2 * g2 + p) + e] + bv[e];
+          v = v > 0.0f ? v : 0.0f;
+          const __bf16 hv = (__bf16)v;
+          gh[set][m][4 * p + e] = hv;
+          gl[set][m][4 * p + e] = (__bf16)(v - (float)hv);
+        }
+      }
+    }
+  };
+  if (L2) {
+    w2read(0);
+    if (RSX_DFM_L2PIPE) build(0, 0);
+  }
+  auto step = [&](int st) __attribute__((always_inline)) {
+    const int half = st >> 4, t = st & 15, b = st & 1;
+    if (t == 0) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc2[m][q][r] = 0.0f;
+    }
+    if (st + 1 < NS) w2read(st + 1);
+    if (!RSX_DFM_L2PIPE) build(st, b);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const bf16x8 wh = w2h[b][q], wl = w2l[b][q];
+        acc2[m][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, gh[b][m], acc2[m][q], 0, 0, 0);
+        acc2[m][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, gl[b][m], acc2[m][q], 0, 0, 0);
+        acc2[m][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, gh[b][m], acc2[m][q], 0, 0, 0);
+      }
+    }
+    if (RSX_DFM_L2PIPE && st + 1 < NS) {  // the next step's fragments in this step's MFMA issue gaps
+      build(st + 1, b ^ 1);
+#pragma unroll
+      for (int i = 0; i < 6 * MT; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (t == 15) {  // relu(H2 + b2) . wo over this half's 64 outputs
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int nb = 32 * (2 * half + q) + 8 * g + 4 * h;
+            const float4 bb = *reinterpret_cast<const float4*>(b2s + nb);
+            const float4 ww = *reinterpret_cast<const float4*>(wos + nb);
+            dot[m] += fmaxf(acc2[m][q][4 * g + 0] + bb.x, 0.0f) * ww.x;
+            dot[m] += fmaxf(acc2[m][q][4 * g + 1] + bb.y, 0.0f) * ww.y;
+            dot[m] += fmaxf(acc2[m][q][4 * g + 2] + bb.z, 0.0f) * ww.z;
+            dot[m] += fmaxf(acc2[m][q][4 * g + 3] + bb.w, 0.0f) * ww.w;
+          }
+    }
+  };
+#pragma unroll
+  for (int st = 0; st < (L2 ? NS : 0); ++st) step(st);
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    float fm = -fq[m];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) fm += fs[m][k] * fs[m][k];
+    const float d = dot[m] + __shfl_xor(dot[m], 32, 64);
+    fm += __shfl_xor(fm, 32, 64);
+    const float first = fw[m] + __shfl_xor(fw[m], 32, 64);
+    const int64_t row = m0 + 32 * m + c;
+    if (h == 0 && row < a.R) {
+      const float v = a.bias + first + 0.5f * fm + d;
+      a.logit[row] = v;
+      if (a.prob) a.prob[row] = 1.0f / (1.0f + expf(-v));
+    }
+  }
+}
+
 // W1 [256][F*16] -> [F][8192]: hi at w1_idx(n, s), lo at 4096 + w1_idx(n, s), s = k-slot with
 // V index kperm(s) = (s & 3) + 8 * ((s >> 2) & 1) + 4 * (s >> 3)
 __global__ __launch_bounds__(256) void deepfm_prep3_k(const float* w1, int F, __bf16* out) {
@@ -1296,16 +1704,29 @@ RSX_API int rsx_deepfm_fused_run(const int64_t* x, int64_t R, int F, const float
     r.w2hi = wsb + m1;
     r.w2lo = wsb + m1 + n2;
     r.b1 = b1; r.b2 = b2; r.wo = wo; r.logit = logit; r.prob = prob;
-    static const bool v4 = [] {
+    // RSX_DEEPFM_ROWS (A/B): unset = deepfm_rows2m_k<F, 1> (eight 32-row waves), 2 = <F, 2> (four
+    // 64-row waves), 5 = deepfm_rows5_k, 4 = deepfm_rows_k with RSX_DEEPFM_ABL ablations;
+    // RSX_DEEPFM_ABL with rows2m: layer 1 only (timing, wrong results)
+    static const char mode = [] {
       const char* e = getenv("RSX_DEEPFM_ROWS");
-      return e && e[0] == '4';
+      return e && (e[0] == '2' || e[0] == '4' || e[0] == '5') ? e[0] : 'w';
     }();
     if (!packed) {
       hipLaunchKernelGGL((deepfm_rows5_k<kRowsF, false>), dim3((unsigned)grid), dim3(320), 0, st, r);
       RSX_LAUNCHED();
       return 0;
     }
-    if (!v4) {
+    if (mode == 'w' || mode == '2') {
+      const bool l1 = getenv("RSX_DEEPFM_ABL") != nullptr;
+      const dim3 g((unsigned)((R + 255) / 256));  // 256 rows per workgroup
+      if (mode == 'w' && l1) hipLaunchKernelGGL((deepfm_rows2m_k<kRowsF, 1, false>), g, dim3(512), 0, st, r);
+      else if (mode == 'w') hipLaunchKernelGGL((deepfm_rows2m_k<kRowsF, 1>), g, dim3(512), 0, st, r);
+      else if (l1) hipLaunchKernelGGL((deepfm_rows2m_k<kRowsF, 2, false>), g, dim3(256), 0, st, r);
+      else hipLaunchKernelGGL((deepfm_rows2m_k<kRowsF, 2>), g, dim3(256), 0, st, r);
+      RSX_LAUNCHED();
+      return 0;
+    }
+    if (mode == '5') {
       hipLaunchKernelGGL((deepfm_rows5_k<kRowsF, true>), dim3((unsigned)grid), dim3(320), 0, st, r);
       RSX_LAUNCHED();
       return 0;
