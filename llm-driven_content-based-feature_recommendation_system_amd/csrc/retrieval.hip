@@ -420,9 +420,13 @@ __global__ __launch_bounds__(256) void topk_final_k(const float* bs, const int* 
 
 // ---- bf16 path (large corpora): one full scan at bf16 MFMA rate, exact fp32 rescoring ----------
 // P0 (topk_bf16_prep_k): the corpus as a bf16 image (RNE) and max_j ||w_j||.
-// Rounding bound: |a - e| <= delta_q = ||u|| max||w|| (2^-7 + 2^-12) between the bf16 score a
-//     (bf16 RNE operands: 2^-7 + 2^-16 relative per product, fp32 accumulation) and the fp32
-//     score e of the rescoring (fp32 accumulation; both accumulations < 2^-16 relative).
+// Rounding bound (query_delta): |a - e| <= delta_q between the bf16 score a (bf16 RNE operands,
+//     fp32 accumulation) and the fp32 score e of the rescoring: with u = u' + du, w = w' + dw (u',
+//     w' the bf16 operands), u.w - u'.w' = u'.dw + du.w' + du.dw, so by Cauchy-Schwarz
+//     delta_q = ||u|| D + ||du|| W + 3 ||du|| D + 2^-12 ||u|| W, D = max_j ||dw_j||, W = max_j ||w_j||
+//     (the last term covers both fp32 accumulations, each < 2^-16 relative). Round 4 used the
+//     elementwise worst case (2^-7 + 2^-12) ||u|| W; the residual norms are ~0.58 of it on spread
+//     data, so the band of scores above t_q (the appends of P3) and the margin set of P4 narrow.
 // P1 (topk_bf16_scan_k<MODE 0>): a strided sample of the corpus (every S-th 32-item tile of each
 //     split, S ~ 8 nsplit / k so that ~4 collected entries per stream are expected in P3) over
 //     ns0 <= nsplit splits (sample_nsplit); each lane keeps its best T0 sample scores in registers
@@ -442,15 +446,15 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kImgStride = 272;   // bytes per staged item row: 256 + 16 (conflict-free ds_read_b128)
 constexpr int kStreamCap = 32;    // P3 entries per lane stream
 constexpr int kSelMax = 8192;     // P4 entries per query (LDS sort)
-constexpr float kDeltaRel = 0.0078125f + 0.000244140625f;  // 2^-7 + 2^-12
 
-// 16 threads per row, 8 floats each; 4 rows per wave per step
+// 16 threads per row, 8 floats each; 4 rows per wave per step. hdr[0] = max_j ||w_j||, hdr[1] =
+// max_j ||w_j - bf16(w_j)|| (float bits; both inflated against their own fp32 rounding)
 __global__ __launch_bounds__(256) void topk_bf16_prep_k(const float* __restrict__ I, int64_t ldi, int64_t NI,
-                                                        __bf16* __restrict__ img, unsigned* wmax_bits) {
+                                                        __bf16* __restrict__ img, unsigned* hdr) {
   const int lane = threadIdx.x & 63, sub = lane >> 4, c = lane & 15;
   const int64_t wave_g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t nw = (int64_t)gridDim.x * 4;
-  float mx = 0.0f;
+  float mx = 0.0f, md = 0.0f;
   for (int64_t j0 = wave_g * 8; j0 < NI; j0 += nw * 8) {
     float4 v[2][2];
 #pragma unroll
@@ -475,12 +479,24 @@ __global__ __launch_bounds__(256) void topk_bf16_prep_k(const float* __restrict_
       bf16x8 h;
       h[0] = (__bf16)a.x; h[1] = (__bf16)a.y; h[2] = (__bf16)a.z; h[3] = (__bf16)a.w;
       h[4] = (__bf16)b.x; h[5] = (__bf16)b.y; h[6] = (__bf16)b.z; h[7] = (__bf16)b.w;
+      const float f[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      float dd = 0.0f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float r = f[e] - (float)h[e];  // exact (Sterbenz)
+        dd = fmaf(r, r, dd);
+      }
+      md = fmaxf(md, sqrtf(rsx::wave_sum_width(dd, 16)));
       if (j < NI) *reinterpret_cast<bf16x8*>(img + j * kD + 8 * c) = h;
     }
   }
-  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  for (int o = 32; o > 0; o >>= 1) {
+    mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    md = fmaxf(md, __shfl_xor(md, o, 64));
+  }
   // non-negative floats order like their bit patterns
-  if (lane == 0 && mx > 0.0f) atomicMax(wmax_bits, __float_as_uint(mx * 1.0000001f));
+  if (lane == 0 && mx > 0.0f) atomicMax(hdr, __float_as_uint(mx * 1.0000001f));
+  if (lane == 0 && md > 0.0f) atomicMax(hdr + 1, __float_as_uint(md * 1.0001f));
 }
 
 struct BfArgs {
@@ -846,10 +862,15 @@ __device__ __forceinline__ void bitonic_desc_n(float* ss, int* si, int P) {
   }
 }
 
-// ||u_q|| * 1.0000001 (fixed-order reduction by the block's first wave; every wave computes it)
-__device__ __forceinline__ float query_norm(const float* U, int64_t ldu, int64_t q) {
+// delta_q (see the bf16 path's header): ||u|| and ||u - bf16(u)|| by fixed-order wave reductions
+// (every wave computes them), hdr = the corpus header of topk_bf16_prep_k
+__device__ __forceinline__ float query_delta(const float* U, int64_t ldu, int64_t q, const unsigned* hdr) {
   const float2 uv = reinterpret_cast<const float2*>(U + q * ldu)[threadIdx.x & 63];
-  return sqrtf(rsx::wave_sum_width(uv.x * uv.x + uv.y * uv.y, 64)) * 1.0000001f;
+  const float dx = uv.x - (float)(__bf16)uv.x, dy = uv.y - (float)(__bf16)uv.y;
+  const float nu = sqrtf(rsx::wave_sum_width(uv.x * uv.x + uv.y * uv.y, 64)) * 1.0000001f;
+  const float nd = sqrtf(rsx::wave_sum_width(dx * dx + dy * dy, 64)) * 1.0001f;
+  const float W = __uint_as_float(hdr[0]), D = __uint_as_float(hdr[1]);
+  return (nu * D + nd * W + 3.0f * nd * D + 0.000244140625f * nu * W) * 1.00001f + 1e-30f;
 }
 
 // Order-preserving uint key of a float (larger float <=> larger key).
@@ -965,7 +986,7 @@ __global__ __launch_bounds__(256) void topk_bf16_thresh_k(const float* __restric
   }
   nv = rsx::wave_sum_width(nv, 64);
   if ((threadIdx.x & 63) == 0) atomicAdd(&nval_s, nv);
-  const float delta = query_norm(U, ldu, q) * __uint_as_float(*wmax_bits) * kDeltaRel + 1e-30f;
+  const float delta = query_delta(U, ldu, q, wmax_bits);
   __syncthreads();
   if (nval_s < K) {  // block-uniform
     if (threadIdx.x == 0) thr[q] = -INFINITY;
@@ -998,7 +1019,7 @@ __global__ __launch_bounds__(256) void topk_bf16_select_k(const float2* __restri
   __shared__ int bad_s, nsel_s;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t q = blockIdx.x;
-  const float delta = query_norm(U, ldu, q) * __uint_as_float(*wmax_bits) * kDeltaRel + 1e-30f;
+  const float delta = query_delta(U, ldu, q, wmax_bits);
   if (tid == 0) { bad_s = 0; nsel_s = 0; }
   __syncthreads();
   // counts (nstreams <= 512) -> exclusive prefix in LDS: wave 0, eight streams per lane
@@ -1313,7 +1334,8 @@ FastLayout fast_layout(int64_t Q, int64_t NI, int64_t k, const FastPlan& p) {
 //   int32 [0] queries the bf16 path sent to the exact kernels (all chunks), [1] path id
 //   (rsx_topk_path), [2] the fast path's whole-batch fallback flag, [3] the current chunk's
 //   fallback-query count (indexes qmap).
-// The bf16 path's corpus image (rsx_topk_prepare_corpus: a 256-byte header holding max ||w|| bits,
+// The bf16 path's corpus image (rsx_topk_prepare_corpus: a 256-byte header holding the bits of
+// max ||w|| and max ||w - bf16(w)||,
 // then the [NI][128] bf16 image) either lives in the caller's cached buffer or is built into the
 // workspace per call. Queries run in chunks of at most kQChunk (workspace bounded in Q).
 constexpr int64_t kHeader = 256;
@@ -1386,7 +1408,7 @@ int topk_path(int64_t Q, int64_t NI, int64_t k) {
 }
 
 void launch_prep(const float* I, int64_t ldi, int64_t NI, char* corpus, hipStream_t st) {
-  (void)hipMemsetAsync(corpus, 0, 4, st);
+  (void)hipMemsetAsync(corpus, 0, 8, st);  // max ||w||, max ||w - bf16(w)||
   int64_t pb = (NI + 31) / 32;
   if (pb > 4096) pb = 4096;
   hipLaunchKernelGGL(topk_bf16_prep_k, dim3((unsigned)pb), dim3(256), 0, st, I, ldi, NI,
