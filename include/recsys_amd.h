@@ -334,7 +334,7 @@ int rsx_retrieve_topk(const float* U, int64_t ldu, const float* I, int64_t ldi, 
 int rsx_topk_path(int64_t Q, int64_t NI, int64_t k);
 /* Path 2 with a caller-cached corpus image (a static corpus, e.g. the serving item matrix of
  * controller.py:62-124 or evaluate_model's normalised item table, :672): rsx_topk_prepare_corpus
- * writes max ||w|| and the bf16 image of I into `corpus` (rsx_topk_corpus_bytes(NI) bytes) once;
+ * writes max ||w||, max ||w - bf16(w)|| and the bf16 image of I into `corpus` (rsx_topk_corpus_bytes(NI) bytes) once;
  * rsx_retrieve_topk_corpus then skips that pass (ws: rsx_topk_workspace_bytes_corpus). I must
  * be the corpus the image was made from (the exact rescoring reads it). */
 int64_t rsx_topk_corpus_bytes(int64_t NI);
