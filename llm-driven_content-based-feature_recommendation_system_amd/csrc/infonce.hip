@@ -1612,9 +1612,6 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_fwd_x3_k(GArgs a) {
 // interleaved with G of tile t (dots_g_x3) over a three-deep LDS ring.
 template <bool ROW_OWNED, bool HALFG = true>
 __global__ __launch_bounds__(256, RSX_BWD_X3_OCC) void nce_grouped_bwd_x3_k(GArgs a) {
-#ifdef RSX_NCE_PRIO
-  if ((blockIdx.x >> RSX_NCE_PRIO) & 1) __builtin_amdgcn_s_setprio(1);
-#endif
   constexpr int kRing = RSX_BWD_X3_PIPE ? 3 : 2;
   __shared__ __attribute__((aligned(16))) X3Tile sT[kRing];
   __shared__ __attribute__((aligned(16))) float sM0[kRing][kTile];  // rows: bias_d*log2e | cols: lse_i*log2e (+inf past the split)
@@ -2363,9 +2360,6 @@ struct X3StageT {
 // merge, and should not evict the streamed B images from L2).
 template <int NW, bool NT>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void nce_grouped_fwdg_x3p_k(GArgs a) {
-#ifdef RSX_NCE_PRIO
-  if ((blockIdx.x >> RSX_NCE_PRIO) & 1) __builtin_amdgcn_s_setprio(1);
-#endif
   constexpr int kRows = 32 * NW;
   __shared__ __attribute__((aligned(16))) X3Tile sT[3];  // ring: t-1 (deferred k-step), t, t+1
   __shared__ __attribute__((aligned(16))) float sB2[3][kTile];   // -bias_d * log2e (-inf past the split)
