@@ -543,8 +543,9 @@ def bench_retrieve_rerank(args, device, deepfm, rank=0, world=1):
                                        "MFMA peak (the scan's arithmetic); fp32-MFMA peak 157.3 TF for reference",
                           "corpus_hbm_bytes": int((hi - lo) * 128 * (4 + 2 + 2))}}
     if world > 1:
+        coll = "RCCL" if torch.distributed.get_backend() == "nccl" else torch.distributed.get_backend()
         line["sharding"] = (f"corpus by item range ({hi - lo} rows on rank {rank}), per-rank top-{K} with global "
-                            f"indices all-gathered over RCCL and merged (score desc, index asc); DeepFM by query "
+                            f"indices all-gathered over {coll} and merged (score desc, index asc); DeepFM by query "
                             f"({q1 - q0} queries x {K} rows per rank)")
     return line, (out[0], out[2], cand)
 

@@ -399,9 +399,15 @@ RSX_API int rsx_ln_fwd(const float* x, const float* res, float p_drop, uint64_t 
   return 0;
 }
 
+// An upper bound of bwd_blocks(T', D) for every T' <= T (bwd_blocks itself is not monotonic in T:
+// rounding rows-per-block up to the quantum can leave a larger T with fewer blocks), so a caller may
+// size one workspace by its largest row count and use it for smaller ones (the tower backward's
+// tail rows R < T: rsx_tower_bwd).
 RSX_API int64_t rsx_ln_bwd_workspace_floats(int64_t T, int64_t D) {
-  int64_t rpb;
-  return bwd_blocks(T, D, rpb) * 2 * D + 64;
+  if (T <= 0) return 64;
+  const int64_t quantum = D > 256 ? 4 : 4 * (64 / (D / 4));
+  const int64_t b = (T + quantum - 1) / quantum;
+  return (b < kMaxBlocks ? b : kMaxBlocks) * 2 * D + 64;
 }
 
 RSX_API int rsx_ln_bwd(const float* s, const float* mean, const float* rstd, const float* w, const float* b, int act,
