@@ -40,3 +40,17 @@ def test_clip_adamw_declines_what_it_does_not_reproduce():
     assert not ops._adamw_native_ok(torch.optim.Adam([p]))
     assert ops._adamw_native_ok(torch.optim.AdamW([p], lr=5e-4, weight_decay=0.01))
     assert len(torch.optim.AdamW([p]).state) == 0
+
+
+def test_ln_bwd_workspace_is_monotonic_in_rows():
+    """rsx_ln_bwd_workspace_floats(T) must cover every smaller row count: the tower backward sizes
+    one workspace by T and runs its tail rows (R < T) on it (the block split itself is not monotonic
+    in T; the 2-rank rehearsal once failed with 'workspace too small'). Host-only C-ABI call."""
+    from recsys_amd import _native as N
+    lib = N.lib()
+    for D in (64, 128, 256):
+        prev = 0
+        for T in list(range(1, 5000, 37)) + list(range(150_000, 420_000, 997)):
+            w = lib.rsx_ln_bwd_workspace_floats(T, D)
+            assert w >= prev, (D, T, w, prev)
+            prev = w
