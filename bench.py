@@ -40,7 +40,7 @@ FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32-input MFMA (= f
 BF16_MFMA_PEAK_TFLOPS = 16 * FP32_MFMA_PEAK_TFLOPS  # 2516.8: dense bf16 MFMA (16x the f32 rate, same guide)
 # bf16x3: every fp32-equivalent FLOP is three bf16 MFMA products (hi*hi + hi*lo + lo*hi)
 BF16X3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 3
-TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r04_nce_fwdg_traffic_b8192.json")
+TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r05_nce_fwdg_traffic_b8192.json")
 HBM_PEAK_GBS = 8000.0
 
 
