@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 
 import torch
 
@@ -745,6 +746,11 @@ def _adamw_native_ok(opt) -> bool:
     return True
 
 
+# per-optimizer pointer / size arrays of rsx_clip_adamw, reused while the parameter list, the
+# clip set and the state tensors are the same objects (rebuilt otherwise; gradients every step)
+_ADAMW_CACHE: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+
+
 def clip_adamw_step(optimizer, clip_params, max_norm: float):
     """torch.nn.utils.clip_grad_norm_(clip_params, max_norm) followed by optimizer.step() for a
     torch.optim.AdamW, as two launches (rsx_clip_adamw) instead of torch's ~10 (per-tensor norms,
@@ -773,8 +779,6 @@ def clip_adamw_step(optimizer, clip_params, max_norm: float):
         return None
     N.ensure_device(items[0][0])
     state = optimizer.state
-    dev_steps, cpu_steps = [], []
-    m_l, v_l = [], []
     for p, gr, g in items:
         st = state[p]
         if len(st) == 0:   # torch.optim.Adam._init_group
@@ -782,39 +786,50 @@ def clip_adamw_step(optimizer, clip_params, max_norm: float):
                           else torch.tensor(0.0, dtype=torch.float32))
             st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
             st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-        m, v, s = st["exp_avg"], st["exp_avg_sq"], st["step"]
-        if not (m.is_contiguous() and v.is_contiguous() and m.dtype == torch.float32 and v.dtype == torch.float32):
-            return None
-        m_l.append(m)
-        v_l.append(v)
-        (dev_steps if s.device.type == "cuda" else cpu_steps).append(s)
+    sts = [state[p] for p, _, _ in items]
+    sig = (tuple(id(p) for p, _, _ in items), frozenset(clip_ids),
+           tuple((id(st["exp_avg"]), id(st["exp_avg_sq"]), id(st["step"])) for st in sts))
+    c = _ADAMW_CACHE.get(optimizer)
+    if c is None or c["sig"] != sig:
+        m_l, v_l, dev_steps, cpu_steps = [], [], [], []
+        for st in sts:
+            m, v, s = st["exp_avg"], st["exp_avg_sq"], st["step"]
+            if not (m.is_contiguous() and v.is_contiguous() and m.dtype == torch.float32 and v.dtype == torch.float32):
+                return None
+            m_l.append(m)
+            v_l.append(v)
+            (dev_steps if s.device.type == "cuda" else cpu_steps).append(s)
+        n = len(items)
+        numel = N.i64_array([p.numel() for p, _, _ in items])
+        clip = (ctypes.c_int * n)(*[1 if id(p) in clip_ids else 0 for p, _, _ in items])
+        steps_t = [st["step"] for st in sts]
+        c = {"sig": sig, "n": n, "dev_steps": dev_steps, "cpu_steps": cpu_steps, "steps_t": steps_t,
+             # the tensors are held so that the ids in sig cannot be reused by other objects
+             "hold": (m_l, v_l, [p for p, _, _ in items]),
+             "ps": N.ptr_array([p for p, _, _ in items]), "ms": N.ptr_array(m_l), "vs": N.ptr_array(v_l),
+             "numel": numel, "clip": clip,
+             "step_d": N.ptr_array([s if s.device.type == "cuda" else None for s in steps_t]) if dev_steps else None,
+             "nbytes": N.lib().rsx_clip_adamw_workspace_bytes(n, numel, clip)}
+        _ADAMW_CACHE[optimizer] = c
+    n = c["n"]
     # the step counts first, as torch's AdamW does (one multi-tensor launch for device counts)
-    if dev_steps:
-        torch._foreach_add_(dev_steps, 1.0)
-    if cpu_steps:
-        torch._foreach_add_(cpu_steps, 1.0)
-    n = len(items)
-    ps = N.ptr_array([p for p, _, _ in items])
+    if c["dev_steps"]:
+        torch._foreach_add_(c["dev_steps"], 1.0)
+    if c["cpu_steps"]:
+        torch._foreach_add_(c["cpu_steps"], 1.0)
     gs = N.ptr_array([gr for _, gr, _ in items])
-    ms = N.ptr_array(m_l)
-    vs = N.ptr_array(v_l)
-    numel = N.i64_array([p.numel() for p, _, _ in items])
-    clip = (ctypes.c_int * n)(*[1 if id(p) in clip_ids else 0 for p, _, _ in items])
-    steps_t = [state[p]["step"] for p, _, _ in items]
-    step_h = (ctypes.c_float * n)(*[0.0 if s.device.type == "cuda" else float(s) for s in steps_t])
-    step_d = N.ptr_array([s if s.device.type == "cuda" else None for s in steps_t]) if dev_steps else None
+    step_h = (ctypes.c_float * n)(*[0.0 if s.device.type == "cuda" else float(s) for s in c["steps_t"]])
     lr = (ctypes.c_double * n)(*[g["lr"] for _, _, g in items])   # doubles, as torch's kernels take them
     wd = (ctypes.c_double * n)(*[g["weight_decay"] for _, _, g in items])
     b1 = (ctypes.c_double * n)(*[g["betas"][0] for _, _, g in items])
     b2 = (ctypes.c_double * n)(*[g["betas"][1] for _, _, g in items])
     eps = (ctypes.c_double * n)(*[g["eps"] for _, _, g in items])
-    lib = N.lib()
-    nbytes = lib.rsx_clip_adamw_workspace_bytes(n, numel, clip)
     dev = items[0][0].device
+    nbytes = c["nbytes"]
     ws = torch.empty(nbytes, device=dev, dtype=torch.uint8)
     norm = torch.empty((), device=dev, dtype=torch.float32)
-    rc = lib.rsx_clip_adamw(n, ps, gs, ms, vs, numel, clip, step_h, step_d, lr, wd, b1, b2, eps, float(max_norm),
-                            N.ptr(ws), nbytes, N.ptr(norm), N.stream())
+    rc = N.lib().rsx_clip_adamw(n, c["ps"], gs, c["ms"], c["vs"], c["numel"], c["clip"], step_h, c["step_d"], lr, wd,
+                                b1, b2, eps, float(max_norm), N.ptr(ws), nbytes, N.ptr(norm), N.stream())
     N.check(rc, "clip_adamw")
     optimizer._opt_called = True   # what torch's step wrapper records (LR schedulers check it)
     return norm
