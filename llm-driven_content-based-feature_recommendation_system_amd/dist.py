@@ -630,7 +630,7 @@ def contrastive_step_dp(model, item_tower, log_q_tensor, batch, optimizer, cfg, 
     objective.backward()
     bucket()
     # clip + AdamW in two launches (rsx_clip_adamw); torch's pair for optimizers it does not cover
-    if ops.clip_adamw_step(optimizer, model.parameters(), max_norm) is None:
+    if ops.clip_adamw_step(optimizer, ops.module_params(model), max_norm) is None:
         torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=max_norm)
         optimizer.step()
     return total, main, cl

@@ -751,6 +751,21 @@ def _adamw_native_ok(opt) -> bool:
 _ADAMW_CACHE: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
 
 
+def module_params(model):
+    """The set of model.parameters() (same members: every registered, non-None parameter of the
+    module tree, each once) by a plain walk of _modules / _parameters: the clip set of the step,
+    where only membership matters, without named_parameters()' prefix strings (~0.2 ms per step)."""
+    out, seen, stack = [], set(), [model]
+    while stack:
+        m = stack.pop()
+        for p in m._parameters.values():
+            if p is not None and id(p) not in seen:
+                seen.add(id(p))
+                out.append(p)
+        stack.extend(c for c in m._modules.values() if c is not None)
+    return out
+
+
 def clip_adamw_step(optimizer, clip_params, max_norm: float):
     """torch.nn.utils.clip_grad_norm_(clip_params, max_norm) followed by optimizer.step() for a
     torch.optim.AdamW, as two launches (rsx_clip_adamw) instead of torch's ~10 (per-tensor norms,

@@ -205,7 +205,7 @@ def contrastive_step(model, item_tower, log_q_tensor, batch, optimizer, scaler, 
         total.backward()
         if grad_sync is not None:
             grad_sync()
-        if ops.clip_adamw_step(optimizer, model.parameters(), max_norm) is None:   # rsx_clip_adamw
+        if ops.clip_adamw_step(optimizer, ops.module_params(model), max_norm) is None:   # rsx_clip_adamw
             torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=max_norm)
             optimizer.step()
     return total.detach(), main.detach(), cl.detach()
@@ -285,7 +285,7 @@ def train_user_tower(epoch, model, item_tower, log_q_tensor, dataloader, optimiz
         optimizer.zero_grad(set_to_none=True)
         total, main, cl, stats = hard_emphasis_losses(model, item_tower, log_q_tensor, batch, cfg, lookup)
         total.backward()
-        if ops.clip_adamw_step(optimizer, model.parameters(), 5.0) is None:
+        if ops.clip_adamw_step(optimizer, ops.module_params(model), 5.0) is None:
             torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=5.0)
             optimizer.step()
         tot += total.item()

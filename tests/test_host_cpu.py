@@ -54,3 +54,15 @@ def test_ln_bwd_workspace_is_monotonic_in_rows():
             w = lib.rsx_ln_bwd_workspace_floats(T, D)
             assert w >= prev, (D, T, w, prev)
             prev = w
+
+
+def test_module_params_same_set_as_parameters():
+    """ops.module_params (the clip set of the native clip+AdamW) holds exactly model.parameters():
+    shared parameters once, None slots skipped, nested and tied modules walked."""
+    lin = torch.nn.Linear(4, 4)
+    model = torch.nn.Sequential(lin, torch.nn.ReLU(), torch.nn.Sequential(torch.nn.Linear(4, 2), lin))
+    model.register_parameter("nothing", None)
+    model.extra = torch.nn.Parameter(torch.zeros(3))
+    got = ops.module_params(model)
+    assert len(got) == len(list(model.parameters()))
+    assert {id(p) for p in got} == {id(p) for p in model.parameters()}
