@@ -374,9 +374,10 @@ int rsx_deepfm_fused(const int64_t* x, int64_t R, int F, const float* const* V, 
  * F in [25, 48] runs the persistent kernel (one workgroup per CU looping over 64-row blocks). */
 int rsx_deepfm_fused_prep(int F, const float* w1, const float* w2, void* ws, void* stream);
 /* packed: nullable per-field tables from rsx_deepfm_pack, read instead of V/W when
- * rsx_deepfm_fused_uses_packed(F) == 1 (F = 39: the row-owning kernel; other F in [25, 48]: the
- * persistent kernel): a field's V row and first-order weight then share one 128-B line, halving
- * the lines fetched per (row, field) on random ids. NULL: V/W are read directly. */
+ * rsx_deepfm_fused_uses_packed(F) == 1 (F = 39: deepfm_rows2m_k, 256-row workgroups of eight 32-row
+ * waves, 130 KiB of LDS; other F in [25, 48]: the persistent kernel): a field's V row and first-order
+ * weight then share one 128-B line, halving the lines fetched per (row, field) on random ids. NULL:
+ * V/W are read directly (F = 39: deepfm_rows5_k). */
 int rsx_deepfm_fused_run(const int64_t* x, int64_t R, int F, const float* const* V, const float* const* W,
                          const float* const* packed, float bias, const float* b1, const float* b2, const float* wo,
                          const void* ws, float* logit, float* prob, void* stream);
