@@ -306,7 +306,7 @@ int rsx_ids_check(const int64_t* ids, int64_t n, int64_t lo, int64_t hi, int64_t
  *      item-id segment-sum plan: 16 perm [2T], 17 cb [C+1], 18 chunk ids [C], 19 ch_off [U+1],
  *      20 ids [U] (all i64); the grouped-loss index: 21 uniq [D] i64, 22 colcnt [D] f32,
  *      23 row_col, 24 row_beg, 25 row_end, 26 exc_cols [N] i32, 27 exc_s, 28 exc_e, 29 exc_n [E]
- *      i32, 30 col_beg, 31 col_end [D] i32; 32 last_t [B] i64 (DuoRec targets).
+ *      i32, 30 col_beg, 31 col_end [D] i32; 32 last_t [B] i32 (the SupCon keys: last targets).
  * ws: rsx_step_index_workspace_bytes(B, L, n_items), the same buffer for all three calls. */
 int64_t rsx_step_index_workspace_bytes(int64_t B, int64_t L, int64_t n_items);
 int rsx_step_index_count(const uint8_t* pm, const int64_t* tgt, const int64_t* item, int64_t B, int64_t L,

@@ -224,7 +224,7 @@ struct FillOut {
   int64_t* seg2_64;
   int64_t* tok_ids;  // [6][2T]
   int *row_col, *row_beg, *row_end, *exc_cols;
-  int64_t* last_t;
+  int* last_t;  // int32: the SupCon kernel's key type (ids < n_items < 2^31)
 };
 
 __global__ __launch_bounds__(256) void si_tokens_k(const uint8_t* pm, const int64_t* tgt, const int64_t* ids0,
@@ -295,7 +295,7 @@ __global__ __launch_bounds__(256) void si_tokens_k(const uint8_t* pm, const int6
   }
   if (lane == 0) {
     f.last_tok[b] = t0 + __popcll(u.sm & ((u.last == 0) ? 0ull : (~0ull >> (64 - u.last))));
-    f.last_t[b] = tgt[b * L + u.last];
+    f.last_t[b] = (int)tgt[b * L + u.last];
     f.seg1[b] = (int)t0;
     f.seg1_64[b] = t0;
     f.seg2[b] = (int)t0;
@@ -538,7 +538,7 @@ RSX_API int rsx_step_index_fill(const uint8_t* pm, const int64_t* tgt, const int
   f.flat2 = (int64_t*)out[8]; f.user2 = (int64_t*)out[9]; f.pos2 = (int64_t*)out[10]; f.pad2 = (uint8_t*)out[11];
   f.seg2 = (int*)out[12]; f.seg2_64 = (int64_t*)out[13]; f.tok_ids = (int64_t*)out[14];
   f.row_col = (int*)out[23]; f.row_beg = (int*)out[24]; f.row_end = (int*)out[25]; f.exc_cols = (int*)out[26];
-  f.last_t = (int64_t*)out[32];
+  f.last_t = (int*)out[32];
   const unsigned gu = (unsigned)((B + 3) / 4);
   hipLaunchKernelGGL(si_tokens_k, dim3(gu), dim3(256), 0, st, pm, tgt, seq_ids[0], seq_ids[1], seq_ids[2],
                      seq_ids[3], seq_ids[4], seq_ids[5], B, (int)L, T, at<int>(ws, l.offT), at<int>(ws, l.offN),

@@ -383,7 +383,7 @@ def _prepare_step_index_device(batch, pretrained_vecs, pretrained_lookup, n_item
              ((2 * B + 1,), i64), ((6, 2 * T), i64), (((2 * T, 128), f32) if pretrained_vecs is None else None),
              ((2 * T,), i64), ((C + 1,), i64), ((C,), i64), ((U + 1,), i64), ((U,), i64), ((D,), i64), ((D,), f32),
              ((Nr,), i32), ((Nr,), i32), ((Nr,), i32), ((Nr,), i32), ((E,), i32), ((E,), i32), ((E,), i32),
-             ((D,), i32), ((D,), i32), ((B,), i64)]
+             ((D,), i32), ((D,), i32), ((B,), i32)]
     out = _carve(specs, dev)  # the 33 index arrays out of ONE allocation
     lk = ops._c(pretrained_lookup) if pretrained_vecs is None else None
     N.check(lib.rsx_step_index_fill(N.ptr(pm8), N.ptr(tgt), N.ptr_array(seq), N.ptr(lk),
@@ -458,7 +458,7 @@ def prepare_step_index(batch, pretrained_vecs=None, pretrained_lookup=None, n_it
         user_loc = pk.tok_user[pk.valid_tok] + rank * B
         t_glob = all_gather_var(t_loc, ix.counts, group=grp)
         ix.groups = ops.TargetGroups(t_loc, user_loc, t_cols=t_glob)
-    ix.last_t = target_ids.reshape(-1)[pk.flat[pk.last_tok]]
+    ix.last_t = target_ids.reshape(-1)[pk.flat[pk.last_tok]].to(torch.int32)  # the SupCon keys (as rsx_step_index_fill)
     ix.t_glob_last = all_gather_var(ix.last_t, [B] * ws, group=grp)
     return ix
 
