@@ -183,6 +183,53 @@ class _Heartbeat:
         return False
 
 
+def _walk_clocks(obj, out, path=""):
+    """Collect {path: MHz} for every clock entry of an amd-smi / rocm-smi JSON document."""
+    if isinstance(obj, dict):
+        for k, v in obj.items():
+            _walk_clocks(v, out, f"{path}/{k}")
+    elif isinstance(obj, list):
+        for i, v in enumerate(obj):
+            _walk_clocks(v, out, f"{path}[{i}]")
+    else:
+        import re
+        low = path.lower()
+        if ("clk" in low or "clock" in low) and not any(w in low for w in ("min_", "max_", "_locked", "deep_sleep",
+                                                                          "level")):
+            m = re.search(r"([0-9]+(?:\.[0-9]+)?)", str(obj))
+            if m and (low.endswith("/value") or "mhz" in str(obj).lower() or low.endswith("clock speed:")):
+                out[path] = float(m.group(1))
+
+
+def gpu_clocks():
+    """Shader (SCLK) and memory (MCLK) clocks of the visible GPU right now, from amd-smi (rocm-smi as a
+    fallback): {"sclk_mhz", "mclk_mhz", "source"} (None where the tool or field is missing). Bench lines
+    from different boxes are only comparable at equal clocks."""
+    import subprocess
+    res = {"sclk_mhz": None, "mclk_mhz": None, "source": None}
+    for cmd in (["amd-smi", "metric", "-c", "--json"], ["rocm-smi", "--showclocks", "--json"]):
+        try:
+            p = subprocess.run(cmd, capture_output=True, text=True, timeout=20)
+            out = p.stdout
+            start = min([i for i in (out.find("{"), out.find("[")) if i >= 0], default=-1)
+            if start < 0:
+                continue
+            doc = json.JSONDecoder().raw_decode(out[start:])[0]  # the tools may print warnings around it
+        except (OSError, ValueError, subprocess.SubprocessError):
+            continue
+        flat = {}
+        _walk_clocks(doc, flat)
+        sc = [v for k, v in flat.items() if any(w in k.lower() for w in ("gfx", "sclk"))]
+        mc = [v for k, v in flat.items() if any(w in k.lower() for w in ("/mem", "mclk"))]
+        if sc or mc:
+            # amd-smi reports one shader clock per XCD (gfx_0..gfx_7): their mean, and the spread
+            res.update({"sclk_mhz": round(sum(sc) / len(sc), 1) if sc else None,
+                        "sclk_range_mhz": [min(sc), max(sc)] if sc else None,
+                        "mclk_mhz": max(mc) if mc else None, "source": " ".join(cmd[:2])})
+            break
+    return res
+
+
 def cpu_threads(args):
     """(threads, host info, rule): BASELINE.md's P = physical host cores, capped by this
     process's affinity mask and cgroup CPU quota (the GPU box grants a share of the host)."""
@@ -214,12 +261,53 @@ def cpu_timed(fn, warm=2, reps=5, single_over_s=60.0):
     return ts[len(ts) // 2], reps
 
 
-def cpu_baseline(args, items, cfg, batch_size, batch_seed):
+def gpu_step_from_state(state, cfg, items, batch, device):
+    """One GPU train step exactly as the headline times it (dist.contrastive_step_dp: packed two-view
+    tower, grouped LogQ + DuoRec kernels, backward, native clip + AdamW) from a given state -- the
+    oracle's tower weights, item matrix and AdamW moments (state["model"], ["W"], ["opt"]) -- at dropout
+    0 on `batch` (CPU tensors). -> oracle.agreement.capture of the result (CPU copies)."""
+    import dataclasses
+    from oracle import agreement as OA
+    from recsys_amd import dist as D
+    from recsys_amd.tower_code import v1_usertower_train as TT
+    from recsys_amd.tower_code.v1_refine_usertower import SASRecUserTower
+    cfg0 = dataclasses.replace(cfg, dropout=0.0)
+    model = SASRecUserTower(cfg0).to(device)
+    model.load_state_dict(state["model"])
+    model.train()
+    W = state["W"]
+    it = TT.SASRecItemTower(W.shape[0] - 1, W.shape[1], items.log_q.clone()).to(device)
+    it.init_from_pretrained(W.to(device))
+    it.set_freeze_state(False)
+    opt = torch.optim.AdamW(model.parameters(), lr=cfg.lr, weight_decay=cfg.weight_decay, fused=True)
+    opt.add_param_group({"params": list(it.parameters()), "lr": cfg.lr * 0.05})
+    opt.load_state_dict(state["opt"])
+    bucket = D.GradBucket(list(model.parameters()) + list(it.parameters()))
+    bd = {k: (v.to(device) if torch.is_tensor(v) else v) for k, v in batch.items()}
+    lookup = items.pretrained.to(device)
+    ix = D.prepare_step_index(bd, pretrained_lookup=lookup)
+    losses = D.contrastive_step_dp(model, it, it.log_q, bd, opt, cfg0, lookup, bucket, index=ix)
+    torch.cuda.synchronize()
+    return OA.capture(model, it.item_matrix.weight, losses)
+
+
+def oracle_state(model, W, opt):
+    """CPU copies of the oracle's step state (what gpu_step_from_state starts from)."""
+    import copy
+    return {"model": {k: v.detach().clone() for k, v in model.state_dict().items()}, "W": W.detach().clone(),
+            "opt": copy.deepcopy(opt.state_dict())}
+
+
+def cpu_baseline(args, items, cfg, batch_size, batch_seed, device=None):
     """The oracle (CPU PyTorch fp32 restatement of tower_code/v1_usertower_train.py:717-893) on
     the SAME global batch the GPU headline runs (same generator, same seed), dropout p = 0
     (BASELINE.md): one timed step after a small warm-up step; the main loss row-chunked (same
-    arithmetic, bounded RAM)."""
+    arithmetic, bounded RAM). With `device`, the GPU step is then run from the oracle's own pre-step
+    state (weights, item matrix, AdamW moments after the warm-up) on the same batch at dropout 0, and
+    the two results are compared (oracle/agreement.py: losses 1e-4, gradients 1e-3 of scale,
+    post-AdamW parameters 1e-5): "agreement_with_gpu"."""
     import dataclasses
+    from oracle import agreement as OA
     from oracle import user_tower as O
     from recsys_amd import synth
     threads, info, rule = cpu_threads(args)
@@ -236,21 +324,31 @@ def cpu_baseline(args, items, cfg, batch_size, batch_seed):
     O.contrastive_step(model, W, items.log_q, warm, opt, items.pretrained, loss_chunk=args.cpu_loss_chunk)
     batch = synth.make_batch(items, batch_size, seed=batch_seed)
     n_valid = int((~batch["padding_mask"]).sum())
+    state = oracle_state(model, W, opt) if device is not None else None
     with _Heartbeat(f"cpu_baseline step ({batch_size} users, {n_valid} valid steps)"):
         t0 = time.perf_counter()
-        O.contrastive_step(model, W, items.log_q, batch, opt, items.pretrained, loss_chunk=args.cpu_loss_chunk)
+        losses = O.contrastive_step(model, W, items.log_q, batch, opt, items.pretrained,
+                                    loss_chunk=args.cpu_loss_chunk)
         dt = time.perf_counter() - t0
     torch.set_num_threads(prev_threads)
-    return {"value": round(batch_size / dt, 3), "unit": "pairs/s", "cores": threads,
-            "kind": "port",
-            "threads_rule": rule,
-            "host": info,
-            "sample": (f"oracle/user_tower.py contrastive_step (fp32 PyTorch CPU, dropout 0, AdamW) on the GPU "
-                       f"headline's first global batch ({batch_size} users, {n_valid} valid steps, same seed); "
-                       f"ONE timed step ({dt:.1f} s) after a 64-user warm-up step; main loss evaluated over "
-                       f"{args.cpu_loss_chunk}-row chunks of the N x N logits under activation checkpointing "
-                       f"(same per-element arithmetic; the one-shot N x N tensors would need ~{4 * n_valid ** 2 / 1e9:.0f} GB)"),
-            "seconds_per_step": round(dt, 2)}
+    out = {"value": round(batch_size / dt, 3), "unit": "pairs/s", "cores": threads,
+           "kind": "port",
+           "threads_rule": rule,
+           "host": info,
+           "sample": (f"oracle/user_tower.py contrastive_step (fp32 PyTorch CPU, dropout 0, AdamW) on the GPU "
+                      f"headline's first global batch ({batch_size} users, {n_valid} valid steps, same seed); "
+                      f"ONE timed step ({dt:.1f} s) after a 64-user warm-up step; main loss evaluated over "
+                      f"{args.cpu_loss_chunk}-row chunks of the N x N logits under activation checkpointing "
+                      f"(same per-element arithmetic; the one-shot N x N tensors would need ~{4 * n_valid ** 2 / 1e9:.0f} GB)"),
+           "seconds_per_step": round(dt, 2)}
+    if device is not None:
+        ref = OA.capture(model, W, losses)
+        dut = gpu_step_from_state(state, cfg, items, batch, device)
+        agr = OA.compare_step(ref, dut)
+        agr["what"] = ("the GPU step (dist.contrastive_step_dp, dropout 0) from the oracle's pre-step state on the "
+                       "same batch vs this timed oracle step: losses, clipped gradients, post-AdamW parameters")
+        out["agreement_with_gpu"] = agr
+    return out
 
 
 def deepfm_cpu_state(model):
@@ -269,22 +367,38 @@ def _deepfm_cpu(st, x):
     return OD.deepfm_forward(x, st["emb"], st["lin"], st["bias"], st["ws"], st["bs"], st["wo"], dtype=torch.float32)
 
 
-def cpu_baseline_deepfm(args, st, x):
+def cpu_baseline_deepfm(args, st, x, gpu_logits=None):
     """configs[2] on the host: oracle/deepfm.py (gather + FM + DNN, fp32) on the GPU line's own
-    65,536 Zipf(1.1) rows over the same 39 x 1e6-row tables."""
+    65,536 Zipf(1.1) rows over the same 39 x 1e6-row tables. With gpu_logits (the GPU line's output
+    for the same rows), the timed call's logits are compared with it: "agreement_with_gpu" (every
+    row within 1e-4, the north star's logit tolerance; asserted)."""
     threads, info, rule = cpu_threads(args)
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     xc = x.cpu()
+    res = {}
+
+    def call():
+        res["out"] = _deepfm_cpu(st, xc)
+
     with torch.no_grad(), _Heartbeat("cpu_baseline deepfm"):
-        dt, n = cpu_timed(lambda: _deepfm_cpu(st, xc))
+        dt, n = cpu_timed(call)
     torch.set_num_threads(prev)
     R = xc.shape[0]
-    return {"value": round(R / dt, 1), "unit": "rows/s", "cores": threads, "kind": "port", "threads_rule": rule,
-            "sample": (f"oracle/deepfm.py deepfm_forward (fp32 PyTorch CPU: 39 table gathers, FM, DNN 624-256-128-1) "
-                       f"on the GPU line's {R} rows (the whole batch, same ids and tables); median of {n} calls "
-                       f"after 2 warm-up calls"),
-            "seconds_per_call": round(dt, 4)}
+    out = {"value": round(R / dt, 1), "unit": "rows/s", "cores": threads, "kind": "port", "threads_rule": rule,
+           "sample": (f"oracle/deepfm.py deepfm_forward (fp32 PyTorch CPU: 39 table gathers, FM, DNN 624-256-128-1) "
+                      f"on the GPU line's {R} rows (the whole batch, same ids and tables); median of {n} calls "
+                      f"after 2 warm-up calls"),
+           "seconds_per_call": round(dt, 4)}
+    if gpu_logits is not None:
+        ref = res["out"][0].reshape(-1).double()
+        got = gpu_logits.detach().reshape(-1).double().cpu()
+        err = (got - ref).abs()
+        out["agreement_with_gpu"] = {"rows": R, "logit_max_abs_err": float(err.max()),
+                                     "logit_mean_abs_err": float(err.mean()), "tol": 1e-4,
+                                     "ok": bool(float(err.max()) <= 1e-4)}
+        assert out["agreement_with_gpu"]["ok"], out["agreement_with_gpu"]
+    return out
 
 
 def cpu_baseline_retrieve_rerank(args, st, gpu_out, Qs=512, K=100, F=39, chunk=250_000):
@@ -341,15 +455,32 @@ def cpu_baseline_item_tower(args, gpu_model, inputs):
     ref.load_state_dict({k: v.detach().cpu() for k, v in gpu_model.state_dict().items()})
     ref.eval()
     xs = [t.cpu() for t in inputs]
+    res = {}
+
+    def call():
+        res["out"] = ref(*xs)
+
     with torch.no_grad(), _Heartbeat("cpu_baseline item tower"):
-        dt, n = cpu_timed(lambda: ref(*xs), warm=1, reps=3)
+        dt, n = cpu_timed(call, warm=1, reps=3)
     torch.set_num_threads(prev)
     B = xs[0].shape[0]
-    return {"value": round(B / dt, 1), "unit": "items/s", "cores": threads, "kind": "port", "threads_rule": rule,
-            "sample": (f"oracle/item_tower.py OracleHybridItemTower forward (fp32 PyTorch CPU, eval) on the GPU "
-                       f"line's {B} items and weights (bert-base-shaped local BERT); median of {n} calls after 1 "
-                       f"warm-up call"),
-            "seconds_per_call": round(dt, 4)}
+    out = {"value": round(B / dt, 1), "unit": "items/s", "cores": threads, "kind": "port", "threads_rule": rule,
+           "sample": (f"oracle/item_tower.py OracleHybridItemTower forward (fp32 PyTorch CPU, eval) on the GPU "
+                      f"line's {B} items and weights (bert-base-shaped local BERT, all 12 layers); median of {n} "
+                      f"calls after 1 warm-up call"),
+           "seconds_per_call": round(dt, 4)}
+    # the timed call's output against the GPU module's on the same inputs (eval, same weights):
+    # atol 1e-5 / rtol 1e-4 (tests/test_gpu_item_tower.py's bound, here through all 12 BERT layers)
+    with torch.no_grad():
+        got = gpu_model(*inputs).float().cpu()
+    exp = res["out"].float()
+    err = (got - exp).abs()
+    bound = 1e-5 + 1e-4 * exp.abs()
+    out["agreement_with_gpu"] = {"items": B, "max_abs_err": float(err.max()),
+                                 "max_err_over_bound": float((err / bound).max()), "atol": 1e-5, "rtol": 1e-4,
+                                 "ok": bool((err <= bound).all())}
+    assert out["agreement_with_gpu"]["ok"], out["agreement_with_gpu"]
+    return out
 
 
 def bench_deepfm(args, device):
@@ -721,7 +852,7 @@ def bench_eval_forward(args, device, model, items, users=4096, iters=10):
 
 
 def train_bench(args, global_batch, steps, warmup, items, cfg, model, item_tower, opt, bucket, rank, world,
-                device):
+                device, sample_clocks=False):
     """Times `steps` full train steps (after `warmup`) on this rank's slice of two seeded global
     batches of `global_batch` users (seeds args.seed + 100, + 101). -> dict with the max-over-ranks
     seconds, per-op HIP-event times, last losses, per-batch valid counts per rank, per-batch distinct
@@ -775,6 +906,10 @@ def train_bench(args, global_batch, steps, warmup, items, cfg, model, item_tower
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
+    clk0 = gpu_clocks() if sample_clocks else None
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
     retries0 = torch.cuda.memory_stats().get("num_alloc_retries", 0)
     enqueue.clear()
     ops.timing_start()
@@ -788,6 +923,7 @@ def train_bench(args, global_batch, steps, warmup, items, cfg, model, item_tower
     if world > 1:
         torch.distributed.barrier()
     t1 = time.perf_counter()
+    clk1 = gpu_clocks() if sample_clocks else None
     kernel_times = ops.timing_stop()
     kev = (ctypes.c_float * 256)()
     n_kev = N.lib().rsx_kernel_events_read(kev, 256)
@@ -848,7 +984,8 @@ def train_bench(args, global_batch, steps, warmup, items, cfg, model, item_tower
         D.all_reduce_(elapsed, op=torch.distributed.ReduceOp.MAX)
     return {"elapsed": float(elapsed.item()), "kernel_times": kernel_times, "losses": losses, "n_glob": n_glob,
             "n_dist": n_dist, "n_tok": n_tok, "host_enqueue_ms": round(1e3 * sum(enqueue) / max(len(enqueue), 1), 3),
-            "host_unloaded": host_unloaded, "alloc_retries": int(retries), "fwdg_kernel_ms": fwdg_kernel_ms}
+            "host_unloaded": host_unloaded, "alloc_retries": int(retries), "fwdg_kernel_ms": fwdg_kernel_ms,
+            "clocks": {"before_timed_steps": clk0, "after_timed_steps": clk1} if sample_clocks else None}
 
 
 def nce_roofline(args, tb, global_batch, rank, world, precision):
@@ -945,6 +1082,7 @@ def main():
     elif args.blas == "ck":
         torch.backends.cuda.preferred_blas_library("ck")
     import recsys_amd  # noqa: F401
+    from recsys_amd import _native as N
     from recsys_amd import dist as D
     from recsys_amd import ops, synth
     from recsys_amd.tower_code import v1_usertower_train as TT
@@ -971,7 +1109,7 @@ def main():
 
     # two distinct global batches, this rank's user slice of each, resident in HBM
     tb = train_bench(args, args.batch, args.steps, args.warmup, items, cfg, model, item_tower, opt, bucket, rank,
-                     world, device)
+                     world, device, sample_clocks=(rank == 0))
     total_loss = float(tb["losses"][0].item())
     kt = {k: {"launches": n, "avg_ms": round(t / max(n, 1), 4)} for k, (n, t) in sorted(tb["kernel_times"].items())}
     result = {
@@ -1013,6 +1151,9 @@ def main():
         "alloc_retries": tb["alloc_retries"],
         "kernels": kt,
         "final_loss": round(total_loss, 5),
+        "gpu_clocks": tb["clocks"],
+        "device": torch.cuda.get_device_name(device),
+        "build": N.build_info(),
     }
     del tb
     if world == 1 and not args.no_batch4096 and args.batch != 4096:
@@ -1085,7 +1226,9 @@ def main():
         if cpu_lines:
             dst = deepfm_cpu_state(deepfm)
             line = result["secondary"]
-            line["cpu_baseline"] = cpu_baseline_deepfm(args, dst, dfm_x)
+            with torch.no_grad():
+                dfm_logits = deepfm.forward_logits(dfm_x)[0].float().cpu()
+            line["cpu_baseline"] = cpu_baseline_deepfm(args, dst, dfm_x, dfm_logits)
             line["gpu_over_cpu"] = round(line["value"] / line["cpu_baseline"]["value"], 1)
             if not args.no_rerank:
                 line = result["secondary_retrieve_rerank"]
@@ -1113,11 +1256,11 @@ def main():
         result["secondary_item_refresh"] = bench_item_refresh(args, device)
         result["secondary_hnm"] = bench_hnm(args, device)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args, items, cfg, args.batch, args.seed + 100)
+        result["cpu_baseline"] = cpu_baseline(args, items, cfg, args.batch, args.seed + 100, device)
         result["gpu_over_cpu"] = round(result["value"] / result["cpu_baseline"]["value"], 1)
         if "secondary_batch4096" in result:       # configs[1]: the same step at 4,096 users
             line = result["secondary_batch4096"]
-            line["cpu_baseline"] = cpu_baseline(args, items, cfg, 4096, args.seed + 100)
+            line["cpu_baseline"] = cpu_baseline(args, items, cfg, 4096, args.seed + 100, device)
             line["gpu_over_cpu"] = round(line["value"] / line["cpu_baseline"]["value"], 1)
         if "strong_32768" in result:
             result["strong_32768"]["cpu_baseline"] = None

@@ -29,6 +29,9 @@ extern "C" {
 const char* rsx_last_error(void);
 int rsx_abi_version(void);
 const char* rsx_target_arch(void);
+/* sha256 (first 16 hex digits) of the sources the library was built from (csrc/Makefile: the .hip
+ * files sorted by name, rsx_common.h, this header): a caller can tell a stale prebuilt binary. */
+const char* rsx_build_hash(void);
 
 /* ---- A2: SASRecUserTower embedding stage --------------------------------------------
  * Replaces tower_code/v1_refine_usertower.py:434-459:
@@ -152,9 +155,16 @@ int rsx_nce_bwd_x3(const float* A, const float* B, const float* bias, const int*
  * precision: RSX_NCE_FP32 (0) = logits on the fp32-input MFMA (exact fp32 products);
  *            RSX_NCE_BF16X3 (1) = logits as hi*hi + hi*lo + lo*hi of a bf16 hi/lo split
  *            (fp32 accumulate, max |dot error| ~3e-6 on unit vectors), 5.3x fewer MFMA cycles;
- *            the gradient products (dS x rows) use the same split. */
+ *            the gradient products (dS x rows) use the same split;
+ *            RSX_NCE_F16 (2) = in the fused forward and the column pass: logits as the same three
+ *            products of an fp16 hi/lo split of x * 2^8 on the fp16 MFMA (~2^-22 relative per term,
+ *            tighter than bf16x3), gradient products as ONE fp16 MFMA of the rounded softmax weights
+ *            and the rows' fp16 hi image (the reference's autocast(float16) arithmetic for these
+ *            products, v1_usertower_train.py:787, with fp32 accumulation; RSX_NCE_F16_GP=2 adds the
+ *            lo image); elsewhere (rsx_nce_grouped_fwd, the row pass) as RSX_NCE_BF16X3. */
 #define RSX_NCE_FP32 0
 #define RSX_NCE_BF16X3 1
+#define RSX_NCE_F16 2
 /* ws for the grouped pair: >= rsx_nce_grouped_workspace_floats(N, D, nsplit_fwd, 8, precision)
  * (bf16x3 adds the hi/lo bf16 images of A and B; the forward writes B's, the backward's
  * column pass A's). The grouped backward's nsplit is 8. */
@@ -163,7 +173,7 @@ int rsx_nce_grouped_fwd(const float* A, const float* B, const float* bias, const
                         const int* row_beg, const int* row_end, const int* exc_cols, int64_t N, int64_t D,
                         int64_t lda, int64_t ldb, float tau, int precision, int nsplit, float* ws, float* out2,
                         void* stream);
-/* Forward fused with the row-side gradient (bf16x3 only): same loss as rsx_nce_grouped_fwd
+/* Forward fused with the row-side gradient (precision RSX_NCE_BF16X3 or RSX_NCE_F16): same loss as rsx_nce_grouped_fwd
  * (out2, and lse in ws for a later column pass), plus ga [N][128] = d(sum of row losses)/dA
  * per unit upstream gradient, i.e. dA = gout * ga. The row gradient is a softmax-weighted sum
  * of B's rows (an attention output), accumulated in the same sweep over S as the loss, so the
@@ -172,8 +182,8 @@ int rsx_nce_grouped_fwd(const float* A, const float* B, const float* bias, const
  * (tower_code/v1_usertower_train.py:787-845) plus the row half of its autograd backward. */
 int rsx_nce_grouped_fwd_grad(const float* A, const float* B, const float* bias, const float* colcnt,
                              const int* row_col, const int* row_beg, const int* row_end, const int* exc_cols,
-                             int64_t N, int64_t D, int64_t lda, int64_t ldb, float tau, int nsplit, float* ws,
-                             float* out2, float* ga, void* stream);
+                             int64_t N, int64_t D, int64_t lda, int64_t ldb, float tau, int precision, int nsplit,
+                             float* ws, float* out2, float* ga, void* stream);
 /* Measurement hooks (no reference counterpart; bench.py's roofline): while enabled,
  * rsx_nce_grouped_fwd_grad brackets the fused forward kernel's own launch (not the B split or the
  * merge) with two HIP events on its stream; rsx_kernel_events_read waits for them and writes up to
@@ -214,7 +224,8 @@ int rsx_static_embed_bwd(const int64_t* const* ids, const float* const* tables, 
  * Backward: ds_out = LN-backward(dy) + ds_in (ds_in nullable), dres = dropout-backward(ds_out),
  * dw/db via per-block partials (ws >= rsx_ln_bwd_workspace_floats). D in {64, 128, 256}; the
  * forward also takes D in {512, 768, 1024} (the item tower's BERT LayerNorms, item_tower.py:175,
- * inference: rsx_ln_bwd stays at D <= 256). */
+ * inference: rsx_ln_bwd stays at D <= 256). rsx_ln_bwd_workspace_floats returns -1 for a D that
+ * rsx_ln_bwd does not accept. */
 int rsx_ln_fwd(const float* x, const float* res, float p_drop, uint64_t seed, const float* w, const float* b,
                float eps, int act, int64_t T, int64_t D, float* sum_out, float* y, float* mean, float* rstd,
                void* stream);
@@ -462,7 +473,10 @@ int rsx_loss_combine_bwd(const float* g, const float* cnt, float inv_n, float in
  * dim[ntab], padding_idx[ntab]} with sum(dim) + P == K <= 128, C == 4, P == 16; the ids and cont
  * hold src rows and output row r reads input row r % src (U % src == 0: the contrastive step's two
  * dropout views share their users' inputs, so they are not duplicated). arena:
- * rsx_static_profile_arena_bytes(U), written by the forward and read by the backward.
+ * rsx_static_profile_arena_bytes(U), written by the forward and read by the backward; its first
+ * int32 is an error flag the forward sets when an id lies outside [0, rows_j) (nn.Embedding's
+ * IndexError: such an id reads row 0 and the backward scatters to row 0, never out of bounds; the
+ * caller raises on the flag, ops.py _StaticProfile).
  * Backward: grads[] parallel to p[] (the ids' and cont's slots unused), every gradient WRITTEN
  * (padding rows 0); U > 0; ws: rsx_static_profile_bwd_workspace_bytes(U). Dropout mask
  * hash(seed, row * 128 + col). */

@@ -24,13 +24,14 @@ c_i = ctypes.c_int
 c_f = ctypes.c_float
 c_u64 = ctypes.c_uint64
 
-ABI_VERSION = 4  # rsx_abi_version() of the library these signatures describe
+ABI_VERSION = 5  # rsx_abi_version() of the library these signatures describe
 
 # name -> (restype, argtypes)
 _SIGS = {
     "rsx_last_error": (ctypes.c_char_p, []),
     "rsx_abi_version": (c_i, []),
     "rsx_target_arch": (ctypes.c_char_p, []),
+    "rsx_build_hash": (ctypes.c_char_p, []),
     "rsx_seq_embed_fwd": (c_i, [c_p, c_p, c_p, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_i64, c_i64, c_i64, c_f, c_u64,
                                 c_p, c_p, c_p, c_p]),
     "rsx_seq_embed_bwd_workspace_floats": (c_i64, [c_i64, c_i64, c_i64]),
@@ -57,7 +58,7 @@ _SIGS = {
     "rsx_kernel_events": (c_i, [c_i]),
     "rsx_kernel_events_read": (c_i, [c_p, c_i]),
     "rsx_nce_grouped_fwd_grad": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_f, c_i,
-                                       c_p, c_p, c_p, c_p]),
+                                       c_i, c_p, c_p, c_p, c_p]),
     "rsx_nce_grouped_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64,
                                   c_i64, c_i64, c_f, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_i, c_p]),
     "rsx_deepfm_embed": (c_i, [c_p, c_i64, c_i, c_i, c_p, c_p, c_f, c_p, c_p, c_p]),
@@ -153,6 +154,30 @@ def load(path: str = LIB_PATH):
 
 def lib():
     return _lib if _lib is not None else load()
+
+
+def source_hash() -> str:
+    """sha256 (first 16 hex digits) of the library's sources in this tree, in csrc/Makefile's order
+    (the .hip files sorted by name, rsx_common.h, include/recsys_amd.h): equal to
+    rsx_build_hash() of a library built from them."""
+    import glob
+    import hashlib
+    csrc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc")
+    files = sorted(glob.glob(os.path.join(csrc, "*.hip")), key=lambda f: os.path.basename(f).encode())
+    files += [os.path.join(csrc, "rsx_common.h"),
+              os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "recsys_amd.h")]
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def build_info() -> dict:
+    """The loaded library's source stamp against this tree's sources (fresh = built from them)."""
+    built = lib().rsx_build_hash().decode()
+    src = source_hash()
+    return {"lib_hash": built, "src_hash": src, "fresh": built == src}
 
 
 def check(rc: int, what: str = "") -> None:

@@ -38,7 +38,7 @@ constexpr int kOwnRows = 32 * kWaves;  // owner rows per workgroup
 constexpr int kLdsStride = kD + 4;     // padded row (conflict-free ds_read_b128 columns)
 
 enum : int { F_EXCL_DIAG = 1, F_MASK_K1 = 2, F_MASK_K2 = 4, F_POS = 8 };
-enum : int { RSX_NCE_FP32 = 0, RSX_NCE_BF16X3 = 1 };
+enum : int { RSX_NCE_FP32 = 0, RSX_NCE_BF16X3 = 1, RSX_NCE_F16 = 2 };
 constexpr int kNsplitBwdGrouped = 8;  // fixed: the image region's offset in ws depends on it  // logit/gradient precision of the grouped kernels
 
 struct FwdArgs {
@@ -2555,6 +2555,556 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void nce_grouped_fwdg_x3p_k(GArgs 
   }
 }
 
+// =====================================================================================
+// fp16 form of the fused forward and the column pass (precision RSX_NCE_F16).
+// Logits: every operand is split into fp16 hi + lo of x * 2^8 (unit-vector components scaled into
+// fp16's normal range; lo carries the next 11 bits), S = hi*hi' + hi*lo' + lo*hi' on
+// v_mfma_f32_32x32x16_f16 with fp32 accumulation: |dot error| ~2^-22 relative per term, tighter
+// than bf16x3 (2^-16) at the same MFMA count; the 2^16 product scale is folded into 1/tau.
+// Gradient products (the softmax weights G against the streamed rows): G rounded to fp16 once and
+// multiplied by the rows' fp16 hi image (GP = 1: one MFMA per k-step instead of three) or by hi and
+// lo (GP = 2: only G's rounding, 2^-11 relative per weight). This is the reference's own GPU
+// arithmetic for these products (autocast(float16), v1_usertower_train.py:787) with fp32
+// accumulation; the gradient scales (the 2^8 row scale, the column pass's per-owner factor and
+// its 2^14 weight scale) are applied to the fp32 accumulators after the sweep.
+// The images keep the bf16x3 layout and LDS tiles (16-bit containers: bf16x8 vectors carry fp16
+// bits and are bit-cast at the MFMA).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+constexpr float kHScale = 256.0f;         // operand scale 2^8
+constexpr float kHUnscale = 1.0f / 256.0f;
+constexpr float kHS2 = 1.0f / 65536.0f;   // S product scale 2^-16
+constexpr float kHGS = 14.0f;             // column pass: G weights scaled by 2^14 (<= 16384)
+
+__device__ __forceinline__ f32x16 mfma_h(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+                                                0);
+}
+
+__device__ __forceinline__ uint32_t pack_h(float a, float b) {
+  const f16x2 v = {(_Float16)a, (_Float16)b};
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+__device__ __forceinline__ void split8_h(const float4& a, const float4& b, bf16x8& h, bf16x8& l) {
+  const float f[8] = {a.x * kHScale, a.y * kHScale, a.z * kHScale, a.w * kHScale,
+                      b.x * kHScale, b.y * kHScale, b.z * kHScale, b.w * kHScale};
+  f16x8 hv, lv;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const _Float16 hk = (_Float16)f[k];
+    hv[k] = hk;
+    lv[k] = (_Float16)(f[k] - (float)hk);
+  }
+  h = __builtin_bit_cast(bf16x8, hv);
+  l = __builtin_bit_cast(bf16x8, lv);
+}
+
+__device__ __forceinline__ void load_owner_h(bf16x8 (&uh)[8], bf16x8 (&ul)[8], const float* base, int64_t row,
+                                             int64_t ld, bool ok, int h) {
+  const float4* src = reinterpret_cast<const float4*>(base + (ok ? row : 0) * ld + h * 64);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
+    if (ok) {
+      v0 = src[2 * s];
+      v1 = src[2 * s + 1];
+    }
+    split8_h(v0, v1, uh[s], ul[s]);
+  }
+}
+
+// rows x 128 fp32 -> fp16 hi/lo images of x * 2^8 (nce_split_k's layout)
+__global__ __launch_bounds__(256) void nce_split_h_k(const float* src, int64_t ld, int64_t rows, __bf16* hi,
+                                                     __bf16* lo) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * (kD / 8)) return;
+  const int64_t r = i / (kD / 8), c8 = i % (kD / 8);
+  const float4* p = reinterpret_cast<const float4*>(src + r * ld + c8 * 8);
+  bf16x8 h, l;
+  split8_h(p[0], p[1], h, l);
+  *reinterpret_cast<bf16x8*>(hi + r * kD + c8 * 8) = h;
+  *reinterpret_cast<bf16x8*>(lo + r * kD + c8 * 8) = l;
+}
+
+// S tile (dots_x3 on the fp16 MFMA): acc[r] = 2^16 <streamed row tile_row(r,h), owner row c>
+__device__ __forceinline__ f32x16 dots_h3(const X3Tile& t, int c, int h, const bf16x8 (&uh)[8],
+                                          const bf16x8 (&ul)[8]) {
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+  const int base = img_off(c, 64 * h);
+  bf16x8 ah = *reinterpret_cast<const bf16x8*>(&t.hi[base]);
+  bf16x8 al = *reinterpret_cast<const bf16x8*>(&t.lo[base]);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    bf16x8 nh = ah, nl = al;
+    if (s < 7) {
+      nh = *reinterpret_cast<const bf16x8*>(&t.hi[base + 8 * (s + 1)]);
+      nl = *reinterpret_cast<const bf16x8*>(&t.lo[base + 8 * (s + 1)]);
+    }
+    acc = mfma_h(al, uh[s], acc);
+    acc = mfma_h(ah, ul[s], acc);
+    acc = mfma_h(ah, uh[s], acc);
+    __builtin_amdgcn_sched_barrier(0);
+    ah = nh;
+    al = nl;
+  }
+  return acc;
+}
+
+// g = 2^(x - m) for a pair, summed into sum (fp32, before rounding) and packed as two fp16
+__device__ __forceinline__ void exp_h_pair(float a, float b, float m, uint32_t& og, f32x2& sum) {
+  f32x2 v = {a, b};
+  const f32x2 mm = {m, m};
+  v = v - mm;
+  v.x = __builtin_amdgcn_exp2f(v.x);
+  v.y = __builtin_amdgcn_exp2f(v.y);
+  sum = sum + v;
+  og = pack_h(v.x, v.y);
+}
+
+// grad_half_x3 in fp16: gacc[nb] += G_ks^T X over tile t (nb = 0..3, ks fixed), G one fp16
+// fragment; X the streamed rows' hi image (GP = 2: + lo). WORK: the exp / pack of G pair nb of
+// half xh of the next operand placed under step nb's MFMAs.
+template <bool WORK, int GP>
+__device__ __forceinline__ void grad_half_h(f32x16 (&gacc)[4], const bf16x8& g, const X3Tile& t, int base, int ks,
+                                            const f32x16& x, int xh, float m, uint32_t (&og)[4], f32x2& sum) {
+  bf16x8 bh, bl;
+  grad_rd(t.hi, base, ks, 0, bh);
+  if (GP == 2) grad_rd(t.lo, base, ks, 0, bl);
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) {
+    bf16x8 nh = bh, nl = bl;
+    if (nb < 3) {
+      grad_rd(t.hi, base, ks, nb + 1, nh);
+      if (GP == 2) grad_rd(t.lo, base, ks, nb + 1, nl);
+    }
+    if (GP == 2) gacc[nb] = mfma_h(g, bl, gacc[nb]);
+    gacc[nb] = mfma_h(g, bh, gacc[nb]);
+    if (WORK) {
+      exp_h_pair(x[8 * xh + 2 * nb], x[8 * xh + 2 * nb + 1], m, og[nb], sum);
+      asm volatile("" : "+v"(og[nb]));  // pins the work to this step (no sinking)
+      __builtin_amdgcn_sched_group_barrier(0x100, 2 * GP, 0);  // next step's transposed reads
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+      if (GP == 2) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    bh = nh;
+    bl = nl;
+  }
+}
+
+// The fused forward (nce_grouped_fwdg_x3p_k's pipeline: 3-slot LDS ring, k-step 1 of each tile's
+// gradient product deferred to the next iteration, lazy running max) on the fp16 products.
+template <int GP>
+__global__ __launch_bounds__(256, 2) void nce_grouped_fwdg_h_k(GArgs a) {
+  constexpr int NW = 4, kRows = 32 * NW;
+  __shared__ __attribute__((aligned(16))) X3Tile sT[3];
+  __shared__ __attribute__((aligned(16))) float sB2[3][kTile];
+  __shared__ __attribute__((aligned(16))) float sCnt[3][kTile];
+  __shared__ __attribute__((aligned(16))) float sAlpha[NW][32];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, c = lane & 31;
+  int split;
+  int64_t rb, j_begin, j_end;
+  fwdg_geometry(a, split, rb, j_begin, j_end);
+  const int64_t i = rb * kRows + wave * 32 + c;
+  const bool row_ok = i < a.N;
+  bf16x8 uh[8], ul[8];
+  load_owner_h(uh, ul, a.A, i, a.lda, row_ok, h);
+  constexpr int kNone = 0x7fffffff;
+  int di = -1, p = 0, e = 0, next = kNone;
+  if (row_ok) {
+    di = a.row_col[i];
+    p = a.row_beg[i];
+    e = a.row_end[i];
+    p = lower_bound_i(a.exc_cols, p, e, j_begin);
+    next = (p < e) ? a.exc_cols[p] : kNone;
+  }
+  const float it2 = a.inv_tau * kLog2e * kHS2;
+  float m = -INFINITY, l = 0.0f;
+  f32x16 gacc[4];
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) gacc[kb][r] = 0.0f;
+  X3StageT<NW> stg;
+  float stg_b = 0.0f, stg_c = 0.0f;
+  auto gload = [&](int64_t j0) {
+    const int64_t j = j0 + ((tid >> 3) & 31);
+    stg.load(a.bhi, a.blo, j, j < j_end, tid);
+    if (tid < kTile) {
+      const int64_t jj = j0 + tid;
+      const bool ok = jj < j_end;
+      stg_b = ok ? (a.bias ? a.bias[jj] : 0.0f) : INFINITY;
+      stg_c = ok ? a.colcnt[jj] : 0.0f;
+    }
+  };
+  auto lstore = [&](int buf) {
+    stg.store(sT[buf], tid);
+    if (tid < kTile) {
+      sB2[buf][tid] = -(stg_b * kLog2e) + __log2f(stg_c);
+      sCnt[buf][tid] = stg_c;
+    }
+  };
+  if (j_begin < j_end) {
+    gload(j_begin);
+    lstore(0);
+    __syncthreads();
+    int cur = 0, prev = 0;
+    bf16x8 pg;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) pg[k] = (__bf16)0.0f;  // zero bits = fp16 zero
+    const int gbase = grad_lane_base(lane);
+    for (int64_t j0 = j_begin; j0 < j_end; j0 += kTile) {
+      const bool has_next = j0 + kTile < j_end;
+      const bool exc = (int64_t)next < j0 + kTile;
+      if (has_next) gload(j0 + kTile);
+      f32x16 acc = dots_h3(sT[cur], c, h, uh, ul);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 nb = *reinterpret_cast<const float4*>(&sB2[cur][8 * g + 4 * h]);
+        acc[4 * g + 0] = fmaf(acc[4 * g + 0], it2, nb.x);
+        acc[4 * g + 1] = fmaf(acc[4 * g + 1], it2, nb.y);
+        acc[4 * g + 2] = fmaf(acc[4 * g + 2], it2, nb.z);
+        acc[4 * g + 3] = fmaf(acc[4 * g + 3], it2, nb.w);
+      }
+      if (exc) {
+        int q = p;
+        while (q < e && (int64_t)a.exc_cols[q] < j0 + kTile) ++q;
+        float n[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) n[r] = 0.0f;
+        for (int k = p; k < q; ++k) {
+          const int tk = (int)(a.exc_cols[k] - j0);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) n[r] += (tk == tile_row(r, h)) ? 1.0f : 0.0f;
+        }
+        const int tl = ((int64_t)di < j_end) ? (int)(di - j0) : -1;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 cw = *reinterpret_cast<const float4*>(&sCnt[cur][8 * g + 4 * h]);
+          const float cv[4] = {cw.x, cw.y, cw.z, cw.w};
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int r = 4 * g + t;
+            const float wn = (tile_row(r, h) == tl) ? 1.0f : cv[t] - n[r];
+            if (wn != cv[t]) acc[r] = (wn > 0.0f) ? acc[r] + __log2f(wn / cv[t]) : -INFINITY;
+          }
+        }
+        p = q;
+        next = (p < e) ? a.exc_cols[p] : kNone;
+      }
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, acc[r]);
+      {
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(tmax), __float_as_uint(tmax), false, false);
+        tmax = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+      }
+      if (!row_ok) tmax = -INFINITY;
+      const bool raise = tmax > m + kLazyLog2;
+      if (__any(raise)) {
+        {
+          uint32_t dg[4];
+          f32x2 ds = {0.0f, 0.0f};
+          grad_half_h<false, GP>(gacc, pg, sT[prev], gbase, 1, acc, 0, 0.0f, dg, ds);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) pg[k] = (__bf16)0.0f;
+        }
+        const float alpha = raise ? ((m == -INFINITY) ? 0.0f : __builtin_amdgcn_exp2f(m - tmax)) : 1.0f;
+        if (raise) {
+          l *= alpha;
+          m = tmax;
+        }
+        if (h == 0) sAlpha[wave][c] = alpha;
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float al = sAlpha[wave][tile_row(r, h)];
+#pragma unroll
+          for (int kb = 0; kb < 4; ++kb) gacc[kb][r] *= al;
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+      const float ms = (m == -INFINITY) ? 0.0f : m;
+      uint32_t g0[4], g1[4];
+      f32x2 sum = {0.0f, 0.0f};
+      grad_half_h<true, GP>(gacc, pg, sT[prev], gbase, 1, acc, 0, ms, g0, sum);
+      const u32x4 g0v = {g0[0], g0[1], g0[2], g0[3]};
+      grad_half_h<true, GP>(gacc, __builtin_bit_cast(bf16x8, g0v), sT[cur], gbase, 0, acc, 1, ms, g1, sum);
+      l += sum.x + sum.y;
+      const u32x4 g1v = {g1[0], g1[1], g1[2], g1[3]};
+      pg = __builtin_bit_cast(bf16x8, g1v);
+      prev = cur;
+      const int nxt = (cur == 2) ? 0 : cur + 1;
+      if (has_next) lstore(nxt);
+      __builtin_amdgcn_s_waitcnt(kVmcnt0);
+      __syncthreads();
+      cur = nxt;
+    }
+    {
+      uint32_t dg[4];
+      f32x2 ds = {0.0f, 0.0f};
+      f32x16 z;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) z[r] = 0.0f;
+      grad_half_h<false, GP>(gacc, pg, sT[prev], gbase, 1, z, 0, 0.0f, dg, ds);
+    }
+  }
+  const float lt = l + __shfl_xor(l, 32, 64);
+  if (h == 0 && row_ok) {
+    const int64_t stride = (int64_t)a.nslots * a.N;
+    const int64_t o = (int64_t)split * a.N + i;
+    a.part[o] = (m == -INFINITY) ? -INFINITY : m * kLn2;
+    a.part[stride + o] = lt;
+    a.part[2 * stride + o] = 0.0f;
+    a.part[3 * stride + o] = 0.0f;
+  }
+  const int64_t own_base = rb * kRows + wave * 32;
+  float* dst = a.dout + (int64_t)split * a.N * kD;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int64_t orow = own_base + tile_row(r, h);
+    if (orow < a.N) {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) dst[orow * kD + kb * 32 + c] = gacc[kb][r] * kHUnscale;
+    }
+  }
+}
+
+// k-step ks of the column pass's gradient product in fp16, gacc[nb] += G'_ks^T X, with (WORK) the
+// next k-step's G' pair nb: g' = 2^(S it2 - (m0 + o_m2) + 14) (the owner factor fo applied after
+// the sweep)
+template <bool WORK, int GP>
+__device__ __forceinline__ void grad_half_gh(f32x16 (&gacc)[4], const bf16x8& g, const X3Tile& t, int base, int ks,
+                                             const f32x16& S, int h, const float* m0, float o_m2s, float it2,
+                                             uint32_t (&og)[4]) {
+  bf16x8 bh, bl;
+  grad_rd(t.hi, base, ks, 0, bh);
+  if (GP == 2) grad_rd(t.lo, base, ks, 0, bl);
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) {
+    bf16x8 nh = bh, nl = bl;
+    if (nb < 3) {
+      grad_rd(t.hi, base, ks, nb + 1, nh);
+      if (GP == 2) grad_rd(t.lo, base, ks, nb + 1, nl);
+    }
+    if (GP == 2) gacc[nb] = mfma_h(g, bl, gacc[nb]);
+    gacc[nb] = mfma_h(g, bh, gacc[nb]);
+    if (WORK) {
+      const int pp = 4 + nb;  // rows 2pp, 2pp+1
+      const f32x4 q0 = *reinterpret_cast<const f32x4*>(m0 + 8 * (pp >> 1) + 4 * h);
+      float gp[2];
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr) {
+        const int r = 2 * pp + rr, e = r & 3;
+        gp[rr] = __builtin_amdgcn_exp2f(fmaf(S[r], it2, -(q0[e] + o_m2s)));
+      }
+      og[nb] = pack_h(gp[0], gp[1]);
+      asm volatile("" : "+v"(og[nb]));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    bh = nh;
+    bl = nl;
+  }
+}
+
+// exception-tile form (grad_x3s on fp16): the 16 G' values in registers -> two fp16 fragments,
+// then the eight (ks, nb) steps, software-pipelined by one
+template <int GP>
+__device__ __forceinline__ void grad_tile_h(f32x16 (&gacc)[4], const f32x16& G, const X3Tile& t, int base) {
+  bf16x8 gf[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    u32x4 v;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = pack_h(G[8 * ks + 2 * q], G[8 * ks + 2 * q + 1]);
+    gf[ks] = __builtin_bit_cast(bf16x8, v);
+  }
+  bf16x8 bh, bl;
+  grad_rd(t.hi, base, 0, 0, bh);
+  if (GP == 2) grad_rd(t.lo, base, 0, 0, bl);
+#pragma unroll
+  for (int step = 0; step < 8; ++step) {
+    bf16x8 nh = bh, nl = bl;
+    if (step < 7) {
+      grad_rd(t.hi, base, (step + 1) >> 2, (step + 1) & 3, nh);
+      if (GP == 2) grad_rd(t.lo, base, (step + 1) >> 2, (step + 1) & 3, nl);
+    }
+    const int ks = step >> 2, nb = step & 3;
+    if (GP == 2) gacc[nb] = mfma_h(gf[ks], bl, gacc[nb]);
+    gacc[nb] = mfma_h(gf[ks], bh, gacc[nb]);
+    __builtin_amdgcn_sched_barrier(0);
+    bh = nh;
+    bl = nl;
+  }
+}
+
+// Column pass of the grouped backward (nce_grouped_bwd_x3_k<false, true>'s structure) on the fp16
+// products: owner = distinct target column o (registers), streamed = user rows (A's fp16 images).
+template <int GP>
+__global__ __launch_bounds__(256, 2) void nce_grouped_bwd_cols_h_k(GArgs a) {
+  __shared__ __attribute__((aligned(16))) X3Tile sT[2];
+  __shared__ __attribute__((aligned(16))) float sM0[2][kTile];  // lse_i * log2e (+inf past the split)
+  __shared__ __attribute__((aligned(16))) int sM2[2][kTile];    // d(i)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, c = lane & 31;
+  int split, ob;
+  const int64_t n_own = a.M, n_str = a.N;
+  if (a.split_major) {
+    const int b = blockIdx.x, xcd = b & 7, q = b >> 3;
+    const int nob = (int)((n_own + kOwnRows - 1) / kOwnRows);
+    split = xcd + 8 * (q / nob);
+    ob = q % nob;
+  } else {
+    remap_block(a.nsplit, split, ob);
+  }
+  const float gs = a.gout[0] * a.inv_tau;
+  const float it2 = a.inv_tau * kLog2e * kHS2;
+  const int64_t o = (int64_t)ob * kOwnRows + wave * 32 + c;
+  const bool own_ok = o < n_own;
+  bf16x8 uh[8], ul[8];
+  load_owner_h(uh, ul, a.B, o, a.ldb, own_ok, h);
+  const int64_t s_begin = (int64_t)split * a.span;
+  int64_t s_end = s_begin + a.span;
+  if (s_end > n_str) s_end = n_str;
+  constexpr int kNone = 0x7fffffff;
+  float o_m2 = 0.0f, o_cnt = 0.0f;
+  int p = 0, e = 0;
+  if (own_ok) {
+    o_m2 = a.bias ? a.bias[o] * kLog2e : 0.0f;
+    o_cnt = a.colcnt[o];
+    p = a.col_beg[o];
+    e = a.col_end[o];
+    p = lower_bound_i(a.exc_e, p, e, s_begin + 1);
+  }
+  const float o_m2s = o_m2 - kHGS;                                   // the 2^14 weight scale
+  const float fo = own_ok ? gs * o_cnt : 0.0f;                       // applied after the sweep
+  const float inv_cnt = (own_ok && o_cnt > 0.0f) ? 1.0f / o_cnt : 0.0f;  // exception tiles' G' = g / c_o
+  int q = p, e_first = 0, s_next = kNone;
+  if (own_ok && q < e) s_next = a.exc_s[q];
+
+  f32x16 gacc[4];
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) gacc[kb][r] = 0.0f;
+
+  X3Stage stg;
+  float stg0 = 0.0f;
+  int stg2 = 0;
+  auto gload = [&](int64_t s0) {
+    const int64_t sidx = s0 + (tid >> 3);
+    stg.load(a.ahi, a.alo, sidx, sidx < s_end, tid);
+    if (tid < kTile) {
+      const int64_t ss = s0 + tid;
+      const bool ok = ss < s_end;
+      stg0 = ok ? a.lse[ss] : INFINITY;
+      stg2 = ok ? a.row_col[ss] : -2;
+    }
+  };
+  auto lstore = [&](int buf) {
+    stg.store(sT[buf], tid);
+    if (tid < kTile) {
+      sM0[buf][tid] = stg0 * kLog2e;
+      sM2[buf][tid] = stg2;
+    }
+  };
+  auto exc_flag = [&](int64_t s0) -> bool {
+    while (p < q && (int64_t)e_first <= s0) {
+      ++p;
+      if (p < q) e_first = a.exc_e[p];
+    }
+    while ((int64_t)s_next < s0 + kTile) {
+      if (p == q) e_first = a.exc_e[q];
+      ++q;
+      s_next = (q < e) ? a.exc_s[q] : kNone;
+    }
+    return q != p;
+  };
+
+  if (s_begin < s_end) {
+    const int ntile = (int)((s_end - s_begin + kTile - 1) / kTile);
+    gload(s_begin);
+    lstore(0);
+    __syncthreads();
+    int cur = 0;
+    const int gbase = grad_lane_base(lane);
+    for (int t = 0; t < ntile; ++t) {
+      const int64_t s0 = s_begin + (int64_t)t * kTile;
+      const bool has_next = t + 1 < ntile;
+      const bool exc = exc_flag(s0);
+      if (has_next) gload(s0 + kTile);
+      f32x16 acc = dots_h3(sT[cur], c, h, uh, ul);
+      if (__any(exc)) {
+        float n[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) n[r] = 0.0f;
+        if (exc) {
+          for (int k = p; k < q; ++k) {
+            const int ks = (int)(a.exc_s[k] - s0), ke = (int)(a.exc_e[k] - s0);
+            const float nk = (float)a.exc_n[k];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) n[r] += (tile_row(r, h) >= ks && tile_row(r, h) < ke) ? nk : 0.0f;
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int tr = tile_row(r, h);
+          const float x = fmaf(acc[r], it2, -(sM0[cur][tr] + o_m2));
+          const bool lab = exc && sM2[cur][tr] == (int)o;
+          const float wr = lab ? 1.0f : o_cnt - n[r];
+          const float g = (wr > 0.0f ? wr * __builtin_amdgcn_exp2f(x) : 0.0f) - (lab ? 1.0f : 0.0f);
+          acc[r] = g * inv_cnt * 16384.0f;  // G' = 2^14 g / c_o
+        }
+        grad_tile_h<GP>(gacc, acc, sT[cur], gbase);
+      } else {
+        // G' rows of k-step 0, then k-step 0's product with k-step 1's rows under its MFMAs
+        u32x4 g0;
+#pragma unroll
+        for (int pp = 0; pp < 4; ++pp) {
+          const f32x4 q0 = *reinterpret_cast<const f32x4*>(&sM0[cur][8 * (pp >> 1) + 4 * h]);
+          float gp[2];
+#pragma unroll
+          for (int rr = 0; rr < 2; ++rr) {
+            const int r = 2 * pp + rr, ee = r & 3;
+            gp[rr] = __builtin_amdgcn_exp2f(fmaf(acc[r], it2, -(q0[ee] + o_m2s)));
+          }
+          g0[pp] = pack_h(gp[0], gp[1]);
+        }
+        uint32_t g1[4];
+        grad_half_gh<true, GP>(gacc, __builtin_bit_cast(bf16x8, g0), sT[cur], gbase, 0, acc, h, sM0[cur], o_m2s, it2,
+                               g1);
+        const u32x4 g1v = {g1[0], g1[1], g1[2], g1[3]};
+        grad_half_gh<false, GP>(gacc, __builtin_bit_cast(bf16x8, g1v), sT[cur], gbase, 1, acc, h, sM0[cur], o_m2s,
+                                it2, g1);
+      }
+      if (has_next) lstore(cur ^ 1);
+      __builtin_amdgcn_s_waitcnt(kVmcnt0);
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+  const int64_t own_base = (int64_t)ob * kOwnRows + wave * 32;
+  float* dst = a.dout + (int64_t)split * n_own * kD;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int tr = tile_row(r, h);
+    const float f = __shfl(fo, tr, 64) * (kHUnscale / 16384.0f);  // owner tr's factor, 2^-8 row scale, 2^-14
+    const int64_t orow = own_base + tr;
+    if (orow < n_own) {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) dst[orow * kD + kb * 32 + c] = gacc[kb][r] * f;
+    }
+  }
+}
+
 // merge of the fused forward: lse / row loss as nce_grouped_merge_k, plus the row gradient
 // per unit upstream gradient  ga_i = (sum_s O_s e^(m_s - M) / sum_s l_s e^(m_s - M) - B_d(i)) / tau
 __global__ __launch_bounds__(256) void nce_grouped_merge_g_k(const float* A, const float* B, const float* bias,
@@ -2624,7 +3174,7 @@ RSX_API int64_t rsx_nce_workspace_floats(int64_t N, int64_t M, int nsplit_fwd, i
 RSX_API int64_t rsx_nce_grouped_workspace_floats(int64_t N, int64_t D, int nsplit_fwd, int nsplit_bwd,
                                                  int precision) {
   const int64_t base = (rsx_nce_workspace_floats(N, D, nsplit_fwd, nsplit_bwd) + 63) / 64 * 64;
-  return base + (precision == RSX_NCE_BF16X3 ? (N + D) * kD + 64 : 0);
+  return base + (precision != RSX_NCE_FP32 ? (N + D) * kD + 64 : 0);
 }
 
 namespace {
@@ -2644,6 +3194,20 @@ Images grouped_images(float* ws, int64_t N, int64_t D, int nsplit_fwd, int nspli
 void launch_split(const float* src, int64_t ld, int64_t rows, __bf16* hi, __bf16* lo, hipStream_t st) {
   const int64_t n = rows * (kD / 8);
   if (n > 0) hipLaunchKernelGGL(nce_split_k, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, src, ld, rows, hi, lo);
+}
+// the fp16 images of RSX_NCE_F16 (x * 2^8, hi + lo)
+void launch_split_h(const float* src, int64_t ld, int64_t rows, __bf16* hi, __bf16* lo, hipStream_t st) {
+  const int64_t n = rows * (kD / 8);
+  if (n > 0)
+    hipLaunchKernelGGL(nce_split_h_k, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, src, ld, rows, hi, lo);
+}
+// RSX_NCE_F16_GP = 1 | 2: MFMAs per gradient-product k-step in the fp16 kernels (default 1)
+int f16_gp() {
+  static const int v = [] {
+    const char* e = getenv("RSX_NCE_F16_GP");
+    return (e && e[0] == '2') ? 2 : 1;
+  }();
+  return v;
 }
 }  // namespace
 
@@ -2935,7 +3499,11 @@ RSX_API int rsx_nce_grouped_fwd(const float* A, const float* B, const float* bia
                                 int64_t N, int64_t D, int64_t lda, int64_t ldb, float tau, int precision, int nsplit,
                                 float* ws, float* out2, void* stream) {
   RSX_ARG(A && B && colcnt && row_col && row_beg && row_end && exc_cols && ws && out2, "null tensor");
-  RSX_ARG(precision == RSX_NCE_FP32 || precision == RSX_NCE_BF16X3, "precision must be 0 (fp32) or 1 (bf16x3)");
+  RSX_ARG(precision == RSX_NCE_FP32 || precision == RSX_NCE_BF16X3 || precision == RSX_NCE_F16,
+          "precision must be 0 (fp32), 1 (bf16x3) or 2 (f16)");
+  // the loss alone has no gradient product: RSX_NCE_F16 runs the bf16x3 logits here (its B
+  // images are bf16, which is what a following row pass of rsx_nce_grouped_bwd reads)
+  if (precision == RSX_NCE_F16) precision = RSX_NCE_BF16X3;
   RSX_ARG(nsplit == 1 || nsplit == 2 || nsplit == 4 || (nsplit >= 8 && nsplit <= 64 && nsplit % 8 == 0),
           "nsplit must be 1, 2, 4 or a multiple of 8 in [8,64]");
   RSX_ARG(lda % 4 == 0 && ldb % 4 == 0 && lda >= kD && ldb >= kD, "row strides must be >=128 and multiples of 4");
@@ -3056,8 +3624,9 @@ RSX_API int rsx_kernel_events_read(float* ms, int max_n) {
 RSX_API int rsx_nce_grouped_fwd_grad(const float* A, const float* B, const float* bias, const float* colcnt,
                                      const int* row_col, const int* row_beg, const int* row_end,
                                      const int* exc_cols, int64_t N, int64_t D, int64_t lda, int64_t ldb, float tau,
-                                     int nsplit, float* ws, float* out2, float* ga, void* stream) {
+                                     int precision, int nsplit, float* ws, float* out2, float* ga, void* stream) {
   RSX_ARG(A && B && colcnt && row_col && row_beg && row_end && exc_cols && ws && out2 && ga, "null tensor");
+  RSX_ARG(precision == RSX_NCE_BF16X3 || precision == RSX_NCE_F16, "precision must be 1 (bf16x3) or 2 (f16)");
   RSX_ARG(nsplit == 1 || nsplit == 2 || nsplit == 4 || nsplit == 8, "nsplit must be 1, 2, 4 or 8");
   RSX_ARG(lda % 4 == 0 && ldb % 4 == 0 && lda >= kD && ldb >= kD, "row strides must be >=128 and multiples of 4");
   RSX_ARG(((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0, "A/B must be 16-byte aligned");
@@ -3076,8 +3645,9 @@ RSX_API int rsx_nce_grouped_fwd_grad(const float* A, const float* B, const float
   // as fill whole rounds of the grid at two workgroups per CU; the remaining row blocks run 8
   // half-length splits, dispatched last, so the grid's final round is short and full
   // (batch 8192: 1,152 row blocks x 4 = 9 rounds of 512, then 45 x 8 half-length workgroups)
-  const bool piped = fwdg_pipelined();
-  const int nw = piped ? fwdg_waves() : kWaves;
+  const bool h16 = precision == RSX_NCE_F16;
+  const bool piped = h16 || fwdg_pipelined();
+  const int nw = (piped && !h16) ? fwdg_waves() : kWaves;
   const int64_t rows_wg = 32 * nw;
   const int64_t rbs = (N + rows_wg - 1) / rows_wg;
   const int ns1 = nsplit == 8 ? 4 : nsplit;
@@ -3106,7 +3676,8 @@ RSX_API int rsx_nce_grouped_fwd_grad(const float* A, const float* B, const float
   const Images im = grouped_images(ws, N, D, nsplit, kNsplitBwdGrouped);
   g.bhi = im.bhi;
   g.blo = im.blo;
-  launch_split(B, ldb, D, im.bhi, im.blo, st);
+  if (h16) launch_split_h(B, ldb, D, im.bhi, im.blo, st);
+  else launch_split(B, ldb, D, im.bhi, im.blo, st);
   RSX_LAUNCHED();
   const int blocks = (int)(rb1 * ns1 + (rbs - rb1) * (nsplit == 8 ? 8 : 0));
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -3118,7 +3689,11 @@ RSX_API int rsx_nce_grouped_fwd_grad(const float* A, const float* B, const float
       k.ev.emplace_back(ev0, ev1);
     }
   }
-  if (!piped)
+  if (h16 && f16_gp() == 2)
+    hipLaunchKernelGGL(nce_grouped_fwdg_h_k<2>, dim3(blocks), dim3(256), 0, st, g);
+  else if (h16)
+    hipLaunchKernelGGL(nce_grouped_fwdg_h_k<1>, dim3(blocks), dim3(256), 0, st, g);
+  else if (!piped)
     hipLaunchKernelGGL(nce_grouped_fwdg_x3_k, dim3(blocks), dim3(256), 0, st, g);
   else if (nw == 8 && fwdg_nt())
     hipLaunchKernelGGL((nce_grouped_fwdg_x3p_k<8, true>), dim3(blocks), dim3(512), 0, st, g);
@@ -3158,7 +3733,8 @@ RSX_API int rsx_nce_grouped_bwd(const float* A, const float* B, const float* bia
                                 int accumulate, void* stream) {
   RSX_ARG(gout != nullptr && ws != nullptr, "gout/ws required");
   RSX_ARG(nsplit == kNsplitBwdGrouped, "grouped backward nsplit must be 8");
-  RSX_ARG(precision == RSX_NCE_FP32 || precision == RSX_NCE_BF16X3, "precision must be 0 (fp32) or 1 (bf16x3)");
+  RSX_ARG(precision == RSX_NCE_FP32 || precision == RSX_NCE_BF16X3 || precision == RSX_NCE_F16,
+          "precision must be 0 (fp32), 1 (bf16x3) or 2 (f16)");
   RSX_ARG(!dB || (col_beg && col_end && exc_s && exc_e && exc_n), "column exception lists required for dB");
   hipStream_t st = (hipStream_t)stream;
   if (N == 0) return 0;
@@ -3187,7 +3763,7 @@ RSX_API int rsx_nce_grouped_bwd(const float* A, const float* B, const float* bia
     const int64_t own_blocks = (n_own + kOwnRows - 1) / kOwnRows;
     int ps = (own_blocks * 4 >= 1024) ? 4 : nsplit;
     g.split_major = 0;
-    if (!row_owned && precision == RSX_NCE_BF16X3) {
+    if (!row_owned && precision != RSX_NCE_FP32) {
       // column pass: 32 (else 16) splits in a split-major block order, so each XCD's L2 holds the
       // one split of A's images it streams (the 8-split span, N/8 rows = 9.8 MB at batch 8192, does
       // not fit a 4-MB L2): 5.5 -> 5.0-5.1 ms at batch 8192 (profiles/r02_nce_colsplit_ab.json).
@@ -3210,16 +3786,25 @@ RSX_API int rsx_nce_grouped_bwd(const float* A, const float* B, const float* bia
     g.span = round_up((n_str + ps - 1) / ps, kTile);
     if (g.span < kTile) g.span = kTile;
     const int blocks = (int)(own_blocks * ps);
-    const bool x3 = precision == RSX_NCE_BF16X3;
+    const bool h16 = precision == RSX_NCE_F16;
+    const bool x3 = precision != RSX_NCE_FP32;
     if (x3) {
       const Images im = grouped_images(ws, N, D, nsplit_fwd, kNsplitBwdGrouped);
       g.ahi = im.ahi; g.alo = im.alo; g.bhi = im.bhi; g.blo = im.blo;
       if (!row_owned) {  // B's images come from the forward; A's are made here, for the col pass
-        launch_split(A, lda, N, im.ahi, im.alo, st);
+        if (h16) launch_split_h(A, lda, N, im.ahi, im.alo, st);
+        else launch_split(A, lda, N, im.ahi, im.alo, st);
+        RSX_LAUNCHED();
+      } else if (h16) {  // the row pass streams bf16 images of B (a fused f16 forward left fp16 ones)
+        launch_split(B, ldb, D, im.bhi, im.blo, st);
         RSX_LAUNCHED();
       }
     }
-    if (row_owned && x3) hipLaunchKernelGGL((nce_grouped_bwd_x3_k<true, false>), dim3(blocks), dim3(256), 0, st, g);
+    if (!row_owned && h16 && f16_gp() == 2)
+      hipLaunchKernelGGL(nce_grouped_bwd_cols_h_k<2>, dim3(blocks), dim3(256), 0, st, g);
+    else if (!row_owned && h16)
+      hipLaunchKernelGGL(nce_grouped_bwd_cols_h_k<1>, dim3(blocks), dim3(256), 0, st, g);
+    else if (row_owned && x3) hipLaunchKernelGGL((nce_grouped_bwd_x3_k<true, false>), dim3(blocks), dim3(256), 0, st, g);
     else if (x3 && bwd_halfg()) hipLaunchKernelGGL((nce_grouped_bwd_x3_k<false, true>), dim3(blocks), dim3(256), 0, st, g);
     else if (x3) hipLaunchKernelGGL((nce_grouped_bwd_x3_k<false, false>), dim3(blocks), dim3(256), 0, st, g);
     else if (row_owned) hipLaunchKernelGGL(nce_grouped_bwd_k<true>, dim3(blocks), dim3(256), 0, st, g);

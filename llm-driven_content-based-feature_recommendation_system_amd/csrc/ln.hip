@@ -404,6 +404,8 @@ RSX_API int rsx_ln_fwd(const float* x, const float* res, float p_drop, uint64_t 
 // size one workspace by its largest row count and use it for smaller ones (the tower backward's
 // tail rows R < T: rsx_tower_bwd).
 RSX_API int64_t rsx_ln_bwd_workspace_floats(int64_t T, int64_t D) {
+  // the row widths rsx_ln_bwd accepts; anything else is an error (-1), never a division by D / 4 = 0
+  if (!(D == 64 || D == 128 || D == 256 || D == 512 || D == 768 || D == 1024 || D == 2048)) return -1;
   if (T <= 0) return 64;
   const int64_t quantum = D > 256 ? 4 : 4 * (64 / (D / 4));
   const int64_t b = (T + quantum - 1) / quantum;

@@ -33,12 +33,15 @@ struct Cfg {
 };
 
 struct ArenaLayout {
-  int64_t X, Wp, H, mean, rstd, ug, total;
+  int64_t flag, sid, X, Wp, H, mean, rstd, ug, total;
 };
+// flag (int32 at byte 0): set when an id was outside its table; sid: the ids as the forward read
+// them (out-of-range ids replaced by 0), [ntab][src] int64, what the backward scatters by
 ArenaLayout arena_layout(int64_t U) {
   ArenaLayout s{};
   int64_t o = 0;
   auto take = [&](int64_t n) { const int64_t r = o; o += al(n); return r; };
+  s.flag = take(1); s.sid = take(2 * kMaxTab * U);
   s.X = take(U * kKp); s.Wp = take(kD * kKp); s.H = take(U * kD); s.mean = take(U); s.rstd = take(U);
   s.ug = take(kMaxTab + 1);
   s.total = o;
@@ -94,6 +97,7 @@ int parse(Cfg& c, const int64_t* dims) {
 struct InArgs {
   const int64_t* ids[kMaxTab];
   const float* tab[kMaxTab];
+  int64_t rows[kMaxTab];
   int dim[kMaxTab];
   int col_off[kMaxTab + 1];
   int ntab, C, P, K, ncols;
@@ -105,6 +109,8 @@ struct InArgs {
   float* X;           // [U, 128]
   float* Wp;          // [128, 128]
   float* ug;          // [ntab + 1] sigmoid(static_gate), for the backward
+  int64_t* sid;       // [ntab][src] checked ids (0 where out of range)
+  int* flag;          // set to 1 when any id was out of range
   int64_t U, src, x_blocks;
 };
 
@@ -128,7 +134,12 @@ __global__ __launch_bounds__(256) void prof_in_k(InArgs a) {
   if (c < a.ncols) {
     int j = 0;
     while (j + 1 < a.ntab && c >= a.col_off[j + 1]) ++j;
-    const int64_t id = a.ids[j][r];
+    int64_t id = a.ids[j][r];
+    if (id < 0 || id >= a.rows[j]) {  // nn.Embedding raises here; this read stays in bounds
+      id = 0;
+      *a.flag = 1;
+    }
+    if (c == a.col_off[j] && e / kKp < a.src) a.sid[j * a.src + r] = id;
     v = a.tab[j][id * a.dim[j] + (c - a.col_off[j])] * sigm(a.gate[j]);
   } else if (c < a.K) {
     const int q = c - a.ncols;
@@ -252,14 +263,18 @@ RSX_API int rsx_static_profile_fwd(const void* const* p, const int64_t* dims, fl
   for (int i = 0; i < RSX_SP_N; ++i)
     if ((i < RSX_SP_IDS + c.ntab || i >= RSX_SP_IDS + kMaxTab) && (i < RSX_SP_TABLES + c.ntab || i >= RSX_SP_TABLES + kMaxTab))
       RSX_ARG(p[i] != nullptr, "null input / parameter pointer");
-  if (c.U == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   float* A = static_cast<float*>(arena);
+  if (c.U == 0) {
+    (void)hipMemsetAsync(A + s.flag, 0, sizeof(int), st);
+    return 0;
+  }
   InArgs a{};
   for (int j = 0; j < c.ntab; ++j) {
     a.ids[j] = static_cast<const int64_t*>(p[RSX_SP_IDS + j]);
     a.tab[j] = static_cast<const float*>(p[RSX_SP_TABLES + j]);
     a.dim[j] = (int)c.dims[j];
+    a.rows[j] = c.rows[j];
   }
   for (int j = 0; j <= c.ntab; ++j) a.col_off[j] = c.col_off[j];
   a.ntab = c.ntab; a.C = c.C; a.P = c.P; a.K = c.K; a.ncols = c.ncols;
@@ -269,6 +284,9 @@ RSX_API int rsx_static_profile_fwd(const void* const* p, const int64_t* dims, fl
   a.bc = static_cast<const float*>(p[RSX_SP_BC]);
   a.wm = static_cast<const float*>(p[RSX_SP_WM]);
   a.X = A + s.X; a.Wp = A + s.Wp; a.ug = A + s.ug;
+  a.sid = reinterpret_cast<int64_t*>(A + s.sid);
+  a.flag = reinterpret_cast<int*>(A + s.flag);
+  (void)hipMemsetAsync(a.flag, 0, sizeof(int), st);
   a.U = c.U;
   a.src = c.src;
   a.x_blocks = (c.U * kKp + 255) / 256;
@@ -318,8 +336,8 @@ RSX_API int rsx_static_profile_bwd(const void* const* p, const int64_t* dims, fl
   const int64_t* ids[kMaxTab];
   const float* tabs[kMaxTab];
   float* dtabs[kMaxTab];
-  for (int j = 0; j < c.ntab; ++j) {
-    ids[j] = static_cast<const int64_t*>(p[RSX_SP_IDS + j]);
+  for (int j = 0; j < c.ntab; ++j) {  // the ids the forward checked (no out-of-range scatter)
+    ids[j] = reinterpret_cast<const int64_t*>(A + s.sid) + j * c.src;
     tabs[j] = static_cast<const float*>(p[RSX_SP_TABLES + j]);
     dtabs[j] = grads[RSX_SP_TABLES + j];
   }

@@ -16,8 +16,14 @@ void set_error(const char* fmt, ...) {
 
 RSX_API const char* rsx_last_error(void) { return rsx::g_err; }
 
-RSX_API int rsx_abi_version(void) { return 4; }
+RSX_API int rsx_abi_version(void) { return 5; }
 
 // Device the library's kernels were compiled for; callers compare against the
 // running device's gcnArchName before the first launch.
 RSX_API const char* rsx_target_arch(void) { return "gfx950"; }
+
+#ifndef RSX_SRC_HASH
+#define RSX_SRC_HASH "unknown"
+#endif
+// sha256 (first 16 hex digits) of the sources this library was built from (csrc/Makefile)
+RSX_API const char* rsx_build_hash(void) { return RSX_SRC_HASH; }

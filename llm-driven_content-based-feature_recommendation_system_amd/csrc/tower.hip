@@ -10,7 +10,10 @@
 //
 // Every launch below is one of this library's per-op entry points with exactly the arguments the
 // per-op path passes (same kernels, same reduction orders, same dropout seeds), so the two paths
-// give bit-identical results; what changes is the host side: ~45 forward and ~60 backward
+// give bit-identical results (tail mode aside: there the last layer's per-row ops past the
+// attention key their dropout masks by the R kept rows' own index, so at p > 0 view 2's kept rows
+// draw different -- equally independent -- masks than the all-rows program; view 1's rows and
+// every p = 0 result are unchanged, see rsx_tower_fwd); what changes is the host side: ~45 forward and ~60 backward
 // launches issued from here instead of one interpreted call (plus an autograd node and tensor
 // allocations) each. Buffers: the caller's arena holds the activations the backward reads, the
 // caller's workspace the backward's temporaries; nothing is allocated here.
@@ -130,8 +133,9 @@ struct View {  // typed views of the pointer table
 // instead of the whole causal attention of view 2's sequences, one wave per (user, head) forms
 // that single row: lane k holds key k of the user's segment (L <= 64), fp32 scores over the
 // head's 32 dims (scaled by 1/sqrt(32)), causal (key index <= query index) + key-padding mask,
-// softmax, dropout on the probabilities (keep-mask hash(seed, ((b * 4 + h) * 64 + k)), scaled by
-// 1 / (1 - p)), out = P V. A query with no valid key gets zero output (the training path's
+// softmax, dropout on the probabilities (keep-mask hash(seed, ((q * 4 + h) * 64 + k)) with q the
+// query's packed row: the key mha_fwd_x3 gives that row, so view 2's mask is the full program's and
+// independent of view 1's), scaled by 1 / (1 - p)), out = P V. A query with no valid key gets zero output (the training path's
 // fully-masked-row semantics). lse (natural log, -inf when masked) is kept for the backward.
 struct LastQ {
   const float* qkv;        // [T, 384]
@@ -178,7 +182,7 @@ __global__ __launch_bounds__(256) void tw_lastq_fwd_k(LastQ a) {
     return;
   }
   float pr = pe / l;
-  pr = a.drop.apply(pr, (uint64_t)(j * kHeads + hd) * 64 + lane);
+  pr = a.drop.apply(pr, ((uint64_t)q * kHeads + hd) * 64 + lane);
   const float* vr = a.qkv + kr * kQKV + 2 * kD + kDh * hd;
   float acc = 0.0f;  // lane d < 32 ends with output dim d
   for (int d = 0; d < kDh; ++d) {
@@ -216,7 +220,7 @@ __global__ __launch_bounds__(256) void tw_lastq_bwd_k(LastQ a) {
       dv += g.x * w.x + g.y * w.y + g.z * w.z + g.w * w.w;
     }
     p = expf(d * 0.17677669529663687f - lse);
-    const uint64_t idx = (uint64_t)(j * kHeads + hd) * 64 + lane;
+    const uint64_t idx = ((uint64_t)q * kHeads + hd) * 64 + lane;
     dp = a.drop.apply(dv, idx);       // d/dP of out = sum_k D_k P_k v_k
   }
   float sdp = p * dp;
@@ -232,7 +236,7 @@ __global__ __launch_bounds__(256) void tw_lastq_bwd_k(LastQ a) {
   const float dq_d = dq;  // lanes 0..31 hold dQ
   if (in) {
     float* drow = a.dqkv + kr * kQKV;
-    const float pd = valid ? a.drop.apply(p, (uint64_t)(j * kHeads + hd) * 64 + lane) : 0.0f;  // D_k P_k
+    const float pd = valid ? a.drop.apply(p, ((uint64_t)q * kHeads + hd) * 64 + lane) : 0.0f;  // D_k P_k
 #pragma unroll
     for (int e = 0; e < kDh; e += 4) {
       const float4 x = *reinterpret_cast<const float4*>(qr + e), g = *reinterpret_cast<const float4*>(dor + e);

@@ -28,15 +28,17 @@ _NSPLIT_BWD = 8
 
 # Logit precision of the grouped (live LogQ) loss kernels, include/recsys_amd.h RSX_NCE_*:
 # "bf16x3" = hi/lo bf16 split on the bf16 MFMA (max |dot error| ~3e-6 on unit vectors; the
-# reference computes these logits in fp16 under AMP), "fp32" = fp32-input MFMA.
-NCE_PRECISIONS = {"fp32": 0, "bf16x3": 1}
+# reference computes these logits in fp16 under AMP), "fp32" = fp32-input MFMA, "f16" = the fused
+# forward and the column pass on the fp16 MFMA: logits from an fp16 hi/lo split (tighter than
+# bf16x3), gradient products as one fp16 MFMA (the reference's autocast-fp16 arithmetic for them).
+NCE_PRECISIONS = {"fp32": 0, "bf16x3": 1, "f16": 2}
 _nce_precision = os.environ.get("RSX_NCE_PRECISION", "bf16x3")
 if _nce_precision not in NCE_PRECISIONS:
     raise ValueError(f"RSX_NCE_PRECISION must be one of {sorted(NCE_PRECISIONS)}")
 
 
 def set_nce_precision(mode: str) -> str:
-    """Set the grouped-loss logit precision ("fp32" | "bf16x3"); returns the previous mode."""
+    """Set the grouped-loss precision ("fp32" | "bf16x3" | "f16"); returns the previous mode."""
     global _nce_precision
     if mode not in NCE_PRECISIONS:
         raise ValueError(f"precision must be one of {sorted(NCE_PRECISIONS)}")
@@ -486,7 +488,7 @@ class _NCE(torch.autograd.Function):
         A = _c(A)
         B = _c(B)
         n, m = A.shape[0], B.shape[0]
-        x3 = _nce_precision == "bf16x3"
+        x3 = _nce_precision != "fp32"  # "f16" only changes the grouped kernels
         nws = (N.lib().rsx_nce_x3_workspace_floats(n, m) if x3
                else N.lib().rsx_nce_workspace_floats(n, m, _NSPLIT_FWD, _NSPLIT_BWD))
         ws = torch.empty(nws, device=A.device, dtype=torch.float32)
@@ -622,14 +624,14 @@ class _NCEGrouped(torch.autograd.Function):
         nws = N.lib().rsx_nce_grouped_workspace_floats(n, d, _NSPLIT_FWD_GROUPED, _NSPLIT_BWD, prec)
         ws = torch.empty(nws, device=A.device, dtype=torch.float32)
         out2 = torch.empty(2, device=A.device, dtype=torch.float32)
-        fused = _NCE_FUSED_ROWGRAD and prec == NCE_PRECISIONS["bf16x3"] and ctx.needs_input_grad[0]
+        fused = _NCE_FUSED_ROWGRAD and prec != NCE_PRECISIONS["fp32"] and ctx.needs_input_grad[0]
         ga = None
         with timed(f"{tag}/nce_fwd"):
             if fused:
                 ga = torch.empty(n, 128, device=A.device, dtype=torch.float32)
                 rc = N.lib().rsx_nce_grouped_fwd_grad(
                     N.ptr(A), N.ptr(B), N.ptr(bias), N.ptr(grp.colcnt), N.ptr(grp.row_col), N.ptr(grp.row_beg),
-                    N.ptr(grp.row_end), N.ptr(grp.exc_cols), n, d, A.stride(0), B.stride(0), tau,
+                    N.ptr(grp.row_end), N.ptr(grp.exc_cols), n, d, A.stride(0), B.stride(0), tau, prec,
                     _NSPLIT_FWD_GROUPED, N.ptr(ws), N.ptr(out2), N.ptr(ga), N.stream())
             else:
                 rc = N.lib().rsx_nce_grouped_fwd(
@@ -675,7 +677,7 @@ class _NCEGrouped(torch.autograd.Function):
 def nce_grouped_sum(A, B_distinct, bias, groups: TargetGroups, tau=0.1, tag="nce", precision=None):
     """(sum of row losses, N) of the live LogQ loss with same-item / same-user masking, with
     the columns given as the distinct targets (B_distinct[d] = normalised item groups.uniq[d]).
-    precision: "fp32" | "bf16x3" | None (= set_nce_precision / RSX_NCE_PRECISION)."""
+    precision: "fp32" | "bf16x3" | "f16" | None (= set_nce_precision / RSX_NCE_PRECISION)."""
     if bias is not None:
         bias = _c(bias.to(torch.float32))
     prec = NCE_PRECISIONS[precision or _nce_precision]
@@ -935,11 +937,18 @@ class _StaticProfile(torch.autograd.Function):
         rc = lib.rsx_static_profile_fwd(p_arr, dims, eps, p_drop, seed, N.ptr(arena), arena.numel(), N.ptr(out),
                                         N.stream())
         N.check(rc, "static_profile_fwd")
+        # the kernel range-checks the nine ids (an out-of-range id reads and scatters row 0 and sets
+        # the flag in the arena's first int32): raised as IndexError at the next poll / check
+        _STATIC_IDS.watch(arena[:4].view(torch.int32))
+        # the parameters and tables through autograd's saved tensors, so an in-place change between
+        # forward and backward raises instead of the backward reading the new values
+        ctx.save_for_backward(*params, *tables)
         ctx.keep = (p_arr, dims, ptrs, arena, p_drop, seed, U)
         return out
 
     @staticmethod
     def backward(ctx, dout):
+        ctx.saved_tensors  # noqa: B018 -- the version check of the saved parameters and tables
         p_arr, dims, ptrs, arena, p_drop, seed, U = ctx.keep
         nt = len(ctx.needs_input_grad) - 9
         likes = [ptrs[_SP_GATE]] + [None] + ptrs[_SP_GATE + 2:_SP_N] + ptrs[_SP_TABLES:_SP_TABLES + nt]
@@ -1555,6 +1564,9 @@ class _TowerPacked(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
+        if ctx.keep is None:  # the arena (the forward's activations) is released by the first backward
+            raise RuntimeError("tower_packed: a second backward through the same forward (retain_graph=True) "
+                               "is not supported; run the forward again")
         pv, gate, profile, out, *params = ctx.saved_tensors
         inputs, arena, ptrs, dims, fargs, seeds_arr = ctx.keep
         T, U, L, nl, C = ctx.shape
@@ -1862,17 +1874,32 @@ class IdRangeGuard:
         self.pending.append((ev, host, flag, int(n)))
         return out
 
+    def watch(self, flag, n=None):
+        """Track a device int32 flag that a kernel sets for an out-of-range id (rsx_static_profile_fwd)
+        in the same asynchronous way."""
+        self.poll()
+        host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+        host.copy_(flag, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.pending.append((ev, host, flag, n))
+
     def poll(self, wait=False):
         while self.pending and (wait or self.pending[0][0].query()):
             ev, host, _, n = self.pending.pop(0)
             ev.synchronize()
             if int(host[0]):
                 self.pending.clear()
-                raise IndexError(f"{self.what}: id out of range [0, {n})")
+                rng = "its table's range" if n is None else f"[0, {n})"
+                raise IndexError(f"{self.what}: id out of range {rng}")
 
     def check(self):
         """Raise for any call so far whose ids were out of range (waits for their checks)."""
         self.poll(wait=True)
+
+
+# the static profile's nine lookups (v1_refine_usertower.py:472-481), checked inside prof_in_k
+_STATIC_IDS = IdRangeGuard("static profile ids (SASRecUserTower's nine nn.Embedding lookups)")
 
 
 _TOPK_PATHS = {0: "list", 1: "fast", 2: "bf16"}

@@ -125,3 +125,31 @@ def test_static_profile_shared_rows_equal_doubled_inputs():
     assert torch.equal(res[0][0], res[1][0])
     for n in res[0][1]:
         assert torch.equal(res[0][1][n], res[1][1][n]), n
+
+
+def test_static_profile_out_of_range_id_raises_and_stays_in_bounds():
+    """An id outside its table (nn.Embedding raises IndexError, v1_refine_usertower.py:472-481): the
+    kernel reads and scatters row 0 instead (no out-of-bounds access) and the flag it sets in the
+    arena is raised as IndexError at the guard's check; an in-place change of a saved parameter
+    between forward and backward is caught by autograd's version check."""
+    m = _model()
+    ids, cont = _inputs(64)
+    ops._STATIC_IDS.check()
+    bad = [t.clone() for t in ids]
+    bad[4][7] = 4          # channel table has 4 rows
+    bad[0][3] = -1
+    before = [e.weight.detach().clone() for e in (m.age_emb, m.channel_emb)]
+    out = ops.static_profile(m, bad, cont, 0.0)
+    out.sum().backward()
+    torch.cuda.synchronize()
+    with pytest.raises(IndexError, match="out of range"):
+        ops._STATIC_IDS.check()
+    assert torch.isfinite(out).all()
+    assert torch.equal(before[0], m.age_emb.weight) and torch.equal(before[1], m.channel_emb.weight)
+    ops._STATIC_IDS.check()  # cleared: in-range ids pass again
+    out = ops.static_profile(m, ids, cont, 0.0)
+    with torch.no_grad():
+        m.static_mlp[0].weight.mul_(2.0)
+    with pytest.raises(RuntimeError, match="modified by an inplace operation"):
+        out.sum().backward()
+    ops._STATIC_IDS.check()

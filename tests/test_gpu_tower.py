@@ -321,3 +321,36 @@ def test_native_tower_tail_rows(gpu):
     for n in g1:
         scale = float(g2[n].abs().max()) + 1e-30
         assert (g1[n] - g2[n]).abs().max().item() <= 2e-5 * scale, n
+
+
+def test_native_tower_tail_rows_dropout(gpu):
+    """Tail form at p = 0.2 (the headline step's setting): view 1's rows are keyed exactly as in the
+    per-op all-rows program (attention by packed row, per-row ops by row index < T/2), so they are
+    bit-identical to it; view 2's last query rows key their attention mask by their packed row as
+    well (it used the user index, i.e. view 1's token masks), while the last layer's
+    per-row ops past the attention key view 2's kept rows by their tail index (a different draw than
+    the all-rows program, not shared with any view-1 row), so those rows are only checked to be
+    finite and dropout-perturbed."""
+    cfg = small_cfg(num_items=500, dropout=0.2)
+    items = small_universe(500)
+    batch = to_dev(synth.make_batch(items, 96, seed=23), gpu)
+    lookup = items.pretrained.to(gpu)
+    from recsys_amd import dist as D
+    ix = D.prepare_step_index(batch, pretrained_lookup=lookup)
+    pk, pk2, tok_ids, pv, static = ix.packed
+    outs = []
+    for native in (True, False):
+        torch.manual_seed(5)
+        model = T.SASRecUserTower(cfg).to(gpu).train()
+        prev = ops._TOWER_NATIVE
+        ops._TOWER_NATIVE = native
+        try:
+            outs.append(model.forward_packed(pk2, pv, tok_ids, *static, tail_last=pk.last_tok).detach())
+        finally:
+            ops._TOWER_NATIVE = prev
+    torch.cuda.synchronize()
+    o1, o2 = outs
+    T1 = pk.flat.numel()
+    assert torch.equal(o1[:T1], o2[:T1])
+    assert torch.isfinite(o1).all()
+    assert (o1[T1:] - o2[T1:]).abs().max().item() > 1e-3   # different (independent) post-attention masks

@@ -54,6 +54,9 @@ def test_ln_bwd_workspace_is_monotonic_in_rows():
             w = lib.rsx_ln_bwd_workspace_floats(T, D)
             assert w >= prev, (D, T, w, prev)
             prev = w
+    # an unsupported row width is an error code, not a division by zero (D / 4 == 0 for D < 4)
+    for D in (0, 1, 3, 4, 100, 4096):
+        assert lib.rsx_ln_bwd_workspace_floats(1000, D) == -1
 
 
 def test_module_params_same_set_as_parameters():

@@ -35,6 +35,15 @@ def test_library_exports_every_declared_symbol():
     assert lib.rsx_target_arch() == b"gfx950"
 
 
+def test_library_is_built_from_this_tree():
+    """rsx_build_hash() (csrc/Makefile's sha256 stamp of the sources) equals the hash of the sources
+    in this tree: the .so the tests load is not a stale build."""
+    if not os.path.exists(_native.LIB_PATH):
+        pytest.skip("library not built (run __graft_entry__.build())")
+    info = _native.build_info()
+    assert info["fresh"], info
+
+
 def _prototypes():
     """{name: parameter count} of every prototype in the header."""
     text = open(HEADER).read()
