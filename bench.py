@@ -40,7 +40,9 @@ FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32-input MFMA (= f
 BF16_MFMA_PEAK_TFLOPS = 16 * FP32_MFMA_PEAK_TFLOPS  # 2516.8: dense bf16 MFMA (16x the f32 rate, same guide)
 # bf16x3: every fp32-equivalent FLOP is three bf16 MFMA products (hi*hi + hi*lo + lo*hi)
 BF16X3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 3
-TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r05_nce_fwdg_traffic_b8192.json")
+# f16 loss mode: logits 3 fp16 MFMAs per product, gradient products 1: 2 MFMA passes per algorithmic FLOP
+F16_SPLIT_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 2
+TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r06_nce_fwdg_h_traffic_b8192.json")
 HBM_PEAK_GBS = 8000.0
 
 
@@ -81,8 +83,10 @@ def parse():
     ap.add_argument("--no-rerank", action="store_true", help="skip the retrieve->rerank secondary metric")
     ap.add_argument("--corpus", type=int, default=1_000_000, help="retrieve->rerank corpus size")
     ap.add_argument("--no-item-tower", action="store_true", help="skip the item-tower secondary metric")
-    ap.add_argument("--nce-precision", default="bf16x3", choices=["bf16x3", "fp32"],
-                    help="logit precision of the grouped LogQ loss kernels (ops.set_nce_precision)")
+    ap.add_argument("--nce-precision", default="f16", choices=["f16", "bf16x3", "fp32"],
+                    help="precision of the grouped LogQ loss kernels (ops.set_nce_precision): f16 = fp16x3 logits "
+                         "and single-fp16-MFMA gradient products (default), bf16x3 = both products as three bf16 "
+                         "MFMAs, fp32 = fp32-input MFMA")
     ap.add_argument("--no-prefetch-index", action="store_true",
                     help="build each batch's index inside its own step (host syncs mid-step)")
     ap.add_argument("--unfused-adamw", action="store_true", help="torch's foreach AdamW instead of fused")
@@ -348,6 +352,7 @@ def cpu_baseline(args, items, cfg, batch_size, batch_seed, device=None):
         agr["what"] = ("the GPU step (dist.contrastive_step_dp, dropout 0) from the oracle's pre-step state on the "
                        "same batch vs this timed oracle step: losses, clipped gradients, post-AdamW parameters")
         out["agreement_with_gpu"] = agr
+        assert agr["ok"], agr
     return out
 
 
@@ -1002,7 +1007,8 @@ def nce_roofline(args, tb, global_batch, rank, world, precision):
     for i in range(args.warmup, args.warmup + args.steps):
         flops += 4.0 * n_glob[i % 2][rank] * n_dist[i % 2] * 128
     x3 = precision == "bf16x3"
-    fused = x3 and ops._NCE_FUSED_ROWGRAD
+    h16 = precision == "f16"
+    fused = (x3 or h16) and ops._NCE_FUSED_ROWGRAD
     timer = "main/nce_fwd" if fused else "main/nce_bwd_rows"
     launches, ms = kernel_times.get(timer, (0, 0.0))
     op_window_s = (ms / 1e3) / max(launches, 1)
@@ -1012,7 +1018,9 @@ def nce_roofline(args, tb, global_batch, rank, world, precision):
     if kernel_only:  # the fused kernel's own launches (events around it alone), not the op window
         avg_s = sum(kms) / len(kms) / 1e3
     achieved = (flops / max(launches, 1)) / avg_s / 1e12 if launches else None
-    peak = BF16X3_PEAK_TFLOPS if x3 else FP32_MFMA_PEAK_TFLOPS
+    # f16: the S product is three fp16 MFMAs per product, the gradient product one: two MFMA passes per
+    # algorithmic FLOP on average, i.e. the dense fp16 MFMA peak (= bf16's, 2516.8 TF) / 2
+    peak = BF16X3_PEAK_TFLOPS if x3 else (F16_SPLIT_PEAK_TFLOPS if h16 else FP32_MFMA_PEAK_TFLOPS)
     traffic, traffic_src, alg_bytes = None, None, None
     if os.path.exists(TRAFFIC_FILE):
         with open(TRAFFIC_FILE) as f:
@@ -1022,6 +1030,8 @@ def nce_roofline(args, tb, global_batch, rank, world, precision):
             traffic, traffic_src = tr.get("hbm_bytes_per_launch"), os.path.basename(TRAFFIC_FILE)
             alg_bytes = tr.get("algorithmic_bytes_per_launch")
     fwdg = "nce_grouped_fwdg_x3_k" if os.environ.get("RSX_NCE_FWDG", "1") == "0" else "nce_grouped_fwdg_x3p_k"
+    if h16:
+        fwdg = f"nce_grouped_fwdg_h_k<{2 if os.environ.get('RSX_NCE_F16_GP') == '2' else 1}>"
     return {"kernel": (f"{fwdg} (main LogQ loss forward fused with the row gradient)"
                        if fused else ("nce_grouped_bwd_x3_k<true>" if x3 else "nce_grouped_bwd_k<true>")
                        + " (main LogQ loss backward, row-owned)"),
@@ -1033,7 +1043,10 @@ def nce_roofline(args, tb, global_batch, rank, world, precision):
             "traffic": traffic, "traffic_source": traffic_src, "algorithmic_bytes": alg_bytes,
             "traffic_over_algorithmic": round(traffic / alg_bytes, 3) if traffic and alg_bytes else None,
             "flops_per_launch": round(flops / max(launches, 1)), "avg_launch_ms": round(avg_s * 1e3, 4),
-            "peak_note": ("bf16 dense MFMA 2516.8 TF / 3 split products" if x3 else "fp32-input MFMA dense")}
+            "peak_note": ("bf16 dense MFMA 2516.8 TF / 3 split products" if x3 else
+                          ("fp16 dense MFMA 2516.8 TF / 2 (logits 3 MFMAs, gradient product 1 per 16-deep step)"
+                           if h16 else "fp32-input MFMA dense")),
+            "bf16x3_equivalent_frac": (round(achieved / BF16X3_PEAK_TFLOPS, 4) if (h16 and achieved) else None)}
 
 
 def gather_roofline(args, tb):
@@ -1128,7 +1141,11 @@ def main():
         "higher_is_better": True,
         "scaling": scaling,
         "vs_baseline": None,
-        "dtype": "fp32+bf16x3" if args.nce_precision == "bf16x3" else "fp32",
+        "dtype": {"f16": "fp32+bf16x3+f16", "bf16x3": "fp32+bf16x3", "fp32": "fp32"}[args.nce_precision],
+        "dtype_note": ("fp32 storage and accumulation; token GEMMs bf16x3; grouped LogQ loss (f16): logits as three "
+                       "fp16 MFMAs of an fp16 hi/lo split (~2^-22 per term), gradient products as one fp16 MFMA "
+                       "(the reference trains under autocast(float16), v1_usertower_train.py:787)"
+                       if args.nce_precision == "f16" else None),
         "data": "synthetic (seeded H&M-shaped users/items: sample-calibrated lengths, Zipf(1.0) items; "
                 "random-init weights)",
         "config": {"workload": "user-tower two-view contrastive train step (fwd x2 + LogQ in-batch loss + "

@@ -2575,6 +2575,7 @@ constexpr float kHScale = 256.0f;         // operand scale 2^8
 constexpr float kHUnscale = 1.0f / 256.0f;
 constexpr float kHS2 = 1.0f / 65536.0f;   // S product scale 2^-16
 constexpr float kHGS = 14.0f;             // column pass: G weights scaled by 2^14 (<= 16384)
+constexpr float kHGSv = 16384.0f;
 
 __device__ __forceinline__ f32x16 mfma_h(const bf16x8& a, const bf16x8& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
@@ -2727,7 +2728,7 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_fwdg_h_k(GArgs a) {
     next = (p < e) ? a.exc_cols[p] : kNone;
   }
   const float it2 = a.inv_tau * kLog2e * kHS2;
-  float m = -INFINITY, l = 0.0f;
+  float m = -INFINITY, l = 0.0f, lab_x = -INFINITY;
   f32x16 gacc[4];
 #pragma unroll
   for (int kb = 0; kb < 4; ++kb)
@@ -2795,6 +2796,7 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_fwdg_h_k(GArgs a) {
             const int r = 4 * g + t;
             const float wn = (tile_row(r, h) == tl) ? 1.0f : cv[t] - n[r];
             if (wn != cv[t]) acc[r] = (wn > 0.0f) ? acc[r] + __log2f(wn / cv[t]) : -INFINITY;
+            if (tile_row(r, h) == tl) lab_x = acc[r];  // the label's logit (weight 1), see below
           }
         }
         p = q;
@@ -2833,6 +2835,16 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_fwdg_h_k(GArgs a) {
         __builtin_amdgcn_wave_barrier();
       }
       const float ms = (m == -INFINITY) ? 0.0f : m;
+      if (lab_x != -INFINITY) {
+        // the label column enters the sum l here and is left out of the gradient product: the merge
+        // adds its term as (p_pos - 1) B_d(i) in fp32 (near convergence p_pos B_d(i) and the label's
+        // -B_d(i) cancel, and an fp16-rounded p_pos B_d(i) would leave a 2^-12 |B| residue)
+        l += __builtin_amdgcn_exp2f(lab_x - ms);
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (tile_row(r, h) == (int)(di - j0)) acc[r] = -INFINITY;
+        lab_x = -INFINITY;
+      }
       uint32_t g0[4], g1[4];
       f32x2 sum = {0.0f, 0.0f};
       grad_half_h<true, GP>(gacc, pg, sT[prev], gbase, 1, acc, 0, ms, g0, sum);
@@ -2879,8 +2891,11 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_fwdg_h_k(GArgs a) {
 }
 
 // k-step ks of the column pass's gradient product in fp16, gacc[nb] += G'_ks^T X, with (WORK) the
-// next k-step's G' pair nb: g' = 2^(S it2 - (m0 + o_m2) + 14) (the owner factor fo applied after
-// the sweep)
+// next k-step's G' pair nb: G' = 2^14 min(c_o p1, 1), c_o p1 = 2^(S it2 - m0 - bias_o) c_o = 2^(S it2 -
+// (m0 + o_m2s)) / 2^14: row i's softmax mass on target o when (i, o) is not an exception pair (<= 1: lse_i
+// sums every column with its multiplicity); on exception pairs (same user / label, where the true weight
+// is below c_o) the clamp keeps the term finite and within 1, and the exception product replaces it.
+// The uniform factor gout / tau and the 2^-14 scale are applied after the sweep
 template <bool WORK, int GP>
 __device__ __forceinline__ void grad_half_gh(f32x16 (&gacc)[4], const bf16x8& g, const X3Tile& t, int base, int ks,
                                              const f32x16& S, int h, const float* m0, float o_m2s, float it2,
@@ -2904,7 +2919,7 @@ __device__ __forceinline__ void grad_half_gh(f32x16 (&gacc)[4], const bf16x8& g,
 #pragma unroll
       for (int rr = 0; rr < 2; ++rr) {
         const int r = 2 * pp + rr, e = r & 3;
-        gp[rr] = __builtin_amdgcn_exp2f(fmaf(S[r], it2, -(q0[e] + o_m2s)));
+        gp[rr] = fminf(__builtin_amdgcn_exp2f(fmaf(S[r], it2, -(q0[e] + o_m2s))), kHGSv);
       }
       og[nb] = pack_h(gp[0], gp[1]);
       asm volatile("" : "+v"(og[nb]));
@@ -2915,44 +2930,21 @@ __device__ __forceinline__ void grad_half_gh(f32x16 (&gacc)[4], const bf16x8& g,
   }
 }
 
-// exception-tile form (grad_x3s on fp16): the 16 G' values in registers -> two fp16 fragments,
-// then the eight (ks, nb) steps, software-pipelined by one
-template <int GP>
-__device__ __forceinline__ void grad_tile_h(f32x16 (&gacc)[4], const f32x16& G, const X3Tile& t, int base) {
-  bf16x8 gf[2];
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    u32x4 v;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) v[q] = pack_h(G[8 * ks + 2 * q], G[8 * ks + 2 * q + 1]);
-    gf[ks] = __builtin_bit_cast(bf16x8, v);
-  }
-  bf16x8 bh, bl;
-  grad_rd(t.hi, base, 0, 0, bh);
-  if (GP == 2) grad_rd(t.lo, base, 0, 0, bl);
-#pragma unroll
-  for (int step = 0; step < 8; ++step) {
-    bf16x8 nh = bh, nl = bl;
-    if (step < 7) {
-      grad_rd(t.hi, base, (step + 1) >> 2, (step + 1) & 3, nh);
-      if (GP == 2) grad_rd(t.lo, base, (step + 1) >> 2, (step + 1) & 3, nl);
-    }
-    const int ks = step >> 2, nb = step & 3;
-    if (GP == 2) gacc[nb] = mfma_h(gf[ks], bl, gacc[nb]);
-    gacc[nb] = mfma_h(gf[ks], bh, gacc[nb]);
-    __builtin_amdgcn_sched_barrier(0);
-    bh = nh;
-    bl = nl;
-  }
-}
-
-// Column pass of the grouped backward (nce_grouped_bwd_x3_k<false, true>'s structure) on the fp16
-// products: owner = distinct target column o (registers), streamed = user rows (A's fp16 images).
+// Column pass of the grouped backward on the fp16 products: owner = distinct target column o (its fp16
+// hi/lo fragments in registers), streamed = user rows (A's fp16 images). Every (row, column) pair is
+// first taken with the common weight G' = 2^14 min(c_o p1_io, 1) (p1 = one column instance's softmax
+// probability; the clamp only acts on exception pairs); on the rare tiles where the owner's same-user
+// rows or label rows appear (the user-range lists exc_s / exc_e / exc_n), a second product adds
+// dG' = G'_exact - G'_common for those pairs, formed from the same S tile in fp32 before its one
+// rounding (v1_refine_usertower.py:846-858: same-user mask, label column). The correction runs after
+// the common product, when its G fragments are dead: folded into the common product, the exception
+// bookkeeping needs ~60 more VGPRs than the 256 a two-wave-per-SIMD kernel has (and with the owner
+// fragments moved to LDS instead the pass is LDS-bound).
 template <int GP>
 __global__ __launch_bounds__(256, 2) void nce_grouped_bwd_cols_h_k(GArgs a) {
   __shared__ __attribute__((aligned(16))) X3Tile sT[2];
   __shared__ __attribute__((aligned(16))) float sM0[2][kTile];  // lse_i * log2e (+inf past the split)
-  __shared__ __attribute__((aligned(16))) int sM2[2][kTile];    // d(i)
+  __shared__ __attribute__((aligned(16))) int sM2[2][kTile];    // d(i) (-2 past the split)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, c = lane & 31;
   int split, ob;
@@ -2975,18 +2967,16 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_bwd_cols_h_k(GArgs a) {
   int64_t s_end = s_begin + a.span;
   if (s_end > n_str) s_end = n_str;
   constexpr int kNone = 0x7fffffff;
-  float o_m2 = 0.0f, o_cnt = 0.0f;
+  // exponent offset of G' = 2^14 c_o 2^(x): bias_o log2e - log2 c_o - 14 (no owner: +inf -> G' = 0)
+  float o_m2s = INFINITY, o_cnt = 0.0f;
   int p = 0, e = 0;
   if (own_ok) {
-    o_m2 = a.bias ? a.bias[o] * kLog2e : 0.0f;
     o_cnt = a.colcnt[o];
+    o_m2s = (a.bias ? a.bias[o] * kLog2e : 0.0f) - __log2f(o_cnt) - kHGS;
     p = a.col_beg[o];
     e = a.col_end[o];
-    p = lower_bound_i(a.exc_e, p, e, s_begin + 1);
+    p = lower_bound_i(a.exc_e, p, e, s_begin + 1);  // first user range ending after s_begin
   }
-  const float o_m2s = o_m2 - kHGS;                                   // the 2^14 weight scale
-  const float fo = own_ok ? gs * o_cnt : 0.0f;                       // applied after the sweep
-  const float inv_cnt = (own_ok && o_cnt > 0.0f) ? 1.0f / o_cnt : 0.0f;  // exception tiles' G' = g / c_o
   int q = p, e_first = 0, s_next = kNone;
   if (own_ok && q < e) s_next = a.exc_s[q];
 
@@ -3016,6 +3006,7 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_bwd_cols_h_k(GArgs a) {
       sM2[buf][tid] = stg2;
     }
   };
+  // user row ranges [p, q) of the owner's column intersecting tile s0 (before the prefetch: may load)
   auto exc_flag = [&](int64_t s0) -> bool {
     while (p < q && (int64_t)e_first <= s0) {
       ++p;
@@ -3042,12 +3033,33 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_bwd_cols_h_k(GArgs a) {
       const bool exc = exc_flag(s0);
       if (has_next) gload(s0 + kTile);
       f32x16 acc = dots_h3(sT[cur], c, h, uh, ul);
+      // G' rows of k-step 0, then k-step 0's product with k-step 1's rows under its MFMAs
+      u32x4 g0;
+#pragma unroll
+      for (int pp = 0; pp < 4; ++pp) {
+        const f32x4 q0 = *reinterpret_cast<const f32x4*>(&sM0[cur][8 * (pp >> 1) + 4 * h]);
+        float gp[2];
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr) {
+          const int r = 2 * pp + rr, ee = r & 3;
+          gp[rr] = fminf(__builtin_amdgcn_exp2f(fmaf(acc[r], it2, -(q0[ee] + o_m2s))), kHGSv);
+        }
+        g0[pp] = pack_h(gp[0], gp[1]);
+      }
+      uint32_t g1[4];
+      grad_half_gh<true, GP>(gacc, __builtin_bit_cast(bf16x8, g0), sT[cur], gbase, 0, acc, h, sM0[cur], o_m2s, it2,
+                             g1);
+      const u32x4 g1v = {g1[0], g1[1], g1[2], g1[3]};
+      grad_half_gh<false, GP>(gacc, __builtin_bit_cast(bf16x8, g1v), sT[cur], gbase, 1, acc, h, sM0[cur], o_m2s, it2,
+                              g1);
       if (__any(exc)) {
-        float n[16];
+        // dG' = 2^14 (w p1 - lab) - 2^14 min(c_o p1, 1) on the owner's exception rows (0 elsewhere):
+        // w = c_o - n (the user's own rows of target o) or 1 (label), from the same S as the common term
+        float n[16];  // multiplicity n of the user range holding streamed row tr (0: none)
 #pragma unroll
         for (int r = 0; r < 16; ++r) n[r] = 0.0f;
         if (exc) {
-          for (int k = p; k < q; ++k) {
+          for (int k = p; k < q; ++k) {  // each range's bounds loaded once
             const int ks = (int)(a.exc_s[k] - s0), ke = (int)(a.exc_e[k] - s0);
             const float nk = (float)a.exc_n[k];
 #pragma unroll
@@ -3057,33 +3069,27 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_bwd_cols_h_k(GArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int tr = tile_row(r, h);
-          const float x = fmaf(acc[r], it2, -(sM0[cur][tr] + o_m2));
+          const float nr = n[r];
           const bool lab = exc && sM2[cur][tr] == (int)o;
-          const float wr = lab ? 1.0f : o_cnt - n[r];
-          const float g = (wr > 0.0f ? wr * __builtin_amdgcn_exp2f(x) : 0.0f) - (lab ? 1.0f : 0.0f);
-          acc[r] = g * inv_cnt * 16384.0f;  // G' = 2^14 g / c_o
-        }
-        grad_tile_h<GP>(gacc, acc, sT[cur], gbase);
-      } else {
-        // G' rows of k-step 0, then k-step 0's product with k-step 1's rows under its MFMAs
-        u32x4 g0;
-#pragma unroll
-        for (int pp = 0; pp < 4; ++pp) {
-          const f32x4 q0 = *reinterpret_cast<const f32x4*>(&sM0[cur][8 * (pp >> 1) + 4 * h]);
-          float gp[2];
-#pragma unroll
-          for (int rr = 0; rr < 2; ++rr) {
-            const int r = 2 * pp + rr, ee = r & 3;
-            gp[rr] = __builtin_amdgcn_exp2f(fmaf(acc[r], it2, -(q0[ee] + o_m2s)));
+          float dg = 0.0f;
+          if (exc && (nr > 0.0f || lab)) {
+            const float ex = __builtin_amdgcn_exp2f(fmaf(acc[r], it2, -(sM0[cur][tr] + o_m2s)));  // 2^14 c_o p1
+            const float rc = __builtin_amdgcn_rcpf(o_cnt);
+            const float w = lab ? 1.0f : fmaxf(o_cnt - nr, 0.0f);
+            dg = (w * rc) * ex - (lab ? kHGSv : 0.0f) - fminf(ex, kHGSv);
           }
-          g0[pp] = pack_h(gp[0], gp[1]);
+          acc[r] = dg;
         }
-        uint32_t g1[4];
-        grad_half_gh<true, GP>(gacc, __builtin_bit_cast(bf16x8, g0), sT[cur], gbase, 0, acc, h, sM0[cur], o_m2s, it2,
-                               g1);
-        const u32x4 g1v = {g1[0], g1[1], g1[2], g1[3]};
-        grad_half_gh<false, GP>(gacc, __builtin_bit_cast(bf16x8, g1v), sT[cur], gbase, 1, acc, h, sM0[cur], o_m2s,
-                                it2, g1);
+        u32x4 d0, d1;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          d0[qq] = pack_h(acc[2 * qq], acc[2 * qq + 1]);
+          d1[qq] = pack_h(acc[8 + 2 * qq], acc[8 + 2 * qq + 1]);
+        }
+        grad_half_gh<false, GP>(gacc, __builtin_bit_cast(bf16x8, d0), sT[cur], gbase, 0, acc, h, sM0[cur], o_m2s, it2,
+                                g1);
+        grad_half_gh<false, GP>(gacc, __builtin_bit_cast(bf16x8, d1), sT[cur], gbase, 1, acc, h, sM0[cur], o_m2s, it2,
+                                g1);
       }
       if (has_next) lstore(cur ^ 1);
       __builtin_amdgcn_s_waitcnt(kVmcnt0);
@@ -3093,11 +3099,10 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_bwd_cols_h_k(GArgs a) {
   }
   const int64_t own_base = (int64_t)ob * kOwnRows + wave * 32;
   float* dst = a.dout + (int64_t)split * n_own * kD;
+  const float f = gs * (kHUnscale / kHGSv);  // gout / tau, the 2^-8 row scale and the 2^-14 weight scale
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    const int tr = tile_row(r, h);
-    const float f = __shfl(fo, tr, 64) * (kHUnscale / 16384.0f);  // owner tr's factor, 2^-8 row scale, 2^-14
-    const int64_t orow = own_base + tr;
+    const int64_t orow = own_base + tile_row(r, h);
     if (orow < n_own) {
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) dst[orow * kD + kb * 32 + c] = gacc[kb][r] * f;
@@ -3112,7 +3117,8 @@ __global__ __launch_bounds__(256) void nce_grouped_merge_g_k(const float* A, con
                                                              int64_t ldb, float inv_tau, int nsplit,
                                                              const float* part, const float* opart,
                                                              float* lse_out, float* row_loss, float* row_valid,
-                                                             float* ga, int64_t rows1, int nsplit2, int nslots) {
+                                                             float* ga, int64_t rows1, int nsplit2, int nslots,
+                                                             int lab_out) {
   const int lane = threadIdx.x & 63;
   const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= N) return;
@@ -3152,7 +3158,10 @@ __global__ __launch_bounds__(256) void nce_grouped_merge_g_k(const float* A, con
       acc.y = fs != 0.0f ? fmaf(fs, v[s].y, acc.y) : acc.y;
     }
   }
-  reinterpret_cast<float2*>(ga + i * kD)[lane] = make_float2((acc.x - y.x) * inv_tau, (acc.y - y.y) * inv_tau);
+  // lab_out: the kernel left the label column out of its partial rows (nce_grouped_fwdg_h_k): its term
+  // p_pos B_d(i) and the label's -B_d(i) enter together as (p_pos - 1) B_d(i), p_pos = e^(s_ii - lse)
+  const float cy = lab_out ? ((lse == -INFINITY) ? -1.0f : __expf(sii - lse) - 1.0f) : -1.0f;
+  reinterpret_cast<float2*>(ga + i * kD)[lane] = make_float2(fmaf(cy, y.x, acc.x) * inv_tau, fmaf(cy, y.y, acc.y) * inv_tau);
   if (lane == 0) {
     lse_out[i] = lse;
     row_loss[i] = lse - sii;
@@ -3707,7 +3716,7 @@ RSX_API int rsx_nce_grouped_fwd_grad(const float* A, const float* B, const float
   if (ev1) (void)hipEventRecord(ev1, st);
   hipLaunchKernelGGL(nce_grouped_merge_g_k, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, A, B, bias, row_col,
                      N, lda, ldb, g.inv_tau, ns1, part, opart, lse, row_loss, row_valid, ga, rb1 * rows_wg, 8,
-                     nsplit);
+                     nsplit, h16 ? 1 : 0);
   RSX_LAUNCHED();
   hipLaunchKernelGGL(nce_reduce_k, dim3(1), dim3(1024), 0, st, row_loss, row_valid, N, out2);
   RSX_LAUNCHED();

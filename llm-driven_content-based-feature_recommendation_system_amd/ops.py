@@ -32,7 +32,7 @@ _NSPLIT_BWD = 8
 # forward and the column pass on the fp16 MFMA: logits from an fp16 hi/lo split (tighter than
 # bf16x3), gradient products as one fp16 MFMA (the reference's autocast-fp16 arithmetic for them).
 NCE_PRECISIONS = {"fp32": 0, "bf16x3": 1, "f16": 2}
-_nce_precision = os.environ.get("RSX_NCE_PRECISION", "bf16x3")
+_nce_precision = os.environ.get("RSX_NCE_PRECISION", "f16")
 if _nce_precision not in NCE_PRECISIONS:
     raise ValueError(f"RSX_NCE_PRECISION must be one of {sorted(NCE_PRECISIONS)}")
 

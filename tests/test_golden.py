@@ -141,7 +141,7 @@ def test_golden_oracle_deepfm_and_retrieval():
 
 # ------------------------------------------------------------------ GPU: HIP path vs fixtures
 @pytest.mark.gpu
-@pytest.mark.parametrize("precision", ["bf16x3", "fp32"])
+@pytest.mark.parametrize("precision", ["bf16x3", "fp32", "f16"])
 def test_golden_gpu_user_tower(gpu, precision):
     from recsys_amd import ops
     from recsys_amd.tower_code import v1_usertower_train as TT
@@ -155,7 +155,8 @@ def test_golden_gpu_user_tower(gpu, precision):
     pre = t["in.pretrained"].to(gpu)
     kw = {k: batch[k] for k in FORWARD_KEYS}
     kw["pretrained_vecs"] = TT.lookup_pretrained(pre, batch["item_ids"])
-    prev_n, prev_g = ops.set_nce_precision(precision), ops.set_gemm_precision(precision)
+    prev_n = ops.set_nce_precision(precision)
+    prev_g = ops.set_gemm_precision("fp32" if precision == "fp32" else "bf16x3")
     try:
         with torch.no_grad():
             torch.testing.assert_close(dut(**kw, training_mode=True).cpu(), t["out.train"], atol=2e-5, rtol=1e-4)
@@ -177,20 +178,29 @@ def test_golden_gpu_user_tower(gpu, precision):
 
 
 @pytest.mark.gpu
-def test_golden_gpu_losses(gpu):
+@pytest.mark.parametrize("precision", ["bf16x3", "f16"])
+def test_golden_gpu_losses(gpu, precision):
+    """Loss fixtures; the live LogQ loss in the given grouped-loss precision: bf16x3 gradients within
+    1e-4 of their scale, f16 (single fp16 MFMA gradient products, the reference's autocast arithmetic)
+    within 1e-3 (its logits are fp16x3: the loss stays within 1e-4)."""
     from recsys_amd import item_tower as IT
     from recsys_amd import ops
     from recsys_amd.tower_code import v1_refine_usertower as T
+    gtol = 1e-4 if precision == "bf16x3" else 1e-3
     t, meta = load("logq_loss_n257")
     U = t["in.user"].to(gpu).requires_grad_(True)
     Wt = t["in.items"].to(gpu).requires_grad_(True)
-    loss = T.inbatch_corrected_logq_loss(ops.l2_normalize(U), ops.l2_normalize(Wt), t["in.target_ids"].to(gpu),
-                                         t["in.user_ids"].to(gpu), t["in.log_q"].to(gpu), meta["temperature"],
-                                         meta["lambda_logq"])
-    loss.backward()
+    prev = ops.set_nce_precision(precision)
+    try:
+        loss = T.inbatch_corrected_logq_loss(ops.l2_normalize(U), ops.l2_normalize(Wt), t["in.target_ids"].to(gpu),
+                                             t["in.user_ids"].to(gpu), t["in.log_q"].to(gpu), meta["temperature"],
+                                             meta["lambda_logq"])
+        loss.backward()
+    finally:
+        ops.set_nce_precision(prev)
     assert abs(loss.item() - t["out.loss"].item()) < 1e-4
-    assert_grad_close(U.grad.cpu(), t["g.user"], 1e-4, "user")
-    assert_grad_close(Wt.grad.cpu(), t["g.items"], 1e-4, "items")
+    assert_grad_close(U.grad.cpu(), t["g.user"], gtol, "user")
+    assert_grad_close(Wt.grad.cpu(), t["g.items"], gtol, "items")
 
     t, meta = load("duorec_b96")
     z1 = t["in.z1"].to(gpu).requires_grad_(True)

@@ -3,13 +3,14 @@ tools/nce_micro.py (rocprofv3 --pmc, separate passes; see tools/steps_final_r01.
 
 FETCH_SIZE is doubled (gfx950 reports half the bytes of 16-B/lane streaming reads,
 MI355X_MICROARCH.md HBM section); WRITE_SIZE is taken as reported.
-  python tools/make_traffic.py gpurun_out/pmcf gpurun_out/pmcw out.json [global_batch N D [nslots]]"""
+  python tools/make_traffic.py gpurun_out/pmcf gpurun_out/pmcw out.json [global_batch N D [nslots [kernel precision]]]"""
 import csv
 import glob
 import json
 import sys
 
-KERNEL = "nce_grouped_fwdg_x3"  # both forms: x3_k (RSX_NCE_FWDG=0) and the pipelined x3p_k
+KERNEL = sys.argv[8] if len(sys.argv) > 8 else "nce_grouped_fwdg_x3"  # default: x3_k and the pipelined x3p_k
+PRECISION = sys.argv[9] if len(sys.argv) > 9 else "bf16x3"
 
 
 def vals(d, counter):
@@ -35,8 +36,8 @@ def main():
     # kernel outside this launch
     alg = 4 * (N + D) * 128 + ns * 4 * N * 128 + ns * 4 * 4 * N
     out = {
-        "kernel": "nce_grouped_fwdg_x3p_k (grouped LogQ forward fused with the row gradient, pipelined)",
-        "precision": "bf16x3", "global_batch": batch, "rows_N": N, "distinct_targets_D": D, "partial_slots": ns,
+        "kernel": KERNEL + " (grouped LogQ forward fused with the row gradient, pipelined)",
+        "precision": PRECISION, "global_batch": batch, "rows_N": N, "distinct_targets_D": D, "partial_slots": ns,
         "fetch_size_kb_raw": round(f, 1), "write_size_kb": round(w, 1),
         "hbm_bytes_per_launch": hbm,
         "correction": "FETCH_SIZE doubled (gfx950 reports half the bytes of 16-B/lane streaming reads, "

@@ -26,7 +26,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "fp32"])
+    ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "fp32", "f16"])
+    ap.add_argument("--compare", action="store_true",
+                    help="also report the loss / gradient deviation from the fp32 mode on the same inputs")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--global-batch", type=int, default=0,
                     help="emulate one rank of a DP run: rows of the first --batch users, columns = the "
@@ -75,6 +77,20 @@ def main():
            "fwd_kernel_ms": round(sum(kms) / len(kms), 4) if kms else None,
            "fwd_kernel_frac_bf16x3": (round(flops / (sum(kms) / len(kms) / 1e3) / 838.9e12, 4) if kms else None),
            "avg_ms": {k: round(ms / max(cnt, 1), 4) for k, (cnt, ms) in sorted(kt.items())}}
+    if args.compare:
+        def run(prec):
+            U.grad = None
+            B.grad = None
+            s1, _ = ops.nce_grouped_sum(U, B, bias, grp, tau=0.1, tag="cmp", precision=prec)
+            s1.backward()
+            return float(s1.item()), U.grad.detach().clone(), B.grad.detach().clone()
+        l0, gu0, gb0 = run("fp32")
+        l1, gu1, gb1 = run(args.precision)
+        out["vs_fp32"] = {"loss_rel": abs(l1 - l0) / abs(l0),
+                          "grad_u_max_err_over_scale": float((gu1 - gu0).abs().max() / gu0.abs().max()),
+                          "grad_b_max_err_over_scale": float((gb1 - gb0).abs().max() / gb0.abs().max()),
+                          "grad_u_rel_fro": float((gu1 - gu0).norm() / gu0.norm()),
+                          "grad_b_rel_fro": float((gb1 - gb0).norm() / gb0.norm())}
     print(json.dumps(out), flush=True)
 
 
