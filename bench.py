@@ -821,6 +821,81 @@ def bench_item_tower(args, device):
         (model, [std, re_ids, re_mask, txt, txt_mask])
 
 
+def bench_simcse_train(args, device, B=192, iters=3):
+    """The item tower's SimCSE training step (item_tower.py:1061-1105; verdict r5 item 6):
+    SimCSEModelWrapper(HybridItemTower with a bert-base-shaped local BERT, OptimizedItemTower), two
+    views of B synthetic products (the second with 20 % of its RE and text tokens dropped, as
+    SimCSERecSysDataset's corruption), symmetric SimCSE loss (fused InfoNCE kernel), backward, AdamW
+    with BERT in its own group at lr 1e-5 (:1012-1022). items/s, plus BERT's share of the step: the
+    text BERT's forward + backward on the same two views timed alone (HF BertModel under grad, the
+    reference's own module), priced at the fp32 MFMA peak (the arithmetic torch runs it in here)."""
+    import numpy as np
+    from recsys_amd import item_tower as IT
+    R, S = 32, 32
+    torch.manual_seed(args.seed)
+    bert = IT.build_local_bert()
+    enc = IT.HybridItemTower(384, 6, 128, 128, bert_model=bert).to(device).train()
+    proj = IT.OptimizedItemTower(128, 128).to(device)
+    model = IT.SimCSEModelWrapper(enc, proj).train()
+    bert_params = [p for n, p in model.named_parameters() if "bert_model" in n]
+    other = [p for n, p in model.named_parameters() if "bert_model" not in n]
+    opt = torch.optim.AdamW([{"params": bert_params, "lr": 1e-5}, {"params": other, "lr": 1e-3}])
+    rng = np.random.default_rng(args.seed + 21)
+
+    def view(drop):
+        std = torch.from_numpy(rng.integers(0, 384, (B, 6))).to(device)
+        lens = rng.integers(2, R + 1, (B, 9))
+        re_mask = (np.arange(R)[None, None, :] < lens[..., None]).astype(np.int64)
+        tl = rng.integers(2, S + 1, (B,))
+        txt_mask = (np.arange(S)[None, :] < tl[:, None]).astype(np.int64)
+        if drop:  # keep [CLS] (position 0) and the first RE token
+            re_mask[..., 1:] *= (rng.random((B, 9, R - 1)) >= 0.2)
+            txt_mask[:, 1:] *= (rng.random((B, S - 1)) >= 0.2)
+        re_ids = torch.from_numpy(rng.integers(1000, 30521, (B, 9, R)) * re_mask).to(device)
+        txt = torch.from_numpy(rng.integers(1000, 30521, (B, S)) * txt_mask).to(device)
+        return [std, re_ids, torch.from_numpy(re_mask).to(device), txt, torch.from_numpy(txt_mask).to(device)]
+
+    v1 = view(False)
+    v2 = [v1[0]] + view(True)[1:]
+    for _ in range(2):
+        IT.simcse_train_step(model, v1, v2, opt)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        loss, _, _ = IT.simcse_train_step(model, v1, v2, opt)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / iters
+    # BERT alone: forward + backward of both views' text (the CLS rows' gradient seeded with ones)
+    def bert_step():
+        for v in (v1, v2):
+            cls = bert(input_ids=v[3], attention_mask=v[4]).last_hidden_state[:, 0, :]
+            cls.sum().backward()
+    bert_step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        bert_step()
+    torch.cuda.synchronize()
+    bt = (time.perf_counter() - t0) / iters
+    opt.zero_grad(set_to_none=True)
+    cfg = bert.config
+    Dm, F_, nl = cfg.hidden_size, cfg.intermediate_size, cfg.num_hidden_layers
+    tokens = 2 * B * S  # HF BertModel runs the padded [B, S] grid of both views
+    fwd_flops = nl * tokens * 2 * (4 * Dm * Dm + 2 * Dm * F_) + nl * 2 * (2 * B) * S * S * Dm * 2
+    flops = 3 * fwd_flops  # forward + backward (dX and dW)
+    return {"metric": f"SimCSE item-tower train step items/sec (two views, batch {B}, bert-base-shaped local BERT "
+                      "fine-tuned, AdamW)",
+            "value": round(B / dt, 1), "unit": "items/s", "ms_per_step": round(dt * 1e3, 3), "batch": B,
+            "loss": round(float(loss.item()), 5),
+            "bert": {"module": "transformers BertModel under grad (both views' text, fwd + bwd)",
+                     "ms_per_step": round(bt * 1e3, 3), "share_of_step": round(bt / dt, 3),
+                     "flops_per_step": int(flops), "achieved_TFLOPs": round(flops / bt / 1e12, 2),
+                     "peak_TFLOPs": FP32_MFMA_PEAK_TFLOPS, "frac": round(flops / bt / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
+                     "note": "HF BertModel in fp32 (torch's library GEMMs); the native packed-token BERT "
+                             "(item_tower.bert_cls_packed) is inference-only"},
+            "data": "synthetic std / RE / text ids, RE lengths U{2..32}, text lengths U{2..32}, random weights"}
+
+
 def bench_eval_forward(args, device, model, items, users=4096, iters=10):
     """evaluate_model's tower pass (tower_code/v1_usertower_train.py:548-711 on the GPU:
     SASRecUserTower forward in eval mode, training_mode=False -> the last position's [B, D]
@@ -990,7 +1065,8 @@ def train_bench(args, global_batch, steps, warmup, items, cfg, model, item_tower
     return {"elapsed": float(elapsed.item()), "kernel_times": kernel_times, "losses": losses, "n_glob": n_glob,
             "n_dist": n_dist, "n_tok": n_tok, "host_enqueue_ms": round(1e3 * sum(enqueue) / max(len(enqueue), 1), 3),
             "host_unloaded": host_unloaded, "alloc_retries": int(retries), "fwdg_kernel_ms": fwdg_kernel_ms,
-            "clocks": {"before_timed_steps": clk0, "after_timed_steps": clk1} if sample_clocks else None}
+            "clocks": {"before_timed_steps": clk0, "after_timed_steps": clk1} if sample_clocks else None,
+            "users_local": b_loc}
 
 
 def nce_roofline(args, tb, global_batch, rank, world, precision):
@@ -1047,6 +1123,72 @@ def nce_roofline(args, tb, global_batch, rank, world, precision):
                           ("fp16 dense MFMA 2516.8 TF / 2 (logits 3 MFMAs, gradient product 1 per 16-deep step)"
                            if h16 else "fp32-input MFMA dense")),
             "bf16x3_equivalent_frac": (round(achieved / BF16X3_PEAK_TFLOPS, 4) if (h16 and achieved) else None)}
+
+
+def tower_bytes(T, R, U, layers=2):
+    """Algorithmic HBM bytes of one rsx_tower_fwd / rsx_tower_bwd call (csrc/tower.hip, the packed user
+    tower of v1_refine_usertower.py:417-510 and its backward): every activation row each launch of the
+    program reads and writes once, fp32 (a d-row is 512 B, a QKV row 1,536 B, an FFN row 1,024 B), plus
+    8 B of LayerNorm statistics per normed row; weights (< 1 MB per layer) and the step's index arrays
+    are not counted. T = packed tokens of both views, R = the tail rows (T/2 + B: the last layer past its
+    attention and the head run on those), U = 2B user rows. -> (forward bytes, backward bytes)."""
+    d, q, f, st = 512, 1536, 1024, 8
+    fwd = 2 * d * T                          # item_proj
+    fwd += (2064 + st) * T                   # embedding stage (SURVEY 8d: 3 live rows + out + ids) + stats
+    fwd += (2 * d + st) * T                  # first norm1
+    bwd = 0
+    for layer in range(layers):
+        P = R if layer == layers - 1 else T  # rows past the attention
+        fwd += (d + q) * T + (q + d + 16) * T             # in_proj; attention (+ lse)
+        if P != T:
+            fwd += 2 * d * P                              # tail: the residual rows gathered
+        fwd += (4 * d + st) * P                           # out_proj + residual + norm2
+        fwd += (d + 2 * f) * P + (f + d) * P              # FFN1 (gelu' and act), FFN2
+        fwd += (4 * d + st) * P if layer < layers - 1 else 3 * d * P  # residual + next norm1 / closing add
+        bwd += (5 * d + st) * P if layer < layers - 1 else 2 * d * P  # next norm1 backward / dropout backward
+        bwd += (d + 2 * f) * P + (d + f) * P + (f + d) * P + (f + d) * P  # dGELU, dW2, dW1, dX of FFN1
+        bwd += (5 * d + st) * P + 2 * d * P + 2 * d * P   # norm2 backward, dX / dW of out_proj
+        if P != T:
+            bwd += 2 * d * T                              # tail: residual gradient expanded to every row
+        bwd += (q + 2 * d + 16 + q) * T                   # attention backward
+        bwd += (q + d) * T + (q + d) * T                  # dX / dW of in_proj
+    fwd += 2 * d * U + 2 * d * R + (2 * d + st) * R + 2 * d * R + (2 * d + 4) * R  # head (profile, rowadd, LN+GELU, proj, norm)
+    bwd += (3 * d + 4) * R + 2 * d * R + 2 * d * R + (3 * d + st) * R + d * R    # head: norm, proj dX/dW, LN+GELU
+    bwd += 2 * d * R + 2 * d * R + 4 * d * U                                     # output_proj[0]: dX, dW, profile half
+    bwd += (4 * d + st) * T + 3584 * T + 2 * d * T  # first norm1; embedding backward (DESIGN 4); item_proj dW
+    return fwd, bwd
+
+
+def tower_roofline(tb, steps, warmup):
+    """The user tower program's HBM roofline: tower_bytes per launch over the average
+    launch time of rsx_tower_fwd / rsx_tower_bwd (HIP events around each native call, timed steps)."""
+    kt = tb["kernel_times"]
+    out = {}
+    T = [2 * n for n in tb["n_tok"]]
+    B = tb.get("users_local")
+    if not B:
+        return None
+    for name, idx in (("tower_fwd", 0), ("tower_bwd", 1)):
+        n, ms = kt.get(name, (0, 0.0))
+        if not n:
+            return None
+        by = sum(tower_bytes(T[i % 2], T[i % 2] // 2 + B, 2 * B)[idx] for i in range(warmup, warmup + steps)) / steps
+        avg = ms / n / 1e3
+        out[name] = {"bound": "hbm", "avg_launch_ms": round(avg * 1e3, 4), "algorithmic_bytes": int(by),
+                     "bytes_per_packed_token": round(by / (sum(T) / 2), 1),
+                     "achieved": round(by / avg / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(by / avg / 1e9 / HBM_PEAK_GBS, 4)}
+    tr = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r06_tower_traffic_b8192.json")
+    if os.path.exists(tr):
+        with open(tr) as f:
+            t = json.load(f)
+        for name in ("tower_fwd", "tower_bwd"):
+            if name in t and name in out:
+                out[name]["traffic"] = t[name].get("hbm_bytes_per_call")
+                out[name]["traffic_source"] = os.path.basename(tr)
+    out["model"] = ("bench.tower_bytes: each activation row read / written once per launch of the program, fp32; "
+                    "weights and index arrays not counted")
+    return out
 
 
 def gather_roofline(args, tb):
@@ -1163,6 +1305,7 @@ def main():
                    "dense_projection_blas": args.blas, "nce_logit_precision": args.nce_precision},
         "roofline": nce_roofline(args, tb, args.batch, rank, world, args.nce_precision),
         "gather_roofline": gather_roofline(args, tb),
+        "tower_roofline": tower_roofline(tb, args.steps, args.warmup),
         "host_enqueue_ms_per_step": tb["host_enqueue_ms"],
         "host_ms_per_step_unloaded": tb["host_unloaded"],
         "alloc_retries": tb["alloc_retries"],
@@ -1271,6 +1414,8 @@ def main():
             line["gpu_over_cpu"] = round(line["value"] / line["cpu_baseline"]["value"], 1)
         del it_model, it_inputs
         result["secondary_item_refresh"] = bench_item_refresh(args, device)
+        result["secondary_simcse_train"] = [bench_simcse_train(args, device, B) for B in (192, 768)]
+        torch.cuda.empty_cache()
         result["secondary_hnm"] = bench_hnm(args, device)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, items, cfg, args.batch, args.seed + 100, device)

@@ -36,6 +36,15 @@ constexpr int kMaxF = 64;
 constexpr int kFC = 13;          // fields per chunk
 constexpr int kBM = 64;          // rows per workgroup
 constexpr int kN1 = 256, kN2 = 128;
+
+// element offset of lane half h's 8-element chunk of W2 row n2 in k-step ks ([16][128][2][8] image):
+// the two 16-B halves of a row are swapped on bit 3 of n2, so the 16 lanes (c = 0..15 or 16..31, one
+// h) of a ds_read_b128 group cover all 64 banks when the image is read from LDS (deepfm_rows2m_k);
+// without it lanes c and c + 8 hit the same banks (1.05e6 conflicts per call, r05 PMC)
+__device__ __host__ __forceinline__ int w2_off(int ks, int n2, int h) {
+  return ((ks * kN2 + n2) * 2 + (h ^ ((n2 >> 3) & 1))) * 8;
+}
+
 constexpr int kChunkElems = kFC * kBM * 16;  // bf16 per image per chunk
 
 struct FArgs {
@@ -272,7 +281,7 @@ __global__ __launch_bounds__(512, 1) void deepfm_fused_k(FArgs a) {
 #pragma unroll
       for (int j2 = 0; j2 < 2; ++j2) {
         const int n2 = 64 * half + 32 * j2 + c;
-        const int64_t o = (((int64_t)ks * kN2 + n2) * 2 + h) * 8;
+        const int64_t o = w2_off(ks, n2, h);
         const bf16x8 ah = *reinterpret_cast<const bf16x8*>(a.w2hi + o);
         const bf16x8 al = *reinterpret_cast<const bf16x8*>(a.w2lo + o);
 #pragma unroll
@@ -312,7 +321,8 @@ __global__ __launch_bounds__(256) void deepfm_prep_k(const float* w1, int F, int
   }
   const int64_t j = i - n1;
   if (j < 16 * kN2 * 16) {
-    const int el = (int)(j % 8), hh = (int)((j / 8) % 2), n2 = (int)((j / 16) % kN2), ks = (int)(j / (16 * kN2));
+    const int el = (int)(j % 8), hs = (int)((j / 8) % 2), n2 = (int)((j / 16) % kN2), ks = (int)(j / (16 * kN2));
+    const int hh = hs ^ ((n2 >> 3) & 1);  // the stored half (w2_off's swizzle)
     const int k = 16 * ks + 8 * (el >> 2) + 4 * hh + (el & 3);
     const float v = w2[(int64_t)n2 * kN1 + k];
     const __bf16 hv = (__bf16)v;
@@ -865,7 +875,7 @@ __global__ __launch_bounds__(256, 1) void deepfm_rows_k(RArgs a) {
     const int half = st >> 4, t = st & 15, b = st % (P + 1);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      const int o = ((t * kN2 + 32 * (2 * half + q) + c) * 2 + h) * 8;
+      const int o = w2_off(t, 32 * (2 * half + q) + c, h);
       w2h[b][q] = *reinterpret_cast<const bf16x8*>(a.w2hi + o);
       w2l[b][q] = *reinterpret_cast<const bf16x8*>(a.w2lo + o);
     }
@@ -1109,7 +1119,7 @@ __global__ __launch_bounds__(320, 1) void deepfm_rows5_k(RArgs a) {
     const int half = st >> 4, t = st & 15, b = st % (P + 1);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      const int o = ((t * kN2 + 32 * (2 * half + q) + c) * 2 + h) * 8;
+      const int o = w2_off(t, 32 * (2 * half + q) + c, h);
       w2h[b][q] = *reinterpret_cast<const bf16x8*>(a.w2hi + o);
       w2l[b][q] = *reinterpret_cast<const bf16x8*>(a.w2lo + o);
     }
@@ -1484,7 +1494,7 @@ __global__ __launch_bounds__(512 / MT, 1) void deepfm_rows2m_k(RArgs a) {
     const int half = st >> 4, t = st & 15, b = st & 1;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {  // piece 4 t + 2 half + q of each image; 16 B at lane (c, h)
-      const int p = 4 * t + 2 * half + q, o = (2 * c + h) * 16;
+      const int p = 4 * t + 2 * half + q, o = 2 * (w2_off(0, c, h));  // bytes within the piece
       w2h[b][q] = *reinterpret_cast<const bf16x8*>(lds + 1024 * p + o);
       w2l[b][q] = *reinterpret_cast<const bf16x8*>(lds + 1024 * (64 + p) + o);
     }

@@ -275,6 +275,149 @@ __global__ __launch_bounds__(64) void mha_bwd_k(BwdArgs a) {
   }
 }
 
+// ---- backward for head dim 64 (the item tower's bert-base text encoder under grad) -------------
+// One wave per (sequence, head), fp32 on the VALU (the attention is ~1 % of a BERT layer's FLOPs; the
+// GEMMs around it carry the step). Pass 0: lane j holds key / value row j in registers and walks the
+// queries i (Q_i, dO_i broadcast from LDS), writing dS_ij and the dropped-out probability Pd_ij to LDS
+// (mha_bwd_k's formulas: same mask, dropout hash and softmax). Then dK_j = sum_i dS_ij Q_i and
+// dV_j = sum_i Pd_ij dO_i (lane j), and dQ_i = sum_j dS_ij K_j (lane i), 64 accumulators each.
+// LM = the longest sequence the launch may hold (32: 33 KB of LDS, four waves per CU; 64: 81 KB).
+template <int LM>
+__global__ __launch_bounds__(64) void mha_bwd64_k(BwdArgs a) {
+  constexpr int DH = 64, V4 = DH / 4;
+  __shared__ __attribute__((aligned(16))) float sQ[LM][DH];
+  __shared__ __attribute__((aligned(16))) float sK[LM][DH];
+  __shared__ __attribute__((aligned(16))) float sdO[LM][DH];
+  __shared__ float sDS[LM][LM + 1], sPD[LM][LM + 1];
+  __shared__ float sLse[LM], sDelta[LM];
+  __shared__ int sPad[LM];
+  const int D = a.H * DH;
+  const int b = blockIdx.x / a.H, hd = blockIdx.x % a.H;
+  const int lane = threadIdx.x;
+  const int64_t tok0 = a.seg ? (int64_t)a.seg[b] : (int64_t)b * a.L;
+  int L = a.seg ? (a.seg[b + 1] - a.seg[b]) : a.L;
+  if (L > LM) L = LM;  // the host sizes LM by the longest sequence
+  const float* base = a.qkv + tok0 * 3 * D;
+  const float* dob = a.dout + tok0 * D;
+  for (int t = lane; t < L * V4; t += 64) {
+    const int r = t / V4, c4 = t % V4;
+    const float4* rowp = reinterpret_cast<const float4*>(base + (int64_t)r * 3 * D);
+    reinterpret_cast<float4*>(&sQ[r][0])[c4] = rowp[(hd * DH) / 4 + c4];
+    reinterpret_cast<float4*>(&sK[r][0])[c4] = rowp[(D + hd * DH) / 4 + c4];
+    reinterpret_cast<float4*>(&sdO[r][0])[c4] = reinterpret_cast<const float4*>(dob + (int64_t)r * D + hd * DH)[c4];
+  }
+  if (lane < L) {
+    sPad[lane] = a.kpad ? (int)a.kpad[tok0 + lane] : 0;
+    sLse[lane] = a.lse[(tok0 + lane) * a.H + hd];
+    const float4* op = reinterpret_cast<const float4*>(a.out + (tok0 + lane) * D + hd * DH);
+    const float4* dp = reinterpret_cast<const float4*>(dob + (int64_t)lane * D + hd * DH);
+    float d = 0.0f;
+#pragma unroll
+    for (int t = 0; t < V4; ++t) {
+      const float4 x = op[t], y = dp[t];
+      d += x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
+    }
+    sDelta[lane] = d;
+  }
+  __syncthreads();
+  const int j = lane;
+  const bool jok = j < L;
+  {  // pass 0
+    float kj[DH], vj[DH];
+    if (jok) {
+      const float4* vp = reinterpret_cast<const float4*>(base + (int64_t)j * 3 * D + 2 * D + hd * DH);
+#pragma unroll
+      for (int t = 0; t < V4; ++t) {
+        const float4 kk = reinterpret_cast<const float4*>(&sK[j][0])[t];
+        const float4 vv = vp[t];
+        kj[4 * t] = kk.x; kj[4 * t + 1] = kk.y; kj[4 * t + 2] = kk.z; kj[4 * t + 3] = kk.w;
+        vj[4 * t] = vv.x; vj[4 * t + 1] = vv.y; vj[4 * t + 2] = vv.z; vj[4 * t + 3] = vv.w;
+      }
+    }
+    const bool jpad = jok ? (sPad[j] != 0) : true;
+    for (int i = 0; i < L; ++i) {
+      const float lse_i = sLse[i];
+      float ds = 0.0f, pd = 0.0f;
+      if (jok && !jpad && (!a.causal || j <= i) && lse_i != -INFINITY) {
+        float sdot = 0.0f, pdot = 0.0f;
+#pragma unroll
+        for (int t = 0; t < V4; ++t) {
+          const float4 qv = reinterpret_cast<const float4*>(&sQ[i][0])[t];
+          const float4 gv = reinterpret_cast<const float4*>(&sdO[i][0])[t];
+          sdot = fmaf(qv.x, kj[4 * t], sdot); sdot = fmaf(qv.y, kj[4 * t + 1], sdot);
+          sdot = fmaf(qv.z, kj[4 * t + 2], sdot); sdot = fmaf(qv.w, kj[4 * t + 3], sdot);
+          pdot = fmaf(gv.x, vj[4 * t], pdot); pdot = fmaf(gv.y, vj[4 * t + 1], pdot);
+          pdot = fmaf(gv.z, vj[4 * t + 2], pdot); pdot = fmaf(gv.w, vj[4 * t + 3], pdot);
+        }
+        const float p = __expf(sdot * a.scale - lse_i);
+        const uint64_t idx = ((uint64_t)(tok0 + i) * a.H + hd) * kLMax + j;
+        pd = p;
+        float dp = pdot;
+        if (a.drop.active()) {
+          const bool keep = rsx::hash_u32(a.drop.seed, idx) >= a.drop.thresh;
+          pd = keep ? p * a.drop.scale : 0.0f;
+          dp = keep ? pdot * a.drop.scale : 0.0f;
+        }
+        ds = p * (dp - sDelta[i]) * a.scale;
+      }
+      if (j < LM) {
+        sDS[i][j] = ds;
+        sPD[i][j] = pd;
+      }
+    }
+  }
+  __syncthreads();
+  float* db = a.dqkv + tok0 * 3 * D;
+  float acc[DH];
+  if (jok) {  // dK_j
+#pragma unroll
+    for (int e = 0; e < DH; ++e) acc[e] = 0.0f;
+    for (int i = 0; i < L; ++i) {
+      const float w = sDS[i][j];
+#pragma unroll
+      for (int t = 0; t < V4; ++t) {
+        const float4 qv = reinterpret_cast<const float4*>(&sQ[i][0])[t];
+        acc[4 * t] = fmaf(w, qv.x, acc[4 * t]); acc[4 * t + 1] = fmaf(w, qv.y, acc[4 * t + 1]);
+        acc[4 * t + 2] = fmaf(w, qv.z, acc[4 * t + 2]); acc[4 * t + 3] = fmaf(w, qv.w, acc[4 * t + 3]);
+      }
+    }
+    float4* kp = reinterpret_cast<float4*>(db + (int64_t)j * 3 * D + D + hd * DH);
+#pragma unroll
+    for (int t = 0; t < V4; ++t) kp[t] = make_float4(acc[4 * t], acc[4 * t + 1], acc[4 * t + 2], acc[4 * t + 3]);
+#pragma unroll
+    for (int e = 0; e < DH; ++e) acc[e] = 0.0f;  // dV_j
+    for (int i = 0; i < L; ++i) {
+      const float w = sPD[i][j];
+#pragma unroll
+      for (int t = 0; t < V4; ++t) {
+        const float4 gv = reinterpret_cast<const float4*>(&sdO[i][0])[t];
+        acc[4 * t] = fmaf(w, gv.x, acc[4 * t]); acc[4 * t + 1] = fmaf(w, gv.y, acc[4 * t + 1]);
+        acc[4 * t + 2] = fmaf(w, gv.z, acc[4 * t + 2]); acc[4 * t + 3] = fmaf(w, gv.w, acc[4 * t + 3]);
+      }
+    }
+    float4* vq = reinterpret_cast<float4*>(db + (int64_t)j * 3 * D + 2 * D + hd * DH);
+#pragma unroll
+    for (int t = 0; t < V4; ++t) vq[t] = make_float4(acc[4 * t], acc[4 * t + 1], acc[4 * t + 2], acc[4 * t + 3]);
+  }
+  const int i = lane;
+  if (i < L) {  // dQ_i
+#pragma unroll
+    for (int e = 0; e < DH; ++e) acc[e] = 0.0f;
+    for (int jj = 0; jj < L; ++jj) {
+      const float w = sDS[i][jj];
+#pragma unroll
+      for (int t = 0; t < V4; ++t) {
+        const float4 kv = reinterpret_cast<const float4*>(&sK[jj][0])[t];
+        acc[4 * t] = fmaf(w, kv.x, acc[4 * t]); acc[4 * t + 1] = fmaf(w, kv.y, acc[4 * t + 1]);
+        acc[4 * t + 2] = fmaf(w, kv.z, acc[4 * t + 2]); acc[4 * t + 3] = fmaf(w, kv.w, acc[4 * t + 3]);
+      }
+    }
+    float4* qp = reinterpret_cast<float4*>(db + (int64_t)i * 3 * D + hd * DH);
+#pragma unroll
+    for (int t = 0; t < V4; ++t) qp[t] = make_float4(acc[4 * t], acc[4 * t + 1], acc[4 * t + 2], acc[4 * t + 3]);
+  }
+}
+
 // ---- backward on the fp32-input MFMA (head dim 32) ---------------------------------------
 // One wave per (sequence, head), four independent waves per workgroup, no LDS: every MFMA
 // operand is either a token row the lane loads itself (16 contiguous floats of dims
@@ -1696,7 +1839,7 @@ RSX_API int rsx_mha_bwd(const float* qkv, const uint8_t* key_pad, const int* seg
                         float p_drop, uint64_t seed, float* dqkv, void* stream) {
   RSX_ARG(qkv && out && lse && dout && dqkv, "null tensor");
   RSX_ARG(L >= 1 && L <= kLMax, "L must be in [1,64]");
-  RSX_ARG(Dh == 16 || Dh == 32, "backward head dim must be 16 or 32");
+  RSX_ARG(Dh == 16 || Dh == 32 || Dh == 64, "backward head dim must be 16, 32 or 64");
   RSX_ARG(p_drop >= 0.0f && p_drop < 1.0f, "p_drop must be in [0,1)");
   if (B == 0) return 0;
   BwdArgs a;
@@ -1707,6 +1850,8 @@ RSX_API int rsx_mha_bwd(const float* qkv, const uint8_t* key_pad, const int* seg
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)(B * H));
   if (Dh == 16) hipLaunchKernelGGL(mha_bwd_k<16>, grid, dim3(64), 0, st, a);
+  else if (Dh == 64 && L <= 32) hipLaunchKernelGGL(mha_bwd64_k<32>, grid, dim3(64), 0, st, a);  // L: the longest sequence
+  else if (Dh == 64) hipLaunchKernelGGL(mha_bwd64_k<64>, grid, dim3(64), 0, st, a);
   else hipLaunchKernelGGL(mha_bwd_mfma_k, dim3((unsigned)((B * H + 3) / 4)), dim3(256), 0, st, a);
   RSX_LAUNCHED();
   return 0;

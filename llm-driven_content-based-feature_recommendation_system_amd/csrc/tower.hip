@@ -183,14 +183,28 @@ __global__ __launch_bounds__(256) void tw_lastq_fwd_k(LastQ a) {
   }
   float pr = pe / l;
   pr = a.drop.apply(pr, ((uint64_t)q * kHeads + hd) * 64 + lane);
-  const float* vr = a.qkv + kr * kQKV + 2 * kD + kDh * hd;
-  float acc = 0.0f;  // lane d < 32 ends with output dim d
-  for (int d = 0; d < kDh; ++d) {
-    float t = (in && pr != 0.0f) ? pr * vr[d] : 0.0f;
-    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
-    if (lane == d) acc = t;
+  // out[d] = sum_k pr_k V_k[d]: each lane writes its pr_k V_k row to LDS, lane d sums column d (one
+  // pass over the keys instead of a 6-step wave reduction per output dim)
+  __shared__ float sP[kHeads][64][kDh + 1];
+  {
+    const float* vr = a.qkv + kr * kQKV + 2 * kD + kDh * hd;
+#pragma unroll
+    for (int e = 0; e < kDh; e += 4) {
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (in && pr != 0.0f) v = *reinterpret_cast<const float4*>(vr + e);
+      sP[hd][lane][e] = pr * v.x;
+      sP[hd][lane][e + 1] = pr * v.y;
+      sP[hd][lane][e + 2] = pr * v.z;
+      sP[hd][lane][e + 3] = pr * v.w;
+    }
   }
-  if (lane < kDh) orow[lane] = acc;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS stores done
+  if (lane < kDh) {
+    float acc = 0.0f;  // keys in order 0..len-1 (rows past len hold zeros)
+    for (int k = 0; k < len; ++k) acc += sP[hd][k][lane];
+    orow[lane] = acc;
+  }
   if (lane == 0) a.lse[j * kHeads + hd] = m + logf(l);
 }
 
@@ -226,14 +240,22 @@ __global__ __launch_bounds__(256) void tw_lastq_bwd_k(LastQ a) {
   float sdp = p * dp;
   for (int o = 32; o > 0; o >>= 1) sdp += __shfl_xor(sdp, o, 64);
   const float ds = valid ? p * (dp - sdp) * 0.17677669529663687f : 0.0f;  // dL/dscore, scale folded in
-  // dQ = sum_k ds_k K_k (lane d < 32 ends with dim d)
-  float dq = 0.0f;
-  for (int d = 0; d < kDh; ++d) {
-    float t = valid ? ds * kk[d] : 0.0f;
-    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
-    if (lane == d) dq = t;
+  // dQ = sum_k ds_k K_k: each lane's ds_k K_k row to LDS, lane d sums column d
+  __shared__ float sP[kHeads][64][kDh + 1];
+#pragma unroll
+  for (int e = 0; e < kDh; e += 4) {
+    float4 kv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (valid) kv = *reinterpret_cast<const float4*>(kk + e);
+    sP[hd][lane][e] = ds * kv.x;
+    sP[hd][lane][e + 1] = ds * kv.y;
+    sP[hd][lane][e + 2] = ds * kv.z;
+    sP[hd][lane][e + 3] = ds * kv.w;
   }
-  const float dq_d = dq;  // lanes 0..31 hold dQ
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS stores done
+  float dq_d = 0.0f;  // lanes 0..31 hold dQ
+  if (lane < kDh)
+    for (int k = 0; k < len; ++k) dq_d += sP[hd][k][lane];
   if (in) {
     float* drow = a.dqkv + kr * kQKV;
     const float pd = valid ? a.drop.apply(p, ((uint64_t)q * kHeads + hd) * 64 + lane) : 0.0f;  // D_k P_k

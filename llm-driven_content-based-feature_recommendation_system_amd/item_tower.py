@@ -23,6 +23,7 @@ and ``simcse_train_step`` is its per-batch GPU step.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 from typing import Optional
 
@@ -114,6 +115,21 @@ def build_local_bert(hidden_size: int = 768, num_layers: int = 12, num_heads: in
     return BertModel(cfg)
 
 
+# RSX_BERT_TRAIN_NATIVE=0: the text BERT under grad runs through transformers' BertModel (A/B)
+_BERT_TRAIN_NATIVE = os.environ.get("RSX_BERT_TRAIN_NATIVE", "1") != "0"
+
+
+@contextlib.contextmanager
+def bert_train_native(on: bool):
+    """Temporarily route HybridItemTower's BERT under grad through bert_cls_packed_train (on) or BertModel."""
+    global _BERT_TRAIN_NATIVE
+    prev, _BERT_TRAIN_NATIVE = _BERT_TRAIN_NATIVE, bool(on)
+    try:
+        yield
+    finally:
+        _BERT_TRAIN_NATIVE = prev
+
+
 def _bert_qkv(att_self):
     """[3D, D] weight / [3D] bias of BertSelfAttention's query, key, value concatenated (the
     qkv row layout of rsx_mha_fwd: Q | K | V, head h at columns h*dh), rebuilt when one changes."""
@@ -181,6 +197,56 @@ def bert_cls_packed(bert, input_ids, attn_mask):
         inter = _bert_linear(h, layer.intermediate.dense, gelu=True)
         ln = layer.output.LayerNorm
         h = ops.add_layer_norm_infer(_bert_linear(inter, layer.output.dense), h, ln.weight, ln.bias, ln.eps)
+    if len(layers) == 0:
+        h = h[cls_rows]
+    return h
+
+
+def bert_cls_packed_train(bert, input_ids, attn_mask):
+    """BertModel(input_ids, attention_mask).last_hidden_state[:, 0] under autograd, for the SimCSE
+    training step (item_tower.py:264-272 with BERT fine-tuned at lr 1e-5, :1012-1022), over the packed
+    valid tokens: the embedding sum (word + position = column index + token type 0) and its LayerNorm,
+    then per layer the fused QKV token linear (bf16x3 GEMM forward / dX, split-K weight gradient), the
+    varlen attention (bf16x3 forward, the head-dim-64 fp32 backward mha_bwd64_k), the out-projection,
+    residual + dropout + LayerNorm (one kernel each way), the GELU feed-forward (GELU in the GEMM
+    epilogue) and the second residual + LayerNorm. The last layer's attention output, out-projection
+    and feed-forward run on the [CLS] rows only (the only rows read); its keys and values still see
+    every token. Dropout: attention probabilities and the two residual branches by the library's counter
+    hash, the embedding output by torch (BertModel's placements; its RNG stream is not reproduced).
+    Call only when bert_packed_ok()."""
+    B, S = input_ids.shape
+    m = attn_mask != 0
+    flat = m.reshape(-1).nonzero().squeeze(1)
+    seg = torch.zeros(B + 1, device=input_ids.device, dtype=torch.int64)
+    seg[1:] = torch.cumsum(m.sum(dim=1), 0)
+    cls_rows = seg[:-1]
+    seg32 = seg.to(torch.int32)
+    emb = bert.embeddings
+    ids = input_ids.reshape(-1)[flat]
+    pos = flat % S
+    x = emb.word_embeddings(ids) + emb.position_embeddings(pos) + emb.token_type_embeddings(torch.zeros_like(ids))
+    h = ops.layer_norm(x, emb.LayerNorm.weight, emb.LayerNorm.bias, emb.LayerNorm.eps)
+    cfg = bert.config
+    p_h = cfg.hidden_dropout_prob if bert.training else 0.0
+    p_a = cfg.attention_probs_dropout_prob if bert.training else 0.0
+    h = F.dropout(h, p_h, bert.training)
+    H = cfg.num_attention_heads
+    layers = bert.encoder.layer
+    for li, layer in enumerate(layers):
+        att = layer.attention
+        sa = att.self
+        wqkv = torch.cat([sa.query.weight, sa.key.weight, sa.value.weight], 0)
+        bqkv = torch.cat([sa.query.bias, sa.key.bias, sa.value.bias], 0)
+        ctx = ops.mha(ops.linear_tok(h, wqkv, bqkv), None, H, causal=False, p_drop=p_a, seg_off=seg32, max_len=S)
+        if li == len(layers) - 1:
+            ctx, h = ctx[cls_rows], h[cls_rows]
+        ln = att.output.LayerNorm
+        _, h = ops.add_layer_norm(h, ops.linear_tok(ctx, att.output.dense.weight, att.output.dense.bias), ln.weight,
+                                  ln.bias, ln.eps, p_drop=p_h)
+        f = ops.ffn(h, layer.intermediate.dense.weight, layer.intermediate.dense.bias, layer.output.dense.weight,
+                    layer.output.dense.bias, p_drop=0.0)
+        ln = layer.output.LayerNorm
+        _, h = ops.add_layer_norm(h, f, ln.weight, ln.bias, ln.eps, p_drop=p_h)
     if len(layers) == 0:
         h = h[cls_rows]
     return h
@@ -268,6 +334,9 @@ class HybridItemTower(nn.Module):
         if (not torch.is_grad_enabled() and not self.bert_model.training
                 and bert_packed_ok(self.bert_model, text_input_ids, text_attn_mask)):
             cls = bert_cls_packed(self.bert_model, text_input_ids, text_attn_mask)       # inference
+        elif (torch.is_grad_enabled() and _BERT_TRAIN_NATIVE
+              and bert_packed_ok(self.bert_model, text_input_ids, text_attn_mask)):
+            cls = bert_cls_packed_train(self.bert_model, text_input_ids, text_attn_mask)  # training (SimCSE)
         else:
             cls = self.bert_model(input_ids=text_input_ids, attention_mask=text_attn_mask).last_hidden_state[:, 0, :]
         t = self.text_proj

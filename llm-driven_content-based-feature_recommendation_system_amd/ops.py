@@ -246,7 +246,7 @@ def _mha_x3_fwd(Dh):  # the bf16x3 forward also covers head dim 64 (BERT inferen
 
 class _MHA(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, key_pad, seg_off, H, causal, p_drop, seed):
+    def forward(ctx, qkv, key_pad, seg_off, H, causal, p_drop, seed, max_len=None):
         N.ensure_device(qkv)
         qkv = _c(qkv)
         D3 = qkv.shape[-1]
@@ -255,8 +255,8 @@ class _MHA(torch.autograd.Function):
         Dh = D // H
         if seg_off is None:
             B, L = qkv.shape[0], qkv.shape[1]
-        else:
-            B, L = seg_off.numel() - 1, 64
+        else:  # packed: L bounds the segment lengths (the head-dim-64 backward sizes its LDS by it)
+            B, L = seg_off.numel() - 1, int(max_len) if max_len else 64
         out = torch.empty(qkv.shape[:-1] + (D,), device=qkv.device, dtype=torch.float32)
         lse = torch.empty(T, H, device=qkv.device, dtype=torch.float32)
         kp = None
@@ -280,7 +280,7 @@ class _MHA(torch.autograd.Function):
         rc = fn(N.ptr(qkv), N.ptr(kp), N.ptr(seg_off), N.ptr(out), N.ptr(lse), N.ptr(dout), B, L, H, Dh, causal,
                 p_drop, seed, N.ptr(dqkv), N.stream())
         N.check(rc, "mha_bwd")
-        return dqkv, None, None, None, None, None, None
+        return dqkv, None, None, None, None, None, None, None
 
 
 class _QKVMHA(torch.autograd.Function):
@@ -352,12 +352,13 @@ def qkv_mha(x, w, b, key_pad, num_heads, causal, p_drop=0.0, seg_off=None):
     return mha(linear_tok(x, w, b), key_pad, num_heads, causal, p_drop, seg_off)
 
 
-def mha(qkv, key_pad, num_heads, causal, p_drop=0.0, seg_off=None):
-    """Dense: qkv [B, L, 3D], key_pad [B, L]. Packed: qkv [T, 3D], key_pad [T], seg_off [B+1] int32."""
+def mha(qkv, key_pad, num_heads, causal, p_drop=0.0, seg_off=None, max_len=None):
+    """Dense: qkv [B, L, 3D], key_pad [B, L]. Packed: qkv [T, 3D], key_pad [T], seg_off [B+1] int32;
+    max_len (packed, optional) = an upper bound of the segment lengths (<= 64)."""
     seed = next_seed() if p_drop > 0 else 0
     if seg_off is not None:
         seg_off = _c(seg_off.to(torch.int32))
-    return _MHA.apply(qkv, key_pad, seg_off, int(num_heads), bool(causal), float(p_drop), seed)
+    return _MHA.apply(qkv, key_pad, seg_off, int(num_heads), bool(causal), float(p_drop), seed, max_len)
 
 
 # ----------------------------------------------------------------------------------------

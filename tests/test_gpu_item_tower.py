@@ -299,6 +299,61 @@ def test_bert_cls_packed_matches_bertmodel(gpu, hidden, heads, layers):
     torch.testing.assert_close(got, want, atol=2e-4, rtol=1e-4)
 
 
+@pytest.mark.parametrize("hidden,heads,layers,S", [(768, 12, 2, 32), (256, 4, 2, 48), (512, 8, 1, 24)])
+def test_bert_cls_packed_train_matches_bertmodel(gpu, hidden, heads, layers, S):
+    """The packed BERT under autograd (item_tower.bert_cls_packed_train: bf16x3 token GEMMs, varlen
+    attention with the fp32 head-dim-64 backward, fused residual + LayerNorm both ways, [CLS]-only last
+    layer) against HF BertModel's dense masked forward and backward, eval mode (dropout off): the [CLS]
+    rows atol 2e-4 / rtol 1e-4, every parameter gradient of a random projection of them within 1e-3 of
+    that gradient's scale (max |g|) -- the SimCSE step's BERT fine-tuning (item_tower.py:264-272)."""
+    ref = IT.build_local_bert(hidden_size=hidden, num_layers=layers, num_heads=heads, intermediate=4 * hidden,
+                              vocab_size=2000, max_position=64, seed=11).to(gpu).eval()
+    dut = copy.deepcopy(ref)
+    g = torch.Generator().manual_seed(hidden + S)
+    B = 40
+    tl = torch.randint(1, S + 1, (B,), generator=g)
+    tl[0], tl[1] = 1, S
+    mask = (torch.arange(S).view(1, S) < tl.unsqueeze(-1)).long()
+    ids = torch.randint(1000, 2000, (B, S), generator=g) * mask
+    ids[:, 0] = 101
+    ids, mask = ids.to(gpu), mask.to(gpu)
+    w = torch.randn(B, hidden, generator=g).to(gpu)
+    assert IT.bert_packed_ok(dut, ids, mask)
+    got = IT.bert_cls_packed_train(dut, ids, mask)
+    want = ref(input_ids=ids, attention_mask=mask).last_hidden_state[:, 0, :]
+    torch.testing.assert_close(got.detach(), want.detach(), atol=2e-4, rtol=1e-4)
+    (got * w).sum().backward()
+    (want * w).sum().backward()
+    used = 0
+    # the key bias's gradient is zero in exact arithmetic (a shift of every key adds a per-row constant to the
+    # scores): both sides hold rounding noise there, judged against the largest gradient of the model
+    floor = 1e-4 * max(float(p.grad.abs().max()) for p in ref.parameters() if p.grad is not None)
+    for (n, pr), (_, pd) in zip(ref.named_parameters(), dut.named_parameters()):
+        if pr.grad is None:                     # the pooler: not on the [CLS]-hidden path
+            assert pd.grad is None or not pd.grad.any(), n
+            continue
+        used += 1
+        scale = max(float(pr.grad.abs().max()), floor if n.endswith("key.bias") else 0.0) + 1e-30
+        err = float((pd.grad - pr.grad).abs().max()) / scale
+        assert err <= 1e-3, (n, err)
+    assert used == 5 + 16 * layers
+
+
+def test_bert_train_dropout_active(gpu):
+    """Training mode: the packed path applies BERT's dropouts (two calls differ, both finite, the
+    gradients flow to every encoder weight)."""
+    bert = IT.build_local_bert(hidden_size=256, num_layers=2, num_heads=4, intermediate=1024, vocab_size=2000,
+                               max_position=64, seed=12).to(gpu).train()
+    x = [t.to(gpu) for t in _inputs(16, seed=6)]
+    a = IT.bert_cls_packed_train(bert, x[3], x[4])
+    b = IT.bert_cls_packed_train(bert, x[3], x[4])
+    assert torch.isfinite(a).all() and not torch.equal(a, b)
+    a.sum().backward()
+    for n, p in bert.named_parameters():
+        if "pooler" not in n:
+            assert p.grad is not None and torch.isfinite(p.grad).all(), n
+
+
 def test_item_tower_inference_uses_packed_bert_and_falls_back(gpu):
     """HybridItemTower under no_grad + eval takes the packed BERT (same vectors as the module
     path with gradients enabled); a batch whose position 0 is masked in some row is not
@@ -308,7 +363,8 @@ def test_item_tower_inference_uses_packed_bert_and_falls_back(gpu):
     torch.manual_seed(1)
     tower = IT.HybridItemTower(384, 6, 128, 128, bert_model=bert).to(gpu).eval()
     x = [t.to(gpu) for t in _inputs(32, seed=4)]
-    want = tower(*x).detach()                                      # grad enabled: BertModel
+    with IT.bert_train_native(False):
+        want = tower(*x).detach()                                  # grad enabled, native train path off: BertModel
     with torch.no_grad():
         got = tower(*x)
     torch.testing.assert_close(got, want, atol=2e-4, rtol=1e-4)

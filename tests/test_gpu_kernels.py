@@ -182,7 +182,9 @@ def mha_precision(request):
 
 @pytest.mark.parametrize("L,H,dh,causal,use_pad", [(50, 4, 32, True, True), (16, 4, 32, False, False),
                                                    (16, 4, 16, False, False), (7, 2, 32, True, False),
-                                                   (64, 4, 32, True, True), (33, 1, 32, False, True)])
+                                                   (64, 4, 32, True, True), (33, 1, 32, False, True),
+                                                   (50, 4, 64, True, True), (20, 2, 64, False, True),
+                                                   (32, 12, 64, False, False)])
 def test_mha_forward_backward(gpu, mha_precision, L, H, dh, causal, use_pad):
     g = torch.Generator().manual_seed(L * 7 + dh)
     B = 33
@@ -205,13 +207,14 @@ def test_mha_forward_backward(gpu, mha_precision, L, H, dh, causal, use_pad):
         assert (out[pad.to(gpu)] == 0).all()
 
 
-@pytest.mark.parametrize("dh", [32, 16])
-def test_mha_packed_segments(gpu, mha_precision, dh):
-    """Packed variable-length segments (seg_off, lengths 1..51, a padded last key in some):
-    outputs and dqkv equal the per-segment dense float64 reference (atol _MHA_TOL)."""
+@pytest.mark.parametrize("dh,max_len", [(32, None), (16, None), (64, None), (64, 32)])
+def test_mha_packed_segments(gpu, mha_precision, dh, max_len):
+    """Packed variable-length segments (seg_off, lengths 1..51 -- 1..32 with max_len 32, the head-dim-64
+    backward's small-LDS instance --, a padded last key in some): outputs and dqkv equal the per-segment
+    dense float64 reference (atol _MHA_TOL)."""
     g = torch.Generator().manual_seed(dh)
     H = 4
-    lens = torch.randint(1, 52, (37,), generator=g)
+    lens = torch.randint(1, (max_len or 51) + 1, (37,), generator=g)
     seg = torch.cat([torch.zeros(1, dtype=torch.long), torch.cumsum(lens, 0)])
     T = int(seg[-1])
     qkv = torch.randn(T, 3 * H * dh, generator=g)
@@ -226,7 +229,7 @@ def test_mha_packed_segments(gpu, mha_precision, dh):
     dout = torch.randn(ref.shape, generator=g, dtype=torch.float64)
     (ref * dout).sum().backward()
     qd = qkv.to(gpu).requires_grad_()
-    out = ops.mha(qd, pad.to(gpu), H, True, seg_off=seg.to(gpu))
+    out = ops.mha(qd, pad.to(gpu), H, True, seg_off=seg.to(gpu), max_len=max_len)
     torch.testing.assert_close(out.cpu().double(), ref.detach(), atol=_MHA_TOL[mha_precision][0], rtol=1e-5)
     (out * dout.float().to(gpu)).sum().backward()
     torch.testing.assert_close(qd.grad.cpu().double(), q64.grad, atol=_MHA_TOL[mha_precision][1], rtol=1e-4)

@@ -15,7 +15,7 @@ PRECISION = sys.argv[9] if len(sys.argv) > 9 else "bf16x3"
 
 def vals(d, counter):
     out = []
-    for f in glob.glob(d + "/*counter_collection.csv"):
+    for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == counter:
                 out.append(float(r["Counter_Value"]))
