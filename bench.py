@@ -865,34 +865,63 @@ def bench_simcse_train(args, device, B=192, iters=3):
         loss, _, _ = IT.simcse_train_step(model, v1, v2, opt)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / iters
-    # BERT alone: forward + backward of both views' text (the CLS rows' gradient seeded with ones)
-    def bert_step():
+    # the same step with the text BERT through transformers' BertModel (the reference's module) instead
+    with IT.bert_train_native(False):
+        IT.simcse_train_step(model, v1, v2, opt)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            IT.simcse_train_step(model, v1, v2, opt)
+        torch.cuda.synchronize()
+        dt_hf = (time.perf_counter() - t0) / iters
+
+    # BERT alone: forward + backward of both views' text (the CLS rows' gradient seeded with ones),
+    # native packed path (what the step runs) and HF BertModel
+    def bert_step(native):
         for v in (v1, v2):
-            cls = bert(input_ids=v[3], attention_mask=v[4]).last_hidden_state[:, 0, :]
+            if native:
+                cls = IT.bert_cls_packed_train(bert, v[3], v[4])
+            else:
+                cls = bert(input_ids=v[3], attention_mask=v[4]).last_hidden_state[:, 0, :]
             cls.sum().backward()
-    bert_step()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(iters):
-        bert_step()
-    torch.cuda.synchronize()
-    bt = (time.perf_counter() - t0) / iters
+
+    def timed(native):
+        bert_step(native)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            bert_step(native)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / iters
+
+    assert IT.bert_packed_ok(bert, v1[3], v1[4]) and IT.bert_packed_ok(bert, v2[3], v2[4])
+    bt = timed(True)
+    bt_hf = timed(False)
     opt.zero_grad(set_to_none=True)
     cfg = bert.config
     Dm, F_, nl = cfg.hidden_size, cfg.intermediate_size, cfg.num_hidden_layers
-    tokens = 2 * B * S  # HF BertModel runs the padded [B, S] grid of both views
-    fwd_flops = nl * tokens * 2 * (4 * Dm * Dm + 2 * Dm * F_) + nl * 2 * (2 * B) * S * S * Dm * 2
+    lens = torch.cat([v1[4].sum(1), v2[4].sum(1)]).double()
+    tok, rows = float(lens.sum()), float(lens.numel())
+    attn = 2 * 2 * float((lens * lens).sum()) * Dm  # S = QK^T and O = PV per layer
+    # the packed path's forward: every layer's QKV and attention on the valid tokens; out-proj and FFN on
+    # every token except in the last layer, which runs them on the [CLS] rows only
+    fwd_flops = (nl * (tok * 2 * 3 * Dm * Dm + attn) + (nl - 1) * tok * 2 * (Dm * Dm + 2 * Dm * F_)
+                 + rows * 2 * (Dm * Dm + 2 * Dm * F_))
     flops = 3 * fwd_flops  # forward + backward (dX and dW)
     return {"metric": f"SimCSE item-tower train step items/sec (two views, batch {B}, bert-base-shaped local BERT "
                       "fine-tuned, AdamW)",
             "value": round(B / dt, 1), "unit": "items/s", "ms_per_step": round(dt * 1e3, 3), "batch": B,
             "loss": round(float(loss.item()), 5),
-            "bert": {"module": "transformers BertModel under grad (both views' text, fwd + bwd)",
+            "ms_per_step_with_hf_bertmodel": round(dt_hf * 1e3, 3),
+            "bert": {"module": "item_tower.bert_cls_packed_train (packed valid tokens, bf16x3 token GEMMs, varlen "
+                               "attention, fused residual+LayerNorm; both views' text, fwd + bwd)",
                      "ms_per_step": round(bt * 1e3, 3), "share_of_step": round(bt / dt, 3),
+                     "valid_tokens": int(tok), "padded_tokens": int(2 * B * S),
                      "flops_per_step": int(flops), "achieved_TFLOPs": round(flops / bt / 1e12, 2),
-                     "peak_TFLOPs": FP32_MFMA_PEAK_TFLOPS, "frac": round(flops / bt / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
-                     "note": "HF BertModel in fp32 (torch's library GEMMs); the native packed-token BERT "
-                             "(item_tower.bert_cls_packed) is inference-only"},
+                     "peak_TFLOPs": round(BF16X3_PEAK_TFLOPS, 1), "frac": round(flops / bt / 1e12 / BF16X3_PEAK_TFLOPS, 4),
+                     "peak_note": "bf16 dense MFMA 2516.8 TF / 3 split products (the token GEMMs' arithmetic)",
+                     "hf_bertmodel_ms_per_step": round(bt_hf * 1e3, 3),
+                     "hf_note": "transformers BertModel under grad on the padded [B, S] grid, fp32 (torch's library GEMMs)"},
             "data": "synthetic std / RE / text ids, RE lengths U{2..32}, text lengths U{2..32}, random weights"}
 
 
