@@ -756,6 +756,62 @@ def bench_hnm(args, device):
             "data": "synthetic normalised item table, Gaussian user rows, uniform targets"}
 
 
+def bench_hard_emphasis(args, device, N=16384):
+    """full_batch_hard_emphasis_loss (tower_code/v1_refine_usertower.py:762-822; verdict r5 item 8) forward +
+    backward at N = 16,384 rows, d = 128, 47,063-item table: mining (rsx_hnm_mine) + the masked InfoNCE with
+    the mined columns' margin (ops.nce_emphasis_loss, no N x N tensor). rows/s, and the same loss in the
+    reference's dense form (N x N cosines, emphasis scatter_, masked_fill, F.cross_entropy in torch fp32 on
+    this GPU, same mined columns) timed beside it with its peak memory."""
+    from recsys_amd.tower_code import v1_refine_usertower as T
+    import torch.nn.functional as F
+    I = 47063
+    g = torch.Generator(device="cpu").manual_seed(23)
+    W = F.normalize(torch.randn(I, 128, generator=g), dim=1).to(device).requires_grad_()
+    lq = torch.log_softmax(torch.randn(I, generator=g), 0).to(device)
+    t = torch.randint(1, I, (N,), generator=g).to(device)
+    U = torch.randn(N, 128, generator=g).to(device).requires_grad_()
+    tau, margin = 0.1, 0.2
+
+    def step():
+        loss, st = T.full_batch_hard_emphasis_loss(U, W, t, lq, temperature=tau, hard_margin=margin)
+        loss.backward()
+        return loss
+
+    def dense_step():  # the reference's arithmetic on the same mined columns
+        u, it = F.normalize(U, dim=1), F.normalize(W[t], dim=1)
+        k = max(1, int((N - 1) * 0.01))
+        top, _, _ = T.ops.hnm_mine(u.detach(), it.detach(), t, k, 0.9, 1.0)
+        logits = (u @ it.T) / tau - lq[t].view(1, -1)
+        emph = torch.zeros_like(logits).scatter_(1, top, margin / tau)
+        same = t.view(-1, 1) == t.view(1, -1)
+        same.fill_diagonal_(False)
+        loss = F.cross_entropy((logits + emph).masked_fill(same, float("-inf")), torch.arange(N, device=device))
+        loss.backward()
+        return loss
+
+    out = {}
+    for name, fn in (("native", step), ("dense_torch", dense_step)):
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize()
+        torch.cuda.reset_peak_memory_stats()
+        base = torch.cuda.memory_allocated()
+        iters = 10
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            loss = fn()
+        torch.cuda.synchronize()
+        out[name] = {"ms_per_step": round((time.perf_counter() - t0) / iters * 1e3, 4), "loss": round(float(loss), 6),
+                     "peak_extra_mem_mb": round((torch.cuda.max_memory_allocated() - base) / 2 ** 20, 1)}
+        U.grad = None
+        W.grad = None
+    dt = out["native"]["ms_per_step"] / 1e3
+    return {"metric": f"hard-emphasis loss fwd+bwd rows/sec (full_batch_hard_emphasis_loss, N={N}, d=128)",
+            "value": round(N / dt, 1), "unit": "rows/s", "ms_per_step": out["native"]["ms_per_step"],
+            "k": max(1, int((N - 1) * 0.01)), "native": out["native"], "reference_form_dense_torch": out["dense_torch"],
+            "data": "synthetic normalised item table, Gaussian user rows, uniform targets; tau 0.1, margin 0.2"}
+
+
 def bench_item_refresh(args, device):
     """refresh-item-vectors (utils/inference_utils.py:74-207) on one GPU: the
     endpoint's eval forward over batches of 4 x 192 = 768 products, d = 128 (the serving
@@ -1444,6 +1500,7 @@ def main():
         del it_model, it_inputs
         result["secondary_item_refresh"] = bench_item_refresh(args, device)
         result["secondary_simcse_train"] = [bench_simcse_train(args, device, B) for B in (192, 768)]
+        result["secondary_hard_emphasis"] = bench_hard_emphasis(args, device)
         torch.cuda.empty_cache()
         result["secondary_hnm"] = bench_hnm(args, device)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -142,6 +142,25 @@ int rsx_nce_bwd_x3(const float* A, const float* B, const float* bias, const int*
                    int64_t diag_offset, float tau, int flags, const float* gout, float* ws, float* dA, float* dB,
                    int accumulate, void* stream);
 
+/* Hard-emphasis term of full_batch_hard_emphasis_loss (replaces the reference's dense emphasis tensor,
+ * scatter_ and masked cross-entropy over N x N logits, tower_code/v1_refine_usertower.py:762-822): row i's
+ * K mined columns top[i*K + r] (int64, from rsx_hnm_mine) get +margin (already divided by tau) on top of
+ * the flags-2 objective (k1 = target ids: same-item columns off the label excluded; bias = lambda*logQ).
+ * Call rsx_nce_emphasis_fwd after rsx_nce_fwd / rsx_nce_fwd_x3 on the same ws (precision RSX_NCE_FP32 with
+ * that call's nsplit_fwd, or RSX_NCE_BF16X3): each row's log-sum-exp and loss are corrected in ws from the
+ * K mined logits alone and out2 is recomputed. Then rsx_nce_bwd(_x3) gives the dense gradient and
+ * rsx_nce_emphasis_bwd adds the mined entries' extra (e^margin - 1) softmax weight into dA [N,128] / dB [M,128]
+ * (nullable; dB by vector atomics: the summation order of a column shared by several rows is not fixed).
+ * Mined ids outside [0, M) are skipped. O(N K) work and memory. */
+int rsx_nce_emphasis_fwd(const float* A, const float* B, const float* bias, const int* k1a, const int* k1b,
+                         const int64_t* top, int64_t N, int64_t M, int64_t K, int64_t lda, int64_t ldb,
+                         int64_t diag_offset, float tau, float margin, int precision, int nsplit_fwd, float* ws,
+                         float* out2, void* stream);
+int rsx_nce_emphasis_bwd(const float* A, const float* B, const float* bias, const int* k1a, const int* k1b,
+                         const int64_t* top, int64_t N, int64_t M, int64_t K, int64_t lda, int64_t ldb,
+                         int64_t diag_offset, float tau, float margin, int precision, int nsplit_fwd,
+                         const float* gout, float* ws, float* dA, float* dB, void* stream);
+
 /* ---- A6 grouped: the live LogQ loss over the batch's DISTINCT targets ------------------
  * Same objective as rsx_nce_fwd flags 6 on columns normalize(item_matrix)[t_j], evaluated
  * over the D distinct targets (B[d] = normalised item uniq[d], bias[d] = logQ*lambda) with

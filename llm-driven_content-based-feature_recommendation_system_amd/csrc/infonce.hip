@@ -3503,6 +3503,156 @@ RSX_API int rsx_nce_bwd_x3(const float* A, const float* B, const float* bias, co
   return 0;
 }
 
+// ---- hard-emphasis term (full_batch_hard_emphasis_loss, v1_refine_usertower.py:762-822) ----------------
+// The reference adds +margin to each row's K mined logits (torch.zeros_like(logits).scatter_) before the
+// same-item mask and the cross-entropy, over an N x N logit tensor. Here the dense part is the flags-2
+// InfoNCE above (never materialised) and the K entries per row are a sparse correction on its row
+// statistics: with E_i = sum over allowed mined j of exp(S_ij - lse_i),
+//   lse'_i = lse_i + log1p((e^margin - 1) E_i),   loss'_i = loss_i + (lse'_i - lse_i) - margin [i's own column mined],
+// and, once lse'_i replaces lse_i in the workspace, the dense backward's exp(S_ij - lse'_i) - [j = label] is
+// exactly the emphasised softmax gradient off the mined entries; rsx_nce_emphasis_bwd adds the mined
+// entries' remaining (e^margin - 1) exp(S_ij - lse'_i). One wave per row, fp32 dot products (lane = two
+// of the 128 dims), K mined columns walked in order.
+namespace {
+struct EmphArgs {
+  const float* A; const float* B; const float* bias;
+  const int* k1a; const int* k1b;
+  const int64_t* top;
+  int64_t N, M, K, lda, ldb, diag_off;
+  float inv_tau, margin, em1;  // em1 = e^margin - 1
+  float* lse; float* row_loss;
+  const float* gout; float* dA; float* dB;
+};
+
+__device__ __forceinline__ float emph_dot(const float2 x, const float* brow, int lane) {
+  const float2 y = reinterpret_cast<const float2*>(brow)[lane];
+  float d = x.x * y.x + x.y * y.y;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+  return d;
+}
+
+__global__ __launch_bounds__(256) void nce_emph_fwd_k(EmphArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= a.N) return;
+  const float lse = a.lse[i];
+  if (lse == -INFINITY) return;
+  const float2 x = reinterpret_cast<const float2*>(a.A + i * a.lda)[lane];
+  const int64_t lab = i + a.diag_off;
+  const int ki = a.k1a ? a.k1a[i] : 0;
+  float e = 0.0f;
+  bool self = false;
+  for (int64_t r = 0; r < a.K; ++r) {
+    const int64_t j = a.top[i * a.K + r];
+    if (j < 0 || j >= a.M) continue;                       // host-checked; never read out of bounds
+    if (j != lab && a.k1b && a.k1b[j] == ki) continue;      // same item off the label: -inf in the reference
+    const float s = emph_dot(x, a.B + j * a.ldb, lane) * a.inv_tau - (a.bias ? a.bias[j] : 0.0f);
+    e += __expf(s - lse);
+    self |= j == lab;
+  }
+  if (lane == 0) {
+    const float dl = log1pf(a.em1 * e);
+    a.lse[i] = lse + dl;
+    a.row_loss[i] += dl - (self ? a.margin : 0.0f);
+  }
+}
+
+__global__ __launch_bounds__(256) void nce_emph_bwd_k(EmphArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= a.N) return;
+  const float lse = a.lse[i];
+  if (lse == -INFINITY) return;
+  const float2 x = reinterpret_cast<const float2*>(a.A + i * a.lda)[lane];
+  const int64_t lab = i + a.diag_off;
+  const int ki = a.k1a ? a.k1a[i] : 0;
+  const float c0 = a.gout[0] * a.em1 * a.inv_tau;
+  float2 acc = make_float2(0.0f, 0.0f);
+  for (int64_t r = 0; r < a.K; ++r) {
+    const int64_t j = a.top[i * a.K + r];
+    if (j < 0 || j >= a.M) continue;
+    if (j != lab && a.k1b && a.k1b[j] == ki) continue;
+    const float* brow = a.B + j * a.ldb;
+    const float s = emph_dot(x, brow, lane) * a.inv_tau - (a.bias ? a.bias[j] : 0.0f);
+    const float c = c0 * __expf(s - lse);
+    const float2 y = reinterpret_cast<const float2*>(brow)[lane];
+    acc.x = fmaf(c, y.x, acc.x);
+    acc.y = fmaf(c, y.y, acc.y);
+    if (a.dB) {  // mined columns are shared between rows: vector atomics (order not deterministic)
+      atomicAdd(a.dB + j * kD + 2 * lane, c * x.x);
+      atomicAdd(a.dB + j * kD + 2 * lane + 1, c * x.y);
+    }
+  }
+  if (a.dA) {  // row i belongs to this wave alone
+    float2* d = reinterpret_cast<float2*>(a.dA + i * kD) + lane;
+    float2 v = *d;
+    v.x += acc.x;
+    v.y += acc.y;
+    *d = v;
+  }
+}
+
+int emph_setup(EmphArgs& e, const float* A, const float* B, const float* bias, const int* k1a, const int* k1b,
+               const int64_t* top, int64_t N, int64_t M, int64_t K, int64_t lda, int64_t ldb, int64_t diag_offset,
+               float tau, float margin, int precision, int nsplit_fwd, float* ws) {
+  RSX_ARG(A && B && top && ws, "null tensor");
+  RSX_ARG(precision == RSX_NCE_FP32 || precision == RSX_NCE_BF16X3, "precision must be 0 (fp32) or 1 (bf16x3)");
+  RSX_ARG(N >= 0 && M >= 0 && K >= 0, "negative size");
+  RSX_ARG(diag_offset >= 0 && diag_offset + N <= M, "need 0 <= diag_offset and diag_offset + N <= M");
+  RSX_ARG(lda % 2 == 0 && ldb % 2 == 0 && lda >= kD && ldb >= kD, "row strides must be >= 128 and even");
+  RSX_ARG((k1a == nullptr) == (k1b == nullptr), "k1 keys: both or neither");
+  RSX_ARG(tau > 0.0f, "tau must be > 0");
+  const int nf = precision == RSX_NCE_FP32 ? nsplit_fwd : plain_plan(N, M).nf;
+  RSX_ARG(nf >= 1, "nsplit_fwd must be >= 1");
+  e.A = A; e.B = B; e.bias = bias; e.k1a = k1a; e.k1b = k1b; e.top = top;
+  e.N = N; e.M = M; e.K = K; e.lda = lda; e.ldb = ldb; e.diag_off = diag_offset;
+  e.inv_tau = 1.0f / tau;
+  e.margin = margin;
+  e.em1 = expm1f(margin);
+  e.lse = ws + 4 * (int64_t)nf * N;
+  e.row_loss = e.lse + N;
+  e.gout = nullptr; e.dA = nullptr; e.dB = nullptr;
+  return 0;
+}
+}  // namespace
+
+RSX_API int rsx_nce_emphasis_fwd(const float* A, const float* B, const float* bias, const int* k1a, const int* k1b,
+                                 const int64_t* top, int64_t N, int64_t M, int64_t K, int64_t lda, int64_t ldb,
+                                 int64_t diag_offset, float tau, float margin, int precision, int nsplit_fwd,
+                                 float* ws, float* out2, void* stream) {
+  EmphArgs e;
+  const int rc = emph_setup(e, A, B, bias, k1a, k1b, top, N, M, K, lda, ldb, diag_offset, tau, margin, precision,
+                            nsplit_fwd, ws);
+  if (rc) return rc;
+  RSX_ARG(out2 != nullptr, "null output");
+  if (N == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (K > 0) {
+    hipLaunchKernelGGL(nce_emph_fwd_k, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, e);
+    RSX_LAUNCHED();
+  }
+  hipLaunchKernelGGL(nce_reduce_k, dim3(1), dim3(1024), 0, st, e.row_loss, e.row_loss + N, N, out2);
+  RSX_LAUNCHED();
+  return 0;
+}
+
+RSX_API int rsx_nce_emphasis_bwd(const float* A, const float* B, const float* bias, const int* k1a, const int* k1b,
+                                 const int64_t* top, int64_t N, int64_t M, int64_t K, int64_t lda, int64_t ldb,
+                                 int64_t diag_offset, float tau, float margin, int precision, int nsplit_fwd,
+                                 const float* gout, float* ws, float* dA, float* dB, void* stream) {
+  EmphArgs e;
+  const int rc = emph_setup(e, A, B, bias, k1a, k1b, top, N, M, K, lda, ldb, diag_offset, tau, margin, precision,
+                            nsplit_fwd, ws);
+  if (rc) return rc;
+  RSX_ARG(gout != nullptr, "gout required");
+  if (N == 0 || K == 0 || (!dA && !dB)) return 0;
+  e.gout = gout; e.dA = dA; e.dB = dB;
+  hipLaunchKernelGGL(nce_emph_bwd_k, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, (hipStream_t)stream, e);
+  RSX_LAUNCHED();
+  return 0;
+}
+
 RSX_API int rsx_nce_grouped_fwd(const float* A, const float* B, const float* bias, const float* colcnt,
                                 const int* row_col, const int* row_beg, const int* row_end, const int* exc_cols,
                                 int64_t N, int64_t D, int64_t lda, int64_t ldb, float tau, int precision, int nsplit,

@@ -1011,7 +1011,9 @@ __global__ __launch_bounds__(256) void mha_fwd_x3b64_k(FwdArgs a) {
   else mha_fwd_x3b64_seq<4>(a, hd, tok0, L, lane);
 }
 
-__global__ __launch_bounds__(256) void mha_fwd_x3b_k(FwdArgs a) {
+// three waves per SIMD (168 VGPRs, no spills; the default allocation took 176 and ran two): 166.6 ->
+// 136.7 us on the headline tower's first layer (round 6, tools/tower_micro.py under rocprofv3)
+__global__ __launch_bounds__(256, 3) void mha_fwd_x3b_k(FwdArgs a) {
   const int lane = threadIdx.x & 63;
   const int64_t unit = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (unit >= (int64_t)a.B * a.H) return;  // whole wave exits together
@@ -1398,6 +1400,9 @@ constexpr int kStashLd = 20;     // tile row stride (floats): conflict-free writ
 constexpr int kStashPairs = 10;  // causal pairs kb <= qb < 4
 __device__ __forceinline__ int stash_slot(int kb, int qb) { return (qb * (qb + 1) >> 1) + kb; }
 
+// Measured and not kept (round 6): a second instance for sequences of <= 32 tokens with a 3-pair stash
+// (15 KB of LDS) at four waves per SIMD: 128 VGPRs with 49 spilled, 319 + 245 us against 367 us for this
+// kernel alone on the headline tower's first layer.
 __global__ __launch_bounds__(256) void mha_bwd_x3s_k(BwdArgs a) {
   // dS tiles of this wave's (kb, qb <= ... ) pairs, [16 query rows][16 key columns] at row stride 20
   __shared__ __attribute__((aligned(16))) float sDS[4][kStashPairs][16 * kStashLd];

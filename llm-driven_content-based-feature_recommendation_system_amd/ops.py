@@ -556,6 +556,85 @@ def nce_loss(A, B, bias=None, k1a=None, k1b=None, k2a=None, k2b=None, tau=0.1, f
     return total / cnt.clamp(min=1.0)
 
 
+class _NCEEmphasis(torch.autograd.Function):
+    """(sum of row losses, N) of full_batch_hard_emphasis_loss's cross-entropy (v1_refine_usertower.py
+    :762-822): S = A B^T / tau - bias, same-key columns off the diagonal excluded (flags MASK_K1), and
+    +margin on each row's mined columns top [N, K] -- the dense flags-2 InfoNCE pass plus the O(N K)
+    rsx_nce_emphasis_fwd / _bwd correction; no N x N tensor."""
+
+    @staticmethod
+    def forward(ctx, A, B, bias, k1, top, tau, margin, tag):
+        N.ensure_device(A)
+        A = _c(A)
+        B = _c(B)
+        n, m = A.shape[0], B.shape[0]
+        K = top.shape[1] if top.dim() == 2 else 0
+        top = _c(top.to(torch.int64))
+        x3 = _nce_precision != "fp32"
+        prec = 1 if x3 else 0
+        nws = (N.lib().rsx_nce_x3_workspace_floats(n, m) if x3
+               else N.lib().rsx_nce_workspace_floats(n, m, _NSPLIT_FWD, _NSPLIT_BWD))
+        ws = torch.empty(nws, device=A.device, dtype=torch.float32)
+        out2 = torch.empty(2, device=A.device, dtype=torch.float32)
+        flags = NCE_MASK_ITEM
+        with timed(f"{tag}/nce_fwd"):
+            if x3:
+                rc = N.lib().rsx_nce_fwd_x3(N.ptr(A), N.ptr(B), N.ptr(bias), N.ptr(k1), N.ptr(k1), None, None, n, m,
+                                            A.stride(0), B.stride(0), 0, tau, flags, N.ptr(ws), N.ptr(out2), N.stream())
+            else:
+                rc = N.lib().rsx_nce_fwd(N.ptr(A), N.ptr(B), N.ptr(bias), N.ptr(k1), N.ptr(k1), None, None, n, m,
+                                         A.stride(0), B.stride(0), 0, tau, flags, _NSPLIT_FWD, N.ptr(ws), N.ptr(out2),
+                                         N.stream())
+            N.check(rc, "nce_fwd")
+            rc = N.lib().rsx_nce_emphasis_fwd(N.ptr(A), N.ptr(B), N.ptr(bias), N.ptr(k1), N.ptr(k1), N.ptr(top), n, m,
+                                              K, A.stride(0), B.stride(0), 0, tau, margin, prec, _NSPLIT_FWD,
+                                              N.ptr(ws), N.ptr(out2), N.stream())
+            N.check(rc, "nce_emphasis_fwd")
+        ctx.save_for_backward(A, B, bias, k1, top, ws)
+        ctx.cfg = (n, m, K, tau, margin, tag, x3)
+        cnt = out2[1]
+        ctx.mark_non_differentiable(cnt)
+        return out2[0], cnt
+
+    @staticmethod
+    def backward(ctx, g, _gcnt):
+        A, B, bias, k1, top, ws = ctx.saved_tensors
+        n, m, K, tau, margin, tag, x3 = ctx.cfg
+        g = _c(g.reshape(1).to(torch.float32))
+        head = (N.ptr(A), N.ptr(B), N.ptr(bias), N.ptr(k1), N.ptr(k1), None, None, n, m, A.stride(0), B.stride(0), 0,
+                tau, NCE_MASK_ITEM)
+        if x3:
+            fn, args = N.lib().rsx_nce_bwd_x3, head + (N.ptr(g), N.ptr(ws))
+        else:
+            fn, args = N.lib().rsx_nce_bwd, head + (_NSPLIT_FWD, _NSPLIT_BWD, N.ptr(g), N.ptr(ws))
+        dA = torch.empty_like(A) if ctx.needs_input_grad[0] else None
+        dB = torch.empty_like(B) if ctx.needs_input_grad[1] else None
+        with timed(f"{tag}/nce_bwd"):
+            if dA is not None:
+                N.check(fn(*args, N.ptr(dA), None, 0, N.stream()), "nce_bwd(rows)")
+            if dB is not None:
+                N.check(fn(*args, None, N.ptr(dB), 0, N.stream()), "nce_bwd(cols)")
+            if dA is not None or dB is not None:
+                rc = N.lib().rsx_nce_emphasis_bwd(N.ptr(A), N.ptr(B), N.ptr(bias), N.ptr(k1), N.ptr(k1), N.ptr(top),
+                                                  n, m, K, A.stride(0), B.stride(0), 0, tau, margin, 1 if x3 else 0,
+                                                  _NSPLIT_FWD, N.ptr(g), N.ptr(ws), N.ptr(dA), N.ptr(dB), N.stream())
+                N.check(rc, "nce_emphasis_bwd")
+        return dA, dB, None, None, None, None, None, None
+
+
+def nce_emphasis_loss(A, B, keys, top, margin, bias=None, tau=0.1, tag="hard_emphasis"):
+    """Mean over the N rows of CE(A B^T / tau - bias + margin on each row's mined columns top [N, K],
+    same-key columns off the diagonal at -inf; label = diagonal) -- full_batch_hard_emphasis_loss's
+    objective (v1_refine_usertower.py:546-554) without its N x N tensors. margin is in logit units
+    (the reference's hard_margin / temperature). A [N, 128], B [N, 128], keys [N] int."""
+    if A.shape[0] != B.shape[0]:
+        raise ValueError("nce_emphasis_loss: A and B must have the same number of rows (label = diagonal)")
+    if bias is not None:
+        bias = _c(bias.to(torch.float32))
+    total, cnt = _NCEEmphasis.apply(A, B, bias, _c(keys.to(torch.int32)), top, float(tau), float(margin), str(tag))
+    return total / cnt.clamp(min=1.0)
+
+
 # ----------------------------------------------------------------------------------------
 # Grouped form of the live LogQ loss (distinct targets as columns, exact multiplicities)
 class TargetGroups:

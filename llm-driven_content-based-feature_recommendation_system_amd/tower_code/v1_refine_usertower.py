@@ -530,26 +530,18 @@ def inbatch_mixed_hnm_loss_with_stats(user_emb, item_tower_emb, target_ids, log_
 def full_batch_hard_emphasis_loss(user_emb, item_tower_emb, target_ids, log_q_tensor, top_k_percent=0.01,
                                   hard_margin=0.2, hnm_threshold=0.90, temperature=0.1, lambda_logq=1.0):
     """Reference :762-822 (the loss of train_user_tower, v1_usertower_train.py:459-469).
-    N x N over the batch (N <= a few thousand last-step rows): cosine logits, ignore mask
-    (same item, or item-item cosine > hnm_threshold off the diagonal), top-k hard negatives
-    (k = max(1, floor((N-1) * top_k_percent))) mined on the masked cosines get +margin/tau,
-    same-item off-diagonal columns -> -inf, CE against the diagonal. Column rows are gathered +
-    L2-normalised by rsx_gather_rows and the mining (both products, mask, top-k) is the fused
-    rsx_hnm_mine kernel; the N x N logits for the full-batch CE are one GEMM.
+    Cosine logits over the batch, ignore mask (same item, or item-item cosine > hnm_threshold off the
+    diagonal), top-k hard negatives (k = max(1, floor((N-1) * top_k_percent))) mined on the masked cosines
+    get +margin/tau, same-item off-diagonal columns -> -inf, CE against the diagonal. Column rows are
+    gathered + L2-normalised by rsx_gather_rows, the mining (both products, mask, top-k) is the fused
+    rsx_hnm_mine kernel, and the cross-entropy is ops.nce_emphasis_loss: the dense masked InfoNCE pass
+    plus an O(N k) correction for the mined columns' margin -- no N x N tensor in either direction.
     Returns (loss, {"avg_hn_similarity", "num_hard"})."""
     N = user_emb.size(0)
-    device = user_emb.device
     tgt = target_ids.reshape(-1)
     u, it = _hnm_rows(user_emb, item_tower_emb, tgt)
     num_k = max(1, int((N - 1) * top_k_percent))
     top_idx, top_cos, _ = ops.hnm_mine(u, it, tgt, num_k, hnm_threshold, 1.0)
-    cos = u @ it.T
-    same = tgt.unsqueeze(1) == tgt.unsqueeze(0)
-    diag = torch.eye(N, dtype=torch.bool, device=device)
-    logits = cos / temperature
-    if lambda_logq > 0.0:
-        logits = logits - log_q_tensor[tgt].view(1, -1) * lambda_logq
-    emphasis = torch.zeros_like(logits).scatter_(1, top_idx, hard_margin / temperature)
-    logits = (logits + emphasis).masked_fill(same & ~diag, float("-inf"))
-    loss = F.cross_entropy(logits, torch.arange(N, device=device))
+    bias = log_q_tensor[tgt] * lambda_logq if lambda_logq > 0.0 else None
+    loss = ops.nce_emphasis_loss(u, it, tgt, top_idx, hard_margin / temperature, bias=bias, tau=temperature)
     return loss, {"avg_hn_similarity": top_cos.mean().item(), "num_hard": num_k}

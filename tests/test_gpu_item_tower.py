@@ -10,6 +10,7 @@ import torch.nn.functional as F
 
 import recsys_amd  # noqa: F401
 from recsys_amd import item_tower as IT
+from recsys_amd import ops
 from recsys_amd.tower_code import v1_refine_usertower as T
 from recsys_amd.tower_code import v1_usertower_train as TT
 from recsys_amd import synth
@@ -195,6 +196,44 @@ def test_hard_emphasis_loss_parity(gpu, N, lambda_logq):
     assert abs(s_dut["avg_hn_similarity"] - s_ref["avg_hn_similarity"]) < 1e-5
     torch.testing.assert_close(u2.grad.cpu(), u1.grad, atol=1e-6, rtol=1e-4)
     torch.testing.assert_close(w2.grad.cpu(), w1.grad, atol=1e-6, rtol=1e-4)
+
+
+@pytest.mark.parametrize("N", [4096])
+def test_hard_emphasis_loss_large_matches_dense_form(gpu, N):
+    """ops.nce_emphasis_loss (dense masked InfoNCE + O(N k) margin correction, no N x N tensor) against the
+    reference's own dense arithmetic (:546-554: N x N cosines, scatter_ of margin / tau on the mined columns,
+    same-item masked_fill, F.cross_entropy) in float64 on the same mined columns, with duplicated targets
+    (same-item masking) and mined columns on rows that share a target: loss 1e-5 relative, gradients
+    1e-4 of their scale."""
+    g = torch.Generator().manual_seed(N + 1)
+    I = 1500                                                   # ~N / I repeats per target: many same-item pairs
+    W = F.normalize(torch.randn(I, 128, generator=g), dim=1)
+    lq = torch.log_softmax(torch.randn(I, generator=g), 0)
+    t = torch.randint(0, I, (N,), generator=g)
+    U = torch.randn(N, 128, generator=g)
+    tau, margin = 0.1, 0.2
+    u2 = U.to(gpu).requires_grad_()
+    w2 = W.to(gpu).requires_grad_()
+    loss, st = T.full_batch_hard_emphasis_loss(u2, w2, t.to(gpu), lq.to(gpu), temperature=tau, hard_margin=margin)
+    loss.backward()
+    k = st["num_hard"]
+    un = F.normalize(U.to(gpu), dim=1)
+    itn = F.normalize(W.to(gpu)[t.to(gpu)], dim=1)
+    top, _, _ = ops.hnm_mine(un, itn, t.to(gpu), k, 0.9, 1.0)
+    top = top.cpu()
+    u1 = U.double().requires_grad_()
+    w1 = W.double().requires_grad_()
+    u, it = F.normalize(u1, dim=1), F.normalize(w1[t], dim=1)
+    logits = (u @ it.T) / tau - lq.double()[t].view(1, -1)
+    emph = torch.zeros_like(logits).scatter_(1, top, margin / tau)
+    same = t.view(-1, 1) == t.view(1, -1)
+    same.fill_diagonal_(False)
+    ref = F.cross_entropy((logits + emph).masked_fill(same, float("-inf")), torch.arange(N))
+    ref.backward()
+    assert abs(loss.item() - ref.item()) <= 1e-5 * abs(ref.item())
+    for got, want in ((u2.grad, u1.grad), (w2.grad, w1.grad)):
+        err = float((got.cpu().double() - want).abs().max()) / float(want.abs().max())
+        assert err <= 1e-4, err
 
 
 def test_hard_emphasis_step_parity(gpu):
