@@ -293,7 +293,10 @@ struct WsArgs {
   int groups;   // workgroups per column block
 };
 
-template <int KC, int NBW, int EPI, int WV>
+// PF (WV = 4): the next 16-k step's B fragments are read from LDS while this step's MFMAs run (one wave
+// per SIMD has no other wave to cover an LDS round trip; without PF hipcc re-reads each fragment right
+// before its MFMA and waits for it), with two A chunks per wave instead of three for the registers.
+template <int KC, int NBW, int EPI, int WV, bool PF = false>
 __global__ __launch_bounds__(64 * WV, 1) void gemm_ws_k(WsArgs w) {
   constexpr int kWsThreads = 64 * WV, kWsWaves = WV;
   constexpr int NT = NBW / 32;
@@ -379,6 +382,34 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_ws_k(WsArgs w) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) z[j][g] = *reinterpret_cast<const float4*>(xrow + 32 * j + 8 * g);
     }
+    if constexpr (PF) {
+      u32x4 wf[2][NT][2];
+      auto wload = [&](int s, u32x4 (&wd)[NT][2]) {
+        const u32x4* wp = sW + ((q * 8 + s) * NT) * 128 + lane;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          wd[j][0] = wp[j * 128];
+          wd[j][1] = wp[j * 128 + 64];
+        }
+      };
+      wload(0, wf[0]);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        if (s + 1 < 8) wload(s + 1, wf[(s + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);  // keep the reads here: hipcc otherwise sinks each to its MFMA
+        u32x4 hi, lo;
+        split8(buf[2 * s], buf[2 * s + 1], hi, lo);
+        const bf16x8 xh = __builtin_bit_cast(bf16x8, hi), xl = __builtin_bit_cast(bf16x8, lo);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const bf16x8 wh = __builtin_bit_cast(bf16x8, wf[s & 1][j][0]);
+          const bf16x8 wl = __builtin_bit_cast(bf16x8, wf[s & 1][j][1]);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, xh, acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xl, acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xh, acc[j], 0, 0, 0);
+        }
+      }
+    } else {
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       u32x4 hi, lo;
@@ -393,6 +424,7 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_ws_k(WsArgs w) {
         acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xl, acc[j], 0, 0, 0);
         acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xh, acc[j], 0, 0, 0);
       }
+    }
     }
     if (q != KC - 1) return;
     // epilogue. Rows past M loaded A row M-1 and computed exactly row M-1's values; they are
@@ -499,7 +531,7 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_ws_k(WsArgs w) {
   // loop then carry the same outstanding-load pattern, so the compiler's vmcnt waits stay
   // per buffer instead of draining the prefetches. The trailing re-loads are never used.
   const int last = nitems - 1;
-  if constexpr (WV == 8) {
+  if constexpr (WV == 8 || PF) {
     float4 b0[16], b1[16];
     load(0, b0);
     load(last < 1 ? last : 1, b1);
@@ -563,7 +595,7 @@ bool ws_enabled() {
   return on == 1;
 }
 
-template <int KC, int NBW, int WV>
+template <int KC, int NBW, int WV, bool PF = false>
 void launch_ws_w(const GArgs& g, hipStream_t st) {
   constexpr int kWsThreads = 64 * WV, kWsWaves = WV;
   WsArgs w;
@@ -576,14 +608,14 @@ void launch_ws_w(const GArgs& g, hipStream_t st) {
   if (groups > blocks_rows) groups = (int)blocks_rows;
   w.groups = groups;
   const int grid = (w.nblk * groups + 7) / 8 * 8;
-  if (g.epi == EPI_BIAS) hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_BIAS, WV>), dim3(grid), dim3(kWsThreads), 0, st, w);
+  if (g.epi == EPI_BIAS) hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_BIAS, WV, PF>), dim3(grid), dim3(kWsThreads), 0, st, w);
   else if (g.epi == EPI_ROWADD)
-    hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_ROWADD, WV>), dim3(grid), dim3(kWsThreads), 0, st, w);
+    hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_ROWADD, WV, PF>), dim3(grid), dim3(kWsThreads), 0, st, w);
   else if (g.epi == EPI_ADDLN)
-    hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_ADDLN, WV>), dim3(grid), dim3(kWsThreads), 0, st, w);
+    hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_ADDLN, WV, PF>), dim3(grid), dim3(kWsThreads), 0, st, w);
   else if (g.epi == EPI_GELU_DROP)
-    hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_GELU_DROP, WV>), dim3(grid), dim3(kWsThreads), 0, st, w);
-  else hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_DGELU_DROP, WV>), dim3(grid), dim3(kWsThreads), 0, st, w);
+    hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_GELU_DROP, WV, PF>), dim3(grid), dim3(kWsThreads), 0, st, w);
+  else hipLaunchKernelGGL((gemm_ws_k<KC, NBW, EPI_DGELU_DROP, WV, PF>), dim3(grid), dim3(kWsThreads), 0, st, w);
 }
 
 // RSX_GEMM_WS_WAVES = 4 | 8 (A/B): waves per weight-stationary workgroup
@@ -596,9 +628,20 @@ int ws_waves() {
   return v;
 }
 
+// RSX_GEMM_WS_PF = 0 | 1 (A/B): four waves with the B-fragment prefetch (PF) or without
+bool ws_pf() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("RSX_GEMM_WS_PF");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
 template <int KC, int NBW>
 void launch_ws(const GArgs& g, hipStream_t st) {
   if (ws_waves() == 8) launch_ws_w<KC, NBW, 8>(g, st);
+  else if (ws_pf()) launch_ws_w<KC, NBW, 4, true>(g, st);
   else launch_ws_w<KC, NBW, 4>(g, st);
 }
 

@@ -1127,6 +1127,21 @@ struct X3Stage {
     *reinterpret_cast<u32x4*>(&t.lo[o0]) = v[2];
     *reinterpret_cast<u32x4*>(&t.lo[o1]) = v[3];
   }
+  // the hi image alone (a pass whose products never read the streamed rows' lo image)
+  __device__ __forceinline__ void load_hi(const __bf16* hi, int64_t row, bool ok, int tid) {
+    if (ok) {
+      const int64_t o = row * kD + (tid & 7) * 8;
+      v[0] = *reinterpret_cast<const u32x4*>(hi + o);
+      v[1] = *reinterpret_cast<const u32x4*>(hi + o + 64);
+    } else {
+      v[0] = v[1] = u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+  __device__ __forceinline__ void store_hi(X3Tile& t, int tid) const {
+    const int row = tid >> 3, ch = tid & 7;
+    *reinterpret_cast<u32x4*>(&t.hi[img_off(row, 8 * ch)]) = v[0];
+    *reinterpret_cast<u32x4*>(&t.hi[img_off(row, 64 + 8 * ch)]) = v[1];
+  }
 };
 
 // rows x 128 fp32 (row stride ld) -> hi/lo bf16 images [rows][128]; one thread per 8 floats
@@ -2654,6 +2669,29 @@ __device__ __forceinline__ f32x16 dots_h3(const X3Tile& t, int c, int h, const b
   return acc;
 }
 
+// S tile from two fp16 products, hi*hi' + hi*lo' (streamed hi against the owner's hi and lo): the
+// streamed rows' lo image is never read. |dot error| = |<lo, owner>| ~ 2^-11 |x| per component with
+// random signs, ~2e-5 on unit vectors (the column pass's weights only; the logits of the loss keep
+// three products in the forward)
+__device__ __forceinline__ f32x16 dots_h2(const X3Tile& t, int c, int h, const bf16x8 (&uh)[8],
+                                          const bf16x8 (&ul)[8]) {
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+  const int base = img_off(c, 64 * h);
+  bf16x8 ah = *reinterpret_cast<const bf16x8*>(&t.hi[base]);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    bf16x8 nh = ah;
+    if (s < 7) nh = *reinterpret_cast<const bf16x8*>(&t.hi[base + 8 * (s + 1)]);
+    acc = mfma_h(ah, ul[s], acc);
+    acc = mfma_h(ah, uh[s], acc);
+    __builtin_amdgcn_sched_barrier(0);
+    ah = nh;
+  }
+  return acc;
+}
+
 // g = 2^(x - m) for a pair, summed into sum (fp32, before rounding) and packed as two fp16
 __device__ __forceinline__ void exp_h_pair(float a, float b, float m, uint32_t& og, f32x2& sum) {
   f32x2 v = {a, b};
@@ -2940,8 +2978,11 @@ __device__ __forceinline__ void grad_half_gh(f32x16 (&gacc)[4], const bf16x8& g,
 // the common product, when its G fragments are dead: folded into the common product, the exception
 // bookkeeping needs ~60 more VGPRs than the 256 a two-wave-per-SIMD kernel has (and with the owner
 // fragments moved to LDS instead the pass is LDS-bound).
-template <int GP>
+// SPN = products of the S tile: 3 (dots_h3) or 2 (dots_h2, GP = 1 only: with one gradient product on the
+// hi image as well, the streamed rows' lo image is neither staged nor read).
+template <int GP, int SPN = 3>
 __global__ __launch_bounds__(256, 2) void nce_grouped_bwd_cols_h_k(GArgs a) {
+  static_assert(SPN == 3 || (SPN == 2 && GP == 1), "two S products only with one gradient product");
   __shared__ __attribute__((aligned(16))) X3Tile sT[2];
   __shared__ __attribute__((aligned(16))) float sM0[2][kTile];  // lse_i * log2e (+inf past the split)
   __shared__ __attribute__((aligned(16))) int sM2[2][kTile];    // d(i) (-2 past the split)
@@ -2991,7 +3032,8 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_bwd_cols_h_k(GArgs a) {
   int stg2 = 0;
   auto gload = [&](int64_t s0) {
     const int64_t sidx = s0 + (tid >> 3);
-    stg.load(a.ahi, a.alo, sidx, sidx < s_end, tid);
+    if constexpr (SPN == 2) stg.load_hi(a.ahi, sidx, sidx < s_end, tid);
+    else stg.load(a.ahi, a.alo, sidx, sidx < s_end, tid);
     if (tid < kTile) {
       const int64_t ss = s0 + tid;
       const bool ok = ss < s_end;
@@ -3000,7 +3042,8 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_bwd_cols_h_k(GArgs a) {
     }
   };
   auto lstore = [&](int buf) {
-    stg.store(sT[buf], tid);
+    if constexpr (SPN == 2) stg.store_hi(sT[buf], tid);
+    else stg.store(sT[buf], tid);
     if (tid < kTile) {
       sM0[buf][tid] = stg0 * kLog2e;
       sM2[buf][tid] = stg2;
@@ -3032,7 +3075,7 @@ __global__ __launch_bounds__(256, 2) void nce_grouped_bwd_cols_h_k(GArgs a) {
       const bool has_next = t + 1 < ntile;
       const bool exc = exc_flag(s0);
       if (has_next) gload(s0 + kTile);
-      f32x16 acc = dots_h3(sT[cur], c, h, uh, ul);
+      f32x16 acc = SPN == 2 ? dots_h2(sT[cur], c, h, uh, ul) : dots_h3(sT[cur], c, h, uh, ul);
       // G' rows of k-step 0, then k-step 0's product with k-step 1's rows under its MFMAs
       u32x4 g0;
 #pragma unroll
@@ -3215,6 +3258,14 @@ int f16_gp() {
   static const int v = [] {
     const char* e = getenv("RSX_NCE_F16_GP");
     return (e && e[0] == '2') ? 2 : 1;
+  }();
+  return v;
+}
+// RSX_NCE_F16_COLS_S = 2 | 3: products of the column pass's S tile (with GP = 1)
+int f16_cols_s() {
+  static const int v = [] {
+    const char* e = getenv("RSX_NCE_F16_COLS_S");
+    return (e && e[0] == '2') ? 2 : 3;
   }();
   return v;
 }
@@ -3961,6 +4012,8 @@ RSX_API int rsx_nce_grouped_bwd(const float* A, const float* B, const float* bia
     }
     if (!row_owned && h16 && f16_gp() == 2)
       hipLaunchKernelGGL(nce_grouped_bwd_cols_h_k<2>, dim3(blocks), dim3(256), 0, st, g);
+    else if (!row_owned && h16 && f16_cols_s() == 2)
+      hipLaunchKernelGGL((nce_grouped_bwd_cols_h_k<1, 2>), dim3(blocks), dim3(256), 0, st, g);
     else if (!row_owned && h16)
       hipLaunchKernelGGL(nce_grouped_bwd_cols_h_k<1>, dim3(blocks), dim3(256), 0, st, g);
     else if (row_owned && x3) hipLaunchKernelGGL((nce_grouped_bwd_x3_k<true, false>), dim3(blocks), dim3(256), 0, st, g);

@@ -210,7 +210,7 @@ __global__ __launch_bounds__(256) void tw_lastq_fwd_k(LastQ a) {
 
 // Its backward, writing every dqkv row of view 2's user j for head hd (32-column slices of q, k
 // and v): dQ on the query row, dK / dV on the valid keys, zero elsewhere.
-__global__ __launch_bounds__(256, 4) void tw_lastq_bwd_k(LastQ a) {
+__global__ __launch_bounds__(256) void tw_lastq_bwd_k(LastQ a) {
   const int lane = threadIdx.x & 63, hd = threadIdx.x >> 6;
   const int64_t j = blockIdx.x;
   const int64_t s0 = a.seg64[a.B + j], len = a.seg64[a.B + j + 1] - s0;
