@@ -180,7 +180,9 @@ int rsx_nce_emphasis_bwd(const float* A, const float* B, const float* bias, cons
  *            tighter than bf16x3), gradient products as ONE fp16 MFMA of the rounded softmax weights
  *            and the rows' fp16 hi image (the reference's autocast(float16) arithmetic for these
  *            products, v1_usertower_train.py:787, with fp32 accumulation; RSX_NCE_F16_GP=2 adds the
- *            lo image); elsewhere (rsx_nce_grouped_fwd, the row pass) as RSX_NCE_BF16X3. */
+ *            lo image); in the column pass the logits take two of the three products (the streamed rows'
+ *            lo image dropped: ~2e-5 on unit vectors; RSX_NCE_F16_COLS_S=3 keeps three); elsewhere
+ *            (rsx_nce_grouped_fwd, the row pass) as RSX_NCE_BF16X3. */
 #define RSX_NCE_FP32 0
 #define RSX_NCE_BF16X3 1
 #define RSX_NCE_F16 2
