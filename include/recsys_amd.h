@@ -285,6 +285,15 @@ int rsx_linear_wgrad_x3(const float* dY, int64_t ldy, const float* X, int64_t ld
  * N % 128 == 0, K % 32 == 0, A/B 16-byte aligned, leading dimensions multiples of 4. */
 int rsx_gemm_x3(const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias, int64_t M, int N, int K,
                 int epi, float* aux, int64_t ldaux, float p_drop, uint64_t seed, float* C, int64_t ldc, void* stream);
+/* The same with a caller workspace for split-K: when the output has fewer 128 x 128 tiles than the device
+ * has CUs and K is long (K not 128 / 256 / 384), S K-ranges per tile run as separate workgroups writing
+ * partial sums to ws, and one pass adds them in split order and applies epi. ws_floats >=
+ * rsx_gemm_x3_split_floats(M, N, K) (0 = no split for this shape; ws may then be null). Deterministic; the
+ * summation order over K differs from rsx_gemm_x3's (fp32 rounding level). */
+int64_t rsx_gemm_x3_split_floats(int64_t M, int N, int K);
+int rsx_gemm_x3_ws(const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias, int64_t M, int N,
+                   int K, int epi, float* aux, int64_t ldaux, float p_drop, uint64_t seed, float* C, int64_t ldc,
+                   float* ws, int64_t ws_floats, void* stream);
 /* C = epi(A . Bt + bias) with Bt [K, N] as stored (row stride ldbt >= N): the input gradient
  * dX = dY . W of the same token linears straight from W [out, in] (K = out, N = in; autograd's
  * dX GEMM of nn.Linear, v1_refine_usertower.py:447-510), no transposed copy of W; epi / aux /

@@ -90,6 +90,9 @@ _SIGS = {
     "rsx_linear_wgrad": (c_i, [c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i, c_p, c_i64, c_p]),
     "rsx_linear_wgrad_x3": (c_i, [c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i, c_p, c_i64, c_p]),
     "rsx_gemm_x3": (c_i, [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_i, c_i, c_i, c_p, c_i64, c_f, c_u64, c_p, c_i64, c_p]),
+    "rsx_gemm_x3_split_floats": (c_i64, [c_i64, c_i, c_i]),
+    "rsx_gemm_x3_ws": (c_i, [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_i, c_i, c_i, c_p, c_i64, c_f, c_u64, c_p, c_i64, c_p,
+                             c_i64, c_p]),
     "rsx_gemm_x3_tn": (c_i, [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_i, c_i, c_i, c_p, c_i64, c_f, c_u64, c_p, c_i64,
                              c_p]),
     "rsx_loss_combine": (c_i, [c_p, c_p, c_p, c_p, c_f, c_f, c_f, c_f, c_p, c_p, c_p]),

@@ -104,6 +104,9 @@ struct GArgs {
   int64_t ldy;
   int64_t lda, ldb, ldc, ldaux, M;
   int N, K, epi, tiles_n, tiles, per;
+  int ksplit;    // split-K (> 1): workgroup (split, tile), K range [split * kspan, + kspan), raw sums to part
+  int kspan;
+  float* part;   // [ksplit][M][N] partial sums (split-K only)
   int transb;  // weight-stationary path only: B given as Bt [K, ldb] (B[n][k] = Bt[k * ldb + n])
   rsx::Dropout drop;
 };
@@ -176,7 +179,12 @@ __device__ __forceinline__ void epilogue(const GArgs& a, f32x16 (&acc)[2][2], in
 // M block) as one continuous stream of K stages: the prefetch of the next stage (possibly
 // the next tile's first) overlaps the current stage's MFMAs and the finished tile's epilogue,
 // so the load pipeline never drains between tiles.
-template <int EPI>
+// Q = stages of A / B kept in flight in registers (Q = 1: the next stage only). With few output tiles
+// (M of a few thousand tokens and N <= 768: fewer tiles than CUs, one workgroup per CU, e.g. the text
+// BERT's GEMMs) a workgroup's single 16-KB stage in flight leaves it waiting on memory latency for
+// most of each stage; Q = 4 keeps four (64 KB) in flight at 16 VGPRs per stage. Same products and
+// order (bit-identical results).
+template <int EPI, int Q = 1>
 __global__ __launch_bounds__(256, 2) void gemm_x3_nt_k(GArgs a) {
   __shared__ __attribute__((aligned(16))) Img sA[2];
   __shared__ __attribute__((aligned(16))) Img sB[2];
@@ -185,11 +193,13 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_k(GArgs a) {
   const int wm = wave >> 1, wn = wave & 1;
   // XCD-aware block order (the grid is padded to a multiple of 8)
   const int bflat = (blockIdx.x & 7) * ((int)gridDim.x >> 3) + (blockIdx.x >> 3);
-  const int t_begin = bflat * a.per;
-  int t_end = t_begin + a.per;
+  const int split = a.ksplit > 1 ? bflat / a.tiles : 0;
+  const int t_begin = a.ksplit > 1 ? bflat % a.tiles : bflat * a.per;
+  int t_end = a.ksplit > 1 ? t_begin + 1 : t_begin + a.per;
   if (t_end > a.tiles) t_end = a.tiles;
-  if (t_begin >= t_end) return;
-  const int nk = a.K / kBK;
+  if (t_begin >= t_end || split >= (a.ksplit > 1 ? a.ksplit : 1)) return;
+  const int nk = (a.ksplit > 1 ? a.kspan : a.K) / kBK;
+  const int kbase = split * (a.ksplit > 1 ? a.kspan : 0);
   const int nstage = (t_end - t_begin) * nk;
 
   f32x16 acc[2][2];
@@ -204,40 +214,34 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_k(GArgs a) {
   // Rows past M load row m0 instead (unconditional loads: a predicated load would make the
   // compiler wait on each one); their C rows are never stored and no other row depends on them.
   const int srow = tid >> 1, scol = (tid & 1) * (kBK / 2);
-  float4 pa[kF4], pb[kF4];
-  auto gload = [&](int st) {
-    const int t = t_begin + st / nk, k0 = (st % nk) * kBK;
+  float4 pa[Q][kF4], pb[Q][kF4];
+  auto gload_s = [&](int slot, int st) {
+    if (st >= nstage) st = nstage - 1;  // unconditional (clamped): the same outstanding loads on every path
+    const int t = t_begin + st / nk, k0 = kbase + (st % nk) * kBK;
     const int64_t m0 = (int64_t)(t / a.tiles_n) * kBM;
     const int n0 = (t % a.tiles_n) * kBN;
     const float* a_src = a.A + (m0 + srow < a.M ? m0 + srow : m0) * a.lda + scol + k0;
     const float* b_src = a.B + (int64_t)(n0 + srow) * a.ldb + scol + k0;
 #pragma unroll
     for (int q = 0; q < kF4; ++q) {
-      pa[q] = *reinterpret_cast<const float4*>(a_src + 4 * q);
-      pb[q] = *reinterpret_cast<const float4*>(b_src + 4 * q);
+      pa[slot][q] = *reinterpret_cast<const float4*>(a_src + 4 * q);
+      pb[slot][q] = *reinterpret_cast<const float4*>(b_src + 4 * q);
     }
   };
-  auto lstore = [&](int buf) {
+  auto lstore_s = [&](int slot, int buf) {
     const int o = srow * kRow + scol;
 #pragma unroll
     for (int q = 0; q < kF4 / 2; ++q) {
       u32x4 hi, lo;
-      split8(pa[2 * q], pa[2 * q + 1], hi, lo);
+      split8(pa[slot][2 * q], pa[slot][2 * q + 1], hi, lo);
       *reinterpret_cast<u32x4*>(&sA[buf].hi[o + 8 * q]) = hi;
       *reinterpret_cast<u32x4*>(&sA[buf].lo[o + 8 * q]) = lo;
-      split8(pb[2 * q], pb[2 * q + 1], hi, lo);
+      split8(pb[slot][2 * q], pb[slot][2 * q + 1], hi, lo);
       *reinterpret_cast<u32x4*>(&sB[buf].hi[o + 8 * q]) = hi;
       *reinterpret_cast<u32x4*>(&sB[buf].lo[o + 8 * q]) = lo;
     }
   };
-
-  gload(0);
-  lstore(0);
-  __syncthreads();
-  int cur = 0;
-  for (int st = 0; st < nstage; ++st) {
-    const bool has_next = st + 1 < nstage;
-    if (has_next) gload(st + 1);
+  auto compute = [&](int cur, int st, bool epi_in_loop) {
     const Img& ta = sA[cur];
     const Img& tb = sB[cur];
 #pragma unroll
@@ -261,14 +265,89 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_k(GArgs a) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
         }
     }
-    if (st % nk == nk - 1) {  // tile finished: epilogue (resets acc) while the next stage loads
+    if (epi_in_loop && st % nk == nk - 1) {  // tile finished: epilogue (resets acc) while the next stage loads
       const int t = t_begin + st / nk;
       epilogue<EPI>(a, acc, (int64_t)(t / a.tiles_n) * kBM, (t % a.tiles_n) * kBN, wm, wn, h, c);
     }
-    if (has_next) lstore(cur ^ 1);  // cur^1 was read in the previous stage, fenced by its barrier
+  };
+
+  if constexpr (Q == 1) {
+    gload_s(0, 0);
+    lstore_s(0, 0);
     __syncthreads();
-    cur ^= 1;
+    int cur = 0;
+    for (int st = 0; st < nstage; ++st) {
+      const bool has_next = st + 1 < nstage;
+      if (has_next) gload_s(0, st + 1);
+      compute(cur, st, true);
+      if (has_next) lstore_s(0, cur ^ 1);  // cur^1 was read in the previous stage, fenced by its barrier
+      __syncthreads();
+      cur ^= 1;
+    }
+  } else {
+    // stage s lives in register slot s % Q; stages st+1 .. st+Q are in flight while stage st computes.
+    // One tile per workgroup (the host launches this form only with per == 1): the epilogue runs after
+    // the loop, so no branch inside it drains the loads in flight
+    gload_s(0, 0);
+    lstore_s(0, 0);
+#pragma unroll
+    for (int k = 1; k <= Q; ++k) gload_s(k % Q, k);
+    __syncthreads();
+    int cur = 0;
+    for (int st0 = 0; st0 < nstage; st0 += Q) {
+#pragma unroll
+      for (int k = 0; k < Q; ++k) {
+        const int st = st0 + k;
+        if (st >= nstage) break;
+        compute(cur, st, false);
+        if (st + 1 < nstage) lstore_s((k + 1) % Q, cur ^ 1);
+        __syncthreads();
+        gload_s((k + 1) % Q, st + 1 + Q);  // the slot just stored: stage st + 1 + Q (clamped)
+        cur ^= 1;
+      }
+    }
+    const int64_t m0 = (int64_t)(t_begin / a.tiles_n) * kBM;
+    const int n0 = (t_begin % a.tiles_n) * kBN;
+    if (a.ksplit > 1) {  // raw partial sums; gemm_splitk_reduce_k adds the splits in order and applies EPI
+      float* P = a.part + (int64_t)split * a.M * a.N;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int64_t m = m0 + wm * 64 + 32 * i + tile_row(r, h);
+            if (m < a.M) P[m * a.N + n0 + wn * 64 + 32 * j + c] = acc[i][j][r];
+          }
+    } else {
+      epilogue<EPI>(a, acc, m0, n0, wm, wn, h, c);
+    }
   }
+}
+
+// C = EPI(sum over the splits of part, in split order) with epilogue<EPI>'s arithmetic per element
+template <int EPI>
+__global__ __launch_bounds__(256) void gemm_splitk_reduce_k(GArgs a) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= a.M * (int64_t)a.N) return;
+  const int64_t m = e / a.N;
+  const int n = (int)(e % a.N);
+  float v = 0.0f;
+  for (int s = 0; s < a.ksplit; ++s) v += a.part[(int64_t)s * a.M * a.N + e];
+  if (EPI == EPI_DGELU_DROP) v *= a.aux[m * a.ldaux + n];
+  const float bn = a.bias ? a.bias[n] : 0.0f;
+  if (EPI == EPI_BIAS) {
+    v += bn;
+  } else if (EPI == EPI_GELU_DROP) {
+    v += bn;
+    const float cdf = 0.5f * (1.0f + erff(v * 0.70710678118654752f));
+    if (a.aux) a.aux[m * a.ldaux + n] = cdf + v * 0.3989422804014327f * __expf(-0.5f * v * v);
+    v *= cdf;
+    if (a.drop.active()) v = keep(a.drop, (uint32_t)m * (uint32_t)a.N + (uint32_t)n) ? v * a.drop.scale : 0.0f;
+  } else if (a.drop.active()) {
+    v = keep(a.drop, (uint32_t)m * (uint32_t)a.N + (uint32_t)n) ? v * a.drop.scale : 0.0f;
+  }
+  a.C[m * a.ldc + n] = v;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -628,6 +707,17 @@ int ws_waves() {
   return v;
 }
 
+// RSX_GEMM_DEEP = 0 | 1 (A/B): the LDS-staged GEMM with four stages in flight when its tiles fit the chip
+bool deep_prefetch() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("RSX_GEMM_DEEP");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+bool a_nk_long(int K) { return K / kBK >= 16; }
+
 // RSX_GEMM_WS_PF = 0 | 1 (A/B): four waves with the B-fragment prefetch (PF) or without
 bool ws_pf() {
   static int v = -1;
@@ -645,11 +735,35 @@ void launch_ws(const GArgs& g, hipStream_t st) {
   else launch_ws_w<KC, NBW, 4>(g, st);
 }
 
+// split-K plan of the LDS-staged path: with fewer output tiles than CUs (one workgroup per CU at most,
+// e.g. the text BERT's 768-wide GEMMs at a few thousand tokens) and a long K, S K-ranges of >= 256 per
+// tile (S in {8, 4, 3, 2}, tiles * S <= 4 * CUs); M = 3,000 (tools/gemm_bert_micro.py): 768 x 3072 0.135 ->
+// 0.101 ms, 768 x 2304 0.105 -> 0.083 ms. 1 = no split. RSX_GEMM_SPLITK=0 disables it.
+int split_plan(int64_t M, int N, int K) {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("RSX_GEMM_SPLITK");
+    on = (e && e[0] == '0') ? 0 : 1;
+  }
+  if (!on || N % kBN || K % kBK || (K == 128 || K == 256 || K == 384)) return 1;
+  const int64_t tiles = ((M + kBM - 1) / kBM) * (N / kBN);
+  const int cus = num_cus();
+  if (tiles >= cus) return 1;
+  for (int S : {8, 4, 3, 2})  // K ranges of >= 256: at 192 (K = 768, S = 4) 0.046 vs 0.042 ms unsplit
+    if (K % (S * kBK) == 0 && K / S >= 256 && tiles * S <= 4LL * cus) return S;
+  return 1;
+}
 }  // namespace
 
-RSX_API int rsx_gemm_x3(const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias, int64_t M,
+RSX_API int64_t rsx_gemm_x3_split_floats(int64_t M, int N, int K) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  const int S = split_plan(M, N, K);
+  return S > 1 ? (int64_t)S * M * N : 0;
+}
+
+static int gemm_x3_impl(const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias, int64_t M,
                         int N, int K, int epi, float* aux, int64_t ldaux, float p_drop, uint64_t seed, float* C,
-                        int64_t ldc, void* stream) {
+                        int64_t ldc, float* ws, int64_t ws_floats, void* stream) {
   RSX_ARG(A && B && C, "null tensor");
   RSX_ARG(M >= 0 && N > 0 && K > 0 && N % kBN == 0 && K % kBK == 0, "N must be a multiple of 128, K of 32");
   static_assert(kBK == 16 || kBK == 32, "stage depth 16 or 32");
@@ -676,15 +790,51 @@ RSX_API int rsx_gemm_x3(const float* A, int64_t lda, const float* B, int64_t ldb
     if (K == 256) { launch_ws<2, 128>(g, st); RSX_LAUNCHED(); return 0; }
     if (K == 384) { launch_ws<3, 64>(g, st); RSX_LAUNCHED(); return 0; }
   }
+  const int S = split_plan(M, N, K);
+  if (S > 1 && ws && ws_floats >= (int64_t)S * M * N && ldc >= N) {
+    // split-K: (split, tile) workgroups write raw partial sums, then one pass adds them in split order
+    // and applies the epilogue (the epilogue form is not instantiated in the partial kernel)
+    g.per = 1;
+    g.ksplit = S;
+    g.kspan = K / S;
+    g.part = ws;
+    const int64_t blocks = tiles * S;
+    const int grid = (int)((blocks + 7) / 8 * 8);
+    hipLaunchKernelGGL((gemm_x3_nt_k<EPI_BIAS, 4>), dim3(grid), dim3(256), 0, st, g);
+    RSX_LAUNCHED();
+    const unsigned rb = (unsigned)((M * (int64_t)N + 255) / 256);
+    if (epi == EPI_BIAS) hipLaunchKernelGGL(gemm_splitk_reduce_k<EPI_BIAS>, dim3(rb), dim3(256), 0, st, g);
+    else if (epi == EPI_GELU_DROP) hipLaunchKernelGGL(gemm_splitk_reduce_k<EPI_GELU_DROP>, dim3(rb), dim3(256), 0, st, g);
+    else hipLaunchKernelGGL(gemm_splitk_reduce_k<EPI_DGELU_DROP>, dim3(rb), dim3(256), 0, st, g);
+    RSX_LAUNCHED();
+    return 0;
+  }
   // tiles per workgroup: enough workgroups for two per CU, each a continuous stage stream
   g.per = (int)((tiles + RSX_GEMM_BLOCKS - 1) / RSX_GEMM_BLOCKS);
   const int64_t blocks = (tiles + g.per - 1) / g.per;
   const int grid = (int)((blocks + 7) / 8 * 8);
-  if (epi == EPI_BIAS) hipLaunchKernelGGL(gemm_x3_nt_k<EPI_BIAS>, dim3(grid), dim3(256), 0, st, g);
+  // few tiles for the chip (one workgroup per CU at most) and a long K: four stages in flight per workgroup
+  if (deep_prefetch() && g.per == 1 && blocks <= num_cus() && a_nk_long(K)) {
+    if (epi == EPI_BIAS) hipLaunchKernelGGL((gemm_x3_nt_k<EPI_BIAS, 4>), dim3(grid), dim3(256), 0, st, g);
+    else if (epi == EPI_GELU_DROP) hipLaunchKernelGGL((gemm_x3_nt_k<EPI_GELU_DROP, 4>), dim3(grid), dim3(256), 0, st, g);
+    else hipLaunchKernelGGL(gemm_x3_nt_k<EPI_DGELU_DROP>, dim3(grid), dim3(256), 0, st, g);  // Q = 4 spills here
+  } else if (epi == EPI_BIAS) hipLaunchKernelGGL(gemm_x3_nt_k<EPI_BIAS>, dim3(grid), dim3(256), 0, st, g);
   else if (epi == EPI_GELU_DROP) hipLaunchKernelGGL(gemm_x3_nt_k<EPI_GELU_DROP>, dim3(grid), dim3(256), 0, st, g);
   else hipLaunchKernelGGL(gemm_x3_nt_k<EPI_DGELU_DROP>, dim3(grid), dim3(256), 0, st, g);
   RSX_LAUNCHED();
   return 0;
+}
+
+RSX_API int rsx_gemm_x3(const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias, int64_t M,
+                        int N, int K, int epi, float* aux, int64_t ldaux, float p_drop, uint64_t seed, float* C,
+                        int64_t ldc, void* stream) {
+  return gemm_x3_impl(A, lda, B, ldb, bias, M, N, K, epi, aux, ldaux, p_drop, seed, C, ldc, nullptr, 0, stream);
+}
+
+RSX_API int rsx_gemm_x3_ws(const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias, int64_t M,
+                           int N, int K, int epi, float* aux, int64_t ldaux, float p_drop, uint64_t seed, float* C,
+                           int64_t ldc, float* ws, int64_t ws_floats, void* stream) {
+  return gemm_x3_impl(A, lda, B, ldb, bias, M, N, K, epi, aux, ldaux, p_drop, seed, C, ldc, ws, ws_floats, stream);
 }
 
 // C = epi(A . Bt + bias) with the right operand as stored, Bt [K, N] (row stride ldbt >= N): the

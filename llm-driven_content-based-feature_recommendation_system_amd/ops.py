@@ -1284,10 +1284,13 @@ def gemm_x3(a, b, bias=None, epi=EPI_BIAS, aux=None, p_drop=0.0, seed=0, tag=Non
     out = torch.empty(M, n, device=a.device, dtype=torch.float32)
     if M == 0:
         return out
+    nws = N.lib().rsx_gemm_x3_split_floats(M, n, K)  # > 0: split-K for a shape with fewer tiles than CUs
+    ws = torch.empty(nws, device=a.device, dtype=torch.float32) if nws > 0 else None
     with timed(tag or "gemm_x3"):
-        rc = N.lib().rsx_gemm_x3(N.ptr(a), a.stride(0), N.ptr(b), b.stride(0), N.ptr(None if bias is None else _c(bias)),
-                                 M, n, K, epi, N.ptr(aux), 0 if aux is None else aux.stride(0), float(p_drop),
-                                 int(seed), N.ptr(out), out.stride(0), N.stream())
+        rc = N.lib().rsx_gemm_x3_ws(N.ptr(a), a.stride(0), N.ptr(b), b.stride(0),
+                                    N.ptr(None if bias is None else _c(bias)), M, n, K, epi, N.ptr(aux),
+                                    0 if aux is None else aux.stride(0), float(p_drop), int(seed), N.ptr(out),
+                                    out.stride(0), N.ptr(ws), nws, N.stream())
     N.check(rc, "gemm_x3")
     return out
 
