@@ -1080,6 +1080,7 @@ def train_bench(args, global_batch, steps, warmup, items, cfg, model, item_tower
     ops.timing_start()
     from recsys_amd import _native as N
     N.lib().rsx_kernel_events(1)  # HIP events around each fused-forward kernel launch (roofline)
+    N.lib().rsx_gather_events(1)  # and around each embedding-gather launch (gather roofline)
     t0 = time.perf_counter()
     losses = None
     for i in range(steps):
@@ -1094,6 +1095,10 @@ def train_bench(args, global_batch, steps, warmup, items, cfg, model, item_tower
     n_kev = N.lib().rsx_kernel_events_read(kev, 256)
     fwdg_kernel_ms = [float(kev[i]) for i in range(max(n_kev, 0))]
     N.lib().rsx_kernel_events(0)
+    gms, gtok = (ctypes.c_float * 256)(), (ctypes.c_int64 * 256)()
+    n_gev = N.lib().rsx_gather_events_read(gms, gtok, 256)
+    gather_events = [(float(gms[i]), int(gtok[i])) for i in range(max(n_gev, 0))]
+    N.lib().rsx_gather_events(0)
     retries = torch.cuda.memory_stats().get("num_alloc_retries", 0) - retries0
     # drain the prefetched indexes of the steps that never ran
     pending.clear()
@@ -1150,6 +1155,7 @@ def train_bench(args, global_batch, steps, warmup, items, cfg, model, item_tower
     return {"elapsed": float(elapsed.item()), "kernel_times": kernel_times, "losses": losses, "n_glob": n_glob,
             "n_dist": n_dist, "n_tok": n_tok, "host_enqueue_ms": round(1e3 * sum(enqueue) / max(len(enqueue), 1), 3),
             "host_unloaded": host_unloaded, "alloc_retries": int(retries), "fwdg_kernel_ms": fwdg_kernel_ms,
+            "gather_events": gather_events,
             "clocks": {"before_timed_steps": clk0, "after_timed_steps": clk1} if sample_clocks else None,
             "users_local": b_loc}
 
@@ -1284,6 +1290,18 @@ def gather_roofline(args, tb):
     table (24 MB) and the 12-row time table are L2/MALL-resident at this size, so this figure
     credits cache hits as HBM bytes; see secondary_gather_1m for DRAM-resident rows."""
     kernel_times, n_tok = tb["kernel_times"], tb["n_tok"]
+    ev = tb.get("gather_events") or []
+    if ev:  # HIP events around each launch of the gather kernel (issued by the native tower program)
+        ms = sum(e[0] for e in ev) / len(ev)
+        tok = sum(e[1] for e in ev) / len(ev)
+        bpl = 2064.0 * tok
+        return {"kernel": "seq_embed_fwd_k", "bound": "hbm", "bytes_per_token": 2064,
+                "tokens_per_launch": int(tok), "avg_launch_ms": round(ms, 4), "launches": len(ev),
+                "timer": "HIP events around each gather launch inside rsx_tower_fwd (rsx_gather_events), timed steps",
+                "achieved": round(bpl / (ms / 1e3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(bpl / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                "cache_note": "item/time tables cache-resident (47k x 512 B + 12 rows); secondary_gather_1m prices "
+                              "DRAM-resident rows"}
     g_n, g_ms = kernel_times.get("seq_embed_fwd", (0, 0.0))
     if not g_n:
         return None

@@ -212,6 +212,11 @@ int rsx_nce_grouped_fwd_grad(const float* A, const float* B, const float* bias, 
  * Enabling clears the list. */
 int rsx_kernel_events(int on);
 int rsx_kernel_events_read(float* ms, int max_n);
+/* The same for the embedding gather (rsx_seq_embed_fwd's kernel, whichever caller issues it: the per-op
+ * path or rsx_tower_fwd): rsx_gather_events(1) clears and starts recording; _read waits and writes up to
+ * max_n launch times (ms) with each launch's token count. */
+int rsx_gather_events(int on);
+int rsx_gather_events_read(float* ms, int64_t* tokens, int max_n);
 int rsx_nce_grouped_bwd(const float* A, const float* B, const float* bias, const float* colcnt, const int* row_col,
                         const int* row_beg, const int* row_end, const int* exc_cols, const int* col_beg,
                         const int* col_end, const int* exc_s, const int* exc_e, const int* exc_n, int64_t N,

@@ -61,6 +61,8 @@ _SIGS = {
                                   c_p, c_p, c_p]),
     "rsx_kernel_events": (c_i, [c_i]),
     "rsx_kernel_events_read": (c_i, [c_p, c_i]),
+    "rsx_gather_events": (c_i, [c_i]),
+    "rsx_gather_events_read": (c_i, [c_p, c_p, c_i]),
     "rsx_nce_grouped_fwd_grad": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_f, c_i,
                                        c_i, c_p, c_p, c_p, c_p]),
     "rsx_nce_grouped_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64,

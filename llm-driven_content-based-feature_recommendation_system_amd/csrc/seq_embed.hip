@@ -8,6 +8,9 @@
 // by D/4 lanes, each holding one float4, so every global access is 16 B/lane.
 // HBM-bound: per token the live bytes are base row + gathered rows + output row.
 #include "rsx_common.h"
+#include <mutex>
+#include <utility>
+#include <vector>
 
 namespace {
 
@@ -884,7 +887,55 @@ bool fill_fwd(FwdArgs& a, const float* base, const int64_t* const* ids, const fl
   return true;
 }
 
+// Measurement hook (include/recsys_amd.h rsx_gather_events): HIP events around each forward gather launch,
+// whichever caller issues it (the per-op path or the native tower program), for the bench's gather roofline.
+struct GatherEvents {
+  std::mutex mu;
+  bool on = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+  std::vector<int64_t> tokens;
+  void clear() {
+    for (auto& e : ev) {
+      (void)hipEventDestroy(e.first);
+      (void)hipEventDestroy(e.second);
+    }
+    ev.clear();
+    tokens.clear();
+  }
+};
+GatherEvents& gather_events() {
+  static GatherEvents g;
+  return g;
+}
 }  // namespace
+
+RSX_API int rsx_gather_events(int on) {
+  GatherEvents& g = gather_events();
+  std::lock_guard<std::mutex> lk(g.mu);
+  g.clear();
+  g.on = on != 0;
+  return 0;
+}
+
+RSX_API int rsx_gather_events_read(float* ms, int64_t* tokens, int max_n) {
+  RSX_ARG((ms != nullptr && tokens != nullptr) || max_n == 0, "null output");
+  GatherEvents& g = gather_events();
+  std::lock_guard<std::mutex> lk(g.mu);
+  int n = 0;
+  for (size_t k = 0; k < g.ev.size() && n < max_n; ++k) {
+    float t = 0.0f;
+    hipError_t err = hipEventSynchronize(g.ev[k].second);
+    if (err == hipSuccess) err = hipEventElapsedTime(&t, g.ev[k].first, g.ev[k].second);
+    if (err != hipSuccess) {
+      rsx::set_error("%s: %s", __func__, hipGetErrorString(err));
+      return -1;
+    }
+    ms[n] = t;
+    tokens[n] = g.tokens[k];
+    ++n;
+  }
+  return n;
+}
 
 RSX_API int rsx_seq_embed_fwd(const float* base, const int64_t* const* ids, const float* const* tables, int ntab,
                               const float* gate, const float* pos, const int64_t* tok_pos, const float* ln_w,
@@ -901,10 +952,21 @@ RSX_API int rsx_seq_embed_fwd(const float* base, const int64_t* const* ids, cons
   FwdArgs a;
   fill_fwd(a, base, ids, tables, ntab, gate, pos, tok_pos, ln_w, ln_b, eps, T, L, out, mean, rstd, p_drop, seed);
   hipStream_t st = (hipStream_t)stream;
+  GatherEvents& ge = gather_events();
+  std::pair<hipEvent_t, hipEvent_t> evp{nullptr, nullptr};
+  const bool timed = ge.on;  // read without the lock: toggled only between steps by the caller
+  if (timed && hipEventCreate(&evp.first) == hipSuccess && hipEventCreate(&evp.second) == hipSuccess)
+    (void)hipEventRecord(evp.first, st);
   if (D == 64) launch_fwd<64>(a, st);
   else if (D == 128) launch_fwd<128>(a, st);
   else launch_fwd<256>(a, st);
   RSX_LAUNCHED();
+  if (timed && evp.second) {
+    (void)hipEventRecord(evp.second, st);
+    std::lock_guard<std::mutex> lk(ge.mu);
+    ge.ev.push_back(evp);
+    ge.tokens.push_back(T);
+  }
   return 0;
 }
 
