@@ -578,10 +578,13 @@ def _absprod(a, b):
     return a.double().abs() @ b.double().abs().t()
 
 
-@pytest.mark.parametrize("M,N,K", [(1000, 384, 128), (777, 128, 256), (5, 256, 384), (129, 128, 32), (0, 128, 32)])
+@pytest.mark.parametrize("M,N,K", [(1000, 384, 128), (777, 128, 256), (5, 256, 384), (129, 128, 32), (0, 128, 32),
+                                   (1000, 256, 1024), (130, 128, 2048), (3000, 768, 3072), (3000, 2304, 768)])
 def test_gemm_x3_against_float64(gpu, M, N, K):
     """rsx_gemm_x3 (bf16x3 products, fp32 accumulate) vs float64: |C - ref| <= 2e-5 * sum_k
-    |a_mk b_nk| + 1e-6 per element (each bf16x3 product is within 2^-17 of exact)."""
+    |a_mk b_nk| + 1e-6 per element (each bf16x3 product is within 2^-17 of exact). The last four shapes
+    have fewer output tiles than CUs and a long K: split-K through ops.gemm_x3's workspace (S = 4, 8, 4)
+    and the four-stage prefetch (3000 x 2304)."""
     g = torch.Generator().manual_seed(M + N + K)
     a = torch.randn(M, K, generator=g)
     b = torch.randn(N, K, generator=g)
@@ -593,13 +596,15 @@ def test_gemm_x3_against_float64(gpu, M, N, K):
         assert ((c - ref).abs() <= 2e-5 * _absprod(a, b) + 1e-6).all()
 
 
-def test_gemm_x3_gelu_dropout_epilogues(gpu):
+@pytest.mark.parametrize("K,K2", [(128, 128), (1024, 1024)])
+def test_gemm_x3_gelu_dropout_epilogues(gpu, K, K2):
     """EPI_GELU_DROP: C = dropout(gelu(pre)) (kept entries gelu(pre) / (1 - p), drop rate ~p)
     and aux = gelu'(pre), both against float64 from the inputs (bound 2e-5 * sum|a||b| on pre,
     propagated through |gelu'| <= 1.13 and |gelu''| <= 0.6); EPI_DGELU_DROP with the same seed:
-    zero exactly where the forward dropped, (dY W) / (1 - p) * aux elsewhere."""
+    zero exactly where the forward dropped, (dY W) / (1 - p) * aux elsewhere. K = 1024: both GEMMs
+    take the split-K path (the epilogues applied in the reduction pass)."""
     g = torch.Generator().manual_seed(11)
-    M, N, K, p, seed = 1031, 256, 128, 0.2, 12345
+    M, N, p, seed = 1031, 256, 0.2, 12345
     x = torch.randn(M, K, generator=g)
     w1 = torch.randn(N, K, generator=g) / math.sqrt(K)
     b1 = torch.randn(N, generator=g)
@@ -616,8 +621,8 @@ def test_gemm_x3_gelu_dropout_epilogues(gpu):
     assert ((act - gel / (1 - p)).abs()[kept] <= (1.13 * bnd / (1 - p) + 2e-6)[kept]).all()
     frac = 1.0 - kept.double().mean().item()
     assert abs(frac - p) < 0.01
-    w2 = torch.randn(128, N, generator=g) / math.sqrt(N)
-    dy = torch.randn(M, 128, generator=g)
+    w2 = torch.randn(K2, N, generator=g) / math.sqrt(N)
+    dy = torch.randn(M, K2, generator=g)
     dpre = ops.gemm_x3(dy.to(gpu), w2.t().to(gpu), None, ops.EPI_DGELU_DROP, aux.float().to(gpu), p,
                        seed).cpu().double()
     dact = dy.double() @ w2.double()
