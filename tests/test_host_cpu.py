@@ -1,6 +1,8 @@
 """Host-side logic of the round-5 step (no GPU): the step index's single-allocation carving
 (dist._carve) and the native clip+AdamW's applicability rules (ops.clip_adamw_step declines what
 it does not reproduce, leaving torch's clip_grad_norm_ + optimizer.step to run)."""
+import math
+
 import torch
 
 from recsys_amd import dist, ops
@@ -69,3 +71,38 @@ def test_module_params_same_set_as_parameters():
     got = ops.module_params(model)
     assert len(got) == len(list(model.parameters()))
     assert {id(p) for p in got} == {id(p) for p in model.parameters()}
+
+
+def test_emphasis_correction_identity_matches_dense_form():
+    """The arithmetic rsx_nce_emphasis_fwd / _bwd implement (csrc/infonce.hip, nce_emph_*_k), checked in
+    float64 against full_batch_hard_emphasis_loss's dense form (v1_refine_usertower.py:546-554): with lse
+    the masked row log-sum-exp and E_i = sum over allowed mined j of exp(S_ij - lse_i),
+      lse'_i = lse_i + log1p((e^m - 1) E_i),  loss'_i = lse'_i - S_ii - m [i mined],
+    and the gradient w.r.t. S is exp(S_ij - lse'_i) (1 + (e^m - 1) [j mined]) - [j = i] on allowed
+    columns (the dense backward with lse' in the workspace plus the mined entries' extra term)."""
+    g = torch.Generator().manual_seed(3)
+    N, K, m = 40, 5, 0.2 / 0.1
+    S = torch.randn(N, N, generator=g, dtype=torch.float64) * 3
+    keys = torch.randint(0, 25, (N,), generator=g)
+    same = (keys[:, None] == keys[None, :]) & ~torch.eye(N, dtype=torch.bool)
+    top = torch.stack([torch.randperm(N, generator=g)[:K] for _ in range(N)])  # may include masked / diagonal
+    top[0, 0] = 0                                                                # a row whose own column is mined
+    # dense reference (the reference's order: emphasis added, then the same-item mask, then CE)
+    Sd = S.clone().requires_grad_()
+    emph = torch.zeros(N, N, dtype=torch.float64).scatter_(1, top, m)
+    logits = (Sd + emph).masked_fill(same, float("-inf"))
+    ref = torch.nn.functional.cross_entropy(logits, torch.arange(N), reduction="sum")
+    ref.backward()
+    # the decomposition
+    Sm = S.masked_fill(same, float("-inf"))
+    lse = torch.logsumexp(Sm, 1)
+    mined = torch.zeros(N, N, dtype=torch.bool).scatter_(1, top, True) & ~same
+    E = (torch.exp(Sm - lse[:, None]) * mined).sum(1)
+    lse2 = lse + torch.log1p(math.expm1(m) * E)
+    self_mined = mined[torch.arange(N), torch.arange(N)]
+    loss = (lse2 - S.diagonal() - m * self_mined).sum()
+    assert abs(float(loss) - float(ref)) < 1e-9 * abs(float(ref))
+    p2 = torch.exp(Sm - lse2[:, None])
+    grad = p2 * (1 + math.expm1(m) * mined.double()) - torch.eye(N, dtype=torch.float64)
+    grad = grad.masked_fill(same, 0.0)
+    torch.testing.assert_close(grad, Sd.grad, atol=1e-12, rtol=1e-9)
