@@ -160,6 +160,14 @@ int rsx_nce_emphasis_bwd(const float* A, const float* B, const float* bias, cons
                          const int64_t* top, int64_t N, int64_t M, int64_t K, int64_t lda, int64_t ldb,
                          int64_t diag_offset, float tau, float margin, int precision, int nsplit_fwd,
                          const float* gout, float* ws, float* dA, float* dB, void* stream);
+/* The same without float atomics: the mined entries' weights go to cbuf [N*K] (floats) and one wave per
+ * column j adds them into dB from the column-sorted CSR of top (col_ptr [M+1] offsets, col_ent the entry
+ * ids i*K + r in column order; ids outside [0, M) left out) -- deterministic for a fixed entry order. */
+int rsx_nce_emphasis_bwd_csr(const float* A, const float* B, const float* bias, const int* k1a, const int* k1b,
+                             const int64_t* top, int64_t N, int64_t M, int64_t K, int64_t lda, int64_t ldb,
+                             int64_t diag_offset, float tau, float margin, int precision, int nsplit_fwd,
+                             const int64_t* col_ptr, const int64_t* col_ent, float* cbuf, const float* gout,
+                             float* ws, float* dA, float* dB, void* stream);
 
 /* ---- A6 grouped: the live LogQ loss over the batch's DISTINCT targets ------------------
  * Same objective as rsx_nce_fwd flags 6 on columns normalize(item_matrix)[t_j], evaluated

@@ -56,6 +56,8 @@ _SIGS = {
                                    c_i, c_i, c_p, c_p, c_p]),
     "rsx_nce_emphasis_bwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_f, c_f,
                                    c_i, c_i, c_p, c_p, c_p, c_p, c_p]),
+    "rsx_nce_emphasis_bwd_csr": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_f,
+                                       c_f, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "rsx_nce_grouped_workspace_floats": (c_i64, [c_i64, c_i64, c_i, c_i, c_i]),
     "rsx_nce_grouped_fwd": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_f, c_i, c_i,
                                   c_p, c_p, c_p]),

@@ -3576,6 +3576,9 @@ struct EmphArgs {
   float inv_tau, margin, em1;  // em1 = e^margin - 1
   float* lse; float* row_loss;
   const float* gout; float* dA; float* dB;
+  float* cbuf;              // [N*K] per mined entry c_ij (0 where skipped) instead of dB atomics, or null
+  const int64_t* col_ptr;   // [M+1] CSR over the mined entries sorted by column (with cbuf)
+  const int64_t* col_ent;   // [N*K] entry ids i*K + r in column order
 };
 
 __device__ __forceinline__ float emph_dot(const float2 x, const float* brow, int lane) {
@@ -3633,7 +3636,9 @@ __global__ __launch_bounds__(256) void nce_emph_bwd_k(EmphArgs a) {
     const float2 y = reinterpret_cast<const float2*>(brow)[lane];
     acc.x = fmaf(c, y.x, acc.x);
     acc.y = fmaf(c, y.y, acc.y);
-    if (a.dB) {  // mined columns are shared between rows: vector atomics (order not deterministic)
+    if (a.cbuf) {
+      if (lane == 0) a.cbuf[i * a.K + r] = c;
+    } else if (a.dB) {  // mined columns are shared between rows: vector atomics (order not deterministic)
       atomicAdd(a.dB + j * kD + 2 * lane, c * x.x);
       atomicAdd(a.dB + j * kD + 2 * lane + 1, c * x.y);
     }
@@ -3645,6 +3650,30 @@ __global__ __launch_bounds__(256) void nce_emph_bwd_k(EmphArgs a) {
     v.y += acc.y;
     *d = v;
   }
+}
+
+// dB from the per-entry weights: one wave per column j walks the entries mined into it (CSR, entry order
+// fixed by the host's stable sort) and adds c_ij A_i; each dB row belongs to one wave (deterministic)
+__global__ __launch_bounds__(256) void nce_emph_cols_k(EmphArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (j >= a.M) return;
+  const int64_t e0 = a.col_ptr[j], e1 = a.col_ptr[j + 1];
+  if (e0 == e1) return;
+  float2 acc = make_float2(0.0f, 0.0f);
+  for (int64_t e = e0; e < e1; ++e) {
+    const int64_t ent = a.col_ent[e];
+    const float c = a.cbuf[ent];
+    if (c == 0.0f) continue;  // wave-uniform
+    const float2 x = reinterpret_cast<const float2*>(a.A + (ent / a.K) * a.lda)[lane];
+    acc.x = fmaf(c, x.x, acc.x);
+    acc.y = fmaf(c, x.y, acc.y);
+  }
+  float2* d = reinterpret_cast<float2*>(a.dB + j * kD) + lane;
+  float2 v = *d;
+  v.x += acc.x;
+  v.y += acc.y;
+  *d = v;
 }
 
 int emph_setup(EmphArgs& e, const float* A, const float* B, const float* bias, const int* k1a, const int* k1b,
@@ -3667,6 +3696,7 @@ int emph_setup(EmphArgs& e, const float* A, const float* B, const float* bias, c
   e.lse = ws + 4 * (int64_t)nf * N;
   e.row_loss = e.lse + N;
   e.gout = nullptr; e.dA = nullptr; e.dB = nullptr;
+  e.cbuf = nullptr; e.col_ptr = nullptr; e.col_ent = nullptr;
   return 0;
 }
 }  // namespace
@@ -3704,6 +3734,33 @@ RSX_API int rsx_nce_emphasis_bwd(const float* A, const float* B, const float* bi
   e.gout = gout; e.dA = dA; e.dB = dB;
   hipLaunchKernelGGL(nce_emph_bwd_k, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, (hipStream_t)stream, e);
   RSX_LAUNCHED();
+  return 0;
+}
+
+RSX_API int rsx_nce_emphasis_bwd_csr(const float* A, const float* B, const float* bias, const int* k1a,
+                                     const int* k1b, const int64_t* top, int64_t N, int64_t M, int64_t K, int64_t lda,
+                                     int64_t ldb, int64_t diag_offset, float tau, float margin, int precision,
+                                     int nsplit_fwd, const int64_t* col_ptr, const int64_t* col_ent, float* cbuf,
+                                     const float* gout, float* ws, float* dA, float* dB, void* stream) {
+  EmphArgs e;
+  const int rc = emph_setup(e, A, B, bias, k1a, k1b, top, N, M, K, lda, ldb, diag_offset, tau, margin, precision,
+                            nsplit_fwd, ws);
+  if (rc) return rc;
+  RSX_ARG(gout != nullptr, "gout required");
+  RSX_ARG(!dB || (col_ptr && col_ent && cbuf), "dB needs the column CSR and the entry buffer");
+  if (N == 0 || K == 0 || (!dA && !dB)) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  e.gout = gout; e.dA = dA; e.dB = dB;
+  if (dB) {
+    e.cbuf = cbuf; e.col_ptr = col_ptr; e.col_ent = col_ent;
+    (void)hipMemsetAsync(cbuf, 0, (size_t)(N * K) * sizeof(float), st);  // skipped entries keep 0
+  }
+  hipLaunchKernelGGL(nce_emph_bwd_k, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, e);
+  RSX_LAUNCHED();
+  if (dB) {
+    hipLaunchKernelGGL(nce_emph_cols_k, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, st, e);
+    RSX_LAUNCHED();
+  }
   return 0;
 }
 

@@ -590,7 +590,13 @@ class _NCEEmphasis(torch.autograd.Function):
                                               K, A.stride(0), B.stride(0), 0, tau, margin, prec, _NSPLIT_FWD,
                                               N.ptr(ws), N.ptr(out2), N.stream())
             N.check(rc, "nce_emphasis_fwd")
-        ctx.save_for_backward(A, B, bias, k1, top, ws)
+        # the mined entries in column order (stable: a fixed summation order per column) for the
+        # backward's atomic-free dB pass
+        flat = top.reshape(-1)
+        key = torch.where((flat >= 0) & (flat < m), flat, torch.full_like(flat, m))
+        sk, col_ent = torch.sort(key, stable=True)
+        col_ptr = torch.searchsorted(sk, torch.arange(m + 1, device=A.device, dtype=sk.dtype))
+        ctx.save_for_backward(A, B, bias, k1, top, ws, _c(col_ptr), _c(col_ent))
         ctx.cfg = (n, m, K, tau, margin, tag, x3)
         cnt = out2[1]
         ctx.mark_non_differentiable(cnt)
@@ -598,7 +604,7 @@ class _NCEEmphasis(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g, _gcnt):
-        A, B, bias, k1, top, ws = ctx.saved_tensors
+        A, B, bias, k1, top, ws, col_ptr, col_ent = ctx.saved_tensors
         n, m, K, tau, margin, tag, x3 = ctx.cfg
         g = _c(g.reshape(1).to(torch.float32))
         head = (N.ptr(A), N.ptr(B), N.ptr(bias), N.ptr(k1), N.ptr(k1), None, None, n, m, A.stride(0), B.stride(0), 0,
@@ -615,9 +621,12 @@ class _NCEEmphasis(torch.autograd.Function):
             if dB is not None:
                 N.check(fn(*args, None, N.ptr(dB), 0, N.stream()), "nce_bwd(cols)")
             if dA is not None or dB is not None:
-                rc = N.lib().rsx_nce_emphasis_bwd(N.ptr(A), N.ptr(B), N.ptr(bias), N.ptr(k1), N.ptr(k1), N.ptr(top),
-                                                  n, m, K, A.stride(0), B.stride(0), 0, tau, margin, 1 if x3 else 0,
-                                                  _NSPLIT_FWD, N.ptr(g), N.ptr(ws), N.ptr(dA), N.ptr(dB), N.stream())
+                cbuf = torch.empty(n * K, device=A.device, dtype=torch.float32) if dB is not None else None
+                rc = N.lib().rsx_nce_emphasis_bwd_csr(N.ptr(A), N.ptr(B), N.ptr(bias), N.ptr(k1), N.ptr(k1),
+                                                      N.ptr(top), n, m, K, A.stride(0), B.stride(0), 0, tau, margin,
+                                                      1 if x3 else 0, _NSPLIT_FWD, N.ptr(col_ptr), N.ptr(col_ent),
+                                                      N.ptr(cbuf), N.ptr(g), N.ptr(ws), N.ptr(dA), N.ptr(dB),
+                                                      N.stream())
                 N.check(rc, "nce_emphasis_bwd")
         return dA, dB, None, None, None, None, None, None
 
