@@ -82,10 +82,12 @@ __device__ __forceinline__ bool keep(const rsx::Dropout& d, uint32_t idx) {
   return x >= d.thresh;
 }
 
-struct Img {
-  __bf16 hi[kBM * kRow];
-  __bf16 lo[kBM * kRow];
+template <int BK>
+struct ImgT {
+  __bf16 hi[kBM * (BK + 8)];
+  __bf16 lo[kBM * (BK + 8)];
 };
+using Img = ImgT<kBK>;
 
 struct GArgs {
   const float* A;     // [M, lda]
@@ -184,10 +186,11 @@ __device__ __forceinline__ void epilogue(const GArgs& a, f32x16 (&acc)[2][2], in
 // BERT's GEMMs) a workgroup's single 16-KB stage in flight leaves it waiting on memory latency for
 // most of each stage; Q = 4 keeps four (64 KB) in flight at 16 VGPRs per stage. Same products and
 // order (bit-identical results).
-template <int EPI, int Q = 1>
+template <int EPI, int Q = 1, int BK = kBK>
 __global__ __launch_bounds__(256, 2) void gemm_x3_nt_k(GArgs a) {
-  __shared__ __attribute__((aligned(16))) Img sA[2];
-  __shared__ __attribute__((aligned(16))) Img sB[2];
+  constexpr int kRowK = BK + 8, kF4K = BK / 8;
+  __shared__ __attribute__((aligned(16))) ImgT<BK> sA[2];
+  __shared__ __attribute__((aligned(16))) ImgT<BK> sB[2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, c = lane & 31;
   const int wm = wave >> 1, wn = wave & 1;
@@ -198,7 +201,7 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_k(GArgs a) {
   int t_end = a.ksplit > 1 ? t_begin + 1 : t_begin + a.per;
   if (t_end > a.tiles) t_end = a.tiles;
   if (t_begin >= t_end || split >= (a.ksplit > 1 ? a.ksplit : 1)) return;
-  const int nk = (a.ksplit > 1 ? a.kspan : a.K) / kBK;
+  const int nk = (a.ksplit > 1 ? a.kspan : a.K) / BK;
   const int kbase = split * (a.ksplit > 1 ? a.kspan : 0);
   const int nstage = (t_end - t_begin) * nk;
 
@@ -213,25 +216,25 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_k(GArgs a) {
   // staging: thread -> row tid>>1 of both tiles, 16 floats at column (tid&1)*16 of the stage.
   // Rows past M load row m0 instead (unconditional loads: a predicated load would make the
   // compiler wait on each one); their C rows are never stored and no other row depends on them.
-  const int srow = tid >> 1, scol = (tid & 1) * (kBK / 2);
-  float4 pa[Q][kF4], pb[Q][kF4];
+  const int srow = tid >> 1, scol = (tid & 1) * (BK / 2);
+  float4 pa[Q][kF4K], pb[Q][kF4K];
   auto gload_s = [&](int slot, int st) {
     if (st >= nstage) st = nstage - 1;  // unconditional (clamped): the same outstanding loads on every path
-    const int t = t_begin + st / nk, k0 = kbase + (st % nk) * kBK;
+    const int t = t_begin + st / nk, k0 = kbase + (st % nk) * BK;
     const int64_t m0 = (int64_t)(t / a.tiles_n) * kBM;
     const int n0 = (t % a.tiles_n) * kBN;
     const float* a_src = a.A + (m0 + srow < a.M ? m0 + srow : m0) * a.lda + scol + k0;
     const float* b_src = a.B + (int64_t)(n0 + srow) * a.ldb + scol + k0;
 #pragma unroll
-    for (int q = 0; q < kF4; ++q) {
+    for (int q = 0; q < kF4K; ++q) {
       pa[slot][q] = *reinterpret_cast<const float4*>(a_src + 4 * q);
       pb[slot][q] = *reinterpret_cast<const float4*>(b_src + 4 * q);
     }
   };
   auto lstore_s = [&](int slot, int buf) {
-    const int o = srow * kRow + scol;
+    const int o = srow * kRowK + scol;
 #pragma unroll
-    for (int q = 0; q < kF4 / 2; ++q) {
+    for (int q = 0; q < kF4K / 2; ++q) {
       u32x4 hi, lo;
       split8(pa[slot][2 * q], pa[slot][2 * q + 1], hi, lo);
       *reinterpret_cast<u32x4*>(&sA[buf].hi[o + 8 * q]) = hi;
@@ -242,15 +245,15 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_nt_k(GArgs a) {
     }
   };
   auto compute = [&](int cur, int st, bool epi_in_loop) {
-    const Img& ta = sA[cur];
-    const Img& tb = sB[cur];
+    const ImgT<BK>& ta = sA[cur];
+    const ImgT<BK>& tb = sB[cur];
 #pragma unroll
-    for (int ks = 0; ks < kBK / 16; ++ks) {
+    for (int ks = 0; ks < BK / 16; ++ks) {
       bf16x8 ah[2], al[2], bh[2], bl[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const int oa = (wm * 64 + 32 * i + c) * kRow + 16 * ks + 8 * h;
-        const int ob = (wn * 64 + 32 * i + c) * kRow + 16 * ks + 8 * h;
+        const int oa = (wm * 64 + 32 * i + c) * kRowK + 16 * ks + 8 * h;
+        const int ob = (wn * 64 + 32 * i + c) * kRowK + 16 * ks + 8 * h;
         ah[i] = *reinterpret_cast<const bf16x8*>(&ta.hi[oa]);
         al[i] = *reinterpret_cast<const bf16x8*>(&ta.lo[oa]);
         bh[i] = *reinterpret_cast<const bf16x8*>(&tb.hi[ob]);
@@ -717,6 +720,16 @@ bool deep_prefetch() {
   return v == 1;
 }
 bool a_nk_long(int K) { return K / kBK >= 16; }
+// the few-tile forms stage 32 of K per barrier (one workgroup per CU: half the barriers and stage
+// overheads; 80 KB of LDS) when K allows it; RSX_GEMM_FEW_BK=16 keeps 16 (A/B)
+int few_bk(int K) {
+  static int v = 0;
+  if (v == 0) {
+    const char* e = getenv("RSX_GEMM_FEW_BK");
+    v = (e && atoi(e) == 16) ? 16 : 32;
+  }
+  return (v == 32 && K % 32 == 0) ? 32 : 16;
+}
 
 // RSX_GEMM_WS_PF = 0 | 1 (A/B): four waves with the B-fragment prefetch (PF) or without
 bool ws_pf() {
@@ -750,7 +763,7 @@ int split_plan(int64_t M, int N, int K) {
   const int cus = num_cus();
   if (tiles >= cus) return 1;
   for (int S : {8, 4, 3, 2})  // K ranges of >= 256: at 192 (K = 768, S = 4) 0.046 vs 0.042 ms unsplit
-    if (K % (S * kBK) == 0 && K / S >= 256 && tiles * S <= 4LL * cus) return S;
+    if (K % (S * 32) == 0 && K / S >= 256 && tiles * S <= 4LL * cus) return S;
   return 1;
 }
 }  // namespace
@@ -800,7 +813,8 @@ static int gemm_x3_impl(const float* A, int64_t lda, const float* B, int64_t ldb
     g.part = ws;
     const int64_t blocks = tiles * S;
     const int grid = (int)((blocks + 7) / 8 * 8);
-    hipLaunchKernelGGL((gemm_x3_nt_k<EPI_BIAS, 4>), dim3(grid), dim3(256), 0, st, g);
+    if (few_bk(g.kspan) == 32) hipLaunchKernelGGL((gemm_x3_nt_k<EPI_BIAS, 4, 32>), dim3(grid), dim3(256), 0, st, g);
+    else hipLaunchKernelGGL((gemm_x3_nt_k<EPI_BIAS, 4>), dim3(grid), dim3(256), 0, st, g);
     RSX_LAUNCHED();
     const unsigned rb = (unsigned)((M * (int64_t)N + 255) / 256);
     if (epi == EPI_BIAS) hipLaunchKernelGGL(gemm_splitk_reduce_k<EPI_BIAS>, dim3(rb), dim3(256), 0, st, g);
@@ -815,7 +829,11 @@ static int gemm_x3_impl(const float* A, int64_t lda, const float* B, int64_t ldb
   const int grid = (int)((blocks + 7) / 8 * 8);
   // few tiles for the chip (one workgroup per CU at most) and a long K: four stages in flight per workgroup
   if (deep_prefetch() && g.per == 1 && blocks <= num_cus() && a_nk_long(K)) {
-    if (epi == EPI_BIAS) hipLaunchKernelGGL((gemm_x3_nt_k<EPI_BIAS, 4>), dim3(grid), dim3(256), 0, st, g);
+    const bool b32 = few_bk(K) == 32;
+    if (epi == EPI_BIAS && b32) hipLaunchKernelGGL((gemm_x3_nt_k<EPI_BIAS, 4, 32>), dim3(grid), dim3(256), 0, st, g);
+    else if (epi == EPI_BIAS) hipLaunchKernelGGL((gemm_x3_nt_k<EPI_BIAS, 4>), dim3(grid), dim3(256), 0, st, g);
+    else if (epi == EPI_GELU_DROP && b32)
+      hipLaunchKernelGGL((gemm_x3_nt_k<EPI_GELU_DROP, 4, 32>), dim3(grid), dim3(256), 0, st, g);
     else if (epi == EPI_GELU_DROP) hipLaunchKernelGGL((gemm_x3_nt_k<EPI_GELU_DROP, 4>), dim3(grid), dim3(256), 0, st, g);
     else hipLaunchKernelGGL(gemm_x3_nt_k<EPI_DGELU_DROP>, dim3(grid), dim3(256), 0, st, g);  // Q = 4 spills here
   } else if (epi == EPI_BIAS) hipLaunchKernelGGL(gemm_x3_nt_k<EPI_BIAS>, dim3(grid), dim3(256), 0, st, g);
