@@ -1089,16 +1089,15 @@ __device__ __forceinline__ void split8(const float4& a, const float4& b, bf16x8&
 // (fragment s, element j = dim 64h + 8s + j: the chunk 8h + s of the streamed row reads)
 __device__ __forceinline__ void load_owner_x3(bf16x8 (&uh)[8], bf16x8 (&ul)[8], const float* base, int64_t row,
                                               int64_t ld, bool ok, int h) {
+  // all 16 loads issued back to back from a clamped row, then zeroed past the rows (a branch
+  // around each pair made hipcc wait for every pair before issuing the next)
   const float4* src = reinterpret_cast<const float4*>(base + (ok ? row : 0) * ld + h * 64);
+  float4 v[16];
 #pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
-    if (ok) {
-      v0 = src[2 * s];
-      v1 = src[2 * s + 1];
-    }
-    split8(v0, v1, uh[s], ul[s]);
-  }
+  for (int t = 0; t < 16; ++t) v[t] = src[t];
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) split8(ok ? v[2 * s] : z, ok ? v[2 * s + 1] : z, uh[s], ul[s]);
 }
 
 // Streamed operands are split once per call into global hi/lo bf16 images ([rows][128] each,
@@ -2618,16 +2617,15 @@ __device__ __forceinline__ void split8_h(const float4& a, const float4& b, bf16x
 
 __device__ __forceinline__ void load_owner_h(bf16x8 (&uh)[8], bf16x8 (&ul)[8], const float* base, int64_t row,
                                              int64_t ld, bool ok, int h) {
+  // all 16 loads issued back to back from a clamped row, then zeroed past the rows (a branch
+  // around each pair made hipcc wait for every pair before issuing the next)
   const float4* src = reinterpret_cast<const float4*>(base + (ok ? row : 0) * ld + h * 64);
+  float4 v[16];
 #pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
-    if (ok) {
-      v0 = src[2 * s];
-      v1 = src[2 * s + 1];
-    }
-    split8_h(v0, v1, uh[s], ul[s]);
-  }
+  for (int t = 0; t < 16; ++t) v[t] = src[t];
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) split8_h(ok ? v[2 * s] : z, ok ? v[2 * s + 1] : z, uh[s], ul[s]);
 }
 
 // rows x 128 fp32 -> fp16 hi/lo images of x * 2^8 (nce_split_k's layout)

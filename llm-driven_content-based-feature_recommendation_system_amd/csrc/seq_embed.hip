@@ -35,6 +35,21 @@ struct FwdArgs {
   rsx::Dropout drop;
 };
 
+// Loads through pointers taken from the per-table pointer arrays (ids_l / tab_l, BwdLive): hipcc
+// cannot prove those point to global memory and emits flat loads, which count in lgkmcnt as well as
+// vmcnt -- so every LDS shuffle of the row reductions (ds_bpermute + lgkmcnt(0)) also waited for all
+// outstanding row loads. Casting to the global address space gives global loads (vmcnt only).
+// (through a native vector type: a float4 struct load through an address-space-1 pointer still
+// came out as a flat load)
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const f4v gf4v;
+typedef __attribute__((address_space(1))) const int64_t gint64;
+__device__ __forceinline__ float4 ldg4(const float* p) {
+  const f4v v = *(gf4v*)(p);
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ int64_t ldg8(const int64_t* p) { return *(gint64*)(p); }
+
 __device__ __forceinline__ float4 f4_axpy_rn(float4 x, float4 e, float g) {
   // seq_emb += E[id] * g  -- product rounded, then sum rounded (no FMA contraction),
   // matching the reference's separate `* s_g[j]` and `+=` tensor ops.
@@ -58,18 +73,18 @@ __device__ __forceinline__ float4 f4_add_rn(float4 x, float4 p) {
 template <int D>
 __device__ __forceinline__ float4 build_row(const FwdArgs& a, int64_t r, int c, const float* g) {
   float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (a.base) x = reinterpret_cast<const float4*>(a.base + r * D)[c];
+  if (a.base) x = ldg4(a.base + r * D + 4 * c);
 #pragma unroll
   for (int j = 0; j < kMaxTab; ++j) {
     if (j < a.ntab && g[j] != 0.0f) {
-      const int64_t id = a.ids[j][r];
-      const float4 e = reinterpret_cast<const float4*>(a.tab[j] + id * D)[c];
+      const int64_t id = ldg8(a.ids[j] + r);
+      const float4 e = ldg4(a.tab[j] + id * D + 4 * c);
       x = f4_axpy_rn(x, e, g[j]);
     }
   }
   if (a.pos) {
-    const int l = a.tok_pos ? (int)a.tok_pos[r] : (int)(r % a.L);
-    x = f4_add_rn(x, reinterpret_cast<const float4*>(a.pos + (int64_t)l * D)[c]);
+    const int l = a.tok_pos ? (int)ldg8(a.tok_pos + r) : (int)(r % a.L);
+    x = f4_add_rn(x, ldg4(a.pos + (int64_t)l * D + 4 * c));
   }
   return x;
 }
@@ -116,11 +131,16 @@ __device__ __forceinline__ void ln_drop_store(const FwdArgs& a, float4 x, int64_
   }
 }
 
-template <int D, int U, int NL>
+// FULL: the packed tower's configuration (base rows, a position table indexed by tok_pos, LayerNorm)
+// with every operand's presence known at compile time. With the presence tests as run-time branches
+// hipcc closed each of their blocks with a vmcnt(0), so the id -> row chains of one iteration ran
+// one after another instead of all in flight (same loads, same op order, same results).
+template <int D, int U, int NL, bool FULL = false>
 __device__ __forceinline__ void fwd_groups(const FwdArgs& a, const int64_t* const* ids_l, const float* const* tab_l,
                                            const float* g_l, int64_t r0, int sub, int c, float4 w, float4 bb,
                                            bool do_ln) {
   constexpr int RPW = 64 / (D / 4);
+  const bool has_pos = FULL || a.pos, has_base = FULL || a.base;
   int64_t rr[U];
   int64_t id[U][NL > 0 ? NL : 1];
   int lp[U];
@@ -129,31 +149,37 @@ __device__ __forceinline__ void fwd_groups(const FwdArgs& a, const int64_t* cons
     const int64_t r = r0 + u * RPW + sub;
     rr[u] = r < a.T ? r : a.T - 1;  // clamped: out-of-range slots recompute the last row, store nothing
 #pragma unroll
-    for (int k = 0; k < NL; ++k) id[u][k] = ids_l[k][rr[u]];
-    lp[u] = a.pos ? (a.tok_pos ? (int)a.tok_pos[rr[u]] : (int)(rr[u] % a.L)) : 0;
+    for (int k = 0; k < NL; ++k) id[u][k] = ldg8(ids_l[k] + rr[u]);
+    if (FULL) lp[u] = (int)ldg8(a.tok_pos + rr[u]);
+    else lp[u] = a.pos ? (a.tok_pos ? (int)a.tok_pos[rr[u]] : (int)(rr[u] % a.L)) : 0;
   }
   float4 x[U];
 #pragma unroll
   for (int u = 0; u < U; ++u)
-    x[u] = a.base ? reinterpret_cast<const float4*>(a.base + rr[u] * D)[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    x[u] = has_base ? ldg4(a.base + rr[u] * D + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
   float4 e[U][NL > 0 ? NL : 1];
 #pragma unroll
   for (int k = 0; k < NL; ++k)
 #pragma unroll
-    for (int u = 0; u < U; ++u) e[u][k] = reinterpret_cast<const float4*>(tab_l[k] + id[u][k] * D)[c];
+    for (int u = 0; u < U; ++u) e[u][k] = ldg4(tab_l[k] + id[u][k] * D + 4 * c);
+  float4 pv[U];
+  if (FULL) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) pv[u] = ldg4(a.pos + (int64_t)lp[u] * D + 4 * c);
+  }
 #pragma unroll
   for (int k = 0; k < NL; ++k)
 #pragma unroll
     for (int u = 0; u < U; ++u) x[u] = f4_axpy_rn(x[u], e[u][k], g_l[k]);
-  if (a.pos) {
+  if (has_pos) {
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      x[u] = f4_add_rn(x[u], reinterpret_cast<const float4*>(a.pos + (int64_t)lp[u] * D)[c]);
+      x[u] = f4_add_rn(x[u], FULL ? pv[u] : ldg4(a.pos + (int64_t)lp[u] * D + 4 * c));
   }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int64_t r = r0 + u * RPW + sub;
-    ln_drop_store<D>(a, x[u], r, r < a.T, c, w, bb, do_ln);
+    ln_drop_store<D>(a, x[u], r, r < a.T, c, w, bb, FULL || do_ln);
   }
 }
 
@@ -194,6 +220,11 @@ __global__ __launch_bounds__(256) void seq_embed_fwd_k(FwdArgs a) {
       const float4 x = build_row<D>(a, ok ? r : a.T - 1, c, g);
       ln_drop_store<D>(a, x, r, ok, c, w, bb, do_ln);
     }
+    return;
+  }
+  if (nl == 2 && a.base && a.pos && a.tok_pos && do_ln) {  // the packed tower's configuration
+    for (int64_t r0 = wave_g * (RPW * U); r0 < a.T; r0 += nwaves * (RPW * U))
+      fwd_groups<D, U, 2, true>(a, ids_l, tab_l, g_l, r0, sub, c, w, bb, true);
     return;
   }
   for (int64_t r0 = wave_g * (RPW * U); r0 < a.T; r0 += nwaves * (RPW * U)) {
@@ -268,17 +299,17 @@ __device__ __forceinline__ void bwd_groups(const BwdArgs& a, const BwdLive& lv, 
     lp[u] = need_l ? (f.tok_pos ? (int)f.tok_pos[rc[u]] : (int)(rc[u] % f.L)) : 0;
 #pragma unroll
     for (int k = 0; k < NS; ++k)
-      id[u][k] = (NL > 0 && (NL != kMaxTab || k < lv.n)) ? lv.ids[k][rc[u]] : 0;
+      id[u][k] = (NL > 0 && (NL != kMaxTab || k < lv.n)) ? ldg8(lv.ids[k] + rc[u]) : 0;
   }
   float4 dyv[U], xv[U];
   float muv[U], rsv[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    dyv[u] = reinterpret_cast<const float4*>(a.dout + rc[u] * D)[c];
+    dyv[u] = ldg4(a.dout + rc[u] * D + 4 * c);
     xv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
     muv[u] = 0.0f; rsv[u] = 0.0f;
     if (cx.do_ln) {
-      if (f.base) xv[u] = reinterpret_cast<const float4*>(f.base + rc[u] * D)[c];
+      if (f.base) xv[u] = ldg4(f.base + rc[u] * D + 4 * c);
       muv[u] = f.mean[rc[u]];
       rsv[u] = f.rstd[rc[u]];
     }
@@ -290,7 +321,7 @@ __device__ __forceinline__ void bwd_groups(const BwdArgs& a, const BwdLive& lv, 
     for (int u = 0; u < U; ++u) {
       ev[u][k] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (NL > 0 && (NL != kMaxTab || k < lv.n) && need_e && !(ABL & 2))
-        ev[u][k] = reinterpret_cast<const float4*>(lv.tab[k] + id[u][k] * D)[c];
+        ev[u][k] = ldg4(lv.tab[k] + id[u][k] * D + 4 * c);
     }
   if (cx.do_ln) {  // recompute x in the forward's op order: base, + E_j[id] * g_j (j ascending), + pos
 #pragma unroll
@@ -301,7 +332,7 @@ __device__ __forceinline__ void bwd_groups(const BwdArgs& a, const BwdLive& lv, 
     if (f.pos) {
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        xv[u] = f4_add_rn(xv[u], reinterpret_cast<const float4*>(f.pos + (int64_t)lp[u] * D)[c]);
+        xv[u] = f4_add_rn(xv[u], ldg4(f.pos + (int64_t)lp[u] * D + 4 * c));
     }
   }
 #pragma unroll

@@ -62,6 +62,11 @@ def main():
         ev[2].record()
         torch.cuda._sleep(1000)  # marker: iteration ends
         torch.cuda.synchronize()
+        if it == args.iters + 1:  # last iteration: checksums of the output and every gradient (A/B builds
+            # must agree bit for bit: same seeds, same per-element arithmetic)
+            cks = {"out": float(out.detach().double().sum()), "out_abs": float(out.detach().double().abs().sum()),
+                   "grads": float(sum(q.grad.double().abs().sum() for q in model.parameters() if q.grad is not None)),
+                   "profile_grad": float(profile.grad.double().abs().sum())}
         model.zero_grad(set_to_none=True)
         profile.grad = None
         if it >= 2:
@@ -69,7 +74,7 @@ def main():
             bwd_ms.append(ev[1].elapsed_time(ev[2]))
     print(json.dumps({"batch": args.batch, "packed_tokens_T": T, "tail_rows_R": int(out.shape[0]),
                       "tower_fwd_ms": round(sum(fwd_ms) / len(fwd_ms), 4),
-                      "tower_bwd_ms_incl_autograd": round(sum(bwd_ms) / len(bwd_ms), 4)}), flush=True)
+                      "tower_bwd_ms_incl_autograd": round(sum(bwd_ms) / len(bwd_ms), 4), "checksums": cks}), flush=True)
 
 
 if __name__ == "__main__":
