@@ -187,16 +187,11 @@ __global__ __launch_bounds__(256) void tw_lastq_fwd_k(LastQ a) {
   // pass over the keys instead of a 6-step wave reduction per output dim)
   __shared__ float sP[kHeads][64][kDh + 1];
   {
-    // the V row's eight loads issued together from a clamped row and zeroed where unused (a
-    // branch around each load made hipcc wait for every load before issuing the next)
-    const float* vr = a.qkv + (in ? kr : s0) * kQKV + 2 * kD + kDh * hd;
-    const bool use = in && pr != 0.0f;
-    float4 vv[kDh / 4];
-#pragma unroll
-    for (int e = 0; e < kDh; e += 4) vv[e / 4] = *reinterpret_cast<const float4*>(vr + e);
+    const float* vr = a.qkv + kr * kQKV + 2 * kD + kDh * hd;
 #pragma unroll
     for (int e = 0; e < kDh; e += 4) {
-      const float4 v = use ? vv[e / 4] : make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (in && pr != 0.0f) v = *reinterpret_cast<const float4*>(vr + e);
       sP[hd][lane][e] = pr * v.x;
       sP[hd][lane][e + 1] = pr * v.y;
       sP[hd][lane][e + 2] = pr * v.z;
@@ -247,14 +242,10 @@ __global__ __launch_bounds__(256) void tw_lastq_bwd_k(LastQ a) {
   const float ds = valid ? p * (dp - sdp) * 0.17677669529663687f : 0.0f;  // dL/dscore, scale folded in
   // dQ = sum_k ds_k K_k: each lane's ds_k K_k row to LDS, lane d sums column d
   __shared__ float sP[kHeads][64][kDh + 1];
-  // K row loads issued together from a clamped row, zeroed where not valid (as in the forward)
-  const float* kc = a.qkv + (in ? kr : s0) * kQKV + kD + kDh * hd;
-  float4 kvv[kDh / 4];
-#pragma unroll
-  for (int e = 0; e < kDh; e += 4) kvv[e / 4] = *reinterpret_cast<const float4*>(kc + e);
 #pragma unroll
   for (int e = 0; e < kDh; e += 4) {
-    const float4 kv = valid ? kvv[e / 4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 kv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (valid) kv = *reinterpret_cast<const float4*>(kk + e);
     sP[hd][lane][e] = ds * kv.x;
     sP[hd][lane][e + 1] = ds * kv.y;
     sP[hd][lane][e + 2] = ds * kv.z;
@@ -268,17 +259,9 @@ __global__ __launch_bounds__(256) void tw_lastq_bwd_k(LastQ a) {
   if (in) {
     float* drow = a.dqkv + kr * kQKV;
     const float pd = valid ? a.drop.apply(p, ((uint64_t)q * kHeads + hd) * 64 + lane) : 0.0f;  // D_k P_k
-    // all sixteen loads before the first store (dqkv may alias qkv as far as hipcc knows, so loads
-    // interleaved with the stores were issued one pair per memory round trip)
-    float4 xs[kDh / 4], gs[kDh / 4];
 #pragma unroll
     for (int e = 0; e < kDh; e += 4) {
-      xs[e / 4] = *reinterpret_cast<const float4*>(qr + e);
-      gs[e / 4] = *reinterpret_cast<const float4*>(dor + e);
-    }
-#pragma unroll
-    for (int e = 0; e < kDh; e += 4) {
-      const float4 x = xs[e / 4], g = gs[e / 4];
+      const float4 x = *reinterpret_cast<const float4*>(qr + e), g = *reinterpret_cast<const float4*>(dor + e);
       *reinterpret_cast<float4*>(drow + kD + kDh * hd + e) =
           make_float4(ds * x.x, ds * x.y, ds * x.z, ds * x.w);                     // dK
       *reinterpret_cast<float4*>(drow + 2 * kD + kDh * hd + e) =
