@@ -474,7 +474,8 @@ def prepare_step_index_async(batch, pretrained_vecs=None, pretrained_lookup=None
     contrastive_step_dp(..., index=...), which orders the main stream after it."""
     global _PREP_STREAM
     if _PREP_STREAM is None:
-        _PREP_STREAM = torch.cuda.Stream(priority=-1)
+        # RSX_INDEX_PRIORITY (A/B): the side stream's priority (-1 high, the default; 0 normal)
+        _PREP_STREAM = torch.cuda.Stream(priority=int(os.environ.get("RSX_INDEX_PRIORITY", "-1")))
     with torch.cuda.stream(_PREP_STREAM):
         ix = prepare_step_index(batch, pretrained_vecs, pretrained_lookup)
         ix.ready = torch.cuda.Event()
