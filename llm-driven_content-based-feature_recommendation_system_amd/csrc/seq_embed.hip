@@ -50,6 +50,32 @@ __device__ __forceinline__ float4 ldg4(const float* p) {
 }
 __device__ __forceinline__ int64_t ldg8(const int64_t* p) { return *(gint64*)(p); }
 
+// Row sums of the LayerNorm statistics on VALU lane moves (round 6): the xor butterfly of
+// rsx::wave_sum_width in the same order, its partners delivered by v_permlane32_swap / v_permlane16_swap
+// (o = 32, 16) and DPP row_ror (o = 8, 4, 2, 1; after the larger steps a lane's partial depends only on its
+// index mod 2o, and row_ror:o reaches a lane with the same index mod 2o as lane ^ o) instead of
+// ds_bpermute + lgkmcnt waits. Bit-identical sums (tools/probe/dpp_probe.hip on the GPU).
+template <int W>
+__device__ __forceinline__ float lane_sum(float v) {
+  if constexpr (W != 16 && W != 32 && W != 64) {
+    return rsx::wave_sum_width(v, W);
+  } else {
+    if constexpr (W == 64) {
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+      v = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+    }
+    if constexpr (W >= 32) {
+      const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+      v = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+    }
+    v += __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x128, 0xF, 0xF, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x124, 0xF, 0xF, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x122, 0xF, 0xF, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x121, 0xF, 0xF, false));
+    return v;
+  }
+}
+
 __device__ __forceinline__ float4 f4_axpy_rn(float4 x, float4 e, float g) {
   // seq_emb += E[id] * g  -- product rounded, then sum rounded (no FMA contraction),
   // matching the reference's separate `* s_g[j]` and `+=` tensor ops.
@@ -104,11 +130,11 @@ __device__ __forceinline__ void ln_drop_store(const FwdArgs& a, float4 x, int64_
   float4 y = x;
   if (do_ln) {
     float s = (x.x + x.y) + (x.z + x.w);
-    s = rsx::wave_sum_width(s, LPR);
+    s = lane_sum<LPR>(s);
     const float mu = s / (float)D;
     const float4 d = make_float4(x.x - mu, x.y - mu, x.z - mu, x.w - mu);
     float v = d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w;
-    v = rsx::wave_sum_width(v, LPR);
+    v = lane_sum<LPR>(v);
     const float rs = 1.0f / sqrtf(v / (float)D + a.eps);
     y.x = d.x * rs * w.x + bb.x;
     y.y = d.y * rs * w.y + bb.y;
@@ -358,8 +384,8 @@ __device__ __forceinline__ void bwd_groups(const BwdArgs& a, const BwdLive& lv, 
       const float4 dh = make_float4(dy.x * w.x, dy.y * w.y, dy.z * w.z, dy.w * w.w);
       float c1 = (dh.x + dh.y) + (dh.z + dh.w);
       float c2 = dh.x * xh.x + dh.y * xh.y + dh.z * xh.z + dh.w * xh.w;
-      c1 = rsx::wave_sum_width(c1, LPR) / (float)D;
-      c2 = rsx::wave_sum_width(c2, LPR) / (float)D;
+      c1 = lane_sum<LPR>(c1) / (float)D;
+      c2 = lane_sum<LPR>(c2) / (float)D;
       dx.x = (dh.x - c1 - xh.x * c2) * rs;
       dx.y = (dh.y - c1 - xh.y * c2) * rs;
       dx.z = (dh.z - c1 - xh.z * c2) * rs;
