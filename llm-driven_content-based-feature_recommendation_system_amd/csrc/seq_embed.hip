@@ -54,7 +54,9 @@ __device__ __forceinline__ int64_t ldg8(const int64_t* p) { return *(gint64*)(p)
 // rsx::wave_sum_width in the same order, its partners delivered by v_permlane32_swap / v_permlane16_swap
 // (o = 32, 16) and DPP row_ror (o = 8, 4, 2, 1; after the larger steps a lane's partial depends only on its
 // index mod 2o, and row_ror:o reaches a lane with the same index mod 2o as lane ^ o) instead of
-// ds_bpermute + lgkmcnt waits. Bit-identical sums (tools/probe/dpp_probe.hip on the GPU).
+// ds_bpermute + lgkmcnt waits. The sums equal the shuffle form's bit for bit (tools/probe/dpp_probe.hip on
+// the GPU); hipcc generates the neighbouring LayerNorm arithmetic differently around them, so the kernel's
+// outputs can differ from the shuffle-form build in the last bit (DESIGN.md, round 6 second session).
 template <int W>
 __device__ __forceinline__ float lane_sum(float v) {
   if constexpr (W != 16 && W != 32 && W != 64) {
